@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident WebSocket frame decode + payload unmask on MI355X.
+
+Metric (BASELINE.json): "GiB/s WS payload unmasked (device-resident) +
+frames/s, 64 KiB masked frames".  One step = one pass of the hot path
+(gevws_decode_batch_async: header walk, scan, record emit, unmask/compact)
+over one synthetic batch already resident in HBM, plus the RCCL all-reduce of
+the decoded {frames, payload bytes, errors} counts when N > 1.
+
+Default workload (N=1): C3 = 1 048 576 masked binary 64 KiB frames (h = 14)
+over 16 384 connections, generated on the device (seeded splitmix64).  With
+N > 1 every rank decodes its own connections' batch of the same size (weak
+scaling: connections shard by GPU, the payload never crosses GPUs).
+
+Prints ONE JSON line (rank 0).  `roofline` is the unmask kernel's algorithmic
+bytes (h + 2L per frame) over its mean HIP-event duration in the
+timed region; `cpu_baseline` is the C restatement of the reference per-frame
+UnPacket pipeline (oracle/ws_ref.c) timed on this host's cores on a bounded
+sample of the same workload.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "GiB/s WS payload unmasked (device-resident) + frames/s, 64 KiB masked frames"
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def build_layout(name: str, rank: int, conns: int | None):
+    from gev_amd import workloads as w
+    seed = 0x67657600 + 7919 * rank
+    if name == "c3":
+        return w.config_c3(seed=seed, n_conns=conns or 16384)
+    if name == "c2":
+        return w.config_c2(seed=seed, n_conns=conns or 4096)
+    if name == "c4":
+        return w.config_c4(total_payload=16 << 30, n_conns=conns or 65536, seed=seed)
+    if name == "c5":
+        return w.config_c5(n_conns=conns or 256, seed=seed)
+    raise SystemExit(f"unknown config {name}")
+
+
+def cpu_sample_layout(name: str):
+    """A bounded sample of the same workload for the CPU baseline."""
+    from gev_amd import workloads as w
+    if name == "c3":
+        return w.uniform(16, 256, 65536, seed=1, name="4096 x 64 KiB masked binary frames (256 MiB payload)")
+    if name == "c2":
+        return w.uniform(64, 1024, 4096, seed=1, name="65536 x 4 KiB masked binary frames (256 MiB payload)")
+    if name == "c4":
+        return w.config_c4(total_payload=256 << 20, n_conns=1024, seed=1)
+    return w.config_c5(n_conns=32, seed=1)
+
+
+def cpu_baseline(name: str, seconds: float, threads: int):
+    import numpy as np
+    from gev_amd import workloads as w
+    from oracle import ref
+    lay = cpu_sample_layout(name)
+    arena = np.concatenate([w.synth_host(lay), np.zeros(64, np.uint8)])
+    secs, pb, nf = ref.bench_pipeline(arena, lay.conns[:, 0], lay.conns[:, 1], threads=threads,
+                                      min_seconds=seconds)
+    return dict(value=round(pb / secs / 2**30, 4), unit="GiB/s", cores=threads, kind="port",
+                frames_per_s=round(nf / secs, 1),
+                sample=(f"{lay.name}, {lay.n_conns} connections round-robin over {threads} thread(s), "
+                        f"repeated for >= {seconds:.0f} s; oracle/ws_ref.c per-frame UnPacket pipeline "
+                        "(header parse, zero-filled make, ring Read copy, Cipher u64 loop), "
+                        "gcc -O2 -fno-tree-vectorize"))
+
+
+def load_traffic(config_name: str):
+    """HBM bytes per unmask launch from a committed rocprofv3 --pmc pass (see
+    profiles/README.md), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        e = d.get(config_name)
+        return None if e is None else int(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--conns", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads-multi", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import gev_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+
+    eng = gev_amd.Engine(local)
+    t_setup = time.time()
+    lay = build_layout(args.config, rank, args.conns)
+    log(f"rank {rank}: {lay.name}: {lay.n_frames} frames, {lay.n_conns} connections, "
+        f"{lay.arena_bytes / 2**30:.2f} GiB in, {lay.payload_padded / 2**30:.2f} GiB out")
+    arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    arena[lay.arena_bytes:] = 0
+    desc = torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev)
+    conns = torch.from_numpy(lay.conns.copy()).to(dev)
+    eng.synth(arena, desc, lay.n_frames, lay.seed)
+    max_frames, cap = lay.n_frames, lay.payload_padded
+    out = eng.alloc_batch(lay.n_conns, max_frames, cap)
+
+    # correctness gate (outside the timed region): decode(mask(P)) == P on every byte
+    eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, max_frames, cap)
+    mism = torch.zeros(1, dtype=torch.int64, device=dev)
+    eng.verify(desc, lay.n_frames, lay.seed, out, mism)
+    torch.cuda.synchronize()
+    s = out.summary_host()
+    mismatch = int(mism.item())
+    if mismatch or int(s["frames"]) != lay.n_frames or int(s["payload_len"]) != lay.payload_len:
+        raise SystemExit(f"verification failed: mismatch={mismatch} frames={int(s['frames'])}")
+    del desc
+    log(f"rank {rank}: setup+verify {time.time() - t_setup:.1f}s, bit-exact")
+
+    counts = torch.zeros(3, dtype=torch.int64, device=dev)
+    sel = torch.tensor([0, 2, 3], dtype=torch.int64, device=dev)
+    sum64 = out.summary.view(torch.int64)
+
+    def step():
+        eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, max_frames, cap)
+        torch.index_select(sum64, 0, sel, out=counts)
+        if world > 1:
+            dist.all_reduce(counts)  # decoded {frames, payload bytes, errors}, summed over GPUs
+
+    for _ in range(args.warmup):
+        step()
+    eng.timing()  # drop anything recorded so far
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    eng.set_timing(False)
+    phases, calls = eng.timing()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    c = counts.cpu().numpy()
+    frames_step, payload_step, errors = int(c[0]), int(c[1]), int(c[2])
+    if world == 1:
+        frames_step, payload_step = int(s["frames"]), int(s["payload_len"])
+    ms_step = elapsed / args.steps * 1e3
+    value = payload_step * args.steps / elapsed / 2**30
+    mean_ms = [p / max(calls, 1) for p in phases]
+    unmask_ms = mean_ms[3]
+    alg_bytes = lay.algorithmic_bytes()
+    achieved = alg_bytes / (unmask_ms / 1e3) / 1e9
+    pipeline_gbps = alg_bytes / (sum(mean_ms) / 1e3) / 1e9
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: masked frames generated on the device (seeded splitmix64 payloads and keys)",
+        "config": {"workload": lay.name, "connections_per_gpu": lay.n_conns, "frames_per_gpu": lay.n_frames,
+                   "payload_bytes_per_gpu": lay.payload_len, "input_bytes_per_gpu": lay.arena_bytes,
+                   "parallelism": f"connections sharded over {world} GPU(s); RCCL all-reduce of counts"},
+        "frames_per_s": round(frames_step * args.steps / elapsed, 1),
+        "errors": errors,
+        "phases_ms": {"walk_count": round(mean_ms[0], 4), "scan": round(mean_ms[1], 4),
+                      "walk_emit": round(mean_ms[2], 4), "unmask": round(unmask_ms, 4)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_traffic(args.config),
+                     "kernel": "k_unmask", "algorithmic_bytes_per_launch": alg_bytes,
+                     "pipeline_achieved": round(pipeline_gbps, 1),
+                     "pipeline_frac": round(pipeline_gbps / HBM_PEAK_GBPS, 4)},
+        "verified_bit_exact": True,
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu:
+        log("cpu baseline (1 thread)...")
+        result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds, 1)
+        if args.cpu_threads_multi > 1:
+            log(f"cpu baseline ({args.cpu_threads_multi} threads)...")
+            result["cpu_baseline_multi"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0),
+                                                        args.cpu_threads_multi)
+    print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

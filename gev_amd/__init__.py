@@ -1,0 +1,305 @@
+"""gev_amd -- MI355X-native WebSocket frame-decode / payload-unmask engine.
+
+Drop-in for the hot path of gev's websocket plugin
+(plugins/websocket/protocol.go:27-64 ``Protocol.UnPacket``): the decode runs
+in hand-written gfx950 HIP kernels (gev_amd/csrc/gevws_device.hip) behind the
+C ABI of include/gevws.h.  This Python layer is a thin ctypes binding used by
+the tests and bench; torch supplies device memory, streams and
+torch.distributed (plumbing only).
+
+Names mirror the reference: ``RingBuffer`` (github.com/Allenxuxu/ringbuffer as
+gev uses it), ``Connection`` (gev.Connection's websocket context keys),
+``Protocol.unpacket`` / ``Protocol.packet`` (websocket.Protocol),
+``handler_protocol`` (Connection.handlerProtocol, connection.go:208-218).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _abi
+from ._abi import (ERR_CAPACITY, ERR_DEVICE, ERR_INVALID, ERR_LEN_MSB, ERR_NOT_UPGRADED, IN_PAD, NEED_MORE,
+                   OK, PAYLOAD_ALIGN, TILE, Header)
+
+lib = _abi.load()
+
+FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked", "u1"),
+                        ("mask", "u1", (4,)), ("length", "<i8"),
+                        ("payload_off", "<u8"), ("src_off", "<u8")])
+CONN_OUT_DTYPE = np.dtype([("first_frame", "<u8"), ("consumed", "<u8"), ("payload_base", "<u8"),
+                           ("nframes", "<u4"), ("status", "<i4")])
+SUMMARY_DTYPE = np.dtype([("frames", "<u8"), ("payload_bytes", "<u8"), ("payload_len", "<u8"),
+                          ("errors", "<u8"), ("status", "<i4"), ("reserved0", "<u4"), ("reserved", "<u8", (3,))])
+SYNTH_DTYPE = np.dtype([("hdr_off", "<u8"), ("length", "<u8"), ("mask", "<u4"), ("b0", "u1"),
+                        ("len_form", "u1"), ("masked", "u1"), ("pad", "u1")])
+assert FRAME_DTYPE.itemsize == 32 and CONN_OUT_DTYPE.itemsize == 32
+assert SUMMARY_DTYPE.itemsize == 64 and SYNTH_DTYPE.itemsize == 24
+
+
+def status_string(st: int) -> str:
+    return lib.gevws_status_string(st).decode()
+
+
+def device_count() -> int:
+    return lib.gevws_device_count()
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_handle(stream) -> Optional[int]:
+    if stream is None:
+        return _torch().cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+@dataclass
+class Batch:
+    """Device-resident result of one batch decode (all tensors on the GPU)."""
+    frames: "object"      # uint8 [max_frames, 32]  (gevws_frame records)
+    payload: "object"     # uint8 [payload_cap + 16]
+    conn_out: "object"    # uint8 [n_conns, 32]     (gevws_conn_out)
+    summary: "object"     # uint8 [64]              (gevws_summary)
+    n_conns: int
+
+    def summary_host(self) -> np.ndarray:
+        return self.summary.cpu().numpy().view(SUMMARY_DTYPE)[0]
+
+    def frames_host(self) -> np.ndarray:
+        n = int(self.summary_host()["frames"])
+        return self.frames[:n].cpu().numpy().reshape(-1).view(FRAME_DTYPE)
+
+    def conn_out_host(self) -> np.ndarray:
+        return self.conn_out[: self.n_conns].cpu().numpy().reshape(-1).view(CONN_OUT_DTYPE)
+
+    def payload_host(self) -> np.ndarray:
+        n = int(self.summary_host()["payload_bytes"])
+        return self.payload[:n].cpu().numpy()
+
+
+class Engine:
+    """One gevws_ctx (one per event loop / rank) on one GPU."""
+
+    def __init__(self, device: int = 0):
+        if device_count() <= device:
+            raise RuntimeError(f"gev_amd.Engine: no HIP device {device} (found {device_count()}); "
+                               "the decode path has no CPU fallback")
+        self.device = device
+        self._ctx = lib.gevws_ctx_create(device)
+        if not self._ctx:
+            raise RuntimeError("gevws_ctx_create failed")
+
+    def close(self):
+        if self._ctx:
+            lib.gevws_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- timing
+    def set_timing(self, enable: bool):
+        lib.gevws_ctx_set_timing(self._ctx, int(enable))
+
+    def timing(self) -> Tuple[Tuple[float, float, float, float], int]:
+        """(summed ms per phase [walk-count, scan, walk-emit, unmask], calls) since the last query."""
+        ms = (ctypes.c_float * 4)()
+        calls = ctypes.c_uint32()
+        st = lib.gevws_ctx_timing(self._ctx, ms, ctypes.byref(calls))
+        if st != OK:
+            raise RuntimeError(status_string(st))
+        return tuple(ms), calls.value
+
+    # -------------------------------------------------------------- decode
+    def alloc_batch(self, n_conns: int, max_frames: int, payload_cap: int) -> Batch:
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        return Batch(frames=torch.empty((max(max_frames, 1), 32), dtype=torch.uint8, device=dev),
+                     payload=torch.empty(payload_cap + 16, dtype=torch.uint8, device=dev),
+                     conn_out=torch.empty((max(n_conns, 1), 32), dtype=torch.uint8, device=dev),
+                     summary=torch.zeros(64, dtype=torch.uint8, device=dev), n_conns=n_conns)
+
+    def decode_async(self, arena, in_bytes: int, conns, n_conns: int, out: Batch, max_frames: int,
+                     payload_cap: int, stream=None) -> None:
+        """gevws_decode_batch_async on device tensors (arena: uint8 with IN_PAD slack;
+        conns: int64 [n,2] = (off, len))."""
+        st = lib.gevws_decode_batch_async(
+            self._ctx, _stream_handle(stream), arena.data_ptr(), in_bytes,
+            conns.data_ptr() if n_conns else None, n_conns, out.frames.data_ptr(), max_frames,
+            out.payload.data_ptr(), payload_cap, out.conn_out.data_ptr(), out.summary.data_ptr())
+        if st != OK:
+            raise RuntimeError(f"gevws_decode_batch_async: {status_string(st)}")
+
+    def decode(self, arena, in_bytes: int, conns, n_conns: int, max_frames: Optional[int] = None,
+               payload_cap: Optional[int] = None, stream=None) -> Batch:
+        """Decode a device-resident batch; grows capacities once on ERR_CAPACITY."""
+        torch = _torch()
+        if max_frames is None:
+            max_frames = min(in_bytes // 2 + 1, 0xFFFFFFFF)
+        if payload_cap is None:
+            payload_cap = in_bytes + 16 * min(max_frames, in_bytes // 64 + 64) + 64
+        for attempt in range(2):
+            out = self.alloc_batch(n_conns, max_frames, payload_cap)
+            self.decode_async(arena, in_bytes, conns, n_conns, out, max_frames, payload_cap, stream)
+            torch.cuda.synchronize(self.device)
+            s = out.summary_host()
+            if int(s["status"]) == ERR_CAPACITY and attempt == 0:
+                max_frames = max(int(s["frames"]), 1)
+                payload_cap = max(int(s["payload_bytes"]), 16)
+                continue
+            if int(s["status"]) != OK:
+                raise RuntimeError(f"decode: {status_string(int(s['status']))}")
+            return out
+        raise RuntimeError("decode: capacity retry failed")
+
+    def cipher_(self, buf, mask: bytes, offset: int = 0, nbytes: Optional[int] = None,
+                byte_offset: int = 0, stream=None) -> None:
+        """ws.Cipher (cipher.go:14-53) in place on a device uint8 tensor region."""
+        m = (ctypes.c_uint8 * 4)(*mask)
+        n = buf.numel() - byte_offset if nbytes is None else nbytes
+        st = lib.gevws_cipher_async(self._ctx, _stream_handle(stream), buf.data_ptr() + byte_offset, n, m,
+                                    offset)
+        if st != OK:
+            raise RuntimeError(status_string(st))
+
+    # -------------------------------------------------------------- synthetic batches
+    def synth(self, arena, desc_dev, n_frames: int, seed: int, stream=None) -> None:
+        st = lib.gevws_synth_async(self._ctx, _stream_handle(stream), arena.data_ptr(), desc_dev.data_ptr(),
+                                   n_frames, seed)
+        if st != OK:
+            raise RuntimeError(status_string(st))
+
+    def verify(self, desc_dev, n_frames: int, seed: int, out: Batch, mismatch_dev, stream=None) -> None:
+        if out.frames.shape[0] < n_frames:
+            raise ValueError("verify: batch holds fewer frame records than the layout")
+        st = lib.gevws_synth_verify_async(self._ctx, _stream_handle(stream), desc_dev.data_ptr(), n_frames,
+                                          seed, out.frames.data_ptr(), out.payload.data_ptr(),
+                                          out.payload.numel() - 16, mismatch_dev.data_ptr())
+        if st != OK:
+            raise RuntimeError(status_string(st))
+
+
+# ====================================================================== host mirror
+class RingBuffer:
+    """ringbuffer.RingBuffer as gev uses it (New / Write / Length / PeekAll / Retrieve)."""
+
+    def __init__(self, size: int = 4096):
+        self._p = lib.gevws_ring_new(size)
+
+    def __del__(self):
+        if getattr(self, "_p", None):
+            lib.gevws_ring_free(self._p)
+            self._p = None
+
+    def write(self, data: bytes) -> int:
+        buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data) if data else None
+        return lib.gevws_ring_write(self._p, buf, len(data))
+
+    def length(self) -> int:
+        return lib.gevws_ring_length(self._p)
+
+    def capacity(self) -> int:
+        return lib.gevws_ring_capacity(self._p)
+
+    def is_empty(self) -> bool:
+        return self.length() == 0
+
+    def peek_all(self) -> Tuple[bytes, bytes]:
+        a, b = _abi.U8P(), _abi.U8P()
+        na, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        lib.gevws_ring_peek_all(self._p, ctypes.byref(a), ctypes.byref(na), ctypes.byref(b), ctypes.byref(nb))
+        first = ctypes.string_at(a, na.value) if na.value else b""
+        end = ctypes.string_at(b, nb.value) if nb.value else b""
+        return first, end
+
+    def retrieve(self, n: int) -> None:
+        lib.gevws_ring_retrieve(self._p, n)
+
+
+class Connection:
+    """The per-connection context keys of the websocket plugin (protocol.go:11-14)."""
+
+    def __init__(self, upgraded: bool = True):
+        self._p = lib.gevws_conn_new()
+        self.set_upgraded(upgraded)
+
+    def __del__(self):
+        if getattr(self, "_p", None):
+            lib.gevws_conn_free(self._p)
+            self._p = None
+
+    def set_upgraded(self, v: bool) -> None:
+        lib.gevws_conn_set_upgraded(self._p, int(v))
+
+    @property
+    def upgraded(self) -> bool:
+        return bool(lib.gevws_conn_upgraded(self._p))
+
+    def pending(self) -> int:
+        return lib.gevws_conn_pending(self._p)
+
+
+class Protocol:
+    """websocket.Protocol (plugins/websocket/protocol.go:16-69) over the device engine."""
+
+    def __init__(self, engine: Engine):
+        self.engine = engine
+        self._p = lib.gevws_protocol_new(engine._ctx)
+
+    def __del__(self):
+        if getattr(self, "_p", None):
+            lib.gevws_protocol_free(self._p)
+            self._p = None
+
+    def unpacket(self, c: Connection, buffer: RingBuffer) -> Tuple[Optional[Header], Optional[bytes]]:
+        """UnPacket(c, buffer) -> (ctx, out): one frame, or (None, None)."""
+        h = Header()
+        out = _abi.U8P()
+        n = ctypes.c_uint64()
+        st = lib.gevws_protocol_unpacket(self._p, c._p, buffer._p, ctypes.byref(h), ctypes.byref(out),
+                                         ctypes.byref(n))
+        self.last_status = st
+        if st != OK:
+            return None, None
+        return h, (ctypes.string_at(out, n.value) if n.value else b"")
+
+    def unpacket_batch(self, conns: Sequence[Connection], buffers: Sequence[RingBuffer]) -> int:
+        n = len(conns)
+        cs = (ctypes.c_void_p * n)(*[c._p for c in conns])
+        rs = (ctypes.c_void_p * n)(*[b._p for b in buffers])
+        r = lib.gevws_protocol_unpacket_batch(self._p, cs, rs, n)
+        if r < 0:
+            raise RuntimeError(f"unpacket_batch: {status_string(int(r))}")
+        return int(r)
+
+    def packet(self, c: Connection, data: bytes) -> bytes:
+        """Packet(c, data) -> data (protocol.go:67-69)."""
+        return data
+
+
+def handler_protocol(protocol: Protocol, c: Connection, buffer: RingBuffer,
+                     on_message: Callable[[Connection, Optional[Header], bytes], Optional[bytes]]) -> List[bytes]:
+    """Connection.handlerProtocol (connection.go:208-218): UnPacket until (nil, nil),
+    handing each frame to on_message and collecting Packet'ed replies."""
+    replies: List[bytes] = []
+    ctx, data = protocol.unpacket(c, buffer)
+    while ctx is not None or (data is not None and len(data) != 0):
+        send = on_message(c, ctx, data)
+        if send is not None:
+            replies.append(protocol.packet(c, send))
+        ctx, data = protocol.unpacket(c, buffer)
+    return replies
+
+
+__all__ = ["Engine", "Batch", "RingBuffer", "Connection", "Protocol", "Header", "handler_protocol",
+           "status_string", "device_count", "lib", "FRAME_DTYPE", "CONN_OUT_DTYPE", "SUMMARY_DTYPE",
+           "SYNTH_DTYPE", "OK", "NEED_MORE", "ERR_LEN_MSB", "ERR_CAPACITY", "ERR_INVALID", "ERR_DEVICE",
+           "ERR_NOT_UPGRADED", "IN_PAD", "PAYLOAD_ALIGN", "TILE"]

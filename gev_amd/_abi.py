@@ -1,0 +1,124 @@
+"""ctypes binding of gev_amd/libgevws.so (declared in include/gevws.h).
+
+The product path has no CPU fallback: if the HIP library is missing this
+module raises ImportError, and device calls raise when no GPU is present.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgevws.so")
+
+# status codes (gevws.h)
+OK = 0
+NEED_MORE = 1
+ERR_LEN_MSB = -1
+ERR_CAPACITY = -2
+ERR_INVALID = -3
+ERR_DEVICE = -4
+ERR_NOT_UPGRADED = -5
+
+IN_PAD = 64
+PAYLOAD_ALIGN = 16
+TILE = 4096
+
+
+class Header(ctypes.Structure):
+    """gevws_header == ws.Header (plugins/websocket/ws/frame.go:169-176)."""
+    _fields_ = [("fin", ctypes.c_uint8), ("rsv", ctypes.c_uint8), ("opcode", ctypes.c_uint8),
+                ("masked", ctypes.c_uint8), ("mask", ctypes.c_uint8 * 4), ("length", ctypes.c_int64)]
+
+    def as_tuple(self):
+        return (bool(self.fin), self.rsv, self.opcode, bool(self.masked), bytes(self.mask), self.length)
+
+    def __repr__(self):
+        return ("Header(fin=%s, rsv=%d, opcode=%d, masked=%s, mask=%s, length=%d)"
+                % (bool(self.fin), self.rsv, self.opcode, bool(self.masked), bytes(self.mask).hex(),
+                   self.length))
+
+
+class ConnIn(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint64)]
+
+
+class Frame(ctypes.Structure):
+    _fields_ = [("hdr", Header), ("payload_off", ctypes.c_uint64), ("src_off", ctypes.c_uint64)]
+
+
+class ConnOut(ctypes.Structure):
+    _fields_ = [("first_frame", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
+                ("payload_base", ctypes.c_uint64), ("nframes", ctypes.c_uint32), ("status", ctypes.c_int32)]
+
+
+class Summary(ctypes.Structure):
+    _fields_ = [("frames", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64),
+                ("payload_len", ctypes.c_uint64), ("errors", ctypes.c_uint64), ("status", ctypes.c_int32),
+                ("reserved0", ctypes.c_uint32), ("reserved", ctypes.c_uint64 * 3)]
+
+
+class SynthDesc(ctypes.Structure):
+    _fields_ = [("hdr_off", ctypes.c_uint64), ("length", ctypes.c_uint64), ("mask", ctypes.c_uint32),
+                ("b0", ctypes.c_uint8), ("len_form", ctypes.c_uint8), ("masked", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8)]
+
+
+assert ctypes.sizeof(Header) == 16 and ctypes.sizeof(Frame) == 32
+assert ctypes.sizeof(ConnIn) == 16 and ctypes.sizeof(ConnOut) == 32
+assert ctypes.sizeof(Summary) == 64 and ctypes.sizeof(SynthDesc) == 24
+
+P = ctypes.c_void_p
+U8P = ctypes.POINTER(ctypes.c_uint8)
+
+# (name, restype, argtypes) for every symbol include/gevws.h declares.
+SIGNATURES = {
+    "gevws_abi_version": (ctypes.c_int, []),
+    "gevws_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "gevws_device_count": (ctypes.c_int, []),
+    "gevws_ctx_create": (P, [ctypes.c_int]),
+    "gevws_ctx_destroy": (None, [P]),
+    "gevws_ctx_device": (ctypes.c_int, [P]),
+    "gevws_ctx_set_timing": (ctypes.c_int, [P, ctypes.c_int]),
+    "gevws_ctx_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32)]),
+    "gevws_decode_batch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,
+                                                ctypes.c_uint64, P, ctypes.c_uint64, P, P]),
+    "gevws_decode_batch": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,
+                                          ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.POINTER(Summary)]),
+    "gevws_cipher_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint64]),
+    "gevws_synth_async": (ctypes.c_int, [P, P, P, P, ctypes.c_uint64, ctypes.c_uint64]),
+    "gevws_synth_verify_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_uint64, P, P,
+                                                ctypes.c_uint64, P]),
+    "gevws_ring_new": (P, [ctypes.c_uint64]),
+    "gevws_ring_free": (None, [P]),
+    "gevws_ring_write": (ctypes.c_uint64, [P, P, ctypes.c_uint64]),
+    "gevws_ring_length": (ctypes.c_uint64, [P]),
+    "gevws_ring_capacity": (ctypes.c_uint64, [P]),
+    "gevws_ring_peek_all": (None, [P, ctypes.POINTER(U8P), ctypes.POINTER(ctypes.c_uint64),
+                                   ctypes.POINTER(U8P), ctypes.POINTER(ctypes.c_uint64)]),
+    "gevws_ring_retrieve": (None, [P, ctypes.c_uint64]),
+    "gevws_conn_new": (P, []),
+    "gevws_conn_free": (None, [P]),
+    "gevws_conn_set_upgraded": (None, [P, ctypes.c_int]),
+    "gevws_conn_upgraded": (ctypes.c_int, [P]),
+    "gevws_conn_pending": (ctypes.c_uint64, [P]),
+    "gevws_protocol_new": (P, [P]),
+    "gevws_protocol_free": (None, [P]),
+    "gevws_protocol_unpacket": (ctypes.c_int, [P, P, P, ctypes.POINTER(Header), ctypes.POINTER(U8P),
+                                               ctypes.POINTER(ctypes.c_uint64)]),
+    "gevws_protocol_unpacket_batch": (ctypes.c_int64, [P, P, P, ctypes.c_uint32]),
+    "gevws_protocol_packet": (U8P, [P, P, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+}
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"gev_amd: HIP library {path} is missing -- build it first "
+            "(python -c 'import __graft_entry__ as g; g.build()'); there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib

@@ -1,0 +1,738 @@
+// gevws_device.hip -- gfx950 (MI355X / CDNA4) kernels and the device half of
+// the C ABI declared in include/gevws.h.
+//
+// Hot path: for a batch of connections, the
+// repeated websocket.(*Protocol).UnPacket loop of Connection.handlerProtocol
+// (connection.go:208-218 -> plugins/websocket/protocol.go:38-62) is done as
+// four launches on one stream:
+//
+//   1. k_walk_count  one lane per connection walks its header chain
+//                    (ws.VirtualReadHeader, read.go:19-84, plus the
+//                    completeness gate, protocol.go:47) and counts frames,
+//                    payload bytes and consumed bytes; block partial sums.
+//   2. k_scan_blocks one workgroup scans the block partials -> batch totals,
+//                    capacity check.
+//   3. k_walk_emit   block-level scan -> per-connection bases; the chain is
+//                    walked again (headers now L2/MALL-resident) writing one
+//                    32-byte record per frame and the output-tile -> first
+//                    frame map.
+//   4. k_unmask      the byte stream: every lane owns one 16-byte chunk of the
+//                    output arena, finds its frame through the tile map, loads
+//                    16 source bytes (unaligned global_load_dwordx4), XORs the
+//                    4-byte key (ws.Cipher, cipher.go:14-53; the payload phase
+//                    restarts at 0 per frame, protocol.go:54) and stores 16
+//                    aligned bytes.  HBM-bound: h + 2L bytes per frame.
+//
+// No MFMA: this is a byte stream, not a contraction.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "gevws.h"
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int kWalkBlock = 256;
+constexpr int kScanBlock = 1024;
+constexpr int kUnmaskBlock = 256;
+constexpr uint64_t kTile = GEVWS_TILE;
+static_assert(kTile == kUnmaskBlock * 16, "one tile = one 16-byte chunk per lane");
+constexpr int kUnmaskUnroll = 4;
+constexpr int kBlkFields = 4;  // frames, padded payload bytes, payload length, errors
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ u32x4 ld16u(const uint8_t* p) {
+  u32x4 v;
+  __builtin_memcpy(&v, p, 16);  // gfx950 unaligned global_load_dwordx4
+  return v;
+}
+
+__device__ __forceinline__ uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+// 32-bit field starting at byte `off` (0..12) of the 16-byte window lo|hi.
+__device__ __forceinline__ uint32_t window32(uint64_t lo, uint64_t hi, uint32_t off) {
+  const uint32_t sh = off * 8;
+  uint64_t x = (sh == 0) ? lo : (sh < 64 ? ((lo >> sh) | (hi << (64 - sh))) : (hi >> (sh - 64)));
+  return (uint32_t)x;
+}
+
+struct DevHdr {
+  uint32_t b0;
+  uint32_t masked;
+  uint32_t mask;  // little-endian key bytes
+  uint32_t hlen;
+  uint64_t length;
+};
+
+// ws.VirtualReadHeader (read.go:19-84) on the 16 bytes at the cursor.
+// avail < 6 -> NEED_MORE (read.go:20-23); FIN/RSV/opcode (read.go:29-31);
+// MASK + len7 (read.go:33-49); BE16/BE64 extended length (read.go:60-77) with
+// the MSB check (read.go:71-73); key = last 4 header bytes (read.go:78-81).
+// avail < header length (Appendix A U1, ringbuffer-dependent in the reference)
+// -> NEED_MORE.
+__device__ __forceinline__ int parse_header(uint64_t lo, uint64_t hi, uint64_t avail, DevHdr& h) {
+  if (avail < 6) return GEVWS_NEED_MORE;
+  const uint32_t b0 = (uint32_t)(lo & 0xff);
+  const uint32_t b1 = (uint32_t)((lo >> 8) & 0xff);
+  const uint32_t masked = b1 >> 7;
+  const uint32_t len7 = b1 & 0x7f;
+  const uint32_t ext = len7 < 126 ? 0u : (len7 == 126 ? 2u : 8u);
+  const uint32_t hlen = 2 + ext + 4 * masked;
+  if (avail < hlen) return GEVWS_NEED_MORE;
+  uint64_t L;
+  if (len7 < 126) {
+    L = len7;
+  } else if (len7 == 126) {
+    L = (((lo >> 16) & 0xff) << 8) | ((lo >> 24) & 0xff);
+  } else {
+    L = __builtin_bswap64((lo >> 16) | (hi << 48));  // header bytes 2..9, big-endian
+    if (L >> 63) return GEVWS_ERR_LEN_MSB;
+  }
+  h.b0 = b0;
+  h.masked = masked;
+  h.mask = masked ? window32(lo, hi, 2 + ext) : 0u;
+  h.hlen = hlen;
+  h.length = L;
+  return GEVWS_OK;
+}
+
+__device__ __forceinline__ void load_window(const uint8_t* p, uint64_t& lo, uint64_t& hi) {
+  const u32x4 v = ld16u(p);
+  lo = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+  hi = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+}
+
+// Wave-level (64 lanes) inclusive scan of a u64.
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+// Block exclusive scan of NV u64 values per thread (blockDim.x = BS).
+// Returns exclusive prefixes in ex[], block totals in tot[].
+template <int BS, int NV>
+__device__ __forceinline__ void block_excl_scan(const uint64_t (&v)[NV], uint64_t (&ex)[NV],
+                                                uint64_t (&tot)[NV]) {
+  constexpr int NW = BS / 64;
+  __shared__ uint64_t s_w[NV][NW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t inc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    inc[k] = wave_incl_scan(v[k]);
+    if (lane == 63) s_w[k][w] = inc[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    uint64_t base = 0, all = 0;
+    for (int j = 0; j < NW; ++j) {
+      const uint64_t s = s_w[k][j];
+      base += (j < w) ? s : 0;
+      all += s;
+    }
+    ex[k] = base + inc[k] - v[k];
+    tot[k] = all;
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ 1. walk (count)
+__global__ __launch_bounds__(kWalkBlock) void k_walk_count(const uint8_t* __restrict__ in,
+                                                           const gevws_conn_in* __restrict__ conns,
+                                                           uint32_t n, gevws_conn_out* __restrict__ cout,
+                                                           uint64_t* __restrict__ blk) {
+  const uint32_t c = blockIdx.x * kWalkBlock + threadIdx.x;
+  uint64_t nf = 0, pb = 0, pl = 0, err = 0;
+  if (c < n) {
+    const gevws_conn_in ci = conns[c];
+    const uint8_t* s = in + ci.off;
+    uint64_t pos = 0;
+    int32_t st = GEVWS_OK;
+    for (;;) {
+      const uint64_t avail = ci.len - pos;
+      if (avail < 6) break;
+      uint64_t lo, hi;
+      load_window(s + pos, lo, hi);
+      DevHdr h;
+      const int r = parse_header(lo, hi, avail, h);
+      if (r != GEVWS_OK) {
+        if (r < 0) { st = r; err = 1; }
+        break;
+      }
+      if (avail - h.hlen < h.length) break;  // protocol.go:47 gate
+      ++nf;
+      pb += round16(h.length);
+      pl += h.length;
+      pos += h.hlen + h.length;
+    }
+    gevws_conn_out o;
+    o.first_frame = 0;
+    o.consumed = pos;
+    o.payload_base = pb;  // per-connection arena bytes; k_walk_emit turns it into a base
+    o.nframes = (uint32_t)nf;
+    o.status = st;
+    cout[c] = o;
+  }
+  // block partial sums
+  __shared__ uint64_t s_part[kBlkFields][kWalkBlock / 64];
+  const uint64_t vals[kBlkFields] = {nf, pb, pl, err};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kBlkFields; ++k) {
+    const uint64_t s = wave_sum(vals[k]);
+    if (lane == 0) s_part[k][w] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < kBlkFields) {
+    uint64_t s = 0;
+    for (int j = 0; j < kWalkBlock / 64; ++j) s += s_part[threadIdx.x][j];
+    blk[(uint64_t)blockIdx.x * kBlkFields + threadIdx.x] = s;
+  }
+}
+
+// ------------------------------------------------------------------ 2. scan of block partials
+__global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict__ blk, uint32_t nblk,
+                                                            uint64_t max_frames, uint64_t payload_cap,
+                                                            gevws_summary* __restrict__ sum) {
+  uint64_t carry[kBlkFields] = {0, 0, 0, 0};
+  for (uint32_t base = 0; base < nblk; base += kScanBlock) {
+    const uint32_t i = base + threadIdx.x;
+    uint64_t v[kBlkFields], ex[kBlkFields], tot[kBlkFields];
+#pragma unroll
+    for (int k = 0; k < kBlkFields; ++k) v[k] = (i < nblk) ? blk[(uint64_t)i * kBlkFields + k] : 0;
+    block_excl_scan<kScanBlock, kBlkFields>(v, ex, tot);
+    if (i < nblk) {
+      // fields 0/1 become exclusive bases (frames, arena bytes)
+      blk[(uint64_t)i * kBlkFields + 0] = carry[0] + ex[0];
+      blk[(uint64_t)i * kBlkFields + 1] = carry[1] + ex[1];
+    }
+#pragma unroll
+    for (int k = 0; k < kBlkFields; ++k) carry[k] += tot[k];
+  }
+  if (threadIdx.x == 0) {
+    gevws_summary s;
+    memset(&s, 0, sizeof(s));
+    s.frames = carry[0];
+    s.payload_bytes = carry[1];
+    s.payload_len = carry[2];
+    s.errors = carry[3];
+    s.status = (carry[0] > max_frames || carry[1] > payload_cap) ? GEVWS_ERR_CAPACITY : GEVWS_OK;
+    *sum = s;
+  }
+}
+
+// ------------------------------------------------------------------ 3. walk (emit)
+__global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restrict__ in,
+                                                          const gevws_conn_in* __restrict__ conns,
+                                                          uint32_t n, gevws_conn_out* __restrict__ cout,
+                                                          const uint64_t* __restrict__ blk,
+                                                          const gevws_summary* __restrict__ sum,
+                                                          gevws_frame* __restrict__ frames,
+                                                          uint32_t* __restrict__ tile_first) {
+  if (sum->status != GEVWS_OK) return;  // capacity error: nothing written
+  const uint32_t c = blockIdx.x * kWalkBlock + threadIdx.x;
+  uint64_t v[2] = {0, 0};
+  if (c < n) {
+    v[0] = cout[c].nframes;
+    v[1] = cout[c].payload_base;
+  }
+  uint64_t ex[2], tot[2];
+  block_excl_scan<kWalkBlock, 2>(v, ex, tot);
+  if (c >= n) return;
+  const uint64_t f0 = blk[(uint64_t)blockIdx.x * kBlkFields + 0] + ex[0];
+  const uint64_t p0 = blk[(uint64_t)blockIdx.x * kBlkFields + 1] + ex[1];
+  cout[c].first_frame = f0;
+  cout[c].payload_base = p0;
+  const gevws_conn_in ci = conns[c];
+  const uint8_t* s = in + ci.off;
+  uint64_t pos = 0, poff = p0;
+  const uint64_t cnt = v[0];
+  for (uint64_t k = 0; k < cnt; ++k) {
+    uint64_t lo, hi;
+    load_window(s + pos, lo, hi);
+    DevHdr h;
+    parse_header(lo, hi, ci.len - pos, h);  // succeeded in k_walk_count
+    gevws_frame fr;
+    fr.hdr.fin = (uint8_t)(h.b0 >> 7);
+    fr.hdr.rsv = (uint8_t)((h.b0 & 0x70) >> 4);
+    fr.hdr.opcode = (uint8_t)(h.b0 & 0x0f);
+    fr.hdr.masked = (uint8_t)h.masked;
+    memcpy(fr.hdr.mask, &h.mask, 4);
+    fr.hdr.length = (int64_t)h.length;
+    fr.payload_off = poff;
+    fr.src_off = ci.off + pos + h.hlen;
+    frames[f0 + k] = fr;
+    const uint64_t padded = round16(h.length);
+    // output tiles whose first byte lies in [poff, poff + padded)
+    for (uint64_t t = (poff + kTile - 1) / kTile; t * kTile < poff + padded; ++t)
+      tile_first[t] = (uint32_t)(f0 + k);
+    poff += padded;
+    pos += h.hlen + h.length;
+  }
+}
+
+// ------------------------------------------------------------------ 4. unmask / compact
+// Largest frame index f in [tile_first[t], tile_first[t+1]] with payload_off <= p.
+__device__ __forceinline__ uint64_t find_frame(const gevws_frame* __restrict__ frames,
+                                               const uint32_t* __restrict__ tile_first, uint64_t t,
+                                               uint64_t ntiles, uint64_t nframes, uint64_t p) {
+  uint64_t lo = tile_first[t];
+  uint64_t hi = (t + 1 < ntiles) ? (uint64_t)tile_first[t + 1] : nframes - 1;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi + 1) >> 1;
+    if (frames[mid].payload_off <= p) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ u32x4 keep_bytes(u32x4 x, int64_t rem) {
+  // zero bytes at positions >= rem (rem in 1..15): Go's make() zero-fill of the pad
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t valid = rem - 4 * j;
+    const uint32_t m = valid >= 4 ? 0xffffffffu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
+    x[j] &= m;
+  }
+  return x;
+}
+
+template <int U>
+__global__ __launch_bounds__(kUnmaskBlock) void k_unmask(const uint8_t* __restrict__ in,
+                                                         const gevws_frame* __restrict__ frames,
+                                                         const uint32_t* __restrict__ tile_first,
+                                                         const gevws_summary* __restrict__ sum,
+                                                         uint8_t* __restrict__ out) {
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t total = sum->payload_bytes;
+  const uint64_t nframes = sum->frames;
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint32_t lane_off = threadIdx.x * 16;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * U; t0 < ntiles; t0 += (uint64_t)gridDim.x * U) {
+    u32x4 v[U];
+    uint32_t key[U];
+    int64_t rem[U];
+    uint64_t p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t t = t0 + u;
+      p[u] = t * kTile + lane_off;
+      rem[u] = 0;
+      key[u] = 0;
+      v[u] = u32x4{0, 0, 0, 0};
+      if (t < ntiles && p[u] < total) {
+        const uint64_t f = find_frame(frames, tile_first, t, ntiles, nframes, p[u]);
+        const gevws_frame* fr = frames + f;
+        const uint64_t rel = p[u] - fr->payload_off;
+        rem[u] = fr->hdr.length - (int64_t)rel;
+        uint32_t k;
+        memcpy(&k, fr->hdr.mask, 4);
+        key[u] = fr->hdr.masked ? k : 0u;
+        v[u] = ld16u(in + fr->src_off + rel);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (rem[u] > 0) {
+        u32x4 x = v[u] ^ key[u];  // payload phase is 0 mod 4 at every 16-byte chunk
+        if (rem[u] < 16) x = keep_bytes(x, rem[u]);
+        __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + p[u]));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ ws.Cipher on a device buffer
+// p[i] ^= mask[(offset + i) & 3] for i in [0, n): 16-byte aligned chunks of the
+// address space; interior chunks use one rotated 32-bit key, edge chunks go
+// byte by byte.
+__global__ __launch_bounds__(256) void k_cipher(uint8_t* __restrict__ p, uint64_t n, uint32_t key,
+                                                uint64_t offset, uint64_t nchunks) {
+  const uint64_t a0 = reinterpret_cast<uint64_t>(p) & ~uint64_t(15);
+  const uint64_t pe = reinterpret_cast<uint64_t>(p) + n;
+  const uint32_t s = (uint32_t)((offset - reinterpret_cast<uint64_t>(p)) & 3);
+  const uint32_t krot = s ? ((key >> (8 * s)) | (key << (32 - 8 * s))) : key;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nchunks;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t a = a0 + 16 * k;
+    if (a >= reinterpret_cast<uint64_t>(p) && a + 16 <= pe) {
+      u32x4* q = reinterpret_cast<u32x4*>(a);
+      *q = *q ^ krot;
+    } else {
+      for (uint32_t b = 0; b < 16; ++b) {
+        const uint64_t x = a + b;
+        if (x >= reinterpret_cast<uint64_t>(p) && x < pe) {
+          const uint32_t idx = (uint32_t)((offset + (x - reinterpret_cast<uint64_t>(p))) & 3);
+          *reinterpret_cast<uint8_t*>(x) ^= (uint8_t)(key >> (8 * idx));
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ synthetic frames
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ u32x4 plain16(uint64_t seed, uint64_t g, uint64_t i) {
+  const uint64_t b = seed ^ (g * 0x9E3779B97F4A7C15ull);
+  const uint64_t w0 = splitmix64(b + (i >> 3));
+  const uint64_t w1 = splitmix64(b + (i >> 3) + 1);
+  return u32x4{(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+}
+
+__device__ __forceinline__ uint32_t synth_hlen(const gevws_synth_desc& d) {
+  return 2 + (d.len_form == 7 ? 0 : (d.len_form == 16 ? 2 : 8)) + (d.masked ? 4 : 0);
+}
+
+__global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ in,
+                                               const gevws_synth_desc* __restrict__ desc,
+                                               uint64_t n_frames, uint64_t seed) {
+  for (uint64_t g = blockIdx.x; g < n_frames; g += gridDim.x) {
+    const gevws_synth_desc d = desc[g];
+    const uint32_t hlen = synth_hlen(d);
+    uint8_t* h = in + d.hdr_off;
+    if (threadIdx.x == 0) {
+      h[0] = d.b0;
+      const uint8_t mbit = d.masked ? 0x80 : 0;
+      uint32_t e = 2;
+      if (d.len_form == 7) {
+        h[1] = mbit | (uint8_t)d.length;
+      } else if (d.len_form == 16) {
+        h[1] = mbit | 126;
+        h[2] = (uint8_t)(d.length >> 8);
+        h[3] = (uint8_t)d.length;
+        e = 4;
+      } else {
+        h[1] = mbit | 127;
+        for (int k = 0; k < 8; ++k) h[2 + k] = (uint8_t)(d.length >> (56 - 8 * k));
+        e = 10;
+      }
+      if (d.masked)
+        for (int k = 0; k < 4; ++k) h[e + k] = (uint8_t)(d.mask >> (8 * k));
+    }
+    uint8_t* pl = h + hlen;
+    const uint32_t key = d.masked ? d.mask : 0u;
+    for (uint64_t i = (uint64_t)threadIdx.x * 16; i < d.length; i += 256 * 16) {
+      const u32x4 x = plain16(seed, g, i) ^ key;
+      if (i + 16 <= d.length) {
+        __builtin_memcpy(pl + i, &x, 16);
+      } else {
+        for (uint32_t b = 0; b < d.length - i; ++b) pl[i + b] = (uint8_t)(x[b >> 2] >> (8 * (b & 3)));
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_synth_verify(const gevws_synth_desc* __restrict__ desc,
+                                                      uint64_t n_frames, uint64_t seed,
+                                                      const gevws_frame* __restrict__ frames,
+                                                      const uint8_t* __restrict__ payload,
+                                                      uint64_t payload_cap,
+                                                      unsigned long long* __restrict__ mismatch) {
+  uint64_t bad = 0;
+  for (uint64_t g = blockIdx.x; g < n_frames; g += gridDim.x) {
+    const gevws_synth_desc d = desc[g];
+    const gevws_frame fr = frames[g];
+    if (fr.payload_off > payload_cap || round16(d.length) > payload_cap - fr.payload_off) {
+      bad += threadIdx.x == 0 ? d.length + 1 : 0;  // record out of range: never dereferenced
+      continue;
+    }
+    if (threadIdx.x == 0) {
+      uint32_t k;
+      memcpy(&k, fr.hdr.mask, 4);
+      bad += fr.hdr.fin != (d.b0 >> 7);
+      bad += fr.hdr.rsv != ((d.b0 & 0x70) >> 4);
+      bad += fr.hdr.opcode != (d.b0 & 0x0f);
+      bad += fr.hdr.masked != d.masked;
+      bad += k != (d.masked ? d.mask : 0u);
+      bad += (uint64_t)fr.hdr.length != d.length;
+      bad += fr.src_off != d.hdr_off + synth_hlen(d);
+      bad += (fr.payload_off & 15) != 0;
+    }
+    const uint64_t padded = round16(d.length);
+    for (uint64_t i = (uint64_t)threadIdx.x * 16; i < padded; i += 256 * 16) {
+      u32x4 want = plain16(seed, g, i);
+      if (d.length - i < 16) want = keep_bytes(want, (int64_t)(d.length - i));
+      const u32x4 got = *reinterpret_cast<const u32x4*>(payload + fr.payload_off + i);
+      const u32x4 x = got ^ want;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        for (int b = 0; b < 4; ++b) bad += ((x[j] >> (8 * b)) & 0xff) != 0;
+    }
+  }
+  const uint64_t w = wave_sum(bad);
+  if ((threadIdx.x & 63) == 0 && w) atomicAdd(mismatch, (unsigned long long)w);
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+struct gevws_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  bool timing = false;
+  struct EventSet {
+    hipEvent_t e[5];
+  };
+  std::vector<EventSet> evs;  // one set per timed call since the last gevws_ctx_timing
+  size_t evs_used = 0;
+  gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+#define GEVWS_HIP(call)                                                                \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      fprintf(stderr, "[gevws] %s failed: %s\n", #call, hipGetErrorString(e_));          \
+      return GEVWS_ERR_DEVICE;                                                          \
+    }                                                                                   \
+  } while (0)
+
+hipStream_t pick_stream(gevws_ctx* ctx, void* stream) {
+  return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+int ensure_scratch(gevws_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->scratch_bytes) return GEVWS_OK;
+  if (ctx->scratch) {
+    GEVWS_HIP(hipDeviceSynchronize());
+    GEVWS_HIP(hipFree(ctx->scratch));
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+  }
+  size_t want = bytes + bytes / 4 + 4096;
+  GEVWS_HIP(hipMalloc(&ctx->scratch, want));
+  ctx->scratch_bytes = want;
+  return GEVWS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gevws_abi_version(void) { return GEVWS_ABI_VERSION; }
+
+const char* gevws_status_string(int s) {
+  switch (s) {
+    case GEVWS_OK: return "ok";
+    case GEVWS_NEED_MORE: return "header error: not enough";  // ws.ErrHeaderNotReady text
+    case GEVWS_ERR_LEN_MSB: return "header error: the most significant bit must be 0";
+    case GEVWS_ERR_CAPACITY: return "output capacity exceeded";
+    case GEVWS_ERR_INVALID: return "invalid argument";
+    case GEVWS_ERR_DEVICE: return "HIP device error";
+    case GEVWS_ERR_NOT_UPGRADED: return "websocket upgrade (handshake) not supported by this engine";
+    default: return "unknown status";
+  }
+}
+
+int gevws_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+gevws_ctx* gevws_ctx_create(int device) {
+  int n = gevws_device_count();
+  if (device < 0 || device >= n) {
+    fprintf(stderr, "[gevws] gevws_ctx_create: device %d not available (%d visible)\n", device, n);
+    return nullptr;
+  }
+  DeviceGuard g(device);
+  gevws_ctx* ctx = new gevws_ctx();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return nullptr;
+  }
+  if (hipMalloc(reinterpret_cast<void**>(&ctx->d_sum), sizeof(gevws_summary)) != hipSuccess) {
+    gevws_ctx_destroy(ctx);
+    return nullptr;
+  }
+  return ctx;
+}
+
+void gevws_ctx_destroy(gevws_ctx* ctx) {
+  if (!ctx) return;
+  DeviceGuard g(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->d_sum) (void)hipFree(ctx->d_sum);
+  for (auto& set : ctx->evs)
+    for (auto& e : set.e) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int gevws_ctx_device(const gevws_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+int gevws_ctx_set_timing(gevws_ctx* ctx, int enable) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  ctx->timing = enable != 0;
+  return GEVWS_OK;
+}
+
+int gevws_ctx_timing(gevws_ctx* ctx, float ms_sum[4], uint32_t* calls) {
+  if (!ctx || !ms_sum || !calls) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  float acc[4] = {0, 0, 0, 0};
+  for (size_t k = 0; k < ctx->evs_used; ++k) {
+    auto& set = ctx->evs[k];
+    GEVWS_HIP(hipEventSynchronize(set.e[4]));
+    for (int i = 0; i < 4; ++i) {
+      float t = 0;
+      GEVWS_HIP(hipEventElapsedTime(&t, set.e[i], set.e[i + 1]));
+      acc[i] += t;
+    }
+  }
+  for (int i = 0; i < 4; ++i) ms_sum[i] = acc[i];
+  *calls = (uint32_t)ctx->evs_used;
+  ctx->evs_used = 0;
+  return GEVWS_OK;
+}
+
+int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64_t in_bytes,
+                             const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames,
+                             uint64_t max_frames, uint8_t* d_payload, uint64_t payload_cap,
+                             gevws_conn_out* d_conn_out, gevws_summary* d_summary) {
+  (void)in_bytes;
+  if (!ctx || !d_summary) return GEVWS_ERR_INVALID;
+  if (n_conns && (!d_in || !d_conns || !d_conn_out)) return GEVWS_ERR_INVALID;
+  if (max_frames > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;  // tile map holds 32-bit frame ids
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  const uint32_t nblk = (n_conns + kWalkBlock - 1) / kWalkBlock;
+  const uint64_t ntiles_cap = (payload_cap + kTile - 1) / kTile + 1;
+  const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
+  int r = ensure_scratch(ctx, blk_bytes + ntiles_cap * sizeof(uint32_t));
+  if (r != GEVWS_OK) return r;
+  uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
+  uint32_t* tile_first = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes);
+  const bool timed = ctx->timing;
+  hipEvent_t* ev = nullptr;
+  if (timed) {
+    if (ctx->evs_used == ctx->evs.size()) {
+      gevws_ctx::EventSet set;
+      for (auto& e : set.e) GEVWS_HIP(hipEventCreate(&e));
+      ctx->evs.push_back(set);
+    }
+    ev = ctx->evs[ctx->evs_used++].e;
+    GEVWS_HIP(hipEventRecord(ev[0], st));
+  }
+  if (nblk) k_walk_count<<<nblk, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk);
+  if (timed) GEVWS_HIP(hipEventRecord(ev[1], st));
+  k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
+  if (timed) GEVWS_HIP(hipEventRecord(ev[2], st));
+  if (nblk)
+    k_walk_emit<<<nblk, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, d_summary,
+                                              d_frames, tile_first);
+  if (timed) GEVWS_HIP(hipEventRecord(ev[3], st));
+  const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
+  uint64_t grid = (ntiles + kUnmaskUnroll - 1) / kUnmaskUnroll;
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+  k_unmask<kUnmaskUnroll><<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary,
+                                                                    d_payload);
+  if (timed) GEVWS_HIP(hipEventRecord(ev[4], st));
+  GEVWS_HIP(hipGetLastError());
+  return GEVWS_OK;
+}
+
+int gevws_decode_batch(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64_t in_bytes,
+                       const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames,
+                       uint64_t max_frames, uint8_t* d_payload, uint64_t payload_cap,
+                       gevws_conn_out* d_conn_out, gevws_summary* h_summary) {
+  if (!ctx || !h_summary) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  gevws_summary* d_sum = ctx->d_sum;
+  int r = gevws_decode_batch_async(ctx, stream, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames,
+                                   d_payload, payload_cap, d_conn_out, d_sum);
+  if (r == GEVWS_OK) {
+    GEVWS_HIP(hipMemcpyAsync(h_summary, d_sum, sizeof(gevws_summary), hipMemcpyDeviceToHost, st));
+    GEVWS_HIP(hipStreamSynchronize(st));
+    r = h_summary->status;
+  }
+  return r;
+}
+
+int gevws_cipher_async(gevws_ctx* ctx, void* stream, uint8_t* d_p, uint64_t n, const uint8_t mask[4],
+                       uint64_t offset) {
+  if (!ctx || !mask || (n && !d_p)) return GEVWS_ERR_INVALID;
+  if (n == 0) return GEVWS_OK;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  uint32_t key;
+  memcpy(&key, mask, 4);
+  const uint64_t a0 = reinterpret_cast<uint64_t>(d_p) & ~uint64_t(15);
+  const uint64_t nchunks = (reinterpret_cast<uint64_t>(d_p) + n - a0 + 15) / 16;
+  uint64_t grid = (nchunks + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  k_cipher<<<(uint32_t)grid, 256, 0, st>>>(d_p, n, key, offset, nchunks);
+  GEVWS_HIP(hipGetLastError());
+  return GEVWS_OK;
+}
+
+int gevws_synth_async(gevws_ctx* ctx, void* stream, uint8_t* d_in, const gevws_synth_desc* d_desc,
+                      uint64_t n_frames, uint64_t seed) {
+  if (!ctx || (n_frames && (!d_in || !d_desc))) return GEVWS_ERR_INVALID;
+  if (n_frames == 0) return GEVWS_OK;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  uint64_t grid = n_frames < (1u << 20) ? n_frames : (1u << 20);
+  k_synth<<<(uint32_t)grid, 256, 0, st>>>(d_in, d_desc, n_frames, seed);
+  GEVWS_HIP(hipGetLastError());
+  return GEVWS_OK;
+}
+
+int gevws_synth_verify_async(gevws_ctx* ctx, void* stream, const gevws_synth_desc* d_desc,
+                             uint64_t n_frames, uint64_t seed, const gevws_frame* d_frames,
+                             const uint8_t* d_payload, uint64_t payload_cap, uint64_t* d_mismatch) {
+  if (!ctx || !d_mismatch || (n_frames && (!d_desc || !d_frames || !d_payload))) return GEVWS_ERR_INVALID;
+  if (n_frames == 0) return GEVWS_OK;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  uint64_t grid = n_frames < (1u << 16) ? n_frames : (1u << 16);
+  k_synth_verify<<<(uint32_t)grid, 256, 0, st>>>(d_desc, n_frames, seed, d_frames, d_payload, payload_cap,
+                                                  reinterpret_cast<unsigned long long*>(d_mismatch));
+  GEVWS_HIP(hipGetLastError());
+  return GEVWS_OK;
+}
+
+}  // extern "C"

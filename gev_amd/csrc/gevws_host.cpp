@@ -1,0 +1,375 @@
+// gevws_host.cpp -- C++ host side above the device ABI, mirroring the
+// reference's plugin surface for the decode path (Go is absent from this image,
+// so the host side is C++; INTEGRATION.md shows the cgo binding):
+//
+//   RingBuffer  ~ github.com/Allenxuxu/ringbuffer v0.0.11 as gev uses it
+//                 (Write / Length / PeekAll / Retrieve; virtual cursor calls at
+//                 read.go:20,27,63 and protocol.go:47-60 are replaced by the
+//                 device header walk).  Growable circular buffer.
+//   Connection  ~ gev.Connection's KeyValueContext entries the websocket plugin
+//                 keeps (protocol.go:11-14, 28-39) plus the queue of frames
+//                 decoded for it and not yet delivered.
+//   Protocol    ~ websocket.Protocol (plugins/websocket/protocol.go:16-69):
+//                 UnPacket returns one frame per call exactly like the
+//                 reference; its decode runs on the device, batched across
+//                 every connection handed to UnPacketBatch.
+//
+// The decode itself is never done on the host: this file only stages bytes,
+// launches gevws_decode_batch and hands out the device's results.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <vector>
+
+#include "gevws.h"
+
+namespace gevws {
+
+// ------------------------------------------------------------------ logging (gev/log)
+// log.Error prints with the "[Gev]" prefix unless GEV_LOG_LEVEL silences it
+// (log/log.go:51-62).
+static bool log_errors_enabled() {
+  static int level = [] {
+    const char* s = std::getenv("GEV_LOG_LEVEL");
+    if (!s) return 2;
+    if (!strcmp(s, "FATAL") || !strcmp(s, "fatal")) return 0;
+    if (!strcmp(s, "INFO") || !strcmp(s, "info")) return 1;
+    return 2;
+  }();
+  return level >= 1;
+}
+static void log_error(const char* what, int status) {
+  if (log_errors_enabled()) fprintf(stderr, "[Gev] ERROR %s%s\n", what, gevws_status_string(status));
+}
+
+// ------------------------------------------------------------------ ring buffer
+class RingBuffer {
+ public:
+  explicit RingBuffer(uint64_t size) : buf_(size ? size : 1), size_(buf_.size()) {}
+
+  uint64_t Length() const {
+    if (empty_) return 0;
+    return w_ > r_ ? w_ - r_ : size_ - r_ + w_;
+  }
+  uint64_t Capacity() const { return size_; }
+  bool IsEmpty() const { return empty_; }
+
+  uint64_t Write(const uint8_t* p, uint64_t n) {
+    if (n == 0) return 0;
+    const uint64_t free_bytes = size_ - Length();
+    if (n > free_bytes) grow(Length() + n);
+    uint64_t first = std::min<uint64_t>(n, size_ - w_);
+    memcpy(buf_.data() + w_, p, first);
+    if (n > first) memcpy(buf_.data(), p + first, n - first);
+    w_ = (w_ + n) % size_;
+    empty_ = false;
+    return n;
+  }
+
+  void PeekAll(const uint8_t** first, uint64_t* n1, const uint8_t** end, uint64_t* n2) const {
+    *first = *end = nullptr;
+    *n1 = *n2 = 0;
+    if (empty_) return;
+    if (w_ > r_) {
+      *first = buf_.data() + r_;
+      *n1 = w_ - r_;
+      return;
+    }
+    *first = buf_.data() + r_;
+    *n1 = size_ - r_;
+    if (w_ > 0) {
+      *end = buf_.data();
+      *n2 = w_;
+    }
+  }
+
+  void Retrieve(uint64_t n) {
+    const uint64_t len = Length();
+    if (n >= len) {
+      r_ = w_ = 0;
+      empty_ = true;
+      return;
+    }
+    r_ = (r_ + n) % size_;
+  }
+
+ private:
+  void grow(uint64_t need) {
+    uint64_t ns = size_;
+    while (ns < need) ns *= 2;
+    std::vector<uint8_t> nb(ns);
+    const uint8_t *a, *b;
+    uint64_t na, nb2;
+    PeekAll(&a, &na, &b, &nb2);
+    if (na) memcpy(nb.data(), a, na);
+    if (nb2) memcpy(nb.data() + na, b, nb2);
+    const uint64_t len = na + nb2;
+    buf_.swap(nb);
+    size_ = ns;
+    r_ = 0;
+    w_ = len % size_;
+    empty_ = len == 0;
+  }
+
+  std::vector<uint8_t> buf_;
+  uint64_t size_;
+  uint64_t r_ = 0, w_ = 0;
+  bool empty_ = true;
+};
+
+// ------------------------------------------------------------------ connection
+struct Delivered {
+  gevws_header hdr;
+  uint64_t frame_bytes;  // h + L, consumed from the ring on delivery
+  uint64_t payload_off;  // into the batch's host arena
+  std::shared_ptr<std::vector<uint8_t>> arena;
+};
+
+struct Connection {
+  bool upgraded = false;                 // "gev_ws_upgraded" (protocol.go:12, 36)
+  int poisoned = GEVWS_OK;               // sticky ERR_LEN_MSB (Appendix A P9/U3)
+  std::deque<Delivered> queue;           // decoded, not yet returned by UnPacket
+  std::shared_ptr<std::vector<uint8_t>> current;  // keeps the last payload alive
+};
+
+// ------------------------------------------------------------------ protocol
+class Protocol {
+ public:
+  explicit Protocol(gevws_ctx* ctx) : ctx_(ctx) {}
+  ~Protocol() { release(); }
+
+  int UnPacket(Connection* c, RingBuffer* ring, gevws_header* hdr, const uint8_t** out,
+               uint64_t* out_len) {
+    *out = nullptr;
+    *out_len = 0;
+    if (!c->upgraded) {  // protocol.go:28-35: the handshake path
+      log_error("Websocket Upgrade :", GEVWS_ERR_NOT_UPGRADED);
+      return GEVWS_ERR_NOT_UPGRADED;
+    }
+    if (c->queue.empty() && c->poisoned == GEVWS_OK) {
+      Connection* cs[1] = {c};
+      RingBuffer* rs[1] = {ring};
+      int64_t r = UnPacketBatch(cs, rs, 1);
+      if (r < 0) return (int)r;
+    }
+    if (c->queue.empty()) {
+      if (c->poisoned != GEVWS_OK) {  // protocol.go:41-45: log and return (nil, nil)
+        log_error("", c->poisoned);
+        return c->poisoned;
+      }
+      return GEVWS_NEED_MORE;  // ErrHeaderNotReady / gate: silent (nil, nil)
+    }
+    Delivered d = std::move(c->queue.front());
+    c->queue.pop_front();
+    ring->Retrieve(d.frame_bytes);  // VirtualFlush + Read (protocol.go:48-51)
+    c->current = d.arena;
+    *hdr = d.hdr;
+    *out = d.arena->data() + d.payload_off;
+    *out_len = (uint64_t)d.hdr.length;
+    return GEVWS_OK;
+  }
+
+  // One device pass over every listed connection's buffered bytes.
+  int64_t UnPacketBatch(Connection* const* conns, RingBuffer* const* rings, uint32_t n) {
+    // Connections that already hold undelivered frames (or are poisoned) are
+    // skipped: their ring prefix is already decoded.
+    std::vector<uint32_t> sel;
+    sel.reserve(n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (!conns[i]->upgraded || !conns[i]->queue.empty() || conns[i]->poisoned != GEVWS_OK) continue;
+      const uint64_t len = rings[i]->Length();
+      if (len < 6) continue;  // read.go:20-23: nothing can be decoded
+      sel.push_back(i);
+      total += len;
+    }
+    if (sel.empty()) return 0;
+    const uint32_t m = (uint32_t)sel.size();
+    const int dev = gevws_ctx_device(ctx_);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+
+    // stage: PeekAll segments joined per connection into pinned memory
+    std::vector<gevws_conn_in> cin(m);
+    if (!grow_host(&h_in_, &h_in_cap_, total + GEVWS_IN_PAD)) return fail(prev, dev);
+    uint64_t off = 0;
+    for (uint32_t j = 0; j < m; ++j) {
+      const uint8_t *a, *b;
+      uint64_t na, nb;
+      rings[sel[j]]->PeekAll(&a, &na, &b, &nb);
+      memcpy(h_in_ + off, a, na);
+      if (nb) memcpy(h_in_ + off + na, b, nb);
+      cin[j] = {off, na + nb};
+      off += na + nb;
+    }
+    memset(h_in_ + off, 0, GEVWS_IN_PAD);
+    // first attempt sized for the usual case; on ERR_CAPACITY the summary
+    // carries the exact sizes and the batch is run once more
+    uint64_t max_frames = std::min<uint64_t>(total / 2 + 1, 0xFFFFFFFFull);
+    uint64_t payload_cap = total + 16 * std::min<uint64_t>(max_frames, total / 64 + 64) + 64;
+    gevws_summary sum{};
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      if (!grow_dev(&d_in_, &d_in_cap_, total + GEVWS_IN_PAD) ||
+          !grow_dev(&d_conns_, &d_conns_cap_, m * sizeof(gevws_conn_in)) ||
+          !grow_dev(&d_cout_, &d_cout_cap_, m * sizeof(gevws_conn_out)) ||
+          !grow_dev(&d_frames_, &d_frames_cap_, max_frames * sizeof(gevws_frame)) ||
+          !grow_dev(&d_payload_, &d_payload_cap_, payload_cap + 16))
+        return fail(prev, dev);
+      hipStream_t st = nullptr;  // the context's stream is used by the decode; copies sync below
+      if (hipMemcpy(d_in_, h_in_, total + GEVWS_IN_PAD, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d_conns_, cin.data(), m * sizeof(gevws_conn_in), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(prev, dev);
+      (void)st;
+      int r = gevws_decode_batch(ctx_, nullptr, (const uint8_t*)d_in_, total, (gevws_conn_in*)d_conns_, m,
+                                 (gevws_frame*)d_frames_, max_frames, (uint8_t*)d_payload_, payload_cap,
+                                 (gevws_conn_out*)d_cout_, &sum);
+      if (r == GEVWS_ERR_CAPACITY && attempt == 0) {
+        max_frames = std::max<uint64_t>(sum.frames, 1);
+        payload_cap = std::max<uint64_t>(sum.payload_bytes, 16);
+        continue;
+      }
+      if (r != GEVWS_OK) {
+        if (prev != dev) (void)hipSetDevice(prev);
+        return r;
+      }
+      break;
+    }
+    // results back to the host
+    std::vector<gevws_conn_out> cout(m);
+    std::vector<gevws_frame> fr(sum.frames);
+    auto arena = std::make_shared<std::vector<uint8_t>>(sum.payload_bytes ? sum.payload_bytes : 1);
+    if (hipMemcpy(cout.data(), d_cout_, m * sizeof(gevws_conn_out), hipMemcpyDeviceToHost) != hipSuccess ||
+        (sum.frames && hipMemcpy(fr.data(), d_frames_, sum.frames * sizeof(gevws_frame),
+                                 hipMemcpyDeviceToHost) != hipSuccess) ||
+        (sum.payload_bytes && hipMemcpy(arena->data(), d_payload_, sum.payload_bytes,
+                                        hipMemcpyDeviceToHost) != hipSuccess))
+      return fail(prev, dev);
+    if (prev != dev) (void)hipSetDevice(prev);
+    // hand the frames to their connections in stream order
+    for (uint32_t j = 0; j < m; ++j) {
+      Connection* c = conns[sel[j]];
+      const gevws_conn_out& o = cout[j];
+      uint64_t prev_end = cin[j].off;
+      for (uint32_t k = 0; k < o.nframes; ++k) {
+        const gevws_frame& f = fr[o.first_frame + k];
+        Delivered d;
+        d.hdr = f.hdr;
+        d.frame_bytes = f.src_off + (uint64_t)f.hdr.length - prev_end;
+        d.payload_off = f.payload_off;
+        d.arena = arena;
+        prev_end = f.src_off + (uint64_t)f.hdr.length;
+        c->queue.push_back(std::move(d));
+      }
+      if (o.status < 0) c->poisoned = o.status;
+    }
+    return (int64_t)sum.frames;
+  }
+
+ private:
+  int64_t fail(int prev, int dev) {
+    if (prev != dev) (void)hipSetDevice(prev);
+    log_error("device: ", GEVWS_ERR_DEVICE);
+    return GEVWS_ERR_DEVICE;
+  }
+  static bool grow_host(uint8_t** p, uint64_t* cap, uint64_t need) {
+    if (need <= *cap) return true;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    uint64_t want = std::max<uint64_t>(need + need / 2, 1 << 16);
+    if (hipHostMalloc((void**)p, want, hipHostMallocDefault) != hipSuccess) {
+      *cap = 0;
+      return false;
+    }
+    *cap = want;
+    return true;
+  }
+  static bool grow_dev(void** p, uint64_t* cap, uint64_t need) {
+    if (need <= *cap && *p) return true;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    uint64_t want = std::max<uint64_t>(need + need / 2, 4096);
+    if (hipMalloc(p, want) != hipSuccess) {
+      *cap = 0;
+      return false;
+    }
+    *cap = want;
+    return true;
+  }
+  void release() {
+    if (h_in_) (void)hipHostFree(h_in_);
+    for (void* p : {d_in_, d_conns_, d_cout_, d_frames_, d_payload_})
+      if (p) (void)hipFree(p);
+  }
+
+  gevws_ctx* ctx_;
+  uint8_t* h_in_ = nullptr;
+  uint64_t h_in_cap_ = 0;
+  void *d_in_ = nullptr, *d_conns_ = nullptr, *d_cout_ = nullptr, *d_frames_ = nullptr, *d_payload_ = nullptr;
+  uint64_t d_in_cap_ = 0, d_conns_cap_ = 0, d_cout_cap_ = 0, d_frames_cap_ = 0, d_payload_cap_ = 0;
+};
+
+}  // namespace gevws
+
+struct gevws_ring : gevws::RingBuffer {
+  using gevws::RingBuffer::RingBuffer;
+};
+struct gevws_conn : gevws::Connection {};
+struct gevws_protocol : gevws::Protocol {
+  using gevws::Protocol::Protocol;
+};
+
+extern "C" {
+
+gevws_ring* gevws_ring_new(uint64_t size) { return new gevws_ring(size); }
+void gevws_ring_free(gevws_ring* r) { delete r; }
+uint64_t gevws_ring_write(gevws_ring* r, const uint8_t* p, uint64_t n) { return r->Write(p, n); }
+uint64_t gevws_ring_length(const gevws_ring* r) { return r->Length(); }
+uint64_t gevws_ring_capacity(const gevws_ring* r) { return r->Capacity(); }
+void gevws_ring_peek_all(const gevws_ring* r, const uint8_t** first, uint64_t* n_first, const uint8_t** end,
+                         uint64_t* n_end) {
+  r->PeekAll(first, n_first, end, n_end);
+}
+void gevws_ring_retrieve(gevws_ring* r, uint64_t n) { r->Retrieve(n); }
+
+gevws_conn* gevws_conn_new(void) { return new gevws_conn(); }
+void gevws_conn_free(gevws_conn* c) { delete c; }
+void gevws_conn_set_upgraded(gevws_conn* c, int upgraded) { c->upgraded = upgraded != 0; }
+int gevws_conn_upgraded(const gevws_conn* c) { return c->upgraded ? 1 : 0; }
+uint64_t gevws_conn_pending(const gevws_conn* c) { return c->queue.size(); }
+
+gevws_protocol* gevws_protocol_new(gevws_ctx* ctx) { return ctx ? new gevws_protocol(ctx) : nullptr; }
+void gevws_protocol_free(gevws_protocol* p) { delete p; }
+
+int gevws_protocol_unpacket(gevws_protocol* p, gevws_conn* c, gevws_ring* ring, gevws_header* ctx_out,
+                            const uint8_t** out, uint64_t* out_len) {
+  if (!p || !c || !ring || !ctx_out || !out || !out_len) return GEVWS_ERR_INVALID;
+  return p->UnPacket(c, ring, ctx_out, out, out_len);
+}
+
+int64_t gevws_protocol_unpacket_batch(gevws_protocol* p, gevws_conn* const* conns, gevws_ring* const* rings,
+                                      uint32_t n) {
+  if (!p || (n && (!conns || !rings))) return GEVWS_ERR_INVALID;
+  std::vector<gevws::Connection*> cs(n);
+  std::vector<gevws::RingBuffer*> rs(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    cs[i] = conns[i];
+    rs[i] = rings[i];
+  }
+  return p->UnPacketBatch(cs.data(), rs.data(), n);
+}
+
+const uint8_t* gevws_protocol_packet(gevws_protocol* p, gevws_conn* c, const uint8_t* data, uint64_t n,
+                                     uint64_t* out_len) {
+  (void)p;
+  (void)c;
+  if (out_len) *out_len = n;
+  return data;  // protocol.go:67-69: Packet returns data unchanged
+}
+
+}  // extern "C"

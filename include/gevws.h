@@ -1,0 +1,237 @@
+/*
+ * gevws.h -- C ABI of the MI355X-native WebSocket frame-decode / payload-unmask
+ * engine (gev_amd/libgevws.so).
+ *
+ * This is the drop-in boundary for gev's websocket Protocol plugin
+ * (plugins/websocket/protocol.go:27-64, installed via gev.CustomProtocol,
+ * options.go:83-87).  Every entry point names the reference interface it
+ * replaces.  Conventions: plain C structs, caller-owned buffers, nothing
+ * retained after return, int status (>= 0 ok, < 0 error).  One gevws_ctx per
+ * event loop (thread-confined: it owns device scratch); no global mutable
+ * state beyond one-time HIP runtime init.  See INTEGRATION.md for the cgo
+ * binding a gev maintainer would add.
+ */
+#ifndef GEVWS_H
+#define GEVWS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
+
+#define GEVWS_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status codes */
+enum {
+    GEVWS_OK = 0,
+    GEVWS_NEED_MORE = 1,          /* (nil, nil): ws.ErrHeaderNotReady or the
+                                     completeness gate failed (read.go:20-23,
+                                     protocol.go:47, 59-61) */
+    GEVWS_ERR_LEN_MSB = -1,       /* ws.ErrHeaderLengthMSB (read.go:12-16, 71-73);
+                                     the connection stream is poisoned */
+    GEVWS_ERR_CAPACITY = -2,      /* output records / payload arena too small;
+                                     the summary holds the exact sizes needed */
+    GEVWS_ERR_INVALID = -3,       /* bad argument */
+    GEVWS_ERR_DEVICE = -4,        /* HIP runtime error */
+    GEVWS_ERR_NOT_UPGRADED = -5   /* UnPacket before the handshake (protocol.go:28-37);
+                                     the handshake is out of scope, see DESIGN.md */
+};
+
+/* Readable slack the caller must provide after the last byte of a device input
+ * arena (kernels read whole 16-byte vectors). */
+#define GEVWS_IN_PAD 64
+/* Every payload in the output arena starts on this boundary. */
+#define GEVWS_PAYLOAD_ALIGN 16
+/* Output-arena tile (bytes) of the unmask kernel's work map. */
+#define GEVWS_TILE 4096
+
+/* ws.Header, plugins/websocket/ws/frame.go:169-176.  Byte-identical to the Go
+ * struct {Fin bool; Rsv byte; OpCode OpCode; Masked bool; Mask [4]byte;
+ * Length int64} (offsets 0,1,2,3,4..7,8..15; 16 bytes). */
+typedef struct gevws_header {
+    uint8_t fin;
+    uint8_t rsv;
+    uint8_t opcode;
+    uint8_t masked;
+    uint8_t mask[4];
+    int64_t length;
+} gevws_header;
+
+/* One connection's buffered bytes inside the batch input arena: the linear
+ * join of its ring buffer's PeekAll() segments (connection.go:220-251). */
+typedef struct gevws_conn_in {
+    uint64_t off;
+    uint64_t len;
+} gevws_conn_in;
+
+/* One decoded frame = one (ctx, out) pair UnPacket would have returned
+ * (protocol.go:57-58).  Records are ordered by connection, then stream order.
+ * The unmasked payload is payload_arena[payload_off, payload_off+hdr.length);
+ * src_off is the absolute input-arena offset of the payload's first byte, so
+ * the frame's header length is src_off minus the end of the previous frame. */
+typedef struct gevws_frame {
+    gevws_header hdr;
+    uint64_t payload_off;
+    uint64_t src_off;
+} gevws_frame;
+
+/* Per-connection result: what the handlerProtocol loop (connection.go:208-218)
+ * would have consumed before UnPacket returned (nil, nil). */
+typedef struct gevws_conn_out {
+    uint64_t first_frame;   /* index of its first record */
+    uint64_t consumed;      /* bytes of complete frames (sum of h + L) */
+    uint64_t payload_base;  /* arena offset of its first payload */
+    uint32_t nframes;
+    int32_t status;         /* GEVWS_OK or GEVWS_ERR_LEN_MSB */
+} gevws_conn_out;
+
+/* Batch totals (written on the device). */
+typedef struct gevws_summary {
+    uint64_t frames;        /* decoded frames */
+    uint64_t payload_bytes; /* arena bytes used (16-byte rounded lengths) */
+    uint64_t payload_len;   /* sum of payload lengths */
+    uint64_t errors;        /* connections with status < 0 */
+    int32_t status;         /* GEVWS_OK or GEVWS_ERR_CAPACITY */
+    uint32_t reserved0;
+    uint64_t reserved[3];
+} gevws_summary;
+
+typedef struct gevws_ctx gevws_ctx;
+
+/* ---------------------------------------------------------------- library */
+int gevws_abi_version(void);
+const char *gevws_status_string(int status);
+int gevws_device_count(void);
+
+/* One context per event loop (the reference keeps one per-connection header
+ * scratch, protocol.go:37; the batch engine keeps its scratch per loop). */
+gevws_ctx *gevws_ctx_create(int device);
+void gevws_ctx_destroy(gevws_ctx *ctx);
+int gevws_ctx_device(const gevws_ctx *ctx);
+/* Per-phase HIP-event timing of the following decode calls (0 = off). */
+int gevws_ctx_set_timing(gevws_ctx *ctx, int enable);
+/* Waits for the timed calls since the previous query and returns the summed
+ * ms per phase -- [0] header walk (count), [1] scan, [2] header walk (emit),
+ * [3] unmask/compact -- and the number of calls; then resets. */
+int gevws_ctx_timing(gevws_ctx *ctx, float ms_sum[4], uint32_t *calls);
+
+/* ---------------------------------------------------------------- hot path
+ * Device-resident batch decode: for every connection, repeated
+ * websocket.(*Protocol).UnPacket (plugins/websocket/protocol.go:38-62 ->
+ * ws.VirtualReadHeader read.go:19-84 -> completeness gate protocol.go:47 ->
+ * payload copy protocol.go:50-51 -> ws.Cipher cipher.go:14-53) until it would
+ * return (nil, nil), exactly as Connection.handlerProtocol drives it
+ * (connection.go:208-218).  All pointers d_* are device pointers; d_in must
+ * have GEVWS_IN_PAD readable bytes past in_bytes.  Enqueued on `stream`
+ * (hipStream_t, NULL = the context's default stream).  Returns GEVWS_OK when
+ * enqueued; the batch's own outcome is d_summary->status. */
+int gevws_decode_batch_async(gevws_ctx *ctx, void *stream, const uint8_t *d_in, uint64_t in_bytes,
+                             const gevws_conn_in *d_conns, uint32_t n_conns,
+                             gevws_frame *d_frames, uint64_t max_frames,
+                             uint8_t *d_payload, uint64_t payload_cap,
+                             gevws_conn_out *d_conn_out, gevws_summary *d_summary);
+
+/* Synchronous form: same work, waits, copies the summary to *h_summary and
+ * returns its status. */
+int gevws_decode_batch(gevws_ctx *ctx, void *stream, const uint8_t *d_in, uint64_t in_bytes,
+                       const gevws_conn_in *d_conns, uint32_t n_conns, gevws_frame *d_frames,
+                       uint64_t max_frames, uint8_t *d_payload, uint64_t payload_cap,
+                       gevws_conn_out *d_conn_out, gevws_summary *h_summary);
+
+/* ws.Cipher(payload, mask, offset), plugins/websocket/ws/cipher.go:14-53, on a
+ * device buffer in place: p[i] ^= mask[(offset+i) % 4]. */
+int gevws_cipher_async(gevws_ctx *ctx, void *stream, uint8_t *d_p, uint64_t n,
+                       const uint8_t mask[4], uint64_t offset);
+
+/* ---------------------------------------------------------------- synthetic batches
+ * Device-side frame generator used by the bench and the full-size property
+ * tests (no 64 GiB host buffer is ever built).  d_desc describes each frame:
+ * header position in the arena, payload length, key, first header byte, and
+ * length form (7, 16 or 64 bit).  Payload plaintext byte i of frame g is
+ * byte (i & 7) of splitmix64(seed ^ (g * 0x9E3779B97F4A7C15) + (i >> 3)). */
+typedef struct gevws_synth_desc {
+    uint64_t hdr_off;   /* arena offset of the frame's first header byte */
+    uint64_t length;    /* payload length */
+    uint32_t mask;      /* key bytes, little-endian (mask[0] = low byte) */
+    uint8_t b0;         /* FIN | RSV | opcode */
+    uint8_t len_form;   /* 7, 16 or 64 */
+    uint8_t masked;
+    uint8_t pad;
+} gevws_synth_desc;
+
+int gevws_synth_async(gevws_ctx *ctx, void *stream, uint8_t *d_in, const gevws_synth_desc *d_desc,
+                      uint64_t n_frames, uint64_t seed);
+/* Property check of a decoded batch against the generator: counts mismatching
+ * header fields, payload bytes (decode(mask(P)) == P) and non-zero pad bytes
+ * into *d_mismatch (device uint64, accumulated).  Frame g of the batch must be
+ * frame g of d_desc; records pointing outside [0, payload_cap) count as
+ * mismatches and are not dereferenced. */
+int gevws_synth_verify_async(gevws_ctx *ctx, void *stream, const gevws_synth_desc *d_desc,
+                             uint64_t n_frames, uint64_t seed, const gevws_frame *d_frames,
+                             const uint8_t *d_payload, uint64_t payload_cap, uint64_t *d_mismatch);
+
+/* ---------------------------------------------------------------- host mirror
+ * C++ host side above the device ABI, mirroring the reference's plugin
+ * surface for this path (gev.Protocol, protocol.go:10-13; websocket.Protocol,
+ * plugins/websocket/protocol.go:16-69; ringbuffer.RingBuffer as used at
+ * read.go:20,27,63, protocol.go:47-60, connection.go:232-242). */
+typedef struct gevws_ring gevws_ring;
+typedef struct gevws_conn gevws_conn;
+typedef struct gevws_protocol gevws_protocol;
+
+/* ringbuffer.New(size) / Write / Length / PeekAll / Retrieve / IsEmpty. */
+gevws_ring *gevws_ring_new(uint64_t size);
+void gevws_ring_free(gevws_ring *r);
+uint64_t gevws_ring_write(gevws_ring *r, const uint8_t *p, uint64_t n);
+uint64_t gevws_ring_length(const gevws_ring *r);
+uint64_t gevws_ring_capacity(const gevws_ring *r);
+void gevws_ring_peek_all(const gevws_ring *r, const uint8_t **first, uint64_t *n_first,
+                         const uint8_t **end, uint64_t *n_end);
+void gevws_ring_retrieve(gevws_ring *r, uint64_t n);
+
+/* gev.Connection's KeyValueContext as the websocket plugin uses it
+ * (protocol.go:11-14, 28-39): the "gev_ws_upgraded" flag. */
+gevws_conn *gevws_conn_new(void);
+void gevws_conn_free(gevws_conn *c);
+void gevws_conn_set_upgraded(gevws_conn *c, int upgraded);
+int gevws_conn_upgraded(const gevws_conn *c);
+/* Decoded frames still queued for delivery on this connection. */
+uint64_t gevws_conn_pending(const gevws_conn *c);
+
+/* websocket.New(u) (protocol.go:22-24), bound to a device context. */
+gevws_protocol *gevws_protocol_new(gevws_ctx *ctx);
+void gevws_protocol_free(gevws_protocol *p);
+
+/* websocket.(*Protocol).UnPacket(c, buffer) (protocol.go:27-64): one frame per
+ * call.  GEVWS_OK: *ctx_out = the header, (*out, *out_len) = the unmasked
+ * payload (protocol-owned, valid until the next UnPacket on this connection),
+ * h + L bytes consumed from `ring`.  GEVWS_NEED_MORE: (nil, nil), nothing
+ * consumed.  < 0: logged and (nil, nil), as protocol.go:32-34, 41-45.  When the
+ * connection has no queued frames the call decodes its buffered bytes on the
+ * device first. */
+int gevws_protocol_unpacket(gevws_protocol *p, gevws_conn *c, gevws_ring *ring,
+                            gevws_header *ctx_out, const uint8_t **out, uint64_t *out_len);
+
+/* Batched driver for an event loop: one device pass over the buffered bytes of
+ * n connections (stage -> H2D -> decode -> D2H); afterwards
+ * gevws_protocol_unpacket returns their frames in stream order with no further
+ * device work.  Returns the number of frames decoded, or < 0. */
+int64_t gevws_protocol_unpacket_batch(gevws_protocol *p, gevws_conn *const *conns,
+                                      gevws_ring *const *rings, uint32_t n);
+
+/* websocket.(*Protocol).Packet (protocol.go:67-69): identity. */
+const uint8_t *gevws_protocol_packet(gevws_protocol *p, gevws_conn *c, const uint8_t *data,
+                                     uint64_t n, uint64_t *out_len);
+
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
+#ifdef __cplusplus
+}
+#endif
+#endif /* GEVWS_H */

@@ -1,0 +1,103 @@
+"""ctypes binding for oracle/libwsref.so (the C restatement).
+
+TEST INFRASTRUCTURE ONLY -- see ws_oracle.py header.  Used by tests/ (as the
+checker at medium sizes), __graft_entry__.smoke() and bench.py's cpu_baseline.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked", "u1"),
+                        ("mask", "u1", (4,)), ("length", "<i8"),
+                        ("payload_off", "<u8"), ("src_off", "<u8")])
+assert FRAME_DTYPE.itemsize == 32
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return os.path.join(_HERE, "libwsref.so")
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "libwsref.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        P = ctypes.c_void_p
+        L.wsref_cipher.argtypes = [P, ctypes.c_size_t, P, ctypes.c_size_t]
+        L.wsref_cipher.restype = None
+        L.wsref_read_header.argtypes = [P, ctypes.c_uint64, P, P]
+        L.wsref_read_header.restype = ctypes.c_int
+        L.wsref_decode_batch.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint64, P,
+                                         ctypes.c_uint64, P, P, P, P, P]
+        L.wsref_decode_batch.restype = ctypes.c_int64
+        L.wsref_bench_pipeline.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_int, ctypes.c_double,
+                                           P, P, P]
+        L.wsref_bench_pipeline.restype = ctypes.c_double
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def cipher(buf: np.ndarray, mask: bytes, offset: int = 0) -> None:
+    """In-place ws.Cipher word-loop restatement on a uint8 numpy array."""
+    m = np.frombuffer(mask, dtype=np.uint8).copy()
+    lib().wsref_cipher(_ptr(buf), buf.size, _ptr(m), offset)
+
+
+def decode_batch(arena: np.ndarray, conn_off: np.ndarray, conn_len: np.ndarray,
+                 max_frames: int | None = None, payload_cap: int | None = None):
+    """Oracle decode of a batch in the product's output layout.
+
+    Returns dict(frames, payload, conn_first, conn_nframes, conn_status,
+    conn_consumed, total_payload) or raises on capacity error."""
+    n = conn_off.size
+    conn_off = np.ascontiguousarray(conn_off, dtype=np.uint64)
+    conn_len = np.ascontiguousarray(conn_len, dtype=np.uint64)
+    total_in = int(conn_len.sum()) if n else 0
+    if max_frames is None:
+        max_frames = total_in // 2 + 1
+    if payload_cap is None:
+        payload_cap = total_in + 16 * max_frames + 16
+    frames = np.zeros(max_frames, dtype=FRAME_DTYPE)
+    payload = np.zeros(payload_cap, dtype=np.uint8)
+    first = np.zeros(max(n, 1), dtype=np.uint64)
+    nfr = np.zeros(max(n, 1), dtype=np.uint32)
+    st = np.zeros(max(n, 1), dtype=np.int32)
+    cons = np.zeros(max(n, 1), dtype=np.uint64)
+    tot = np.zeros(1, dtype=np.uint64)
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    nf = lib().wsref_decode_batch(_ptr(arena), _ptr(conn_off), _ptr(conn_len), n, _ptr(frames),
+                                  max_frames, _ptr(payload), payload_cap, _ptr(first), _ptr(nfr),
+                                  _ptr(st), _ptr(cons), _ptr(tot))
+    if nf < 0:
+        raise RuntimeError(f"wsref_decode_batch failed: {nf}")
+    tp = int(tot[0])
+    return dict(frames=frames[:nf], payload=payload[:tp], conn_first=first[:n],
+                conn_nframes=nfr[:n], conn_status=st[:n], conn_consumed=cons[:n],
+                total_payload=tp)
+
+
+def bench_pipeline(arena: np.ndarray, conn_off: np.ndarray, conn_len: np.ndarray,
+                   threads: int = 1, min_seconds: float = 10.0):
+    """Time the reference per-frame pipeline; returns (seconds, payload_bytes, frames)."""
+    pb = np.zeros(1, dtype=np.uint64)
+    nf = np.zeros(1, dtype=np.uint64)
+    ck = np.zeros(1, dtype=np.uint64)
+    conn_off = np.ascontiguousarray(conn_off, dtype=np.uint64)
+    conn_len = np.ascontiguousarray(conn_len, dtype=np.uint64)
+    secs = lib().wsref_bench_pipeline(_ptr(arena), _ptr(conn_off), _ptr(conn_len), conn_off.size,
+                                      threads, min_seconds, _ptr(pb), _ptr(nf), _ptr(ck))
+    return secs, int(pb[0]), int(nf[0])

@@ -1,0 +1,287 @@
+"""CPU oracle for the WebSocket frame-decode / payload-unmask hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing under ``gev_amd/`` may import, call or link
+this module: only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg use it, and only as the checker.
+
+This is a plain-Python restatement of the reference (Allenxuxu/gev, Go) written
+from its semantics; no reference source is copied.  Each function cites the
+reference file:line it follows (paths relative to the reference root).
+
+Parity pinning
+--------------
+The reference has no golden vectors or known-answer tests for this path
+ and cannot be built here (no Go toolchain).  The oracle is
+pinned by:
+
+* RFC 6455 §5.7 known-answer frames (see ``RFC6455_KATS`` below), which the
+  reference's header layout (read.go:19-84) and XOR (cipher.go:14-53) must
+  reproduce;
+* properties: ``cipher`` (the Go word-loop transliteration) equals the bytewise
+  definition for every offset mod 4 and every length; involution; chunk/offset
+  composition;
+* the C restatement ``oracle/ws_ref.c`` agreeing with this module.
+
+Edge cases that depend on the un-vendored ``github.com/Allenxuxu/ringbuffer
+v0.0.11`` are **parity unpinned**; the oracle
+takes the RFC-correct choice (NEED_MORE) and the golden fixtures exclude them.
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+# Status codes (mirror include/gevws.h).
+OK = 0
+NEED_MORE = 1          # ws.ErrHeaderNotReady / completeness gate failed -> (nil, nil)
+ERR_LEN_MSB = -1       # ws.ErrHeaderLengthMSB (read.go:12-16, 71-73)
+
+# Opcodes, frame.go:14-25.
+OP_CONTINUATION = 0x0
+OP_TEXT = 0x1
+OP_BINARY = 0x2
+OP_CLOSE = 0x8
+OP_PING = 0x9
+OP_PONG = 0xA
+
+# remain maps mask position [0,4) to bytes processed one by one (cipher.go:56).
+_REMAIN = (0, 3, 2, 1)
+
+
+@dataclass
+class Header:
+    """ws.Header, frame.go:169-176: {Fin bool; Rsv byte; OpCode; Masked bool;
+    Mask [4]byte; Length int64} -- 16 bytes in Go's layout."""
+    fin: bool = False
+    rsv: int = 0
+    opcode: int = 0
+    masked: bool = False
+    mask: bytes = b"\x00\x00\x00\x00"
+    length: int = 0
+
+    def pack(self) -> bytes:
+        """Byte image identical to the Go struct / gevws_header (offsets 0,1,2,3,4..7,8..15)."""
+        return struct.pack("<BBBB4sq", int(self.fin), self.rsv, self.opcode,
+                           int(self.masked), self.mask, self.length)
+
+    @staticmethod
+    def unpack(b: bytes) -> "Header":
+        fin, rsv, op, masked, mask, length = struct.unpack("<BBBB4sq", b)
+        return Header(bool(fin), rsv, op, bool(masked), mask, length)
+
+
+# --------------------------------------------------------------------------- cipher
+def cipher_bytewise(payload: bytearray, mask: bytes, offset: int = 0) -> None:
+    """Definition of the XOR unmask: p[i] ^= mask[(offset+i) % 4]
+    (RFC 6455 §5.3; cipher.go:16-21 is exactly this loop for n < 8)."""
+    for i in range(len(payload)):
+        payload[i] ^= mask[(offset + i) % 4]
+
+
+def cipher(payload: bytearray, mask: bytes, offset: int = 0) -> None:
+    """Transliteration of ws.Cipher, cipher.go:14-53, in place.
+
+    n < 8: bytewise (cipher.go:16-21).  Otherwise ``ln = remain[offset%4]`` head
+    bytes and ``rn = (n-ln)%8`` tail bytes bytewise (cipher.go:24-36), then the
+    body as native-endian uint64 words XORed with ``m<<32|m`` where ``m`` is the
+    native-endian uint32 of the mask (cipher.go:42-51).  Python's ``int.from_bytes
+    (..., 'little')`` stands in for x86 native endianness; the algorithm is
+    endianness-agnostic by construction (cipher.go:38-41).
+    """
+    n = len(payload)
+    if n < 8:
+        for i in range(n):
+            payload[i] ^= mask[(offset + i) % 4]
+        return
+    mpos = offset % 4
+    ln = _REMAIN[mpos]
+    rn = (n - ln) % 8
+    for i in range(ln):
+        payload[i] ^= mask[(mpos + i) % 4]
+    for i in range(n - rn, n):
+        payload[i] ^= mask[(mpos + i) % 4]
+    m = int.from_bytes(mask, "little")
+    m2 = (m << 32) | m
+    words = (n - ln - rn) >> 3
+    for i in range(words):
+        s = ln + (i << 3)
+        v = int.from_bytes(payload[s:s + 8], "little") ^ m2
+        payload[s:s + 8] = v.to_bytes(8, "little")
+
+
+def cipher_np(payload, mask: bytes, offset: int = 0):
+    """numpy form of the bytewise definition for medium sizes (returns a new array)."""
+    import numpy as np
+    p = np.frombuffer(bytes(payload), dtype=np.uint8) if not isinstance(payload, np.ndarray) else payload
+    n = p.shape[0]
+    key = np.frombuffer(mask, dtype=np.uint8)
+    idx = (np.arange(n, dtype=np.int64) + offset) & 3
+    return p ^ key[idx]
+
+
+# --------------------------------------------------------------------------- header
+def read_header(buf, pos: int = 0, avail: Optional[int] = None) -> Tuple[int, Optional[Header], int]:
+    """ws.VirtualReadHeader, read.go:19-84, over a linear view of the ring.
+
+    Returns ``(status, header, header_len)``.
+
+    * ``avail < 6`` -> NEED_MORE even for complete 2..5-byte unmasked frames
+      (read.go:20-23; Appendix A P1).
+    * byte0: FIN = bit7, RSV = (b0 & 0x70) >> 4, opcode = b0 & 0x0F (read.go:29-31).
+    * byte1: MASK = bit7 -> +4 extra; len7 = b1 & 0x7F; 126 -> +2 BE16;
+      127 -> +8 BE64 (read.go:33-49).
+    * 127-form with the length MSB set -> ERR_LEN_MSB (read.go:69-73).
+    * The mask is the last 4 extra bytes (read.go:78-81).
+    * No validation of RSV, reserved opcodes, control-frame size or minimal
+      length encoding (Appendix A P5).
+    * U1 (avail >= 6 but < header length): the reference reads stale scratch
+      bytes (ringbuffer-dependent, unpinned); the oracle answers NEED_MORE.
+    """
+    if avail is None:
+        avail = len(buf) - pos
+    if avail < 6:
+        return NEED_MORE, None, 0
+    b0 = buf[pos]
+    b1 = buf[pos + 1]
+    h = Header()
+    h.fin = (b0 & 0x80) != 0
+    h.rsv = (b0 & 0x70) >> 4
+    h.opcode = b0 & 0x0F
+    extra = 0
+    if b1 & 0x80:
+        h.masked = True
+        extra += 4
+    len7 = b1 & 0x7F
+    if len7 < 126:
+        h.length = len7
+    elif len7 == 126:
+        extra += 2
+    else:
+        extra += 8
+    hlen = 2 + extra
+    if extra == 0:
+        return OK, h, hlen
+    if avail < hlen:               # U1: unpinned -> RFC-correct NEED_MORE
+        return NEED_MORE, None, 0
+    e = pos + 2
+    if len7 == 126:
+        h.length = (buf[e] << 8) | buf[e + 1]
+        e += 2
+    elif len7 == 127:
+        if buf[e] & 0x80:
+            return ERR_LEN_MSB, None, 0
+        h.length = int.from_bytes(bytes(buf[e:e + 8]), "big")
+        e += 8
+    if h.masked:
+        h.mask = bytes(buf[e:e + 4])
+    return OK, h, hlen
+
+
+# --------------------------------------------------------------------------- unpacket
+@dataclass
+class Frame:
+    header: Header
+    payload: bytes
+    header_len: int
+    stream_pos: int  # offset of the frame's first header byte in the connection stream
+
+
+def unpacket(buf, pos: int = 0) -> Tuple[int, Optional[Frame]]:
+    """One call of websocket.(*Protocol).UnPacket's decode branch,
+    plugins/websocket/protocol.go:38-62, on a linear view starting at ``pos``.
+
+    Header (read_header) -> completeness gate ``VirtualLength() >= Length``
+    (protocol.go:47) -> fresh zero-filled slice of Length, filled from the ring
+    (protocol.go:48-51) -> ``Cipher(payload, mask, 0)`` iff Masked
+    (protocol.go:53-55; mask phase restarts at 0 per frame, Appendix A P7).
+    Incomplete -> NEED_MORE with nothing consumed (protocol.go:59-61).
+    """
+    avail = len(buf) - pos
+    st, h, hlen = read_header(buf, pos, avail)
+    if st != OK:
+        return st, None
+    if avail - hlen < h.length:
+        return NEED_MORE, None
+    start = pos + hlen
+    payload = bytearray(bytes(buf[start:start + h.length]))
+    if h.masked:
+        cipher(payload, h.mask, 0)
+    return OK, Frame(h, bytes(payload), hlen, pos)
+
+
+@dataclass
+class StreamResult:
+    frames: List[Frame] = field(default_factory=list)
+    consumed: int = 0
+    status: int = OK       # OK (stopped on NEED_MORE) or ERR_LEN_MSB (connection poisoned)
+
+
+def decode_stream(buf) -> StreamResult:
+    """Connection.handlerProtocol, connection.go:208-218: call UnPacket until it
+    returns (nil, nil), preserving stream order.  A header error stops the loop
+    too (protocol.go:41-45 returns (nil, nil)); ERR_LEN_MSB poisons the stream
+    (Appendix A P9/U3)."""
+    res = StreamResult()
+    pos = 0
+    while True:
+        st, fr = unpacket(buf, pos)
+        if st != OK:
+            res.status = OK if st == NEED_MORE else st
+            break
+        res.frames.append(fr)
+        pos += fr.header_len + fr.header.length
+    res.consumed = pos
+    return res
+
+
+# --------------------------------------------------------------------------- encoder (fixtures)
+def write_header(fin: bool, rsv: int, opcode: int, length: int, masked: bool,
+                 mask: bytes = b"\x00\x00\x00\x00", len_form: Optional[int] = None) -> bytes:
+    """Header serialisation following ws.WriteHeader, write.go:48-84 (minimal
+    length form: <=125 -> 7-bit, <=0xFFFF -> 126+BE16, else 127+BE64) plus the
+    client MASK bit and key (write.go:78-81).  ``len_form`` forces a
+    non-minimal encoding (7, 16 or 64) to build Appendix A P5 cases."""
+    b0 = (0x80 if fin else 0) | ((rsv & 7) << 4) | (opcode & 0x0F)
+    if len_form is None:
+        len_form = 7 if length <= 125 else (16 if length <= 0xFFFF else 64)
+    if len_form == 7:
+        assert length <= 125
+        out = bytearray([b0, length])
+    elif len_form == 16:
+        assert length <= 0xFFFF
+        out = bytearray([b0, 126]) + length.to_bytes(2, "big")
+    else:
+        out = bytearray([b0, 127]) + length.to_bytes(8, "big")
+    if masked:
+        out[1] |= 0x80
+        out += mask
+    return bytes(out)
+
+
+def encode_frame(payload: bytes, opcode: int = OP_BINARY, fin: bool = True, rsv: int = 0,
+                 masked: bool = True, mask: bytes = b"\x00\x00\x00\x00",
+                 len_form: Optional[int] = None) -> bytes:
+    """A complete client->server frame: header + payload XORed with the key."""
+    hdr = write_header(fin, rsv, opcode, len(payload), masked, mask, len_form)
+    body = bytearray(payload)
+    if masked:
+        cipher_bytewise(body, mask, 0)
+    return hdr + bytes(body)
+
+
+# RFC 6455 §5.7 known-answer frames (external KATs; see module docstring).
+RFC6455_KATS = [
+    # (wire bytes, fin, opcode, masked, mask, payload)
+    (bytes.fromhex("810548656c6c6f"), True, OP_TEXT, False, b"\x00" * 4, b"Hello"),
+    (bytes.fromhex("818537fa213d7f9f4d5158"), True, OP_TEXT, True, bytes.fromhex("37fa213d"), b"Hello"),
+    (bytes.fromhex("010348656c"), False, OP_TEXT, False, b"\x00" * 4, b"Hel"),
+    (bytes.fromhex("80026c6f"), True, OP_CONTINUATION, False, b"\x00" * 4, b"lo"),
+    (bytes.fromhex("890548656c6c6f"), True, OP_PING, False, b"\x00" * 4, b"Hello"),
+    (bytes.fromhex("8a8537fa213d7f9f4d5158"), True, OP_PONG, True, bytes.fromhex("37fa213d"), b"Hello"),
+]
+# Header-only KATs (§5.7: 256-byte and 64 KiB unmasked binary messages).
+RFC6455_HEADER_KATS = [
+    (bytes.fromhex("827e0100"), True, OP_BINARY, False, 256, 4),
+    (bytes.fromhex("827f0000000000010000"), True, OP_BINARY, False, 65536, 10),
+]

@@ -1,0 +1,72 @@
+"""Shared test helpers: run the HIP decode through the C ABI on host-built
+batches and compare it with the oracle, field by field and byte by byte."""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import ref
+from oracle import ws_oracle as wo
+
+
+def gpu_decode(engine, arena: bytes | np.ndarray, conns: np.ndarray, **kw):
+    import torch
+    import gev_amd
+    a = np.frombuffer(arena, np.uint8) if isinstance(arena, (bytes, bytearray)) else arena
+    dev = torch.device("cuda", engine.device)
+    d_in = torch.zeros(a.size + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    if a.size:
+        d_in[: a.size] = torch.from_numpy(a.copy()).to(dev)
+    conns = np.ascontiguousarray(conns, dtype=np.int64).reshape(-1, 2)
+    d_conns = torch.from_numpy(conns.copy()).to(dev) if conns.shape[0] else torch.zeros((1, 2), dtype=torch.int64,
+                                                                                         device=dev)
+    out = engine.decode(d_in, a.size, d_conns, conns.shape[0], **kw)
+    return out
+
+
+def host_result(out):
+    s = out.summary_host()
+    return dict(summary=s, frames=out.frames_host(), conn_out=out.conn_out_host(), payload=out.payload_host())
+
+
+def assert_matches_oracle(engine, arena: bytes | np.ndarray, conns: np.ndarray, tag: str = ""):
+    """GPU decode == C oracle decode, bit-exact, incl. the zeroed pad bytes."""
+    a = np.frombuffer(arena, np.uint8).copy() if isinstance(arena, (bytes, bytearray)) else arena
+    conns = np.ascontiguousarray(conns, dtype=np.int64).reshape(-1, 2)
+    want = ref.decode_batch(a, conns[:, 0], conns[:, 1])
+    got = host_result(gpu_decode(engine, a, conns))
+    s = got["summary"]
+    assert int(s["status"]) == 0, tag
+    assert int(s["frames"]) == want["frames"].shape[0], tag
+    assert int(s["payload_bytes"]) == want["total_payload"], tag
+    co = got["conn_out"]
+    assert np.array_equal(co["nframes"], want["conn_nframes"]), tag
+    assert np.array_equal(co["consumed"], want["conn_consumed"]), tag
+    assert np.array_equal(co["status"], want["conn_status"]), tag
+    assert np.array_equal(co["first_frame"], want["conn_first"]), tag
+    assert int(s["errors"]) == int((want["conn_status"] < 0).sum()), tag
+    assert int(s["payload_len"]) == int(want["frames"]["length"].sum()), tag
+    assert got["frames"].tobytes() == want["frames"].tobytes(), tag
+    assert np.array_equal(got["payload"], want["payload"]), tag
+    return got
+
+
+def random_stream(rng, n_frames: int, max_len: int = 3072, tail: bool = True) -> bytes:
+    s = b""
+    for _ in range(n_frames):
+        L = int(rng.integers(0, max_len + 1))
+        forms = [f for f in (7, 16, 64) if (f != 7 or L <= 125) and (f != 16 or L <= 0xFFFF)]
+        form = None if rng.random() < 0.7 else int(rng.choice(forms))
+        s += wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), int(rng.integers(0, 16)),
+                             bool(rng.random() < 0.8), int(rng.integers(0, 8)) if rng.random() < .1 else 0,
+                             bool(rng.random() < 0.85), bytes(rng.integers(0, 256, 4, dtype=np.uint8)), form)
+    if tail and rng.random() < 0.7:
+        t = wo.encode_frame(bytes(rng.integers(0, 256, 200, dtype=np.uint8)), 2, True, 0, True, b"\x01\x02\x03\x04")
+        s += t[: int(rng.integers(1, len(t)))]
+    return s
+
+
+def pack_streams(streams):
+    arena = b"".join(streams)
+    lens = np.array([len(s) for s in streams], np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if len(streams) else np.zeros(0, np.int64)
+    return arena, np.stack([offs, lens], axis=1) if len(streams) else np.zeros((0, 2), np.int64)

@@ -1,0 +1,202 @@
+"""GPU parity suite: the HIP decode path, called through the C ABI, against the
+oracle and the golden vectors -- bit-exact (integer/byte work, no tolerance).
+
+Small and medium batches are compared record by record and byte by byte with
+oracle/ws_ref.c; full BASELINE sizes (C2, C3) are checked with the
+size-independent property decode(mask(P)) == P on the device generator's
+frames (gevws_synth_verify_async), plus an oracle cross-check of a slice."""
+import numpy as np
+import pytest
+
+from oracle import ref
+from oracle import ws_oracle as wo
+from tests._helpers import assert_matches_oracle, gpu_decode, host_result, pack_streams, random_stream
+
+pytestmark = pytest.mark.gpu
+
+
+# --------------------------------------------------------------------------- golden vectors
+def test_golden_vectors(engine, golden):
+    for name, g in golden.items():
+        got = host_result(gpu_decode(engine, g["in"], g["conns"]))
+        co = got["conn_out"]
+        assert np.array_equal(co["nframes"], g["conn_res"][:, 0]), name
+        assert np.array_equal(co["consumed"], g["conn_res"][:, 1]), name
+        assert np.array_equal(co["status"], g["conn_res"][:, 2]), name
+        f = got["frames"]
+        assert np.array_equal(f.view(np.uint8).reshape(-1, 32)[:, :16], g["hdr"]), name
+        assert np.array_equal(f["src_off"], g["src_off"]), name
+        pay = got["payload"]
+        cat = b"".join(pay[int(o):int(o) + int(L)].tobytes() for o, L in zip(f["payload_off"], f["length"]))
+        assert cat == g["payload"].tobytes(), name
+        assert_matches_oracle(engine, g["in"], g["conns"], name)
+
+
+def test_rfc6455_kats_on_device(engine):
+    arena = b"".join(k[0] for k in wo.RFC6455_KATS)
+    got = host_result(gpu_decode(engine, arena, np.array([[0, len(arena)]])))
+    assert int(got["summary"]["frames"]) == len(wo.RFC6455_KATS)
+    for f, k in zip(got["frames"], wo.RFC6455_KATS):
+        o, L = int(f["payload_off"]), int(f["length"])
+        assert got["payload"][o:o + L].tobytes() == k[5]
+
+
+# --------------------------------------------------------------------------- alignment / edge sweeps
+def test_alignment_and_length_sweep(engine):
+    """Every payload start mod 16 x every length class near the 16-byte chunk edges."""
+    rng = np.random.default_rng(11)
+    streams = []
+    lengths = list(range(0, 70)) + [k * 16 + d for k in (5, 8, 63, 64, 256) for d in (-1, 0, 1)] + [4093, 4096, 4099]
+    for lead in range(16):
+        s = bytes(rng.integers(0, 256, lead, dtype=np.uint8))  # garbage prefix consumed as its own conn
+        streams.append(s)
+        body = b""
+        for L in lengths:
+            body += wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), 2, True, 0,
+                                    bool(L % 3), bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+        streams.append(body + b"\x00" * 6)
+    arena, conns = pack_streams(streams)
+    assert_matches_oracle(engine, arena, conns, "alignment sweep")
+
+
+def test_random_batches(engine):
+    rng = np.random.default_rng(12)
+    for trial in range(6):
+        n = int(rng.integers(1, 300))
+        streams = [random_stream(rng, int(rng.integers(0, 25))) for _ in range(n)]
+        arena, conns = pack_streams(streams)
+        assert_matches_oracle(engine, arena, conns, f"trial {trial}")
+
+
+def test_big_frames_cross_tiles(engine):
+    rng = np.random.default_rng(13)
+    s = b""
+    for L in (1 << 20, 65536, 70001, 4096 * 3 + 5, 1, 0, (1 << 20) + 17):
+        s += wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), 2, True, 0, True,
+                             bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+    arena, conns = pack_streams([s, s[:-3], s[5:]])
+    assert_matches_oracle(engine, arena, conns, "big frames")
+
+
+def test_empty_and_tiny_batches(engine):
+    assert_matches_oracle(engine, b"", np.zeros((0, 2), np.int64), "no conns")
+    assert_matches_oracle(engine, b"\x81", np.array([[0, 1], [1, 0]]), "1 byte + empty")
+    arena, conns = pack_streams([b"", b"\x81\x00", b"\x81\x80\x01\x02\x03\x04"])
+    assert_matches_oracle(engine, arena, conns, "tiny")
+
+
+def test_poisoned_connections_isolated(engine):
+    good = wo.encode_frame(b"fine", 1, True, 0, True, b"\x01\x02\x03\x04")
+    bad = bytes([0x82, 0xFF, 0x80, 0, 0, 0, 0, 0, 0, 5, 1, 2, 3, 4]) + b"hello"
+    arena, conns = pack_streams([good + bad + good, good * 3, bad, good])
+    got = assert_matches_oracle(engine, arena, conns, "poison")
+    assert list(got["conn_out"]["status"]) == [-1, 0, -1, 0]
+    assert int(got["summary"]["errors"]) == 2
+
+
+def test_capacity_error_reports_exact_sizes(engine):
+    import torch
+    rng = np.random.default_rng(14)
+    arena, conns = pack_streams([random_stream(rng, 20, tail=False) for _ in range(10)])
+    want = ref.decode_batch(np.frombuffer(arena, np.uint8).copy(), conns[:, 0], conns[:, 1])
+    import gev_amd
+    dev = torch.device("cuda", engine.device)
+    d_in = torch.zeros(len(arena) + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    d_in[: len(arena)] = torch.from_numpy(np.frombuffer(arena, np.uint8).copy()).to(dev)
+    d_conns = torch.from_numpy(conns.copy()).to(dev)
+    out = engine.alloc_batch(conns.shape[0], 5, 64)
+    engine.decode_async(d_in, len(arena), d_conns, conns.shape[0], out, 5, 64)
+    torch.cuda.synchronize()
+    s = out.summary_host()
+    assert int(s["status"]) == gev_amd.ERR_CAPACITY
+    assert int(s["frames"]) == want["frames"].shape[0]
+    assert int(s["payload_bytes"]) == want["total_payload"]
+    # the retrying wrapper then succeeds
+    assert_matches_oracle(engine, arena, conns, "after capacity retry")
+
+
+# --------------------------------------------------------------------------- ws.Cipher on device
+def test_device_cipher_all_offsets_alignments(engine):
+    import torch
+    rng = np.random.default_rng(15)
+    base = rng.integers(0, 256, 70000, dtype=np.uint8)
+    dev = torch.device("cuda", engine.device)
+    for n in list(range(0, 40)) + [63, 64, 65, 1000, 4097, 65536]:
+        for align in (0, 1, 3, 7, 8, 13, 15):
+            for off in range(0, 8):
+                mask = bytes(rng.integers(0, 256, 4, dtype=np.uint8))
+                t = torch.from_numpy(base[:align + n + 16].copy()).to(dev)
+                engine.cipher_(t, mask, off, nbytes=n, byte_offset=align)
+                got = t.cpu().numpy()
+                want = base[:align + n + 16].copy()
+                c = want[align:align + n]
+                ref.cipher(c, mask, off)
+                want[align:align + n] = c
+                assert np.array_equal(got, want), (n, align, off)
+
+
+# --------------------------------------------------------------------------- synthetic full-size properties
+def _synth_decode_verify(engine, layout, check_slice_conns: int = 2):
+    import torch
+    import gev_amd
+    dev = torch.device("cuda", engine.device)
+    arena = torch.empty(layout.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    arena[layout.arena_bytes:] = 0
+    desc = torch.from_numpy(layout.desc.view(np.uint8).copy()).to(dev)
+    conns = torch.from_numpy(layout.conns.copy()).to(dev)
+    engine.synth(arena, desc, layout.n_frames, layout.seed)
+    out = engine.decode(arena, layout.arena_bytes, conns, layout.n_conns, max_frames=layout.n_frames,
+                        payload_cap=layout.payload_padded)
+    s = out.summary_host()
+    assert int(s["frames"]) == layout.n_frames
+    assert int(s["payload_len"]) == layout.payload_len
+    assert int(s["payload_bytes"]) == layout.payload_padded
+    mism = torch.zeros(1, dtype=torch.int64, device=dev)
+    engine.verify(desc, layout.n_frames, layout.seed, out, mism)
+    torch.cuda.synchronize()
+    assert int(mism.item()) == 0
+    co = out.conn_out_host()
+    assert np.array_equal(co["consumed"].astype(np.int64), layout.conns[:, 1])
+    # oracle cross-check of the first connections' streams, byte for byte
+    k = min(check_slice_conns, layout.n_conns)
+    end = int(layout.conns[k - 1, 0] + layout.conns[k - 1, 1])
+    host_in = arena[:end].cpu().numpy()
+    want = ref.decode_batch(host_in, layout.conns[:k, 0], layout.conns[:k, 1])
+    nf = want["frames"].shape[0]
+    got_frames = out.frames[:nf].cpu().numpy().reshape(-1).view(want["frames"].dtype)
+    assert got_frames.tobytes() == want["frames"].tobytes()
+    got_pay = out.payload[: want["total_payload"]].cpu().numpy()
+    assert np.array_equal(got_pay, want["payload"])
+    # and the generator's plaintext on the host for frame 0
+    from gev_amd import workloads
+    L0 = int(layout.desc["length"][0])
+    assert got_pay[:L0].tobytes() == workloads.plaintext(layout.seed, 0, L0)
+    del arena, out
+    torch.cuda.empty_cache()
+
+
+def test_c2_full_size_property(engine):
+    from gev_amd import workloads
+    _synth_decode_verify(engine, workloads.config_c2())
+
+
+def test_c3_full_size_property(engine):
+    import torch
+    from gev_amd import workloads
+    lay = workloads.config_c3()
+    free, _ = torch.cuda.mem_get_info(engine.device)
+    need = lay.arena_bytes + lay.payload_padded + (1 << 30)
+    if free < need:
+        pytest.fail(f"C3 needs {need / 2**30:.1f} GiB of HBM, {free / 2**30:.1f} GiB free")
+    _synth_decode_verify(engine, lay, check_slice_conns=1)
+
+
+def test_c4_power_law_property(engine):
+    from gev_amd import workloads
+    _synth_decode_verify(engine, workloads.config_c4(total_payload=64 << 20, n_conns=512), check_slice_conns=8)
+
+
+def test_c5_fragmented_control_property(engine):
+    from gev_amd import workloads
+    lay = workloads.config_c5(n_conns=16, messages_per_conn=2)
+    _synth_decode_verify(engine, lay, check_slice_conns=16)

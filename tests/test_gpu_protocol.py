@@ -1,0 +1,126 @@
+"""The C++ host mirror of websocket.Protocol (plugins/websocket/protocol.go:27-69)
+driven like gev drives it, with every decode on the device.
+
+Modelled on the reference's only hot-path test, example/websocket/
+wsserver_test.go:101-133 (clients send masked text frames of 1-3072 random
+bytes and expect them back), but without sockets: bytes arrive in the
+connection's ring buffer in read(2)-sized chunks (<= 64 KiB, eventloop.go:15),
+and Connection.handlerProtocol (connection.go:208-218) calls UnPacket until it
+returns (nil, nil).  Expected frames come from the oracle."""
+import numpy as np
+import pytest
+
+import gev_amd
+from oracle import ws_oracle as wo
+
+pytestmark = pytest.mark.gpu
+
+
+def _client_frames(rng, n):
+    out = []
+    for _ in range(n):
+        sz = int(rng.integers(1, 3 * 1024 + 1))  # wsserver_test.go:112
+        data = bytes(rng.integers(0, 256, sz, dtype=np.uint8))
+        out.append((data, wo.encode_frame(data, wo.OP_TEXT, True, 0, True,
+                                          bytes(rng.integers(0, 256, 4, dtype=np.uint8)))))
+    return out
+
+
+def test_echo_over_ring_buffers(engine):
+    rng = np.random.default_rng(21)
+    proto = gev_amd.Protocol(engine)
+    n_conns = 100
+    conns = [gev_amd.Connection(upgraded=True) for _ in range(n_conns)]
+    rings = [gev_amd.RingBuffer(4096) for _ in range(n_conns)]  # DefaultBufferSize (eventloop.go:16)
+    sent = [_client_frames(rng, int(rng.integers(1, 20))) for _ in range(n_conns)]
+    wires = [b"".join(w for _, w in s) for s in sent]
+    got = [[] for _ in range(n_conns)]
+    pos = [0] * n_conns
+
+    def on_message(c, hdr, data):
+        got[idx].append((hdr.opcode, hdr.fin, data))
+        return data  # echo, like the test server's OnMessage
+
+    while any(pos[i] < len(wires[i]) for i in range(n_conns)):
+        for idx in range(n_conns):
+            if pos[idx] >= len(wires[idx]):
+                continue
+            n = int(rng.integers(1, 65537))
+            chunk = wires[idx][pos[idx]:pos[idx] + n]
+            pos[idx] += len(chunk)
+            rings[idx].write(chunk)
+            replies = gev_amd.handler_protocol(proto, conns[idx], rings[idx], on_message)
+            assert all(isinstance(r, bytes) for r in replies)
+    for i in range(n_conns):
+        assert [d for _, _, d in got[i]] == [d for d, _ in sent[i]], i
+        assert all(op == wo.OP_TEXT and fin for op, fin, _ in got[i])
+        assert rings[i].length() == 0
+
+
+def test_batched_driver_matches_oracle(engine):
+    rng = np.random.default_rng(22)
+    proto = gev_amd.Protocol(engine)
+    streams = []
+    for _ in range(64):
+        s = b""
+        for _ in range(int(rng.integers(0, 15))):
+            L = int(rng.integers(0, 4000))
+            s += wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), int(rng.choice([0, 1, 2, 9, 10])),
+                                 bool(rng.random() < .8), 0, bool(rng.random() < .9),
+                                 bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+        s += bytes(rng.integers(0, 256, int(rng.integers(0, 10)), dtype=np.uint8))
+        streams.append(s)
+    conns = [gev_amd.Connection() for _ in streams]
+    rings = []
+    for s in streams:
+        r = gev_amd.RingBuffer(64)
+        r.write(b"\x00" * 40)   # force wrap-around: write, consume, write
+        r.retrieve(40)
+        r.write(s)
+        rings.append(r)
+    n = proto.unpacket_batch(conns, rings)
+    assert n == sum(len(wo.decode_stream(s).frames) for s in streams)
+    for c, r, s in zip(conns, rings, streams):
+        want = wo.decode_stream(s)
+        assert c.pending() == len(want.frames)
+        for fr in want.frames:
+            h, data = proto.unpacket(c, r)
+            assert h is not None
+            assert (bool(h.fin), h.rsv, h.opcode, bool(h.masked), bytes(h.mask), h.length) == (
+                fr.header.fin, fr.header.rsv, fr.header.opcode, fr.header.masked, fr.header.mask, fr.header.length)
+            assert data == fr.payload
+        assert proto.unpacket(c, r) == (None, None)
+        assert proto.last_status == gev_amd.NEED_MORE
+        assert r.length() == len(s) - want.consumed
+
+
+def test_not_upgraded_and_poison(engine):
+    proto = gev_amd.Protocol(engine)
+    c = gev_amd.Connection(upgraded=False)
+    r = gev_amd.RingBuffer()
+    r.write(wo.encode_frame(b"hi", 1, True, 0, True, b"\x01\x02\x03\x04"))
+    assert proto.unpacket(c, r) == (None, None)
+    assert proto.last_status == gev_amd.ERR_NOT_UPGRADED
+    c.set_upgraded(True)
+    r.write(bytes([0x82, 0xFF, 0x80, 0, 0, 0, 0, 0, 0, 5, 1, 2, 3, 4]) + b"hello")
+    h, d = proto.unpacket(c, r)
+    assert d == b"hi"
+    for _ in range(2):   # sticky: logged and (nil, nil) on every later call
+        assert proto.unpacket(c, r) == (None, None)
+        assert proto.last_status == gev_amd.ERR_LEN_MSB
+
+
+def test_need_more_then_complete(engine):
+    proto = gev_amd.Protocol(engine)
+    c = gev_amd.Connection()
+    r = gev_amd.RingBuffer(16)
+    w = wo.encode_frame(bytes(range(200)), 2, True, 0, True, b"\x09\x08\x07\x06")
+    for cut in (1, 5, 6, 7, 8, 100, len(w) - 1):
+        r.write(w[:cut])
+        assert proto.unpacket(c, r) == (None, None)
+        assert proto.last_status == gev_amd.NEED_MORE
+        assert r.length() == cut
+        r.retrieve(cut)
+    r.write(w)
+    h, d = proto.unpacket(c, r)
+    assert d == bytes(range(200)) and h.length == 200 and r.length() == 0
