@@ -105,6 +105,17 @@ class Engine:
         except Exception:
             pass
 
+    # -------------------------------------------------------------- tuning
+    def set_tuning(self, key: int, value: int) -> None:
+        st = lib.gevws_ctx_set_tuning(self._ctx, key, value)
+        if st != OK:
+            raise ValueError(f"set_tuning({key}, {value}): {status_string(st)}")
+
+    @staticmethod
+    def variant_name(i: int) -> Optional[str]:
+        n = lib.gevws_tuning_name(_abi.TUNE_UNMASK_VARIANT, i)
+        return n.decode() if n else None
+
     # -------------------------------------------------------------- timing
     def set_timing(self, enable: bool):
         lib.gevws_ctx_set_timing(self._ctx, int(enable))

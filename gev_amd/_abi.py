@@ -20,6 +20,9 @@ ERR_INVALID = -3
 ERR_DEVICE = -4
 ERR_NOT_UPGRADED = -5
 
+TUNE_UNMASK_VARIANT = 1
+TUNE_UNMASK_GRID = 2
+
 IN_PAD = 64
 PAYLOAD_ALIGN = 16
 TILE = 4096
@@ -79,7 +82,10 @@ SIGNATURES = {
     "gevws_ctx_create": (P, [ctypes.c_int]),
     "gevws_ctx_destroy": (None, [P]),
     "gevws_ctx_device": (ctypes.c_int, [P]),
+    "gevws_ctx_stream": (P, [P]),
     "gevws_ctx_set_timing": (ctypes.c_int, [P, ctypes.c_int]),
+    "gevws_ctx_set_tuning": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
+    "gevws_tuning_name": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32)]),
     "gevws_decode_batch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,
                                                 ctypes.c_uint64, P, ctypes.c_uint64, P, P]),
@@ -111,7 +117,19 @@ SIGNATURES = {
 }
 
 
+def _share_torch_hip_runtime() -> None:
+    """torch wheels bundle their own libamdhip64.so.7; import torch first so
+    that libgevws.so's libamdhip64.so.7 dependency binds to that same runtime
+    (one HIP runtime per process: device pointers, streams and events are
+    shared with torch).  Without torch, /opt/rocm's runtime is used."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    _share_torch_hip_runtime()
     if not os.path.exists(path):
         raise ImportError(
             f"gev_amd: HIP library {path} is missing -- build it first "

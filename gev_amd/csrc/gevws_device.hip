@@ -42,7 +42,6 @@ constexpr int kScanBlock = 1024;
 constexpr int kUnmaskBlock = 256;
 constexpr uint64_t kTile = GEVWS_TILE;
 static_assert(kTile == kUnmaskBlock * 16, "one tile = one 16-byte chunk per lane");
-constexpr int kUnmaskUnroll = 4;
 constexpr int kBlkFields = 4;  // frames, padded payload bytes, payload length, errors
 
 // ------------------------------------------------------------------ helpers
@@ -358,6 +357,101 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask(const uint8_t* __restri
   }
 }
 
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16u_stream(const uint8_t* p) {
+  if constexpr (NT) {
+    // unaligned 16-byte nontemporal load (gfx950 unaligned access mode)
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  } else {
+    return ld16u(p);
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16_stream(uint8_t* p, u32x4 x) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
+  } else {
+    *reinterpret_cast<u32x4*>(p) = x;
+  }
+}
+
+// v2: each workgroup owns a contiguous run of output tiles.  The frame covering
+// the current position is cached in wave-uniform registers (scalar loads of
+// tile_first[t] and the 32-byte record), so while U consecutive tiles lie in
+// one frame the loop is pure streaming: U independent 16-byte loads per lane,
+// XOR, U aligned 16-byte stores.  Steps that straddle frames fall back to a
+// per-lane lookup (tile map + binary search) one tile at a time.
+template <int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v2(const uint8_t* __restrict__ in,
+                                                            const gevws_frame* __restrict__ frames,
+                                                            const uint32_t* __restrict__ tile_first,
+                                                            const gevws_summary* __restrict__ sum,
+                                                            uint8_t* __restrict__ out) {
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t total = sum->payload_bytes;
+  const uint64_t nframes = sum->frames;
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  uint64_t t = (uint64_t)blockIdx.x * per;
+  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+  const uint32_t lane_off = threadIdx.x * 16;
+  uint64_t f_po = 0, f_end = 0, f_src = 0;
+  int64_t f_len = 0;
+  uint32_t f_key = 0;
+  while (t < tend) {
+    const uint64_t base = t * kTile;
+    if (base >= f_end) {  // wave-uniform: refresh the cached frame (scalar loads)
+      const uint64_t* rec = reinterpret_cast<const uint64_t*>(frames + tile_first[t]);
+      const uint64_t w0 = rec[0];  // fin, rsv, opcode, masked, mask[4]
+      f_len = (int64_t)rec[1];
+      f_po = rec[2];
+      f_src = rec[3];
+      f_end = f_po + round16((uint64_t)f_len);
+      f_key = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
+    }
+    if (t + U <= tend && base + U * kTile <= f_end) {
+      const uint64_t rel0 = base - f_po + lane_off;
+      const uint8_t* src = in + f_src + rel0;
+      uint8_t* dst = out + base + lane_off;
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld16u_stream<NTL>(src + u * kTile);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        u32x4 x = v[u] ^ f_key;
+        const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
+        if (rem < 16) x = keep_bytes(x, rem);
+        st16_stream<NTS>(dst + u * kTile, x);
+      }
+      t += U;
+    } else {
+      const uint64_t p = base + lane_off;
+      if (p < total) {
+        uint64_t po = f_po, so = f_src;
+        int64_t L = f_len;
+        uint32_t key = f_key;
+        if (p >= f_end) {
+          const gevws_frame* fr = frames + find_frame(frames, tile_first, t, ntiles, nframes, p);
+          po = fr->payload_off;
+          so = fr->src_off;
+          L = fr->hdr.length;
+          uint32_t k;
+          memcpy(&k, fr->hdr.mask, 4);
+          key = fr->hdr.masked ? k : 0u;
+        }
+        const uint64_t rel = p - po;
+        u32x4 x = ld16u_stream<NTL>(in + so + rel) ^ key;
+        const int64_t rem = L - (int64_t)rel;
+        if (rem < 16) x = keep_bytes(x, rem);
+        st16_stream<NTS>(out + p, x);
+      }
+      t += 1;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
 // p[i] ^= mask[(offset + i) & 3] for i in [0, n): 16-byte aligned chunks of the
 // address space; interior chunks use one rotated 32-bit key, edge chunks go
@@ -500,6 +594,8 @@ struct gevws_ctx {
   std::vector<EventSet> evs;  // one set per timed call since the last gevws_ctx_timing
   size_t evs_used = 0;
   gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
+  int unmask_variant = 0;
+  int unmask_grid = 0;  // 0 = auto
 };
 
 namespace {
@@ -525,8 +621,11 @@ struct DeviceGuard {
     }                                                                                   \
   } while (0)
 
+// NULL = the HIP default (null) stream, as in every HIP/CUDA API; callers
+// that want the context's own stream pass gevws_ctx_stream(ctx).
 hipStream_t pick_stream(gevws_ctx* ctx, void* stream) {
-  return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+  (void)ctx;
+  return reinterpret_cast<hipStream_t>(stream);
 }
 
 int ensure_scratch(gevws_ctx* ctx, size_t bytes) {
@@ -543,7 +642,30 @@ int ensure_scratch(gevws_ctx* ctx, size_t bytes) {
   return GEVWS_OK;
 }
 
+using UnmaskFn = void (*)(const uint8_t*, const gevws_frame*, const uint32_t*, const gevws_summary*, uint8_t*);
+struct UnmaskVariant {
+  UnmaskFn fn;
+  int unroll;
+  const char* name;
+};
+// Variant 0 is the default; the others are kept for A/B measurement
+// (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
+const UnmaskVariant kUnmaskVariants[] = {
+    {k_unmask_v2<16, false, true>, 16, "v2 U16 plain-load nt-store"},
+    {k_unmask<4>, 4, "v1 U4 grid-stride per-lane lookup"},
+    {k_unmask_v2<4, false, true>, 4, "v2 U4 plain-load nt-store"},
+    {k_unmask_v2<8, false, true>, 8, "v2 U8 plain-load nt-store"},
+    {k_unmask_v2<16, false, false>, 16, "v2 U16 plain-load plain-store"},
+    {k_unmask_v2<32, false, true>, 32, "v2 U32 plain-load nt-store"},
+    {k_unmask_v2<16, true, true>, 16, "v2 U16 nt-load nt-store"},
+};
+constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
+
 }  // namespace
+
+static int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const uint8_t* d_in,
+                  const gevws_frame* d_frames, const uint32_t* tile_first, const gevws_summary* d_summary,
+                  uint8_t* d_payload);
 
 extern "C" {
 
@@ -601,6 +723,30 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
 }
 
 int gevws_ctx_device(const gevws_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+void* gevws_ctx_stream(const gevws_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  switch (key) {
+    case GEVWS_TUNE_UNMASK_VARIANT:
+      if (value < 0 || value >= kNumUnmaskVariants) return GEVWS_ERR_INVALID;
+      ctx->unmask_variant = (int)value;
+      return GEVWS_OK;
+    case GEVWS_TUNE_UNMASK_GRID:
+      if (value < 0 || value > (1 << 20)) return GEVWS_ERR_INVALID;
+      ctx->unmask_grid = (int)value;
+      return GEVWS_OK;
+    default:
+      return GEVWS_ERR_INVALID;
+  }
+}
+
+const char* gevws_tuning_name(int key, int64_t value) {
+  if (key == GEVWS_TUNE_UNMASK_VARIANT && value >= 0 && value < kNumUnmaskVariants)
+    return kUnmaskVariants[value].name;
+  return nullptr;
+}
 
 int gevws_ctx_set_timing(gevws_ctx* ctx, int enable) {
   if (!ctx) return GEVWS_ERR_INVALID;
@@ -663,12 +809,8 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     k_walk_emit<<<nblk, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, d_summary,
                                               d_frames, tile_first);
   if (timed) GEVWS_HIP(hipEventRecord(ev[3], st));
-  const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
-  uint64_t grid = (ntiles + kUnmaskUnroll - 1) / kUnmaskUnroll;
-  if (grid > 2048) grid = 2048;
-  if (grid < 1) grid = 1;
-  k_unmask<kUnmaskUnroll><<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary,
-                                                                    d_payload);
+  r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);
+  if (r != GEVWS_OK) return r;
   if (timed) GEVWS_HIP(hipEventRecord(ev[4], st));
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;
@@ -736,3 +878,16 @@ int gevws_synth_verify_async(gevws_ctx* ctx, void* stream, const gevws_synth_des
 }
 
 }  // extern "C"
+
+static int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const uint8_t* d_in,
+                  const gevws_frame* d_frames, const uint32_t* tile_first, const gevws_summary* d_summary,
+                  uint8_t* d_payload) {
+  const UnmaskVariant& v = kUnmaskVariants[ctx->unmask_variant];
+  const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
+  uint64_t grid = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : 1024;  // 4 workgroups per CU (A/B: profiles/)
+  const uint64_t useful = (ntiles + v.unroll - 1) / v.unroll;
+  if (grid > useful) grid = useful;
+  if (grid < 1) grid = 1;
+  v.fn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary, d_payload);
+  return GEVWS_OK;
+}

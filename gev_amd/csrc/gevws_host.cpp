@@ -221,12 +221,13 @@ class Protocol {
           !grow_dev(&d_frames_, &d_frames_cap_, max_frames * sizeof(gevws_frame)) ||
           !grow_dev(&d_payload_, &d_payload_cap_, payload_cap + 16))
         return fail(prev, dev);
-      hipStream_t st = nullptr;  // the context's stream is used by the decode; copies sync below
-      if (hipMemcpy(d_in_, h_in_, total + GEVWS_IN_PAD, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(d_conns_, cin.data(), m * sizeof(gevws_conn_in), hipMemcpyHostToDevice) != hipSuccess)
+      // stage -> H2D -> decode on the context's stream (pinned source: async DMA)
+      void* st = gevws_ctx_stream(ctx_);
+      if (hipMemcpyAsync(d_in_, h_in_, total + GEVWS_IN_PAD, hipMemcpyHostToDevice, (hipStream_t)st) != hipSuccess ||
+          hipMemcpyAsync(d_conns_, cin.data(), m * sizeof(gevws_conn_in), hipMemcpyHostToDevice,
+                         (hipStream_t)st) != hipSuccess)
         return fail(prev, dev);
-      (void)st;
-      int r = gevws_decode_batch(ctx_, nullptr, (const uint8_t*)d_in_, total, (gevws_conn_in*)d_conns_, m,
+      int r = gevws_decode_batch(ctx_, st, (const uint8_t*)d_in_, total, (gevws_conn_in*)d_conns_, m,
                                  (gevws_frame*)d_frames_, max_frames, (uint8_t*)d_payload_, payload_cap,
                                  (gevws_conn_out*)d_cout_, &sum);
       if (r == GEVWS_ERR_CAPACITY && attempt == 0) {

@@ -113,6 +113,16 @@ int gevws_device_count(void);
 gevws_ctx *gevws_ctx_create(int device);
 void gevws_ctx_destroy(gevws_ctx *ctx);
 int gevws_ctx_device(const gevws_ctx *ctx);
+/* The context's own non-blocking hipStream_t (one per event loop). */
+void *gevws_ctx_stream(const gevws_ctx *ctx);
+/* Tuning knobs for measurement (defaults are the tuned choice):
+ * GEVWS_TUNE_UNMASK_VARIANT selects an unmask kernel variant (0 = default),
+ * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto). */
+#define GEVWS_TUNE_UNMASK_VARIANT 1
+#define GEVWS_TUNE_UNMASK_GRID 2
+int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
+/* Human-readable name of a tuning value, or NULL. */
+const char *gevws_tuning_name(int key, int64_t value);
 /* Per-phase HIP-event timing of the following decode calls (0 = off). */
 int gevws_ctx_set_timing(gevws_ctx *ctx, int enable);
 /* Waits for the timed calls since the previous query and returns the summed
@@ -128,7 +138,7 @@ int gevws_ctx_timing(gevws_ctx *ctx, float ms_sum[4], uint32_t *calls);
  * return (nil, nil), exactly as Connection.handlerProtocol drives it
  * (connection.go:208-218).  All pointers d_* are device pointers; d_in must
  * have GEVWS_IN_PAD readable bytes past in_bytes.  Enqueued on `stream`
- * (hipStream_t, NULL = the context's default stream).  Returns GEVWS_OK when
+ * (hipStream_t; NULL = the HIP default stream).  Returns GEVWS_OK when
  * enqueued; the batch's own outcome is d_summary->status. */
 int gevws_decode_batch_async(gevws_ctx *ctx, void *stream, const uint8_t *d_in, uint64_t in_bytes,
                              const gevws_conn_in *d_conns, uint32_t n_conns,

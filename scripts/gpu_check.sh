@@ -1,12 +1,18 @@
 #!/bin/bash
-# one GPU session: parity tests, smoke, short bench (each step time-limited)
-mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
-if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-rc=$?; echo "smoke rc=$rc"; cat gpurun_out/smoke.log | tail -5
-if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 400 python bench.py --steps 10 --warmup 2 --cpu-seconds 5 > gpurun_out/bench.json 2> gpurun_out/bench.err
-rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.err; cat gpurun_out/bench.json
-exit $rc
+# GPU session: parity tests, smoke, A/B of unmask variants, bench, rocprof.
+# Every GPU step has its own time limit; a fault/abort/timeout ends the script.
+OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out
+mkdir -p $OUT
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "== $name"; timeout -k 10 $to "$@" > $OUT/$name.log 2> $OUT/$name.err
+  local rc=$?; echo "$name rc=$rc"; tail -3 $OUT/$name.err
+  return $rc
+}
+step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x
+rc=$?; tail -15 $OUT/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+step smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+step ab 600 python tools/ab_unmask.py --rounds 5 --reps 3 --grids 1024,2048,4096 || exit $?
+cat $OUT/ab.log
+step bench 400 python bench.py --steps 20 --warmup 3 || exit $?
+cat $OUT/bench.log
