@@ -42,7 +42,8 @@ def log(*a):
 
 def build_layout(name: str, rank: int, conns: int | None):
     from gev_amd import workloads as w
-    seed = 0x67657600 + 7919 * rank
+    from gev_amd.dist import rank_seed
+    seed = rank_seed(0x67657600, rank)
     if name == "c3":
         return w.config_c3(seed=seed, n_conns=conns or 16384)
     if name == "c2":
@@ -110,19 +111,16 @@ def main():
 
     import numpy as np
     import torch
-    import torch.distributed as dist
 
     import gev_amd
+    from gev_amd import dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = dist.env()
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+    dist.init("nccl", dev)  # RCCL over xGMI when WORLD_SIZE > 1
 
     eng = gev_amd.Engine(local)
     t_setup = time.time()
@@ -156,33 +154,25 @@ def main():
     def step():
         eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, max_frames, cap)
         torch.index_select(sum64, 0, sel, out=counts)
-        if world > 1:
-            dist.all_reduce(counts)  # decoded {frames, payload bytes, errors}, summed over GPUs
+        dist.reduce_counts(counts)  # decoded {frames, payload bytes, errors}, summed over GPUs
 
     for _ in range(args.warmup):
         step()
     eng.timing()  # drop anything recorded so far
-    if world > 1:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize()
     eng.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    if world > 1:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     eng.set_timing(False)
     phases, calls = eng.timing()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = dist.max_over_ranks(t1 - t0, dev)
     c = counts.cpu().numpy()
     frames_step, payload_step, errors = int(c[0]), int(c[1]), int(c[2])
-    if world == 1:
-        frames_step, payload_step = int(s["frames"]), int(s["payload_len"])
     ms_step = elapsed / args.steps * 1e3
     value = payload_step * args.steps / elapsed / 2**30
     mean_ms = [p / max(calls, 1) for p in phases]
@@ -192,8 +182,7 @@ def main():
     pipeline_gbps = alg_bytes / (sum(mean_ms) / 1e3) / 1e9
 
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
+        dist.finalize()
         return
     result = {
         "metric": METRIC,
@@ -231,8 +220,7 @@ def main():
             result["cpu_baseline_multi"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0),
                                                         args.cpu_threads_multi)
     print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    dist.finalize()
 
 
 if __name__ == "__main__":

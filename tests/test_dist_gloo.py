@@ -1,0 +1,92 @@
+"""N > 1 path on the CPU: two ranks over gloo run the same sharding and
+collective code the bench runs over RCCL (gev_amd/dist.py), with each rank's
+decode done by the oracle.  Checks that the connection -> rank split covers
+every connection exactly once, that the summed counts equal the whole batch's,
+and the max-over-ranks timing reduce."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    import torch
+    from gev_amd import dist, workloads as w
+    from oracle import ref
+    dist.init("gloo")
+    res = {}
+    # strong scaling: one global batch, connections split byte-balanced
+    glob = w.config_c5(n_conns=7, messages_per_conn=1, message_bytes=48 * 1024, seed=3)
+    part = w.shard(glob, rank, world)
+    arena = np.concatenate([w.synth_host(part), np.zeros(64, np.uint8)])
+    r = ref.decode_batch(arena, part.conns[:, 0], part.conns[:, 1])
+    counts = torch.tensor([r["frames"].shape[0], int(r["frames"]["length"].sum()),
+                           int((r["conn_status"] < 0).sum())], dtype=torch.int64)
+    dist.reduce_counts(counts)
+    res["strong"] = counts.tolist()
+    res["strong_conns"] = part.n_conns
+    # weak scaling: every rank its own same-shape batch
+    lay = w.uniform(3, 4, 1000, seed=dist.rank_seed(5, rank))
+    arena = np.concatenate([w.synth_host(lay), np.zeros(64, np.uint8)])
+    r = ref.decode_batch(arena, lay.conns[:, 0], lay.conns[:, 1])
+    counts = torch.tensor([r["frames"].shape[0], int(r["frames"]["length"].sum()), 0], dtype=torch.int64)
+    dist.reduce_counts(counts)
+    res["weak"] = counts.tolist()
+    res["max"] = dist.max_over_ranks(float(rank + 1), "cpu")
+    dist.barrier()
+    dist.finalize()
+    json.dump(res, open(os.path.join(outdir, f"r{rank}.json"), "w"))
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_shard_and_count_reduce(tmp_path, world):
+    import torch.multiprocessing as mp
+    from gev_amd import workloads as w
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+    glob = w.config_c5(n_conns=7, messages_per_conn=1, message_bytes=48 * 1024, seed=3)
+    for r in res:
+        assert r["strong"] == [glob.n_frames, glob.payload_len, 0]
+        assert r["weak"] == [world * 12, world * 12 * 1000, 0]
+        assert r["max"] == float(world)
+    assert sum(r["strong_conns"] for r in res) == glob.n_conns
+
+
+def test_shard_bounds_partition_and_balance():
+    from gev_amd import workloads as w
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        n = int(rng.integers(0, 50))
+        lens = rng.integers(0, 10_000, n)
+        for world in (1, 2, 3, 4, 8):
+            b = w.shard_bounds(lens, world)
+            assert b[0] == 0 and b[-1] == n and len(b) == world + 1
+            assert all(b[i] <= b[i + 1] for i in range(world))
+            if n and lens.sum():
+                share = lens.sum() / world
+                for r in range(world):
+                    got = lens[b[r]:b[r + 1]].sum()
+                    assert got <= share + lens.max() + 1
+
+
+def test_shard_layouts_reassemble():
+    from gev_amd import workloads as w
+    lay = w.config_c4(total_payload=2 << 20, n_conns=16, seed=9)
+    parts = [w.shard(lay, r, 4) for r in range(4)]
+    assert sum(p.n_frames for p in parts) == lay.n_frames
+    assert sum(p.payload_len for p in parts) == lay.payload_len
+    assert sum(p.arena_bytes for p in parts) == lay.arena_bytes
+    assert np.array_equal(np.concatenate([p.desc["length"] for p in parts]), lay.desc["length"])

@@ -200,3 +200,20 @@ def test_c5_fragmented_control_property(engine):
     from gev_amd import workloads
     lay = workloads.config_c5(n_conns=16, messages_per_conn=2)
     _synth_decode_verify(engine, lay, check_slice_conns=16)
+
+
+def test_device_generator_matches_host_generator(engine):
+    """The device frame generator (bench / full-size property tests) writes
+    exactly the bytes of workloads.synth_host, so the oracle-checked slices
+    above stand for the whole batch's format."""
+    import torch
+    import gev_amd
+    from gev_amd import workloads as w
+    dev = torch.device("cuda", engine.device)
+    for lay in (w.uniform(3, 5, 4096 + 7, seed=11), w.config_c5(n_conns=3, messages_per_conn=1, seed=12),
+                w.config_c4(total_payload=1 << 20, n_conns=4, seed=13)):
+        arena = torch.zeros(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+        desc = torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev)
+        engine.synth(arena, desc, lay.n_frames, lay.seed)
+        torch.cuda.synchronize()
+        assert np.array_equal(arena[: lay.arena_bytes].cpu().numpy(), w.synth_host(lay)), lay.name
