@@ -291,6 +291,37 @@ class Protocol:
             raise RuntimeError(f"unpacket_batch: {status_string(int(r))}")
         return int(r)
 
+    def decode_host(self, segments: Sequence[Tuple[bytes, bytes]]):
+        """gevws_decode_host_batch: [(first, end)] host segments per connection ->
+        (frames, payload arena, conn_out, summary) as numpy arrays (the FFI form)."""
+        n = len(segments)
+        keep = []
+        hc = (_abi.HostConn * max(n, 1))()
+        total = 0
+        for i, (a, b) in enumerate(segments):
+            ba = np.frombuffer(a, np.uint8) if a else np.zeros(0, np.uint8)
+            bb = np.frombuffer(b, np.uint8) if b else np.zeros(0, np.uint8)
+            keep += [ba, bb]
+            hc[i].seg0, hc[i].n0 = (ba.ctypes.data if ba.size else None), ba.size
+            hc[i].seg1, hc[i].n1 = (bb.ctypes.data if bb.size else None), bb.size
+            total += ba.size + bb.size
+        max_frames = total // 2 + 1
+        cap = total + 16 * max_frames + 16
+        for _ in range(2):
+            frames = np.zeros(max_frames, FRAME_DTYPE)
+            payload = np.zeros(cap, np.uint8)
+            cout = np.zeros(max(n, 1), CONN_OUT_DTYPE)
+            s = _abi.Summary()
+            r = lib.gevws_decode_host_batch(self._p, hc, n, frames.ctypes.data, max_frames, payload.ctypes.data,
+                                            cap, cout.ctypes.data, ctypes.byref(s))
+            if r == ERR_CAPACITY:
+                max_frames, cap = max(s.frames, 1), max(s.payload_bytes, 16)
+                continue
+            if r < 0:
+                raise RuntimeError(f"decode_host: {status_string(int(r))}")
+            return frames[:s.frames], payload[:s.payload_bytes], cout[:n], s
+        raise RuntimeError("decode_host: capacity retry failed")
+
     def packet(self, c: Connection, data: bytes) -> bytes:
         """Packet(c, data) -> data (protocol.go:67-69)."""
         return data

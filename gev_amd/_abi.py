@@ -61,6 +61,11 @@ class Summary(ctypes.Structure):
                 ("reserved0", ctypes.c_uint32), ("reserved", ctypes.c_uint64 * 3)]
 
 
+class HostConn(ctypes.Structure):
+    _fields_ = [("seg0", ctypes.c_void_p), ("n0", ctypes.c_uint64), ("seg1", ctypes.c_void_p),
+                ("n1", ctypes.c_uint64)]
+
+
 class SynthDesc(ctypes.Structure):
     _fields_ = [("hdr_off", ctypes.c_uint64), ("length", ctypes.c_uint64), ("mask", ctypes.c_uint32),
                 ("b0", ctypes.c_uint8), ("len_form", ctypes.c_uint8), ("masked", ctypes.c_uint8),
@@ -114,6 +119,10 @@ SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_uint64)]),
     "gevws_protocol_unpacket_batch": (ctypes.c_int64, [P, P, P, ctypes.c_uint32]),
     "gevws_protocol_packet": (U8P, [P, P, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    "gevws_decode_host_stream": (ctypes.c_int64, [P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.c_uint64,
+                                                  P, ctypes.c_uint64, P, ctypes.POINTER(Summary)]),
+    "gevws_decode_host_batch": (ctypes.c_int64, [P, P, ctypes.c_uint32, P, ctypes.c_uint64, P, ctypes.c_uint64,
+                                                 P, ctypes.POINTER(Summary)]),
 }
 
 

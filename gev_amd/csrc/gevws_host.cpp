@@ -179,68 +179,23 @@ class Protocol {
     // Connections that already hold undelivered frames (or are poisoned) are
     // skipped: their ring prefix is already decoded.
     std::vector<uint32_t> sel;
+    std::vector<gevws_host_conn> segs;
     sel.reserve(n);
-    uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) {
       if (!conns[i]->upgraded || !conns[i]->queue.empty() || conns[i]->poisoned != GEVWS_OK) continue;
-      const uint64_t len = rings[i]->Length();
-      if (len < 6) continue;  // read.go:20-23: nothing can be decoded
+      if (rings[i]->Length() < 6) continue;  // read.go:20-23: nothing can be decoded
+      gevws_host_conn h;
+      rings[i]->PeekAll(&h.seg0, &h.n0, &h.seg1, &h.n1);
       sel.push_back(i);
-      total += len;
+      segs.push_back(h);
     }
     if (sel.empty()) return 0;
     const uint32_t m = (uint32_t)sel.size();
-    const int dev = gevws_ctx_device(ctx_);
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    if (prev != dev) (void)hipSetDevice(dev);
-
-    // stage: PeekAll segments joined per connection into pinned memory
-    std::vector<gevws_conn_in> cin(m);
-    if (!grow_host(&h_in_, &h_in_cap_, total + GEVWS_IN_PAD)) return fail(prev, dev);
-    uint64_t off = 0;
-    for (uint32_t j = 0; j < m; ++j) {
-      const uint8_t *a, *b;
-      uint64_t na, nb;
-      rings[sel[j]]->PeekAll(&a, &na, &b, &nb);
-      memcpy(h_in_ + off, a, na);
-      if (nb) memcpy(h_in_ + off + na, b, nb);
-      cin[j] = {off, na + nb};
-      off += na + nb;
-    }
-    memset(h_in_ + off, 0, GEVWS_IN_PAD);
-    // first attempt sized for the usual case; on ERR_CAPACITY the summary
-    // carries the exact sizes and the batch is run once more
-    uint64_t max_frames = std::min<uint64_t>(total / 2 + 1, 0xFFFFFFFFull);
-    uint64_t payload_cap = total + 16 * std::min<uint64_t>(max_frames, total / 64 + 64) + 64;
     gevws_summary sum{};
-    for (int attempt = 0; attempt < 2; ++attempt) {
-      if (!grow_dev(&d_in_, &d_in_cap_, total + GEVWS_IN_PAD) ||
-          !grow_dev(&d_conns_, &d_conns_cap_, m * sizeof(gevws_conn_in)) ||
-          !grow_dev(&d_cout_, &d_cout_cap_, m * sizeof(gevws_conn_out)) ||
-          !grow_dev(&d_frames_, &d_frames_cap_, max_frames * sizeof(gevws_frame)) ||
-          !grow_dev(&d_payload_, &d_payload_cap_, payload_cap + 16))
-        return fail(prev, dev);
-      // stage -> H2D -> decode on the context's stream (pinned source: async DMA)
-      void* st = gevws_ctx_stream(ctx_);
-      if (hipMemcpyAsync(d_in_, h_in_, total + GEVWS_IN_PAD, hipMemcpyHostToDevice, (hipStream_t)st) != hipSuccess ||
-          hipMemcpyAsync(d_conns_, cin.data(), m * sizeof(gevws_conn_in), hipMemcpyHostToDevice,
-                         (hipStream_t)st) != hipSuccess)
-        return fail(prev, dev);
-      int r = gevws_decode_batch(ctx_, st, (const uint8_t*)d_in_, total, (gevws_conn_in*)d_conns_, m,
-                                 (gevws_frame*)d_frames_, max_frames, (uint8_t*)d_payload_, payload_cap,
-                                 (gevws_conn_out*)d_cout_, &sum);
-      if (r == GEVWS_ERR_CAPACITY && attempt == 0) {
-        max_frames = std::max<uint64_t>(sum.frames, 1);
-        payload_cap = std::max<uint64_t>(sum.payload_bytes, 16);
-        continue;
-      }
-      if (r != GEVWS_OK) {
-        if (prev != dev) (void)hipSetDevice(prev);
-        return r;
-      }
-      break;
-    }
+    std::vector<gevws_conn_in> cin;
+    DeviceScope scope(gevws_ctx_device(ctx_));
+    int64_t r = StageDecode(segs.data(), m, &sum, cin);
+    if (r < 0) return r;
     // results back to the host
     std::vector<gevws_conn_out> cout(m);
     std::vector<gevws_frame> fr(sum.frames);
@@ -250,8 +205,7 @@ class Protocol {
                                  hipMemcpyDeviceToHost) != hipSuccess) ||
         (sum.payload_bytes && hipMemcpy(arena->data(), d_payload_, sum.payload_bytes,
                                         hipMemcpyDeviceToHost) != hipSuccess))
-      return fail(prev, dev);
-    if (prev != dev) (void)hipSetDevice(prev);
+      return fail();
     // hand the frames to their connections in stream order
     for (uint32_t j = 0; j < m; ++j) {
       Connection* c = conns[sel[j]];
@@ -272,9 +226,90 @@ class Protocol {
     return (int64_t)sum.frames;
   }
 
+  // Host segments in, caller buffers out (gevws_decode_host_batch).
+  int64_t DecodeHost(const gevws_host_conn* segs, uint32_t n, gevws_frame* frames, uint64_t max_frames,
+                     uint8_t* payload, uint64_t payload_cap, gevws_conn_out* conn_out, gevws_summary* sum_out) {
+    gevws_summary sum{};
+    *sum_out = sum;
+    if (n == 0) return 0;
+    std::vector<gevws_conn_in> cin;
+    DeviceScope scope(gevws_ctx_device(ctx_));
+    int64_t r = StageDecode(segs, n, &sum, cin);
+    if (r < 0) return r;
+    // src_off is reported relative to each connection's own stream
+    *sum_out = sum;
+    if (sum.frames > max_frames || sum.payload_bytes > payload_cap) {
+      sum_out->status = GEVWS_ERR_CAPACITY;
+      return GEVWS_ERR_CAPACITY;
+    }
+    if (hipMemcpy(conn_out, d_cout_, n * sizeof(gevws_conn_out), hipMemcpyDeviceToHost) != hipSuccess ||
+        (sum.frames && hipMemcpy(frames, d_frames_, sum.frames * sizeof(gevws_frame),
+                                 hipMemcpyDeviceToHost) != hipSuccess) ||
+        (sum.payload_bytes && hipMemcpy(payload, d_payload_, sum.payload_bytes,
+                                        hipMemcpyDeviceToHost) != hipSuccess))
+      return fail();
+    for (uint32_t j = 0; j < n; ++j)
+      for (uint32_t k = 0; k < conn_out[j].nframes; ++k) frames[conn_out[j].first_frame + k].src_off -= cin[j].off;
+    return (int64_t)sum.frames;
+  }
+
  private:
-  int64_t fail(int prev, int dev) {
-    if (prev != dev) (void)hipSetDevice(prev);
+  struct DeviceScope {
+    int prev = -1, dev;
+    explicit DeviceScope(int d) : dev(d) {
+      if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+      if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceScope() {
+      if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+  };
+
+  // Join each connection's segments into pinned staging, H2D, decode on the
+  // context's stream; results stay in the device buffers.  Retries once with
+  // the exact sizes on ERR_CAPACITY.
+  int64_t StageDecode(const gevws_host_conn* segs, uint32_t m, gevws_summary* sum,
+                      std::vector<gevws_conn_in>& cin) {
+    uint64_t total = 0;
+    for (uint32_t j = 0; j < m; ++j) total += segs[j].n0 + segs[j].n1;
+    cin.resize(m);
+    if (!grow_host(&h_in_, &h_in_cap_, total + GEVWS_IN_PAD)) return fail();
+    uint64_t off = 0;
+    for (uint32_t j = 0; j < m; ++j) {
+      if (segs[j].n0) memcpy(h_in_ + off, segs[j].seg0, segs[j].n0);
+      if (segs[j].n1) memcpy(h_in_ + off + segs[j].n0, segs[j].seg1, segs[j].n1);
+      cin[j] = {off, segs[j].n0 + segs[j].n1};
+      off += cin[j].len;
+    }
+    memset(h_in_ + off, 0, GEVWS_IN_PAD);
+    uint64_t max_frames = std::min<uint64_t>(total / 2 + 1, 0xFFFFFFFFull);
+    uint64_t payload_cap = total + 16 * std::min<uint64_t>(max_frames, total / 64 + 64) + 64;
+    void* st = gevws_ctx_stream(ctx_);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      if (!grow_dev(&d_in_, &d_in_cap_, total + GEVWS_IN_PAD) ||
+          !grow_dev(&d_conns_, &d_conns_cap_, m * sizeof(gevws_conn_in)) ||
+          !grow_dev(&d_cout_, &d_cout_cap_, m * sizeof(gevws_conn_out)) ||
+          !grow_dev(&d_frames_, &d_frames_cap_, max_frames * sizeof(gevws_frame)) ||
+          !grow_dev(&d_payload_, &d_payload_cap_, payload_cap + 16))
+        return fail();
+      if (hipMemcpyAsync(d_in_, h_in_, total + GEVWS_IN_PAD, hipMemcpyHostToDevice, (hipStream_t)st) != hipSuccess ||
+          hipMemcpyAsync(d_conns_, cin.data(), m * sizeof(gevws_conn_in), hipMemcpyHostToDevice,
+                         (hipStream_t)st) != hipSuccess)
+        return fail();
+      int r = gevws_decode_batch(ctx_, st, (const uint8_t*)d_in_, total, (gevws_conn_in*)d_conns_, m,
+                                 (gevws_frame*)d_frames_, max_frames, (uint8_t*)d_payload_, payload_cap,
+                                 (gevws_conn_out*)d_cout_, sum);
+      if (r == GEVWS_ERR_CAPACITY && attempt == 0) {
+        max_frames = std::max<uint64_t>(sum->frames, 1);
+        payload_cap = std::max<uint64_t>(sum->payload_bytes, 16);
+        continue;
+      }
+      return r == GEVWS_OK ? (int64_t)sum->frames : (int64_t)r;
+    }
+    return GEVWS_ERR_CAPACITY;
+  }
+
+  int64_t fail() {
     log_error("device: ", GEVWS_ERR_DEVICE);
     return GEVWS_ERR_DEVICE;
   }
@@ -363,6 +398,20 @@ int64_t gevws_protocol_unpacket_batch(gevws_protocol* p, gevws_conn* const* conn
     rs[i] = rings[i];
   }
   return p->UnPacketBatch(cs.data(), rs.data(), n);
+}
+
+int64_t gevws_decode_host_batch(gevws_protocol* p, const gevws_host_conn* conns, uint32_t n,
+                                gevws_frame* frames, uint64_t max_frames, uint8_t* payload, uint64_t payload_cap,
+                                gevws_conn_out* conn_out, gevws_summary* summary) {
+  if (!p || !summary || (n && (!conns || !conn_out))) return GEVWS_ERR_INVALID;
+  return p->DecodeHost(conns, n, frames, max_frames, payload, payload_cap, conn_out, summary);
+}
+
+int64_t gevws_decode_host_stream(gevws_protocol* p, const uint8_t* seg0, uint64_t n0, const uint8_t* seg1,
+                                 uint64_t n1, gevws_frame* frames, uint64_t max_frames, uint8_t* payload,
+                                 uint64_t payload_cap, gevws_conn_out* conn_out, gevws_summary* summary) {
+  const gevws_host_conn hc = {seg0, n0, seg1, n1};
+  return gevws_decode_host_batch(p, &hc, 1, frames, max_frames, payload, payload_cap, conn_out, summary);
 }
 
 const uint8_t* gevws_protocol_packet(gevws_protocol* p, gevws_conn* c, const uint8_t* data, uint64_t n,

@@ -234,6 +234,34 @@ int gevws_protocol_unpacket(gevws_protocol *p, gevws_conn *c, gevws_ring *ring,
 int64_t gevws_protocol_unpacket_batch(gevws_protocol *p, gevws_conn *const *conns,
                                       gevws_ring *const *rings, uint32_t n);
 
+/* One connection's buffered bytes in host memory, as ringbuffer.PeekAll()
+ * returns them (first, end) -- e.g. two Go slices passed through cgo. */
+typedef struct gevws_host_conn {
+    const uint8_t *seg0;
+    uint64_t n0;
+    const uint8_t *seg1;
+    uint64_t n1;
+} gevws_host_conn;
+
+/* Host-memory form of the batch decode for FFI callers (cgo): the segments of
+ * n connections are staged into pinned memory, decoded on the device and the
+ * results copied into the caller's buffers (frames, 16-byte-aligned payload
+ * arena, per-connection results).  frames[i].src_off is relative to its own
+ * connection's joined segments.  Returns the frame count, GEVWS_ERR_CAPACITY
+ * (with *summary holding the sizes needed), or < 0.  Nothing is retained. */
+int64_t gevws_decode_host_batch(gevws_protocol *p, const gevws_host_conn *conns, uint32_t n,
+                                gevws_frame *frames, uint64_t max_frames, uint8_t *payload,
+                                uint64_t payload_cap, gevws_conn_out *conn_out,
+                                gevws_summary *summary);
+
+/* One connection, segments as plain arguments (cgo may pass Go slice pointers
+ * as arguments but not inside a struct): repeated UnPacket over
+ * seg0 || seg1, i.e. ringbuffer.PeekAll()'s (first, end). */
+int64_t gevws_decode_host_stream(gevws_protocol *p, const uint8_t *seg0, uint64_t n0,
+                                 const uint8_t *seg1, uint64_t n1, gevws_frame *frames,
+                                 uint64_t max_frames, uint8_t *payload, uint64_t payload_cap,
+                                 gevws_conn_out *conn_out, gevws_summary *summary);
+
 /* websocket.(*Protocol).Packet (protocol.go:67-69): identity. */
 const uint8_t *gevws_protocol_packet(gevws_protocol *p, gevws_conn *c, const uint8_t *data,
                                      uint64_t n, uint64_t *out_len);

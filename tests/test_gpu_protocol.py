@@ -124,3 +124,53 @@ def test_need_more_then_complete(engine):
     r.write(w)
     h, d = proto.unpacket(c, r)
     assert d == bytes(range(200)) and h.length == 200 and r.length() == 0
+
+
+def test_decode_host_batch_two_segments(engine):
+    """gevws_decode_host_batch (the cgo entry point): each connection's bytes
+    arrive as the two PeekAll segments of a wrapped ring (connection.go:237-244)."""
+    from tests._helpers import random_stream
+    rng = np.random.default_rng(23)
+    proto = gev_amd.Protocol(engine)
+    streams = [random_stream(rng, int(rng.integers(0, 20))) for _ in range(50)]
+    segs = []
+    for s in streams:
+        cut = int(rng.integers(0, len(s) + 1))
+        segs.append((s[:cut], s[cut:]))
+    frames, payload, cout, summ = proto.decode_host(segs)
+    for ci, s in enumerate(streams):
+        want = wo.decode_stream(s)
+        assert int(cout["nframes"][ci]) == len(want.frames)
+        assert int(cout["consumed"][ci]) == want.consumed
+        assert int(cout["status"][ci]) == want.status
+        for j, fr in enumerate(want.frames):
+            f = frames[int(cout["first_frame"][ci]) + j]
+            assert f.tobytes()[:16] == fr.header.pack()
+            assert int(f["src_off"]) == fr.stream_pos + fr.header_len
+            o = int(f["payload_off"])
+            assert payload[o:o + fr.header.length].tobytes() == fr.payload
+    assert summ.frames == sum(len(wo.decode_stream(s).frames) for s in streams)
+
+
+def test_decode_host_stream_single_connection(engine):
+    import ctypes
+    from gev_amd import _abi
+    rng = np.random.default_rng(24)
+    from tests._helpers import random_stream
+    proto = gev_amd.Protocol(engine)
+    s = random_stream(rng, 30)
+    cut = len(s) // 3
+    a = np.frombuffer(s[:cut], np.uint8).copy()
+    b = np.frombuffer(s[cut:], np.uint8).copy()
+    frames = np.zeros(len(s), gev_amd.FRAME_DTYPE)
+    payload = np.zeros(len(s) * 20 + 64, np.uint8)
+    cout = np.zeros(1, gev_amd.CONN_OUT_DTYPE)
+    summ = _abi.Summary()
+    n = gev_amd.lib.gevws_decode_host_stream(proto._p, a.ctypes.data, a.size, b.ctypes.data, b.size,
+                                             frames.ctypes.data, frames.size, payload.ctypes.data, payload.size,
+                                             cout.ctypes.data, ctypes.byref(summ))
+    want = wo.decode_stream(s)
+    assert n == len(want.frames) and int(cout["consumed"][0]) == want.consumed
+    for f, fr in zip(frames[:n], want.frames):
+        o = int(f["payload_off"])
+        assert f.tobytes()[:16] == fr.header.pack() and payload[o:o + fr.header.length].tobytes() == fr.payload
