@@ -452,6 +452,137 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v2(const uint8_t* __res
   }
 }
 
+// v3 = v2's streaming fast path + a cooperative small-frame path.  When the
+// next U tiles are not inside the cached frame, the workgroup takes a window
+// of W tiles, loads the records of every frame overlapping it (tile map gives
+// the index range) into LDS with one coalesced pass, and each lane finds the
+// frame of each of its W chunks by binary search in LDS -- no dependent global
+// loads per chunk.  Windows with more than kWinFrames frames (runs of empty
+// frames) fall back to the per-lane global lookup.
+constexpr int kWinTiles = 4;
+constexpr int kWinFrames = 1024;
+
+template <int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __restrict__ in,
+                                                            const gevws_frame* __restrict__ frames,
+                                                            const uint32_t* __restrict__ tile_first,
+                                                            const gevws_summary* __restrict__ sum,
+                                                            uint8_t* __restrict__ out) {
+  __shared__ uint32_t s_start[kWinFrames];   // frame start relative to the window (clamped at 0)
+  __shared__ int32_t s_lend[kWinFrames];     // payload end relative to the window (clamped)
+  __shared__ uint64_t s_delta[kWinFrames];   // src_off - payload_off (mod 2^64)
+  __shared__ uint32_t s_key[kWinFrames];
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t total = sum->payload_bytes;
+  const uint64_t nframes = sum->frames;
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  uint64_t t = (uint64_t)blockIdx.x * per;
+  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+  const uint32_t lane_off = threadIdx.x * 16;
+  uint64_t f_po = 0, f_end = 0, f_src = 0;
+  int64_t f_len = 0;
+  uint32_t f_key = 0;
+  while (t < tend) {
+    const uint64_t base = t * kTile;
+    if (base >= f_end) {  // workgroup-uniform: refresh the cached frame (scalar loads)
+      const uint64_t* rec = reinterpret_cast<const uint64_t*>(frames + tile_first[t]);
+      const uint64_t w0 = rec[0];
+      f_len = (int64_t)rec[1];
+      f_po = rec[2];
+      f_src = rec[3];
+      f_end = f_po + round16((uint64_t)f_len);
+      f_key = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
+    }
+    if (t + U <= tend && base + U * kTile <= f_end) {
+      const uint64_t rel0 = base - f_po + lane_off;
+      const uint8_t* src = in + f_src + rel0;
+      uint8_t* dst = out + base + lane_off;
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld16u_stream<NTL>(src + u * kTile);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        u32x4 x = v[u] ^ f_key;
+        const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
+        if (rem < 16) x = keep_bytes(x, rem);
+        st16_stream<NTS>(dst + u * kTile, x);
+      }
+      t += U;
+      continue;
+    }
+    // ---- window path
+    const uint64_t wt = (tend - t) < (uint64_t)kWinTiles ? (tend - t) : (uint64_t)kWinTiles;
+    const uint64_t wend_t = t + wt;
+    const uint64_t wbase = base;
+    const uint64_t f_lo = tile_first[t];
+    const uint64_t f_hi = wend_t < ntiles ? (uint64_t)tile_first[wend_t] : nframes - 1;
+    const uint64_t F = f_hi - f_lo + 1;
+    if (F <= (uint64_t)kWinFrames) {
+      __syncthreads();  // previous window's readers are done with the LDS table
+      for (uint64_t i = threadIdx.x; i < F; i += kUnmaskBlock) {
+        const uint64_t* rec = reinterpret_cast<const uint64_t*>(frames + f_lo + i);
+        const uint64_t w0 = rec[0];
+        const uint64_t L = rec[1];
+        const uint64_t po = rec[2];
+        const uint64_t so = rec[3];
+        s_start[i] = po > wbase ? (uint32_t)(po - wbase) : 0u;
+        const uint64_t lend = po + L;  // end of payload bytes
+        s_lend[i] = lend <= wbase ? 0 : (lend - wbase > 0x7fffffffull ? 0x7fffffff : (int32_t)(lend - wbase));
+        s_delta[i] = so - po;
+        s_key[i] = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
+      }
+      __syncthreads();
+      u32x4 v[kWinTiles];
+      uint32_t key[kWinTiles];
+      int32_t rem[kWinTiles];
+#pragma unroll
+      for (int u = 0; u < kWinTiles; ++u) {
+        const uint32_t rel = (uint32_t)(u * kTile) + lane_off;
+        const uint64_t p = wbase + rel;
+        rem[u] = 0;
+        key[u] = 0;
+        v[u] = u32x4{0, 0, 0, 0};
+        if ((uint64_t)u < wt && p < total) {
+          uint32_t lo = 0, hi = (uint32_t)F - 1;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+          }
+          rem[u] = s_lend[lo] - (int32_t)rel;
+          key[u] = s_key[lo];
+          v[u] = ld16u_stream<NTL>(in + (p + s_delta[lo]));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kWinTiles; ++u) {
+        if (rem[u] > 0) {
+          u32x4 x = v[u] ^ key[u];
+          if (rem[u] < 16) x = keep_bytes(x, rem[u]);
+          st16_stream<NTS>(out + wbase + (uint32_t)(u * kTile) + lane_off, x);
+        }
+      }
+      t = wend_t;
+      continue;
+    }
+    // ---- too many frames in the window (runs of empty frames): per-lane lookup, one tile
+    {
+      const uint64_t p = base + lane_off;
+      if (p < total) {
+        const gevws_frame* fr = frames + find_frame(frames, tile_first, t, ntiles, nframes, p);
+        const uint64_t rel = p - fr->payload_off;
+        uint32_t k;
+        memcpy(&k, fr->hdr.mask, 4);
+        u32x4 x = ld16u_stream<NTL>(in + fr->src_off + rel) ^ (fr->hdr.masked ? k : 0u);
+        const int64_t r = fr->hdr.length - (int64_t)rel;
+        if (r < 16) x = keep_bytes(x, r);
+        st16_stream<NTS>(out + p, x);
+      }
+      t += 1;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
 // p[i] ^= mask[(offset + i) & 3] for i in [0, n): 16-byte aligned chunks of the
 // address space; interior chunks use one rotated 32-bit key, edge chunks go
@@ -651,13 +782,13 @@ struct UnmaskVariant {
 // Variant 0 is the default; the others are kept for A/B measurement
 // (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 const UnmaskVariant kUnmaskVariants[] = {
-    {k_unmask_v2<16, false, true>, 16, "v2 U16 plain-load nt-store"},
+    {k_unmask_v3<16, false, true>, 16, "v3 U16 + LDS small-frame window, plain-load nt-store"},
     {k_unmask<4>, 4, "v1 U4 grid-stride per-lane lookup"},
-    {k_unmask_v2<4, false, true>, 4, "v2 U4 plain-load nt-store"},
+    {k_unmask_v2<16, false, true>, 16, "v2 U16 plain-load nt-store"},
     {k_unmask_v2<8, false, true>, 8, "v2 U8 plain-load nt-store"},
-    {k_unmask_v2<16, false, false>, 16, "v2 U16 plain-load plain-store"},
-    {k_unmask_v2<32, false, true>, 32, "v2 U32 plain-load nt-store"},
-    {k_unmask_v2<16, true, true>, 16, "v2 U16 nt-load nt-store"},
+    {k_unmask_v2<4, false, true>, 4, "v2 U4 plain-load nt-store"},
+    {k_unmask_v3<8, false, true>, 8, "v3 U8 + LDS window"},
+    {k_unmask_v3<16, true, true>, 16, "v3 U16 + LDS window, nt-load nt-store"},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 

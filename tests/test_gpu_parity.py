@@ -217,3 +217,22 @@ def test_device_generator_matches_host_generator(engine):
         engine.synth(arena, desc, lay.n_frames, lay.seed)
         torch.cuda.synchronize()
         assert np.array_equal(arena[: lay.arena_bytes].cpu().numpy(), w.synth_host(lay)), lay.name
+
+
+def test_small_frame_window_paths(engine):
+    """The unmask kernel's LDS window path (<= 1024 frames per 16 KiB window)
+    and its fallback (more frames than that: runs of empty frames, 16-byte
+    frames), mixed with frames that straddle windows."""
+    rng = np.random.default_rng(16)
+    m = bytes(rng.integers(0, 256, 4, dtype=np.uint8))
+    tiny16 = b"".join(wo.encode_frame(bytes(rng.integers(0, 256, 16, dtype=np.uint8)), 2, True, 0, True, m)
+                      for _ in range(2500))
+    tiny_mixed = b"".join(wo.encode_frame(bytes(rng.integers(0, 256, int(rng.integers(0, 17)), dtype=np.uint8)),
+                                          2, True, 0, bool(rng.random() < .8), m) for _ in range(3000))
+    empties = b"".join(wo.encode_frame(b"", 9, True, 0, True, m) for _ in range(3000))
+    big = wo.encode_frame(bytes(rng.integers(0, 256, 50000, dtype=np.uint8)), 2, True, 0, True, m)
+    mid = b"".join(wo.encode_frame(bytes(rng.integers(0, 256, int(rng.integers(100, 9000)), dtype=np.uint8)),
+                                   1, True, 0, True, m) for _ in range(40))
+    streams = [tiny16, big + empties + big, tiny_mixed + mid, mid + tiny16[:5000] + big, empties]
+    arena, conns = pack_streams(streams)
+    assert_matches_oracle(engine, arena, conns, "small-frame windows")
