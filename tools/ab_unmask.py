@@ -78,7 +78,7 @@ def main():
         assert int(mism.item()) == 0, (v, g, int(mism.item()))
     print("[ab] all variants verified bit-exact", file=sys.stderr, flush=True)
 
-    n_copy = lay.payload_padded
+    n_copy = min(lay.payload_padded, lay.arena_bytes)
     src = arena[:n_copy]
     dst = out.payload[:n_copy]
     res = {c: [] for c in cfgs}
