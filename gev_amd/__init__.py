@@ -33,6 +33,9 @@ CONN_OUT_DTYPE = np.dtype([("first_frame", "<u8"), ("consumed", "<u8"), ("payloa
                            ("nframes", "<u4"), ("status", "<i4")])
 SUMMARY_DTYPE = np.dtype([("frames", "<u8"), ("payload_bytes", "<u8"), ("payload_len", "<u8"),
                           ("errors", "<u8"), ("status", "<i4"), ("reserved0", "<u4"), ("reserved", "<u8", (3,))])
+OUT_FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked", "u1"),
+                            ("mask", "u1", (4,)), ("length", "<i8"),
+                            ("payload_off", "<u8"), ("payload_len", "<u8")])
 SYNTH_DTYPE = np.dtype([("hdr_off", "<u8"), ("length", "<u8"), ("mask", "<u4"), ("b0", "u1"),
                         ("len_form", "u1"), ("masked", "u1"), ("pad", "u1")])
 assert FRAME_DTYPE.itemsize == 32 and CONN_OUT_DTYPE.itemsize == 32
@@ -170,6 +173,35 @@ class Engine:
                 raise RuntimeError(f"decode: {status_string(int(s['status']))}")
             return out
         raise RuntimeError("decode: capacity retry failed")
+
+    def encode_async(self, frames_dev, n: int, payload, out, out_cap: int, out_off, summary, stream=None) -> None:
+        """gevws_encode_batch_async: FrameToBytes for n records (OUT_FRAME_DTYPE rows as a
+        uint8 [n, 32] device tensor) into `out` (>= out_cap + OUT_PAD bytes)."""
+        st = lib.gevws_encode_batch_async(self._ctx, _stream_handle(stream), frames_dev.data_ptr() if n else None,
+                                          n, payload.data_ptr(), out.data_ptr(), out_cap,
+                                          out_off.data_ptr(), summary.data_ptr())
+        if st != OK:
+            raise RuntimeError(f"gevws_encode_batch_async: {status_string(st)}")
+
+    def encode(self, frames: np.ndarray, payload, out_cap: Optional[int] = None):
+        """Encode host records (OUT_FRAME_DTYPE) whose payloads live in the device
+        tensor `payload`; returns (wire device tensor [total], out_off numpy)."""
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        n = int(frames.shape[0])
+        if out_cap is None:
+            out_cap = int(frames["payload_len"].sum()) + 14 * n
+        fr = torch.from_numpy(np.ascontiguousarray(frames).view(np.uint8).reshape(-1, 32).copy()).to(dev) \
+            if n else torch.zeros((1, 32), dtype=torch.uint8, device=dev)
+        out = torch.empty(out_cap + _abi.OUT_PAD, dtype=torch.uint8, device=dev)
+        off = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        summ = torch.zeros(64, dtype=torch.uint8, device=dev)
+        self.encode_async(fr, n, payload, out, out_cap, off, summ)
+        torch.cuda.synchronize(self.device)
+        s = summ.cpu().numpy().view(SUMMARY_DTYPE)[0]
+        if int(s["status"]) != OK:
+            raise RuntimeError(f"encode: {status_string(int(s['status']))}")
+        return out[: int(s["payload_bytes"])], off[:n].cpu().numpy().astype(np.uint64)
 
     def cipher_(self, buf, mask: bytes, offset: int = 0, nbytes: Optional[int] = None,
                 byte_offset: int = 0, stream=None) -> None:
@@ -343,5 +375,5 @@ def handler_protocol(protocol: Protocol, c: Connection, buffer: RingBuffer,
 
 __all__ = ["Engine", "Batch", "RingBuffer", "Connection", "Protocol", "Header", "handler_protocol",
            "status_string", "device_count", "lib", "FRAME_DTYPE", "CONN_OUT_DTYPE", "SUMMARY_DTYPE",
-           "SYNTH_DTYPE", "OK", "NEED_MORE", "ERR_LEN_MSB", "ERR_CAPACITY", "ERR_INVALID", "ERR_DEVICE",
+           "SYNTH_DTYPE", "OUT_FRAME_DTYPE", "OK", "NEED_MORE", "ERR_LEN_MSB", "ERR_CAPACITY", "ERR_INVALID", "ERR_DEVICE",
            "ERR_NOT_UPGRADED", "IN_PAD", "PAYLOAD_ALIGN", "TILE"]

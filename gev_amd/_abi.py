@@ -20,6 +20,7 @@ ERR_INVALID = -3
 ERR_DEVICE = -4
 ERR_NOT_UPGRADED = -5
 
+OUT_PAD = 16
 TUNE_UNMASK_VARIANT = 1
 TUNE_UNMASK_GRID = 2
 
@@ -96,6 +97,7 @@ SIGNATURES = {
                                                 ctypes.c_uint64, P, ctypes.c_uint64, P, P]),
     "gevws_decode_batch": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,
                                           ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.POINTER(Summary)]),
+    "gevws_encode_batch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, P, ctypes.c_uint64, P, P]),
     "gevws_cipher_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint64]),
     "gevws_synth_async": (ctypes.c_int, [P, P, P, P, ctypes.c_uint64, ctypes.c_uint64]),
     "gevws_synth_verify_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_uint64, P, P,

@@ -583,6 +583,217 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
   }
 }
 
+// ------------------------------------------------------------------ outbound encode (§8f row 1)
+// ws.WriteHeader (write.go:48-84) + ws.FrameToBytes (frame.go:274-278) for a
+// batch of frames: wire[f] = WriteHeader(hdr_f) || payload_f, frames back to
+// back (as handlerProtocol appends Packet output to its tmpBuffer,
+// connection.go:213).  Go's byte arithmetic is kept: Rsv << 4 truncated to a
+// byte, OpCode OR-ed as a whole byte, byte(Length) for any Length <= 125.
+
+__device__ __forceinline__ uint32_t enc_header(const gevws_header& h, uint64_t& lo, uint64_t& hi) {
+  const uint32_t b0 = ((h.fin ? 0x80u : 0u) | ((uint32_t)h.rsv << 4) | h.opcode) & 0xffu;
+  const int64_t L = h.length;
+  uint32_t b1, n;
+  lo = 0;
+  hi = 0;
+  if (L <= 125) {
+    b1 = (uint32_t)L & 0xffu;
+    n = 2;
+  } else if (L <= 0xFFFF) {
+    b1 = 126;
+    lo = ((uint64_t)((L >> 8) & 0xff) << 16) | ((uint64_t)(L & 0xff) << 24);
+    n = 4;
+  } else {
+    b1 = 127;
+    const uint64_t be = __builtin_bswap64((uint64_t)L);  // bytes 2..9, big-endian
+    lo = be << 16;
+    hi = be >> 48;
+    n = 10;
+  }
+  if (h.masked) {
+    b1 |= 0x80;
+    uint32_t k;
+    memcpy(&k, h.mask, 4);
+    if (n == 2) lo |= (uint64_t)k << 16;
+    else if (n == 4) lo |= (uint64_t)k << 32;
+    else hi |= (uint64_t)k << 16;
+    n += 4;
+  }
+  lo |= (uint64_t)b0 | ((uint64_t)b1 << 8);
+  return n;
+}
+
+__device__ __forceinline__ uint32_t enc_hlen(const gevws_header& h) {
+  const int64_t L = h.length;
+  return (L <= 125 ? 2u : (L <= 0xFFFF ? 4u : 10u)) + (h.masked ? 4u : 0u);
+}
+
+__global__ __launch_bounds__(kWalkBlock) void k_enc_size(const gevws_out_frame* __restrict__ fr, uint64_t n,
+                                                         uint64_t* __restrict__ blk) {
+  const uint64_t f = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
+  uint64_t one = 0, wire = 0, pl = 0;
+  if (f < n) {
+    const gevws_out_frame o = fr[f];
+    one = 1;
+    pl = o.payload_len;
+    wire = enc_hlen(o.hdr) + o.payload_len;
+  }
+  __shared__ uint64_t s_part[3][kWalkBlock / 64];
+  const uint64_t vals[3] = {one, wire, pl};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint64_t sm = wave_sum(vals[k]);
+    if (lane == 0) s_part[k][w] = sm;
+  }
+  __syncthreads();
+  if (threadIdx.x < kBlkFields) {
+    uint64_t sm = 0;
+    if (threadIdx.x < 3)
+      for (int j = 0; j < kWalkBlock / 64; ++j) sm += s_part[threadIdx.x][j];
+    blk[(uint64_t)blockIdx.x * kBlkFields + threadIdx.x] = sm;
+  }
+}
+
+__global__ __launch_bounds__(kWalkBlock) void k_enc_emit(const gevws_out_frame* __restrict__ fr, uint64_t n,
+                                                         const uint64_t* __restrict__ blk,
+                                                         const gevws_summary* __restrict__ sum,
+                                                         uint64_t* __restrict__ out_off,
+                                                         uint32_t* __restrict__ tile_first) {
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t f = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
+  uint64_t v[1] = {0};
+  if (f < n) v[0] = enc_hlen(fr[f].hdr) + fr[f].payload_len;
+  uint64_t ex[1], tot[1];
+  block_excl_scan<kWalkBlock, 1>(v, ex, tot);
+  if (f >= n) return;
+  const uint64_t o = blk[(uint64_t)blockIdx.x * kBlkFields + 1] + ex[0];
+  out_off[f] = o;
+  for (uint64_t t = (o + kTile - 1) / kTile; t * kTile < o + v[0]; ++t) tile_first[t] = (uint32_t)f;
+}
+
+// One output byte at absolute position `a` of frame f (global-memory form, used
+// by the fallback path).
+__device__ __forceinline__ uint8_t enc_byte_global(const gevws_out_frame* __restrict__ fr,
+                                                   const uint64_t* __restrict__ out_off,
+                                                   const uint8_t* __restrict__ payload, uint64_t f, uint64_t a) {
+  const gevws_out_frame o = fr[f];
+  uint64_t lo, hi;
+  const uint32_t hl = enc_header(o.hdr, lo, hi);
+  const uint64_t r = a - out_off[f];
+  if (r < hl) return (uint8_t)(r < 8 ? (lo >> (8 * r)) : (hi >> (8 * (r - 8))));
+  return payload[o.payload_off + (r - hl)];
+}
+
+constexpr int kEncWinFrames = 1024;
+
+__global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* __restrict__ fr,
+                                                         const uint8_t* __restrict__ payload,
+                                                         const uint64_t* __restrict__ out_off,
+                                                         const uint32_t* __restrict__ tile_first,
+                                                         const gevws_summary* __restrict__ sum,
+                                                         uint8_t* __restrict__ out) {
+  __shared__ int32_t s_start[kEncWinFrames];  // wire start relative to the window, clamped >= -64
+  __shared__ int32_t s_pend[kEncWinFrames];   // payload end relative to the window, clamped
+  __shared__ uint32_t s_hlen[kEncWinFrames];
+  __shared__ uint64_t s_delta[kEncWinFrames];  // payload_off - out_off - hlen (mod 2^64)
+  __shared__ uint64_t s_h0[kEncWinFrames];
+  __shared__ uint64_t s_h1[kEncWinFrames];
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t total = sum->payload_bytes;  // wire bytes
+  const uint64_t nframes = sum->frames;
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  uint64_t t = (uint64_t)blockIdx.x * per;
+  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+  const uint32_t lane_off = threadIdx.x * 16;
+  while (t < tend) {
+    const uint64_t wt = (tend - t) < (uint64_t)kWinTiles ? (tend - t) : (uint64_t)kWinTiles;
+    const uint64_t wbase = t * kTile;
+    const uint64_t f_lo = tile_first[t];
+    const uint64_t f_hi = (t + wt) < ntiles ? (uint64_t)tile_first[t + wt] : nframes - 1;
+    const uint64_t F = f_hi - f_lo + 1;
+    if (F <= (uint64_t)kEncWinFrames) {
+      __syncthreads();
+      for (uint64_t i = threadIdx.x; i < F; i += kUnmaskBlock) {
+        const gevws_out_frame o = fr[f_lo + i];
+        uint64_t lo, hi;
+        const uint32_t hl = enc_header(o.hdr, lo, hi);
+        const uint64_t oo = out_off[f_lo + i];
+        const int64_t st = (int64_t)(oo - wbase);
+        s_start[i] = st < -64 ? -64 : (int32_t)st;
+        const int64_t pe = st + hl + (int64_t)o.payload_len;
+        s_pend[i] = pe > 0x7fffffffll ? 0x7fffffff : (int32_t)pe;
+        s_hlen[i] = hl;
+        s_delta[i] = o.payload_off - oo - hl;
+        s_h0[i] = lo;
+        s_h1[i] = hi;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kWinTiles; ++u) {
+        const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
+        const uint64_t a = wbase + (uint64_t)rel;
+        if ((uint64_t)u >= wt || a >= total) continue;
+        uint32_t lo = 0, hi = (uint32_t)F - 1;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+        }
+        u32x4 x;
+        if (rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo]) {
+          x = ld16u(payload + (a + s_delta[lo]));  // interior of one payload
+        } else {
+          uint32_t w[4] = {0, 0, 0, 0};
+          uint32_t j = lo;
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const int32_t pos = rel + k;
+            while (j + 1 < (uint32_t)F && s_start[j + 1] <= pos) ++j;
+            uint8_t byte = 0;
+            if (a + k < total) {
+              const int32_t r = pos - s_start[j];
+              if (r < (int32_t)s_hlen[j])
+                byte = (uint8_t)(r < 8 ? (s_h0[j] >> (8 * r)) : (s_h1[j] >> (8 * (r - 8))));
+              else
+                byte = payload[a + k + s_delta[j]];
+            }
+            w[k >> 2] |= (uint32_t)byte << (8 * (k & 3));
+          }
+          x = u32x4{w[0], w[1], w[2], w[3]};
+        }
+        *reinterpret_cast<u32x4*>(out + a) = x;
+      }
+      t += wt;
+      continue;
+    }
+    // more than kEncWinFrames frames in the window (tiny frames): one tile,
+    // per-lane global lookup and byte assembly
+    {
+      const uint64_t a = t * kTile + lane_off;
+      if (a < total) {
+        uint64_t lo = tile_first[t];
+        uint64_t hi = (t + 1 < ntiles) ? (uint64_t)tile_first[t + 1] : nframes - 1;
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi + 1) >> 1;
+          if (out_off[mid] <= a) lo = mid; else hi = mid - 1;
+        }
+        uint32_t w[4] = {0, 0, 0, 0};
+        uint64_t j = lo;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          while (j + 1 < nframes && out_off[j + 1] <= a + k) ++j;
+          const uint32_t byte = (a + k < total) ? enc_byte_global(fr, out_off, payload, j, a + k) : 0u;
+          w[k >> 2] |= byte << (8 * (k & 3));
+        }
+        const u32x4 x = u32x4{w[0], w[1], w[2], w[3]};
+        *reinterpret_cast<u32x4*>(out + a) = x;
+      }
+      t += 1;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
 // p[i] ^= mask[(offset + i) & 3] for i in [0, n): 16-byte aligned chunks of the
 // address space; interior chunks use one rotated 32-bit key, edge chunks go
@@ -963,6 +1174,33 @@ int gevws_decode_batch(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64
     r = h_summary->status;
   }
   return r;
+}
+
+int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_frames, uint64_t n,
+                             const uint8_t* d_payload, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                             gevws_summary* d_summary) {
+  if (!ctx || !d_summary || (n && (!d_frames || !d_out || !d_out_off))) return GEVWS_ERR_INVALID;
+  if (n > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  const uint64_t nblk64 = (n + kWalkBlock - 1) / kWalkBlock;
+  if (nblk64 > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
+  const uint32_t nblk = (uint32_t)nblk64;
+  const uint64_t ntiles_cap = (out_cap + kTile - 1) / kTile + 1;
+  const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
+  int r = ensure_scratch(ctx, blk_bytes + ntiles_cap * sizeof(uint32_t));
+  if (r != GEVWS_OK) return r;
+  uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
+  uint32_t* tile_first = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes);
+  if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk);
+  k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
+  if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_summary, d_out_off, tile_first);
+  uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
+  if (grid > 1024) grid = 1024;
+  if (grid < 1) grid = 1;
+  k_encode<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out);
+  GEVWS_HIP(hipGetLastError());
+  return GEVWS_OK;
 }
 
 int gevws_cipher_async(gevws_ctx* ctx, void* stream, uint8_t* d_p, uint64_t n, const uint8_t mask[4],

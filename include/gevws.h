@@ -153,6 +153,30 @@ int gevws_decode_batch(gevws_ctx *ctx, void *stream, const uint8_t *d_in, uint64
                        uint64_t max_frames, uint8_t *d_payload, uint64_t payload_cap,
                        gevws_conn_out *d_conn_out, gevws_summary *h_summary);
 
+/* ---------------------------------------------------------------- outbound encode
+ * One reply frame: the header to serialise and where its payload bytes are
+ * (e.g. a decoded frame's slot in a payload arena). */
+typedef struct gevws_out_frame {
+    gevws_header hdr;
+    uint64_t payload_off;
+    uint64_t payload_len;
+} gevws_out_frame;
+
+/* Extra writable bytes the caller must provide past out_cap (the encoder
+ * stores whole 16-byte vectors; bytes past the wire total are zeroed). */
+#define GEVWS_OUT_PAD 16
+
+/* ws.FrameToBytes (frame.go:274-278) = ws.WriteHeader (write.go:48-84) +
+ * payload, for n frames at once, written back to back into d_out (the bytes
+ * handlerProtocol appends to its send buffer, connection.go:208-218).
+ * d_out_off[f] receives frame f's wire offset; d_summary->payload_bytes the
+ * wire total, ->payload_len the payload total, ->status GEVWS_ERR_CAPACITY if
+ * the total exceeds out_cap (nothing written).  Device pointers; enqueued on
+ * `stream`. */
+int gevws_encode_batch_async(gevws_ctx *ctx, void *stream, const gevws_out_frame *d_frames, uint64_t n,
+                             const uint8_t *d_payload, uint8_t *d_out, uint64_t out_cap,
+                             uint64_t *d_out_off, gevws_summary *d_summary);
+
 /* ws.Cipher(payload, mask, offset), plugins/websocket/ws/cipher.go:14-53, on a
  * device buffer in place: p[i] ^= mask[(offset+i) % 4]. */
 int gevws_cipher_async(gevws_ctx *ctx, void *stream, uint8_t *d_p, uint64_t n,

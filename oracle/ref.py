@@ -18,6 +18,9 @@ FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked
                         ("mask", "u1", (4,)), ("length", "<i8"),
                         ("payload_off", "<u8"), ("src_off", "<u8")])
 assert FRAME_DTYPE.itemsize == 32
+OUT_FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked", "u1"),
+                            ("mask", "u1", (4,)), ("length", "<i8"),
+                            ("payload_off", "<u8"), ("payload_len", "<u8")])
 
 
 def build() -> str:
@@ -40,6 +43,10 @@ def lib():
         L.wsref_decode_batch.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint64, P,
                                          ctypes.c_uint64, P, P, P, P, P]
         L.wsref_decode_batch.restype = ctypes.c_int64
+        L.wsref_write_header.argtypes = [P, P]
+        L.wsref_write_header.restype = ctypes.c_uint32
+        L.wsref_encode_batch.argtypes = [P, ctypes.c_uint64, P, P, ctypes.c_uint64, P]
+        L.wsref_encode_batch.restype = ctypes.c_int64
         L.wsref_bench_pipeline.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_int, ctypes.c_double,
                                            P, P, P]
         L.wsref_bench_pipeline.restype = ctypes.c_double
@@ -101,3 +108,27 @@ def bench_pipeline(arena: np.ndarray, conn_off: np.ndarray, conn_len: np.ndarray
     secs = lib().wsref_bench_pipeline(_ptr(arena), _ptr(conn_off), _ptr(conn_len), conn_off.size,
                                       threads, min_seconds, _ptr(pb), _ptr(nf), _ptr(ck))
     return secs, int(pb[0]), int(nf[0])
+
+
+def write_header(hdr16: bytes) -> bytes:
+    """ws.WriteHeader on a packed 16-byte ws.Header image."""
+    h = np.frombuffer(hdr16, np.uint8).copy()
+    out = np.zeros(14, np.uint8)
+    n = lib().wsref_write_header(_ptr(h), _ptr(out))
+    return out[:n].tobytes()
+
+
+def encode_batch(frames: np.ndarray, payload: np.ndarray):
+    """FrameToBytes for every record of `frames` (OUT_FRAME_DTYPE), back to back.
+    Returns (wire bytes as uint8 array, out_off)."""
+    frames = np.ascontiguousarray(frames)
+    cap = int(frames["payload_len"].sum()) + 14 * frames.shape[0] + 16
+    out = np.zeros(cap, np.uint8)
+    off = np.zeros(max(frames.shape[0], 1), np.uint64)
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    if payload.size == 0:
+        payload = np.zeros(1, np.uint8)
+    tot = lib().wsref_encode_batch(_ptr(frames), frames.shape[0], _ptr(payload), _ptr(out), cap, _ptr(off))
+    if tot < 0:
+        raise RuntimeError("wsref_encode_batch failed")
+    return out[:tot], off[:frames.shape[0]]

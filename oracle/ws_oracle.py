@@ -235,6 +235,47 @@ def decode_stream(buf) -> StreamResult:
     return res
 
 
+# --------------------------------------------------------------------------- outbound encode (§8f row 1)
+def write_header_go(h: Header) -> bytes:
+    """ws.WriteHeader, write.go:48-84, byte for byte -- including Go's byte
+    arithmetic: ``bts[0] |= h.Rsv << 4`` keeps the low 8 bits, ``OpCode`` is
+    OR-ed as a whole byte, and any Length <= 125 (negative ones too) is written
+    as ``byte(h.Length)``.  The MASK bit and key follow the length
+    (write.go:78-81); the payload is NOT masked by FrameToBytes."""
+    bts = bytearray(14)
+    if h.fin:
+        bts[0] |= 0x80
+    bts[0] |= (h.rsv << 4) & 0xFF
+    bts[0] |= h.opcode & 0xFF
+    L = h.length
+    if L <= 125:
+        bts[1] = L & 0xFF
+        n = 2
+    elif L <= 0xFFFF:
+        bts[1] = 126
+        bts[2:4] = L.to_bytes(2, "big")
+        n = 4
+    else:
+        bts[1] = 127
+        bts[2:10] = L.to_bytes(8, "big")
+        n = 10
+    if h.masked:
+        bts[1] |= 0x80
+        bts[n:n + 4] = h.mask
+        n += 4
+    return bytes(bts[:n])
+
+
+def frame_to_bytes(h: Header, payload: bytes) -> bytes:
+    """ws.FrameToBytes, frame.go:274-278: WriteHeader(&f.Header) + payload."""
+    return write_header_go(h) + bytes(payload)
+
+
+def new_frame(op: int, fin: bool, p: bytes) -> Tuple[Header, bytes]:
+    """ws.NewFrame, frame.go:193-203 (NewBinaryFrame/NewTextFrame/NewPongFrame...)."""
+    return Header(fin=fin, rsv=0, opcode=op, masked=False, mask=b"\x00" * 4, length=len(p)), p
+
+
 # --------------------------------------------------------------------------- encoder (fixtures)
 def write_header(fin: bool, rsv: int, opcode: int, length: int, masked: bool,
                  mask: bytes = b"\x00\x00\x00\x00", len_form: Optional[int] = None) -> bytes:

@@ -231,3 +231,55 @@ double wsref_bench_pipeline(const uint8_t *in, const uint64_t *conn_off, const u
     free(th);
     return wall;
 }
+
+/* ------------------------------------------------------------------ outbound encode
+ * ws.WriteHeader (write.go:48-84) with Go's byte arithmetic, and a batch of
+ * ws.FrameToBytes (frame.go:274-278) written back to back. */
+typedef struct {
+    wsref_header hdr;
+    uint64_t payload_off;
+    uint64_t payload_len;
+} wsref_out_frame;
+
+uint32_t wsref_write_header(const wsref_header *h, uint8_t out[14]) {
+    memset(out, 0, 14);
+    if (h->fin) out[0] |= 0x80;
+    out[0] |= (uint8_t)(h->rsv << 4);
+    out[0] |= h->opcode;
+    uint32_t n;
+    if (h->length <= 125) {
+        out[1] = (uint8_t)h->length;
+        n = 2;
+    } else if (h->length <= 0xFFFF) {
+        out[1] = 126;
+        out[2] = (uint8_t)(h->length >> 8);
+        out[3] = (uint8_t)h->length;
+        n = 4;
+    } else {
+        out[1] = 127;
+        for (int i = 0; i < 8; i++) out[2 + i] = (uint8_t)((uint64_t)h->length >> (56 - 8 * i));
+        n = 10;
+    }
+    if (h->masked) {
+        out[1] |= 0x80;
+        memcpy(out + n, h->mask, 4);
+        n += 4;
+    }
+    return n;
+}
+
+/* Returns the wire total, or WSREF_ERR_CAPACITY. */
+int64_t wsref_encode_batch(const wsref_out_frame *f, uint64_t n, const uint8_t *payload, uint8_t *out,
+                           uint64_t out_cap, uint64_t *out_off) {
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint8_t h[14];
+        uint32_t hl = wsref_write_header(&f[i].hdr, h);
+        if (o + hl + f[i].payload_len > out_cap) return WSREF_ERR_CAPACITY;
+        out_off[i] = o;
+        memcpy(out + o, h, hl);
+        memcpy(out + o + hl, payload + f[i].payload_off, f[i].payload_len);
+        o += hl + f[i].payload_len;
+    }
+    return (int64_t)o;
+}

@@ -101,6 +101,29 @@ def case_multi_conn(rng, n_conns=37):
     return conns
 
 
+def encode_case(rng, n=400):
+    """ws.FrameToBytes inputs: server replies (NewBinaryFrame/NewTextFrame/
+    pong/close) plus hand-built headers exercising Go's byte arithmetic in
+    WriteHeader (Rsv > 7, OpCode > 15, negative and boundary lengths, Masked
+    without payload masking)."""
+    hdrs, pays = [], []
+    for i in range(n):
+        L = int(rng.choice([0, 1, 2, 5, 125, 126, 127, 1000, 3072]))
+        L = min(L, int(rng.integers(0, 3000))) if rng.random() < 0.5 else L
+        if i in (7, 100, 333):
+            L = (65535, 65536, 70000)[(7, 100, 333).index(i)]
+        p = bytes(rng.integers(0, 256, L, dtype=np.uint8)) if L < 4096 else bytes(np.arange(L) % 251)
+        if rng.random() < 0.7:
+            h, p = wo.new_frame(int(rng.choice([1, 2, 8, 9, 10])), True, p)
+        else:
+            h = wo.Header(bool(rng.random() < .5), int(rng.integers(0, 256)), int(rng.integers(0, 256)),
+                          bool(rng.random() < .5), bytes(rng.integers(0, 256, 4, dtype=np.uint8)),
+                          int(rng.choice([len(p), -1, -300, 125, 126, 65535, 65536, (1 << 63) - 1])))
+        hdrs.append(h)
+        pays.append(p)
+    return hdrs, pays
+
+
 CASES = {
     "rfc_kats": case_rfc_kats,
     "header_classes": case_header_classes,
@@ -135,6 +158,13 @@ def build():
         arrays[f"{name}/payload_len"] = np.array([len(p) for p in payloads], np.int64)
         arrays[f"{name}/payload"] = np.frombuffer(b"".join(payloads), np.uint8)
         arrays[f"{name}/conn_res"] = np.array(conn_res, np.int64).reshape(-1, 3)
+    hdrs, pays = encode_case(rng)
+    arrays["encode/hdr"] = np.array([np.frombuffer(h.pack(), np.uint8) for h in hdrs], np.uint8)
+    arrays["encode/payload_len"] = np.array([len(p) for p in pays], np.int64)
+    arrays["encode/payload"] = np.frombuffer(b"".join(pays), np.uint8)
+    wires = [wo.frame_to_bytes(h, p) for h, p in zip(hdrs, pays)]
+    arrays["encode/wire"] = np.frombuffer(b"".join(wires), np.uint8)
+    arrays["encode/out_off"] = np.concatenate([[0], np.cumsum([len(x) for x in wires])[:-1]]).astype(np.int64)
     np.savez_compressed(OUT, **arrays)
     return OUT
 

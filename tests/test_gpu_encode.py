@@ -1,0 +1,130 @@
+"""GPU parity for the outbound encode: the device
+ws.WriteHeader (write.go:48-84) + ws.FrameToBytes (frame.go:274-278), through
+the C ABI (gevws_encode_batch_async), bit-exact against the golden vectors and
+the C oracle, plus the echo round trip decode -> NewBinaryFrame reply ->
+encode -> decode (benchmarks/websocket/server.go:22-29)."""
+import numpy as np
+import pytest
+
+import gev_amd
+from oracle import ref
+from oracle import ws_oracle as wo
+from tests._helpers import gpu_decode, host_result, pack_streams, random_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(engine):
+    import torch
+    return torch.device("cuda", engine.device)
+
+
+def _records(hdrs16: np.ndarray, offs, lens) -> np.ndarray:
+    fr = np.zeros(hdrs16.shape[0], gev_amd.OUT_FRAME_DTYPE)
+    fr.view(np.uint8).reshape(-1, 32)[:, :16] = hdrs16
+    fr["payload_off"] = offs
+    fr["payload_len"] = lens
+    return fr
+
+
+def _encode_check(engine, fr: np.ndarray, payload: np.ndarray, tag=""):
+    import torch
+    d_pay = torch.from_numpy(np.concatenate([payload, np.zeros(16, np.uint8)])).to(_dev(engine))
+    wire, off = engine.encode(fr, d_pay)
+    want, woff = ref.encode_batch(fr, payload)
+    got = wire.cpu().numpy()
+    assert got.size == want.size, tag
+    assert np.array_equal(got, want), (tag, int(np.argmax(got != want)))
+    assert np.array_equal(off, woff), tag
+    return got
+
+
+def test_encode_golden(engine, golden):
+    g = golden["encode"]
+    offs = np.concatenate([[0], np.cumsum(g["payload_len"])[:-1]]).astype(np.uint64)
+    fr = _records(g["hdr"], offs, g["payload_len"])
+    got = _encode_check(engine, fr, g["payload"], "golden")
+    assert np.array_equal(got, g["wire"])
+
+
+def test_encode_random_and_tiny_frames(engine):
+    rng = np.random.default_rng(41)
+    for trial, (n, maxlen) in enumerate([(1, 0), (5, 10), (300, 3000), (3000, 0), (5000, 20), (200, 70000)]):
+        lens = rng.integers(0, maxlen + 1, n)
+        payload = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+        perm = rng.permutation(n)           # payloads need not be in frame order
+        hd = []
+        for i in range(n):
+            h = wo.Header(bool(rng.random() < .7), int(rng.integers(0, 256)) if rng.random() < .1 else 0,
+                          int(rng.integers(0, 16)), bool(rng.random() < .3),
+                          bytes(rng.integers(0, 256, 4, dtype=np.uint8)),
+                          int(lens[perm[i]]) if rng.random() < .9 else int(rng.integers(-5, 70000)))
+            hd.append(np.frombuffer(h.pack(), np.uint8))
+        fr = _records(np.array(hd), offs[perm], lens[perm])
+        _encode_check(engine, fr, payload, f"trial {trial}")
+
+
+def test_encode_empty_batch(engine):
+    import torch
+    fr = np.zeros(0, gev_amd.OUT_FRAME_DTYPE)
+    wire, off = engine.encode(fr, torch.zeros(16, dtype=torch.uint8, device=_dev(engine)))
+    assert wire.numel() == 0 and off.size == 0
+
+
+def test_echo_round_trip_on_device(engine):
+    """Client frames (masked) -> device decode -> server replies
+    NewBinaryFrame(payload) whose payloads are the decoded arena slots -> device
+    encode -> device decode of the reply stream: the same payload bytes."""
+    import torch
+    rng = np.random.default_rng(42)
+    streams = [random_stream(rng, int(rng.integers(0, 30)), max_len=5000) for _ in range(40)]
+    arena, conns = pack_streams(streams)
+    out = gpu_decode(engine, arena, conns)
+    got = host_result(out)
+    f = got["frames"]
+    n = f.shape[0]
+    replies = np.zeros(n, gev_amd.OUT_FRAME_DTYPE)
+    replies["fin"] = 1
+    replies["opcode"] = wo.OP_BINARY
+    replies["length"] = f["length"]
+    replies["payload_off"] = f["payload_off"]
+    replies["payload_len"] = f["length"]
+    wire, off = engine.encode(replies, out.payload)
+    w = wire.cpu().numpy()
+    # the oracle builds the same reply bytes from the oracle's own decode
+    want = b"".join(wo.frame_to_bytes(*wo.new_frame(wo.OP_BINARY, True,
+                                                   got["payload"][int(o):int(o) + int(L)].tobytes()))
+                    for o, L in zip(f["payload_off"], f["length"]))
+    assert w.tobytes() == want
+    back = host_result(gpu_decode(engine, np.concatenate([w, np.zeros(6, np.uint8)]),
+                                  np.array([[0, w.size + 6]])))
+    assert int(back["summary"]["frames"]) == n
+    assert np.array_equal(back["payload"], got["payload"])  # same 16-byte-aligned arena layout
+
+
+def test_echo_round_trip_c2_full_size(engine):
+    """Full C2 batch (262 144 x 4 KiB): decode, encode the binary replies,
+    decode the reply stream, compare the payload arenas on the device."""
+    import torch
+    from gev_amd import workloads
+    lay = workloads.config_c2()
+    dev = _dev(engine)
+    arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    arena[lay.arena_bytes:] = 0
+    engine.synth(arena, torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev), lay.n_frames, lay.seed)
+    conns = torch.from_numpy(lay.conns.copy()).to(dev)
+    out = engine.decode(arena, lay.arena_bytes, conns, lay.n_conns, lay.n_frames, lay.payload_padded)
+    f = out.frames[: lay.n_frames].cpu().numpy().reshape(-1).view(gev_amd.FRAME_DTYPE)
+    replies = np.zeros(lay.n_frames, gev_amd.OUT_FRAME_DTYPE)
+    replies["fin"], replies["opcode"] = 1, wo.OP_BINARY
+    replies["length"] = f["length"]
+    replies["payload_off"], replies["payload_len"] = f["payload_off"], f["length"]
+    wire, _ = engine.encode(replies, out.payload)
+    assert wire.numel() == lay.n_frames * (4 + 4096)
+    w2 = torch.zeros(wire.numel() + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    w2[: wire.numel()] = wire
+    c2 = torch.tensor([[0, wire.numel()]], dtype=torch.int64, device=dev)
+    back = engine.decode(w2, wire.numel(), c2, 1, lay.n_frames, lay.payload_padded)
+    assert int(back.summary_host()["frames"]) == lay.n_frames
+    assert torch.equal(back.payload[: lay.payload_padded], out.payload[: lay.payload_padded])

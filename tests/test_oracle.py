@@ -150,8 +150,12 @@ def test_header_pack_is_go_layout():
 
 
 # --------------------------------------------------------------------------- golden vectors
+def _decode_cases(golden):
+    return {k: v for k, v in golden.items() if k != "encode"}
+
+
 def test_python_oracle_reproduces_golden(golden):
-    for name, g in golden.items():
+    for name, g in _decode_cases(golden).items():
         arena = g["in"].tobytes()
         k = 0
         poff = 0
@@ -169,7 +173,7 @@ def test_python_oracle_reproduces_golden(golden):
 
 
 def test_c_oracle_reproduces_golden(golden):
-    for name, g in golden.items():
+    for name, g in _decode_cases(golden).items():
         r = ref.decode_batch(g["in"].copy(), g["conns"][:, 0], g["conns"][:, 1])
         assert np.array_equal(r["conn_nframes"], g["conn_res"][:, 0]), name
         assert np.array_equal(r["conn_consumed"], g["conn_res"][:, 1]), name
@@ -230,3 +234,61 @@ def test_python_and_c_oracle_agree_random():
             o = int(f["payload_off"])
             assert r["payload"][o:o + fr.header.length].tobytes() == fr.payload
             k += 1
+
+
+# --------------------------------------------------------------------------- outbound encode
+def _h(**kw):
+    return wo.Header(**kw)
+
+
+def test_write_header_rfc_kats():
+    assert wo.write_header_go(_h(fin=True, opcode=1, length=5)) == bytes.fromhex("8105")
+    assert wo.write_header_go(_h(fin=True, opcode=2, length=256)) == bytes.fromhex("827e0100")
+    assert wo.write_header_go(_h(fin=True, opcode=2, length=65536)) == bytes.fromhex("827f0000000000010000")
+    assert wo.write_header_go(_h(fin=True, opcode=1, masked=True, mask=bytes.fromhex("37fa213d"),
+                                 length=5)) == bytes.fromhex("818537fa213d")
+    h, p = wo.new_frame(wo.OP_TEXT, True, b"Hello")
+    assert wo.frame_to_bytes(h, p) == bytes.fromhex("810548656c6c6f")  # RFC 6455 §5.7
+
+
+def test_write_header_go_byte_arithmetic():
+    assert wo.write_header_go(_h(rsv=8, opcode=1, length=0))[0] == 0x81          # Rsv<<4 overflows into FIN
+    assert wo.write_header_go(_h(rsv=0x13, opcode=0x1F, length=0))[0] == 0x3F    # (0x130 & 0xff) | 0x1f
+    assert wo.write_header_go(_h(length=-1)) == bytes([0x00, 0xFF])              # byte(-1), 2-byte form
+    assert wo.write_header_go(_h(length=-1, masked=True, mask=b"abcd")) == bytes([0x00, 0xFF]) + b"abcd"
+    assert wo.write_header_go(_h(length=(1 << 63) - 1))[1:] == bytes([127, 0x7F] + [0xFF] * 7)
+
+
+def test_write_header_python_equals_c():
+    rng = np.random.default_rng(31)
+    for _ in range(3000):
+        h = wo.Header(bool(rng.random() < .5), int(rng.integers(0, 256)), int(rng.integers(0, 256)),
+                      bool(rng.random() < .5), bytes(rng.integers(0, 256, 4, dtype=np.uint8)),
+                      int(rng.choice([int(rng.integers(-(1 << 40), 1 << 40)), int(rng.integers(0, 200)),
+                                      int(rng.integers(60000, 70000)), (1 << 63) - 1, -(1 << 63)])))
+        assert ref.write_header(h.pack()) == wo.write_header_go(h)
+
+
+def test_encode_golden_c_and_python(golden):
+    g = golden["encode"]
+    offs = np.concatenate([[0], np.cumsum(g["payload_len"])[:-1]])
+    fr = np.zeros(g["hdr"].shape[0], ref.OUT_FRAME_DTYPE)
+    fr.view(np.uint8).reshape(-1, 32)[:, :16] = g["hdr"]
+    fr["payload_off"] = offs
+    fr["payload_len"] = g["payload_len"]
+    wire, off = ref.encode_batch(fr, g["payload"])
+    assert np.array_equal(wire, g["wire"]) and np.array_equal(off.astype(np.int64), g["out_off"])
+    py = b"".join(wo.frame_to_bytes(wo.Header.unpack(h.tobytes()), g["payload"][o:o + L].tobytes())
+                  for h, o, L in zip(g["hdr"], offs, g["payload_len"]))
+    assert py == g["wire"].tobytes()
+
+
+def test_encode_decode_round_trip():
+    """decode(FrameToBytes(NewBinaryFrame(p))) == p -- the echo server's reply
+    (benchmarks/websocket/server.go:22-29) read back by a client."""
+    rng = np.random.default_rng(32)
+    for L in (0, 1, 125, 126, 65535, 65536, 70001):
+        p = bytes(rng.integers(0, 256, L, dtype=np.uint8))
+        h, _ = wo.new_frame(wo.OP_BINARY, True, p)
+        res = wo.decode_stream(wo.frame_to_bytes(h, p) + b"\x00" * 6)
+        assert res.frames[0].payload == p and res.frames[0].header.opcode == wo.OP_BINARY
