@@ -686,7 +686,56 @@ __device__ __forceinline__ uint8_t enc_byte_global(const gevws_out_frame* __rest
 }
 
 constexpr int kEncWinFrames = 1024;
+typedef unsigned __int128 u128;
 
+__device__ __forceinline__ u128 u128_of(u32x4 v) {
+  return (u128)v[0] | ((u128)v[1] << 32) | ((u128)v[2] << 64) | ((u128)v[3] << 96);
+}
+__device__ __forceinline__ u32x4 u32x4_of(u128 x) {
+  return u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+}
+// bytes [k0, k1) of a 16-byte lane (0 <= k0 < k1 <= 16)
+__device__ __forceinline__ u128 byte_mask(int k0, int k1) {
+  const u128 hi = (k1 >= 16) ? ~(u128)0 : (((u128)1 << (8 * k1)) - 1);
+  const u128 lo = ((u128)1 << (8 * k0)) - 1;
+  return hi & ~lo;
+}
+
+// Assemble the 16 output bytes at window-relative position `rel` (absolute `a`)
+// from the frames overlapping it (at most 8: every frame is >= 2 wire bytes):
+// header bytes from the frame's serialised header, payload bytes from ONE
+// unaligned 16-byte load per frame (all loads independent).
+__device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
+                                              const int32_t* s_start, const int32_t* s_pend, const uint32_t* s_hlen,
+                                              const uint64_t* s_delta, const uint64_t* s_h0, const uint64_t* s_h1,
+                                              const uint8_t* __restrict__ payload) {
+  u128 acc = 0;
+  const int kmax = (a + 16 <= total) ? 16 : (int)(total - a);
+  for (uint32_t j = lo; j < F && s_start[j] < rel + kmax; ++j) {
+    const int32_t hs = s_start[j];
+    const int32_t ps = hs + (int32_t)s_hlen[j];
+    const int32_t pe = s_pend[j];
+    // header bytes [max(hs, rel), min(ps, rel + kmax))
+    const int32_t h0 = hs > rel ? hs : rel;
+    const int32_t h1 = ps < rel + kmax ? ps : rel + kmax;
+    if (h0 < h1) {
+      const u128 H = (u128)s_h0[j] | ((u128)s_h1[j] << 64);
+      const u128 part = (H >> (8 * (h0 - hs))) << (8 * (h0 - rel));
+      acc |= part & byte_mask(h0 - rel, h1 - rel);
+    }
+    // payload bytes [max(ps, rel), min(pe, rel + kmax))
+    const int32_t p0 = ps > rel ? ps : rel;
+    const int32_t p1 = pe < rel + kmax ? pe : rel + kmax;
+    if (p0 < p1) {
+      const int k0 = p0 - rel;
+      const u128 v = u128_of(ld16u(payload + (a + (uint64_t)k0 + s_delta[j])));
+      acc |= (v << (8 * k0)) & byte_mask(k0, p1 - rel);
+    }
+  }
+  return u32x4_of(acc);
+}
+
+template <int U>
 __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
@@ -707,9 +756,27 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
   uint64_t t = (uint64_t)blockIdx.x * per;
   const uint64_t tend = t + per < ntiles ? t + per : ntiles;
   const uint32_t lane_off = threadIdx.x * 16;
+  uint64_t c_ps = 0, c_pe = 0, c_delta = 0;  // cached frame: payload [c_ps, c_pe) in wire coordinates
   while (t < tend) {
+    const uint64_t base = t * kTile;
+    if (base >= c_pe) {  // workgroup-uniform refresh (scalar loads)
+      const uint64_t f = tile_first[t];
+      const gevws_out_frame o = fr[f];
+      c_ps = out_off[f] + enc_hlen(o.hdr);
+      c_pe = c_ps + o.payload_len;
+      c_delta = o.payload_off - c_ps;
+    }
+    if (t + U <= tend && base >= c_ps && base + U * kTile <= c_pe) {  // inside one payload: stream
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld16u(payload + (base + u * kTile + lane_off + c_delta));
+#pragma unroll
+      for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(out + base + u * kTile + lane_off));
+      t += U;
+      continue;
+    }
     const uint64_t wt = (tend - t) < (uint64_t)kWinTiles ? (tend - t) : (uint64_t)kWinTiles;
-    const uint64_t wbase = t * kTile;
+    const uint64_t wbase = base;
     const uint64_t f_lo = tile_first[t];
     const uint64_t f_hi = (t + wt) < ntiles ? (uint64_t)tile_first[t + wt] : nframes - 1;
     const uint64_t F = f_hi - f_lo + 1;
@@ -741,34 +808,17 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
           if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
         }
         u32x4 x;
-        if (rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo]) {
+        if (rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo])
           x = ld16u(payload + (a + s_delta[lo]));  // interior of one payload
-        } else {
-          uint32_t w[4] = {0, 0, 0, 0};
-          uint32_t j = lo;
-#pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            const int32_t pos = rel + k;
-            while (j + 1 < (uint32_t)F && s_start[j + 1] <= pos) ++j;
-            uint8_t byte = 0;
-            if (a + k < total) {
-              const int32_t r = pos - s_start[j];
-              if (r < (int32_t)s_hlen[j])
-                byte = (uint8_t)(r < 8 ? (s_h0[j] >> (8 * r)) : (s_h1[j] >> (8 * (r - 8))));
-              else
-                byte = payload[a + k + s_delta[j]];
-            }
-            w[k >> 2] |= (uint32_t)byte << (8 * (k & 3));
-          }
-          x = u32x4{w[0], w[1], w[2], w[3]};
-        }
-        *reinterpret_cast<u32x4*>(out + a) = x;
+        else
+          x = enc_assemble(rel, a, total, lo, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0, s_h1, payload);
+        __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + a));
       }
       t += wt;
       continue;
     }
-    // more than kEncWinFrames frames in the window (tiny frames): one tile,
-    // per-lane global lookup and byte assembly
+    // more than kEncWinFrames frames in the window (frames of a few bytes):
+    // one tile, per-lane global lookup and byte assembly
     {
       const uint64_t a = t * kTile + lane_off;
       if (a < total) {
@@ -786,8 +836,7 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
           const uint32_t byte = (a + k < total) ? enc_byte_global(fr, out_off, payload, j, a + k) : 0u;
           w[k >> 2] |= byte << (8 * (k & 3));
         }
-        const u32x4 x = u32x4{w[0], w[1], w[2], w[3]};
-        *reinterpret_cast<u32x4*>(out + a) = x;
+        *reinterpret_cast<u32x4*>(out + a) = u32x4{w[0], w[1], w[2], w[3]};
       }
       t += 1;
     }
@@ -1198,7 +1247,7 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
   if (grid > 1024) grid = 1024;
   if (grid < 1) grid = 1;
-  k_encode<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out);
+  k_encode<4><<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out);
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;
 }

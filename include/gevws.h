@@ -171,7 +171,9 @@ typedef struct gevws_out_frame {
  * handlerProtocol appends to its send buffer, connection.go:208-218).
  * d_out_off[f] receives frame f's wire offset; d_summary->payload_bytes the
  * wire total, ->payload_len the payload total, ->status GEVWS_ERR_CAPACITY if
- * the total exceeds out_cap (nothing written).  Device pointers; enqueued on
+ * the total exceeds out_cap (nothing written).  Payload bytes are read as
+ * 16-byte vectors: d_payload needs 16 readable bytes past its last payload
+ * byte (a decode's payload arena has them).  Device pointers; enqueued on
  * `stream`. */
 int gevws_encode_batch_async(gevws_ctx *ctx, void *stream, const gevws_out_frame *d_frames, uint64_t n,
                              const uint8_t *d_payload, uint8_t *d_out, uint64_t out_cap,

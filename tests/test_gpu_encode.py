@@ -97,8 +97,10 @@ def test_echo_round_trip_on_device(engine):
                                                    got["payload"][int(o):int(o) + int(L)].tobytes()))
                     for o, L in zip(f["payload_off"], f["length"]))
     assert w.tobytes() == want
-    back = host_result(gpu_decode(engine, np.concatenate([w, np.zeros(6, np.uint8)]),
-                                  np.array([[0, w.size + 6]])))
+    # trail with 5 bytes of an incomplete 127-form header: avail >= 6 for every
+    # real frame (read.go:20-23) without adding a decodable frame
+    tail = np.array([0x82, 0x7F, 0, 0, 0], np.uint8)
+    back = host_result(gpu_decode(engine, np.concatenate([w, tail]), np.array([[0, w.size + 5]])))
     assert int(back["summary"]["frames"]) == n
     assert np.array_equal(back["payload"], got["payload"])  # same 16-byte-aligned arena layout
 
@@ -123,7 +125,7 @@ def test_echo_round_trip_c2_full_size(engine):
     wire, _ = engine.encode(replies, out.payload)
     assert wire.numel() == lay.n_frames * (4 + 4096)
     w2 = torch.zeros(wire.numel() + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
-    w2[: wire.numel()] = wire
+    w2[: wire.numel()] = wire   # 4 KiB frames: every frame already has >= 6 bytes behind it
     c2 = torch.tensor([[0, wire.numel()]], dtype=torch.int64, device=dev)
     back = engine.decode(w2, wire.numel(), c2, 1, lay.n_frames, lay.payload_padded)
     assert int(back.summary_host()["frames"]) == lay.n_frames
