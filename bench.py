@@ -118,11 +118,12 @@ def main():
     world, rank, local = dist.env()
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist.init("nccl", dev)  # RCCL over xGMI when WORLD_SIZE > 1
+    gpu = local % max(torch.cuda.device_count(), 1)  # == local on a node with one rank per GPU
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    dist.init(dist.backend(), dev)  # RCCL over xGMI when WORLD_SIZE > 1
 
-    eng = gev_amd.Engine(local)
+    eng = gev_amd.Engine(gpu)
     t_setup = time.time()
     lay = build_layout(args.config, rank, args.conns)
     log(f"rank {rank}: {lay.name}: {lay.n_frames} frames, {lay.n_conns} connections, "

@@ -133,11 +133,14 @@ class Engine:
         return tuple(ms), calls.value
 
     # -------------------------------------------------------------- decode
-    def alloc_batch(self, n_conns: int, max_frames: int, payload_cap: int) -> Batch:
+    def alloc_batch(self, n_conns: int, max_frames: int, payload_cap: int, aux_slots: int = 0) -> Batch:
+        """Output buffers; aux_slots reserves room after the payload arena for
+        close-reply bodies (Engine.serve)."""
         torch = _torch()
         dev = torch.device("cuda", self.device)
+        extra = (aux_slots * _abi.AUX_SLOT + 128) if aux_slots else 0
         return Batch(frames=torch.empty((max(max_frames, 1), 32), dtype=torch.uint8, device=dev),
-                     payload=torch.empty(payload_cap + 16, dtype=torch.uint8, device=dev),
+                     payload=torch.empty(payload_cap + 16 + extra, dtype=torch.uint8, device=dev),
                      conn_out=torch.empty((max(n_conns, 1), 32), dtype=torch.uint8, device=dev),
                      summary=torch.zeros(64, dtype=torch.uint8, device=dev), n_conns=n_conns)
 
@@ -153,15 +156,16 @@ class Engine:
             raise RuntimeError(f"gevws_decode_batch_async: {status_string(st)}")
 
     def decode(self, arena, in_bytes: int, conns, n_conns: int, max_frames: Optional[int] = None,
-               payload_cap: Optional[int] = None, stream=None) -> Batch:
-        """Decode a device-resident batch; grows capacities once on ERR_CAPACITY."""
+               payload_cap: Optional[int] = None, stream=None, aux_slots: int = 0) -> Batch:
+        """Decode a device-resident batch; grows capacities once on ERR_CAPACITY.
+        aux_slots reserves close-reply space for a following Engine.serve."""
         torch = _torch()
         if max_frames is None:
             max_frames = min(in_bytes // 2 + 1, 0xFFFFFFFF)
         if payload_cap is None:
             payload_cap = in_bytes + 16 * min(max_frames, in_bytes // 64 + 64) + 64
         for attempt in range(2):
-            out = self.alloc_batch(n_conns, max_frames, payload_cap)
+            out = self.alloc_batch(n_conns, max_frames, payload_cap, aux_slots)
             self.decode_async(arena, in_bytes, conns, n_conns, out, max_frames, payload_cap, stream)
             torch.cuda.synchronize(self.device)
             s = out.summary_host()
@@ -202,6 +206,39 @@ class Engine:
         if int(s["status"]) != OK:
             raise RuntimeError(f"encode: {status_string(int(s['status']))}")
         return out[: int(s["payload_bytes"])], off[:n].cpu().numpy().astype(np.uint64)
+
+    def dispatch_async(self, frames_dev, n: int, policy: int, payload, aux_off: int, aux_cap: int, replies,
+                       reply_of, summary, stream=None) -> None:
+        """gevws_dispatch_async: HandlerWrap.OnMessage replies for n decoded frames."""
+        st = lib.gevws_dispatch_async(self._ctx, _stream_handle(stream), frames_dev.data_ptr() if n else None, n,
+                                      policy, payload.data_ptr(), aux_off, aux_cap,
+                                      replies.data_ptr(), reply_of.data_ptr(), summary.data_ptr())
+        if st != OK:
+            raise RuntimeError(f"gevws_dispatch_async: {status_string(st)}")
+
+    def serve(self, out: "Batch", policy: int, aux_slots: Optional[int] = None):
+        """One server step after a decode: dispatch (wrap.go:38-90) + encode of
+        the replies.  `out.payload` must have room for the close-reply bodies
+        after the decoded payloads (see alloc_batch(aux_slots=...)).  Returns
+        (wire device tensor, reply_of numpy, summary of the dispatch)."""
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        s = out.summary_host()
+        n = int(s["frames"])
+        aux_off = (int(s["payload_bytes"]) + 127) // 128 * 128
+        aux_cap = out.payload.numel() - 16 - aux_off
+        replies = torch.empty((max(n, 1), 32), dtype=torch.uint8, device=dev)
+        reply_of = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        dsum = torch.zeros(64, dtype=torch.uint8, device=dev)
+        self.dispatch_async(out.frames, n, policy, out.payload, aux_off, max(aux_cap, 0), replies, reply_of, dsum)
+        torch.cuda.synchronize(self.device)
+        ds = dsum.cpu().numpy().view(SUMMARY_DTYPE)[0]
+        if int(ds["status"]) != OK:
+            raise RuntimeError(f"dispatch: {status_string(int(ds['status']))}")
+        nr = int(ds["frames"])
+        rep_host = replies[:nr].cpu().numpy().reshape(-1).view(OUT_FRAME_DTYPE)
+        wire, _ = self.encode(rep_host, out.payload, int(rep_host["payload_len"].sum()) + 14 * nr)
+        return wire, reply_of[:n].cpu().numpy(), ds
 
     def cipher_(self, buf, mask: bytes, offset: int = 0, nbytes: Optional[int] = None,
                 byte_offset: int = 0, stream=None) -> None:

@@ -21,6 +21,10 @@ ERR_DEVICE = -4
 ERR_NOT_UPGRADED = -5
 
 OUT_PAD = 16
+AUX_SLOT = 128
+HANDLER_NONE = 0
+HANDLER_ECHO_BINARY = 1
+HANDLER_ECHO_TEXT = 2
 TUNE_UNMASK_VARIANT = 1
 TUNE_UNMASK_GRID = 2
 
@@ -98,6 +102,8 @@ SIGNATURES = {
     "gevws_decode_batch": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,
                                           ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.POINTER(Summary)]),
     "gevws_encode_batch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, P, ctypes.c_uint64, P, P]),
+    "gevws_dispatch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_int, P, ctypes.c_uint64,
+                                            ctypes.c_uint64, P, P, P]),
     "gevws_cipher_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint64]),
     "gevws_synth_async": (ctypes.c_int, [P, P, P, P, ctypes.c_uint64, ctypes.c_uint64]),
     "gevws_synth_verify_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_uint64, P, P,

@@ -843,6 +843,172 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
   }
 }
 
+// ------------------------------------------------------------------ control-frame dispatch (§8f row 2)
+// HandlerWrap.OnMessage (plugins/websocket/wrap.go:38-90) for decoded frames:
+// close -> util.HandleClose (util.go:27-46) + ShutdownWrite; ping -> pong with
+// the same payload (util.go:49-51); pong -> ping (util.go:54-56, kept as the
+// reference has it); other control opcodes -> nothing; data frames -> the echo
+// policy standing in for the user's WSHandler (empty replies send nothing,
+// wrap.go:72).  Replies are gevws_out_frame records for gevws_encode_batch.
+
+constexpr uint32_t kAuxSlot = 128;  // one close body (<= 125 bytes) per slot
+
+__device__ __constant__ char kErrNotInUse[] = "status code is not in use";
+__device__ __constant__ char kErrAppLevel[] = "status code is only application level";
+__device__ __constant__ char kErrNoMeaning[] = "status code has no meaning yet";
+__device__ __constant__ char kErrUnknown[] = "status code is not defined in spec";
+__device__ __constant__ char kErrUtf8[] = "invalid utf8 sequence in close reason";
+
+// unicode/utf8.ValidString: strict UTF-8.
+__device__ bool utf8_valid(const uint8_t* p, uint64_t n) {
+  uint64_t i = 0;
+  while (i < n) {
+    const uint32_t c = p[i];
+    if (c < 0x80) { ++i; continue; }
+    uint32_t need, lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) need = 1;
+    else if (c == 0xE0) { need = 2; lo = 0xA0; }
+    else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) need = 2;
+    else if (c == 0xED) { need = 2; hi = 0x9F; }
+    else if (c == 0xF0) { need = 3; lo = 0x90; }
+    else if (c >= 0xF1 && c <= 0xF3) need = 3;
+    else if (c == 0xF4) { need = 3; hi = 0x8F; }
+    else return false;
+    if (i + need >= n) return false;  // truncated sequence
+    const uint32_t c1 = p[i + 1];
+    if (c1 < lo || c1 > hi) return false;
+    for (uint32_t k = 2; k <= need; ++k)
+      if ((p[i + k] & 0xC0) != 0x80) return false;
+    i += need + 1;
+  }
+  return true;
+}
+
+// 0: no reply, 1: reply with the frame's own payload, 2: close reply (aux body), 3: bare close header
+__device__ __forceinline__ int disp_kind(const gevws_header& h, int policy, uint32_t& op_out) {
+  const uint32_t op = h.opcode;
+  if (op & 8) {
+    if (op == 0x8) return h.length == 0 ? 3 : 2;
+    if (op == 0x9) { op_out = 0xA; return 1; }
+    if (op == 0xA) { op_out = 0x9; return 1; }
+    return 0;
+  }
+  if (policy == GEVWS_HANDLER_NONE || h.length <= 0) return 0;
+  op_out = policy == GEVWS_HANDLER_ECHO_BINARY ? 0x2u : 0x1u;
+  return 1;
+}
+
+__global__ __launch_bounds__(kWalkBlock) void k_disp_count(const gevws_frame* __restrict__ fr, uint64_t n, int policy,
+                                                           uint64_t* __restrict__ blk) {
+  const uint64_t f = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
+  uint64_t rep = 0, aux = 0, shut = 0;
+  if (f < n) {
+    uint32_t op;
+    const int k = disp_kind(fr[f].hdr, policy, op);
+    rep = k != 0;
+    aux = k == 2;
+    shut = k >= 2;
+  }
+  __shared__ uint64_t s_part[3][kWalkBlock / 64];
+  const uint64_t vals[3] = {rep, aux, shut};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint64_t sm = wave_sum(vals[k]);
+    if (lane == 0) s_part[k][w] = sm;
+  }
+  __syncthreads();
+  if (threadIdx.x < kBlkFields) {
+    uint64_t sm = 0;
+    const int fld = threadIdx.x == 3 ? 2 : (threadIdx.x == 2 ? -1 : threadIdx.x);
+    if (fld >= 0)
+      for (int j = 0; j < kWalkBlock / 64; ++j) sm += s_part[fld][j];
+    blk[(uint64_t)blockIdx.x * kBlkFields + threadIdx.x] = sm;  // [replies, aux slots, 0, shutdowns]
+  }
+}
+
+__device__ void put_close_body(uint8_t* dst, uint32_t code, const uint8_t* reason, uint64_t rlen, uint32_t& n) {
+  // ws.NewCloseFrameBody (frame.go:251-259): BE16 code + reason cropped to 123 bytes
+  const uint64_t crop = rlen < 123 ? rlen : 123;
+  dst[0] = (uint8_t)(code >> 8);
+  dst[1] = (uint8_t)code;
+  for (uint64_t i = 0; i < crop; ++i) dst[2 + i] = reason[i];
+  n = (uint32_t)(2 + crop);
+}
+
+__device__ void put_close_error(uint8_t* dst, const char* msg, uint32_t& n) {
+  uint64_t len = 0;
+  while (msg[len]) ++len;
+  put_close_body(dst, 1002, reinterpret_cast<const uint8_t*>(msg), len, n);  // StatusProtocolError
+}
+
+__global__ __launch_bounds__(kWalkBlock) void k_disp_emit(const gevws_frame* __restrict__ fr, uint64_t n, int policy,
+                                                          const uint8_t* __restrict__ payload, uint64_t aux_off,
+                                                          const uint64_t* __restrict__ blk,
+                                                          const gevws_summary* __restrict__ sum,
+                                                          gevws_out_frame* __restrict__ rep,
+                                                          int64_t* __restrict__ reply_of,
+                                                          uint8_t* __restrict__ aux_base) {
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t f = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
+  uint32_t op = 0;
+  int kind = 0;
+  gevws_frame in;
+  if (f < n) {
+    in = fr[f];
+    kind = disp_kind(in.hdr, policy, op);
+  }
+  uint64_t v[2] = {(uint64_t)(kind != 0), (uint64_t)(kind == 2)};
+  uint64_t ex[2], tot[2];
+  block_excl_scan<kWalkBlock, 2>(v, ex, tot);
+  if (f >= n) return;
+  if (kind == 0) {
+    reply_of[f] = -1;
+    return;
+  }
+  const uint64_t r = blk[(uint64_t)blockIdx.x * kBlkFields + 0] + ex[0];
+  reply_of[f] = (int64_t)r;
+  gevws_out_frame o;
+  memset(&o, 0, sizeof(o));
+  o.hdr.fin = 1;
+  if (kind == 1) {
+    o.hdr.opcode = (uint8_t)op;
+    o.hdr.length = in.hdr.length;
+    o.payload_off = in.payload_off;
+    o.payload_len = (uint64_t)in.hdr.length;
+  } else if (kind == 3) {
+    o.hdr.opcode = 0x8;  // WriteHeader(&Header{Fin: true, OpCode: OpClose}), util.go:28-33
+  } else {
+    const uint64_t slot = blk[(uint64_t)blockIdx.x * kBlkFields + 1] + ex[1];
+    uint8_t* body = aux_base + slot * kAuxSlot;
+    const uint8_t* p = payload + in.payload_off;
+    const uint64_t L = (uint64_t)in.hdr.length;
+    uint32_t code = 0;
+    const uint8_t* reason = p;
+    uint64_t rlen = 0;
+    if (L >= 2) {  // ParseCloseFrameData, read.go:89-102
+      code = ((uint32_t)p[0] << 8) | p[1];
+      reason = p + 2;
+      rlen = L - 2;
+    }
+    uint32_t nb;
+    const bool defined = code == 1000 || code == 1001 || code == 1002 || code == 1003 || code == 1007 ||
+                         code == 1008 || code == 1009 || code == 1010 || code == 1011 || code == 1005 ||
+                         code == 1006 || code == 1015;
+    if (code <= 999) put_close_error(body, kErrNotInUse, nb);
+    else if (code == 1005 || code == 1006 || code == 1015) put_close_error(body, kErrAppLevel, nb);
+    else if (code == 1004) put_close_error(body, kErrNoMeaning, nb);
+    else if (code >= 1000 && code <= 2999 && !defined) put_close_error(body, kErrUnknown, nb);
+    else if (!utf8_valid(reason, rlen)) put_close_error(body, kErrUtf8, nb);
+    else put_close_body(body, code, reason, rlen, nb);
+    o.hdr.opcode = 0x8;
+    o.hdr.length = nb;
+    o.payload_off = aux_off + slot * kAuxSlot;
+    o.payload_len = nb;
+  }
+  rep[r] = o;
+}
+
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
 // p[i] ^= mask[(offset + i) & 3] for i in [0, n): 16-byte aligned chunks of the
 // address space; interior chunks use one rotated 32-bit key, edge chunks go
@@ -1248,6 +1414,29 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   if (grid > 1024) grid = 1024;
   if (grid < 1) grid = 1;
   k_encode<4><<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out);
+  GEVWS_HIP(hipGetLastError());
+  return GEVWS_OK;
+}
+
+int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t n, int policy,
+                         uint8_t* d_payload, uint64_t aux_off, uint64_t aux_cap, gevws_out_frame* d_replies,
+                         int64_t* d_reply_of, gevws_summary* d_summary) {
+  if (!ctx || !d_summary || (n && (!d_frames || !d_payload || !d_replies || !d_reply_of))) return GEVWS_ERR_INVALID;
+  if (policy < GEVWS_HANDLER_NONE || policy > GEVWS_HANDLER_ECHO_TEXT) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  const uint64_t nblk64 = (n + kWalkBlock - 1) / kWalkBlock;
+  if (nblk64 > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
+  const uint32_t nblk = (uint32_t)nblk64;
+  const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
+  int r = ensure_scratch(ctx, blk_bytes);
+  if (r != GEVWS_OK) return r;
+  uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
+  if (nblk) k_disp_count<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, blk);
+  k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, n, aux_cap / kAuxSlot, d_summary);
+  if (nblk)
+    k_disp_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, d_payload, aux_off, blk, d_summary, d_replies,
+                                              d_reply_of, d_payload + aux_off);
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;
 }

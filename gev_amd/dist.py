@@ -31,11 +31,27 @@ def init(backend: str, device=None) -> bool:
     return True
 
 
+def backend() -> str:
+    """RCCL ("nccl") on GPUs; GEV_DIST_BACKEND=gloo rehearses the multi-rank
+    path with several ranks on one GPU (RCCL allows one rank per device)."""
+    return os.environ.get("GEV_DIST_BACKEND", "nccl")
+
+
+def _gloo_host(t):
+    import torch.distributed as dist
+    return dist.get_backend() == "gloo" and t.is_cuda
+
+
 def reduce_counts(counts) -> None:
     """In-place sum over ranks of the int64 [frames, payload_bytes, errors] tensor."""
     import torch.distributed as dist
     if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(counts)
+        if _gloo_host(counts):
+            c = counts.cpu()
+            dist.all_reduce(c)
+            counts.copy_(c)
+        else:
+            dist.all_reduce(counts)
 
 
 def max_over_ranks(value: float, device) -> float:
@@ -43,6 +59,8 @@ def max_over_ranks(value: float, device) -> float:
     import torch.distributed as dist
     t = torch.tensor([value], dtype=torch.float64, device=device)
     if dist.is_initialized() and dist.get_world_size() > 1:
+        if _gloo_host(t):
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

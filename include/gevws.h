@@ -179,6 +179,33 @@ int gevws_encode_batch_async(gevws_ctx *ctx, void *stream, const gevws_out_frame
                              const uint8_t *d_payload, uint8_t *d_out, uint64_t out_cap,
                              uint64_t *d_out_off, gevws_summary *d_summary);
 
+/* ---------------------------------------------------------------- control-frame dispatch
+ * HandlerWrap.OnMessage (plugins/websocket/wrap.go:38-90) over decoded frames:
+ * close -> util.HandleClose reply (util.go:27-46; close-code checks and UTF-8
+ * validation of the reason as CheckCloseFrameData, util.go:65-85) and a
+ * ShutdownWrite; ping -> pong with the same payload; pong -> ping with the
+ * same payload (util.go:54-56, as the reference does); other control opcodes ->
+ * nothing; data frames -> `policy` standing in for the user's WSHandler. */
+enum {
+    GEVWS_HANDLER_NONE = 0,        /* user handler replies nothing */
+    GEVWS_HANDLER_ECHO_BINARY = 1, /* benchmarks/websocket/server.go:22-29 */
+    GEVWS_HANDLER_ECHO_TEXT = 2    /* example/websocket OnMessage shape */
+};
+/* Bytes of aux space per close reply body (bodies are <= 125 bytes). */
+#define GEVWS_AUX_SLOT 128
+
+/* d_frames/n: a decode's records; d_payload: its payload arena, whose region
+ * [aux_off, aux_off + aux_cap) receives the close-reply bodies (one
+ * GEVWS_AUX_SLOT each).  Writes the replies in stream order to d_replies
+ * (capacity n; payload_off relative to d_payload, ready for
+ * gevws_encode_batch_async with the same d_payload) and d_reply_of[f] = reply
+ * index or -1.  d_summary: frames = replies, payload_bytes = aux slots used,
+ * errors = close frames (ShutdownWrite calls), status GEVWS_ERR_CAPACITY if
+ * the aux region is too small. */
+int gevws_dispatch_async(gevws_ctx *ctx, void *stream, const gevws_frame *d_frames, uint64_t n, int policy,
+                         uint8_t *d_payload, uint64_t aux_off, uint64_t aux_cap,
+                         gevws_out_frame *d_replies, int64_t *d_reply_of, gevws_summary *d_summary);
+
 /* ws.Cipher(payload, mask, offset), plugins/websocket/ws/cipher.go:14-53, on a
  * device buffer in place: p[i] ^= mask[(offset+i) % 4]. */
 int gevws_cipher_async(gevws_ctx *ctx, void *stream, uint8_t *d_p, uint64_t n,

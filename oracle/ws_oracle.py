@@ -276,6 +276,97 @@ def new_frame(op: int, fin: bool, p: bytes) -> Tuple[Header, bytes]:
     return Header(fin=fin, rsv=0, opcode=op, masked=False, mask=b"\x00" * 4, length=len(p)), p
 
 
+# --------------------------------------------------------------------------- control-frame dispatch (§8f row 2)
+MAX_CONTROL_PAYLOAD = 125                      # frame.go:9-10
+STATUS_PROTOCOL_ERROR = 1002                   # frame.go:80-83
+_PROTOCOL_DEFINED = {1000, 1001, 1002, 1003, 1007, 1008, 1009, 1010, 1011, 1005, 1006, 1015}  # frame.go:130-147
+_PROTOCOL_RESERVED = {1005, 1006, 1015}        # frame.go:151-160
+ERR_NOT_IN_USE = b"status code is not in use"              # errors.go:17-21
+ERR_APP_LEVEL = b"status code is only application level"
+ERR_NO_MEANING = b"status code has no meaning yet"
+ERR_UNKNOWN = b"status code is not defined in spec"
+ERR_INVALID_UTF8 = b"invalid utf8 sequence in close reason"
+
+HANDLER_NONE = 0          # the user's WSHandler returns nothing
+HANDLER_ECHO_BINARY = 1   # benchmarks/websocket/server.go:22-29 (MessageBinary, data)
+HANDLER_ECHO_TEXT = 2     # example/websocket OnMessage shape (MessageText, data)
+
+
+def utf8_valid(b: bytes) -> bool:
+    """unicode/utf8.ValidString: strict UTF-8 (no surrogates, no overlongs, <= U+10FFFF)."""
+    try:
+        b.decode("utf-8", errors="strict")
+        return True
+    except UnicodeDecodeError:
+        return False
+
+
+def parse_close_frame_data(payload: bytes) -> Tuple[int, bytes]:
+    """ws.ParseCloseFrameData, read.go:89-102."""
+    if len(payload) < 2:
+        return 0, b""
+    return int.from_bytes(payload[:2], "big"), payload[2:]
+
+
+def check_close_frame_data(code: int, reason: bytes) -> Optional[bytes]:
+    """util.CheckCloseFrameData, util/util.go:65-85 (switch order kept)."""
+    if 0 <= code <= 999:
+        return ERR_NOT_IN_USE
+    if code in _PROTOCOL_RESERVED:
+        return ERR_APP_LEVEL
+    if code == 1004:
+        return ERR_NO_MEANING
+    if 1000 <= code <= 2999 and code not in _PROTOCOL_DEFINED:
+        return ERR_UNKNOWN
+    if not utf8_valid(reason):
+        return ERR_INVALID_UTF8
+    return None
+
+
+def new_close_frame_body(code: int, reason: bytes) -> bytes:
+    """ws.NewCloseFrameBody, frame.go:251-259: min(2+len, 125) bytes, reason
+    cropped to 123."""
+    n = min(2 + len(reason), MAX_CONTROL_PAYLOAD)
+    crop = min(MAX_CONTROL_PAYLOAD - 2, len(reason))
+    return (code.to_bytes(2, "big") + reason[:crop])[:n]
+
+
+def handle_close(h: Header, payload: bytes) -> bytes:
+    """util.HandleClose, util/util.go:27-46."""
+    if h.length == 0:
+        return write_header_go(Header(fin=True, opcode=OP_CLOSE))
+    code, reason = parse_close_frame_data(payload)
+    err = check_close_frame_data(code, reason)
+    if err is not None:
+        body = new_close_frame_body(STATUS_PROTOCOL_ERROR, err)
+    else:
+        body = new_close_frame_body(code, reason)
+    return frame_to_bytes(*new_frame(OP_CLOSE, True, body))
+
+
+def on_message(h: Header, payload: bytes, policy: int) -> Tuple[Optional[bytes], bool]:
+    """HandlerWrap.OnMessage, plugins/websocket/wrap.go:38-90, for a decoded frame.
+    Returns (reply bytes or None, ShutdownWrite called).  Control frames:
+    close -> HandleClose + ShutdownWrite (wrap.go:51-56); ping -> pong with the
+    same payload (util.go:49-51); pong -> PING with the same payload (util.go:54-56,
+    the reference's quirk); other control opcodes -> no reply.  Data frames go
+    to the user handler (here an echo policy); an empty reply sends nothing
+    (wrap.go:72)."""
+    op = h.opcode
+    if op & 0x8:
+        if op == OP_CLOSE:
+            return handle_close(h, payload), True
+        if op == OP_PING:
+            return frame_to_bytes(*new_frame(OP_PONG, True, payload)), False
+        if op == OP_PONG:
+            return frame_to_bytes(*new_frame(OP_PING, True, payload)), False
+        return None, False
+    if policy == HANDLER_NONE or len(payload) == 0:
+        return None, False
+    op_out = OP_BINARY if policy == HANDLER_ECHO_BINARY else OP_TEXT
+    return frame_to_bytes(*new_frame(op_out, True, payload)), False
+
+
 # --------------------------------------------------------------------------- encoder (fixtures)
 def write_header(fin: bool, rsv: int, opcode: int, length: int, masked: bool,
                  mask: bytes = b"\x00\x00\x00\x00", len_form: Optional[int] = None) -> bytes:

@@ -292,3 +292,38 @@ def test_encode_decode_round_trip():
         h, _ = wo.new_frame(wo.OP_BINARY, True, p)
         res = wo.decode_stream(wo.frame_to_bytes(h, p) + b"\x00" * 6)
         assert res.frames[0].payload == p and res.frames[0].header.opcode == wo.OP_BINARY
+
+
+# --------------------------------------------------------------------------- control-frame dispatch
+def test_dispatch_oracle_reference_behaviour():
+    H = lambda op, L: wo.Header(fin=True, opcode=op, masked=True, mask=b"abcd", length=L)  # noqa: E731
+    # ping -> pong, pong -> PING (util.go:49-56, the reference's quirk)
+    assert wo.on_message(H(9, 2), b"hi", 0) == (bytes([0x8A, 2]) + b"hi", False)
+    assert wo.on_message(H(10, 2), b"hi", 0) == (bytes([0x89, 2]) + b"hi", False)
+    # empty close -> bare close header + ShutdownWrite (util.go:28-33, wrap.go:56)
+    assert wo.on_message(H(8, 0), b"", 0) == (bytes([0x88, 0x00]), True)
+    # valid close echoes code + reason; reason cropped to 123 bytes (frame.go:251-259)
+    r, sd = wo.on_message(H(8, 2 + 200), (1000).to_bytes(2, "big") + b"x" * 200, 0)
+    assert sd and r[:4] == bytes([0x88, 125, 0x03, 0xE8]) and len(r) == 2 + 125
+    # code/UTF-8 checks in util.go:65-85 order
+    for code, msg in [(999, wo.ERR_NOT_IN_USE), (1005, wo.ERR_APP_LEVEL), (1004, wo.ERR_NO_MEANING),
+                      (1012, wo.ERR_UNKNOWN)]:
+        r, _ = wo.on_message(H(8, 3), code.to_bytes(2, "big") + b"a", 0)
+        assert r == bytes([0x88, 2 + len(msg), 0x03, 0xEA]) + msg
+    r, _ = wo.on_message(H(8, 3), (3000).to_bytes(2, "big") + b"\xff", 0)
+    assert r.endswith(wo.ERR_INVALID_UTF8)
+    # 1-byte close payload: ParseCloseFrameData -> code 0 -> not in use
+    assert wo.on_message(H(8, 1), b"\x03", 0)[0].endswith(wo.ERR_NOT_IN_USE)
+    # reserved control opcodes: nothing; data: the policy; empty data: nothing (wrap.go:72)
+    assert wo.on_message(H(0xB, 1), b"r", 1) == (None, False)
+    assert wo.on_message(H(1, 3), b"abc", wo.HANDLER_ECHO_BINARY)[0] == bytes([0x82, 3]) + b"abc"
+    assert wo.on_message(H(0, 3), b"abc", wo.HANDLER_ECHO_TEXT)[0] == bytes([0x81, 3]) + b"abc"
+    assert wo.on_message(H(2, 0), b"", wo.HANDLER_ECHO_BINARY) == (None, False)
+    assert wo.on_message(H(2, 3), b"abc", wo.HANDLER_NONE) == (None, False)
+
+
+def test_utf8_validation_is_strict():
+    ok = ["", "abc", "héllo", "日本", "\U0001F600", "﻿"]
+    bad = [b"\xff", b"\xc0\xaf", b"\xed\xa0\x80", b"\xe2\x82", b"\xf4\x90\x80\x80", b"\xe0\x80\xaf", b"a\x80"]
+    assert all(wo.utf8_valid(x.encode()) for x in ok)
+    assert not any(wo.utf8_valid(b) for b in bad)
