@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Device-resident websocket server step: decode the client frames of a batch
+(UnPacket), dispatch them as HandlerWrap.OnMessage would with an echo handler
+(wrap.go:38-90; control frames answered per util.go), and encode the replies
+(FrameToBytes) -- timed with HIP events, all on one stream, nothing on the host
+in the timed region.
+
+C1-shaped workload (benchmarks/bench-websocket-pingpong.sh sends masked
+128 B text frames; the server echoes binary, benchmarks/websocket/server.go:25):
+--config c1 = 65 536 connections x 16 frames x 128 B.  --config c5 = fragmented
+text + ping/pong.
+
+    python tools/bench_server.py [--config c1|c5|c2|c3] [--reps 10]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c1")
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import bench
+    import gev_amd
+    from gev_amd import workloads as w
+
+    dev = torch.device("cuda", 0)
+    eng = gev_amd.Engine(0)
+    if args.config == "c1":
+        lay = w.uniform(65536, 16, 128, opcode=0x1, name="C1-shaped: 1048576 x 128 B masked text frames")
+    else:
+        lay = bench.build_layout(args.config, 0, None)
+    arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    arena[lay.arena_bytes:] = 0
+    eng.synth(arena, torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev), lay.n_frames, lay.seed)
+    conns = torch.from_numpy(lay.conns.copy()).to(dev)
+    n = lay.n_frames
+    aux_slots = int((lay.desc["b0"] & 0x0F == 0x8).sum())
+    out = eng.alloc_batch(lay.n_conns, n, lay.payload_padded, aux_slots=aux_slots)
+    aux_off = (lay.payload_padded + 127) // 128 * 128
+    aux_cap = out.payload.numel() - 16 - aux_off
+    replies = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    reply_of = torch.empty(n, dtype=torch.int64, device=dev)
+    dsum = torch.zeros(64, dtype=torch.uint8, device=dev)
+    wire_cap = lay.payload_len + 14 * n
+    wire = torch.empty(wire_cap + gev_amd._abi.OUT_PAD, dtype=torch.uint8, device=dev)
+    off = torch.empty(n, dtype=torch.int64, device=dev)
+    esum = torch.zeros(64, dtype=torch.uint8, device=dev)
+
+    def step():
+        eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, n, lay.payload_padded)
+        eng.dispatch_async(out.frames, n, gev_amd._abi.HANDLER_ECHO_BINARY, out.payload, aux_off, aux_cap,
+                           replies, reply_of, dsum)
+        # every frame of these workloads gets a reply (data echo, pong/ping), so
+        # the reply count is n and no host round trip is needed between stages
+        eng.encode_async(replies, n, out.payload, wire, wire_cap, off, esum)
+
+    step()
+    torch.cuda.synchronize()
+    ds = dsum.cpu().numpy().view(gev_amd.SUMMARY_DTYPE)[0]
+    es = esum.cpu().numpy().view(gev_amd.SUMMARY_DTYPE)[0]
+    assert int(ds["frames"]) == n, "every frame is expected to produce one reply in this workload"
+    assert int(es["status"]) == 0
+    # check: decode the reply stream back; payload arenas match
+    wire_total = int(es["payload_bytes"])
+    w2 = torch.zeros(wire_total + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    w2[:wire_total] = wire[:wire_total]
+    # each connection's replies are contiguous in the wire stream (frames are in
+    # connection order): decode them back per connection
+    co = out.conn_out_host()
+    offs = off.cpu().numpy()
+    starts = offs[co["first_frame"].astype(np.int64)]
+    ends = np.append(starts[1:], wire_total)
+    rc = torch.from_numpy(np.stack([starts, ends - starts], 1).astype(np.int64)).to(dev)
+    back = eng.decode(w2, wire_total, rc, lay.n_conns, n, lay.payload_padded)
+    ok = torch.equal(back.payload[: lay.payload_padded], out.payload[: lay.payload_padded])
+    assert ok, "reply stream does not decode back to the request payloads"
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.reps):
+        step()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.reps
+    print(json.dumps({"path": "device server step: decode + dispatch(echo) + encode", "workload": lay.name,
+                      "frames": n, "connections": lay.n_conns, "ms": round(ms, 4),
+                      "frames_per_s": round(n / ms * 1e3, 1),
+                      "payload_GiBps": round(lay.payload_len / (ms / 1e3) / 2**30, 2),
+                      "wire_out_bytes": wire_total, "round_trip_verified": True}))
+
+
+if __name__ == "__main__":
+    main()
