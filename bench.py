@@ -200,7 +200,8 @@ def main():
         "data": "synthetic: masked frames generated on the device (seeded splitmix64 payloads and keys)",
         "config": {"workload": lay.name, "connections_per_gpu": lay.n_conns, "frames_per_gpu": lay.n_frames,
                    "payload_bytes_per_gpu": lay.payload_len, "input_bytes_per_gpu": lay.arena_bytes,
-                   "parallelism": f"connections sharded over {world} GPU(s); RCCL all-reduce of counts"},
+                   "parallelism": (f"connections sharded over {world} GPU(s); "
+                                   f"{'RCCL' if dist.backend() == 'nccl' else dist.backend()} all-reduce of counts")},
         "frames_per_s": round(frames_step * args.steps / elapsed, 1),
         "errors": errors,
         "phases_ms": {"walk_count": round(mean_ms[0], 4), "scan": round(mean_ms[1], 4),
