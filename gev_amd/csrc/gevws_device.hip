@@ -288,6 +288,19 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
 }
 
 // ------------------------------------------------------------------ 4. unmask / compact
+// Streams of big frames run fastest with one workgroup per CU (fewer
+// concurrent streams: better DRAM row locality); small frames need more
+// workgroups to hide the window path's latency (profiles/r01_grid_*.json).  The
+// batch's mean frame size is only known on the device, so kernels are launched
+// with 4 workgroups per CU and, for big frames, all but the first `big_grid`
+// return at once.  big_grid = 0 disables the adaptation (explicit grid).
+constexpr uint64_t kBigFrameBytes = 48 * 1024;
+
+__device__ __forceinline__ uint32_t active_groups(uint64_t total, uint64_t nframes, uint32_t big_grid) {
+  if (big_grid == 0 || gridDim.x <= big_grid || nframes == 0) return gridDim.x;
+  return total / nframes >= kBigFrameBytes ? big_grid : gridDim.x;
+}
+
 // Largest frame index f in [tile_first[t], tile_first[t+1]] with payload_off <= p.
 __device__ __forceinline__ uint64_t find_frame(const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first, uint64_t t,
@@ -317,7 +330,8 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask(const uint8_t* __restri
                                                          const gevws_frame* __restrict__ frames,
                                                          const uint32_t* __restrict__ tile_first,
                                                          const gevws_summary* __restrict__ sum,
-                                                         uint8_t* __restrict__ out) {
+                                                         uint8_t* __restrict__ out, uint32_t big_grid) {
+  (void)big_grid;
   if (sum->status != GEVWS_OK) return;
   const uint64_t total = sum->payload_bytes;
   const uint64_t nframes = sum->frames;
@@ -388,12 +402,14 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v2(const uint8_t* __res
                                                             const gevws_frame* __restrict__ frames,
                                                             const uint32_t* __restrict__ tile_first,
                                                             const gevws_summary* __restrict__ sum,
-                                                            uint8_t* __restrict__ out) {
+                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
   if (sum->status != GEVWS_OK) return;
   const uint64_t total = sum->payload_bytes;
   const uint64_t nframes = sum->frames;
   const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const uint32_t groups = active_groups(total, nframes, big_grid);
+  if (blockIdx.x >= groups) return;
+  const uint64_t per = (ntiles + groups - 1) / groups;
   uint64_t t = (uint64_t)blockIdx.x * per;
   const uint64_t tend = t + per < ntiles ? t + per : ntiles;
   const uint32_t lane_off = threadIdx.x * 16;
@@ -467,7 +483,7 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
                                                             const gevws_frame* __restrict__ frames,
                                                             const uint32_t* __restrict__ tile_first,
                                                             const gevws_summary* __restrict__ sum,
-                                                            uint8_t* __restrict__ out) {
+                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
   __shared__ uint32_t s_start[kWinFrames];   // frame start relative to the window (clamped at 0)
   __shared__ int32_t s_lend[kWinFrames];     // payload end relative to the window (clamped)
   __shared__ uint64_t s_delta[kWinFrames];   // src_off - payload_off (mod 2^64)
@@ -476,7 +492,9 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
   const uint64_t total = sum->payload_bytes;
   const uint64_t nframes = sum->frames;
   const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const uint32_t groups = active_groups(total, nframes, big_grid);
+  if (blockIdx.x >= groups) return;
+  const uint64_t per = (ntiles + groups - 1) / groups;
   uint64_t t = (uint64_t)blockIdx.x * per;
   const uint64_t tend = t + per < ntiles ? t + per : ntiles;
   const uint32_t lane_off = threadIdx.x * 16;
@@ -741,7 +759,7 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
                                                          const uint64_t* __restrict__ out_off,
                                                          const uint32_t* __restrict__ tile_first,
                                                          const gevws_summary* __restrict__ sum,
-                                                         uint8_t* __restrict__ out) {
+                                                         uint8_t* __restrict__ out, uint32_t big_grid) {
   __shared__ int32_t s_start[kEncWinFrames];  // wire start relative to the window, clamped >= -64
   __shared__ int32_t s_pend[kEncWinFrames];   // payload end relative to the window, clamped
   __shared__ uint32_t s_hlen[kEncWinFrames];
@@ -752,7 +770,9 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
   const uint64_t total = sum->payload_bytes;  // wire bytes
   const uint64_t nframes = sum->frames;
   const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const uint32_t groups = active_groups(total, nframes, big_grid);
+  if (blockIdx.x >= groups) return;
+  const uint64_t per = (ntiles + groups - 1) / groups;
   uint64_t t = (uint64_t)blockIdx.x * per;
   const uint64_t tend = t + per < ntiles ? t + per : ntiles;
   const uint32_t lane_off = threadIdx.x * 16;
@@ -1153,6 +1173,7 @@ struct gevws_ctx {
   gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
+  int num_cus = 256;
 };
 
 namespace {
@@ -1199,7 +1220,8 @@ int ensure_scratch(gevws_ctx* ctx, size_t bytes) {
   return GEVWS_OK;
 }
 
-using UnmaskFn = void (*)(const uint8_t*, const gevws_frame*, const uint32_t*, const gevws_summary*, uint8_t*);
+using UnmaskFn = void (*)(const uint8_t*, const gevws_frame*, const uint32_t*, const gevws_summary*, uint8_t*,
+                         uint32_t);
 struct UnmaskVariant {
   UnmaskFn fn;
   int unroll;
@@ -1260,6 +1282,9 @@ gevws_ctx* gevws_ctx_create(int device) {
     delete ctx;
     return nullptr;
   }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    ctx->num_cus = prop.multiProcessorCount;
   if (hipMalloc(reinterpret_cast<void**>(&ctx->d_sum), sizeof(gevws_summary)) != hipSuccess) {
     gevws_ctx_destroy(ctx);
     return nullptr;
@@ -1411,9 +1436,10 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
   if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_summary, d_out_off, tile_first);
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
-  if (grid > 1024) grid = 1024;
+  if (grid > 4 * (uint64_t)ctx->num_cus) grid = 4 * (uint64_t)ctx->num_cus;
   if (grid < 1) grid = 1;
-  k_encode<4><<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out);
+  k_encode<4><<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
+                                                       (uint32_t)ctx->num_cus);
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;
 }
@@ -1491,10 +1517,11 @@ static int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, c
                   uint8_t* d_payload) {
   const UnmaskVariant& v = kUnmaskVariants[ctx->unmask_variant];
   const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
-  uint64_t grid = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : 1024;  // 4 workgroups per CU (A/B: profiles/)
+  uint64_t grid = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : 4 * (uint64_t)ctx->num_cus;
   const uint64_t useful = (ntiles + v.unroll - 1) / v.unroll;
   if (grid > useful) grid = useful;
   if (grid < 1) grid = 1;
-  v.fn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary, d_payload);
+  v.fn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary, d_payload,
+                                                ctx->unmask_grid ? 0u : (uint32_t)ctx->num_cus);
   return GEVWS_OK;
 }
