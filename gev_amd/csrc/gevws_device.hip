@@ -1438,8 +1438,11 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
   if (grid > 4 * (uint64_t)ctx->num_cus) grid = 4 * (uint64_t)ctx->num_cus;
   if (grid < 1) grid = 1;
+  // no big-frame grid reduction here: every frame boundary takes the window
+  // path, which needs 4 workgroups per CU to hide its latency (C3: 22.6 ms at
+  // 4/CU vs 36 ms at 1/CU, profiles/r01_encode_*.json)
   k_encode<4><<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
-                                                       (uint32_t)ctx->num_cus);
+                                                       0u);
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;
 }
