@@ -153,10 +153,45 @@ __device__ __forceinline__ void block_excl_scan(const uint64_t (&v)[NV], uint64_
 }
 
 // ------------------------------------------------------------------ 1. walk (count)
+// Frame entries recorded by the counting walk so the emit pass need not
+// re-fetch every header line from HBM: 16 bytes per frame in a per-connection
+// slot run whose base derives from the stream's arena offset (no scan needed):
+// base_c = off_c / G + 2c, capacity len_c / G + 2, with the granularity G the
+// smallest power of two >= 64 B that keeps the table within kEntryBudget.  Valid
+// (non-overlapping) when each stream ends before the next one starts, which
+// every connection checks against its neighbours; otherwise, or when a
+// connection's frames outnumber its slots (mean frame < G bytes), or
+// its stream is >= 4 GiB, the emit pass re-walks that connection.
+constexpr uint32_t kEntryGranMinShift = 6;        // 64-byte granularity when the table fits
+constexpr uint64_t kEntryBudget = 1ull << 29;     // entries (8 GiB of scratch) at most
+struct WalkEntry {
+  uint32_t pos;   // header offset in the connection stream
+  uint32_t mask;
+  uint32_t len;   // payload length (< 2^32: the stream is)
+  uint32_t meta;  // b0 | masked << 8 | hlen << 16
+};
+static_assert(sizeof(WalkEntry) == 16, "one dwordx4 per entry");
+
+__device__ __forceinline__ bool entry_slots(const gevws_conn_in* __restrict__ conns, uint32_t n, uint32_t c,
+                                           const gevws_conn_in& ci, uint64_t n_entries, uint32_t gshift,
+                                           uint64_t& base, uint64_t& cap) {
+  if (n_entries == 0 || ci.len >= (1ull << 32)) return false;
+  if (c > 0) {
+    const gevws_conn_in p = conns[c - 1];
+    if (p.off + p.len > ci.off) return false;
+  }
+  if (c + 1 < n && ci.off + ci.len > conns[c + 1].off) return false;
+  base = (ci.off >> gshift) + 2ull * c;
+  cap = (ci.len >> gshift) + 2;
+  return base + cap <= n_entries;
+}
+
 __global__ __launch_bounds__(kWalkBlock) void k_walk_count(const uint8_t* __restrict__ in,
                                                            const gevws_conn_in* __restrict__ conns,
                                                            uint32_t n, gevws_conn_out* __restrict__ cout,
-                                                           uint64_t* __restrict__ blk) {
+                                                           uint64_t* __restrict__ blk,
+                                                           WalkEntry* __restrict__ entries, uint64_t n_entries,
+                                                           uint32_t gshift) {
   const uint32_t c = blockIdx.x * kWalkBlock + threadIdx.x;
   uint64_t nf = 0, pb = 0, pl = 0, err = 0;
   if (c < n) {
@@ -164,11 +199,22 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_count(const uint8_t* __rest
     const uint8_t* s = in + ci.off;
     uint64_t pos = 0;
     int32_t st = GEVWS_OK;
+    uint64_t ebase = 0, ecap = 0;
+    bool rec = entry_slots(conns, n, c, ci, n_entries, gshift, ebase, ecap);
+    // software-pipelined: the next header's 16 bytes are requested before this
+    // frame's entry is stored, so waiting for that load (vmcnt counts loads and
+    // stores in issue order) never waits for the store's completion.  Reading
+    // 16 bytes at any pos <= len stays inside the GEVWS_IN_PAD slack.
+    // Every path into the loop head has exactly [header load, entry store]
+    // outstanding (lanes not recording store to their own sink slot past the
+    // table), so the compiler waits vmcnt(1), not vmcnt(0).
+    WalkEntry* sink = entries + n_entries + c;
+    uint64_t lo, hi;
+    load_window(s, lo, hi);
+    *sink = WalkEntry{0, 0, 0, 0};
     for (;;) {
       const uint64_t avail = ci.len - pos;
       if (avail < 6) break;
-      uint64_t lo, hi;
-      load_window(s + pos, lo, hi);
       DevHdr h;
       const int r = parse_header(lo, hi, avail, h);
       if (r != GEVWS_OK) {
@@ -176,13 +222,22 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_count(const uint8_t* __rest
         break;
       }
       if (avail - h.hlen < h.length) break;  // protocol.go:47 gate
+      const uint64_t next = pos + h.hlen + h.length;
+      load_window(s + next, lo, hi);
+      rec = rec && nf < ecap;
+      WalkEntry e;
+      e.pos = (uint32_t)pos;
+      e.mask = h.mask;
+      e.len = (uint32_t)h.length;
+      e.meta = h.b0 | (h.masked << 8) | (h.hlen << 16);
+      *(rec ? entries + ebase + nf : sink) = e;
       ++nf;
       pb += round16(h.length);
       pl += h.length;
-      pos += h.hlen + h.length;
+      pos = next;
     }
     gevws_conn_out o;
-    o.first_frame = 0;
+    o.first_frame = rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
     o.consumed = pos;
     o.payload_base = pb;  // per-connection arena bytes; k_walk_emit turns it into a base
     o.nframes = (uint32_t)nf;
@@ -238,52 +293,109 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict
 }
 
 // ------------------------------------------------------------------ 3. walk (emit)
-__global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restrict__ in,
-                                                          const gevws_conn_in* __restrict__ conns,
-                                                          uint32_t n, gevws_conn_out* __restrict__ cout,
-                                                          const uint64_t* __restrict__ blk,
-                                                          const gevws_summary* __restrict__ sum,
-                                                          gevws_frame* __restrict__ frames,
-                                                          uint32_t* __restrict__ tile_first) {
+// 3a. per-connection bases: block-level exclusive scan of (frames, arena bytes)
+// on top of the scanned block partials.
+__global__ __launch_bounds__(kWalkBlock) void k_walk_bases(uint32_t n, gevws_conn_out* __restrict__ cout,
+                                                           const uint64_t* __restrict__ blk,
+                                                           const gevws_summary* __restrict__ sum,
+                                                           uint8_t* __restrict__ rec_flags) {
   if (sum->status != GEVWS_OK) return;  // capacity error: nothing written
   const uint32_t c = blockIdx.x * kWalkBlock + threadIdx.x;
   uint64_t v[2] = {0, 0};
+  gevws_conn_out o;
   if (c < n) {
-    v[0] = cout[c].nframes;
-    v[1] = cout[c].payload_base;
+    o = cout[c];
+    v[0] = o.nframes;
+    v[1] = o.payload_base;  // this connection's arena bytes (k_walk_count)
   }
   uint64_t ex[2], tot[2];
   block_excl_scan<kWalkBlock, 2>(v, ex, tot);
   if (c >= n) return;
-  const uint64_t f0 = blk[(uint64_t)blockIdx.x * kBlkFields + 0] + ex[0];
-  const uint64_t p0 = blk[(uint64_t)blockIdx.x * kBlkFields + 1] + ex[1];
-  cout[c].first_frame = f0;
-  cout[c].payload_base = p0;
-  const gevws_conn_in ci = conns[c];
-  const uint8_t* s = in + ci.off;
-  uint64_t pos = 0, poff = p0;
-  const uint64_t cnt = v[0];
-  for (uint64_t k = 0; k < cnt; ++k) {
-    uint64_t lo, hi;
-    load_window(s + pos, lo, hi);
-    DevHdr h;
-    parse_header(lo, hi, ci.len - pos, h);  // succeeded in k_walk_count
-    gevws_frame fr;
-    fr.hdr.fin = (uint8_t)(h.b0 >> 7);
-    fr.hdr.rsv = (uint8_t)((h.b0 & 0x70) >> 4);
-    fr.hdr.opcode = (uint8_t)(h.b0 & 0x0f);
-    fr.hdr.masked = (uint8_t)h.masked;
-    memcpy(fr.hdr.mask, &h.mask, 4);
-    fr.hdr.length = (int64_t)h.length;
-    fr.payload_off = poff;
-    fr.src_off = ci.off + pos + h.hlen;
-    frames[f0 + k] = fr;
-    const uint64_t padded = round16(h.length);
-    // output tiles whose first byte lies in [poff, poff + padded)
-    for (uint64_t t = (poff + kTile - 1) / kTile; t * kTile < poff + padded; ++t)
-      tile_first[t] = (uint32_t)(f0 + k);
-    poff += padded;
-    pos += h.hlen + h.length;
+  rec_flags[c] = o.first_frame != 0 ? 1 : 0;  // k_walk_count's "entries recorded" flag
+  o.first_frame = blk[(uint64_t)blockIdx.x * kBlkFields + 0] + ex[0];
+  o.payload_base = blk[(uint64_t)blockIdx.x * kBlkFields + 1] + ex[1];
+  cout[c] = o;
+}
+
+__device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, uint32_t* __restrict__ tile_first,
+                                            uint64_t f, uint64_t poff, uint64_t src_off, const DevHdr& h) {
+  gevws_frame fr;
+  fr.hdr.fin = (uint8_t)(h.b0 >> 7);
+  fr.hdr.rsv = (uint8_t)((h.b0 & 0x70) >> 4);
+  fr.hdr.opcode = (uint8_t)(h.b0 & 0x0f);
+  fr.hdr.masked = (uint8_t)h.masked;
+  memcpy(fr.hdr.mask, &h.mask, 4);
+  fr.hdr.length = (int64_t)h.length;
+  fr.payload_off = poff;
+  fr.src_off = src_off;
+  frames[f] = fr;
+  const uint64_t padded = round16(h.length);
+  // output tiles whose first byte lies in [poff, poff + padded)
+  for (uint64_t t = (poff + kTile - 1) / kTile; t * kTile < poff + padded; ++t) tile_first[t] = (uint32_t)f;
+}
+
+// 3b. records + tile map, one wave per connection: 64 recorded entries at a
+// time (coalesced), wave prefix sum of their padded lengths -> payload
+// offsets, 64 contiguous 32-byte records per store.  Connections without
+// recorded entries are re-walked afterwards, one lane per connection.
+__global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restrict__ in,
+                                                          const gevws_conn_in* __restrict__ conns, uint32_t n,
+                                                          const gevws_conn_out* __restrict__ cout,
+                                                          const gevws_summary* __restrict__ sum,
+                                                          gevws_frame* __restrict__ frames,
+                                                          uint32_t* __restrict__ tile_first,
+                                                          const WalkEntry* __restrict__ entries, uint64_t n_entries,
+                                                          uint32_t gshift, const uint8_t* __restrict__ rec_flags) {
+  if (sum->status != GEVWS_OK) return;
+  const int lane = threadIdx.x & 63;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (kWalkBlock / 64);
+  for (uint64_t c = (uint64_t)blockIdx.x * (kWalkBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
+    const gevws_conn_out o = cout[c];
+    const uint64_t cnt = o.nframes;
+    if (cnt == 0) continue;
+    if (!rec_flags[c]) continue;  // second phase below
+    const gevws_conn_in ci = conns[c];
+    {
+      uint64_t ebase = 0, ecap = 0;
+      entry_slots(conns, n, (uint32_t)c, ci, n_entries, gshift, ebase, ecap);
+      uint64_t carry = o.payload_base;
+      for (uint64_t k0 = 0; k0 < cnt; k0 += 64) {
+        const uint64_t k = k0 + lane;
+        const bool valid = k < cnt;
+        WalkEntry q = {0, 0, 0, 0};
+        if (valid) q = entries[ebase + k];
+        const uint64_t padded = valid ? round16(q.len) : 0;
+        const uint64_t incl = wave_incl_scan(padded);
+        if (valid) {
+          DevHdr h;
+          h.b0 = q.meta & 0xff;
+          h.masked = (q.meta >> 8) & 1;
+          h.hlen = q.meta >> 16;
+          h.mask = q.mask;
+          h.length = q.len;
+          emit_record(frames, tile_first, o.first_frame + k, carry + incl - padded, ci.off + q.pos + h.hlen, h);
+        }
+        carry += __shfl(incl, 63, 64);
+      }
+    }
+  }
+  // connections without recorded entries: one lane per connection re-walks
+  const uint64_t nthreads = (uint64_t)gridDim.x * kWalkBlock;
+  for (uint64_t c = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x; c < n; c += nthreads) {
+    if (rec_flags[c]) continue;
+    const gevws_conn_out o = cout[c];
+    const gevws_conn_in ci = conns[c];
+    const uint8_t* s = in + ci.off;
+    uint64_t pos = 0, poff = o.payload_base;
+    for (uint64_t k = 0; k < o.nframes; ++k) {
+      uint64_t lo, hi;
+      load_window(s + pos, lo, hi);
+      DevHdr h;
+      parse_header(lo, hi, ci.len - pos, h);  // succeeded in k_walk_count
+      emit_record(frames, tile_first, o.first_frame + k, poff, ci.off + pos + h.hlen, h);
+      poff += round16(h.length);
+      pos += h.hlen + h.length;
+    }
   }
 }
 
@@ -1359,7 +1471,6 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
                              const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames,
                              uint64_t max_frames, uint8_t* d_payload, uint64_t payload_cap,
                              gevws_conn_out* d_conn_out, gevws_summary* d_summary) {
-  (void)in_bytes;
   if (!ctx || !d_summary) return GEVWS_ERR_INVALID;
   if (n_conns && (!d_in || !d_conns || !d_conn_out)) return GEVWS_ERR_INVALID;
   if (max_frames > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;  // tile map holds 32-bit frame ids
@@ -1368,10 +1479,19 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   const uint32_t nblk = (n_conns + kWalkBlock - 1) / kWalkBlock;
   const uint64_t ntiles_cap = (payload_cap + kTile - 1) / kTile + 1;
   const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
-  int r = ensure_scratch(ctx, blk_bytes + ntiles_cap * sizeof(uint32_t));
+  const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
+  uint32_t gshift = kEntryGranMinShift;
+  while ((in_bytes >> gshift) > kEntryBudget) ++gshift;
+  const uint64_t n_entries = (in_bytes >> gshift) + 2ull * n_conns + 2;
+  const size_t flag_bytes = ((size_t)n_conns + 255) & ~size_t(255);
+  // + one sink slot per connection after the table (k_walk_count)
+  int r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + (n_entries + n_conns) * sizeof(WalkEntry));
   if (r != GEVWS_OK) return r;
-  uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
-  uint32_t* tile_first = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes);
+  char* sp = reinterpret_cast<char*>(ctx->scratch);
+  uint64_t* blk = reinterpret_cast<uint64_t*>(sp);
+  uint32_t* tile_first = reinterpret_cast<uint32_t*>(sp + blk_bytes);
+  uint8_t* rec_flags = reinterpret_cast<uint8_t*>(sp + blk_bytes + tile_bytes);
+  WalkEntry* entries = reinterpret_cast<WalkEntry*>(sp + blk_bytes + tile_bytes + flag_bytes);
   const bool timed = ctx->timing;
   hipEvent_t* ev = nullptr;
   if (timed) {
@@ -1383,13 +1503,18 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     ev = ctx->evs[ctx->evs_used++].e;
     GEVWS_HIP(hipEventRecord(ev[0], st));
   }
-  if (nblk) k_walk_count<<<nblk, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk);
+  if (nblk)
+    k_walk_count<<<nblk, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, n_entries, gshift);
   if (timed) GEVWS_HIP(hipEventRecord(ev[1], st));
   k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
   if (timed) GEVWS_HIP(hipEventRecord(ev[2], st));
-  if (nblk)
-    k_walk_emit<<<nblk, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, d_summary,
-                                              d_frames, tile_first);
+  if (nblk) {
+    k_walk_bases<<<nblk, kWalkBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags);
+    uint64_t egrid = ((uint64_t)n_conns + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
+    if (egrid > 8 * (uint64_t)ctx->num_cus) egrid = 8 * (uint64_t)ctx->num_cus;
+    k_walk_emit<<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, d_summary, d_frames,
+                                                         tile_first, entries, n_entries, gshift, rec_flags);
+  }
   if (timed) GEVWS_HIP(hipEventRecord(ev[3], st));
   r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);
   if (r != GEVWS_OK) return r;
