@@ -1285,6 +1285,12 @@ struct gevws_ctx {
   gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
+  // Scratch is per context: calls on a different stream than the previous one
+  // first wait for it (one in-flight batch per context; use one context per
+  // stream for concurrency).
+  hipEvent_t last_done = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool has_last = false;
   int num_cus = 256;
 };
 
@@ -1316,6 +1322,19 @@ struct DeviceGuard {
 hipStream_t pick_stream(gevws_ctx* ctx, void* stream) {
   (void)ctx;
   return reinterpret_cast<hipStream_t>(stream);
+}
+
+// Orders this call after the context's previous one when the stream changes.
+int order_after_last(gevws_ctx* ctx, hipStream_t st) {
+  if (ctx->has_last && ctx->last_stream != st) GEVWS_HIP(hipStreamWaitEvent(st, ctx->last_done, 0));
+  return GEVWS_OK;
+}
+
+int mark_last(gevws_ctx* ctx, hipStream_t st) {
+  GEVWS_HIP(hipEventRecord(ctx->last_done, st));
+  ctx->last_stream = st;
+  ctx->has_last = true;
+  return GEVWS_OK;
 }
 
 int ensure_scratch(gevws_ctx* ctx, size_t bytes) {
@@ -1394,6 +1413,10 @@ gevws_ctx* gevws_ctx_create(int device) {
     delete ctx;
     return nullptr;
   }
+  if (hipEventCreateWithFlags(&ctx->last_done, hipEventDisableTiming) != hipSuccess) {
+    gevws_ctx_destroy(ctx);
+    return nullptr;
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
@@ -1410,6 +1433,7 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->d_sum) (void)hipFree(ctx->d_sum);
+  if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
   for (auto& set : ctx->evs)
     for (auto& e : set.e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1485,7 +1509,9 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   const uint64_t n_entries = (in_bytes >> gshift) + 2ull * n_conns + 2;
   const size_t flag_bytes = ((size_t)n_conns + 255) & ~size_t(255);
   // + one sink slot per connection after the table (k_walk_count)
-  int r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + (n_entries + n_conns) * sizeof(WalkEntry));
+  int r = order_after_last(ctx, st);
+  if (r != GEVWS_OK) return r;
+  r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + (n_entries + n_conns) * sizeof(WalkEntry));
   if (r != GEVWS_OK) return r;
   char* sp = reinterpret_cast<char*>(ctx->scratch);
   uint64_t* blk = reinterpret_cast<uint64_t*>(sp);
@@ -1520,7 +1546,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   if (r != GEVWS_OK) return r;
   if (timed) GEVWS_HIP(hipEventRecord(ev[4], st));
   GEVWS_HIP(hipGetLastError());
-  return GEVWS_OK;
+  return mark_last(ctx, st);
 }
 
 int gevws_decode_batch(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64_t in_bytes,
@@ -1553,7 +1579,9 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   const uint32_t nblk = (uint32_t)nblk64;
   const uint64_t ntiles_cap = (out_cap + kTile - 1) / kTile + 1;
   const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
-  int r = ensure_scratch(ctx, blk_bytes + ntiles_cap * sizeof(uint32_t));
+  int r = order_after_last(ctx, st);
+  if (r != GEVWS_OK) return r;
+  r = ensure_scratch(ctx, blk_bytes + ntiles_cap * sizeof(uint32_t));
   if (r != GEVWS_OK) return r;
   uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
   uint32_t* tile_first = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes);
@@ -1569,7 +1597,7 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   k_encode<4><<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
                                                        0u);
   GEVWS_HIP(hipGetLastError());
-  return GEVWS_OK;
+  return mark_last(ctx, st);
 }
 
 int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t n, int policy,
@@ -1583,7 +1611,9 @@ int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_fram
   if (nblk64 > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
   const uint32_t nblk = (uint32_t)nblk64;
   const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
-  int r = ensure_scratch(ctx, blk_bytes);
+  int r = order_after_last(ctx, st);
+  if (r != GEVWS_OK) return r;
+  r = ensure_scratch(ctx, blk_bytes);
   if (r != GEVWS_OK) return r;
   uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
   if (nblk) k_disp_count<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, blk);
@@ -1592,7 +1622,7 @@ int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_fram
     k_disp_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, d_payload, aux_off, blk, d_summary, d_replies,
                                               d_reply_of, d_payload + aux_off);
   GEVWS_HIP(hipGetLastError());
-  return GEVWS_OK;
+  return mark_last(ctx, st);
 }
 
 int gevws_cipher_async(gevws_ctx* ctx, void* stream, uint8_t* d_p, uint64_t n, const uint8_t mask[4],

@@ -238,3 +238,32 @@ def test_small_frame_window_paths(engine):
     streams = [tiny16, big + empties + big, tiny_mixed + mid, mid + tiny16[:5000] + big, empties]
     arena, conns = pack_streams(streams)
     assert_matches_oracle(engine, arena, conns, "small-frame windows")
+
+
+def test_one_context_two_streams_is_ordered(engine):
+    """A context's scratch is shared by its calls: a call on another stream is
+    ordered after the previous one (gevws_ctx semantics), so two batches
+    issued back to back on two streams through ONE context both decode right."""
+    import torch
+    import gev_amd
+    rng = np.random.default_rng(17)
+    dev = torch.device("cuda", engine.device)
+    batches = []
+    for nconn in (200, 37):
+        streams = [random_stream(rng, int(rng.integers(0, 40))) for _ in range(nconn)]
+        arena, conns = pack_streams(streams)
+        a = np.frombuffer(arena, np.uint8).copy()
+        d_in = torch.zeros(a.size + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+        d_in[: a.size] = torch.from_numpy(a).to(dev)
+        d_c = torch.from_numpy(conns.copy()).to(dev)
+        mf, cap = a.size // 2 + 1, a.size * 9 + 64
+        batches.append((a, conns, d_in, d_c, engine.alloc_batch(nconn, mf, cap), mf, cap))
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    for (a, conns, d_in, d_c, out, mf, cap), s in zip(batches, (s1, s2)):
+        engine.decode_async(d_in, a.size, d_c, conns.shape[0], out, mf, cap, stream=s)
+    torch.cuda.synchronize()
+    for a, conns, d_in, d_c, out, mf, cap in batches:
+        want = ref.decode_batch(a, conns[:, 0], conns[:, 1])
+        assert out.frames_host().tobytes() == want["frames"].tobytes()
+        assert np.array_equal(out.payload_host(), want["payload"])

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--chunk-mib", type=int, default=256)
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--sweep", default="", help="comma list of chunk_mib:streams to measure, e.g. 64:2,128:3")
     args = ap.parse_args()
 
     import numpy as np
@@ -40,16 +41,9 @@ def main():
     dev = torch.device("cuda", 0)
     eng = gev_amd.Engine(0)
     n_frames = int(args.gib * 2**30) // args.frame
-    fpc = max(1, (args.chunk_mib << 20) // args.frame // 16)      # 16 connections per chunk
-    n_conns = max(1, n_frames // fpc)
-    lay = w.uniform(n_conns, fpc, args.frame, name=f"{n_conns * fpc} x {args.frame} B masked binary")
+    lay = w.uniform(max(1, n_frames // 64), 64, args.frame, name=f"{n_frames} x {args.frame} B masked binary")
     stream_bytes = int(lay.conns[0, 1])
-    conns_per_chunk = 16
-    n_chunks = (n_conns + conns_per_chunk - 1) // conns_per_chunk
-    chunk_in = conns_per_chunk * stream_bytes
-    chunk_frames = conns_per_chunk * fpc
-    chunk_pay = chunk_frames * ((args.frame + 15) // 16 * 16)
-
+    fpc = 64
     # build the batch on the device and stage it into pinned host memory
     d_all = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
     d_all[lay.arena_bytes:] = 0
@@ -58,50 +52,65 @@ def main():
     h_in.copy_(d_all)
     del d_all
     torch.cuda.empty_cache()
-    h_pay = torch.empty(n_chunks * chunk_pay, dtype=torch.uint8, pin_memory=True)
-    h_frames = torch.empty((n_chunks * chunk_frames, 32), dtype=torch.uint8, pin_memory=True)
-    h_cout = torch.empty((n_chunks * conns_per_chunk, 32), dtype=torch.uint8, pin_memory=True)
+    pay_frame = (args.frame + 15) // 16 * 16
+    h_pay = torch.empty(lay.n_frames * pay_frame, dtype=torch.uint8, pin_memory=True)
+    h_frames = torch.empty((lay.n_frames, 32), dtype=torch.uint8, pin_memory=True)
+    h_cout = torch.empty((lay.n_conns, 32), dtype=torch.uint8, pin_memory=True)
 
-    S = args.streams
-    streams = [torch.cuda.Stream(dev) for _ in range(S)]
-    d_in = [torch.zeros(chunk_in + gev_amd.IN_PAD, dtype=torch.uint8, device=dev) for _ in range(S)]
-    outs = [eng.alloc_batch(conns_per_chunk, chunk_frames, chunk_pay) for _ in range(S)]
-    conn_tab = np.stack([np.arange(conns_per_chunk, dtype=np.int64) * stream_bytes,
-                         np.full(conns_per_chunk, stream_bytes, np.int64)], 1)
-    d_conns = torch.from_numpy(conn_tab).to(dev)
+    def run(chunk_mib: int, S: int):
+        cpc = max(1, (chunk_mib << 20) // stream_bytes)          # connections per chunk
+        n_chunks = (lay.n_conns + cpc - 1) // cpc
+        chunk_in = cpc * stream_bytes
+        chunk_frames = cpc * fpc
+        chunk_pay = chunk_frames * pay_frame
+        streams = [torch.cuda.Stream(dev) for _ in range(S)]
+        engs = [gev_amd.Engine(0) for _ in range(S)]  # one context (scratch) per stream
+        d_in = [torch.zeros(chunk_in + gev_amd.IN_PAD, dtype=torch.uint8, device=dev) for _ in range(S)]
+        outs = [eng.alloc_batch(cpc, chunk_frames, chunk_pay) for _ in range(S)]
+        conn_tab = np.stack([np.arange(cpc, dtype=np.int64) * stream_bytes,
+                             np.full(cpc, stream_bytes, np.int64)], 1)
+        d_conns = torch.from_numpy(conn_tab).to(dev)
 
-    def one_pass():
-        for c in range(n_chunks):
-            k = c % S
-            s = streams[k]
-            nconn = min(conns_per_chunk, n_conns - c * conns_per_chunk)
-            nin = nconn * stream_bytes
-            with torch.cuda.stream(s):
-                d_in[k][:nin].copy_(h_in[c * chunk_in:c * chunk_in + nin], non_blocking=True)
-                eng.decode_async(d_in[k], nin, d_conns, nconn, outs[k], chunk_frames, chunk_pay, stream=s)
-                h_pay[c * chunk_pay:(c + 1) * chunk_pay].copy_(outs[k].payload[:chunk_pay], non_blocking=True)
-                h_frames[c * chunk_frames:(c + 1) * chunk_frames].copy_(outs[k].frames[:chunk_frames],
-                                                                         non_blocking=True)
-                h_cout[c * conns_per_chunk:(c + 1) * conns_per_chunk].copy_(
-                    outs[k].conn_out[:conns_per_chunk], non_blocking=True)
-        torch.cuda.synchronize()
+        def one_pass():
+            for c in range(n_chunks):
+                k = c % S
+                s = streams[k]
+                nconn = min(cpc, lay.n_conns - c * cpc)
+                nin, nfr = nconn * stream_bytes, nconn * fpc
+                with torch.cuda.stream(s):
+                    d_in[k][:nin].copy_(h_in[c * chunk_in:c * chunk_in + nin], non_blocking=True)
+                    engs[k].decode_async(d_in[k], nin, d_conns, nconn, outs[k], chunk_frames, chunk_pay, stream=s)
+                    f0 = c * chunk_frames
+                    h_pay[f0 * pay_frame:(f0 + nfr) * pay_frame].copy_(outs[k].payload[:nfr * pay_frame],
+                                                                       non_blocking=True)
+                    h_frames[f0:f0 + nfr].copy_(outs[k].frames[:nfr], non_blocking=True)
+                    h_cout[c * cpc:c * cpc + nconn].copy_(outs[k].conn_out[:nconn], non_blocking=True)
+            torch.cuda.synchronize()
 
-    one_pass()  # warm
-    # spot-check: the first chunk's payloads equal the generator's plaintext
-    fr = h_frames[:4].numpy().reshape(-1).view(gev_amd.FRAME_DTYPE)
-    for g in range(4):
-        o = int(fr["payload_off"][g])
-        assert h_pay[o:o + args.frame].numpy().tobytes() == w.plaintext(lay.seed, g, args.frame)
-    times = []
-    for _ in range(args.reps):
-        t0 = time.perf_counter()
-        one_pass()
-        times.append(time.perf_counter() - t0)
-    t = min(times)
+        one_pass()  # warm
+        fr = h_frames[:4].numpy().reshape(-1).view(gev_amd.FRAME_DTYPE)
+        for g in range(4):
+            o = int(fr["payload_off"][g])
+            assert h_pay[o:o + args.frame].numpy().tobytes() == w.plaintext(lay.seed, g, args.frame)
+        last = lay.n_frames - 1
+        assert h_pay[last * pay_frame:last * pay_frame + args.frame].numpy().tobytes() == \
+            w.plaintext(lay.seed, last, args.frame)
+        times = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            one_pass()
+            times.append(time.perf_counter() - t0)
+        t = min(times)
+        del outs, d_in
+        for e in engs:
+            e.close()
+        torch.cuda.empty_cache()
+        return {"chunk_mib": chunk_mib, "streams": S, "chunks": n_chunks, "seconds": round(t, 4),
+                "payload_GiBps": round(lay.payload_len / t / 2**30, 2), "frames_per_s": round(lay.n_frames / t, 1)}
 
     # raw pinned copy rates of the same byte counts
-    d_tmp = torch.empty(chunk_in * min(n_chunks, 8), dtype=torch.uint8, device=dev)
-    n_tmp = d_tmp.numel()
+    n_tmp = min(2 << 30, lay.arena_bytes)
+    d_tmp = torch.empty(n_tmp, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(3):
@@ -113,13 +122,16 @@ def main():
         h_pay[:n_tmp].copy_(d_tmp, non_blocking=True)
     torch.cuda.synchronize()
     d2h = 3 * n_tmp / (time.perf_counter() - t0)
-
+    del d_tmp
+    configs = [(args.chunk_mib, args.streams)]
+    if args.sweep:
+        configs = [tuple(int(x) for x in item.split(":")) for item in args.sweep.split(",")]
+    runs = [run(cm, S) for cm, S in configs]
+    best = max(runs, key=lambda r: r["payload_GiBps"])
     res = {"mode": "host-inclusive (pinned H2D -> decode -> D2H, overlapped)",
            "workload": lay.name, "payload_bytes": lay.payload_len, "input_bytes": lay.arena_bytes,
-           "chunks": n_chunks, "chunk_input_bytes": chunk_in, "streams": S,
-           "seconds": round(t, 4), "payload_GiBps": round(lay.payload_len / t / 2**30, 2),
-           "frames_per_s": round(lay.n_frames / t, 1),
-           "pinned_h2d_GBps": round(h2d / 1e9, 2), "pinned_d2h_GBps": round(d2h / 1e9, 2)}
+           "payload_GiBps": best["payload_GiBps"], "frames_per_s": best["frames_per_s"], "best": best,
+           "runs": runs, "pinned_h2d_GBps": round(h2d / 1e9, 2), "pinned_d2h_GBps": round(d2h / 1e9, 2)}
     print(json.dumps(res))
 
 
