@@ -8,7 +8,7 @@ D2H (payload arena + frame records + per-connection results) on one of S
 streams, so copies in both directions overlap the device work.  Reports payload
 GiB/s host-to-host next to the raw pinned H2D / D2H copy rates on this box.
 
-    python tools/host_inclusive.py [--gib 8] [--chunk-mib 256] [--streams 3] [--reps 3]
+    python tools/host_inclusive.py [--gib 8] [--chunk-mib 64] [--streams 2] [--reps 3] [--sweep 64:2,128:3]
 """
 from __future__ import annotations
 
@@ -26,8 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=8.0, help="payload GiB per pass")
     ap.add_argument("--frame", type=int, default=65536)
-    ap.add_argument("--chunk-mib", type=int, default=256)
-    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--chunk-mib", type=int, default=64)
+    ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--sweep", default="", help="comma list of chunk_mib:streams to measure, e.g. 64:2,128:3")
     args = ap.parse_args()
