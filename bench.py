@@ -67,25 +67,25 @@ def cpu_sample_layout(name: str):
     return w.config_c5(n_conns=32, seed=1)
 
 
-def cpu_baseline(name: str, seconds: float, threads: int):
+def cpu_baseline(name: str, seconds: float, threads: int, vectorized: bool = False):
     import numpy as np
     from gev_amd import workloads as w
     from oracle import ref
     lay = cpu_sample_layout(name)
     arena = np.concatenate([w.synth_host(lay), np.zeros(64, np.uint8)])
     secs, pb, nf = ref.bench_pipeline(arena, lay.conns[:, 0], lay.conns[:, 1], threads=threads,
-                                      min_seconds=seconds)
+                                      min_seconds=seconds, vectorized=vectorized)
     return dict(value=round(pb / secs / 2**30, 4), unit="GiB/s", cores=threads, kind="port",
                 frames_per_s=round(nf / secs, 1),
                 sample=(f"{lay.name}, {lay.n_conns} connections round-robin over {threads} thread(s), "
                         f"repeated for >= {seconds:.0f} s; oracle/ws_ref.c per-frame UnPacket pipeline "
                         "(header parse, zero-filled make, ring Read copy, Cipher u64 loop), "
-                        "gcc -O2 -fno-tree-vectorize"))
+                        + ("gcc -O3 -mavx2 (auto-vectorised)" if vectorized else "gcc -O2 -fno-tree-vectorize")))
 
 
 def load_traffic(config_name: str):
     """HBM bytes per unmask launch from a committed rocprofv3 --pmc pass (see
-    profiles/README.md), or None."""
+    profiles/README.md, DESIGN.md §5), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
@@ -221,6 +221,9 @@ def main():
             log(f"cpu baseline ({args.cpu_threads_multi} threads)...")
             result["cpu_baseline_multi"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0),
                                                         args.cpu_threads_multi)
+        log("cpu baseline (1 thread, auto-vectorised build)...")
+        result["cpu_baseline_vectorized"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0), 1,
+                                                         vectorized=True)
     print(json.dumps(result), flush=True)
     dist.finalize()
 

@@ -13,6 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
+_VEC = None
 
 FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked", "u1"),
                         ("mask", "u1", (4,)), ("length", "<i8"),
@@ -28,13 +29,30 @@ def build() -> str:
     return os.path.join(_HERE, "libwsref.so")
 
 
+def _load(name: str):
+    path = os.path.join(_HERE, name)
+    if not os.path.exists(path):
+        build()
+    return ctypes.CDLL(path)
+
+
+def vec_lib():
+    """The -O3 -mavx2 build of the same restatement (bench pipeline only)."""
+    global _VEC
+    if _VEC is None:
+        L = _load("libwsref_vec.so")
+        P = ctypes.c_void_p
+        L.wsref_bench_pipeline.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_int, ctypes.c_double,
+                                           P, P, P]
+        L.wsref_bench_pipeline.restype = ctypes.c_double
+        _VEC = L
+    return _VEC
+
+
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "libwsref.so")
-        if not os.path.exists(path):
-            build()
-        L = ctypes.CDLL(path)
+        L = _load("libwsref.so")
         P = ctypes.c_void_p
         L.wsref_cipher.argtypes = [P, ctypes.c_size_t, P, ctypes.c_size_t]
         L.wsref_cipher.restype = None
@@ -98,14 +116,16 @@ def decode_batch(arena: np.ndarray, conn_off: np.ndarray, conn_len: np.ndarray,
 
 
 def bench_pipeline(arena: np.ndarray, conn_off: np.ndarray, conn_len: np.ndarray,
-                   threads: int = 1, min_seconds: float = 10.0):
-    """Time the reference per-frame pipeline; returns (seconds, payload_bytes, frames)."""
+                   threads: int = 1, min_seconds: float = 10.0, vectorized: bool = False):
+    """Time the reference per-frame pipeline; returns (seconds, payload_bytes, frames).
+    vectorized=True times the -O3 -mavx2 build of the same C source."""
     pb = np.zeros(1, dtype=np.uint64)
     nf = np.zeros(1, dtype=np.uint64)
     ck = np.zeros(1, dtype=np.uint64)
     conn_off = np.ascontiguousarray(conn_off, dtype=np.uint64)
     conn_len = np.ascontiguousarray(conn_len, dtype=np.uint64)
-    secs = lib().wsref_bench_pipeline(_ptr(arena), _ptr(conn_off), _ptr(conn_len), conn_off.size,
+    L = vec_lib() if vectorized else lib()
+    secs = L.wsref_bench_pipeline(_ptr(arena), _ptr(conn_off), _ptr(conn_len), conn_off.size,
                                       threads, min_seconds, _ptr(pb), _ptr(nf), _ptr(ck))
     return secs, int(pb[0]), int(nf[0])
 
