@@ -15,14 +15,15 @@ gev uses it), ``Connection`` (gev.Connection's websocket context keys),
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import _abi
-from ._abi import (ERR_CAPACITY, ERR_DEVICE, ERR_INVALID, ERR_LEN_MSB, ERR_NOT_UPGRADED, IN_PAD, NEED_MORE,
-                   OK, PAYLOAD_ALIGN, TILE, Header)
+from ._abi import (ERR_CAPACITY, ERR_DEVICE, ERR_HANDSHAKE, ERR_INVALID, ERR_LEN_MSB, ERR_NOT_UPGRADED,
+                   HANDSHAKE, IN_PAD, NEED_MORE, OK, PAYLOAD_ALIGN, TILE, Header)
 
 lib = _abi.load()
 
@@ -274,9 +275,9 @@ class RingBuffer:
     def __init__(self, size: int = 4096):
         self._p = lib.gevws_ring_new(size)
 
-    def __del__(self):
+    def __del__(self, _free=lib.gevws_ring_free):  # bound now: module globals are gone at exit
         if getattr(self, "_p", None):
-            lib.gevws_ring_free(self._p)
+            _free(self._p)
             self._p = None
 
     def write(self, data: bytes) -> int:
@@ -304,17 +305,27 @@ class RingBuffer:
         lib.gevws_ring_retrieve(self._p, n)
 
 
+_CONNS: "weakref.WeakValueDictionary[int, Connection]" = weakref.WeakValueDictionary()
+
+
 class Connection:
     """The per-connection context keys of the websocket plugin (protocol.go:11-14)."""
 
     def __init__(self, upgraded: bool = True):
         self._p = lib.gevws_conn_new()
+        _CONNS[self._p] = self
         self.set_upgraded(upgraded)
 
-    def __del__(self):
+    def __del__(self, _free=lib.gevws_conn_free):  # bound now: module globals are gone at exit
         if getattr(self, "_p", None):
-            lib.gevws_conn_free(self._p)
+            _free(self._p)
             self._p = None
+
+    def handshake(self) -> "HandshakeInfo":
+        """The last handshake's ws.Handshake and error (after UnPacket ran it)."""
+        hs = _abi.Handshake()
+        lib.gevws_conn_handshake(self._p, ctypes.byref(hs))
+        return HandshakeInfo._from(hs)
 
     def set_upgraded(self, v: bool) -> None:
         lib.gevws_conn_set_upgraded(self._p, int(v))
@@ -327,26 +338,225 @@ class Connection:
         return lib.gevws_conn_pending(self._p)
 
 
+class RejectError(Exception):
+    """ws.RejectConnectionError(RejectionStatus(code), RejectionReason(reason),
+    RejectionHeader(header)) (plugins/websocket/ws/errors.go:81-129).  Raise it
+    from an Upgrader hook; any other exception is a plain Go error (HTTP 500,
+    ws.go:325-333)."""
+
+    def __init__(self, reason: str = "", code: int = 0, header: bytes = b""):
+        super().__init__(reason)
+        self.reason, self.code, self.header = reason, code, header
+
+
+class HandshakeError(Exception):
+    """A failed Upgrader.Upgrade: kind = GEVWS_HS_*, reason = err.Error()."""
+
+    def __init__(self, kind: int, reason: str, http_code: int):
+        super().__init__(reason)
+        self.kind, self.reason, self.http_code = kind, reason, http_code
+
+
+@dataclass
+class HandshakeInfo:
+    """ws.Handshake (ws/ws.go:40-47) plus the error of the call."""
+    protocol: bytes
+    extensions: bytes
+    error: int
+    http_code: int
+    reason: str
+
+    @staticmethod
+    def _from(hs: "_abi.Handshake") -> "HandshakeInfo":
+        return HandshakeInfo(ctypes.string_at(hs.protocol, hs.protocol_len) if hs.protocol_len else b"",
+                             ctypes.string_at(hs.extensions, hs.extensions_len) if hs.extensions_len else b"",
+                             hs.error, hs.http_code, (hs.reason or b"").decode())
+
+
+def accept_key(nonce: bytes) -> bytes:
+    """initAcceptFromNonce (ws/nonce.go:23-39) through the C ABI."""
+    assert len(nonce) == 24
+    out = ctypes.create_string_buffer(28)
+    lib.gevws_accept_key(nonce, out)
+    return out.raw
+
+
+class Upgrader:
+    """ws.Upgrader (plugins/websocket/ws/ws.go:49-154) over the C ABI.
+
+    Hooks take the reference's arguments (bytes for []byte):
+      protocol(token) -> bool;  protocol_custom(conn, value) -> (selected, ok);
+      extension(name, [(key, value or None)]) -> bool;
+      extension_custom(conn, value, selected_so_far) -> (selected, ok);
+      on_request(conn, uri), on_host(conn, host), on_header(conn, key, value):
+        return None to accept, raise RejectError / Exception to reject;
+      on_before_upgrade(conn) -> extra response header bytes or None, or raise.
+    ``header`` is Upgrader.Header (raw "Key: value\\r\\n" lines)."""
+
+    def __init__(self, header: bytes = b"", **hooks):
+        self._p = lib.gevws_upgrader_new()
+        self._keep: list = []
+        if header:
+            lib.gevws_upgrader_set_header(self._p, header, len(header))
+        unknown = set(hooks) - {"protocol", "protocol_custom", "extension", "extension_custom", "on_request",
+                                "on_host", "on_header", "on_before_upgrade"}
+        if unknown:
+            raise TypeError(f"unknown Upgrader hooks {sorted(unknown)}")
+        self._hooks = hooks
+        h = _abi.UpgraderHooks()
+        for name, fn in hooks.items():
+            if fn is not None:
+                setattr(h, name, getattr(self, "_c_" + name)())
+        self._cstruct = h
+        lib.gevws_upgrader_set_hooks(self._p, ctypes.byref(h))
+
+    def __del__(self, _free=lib.gevws_upgrader_free):  # bound now: module globals are gone at exit
+        if getattr(self, "_p", None):
+            _free(self._p)
+            self._p = None
+
+    # -- C trampolines (each keeps its own ctypes callback object alive)
+    def _hold(self, b: bytes) -> int:
+        buf = ctypes.create_string_buffer(b, len(b) + 1)
+        self._keep.append(buf)
+        return ctypes.addressof(buf)
+
+    def _reject(self, rej, e: Exception) -> int:
+        r = rej.contents
+        if isinstance(e, RejectError):
+            reason = e.reason.encode()
+            r.code, r.plain = e.code, 0
+            if e.header:
+                r.header, r.header_len = self._hold(e.header), len(e.header)
+        else:
+            reason = str(e).encode()
+            r.code, r.plain = 0, 1
+        r.reason, r.reason_len = self._hold(reason), len(reason)
+        return 1
+
+    @staticmethod
+    def _b(p, n) -> bytes:
+        return ctypes.string_at(p, n) if n else b""
+
+    def _c_protocol(self):
+        fn = self._hooks["protocol"]
+        return _abi.HOOK_PROTOCOL(lambda u, t, n: int(bool(fn(self._b(t, n)))))
+
+    def _c_protocol_custom(self):
+        fn = self._hooks["protocol_custom"]
+
+        def cb(u, c, v, n, sel, sel_n):
+            got, ok = fn(_CONNS.get(c), self._b(v, n))
+            got = got.encode() if isinstance(got, str) else (got or b"")
+            sel[0], sel_n[0] = (self._hold(got) if got else None), len(got)
+            return int(bool(ok))
+        return _abi.HOOK_PROTOCOL_CUSTOM(cb)
+
+    def _c_extension(self):
+        fn = self._hooks["extension"]
+
+        def cb(u, name, n, params, npar):
+            ps = [(self._b(params[i].key, params[i].key_len),
+                   None if not params[i].value else self._b(params[i].value, params[i].value_len))
+                  for i in range(npar)]
+            return int(bool(fn(self._b(name, n), ps)))
+        return _abi.HOOK_EXTENSION(cb)
+
+    def _c_extension_custom(self):
+        fn = self._hooks["extension_custom"]
+
+        def cb(u, c, v, n, cur, cur_n, sel, sel_n):
+            got, ok = fn(_CONNS.get(c), self._b(v, n), self._b(cur, cur_n))
+            got = got or b""
+            sel[0], sel_n[0] = (self._hold(got) if got else None), len(got)
+            return int(bool(ok))
+        return _abi.HOOK_EXTENSION_CUSTOM(cb)
+
+    def _value_hook(self, name):
+        fn = self._hooks[name]
+
+        def cb(u, c, v, n, rej):
+            try:
+                fn(_CONNS.get(c), self._b(v, n))
+                return 0
+            except Exception as e:  # noqa: BLE001 -- every hook error is a rejection
+                return self._reject(rej, e)
+        return _abi.HOOK_ON_VALUE(cb)
+
+    def _c_on_request(self):
+        return self._value_hook("on_request")
+
+    def _c_on_host(self):
+        return self._value_hook("on_host")
+
+    def _c_on_header(self):
+        fn = self._hooks["on_header"]
+
+        def cb(u, c, k, kn, v, vn, rej):
+            try:
+                fn(_CONNS.get(c), self._b(k, kn), self._b(v, vn))
+                return 0
+            except Exception as e:  # noqa: BLE001
+                return self._reject(rej, e)
+        return _abi.HOOK_ON_HEADER(cb)
+
+    def _c_on_before_upgrade(self):
+        fn = self._hooks["on_before_upgrade"]
+
+        def cb(u, c, hdr, hdr_len, rej):
+            try:
+                extra = fn(_CONNS.get(c))
+                if extra:
+                    hdr[0], hdr_len[0] = self._hold(extra), len(extra)
+                return 0
+            except Exception as e:  # noqa: BLE001
+                return self._reject(rej, e)
+        return _abi.HOOK_ON_BEFORE_UPGRADE(cb)
+
+    def upgrade(self, c: "Connection", buffer: "RingBuffer") -> Tuple[bytes, HandshakeInfo, Optional[HandshakeError]]:
+        """Upgrade(c, in) -> (out, hs, err) (ws.go:158-343)."""
+        self._keep.clear()
+        out = _abi.U8P()
+        n = ctypes.c_uint64()
+        hs = _abi.Handshake()
+        st = lib.gevws_upgrader_upgrade(self._p, c._p, buffer._p, ctypes.byref(out), ctypes.byref(n),
+                                        ctypes.byref(hs))
+        if st not in (OK, ERR_HANDSHAKE):
+            raise RuntimeError(f"upgrade: {status_string(st)}")
+        info = HandshakeInfo._from(hs)
+        data = ctypes.string_at(out, n.value) if n.value else b""
+        err = None if st == OK else HandshakeError(info.error, info.reason, info.http_code)
+        return data, info, err
+
+
 class Protocol:
     """websocket.Protocol (plugins/websocket/protocol.go:16-69) over the device engine."""
 
-    def __init__(self, engine: Engine):
+    def __init__(self, engine: Engine, upgrader: Optional[Upgrader] = None):
         self.engine = engine
         self._p = lib.gevws_protocol_new(engine._ctx)
+        self.upgrader = upgrader
+        if upgrader is not None:
+            lib.gevws_protocol_set_upgrader(self._p, upgrader._p)
 
-    def __del__(self):
+    def __del__(self, _free=lib.gevws_protocol_free):  # bound now: module globals are gone at exit
         if getattr(self, "_p", None):
-            lib.gevws_protocol_free(self._p)
+            _free(self._p)
             self._p = None
 
     def unpacket(self, c: Connection, buffer: RingBuffer) -> Tuple[Optional[Header], Optional[bytes]]:
-        """UnPacket(c, buffer) -> (ctx, out): one frame, or (None, None)."""
+        """UnPacket(c, buffer) -> (ctx, out): one frame; (None, response) for
+        the handshake (protocol.go:29-37); or (None, None)."""
+        if self.upgrader is not None:
+            self.upgrader._keep.clear()
         h = Header()
         out = _abi.U8P()
         n = ctypes.c_uint64()
         st = lib.gevws_protocol_unpacket(self._p, c._p, buffer._p, ctypes.byref(h), ctypes.byref(out),
                                          ctypes.byref(n))
         self.last_status = st
+        if st in (HANDSHAKE, ERR_HANDSHAKE):
+            return None, (ctypes.string_at(out, n.value) if n.value else None)
         if st != OK:
             return None, None
         return h, (ctypes.string_at(out, n.value) if n.value else b"")
@@ -411,6 +621,7 @@ def handler_protocol(protocol: Protocol, c: Connection, buffer: RingBuffer,
 
 
 __all__ = ["Engine", "Batch", "RingBuffer", "Connection", "Protocol", "Header", "handler_protocol",
+           "Upgrader", "RejectError", "HandshakeError", "HandshakeInfo", "accept_key", "HANDSHAKE", "ERR_HANDSHAKE",
            "status_string", "device_count", "lib", "FRAME_DTYPE", "CONN_OUT_DTYPE", "SUMMARY_DTYPE",
            "SYNTH_DTYPE", "OUT_FRAME_DTYPE", "OK", "NEED_MORE", "ERR_LEN_MSB", "ERR_CAPACITY", "ERR_INVALID", "ERR_DEVICE",
            "ERR_NOT_UPGRADED", "IN_PAD", "PAYLOAD_ALIGN", "TILE"]

@@ -19,6 +19,22 @@ ERR_CAPACITY = -2
 ERR_INVALID = -3
 ERR_DEVICE = -4
 ERR_NOT_UPGRADED = -5
+HANDSHAKE = 2
+ERR_HANDSHAKE = -6
+
+# handshake error kinds (GEVWS_HS_*)
+HS_OK = 0
+HS_MALFORMED_REQUEST = 1
+HS_BAD_PROTOCOL = 2
+HS_BAD_METHOD = 3
+HS_BAD_HOST = 4
+HS_BAD_UPGRADE = 5
+HS_BAD_CONNECTION = 6
+HS_BAD_SEC_ACCEPT = 7
+HS_BAD_SEC_KEY = 8
+HS_BAD_SEC_VERSION = 9
+HS_UPGRADE_REQUIRED = 10
+HS_HOOK = 11
 
 OUT_PAD = 16
 AUX_SLOT = 128
@@ -77,6 +93,47 @@ class SynthDesc(ctypes.Structure):
                 ("pad", ctypes.c_uint8)]
 
 
+class Reject(ctypes.Structure):
+    """gevws_reject: RejectConnectionError options (ws/errors.go:81-129)."""
+    _fields_ = [("code", ctypes.c_int32), ("plain", ctypes.c_int32), ("reason", ctypes.c_void_p),
+                ("reason_len", ctypes.c_uint64), ("header", ctypes.c_void_p), ("header_len", ctypes.c_uint64)]
+
+
+class ExtParam(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_void_p), ("key_len", ctypes.c_uint64), ("value", ctypes.c_void_p),
+                ("value_len", ctypes.c_uint64)]
+
+
+_VP, _U64 = ctypes.c_void_p, ctypes.c_uint64
+_PU64 = ctypes.POINTER(ctypes.c_uint64)
+_PVP = ctypes.POINTER(ctypes.c_void_p)
+_PREJ = ctypes.POINTER(Reject)
+HOOK_PROTOCOL = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _U64)
+HOOK_PROTOCOL_CUSTOM = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _VP, _U64, _PVP, _PU64)
+HOOK_EXTENSION = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _U64, ctypes.POINTER(ExtParam), ctypes.c_uint32)
+HOOK_EXTENSION_CUSTOM = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _VP, _U64, _VP, _U64, _PVP, _PU64)
+HOOK_ON_VALUE = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _VP, _U64, _PREJ)
+HOOK_ON_HEADER = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _VP, _U64, _VP, _U64, _PREJ)
+HOOK_ON_BEFORE_UPGRADE = ctypes.CFUNCTYPE(ctypes.c_int, _VP, _VP, _PVP, _PU64, _PREJ)
+
+
+class UpgraderHooks(ctypes.Structure):
+    """gevws_upgrader_hooks: ws.Upgrader's function fields (ws/ws.go:51-153)."""
+    _fields_ = [("user", ctypes.c_void_p), ("protocol", HOOK_PROTOCOL),
+                ("protocol_custom", HOOK_PROTOCOL_CUSTOM), ("extension", HOOK_EXTENSION),
+                ("extension_custom", HOOK_EXTENSION_CUSTOM), ("on_request", HOOK_ON_VALUE),
+                ("on_host", HOOK_ON_VALUE), ("on_header", HOOK_ON_HEADER),
+                ("on_before_upgrade", HOOK_ON_BEFORE_UPGRADE)]
+
+
+class Handshake(ctypes.Structure):
+    """gevws_handshake: ws.Handshake (ws/ws.go:40-47) + error."""
+    _fields_ = [("protocol", ctypes.c_void_p), ("protocol_len", ctypes.c_uint64),
+                ("extensions", ctypes.c_void_p), ("extensions_len", ctypes.c_uint64),
+                ("error", ctypes.c_int32), ("http_code", ctypes.c_int32), ("reason", ctypes.c_char_p)]
+
+
+assert ctypes.sizeof(Reject) == 40 and ctypes.sizeof(UpgraderHooks) == 72 and ctypes.sizeof(Handshake) == 48
 assert ctypes.sizeof(Header) == 16 and ctypes.sizeof(Frame) == 32
 assert ctypes.sizeof(ConnIn) == 16 and ctypes.sizeof(ConnOut) == 32
 assert ctypes.sizeof(Summary) == 64 and ctypes.sizeof(SynthDesc) == 24
@@ -127,6 +184,16 @@ SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_uint64)]),
     "gevws_protocol_unpacket_batch": (ctypes.c_int64, [P, P, P, ctypes.c_uint32]),
     "gevws_protocol_packet": (U8P, [P, P, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    "gevws_upgrader_new": (P, []),
+    "gevws_upgrader_free": (None, [P]),
+    "gevws_upgrader_set_header": (None, [P, P, ctypes.c_uint64]),
+    "gevws_upgrader_set_hooks": (None, [P, ctypes.POINTER(UpgraderHooks)]),
+    "gevws_upgrader_upgrade": (ctypes.c_int, [P, P, P, ctypes.POINTER(U8P), ctypes.POINTER(ctypes.c_uint64),
+                                              ctypes.POINTER(Handshake)]),
+    "gevws_conn_handshake": (ctypes.c_int, [P, ctypes.POINTER(Handshake)]),
+    "gevws_handshake_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "gevws_accept_key": (None, [P, P]),
+    "gevws_protocol_set_upgrader": (None, [P, P]),
     "gevws_decode_host_stream": (ctypes.c_int64, [P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.c_uint64,
                                                   P, ctypes.c_uint64, P, ctypes.POINTER(Summary)]),
     "gevws_decode_host_batch": (ctypes.c_int64, [P, P, ctypes.c_uint32, P, ctypes.c_uint64, P, ctypes.c_uint64,

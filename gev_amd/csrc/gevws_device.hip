@@ -1389,7 +1389,9 @@ const char* gevws_status_string(int s) {
     case GEVWS_ERR_CAPACITY: return "output capacity exceeded";
     case GEVWS_ERR_INVALID: return "invalid argument";
     case GEVWS_ERR_DEVICE: return "HIP device error";
-    case GEVWS_ERR_NOT_UPGRADED: return "websocket upgrade (handshake) not supported by this engine";
+    case GEVWS_HANDSHAKE: return "handshake response";
+    case GEVWS_ERR_NOT_UPGRADED: return "connection not upgraded and the protocol has no upgrader";
+    case GEVWS_ERR_HANDSHAKE: return "websocket upgrade failed";
     default: return "unknown status";
   }
 }

@@ -12,7 +12,8 @@
 //   Protocol    ~ websocket.Protocol (plugins/websocket/protocol.go:16-69):
 //                 UnPacket returns one frame per call exactly like the
 //                 reference; its decode runs on the device, batched across
-//                 every connection handed to UnPacketBatch.
+//                 every connection handed to UnPacketBatch.  Before the
+//                 upgrade it runs the HTTP handshake (handshake.cpp, host).
 //
 // The decode itself is never done on the host: this file only stages bytes,
 // launches gevws_decode_batch and hands out the device's results.
@@ -27,6 +28,7 @@
 #include <vector>
 
 #include "gevws.h"
+#include "handshake.hpp"
 #include "ringbuffer.hpp"
 
 namespace gevws {
@@ -47,6 +49,9 @@ static bool log_errors_enabled() {
 static void log_error(const char* what, int status) {
   if (log_errors_enabled()) fprintf(stderr, "[Gev] ERROR %s%s\n", what, gevws_status_string(status));
 }
+static void log_error_text(const char* what, const std::string& text) {
+  if (log_errors_enabled()) fprintf(stderr, "[Gev] ERROR %s%s\n", what, text.c_str());
+}
 
 // ------------------------------------------------------------------ connection
 struct Delivered {
@@ -61,21 +66,34 @@ struct Connection {
   int poisoned = GEVWS_OK;               // sticky ERR_LEN_MSB (Appendix A P9/U3)
   std::deque<Delivered> queue;           // decoded, not yet returned by UnPacket
   std::shared_ptr<std::vector<uint8_t>> current;  // keeps the last payload alive
+  HandshakeResult hs;                    // last Upgrade's response + Handshake
 };
 
 // ------------------------------------------------------------------ protocol
 class Protocol {
  public:
   explicit Protocol(gevws_ctx* ctx) : ctx_(ctx) {}
+  void SetUpgrader(const Upgrader* u) { upgrader_ = u; }
   ~Protocol() { release(); }
 
   int UnPacket(Connection* c, RingBuffer* ring, gevws_header* hdr, const uint8_t** out,
                uint64_t* out_len) {
     *out = nullptr;
     *out_len = 0;
-    if (!c->upgraded) {  // protocol.go:28-35: the handshake path
-      log_error("Websocket Upgrade :", GEVWS_ERR_NOT_UPGRADED);
-      return GEVWS_ERR_NOT_UPGRADED;
+    if (!c->upgraded) {  // protocol.go:28-37: the handshake path
+      if (!upgrader_) {
+        log_error("Websocket Upgrade :", GEVWS_ERR_NOT_UPGRADED);
+        return GEVWS_ERR_NOT_UPGRADED;
+      }
+      upgrader_->Upgrade(static_cast<gevws_conn*>(static_cast<void*>(c)), ring, &c->hs);
+      *out = c->hs.out.empty() ? nullptr : (const uint8_t*)c->hs.out.data();
+      *out_len = c->hs.out.size();
+      if (c->hs.error != GEVWS_HS_OK) {  // (nil, error response or nil), logged
+        log_error_text("Websocket Upgrade :", c->hs.reason);
+        return GEVWS_ERR_HANDSHAKE;
+      }
+      c->upgraded = true;
+      return GEVWS_HANDSHAKE;
     }
     if (c->queue.empty() && c->poisoned == GEVWS_OK) {
       Connection* cs[1] = {c};
@@ -270,6 +288,7 @@ class Protocol {
   }
 
   gevws_ctx* ctx_;
+  const Upgrader* upgrader_ = nullptr;
   uint8_t* h_in_ = nullptr;
   uint64_t h_in_cap_ = 0;
   void *d_in_ = nullptr, *d_conns_ = nullptr, *d_cout_ = nullptr, *d_frames_ = nullptr, *d_payload_ = nullptr;
@@ -282,6 +301,7 @@ struct gevws_ring : gevws::RingBuffer {
   using gevws::RingBuffer::RingBuffer;
 };
 struct gevws_conn : gevws::Connection {};
+struct gevws_upgrader : gevws::Upgrader {};
 struct gevws_protocol : gevws::Protocol {
   using gevws::Protocol::Protocol;
 };
@@ -338,6 +358,68 @@ int64_t gevws_decode_host_stream(gevws_protocol* p, const uint8_t* seg0, uint64_
                                  uint64_t payload_cap, gevws_conn_out* conn_out, gevws_summary* summary) {
   const gevws_host_conn hc = {seg0, n0, seg1, n1};
   return gevws_decode_host_batch(p, &hc, 1, frames, max_frames, payload, payload_cap, conn_out, summary);
+}
+
+gevws_upgrader* gevws_upgrader_new(void) { return new gevws_upgrader(); }
+void gevws_upgrader_free(gevws_upgrader* u) { delete u; }
+void gevws_upgrader_set_header(gevws_upgrader* u, const uint8_t* hdr, uint64_t n) {
+  if (u) u->header = hdr ? std::string((const char*)hdr, n) : std::string();
+}
+void gevws_upgrader_set_hooks(gevws_upgrader* u, const gevws_upgrader_hooks* hooks) {
+  if (u) u->hooks = hooks ? *hooks : gevws_upgrader_hooks{};
+}
+
+static void fill_handshake(const gevws::HandshakeResult& r, gevws_handshake* hs) {
+  hs->protocol = (const uint8_t*)r.protocol.data();
+  hs->protocol_len = r.protocol.size();
+  hs->extensions = (const uint8_t*)r.extensions.data();
+  hs->extensions_len = r.extensions.size();
+  hs->error = r.error;
+  hs->http_code = r.http_code;
+  hs->reason = r.reason.c_str();
+}
+
+int gevws_upgrader_upgrade(const gevws_upgrader* u, gevws_conn* c, gevws_ring* in, const uint8_t** out,
+                           uint64_t* out_len, gevws_handshake* hs) {
+  if (!u || !c || !in || !out || !out_len) return GEVWS_ERR_INVALID;
+  u->Upgrade(c, in, &c->hs);
+  *out = c->hs.out.empty() ? nullptr : (const uint8_t*)c->hs.out.data();
+  *out_len = c->hs.out.size();
+  if (hs) fill_handshake(c->hs, hs);
+  return c->hs.error == GEVWS_HS_OK ? GEVWS_OK : GEVWS_ERR_HANDSHAKE;
+}
+
+int gevws_conn_handshake(const gevws_conn* c, gevws_handshake* hs) {
+  if (!c || !hs) return GEVWS_ERR_INVALID;
+  fill_handshake(c->hs, hs);
+  return GEVWS_OK;
+}
+
+const char* gevws_handshake_error_string(int e) {
+  switch (e) {
+    case GEVWS_HS_OK: return "";
+    case GEVWS_HS_MALFORMED_REQUEST: return "malformed HTTP request";
+    case GEVWS_HS_BAD_PROTOCOL: return "handshake error: bad HTTP protocol version";
+    case GEVWS_HS_BAD_METHOD: return "handshake error: bad HTTP request method";
+    case GEVWS_HS_BAD_HOST: return "handshake error: bad \"Host\" header";
+    case GEVWS_HS_BAD_UPGRADE: return "handshake error: bad \"Upgrade\" header";
+    case GEVWS_HS_BAD_CONNECTION: return "handshake error: bad \"Connection\" header";
+    case GEVWS_HS_BAD_SEC_ACCEPT: return "handshake error: bad \"Sec-WebSocket-Accept\" header";
+    case GEVWS_HS_BAD_SEC_KEY: return "handshake error: bad \"Sec-WebSocket-Key\" header";
+    case GEVWS_HS_BAD_SEC_VERSION:
+    case GEVWS_HS_UPGRADE_REQUIRED: return "handshake error: bad \"Sec-WebSocket-Version\" header";
+    case GEVWS_HS_HOOK: return "rejected by an Upgrader hook";
+    default: return "unknown handshake error";
+  }
+}
+
+void gevws_accept_key(const uint8_t nonce[24], char accept[28]) {
+  const std::string a = gevws::AcceptFromNonce(nonce);
+  memcpy(accept, a.data(), 28);
+}
+
+void gevws_protocol_set_upgrader(gevws_protocol* p, const gevws_upgrader* u) {
+  if (p) p->SetUpgrader(u);
 }
 
 const uint8_t* gevws_protocol_packet(gevws_protocol* p, gevws_conn* c, const uint8_t* data, uint64_t n,

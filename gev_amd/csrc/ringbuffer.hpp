@@ -1,7 +1,7 @@
 // ringbuffer.hpp -- growable circular byte buffer, the part of
 // github.com/Allenxuxu/ringbuffer v0.0.11 (go.mod:7) that gev's read path and
 // the websocket plugin use: Write (connection.go:241-244), Length, PeekAll
-// (connection.go:237-240, ws.go:176-192), Retrieve (consumption of a decoded
+// (connection.go:237-240, ws.go:176-192), Read (ws.go:180), Retrieve (consumption of a decoded
 // frame, protocol.go:48-51).  The un-vendored library's virtual-cursor calls
 // (read.go:20,27,63; protocol.go:47-60) are replaced by the device header walk.
 // Host-only C++ (no HIP): fuzzed under ASan/UBSan by tests/cpp/ring_fuzz.cpp.
@@ -52,6 +52,19 @@ class RingBuffer {
       *end = buf_.data();
       *n2 = w_;
     }
+  }
+
+  // Read(p): copies min(n, Length()) bytes from the front and consumes them
+  // (ws.go:180, 186; protocol.go:51).
+  uint64_t Read(uint8_t* p, uint64_t n) {
+    const uint8_t *a, *b;
+    uint64_t na, nb;
+    PeekAll(&a, &na, &b, &nb);
+    const uint64_t c1 = std::min(n, na), c2 = std::min(n - c1, nb);
+    if (c1) memcpy(p, a, c1);
+    if (c2) memcpy(p + c1, b, c2);
+    Retrieve(c1 + c2);
+    return c1 + c2;
   }
 
   void Retrieve(uint64_t n) {

@@ -38,8 +38,13 @@ enum {
                                      the summary holds the exact sizes needed */
     GEVWS_ERR_INVALID = -3,       /* bad argument */
     GEVWS_ERR_DEVICE = -4,        /* HIP runtime error */
-    GEVWS_ERR_NOT_UPGRADED = -5   /* UnPacket before the handshake (protocol.go:28-37);
-                                     the handshake is out of scope, see DESIGN.md */
+    GEVWS_HANDSHAKE = 2,          /* (nil, out): UnPacket ran the upgrade and `out`
+                                     holds the 101 response (protocol.go:29-37) */
+    GEVWS_ERR_NOT_UPGRADED = -5,  /* UnPacket before the handshake on a protocol
+                                     that has no upgrader (gevws_protocol_set_upgrader) */
+    GEVWS_ERR_HANDSHAKE = -6      /* Upgrader.Upgrade failed (ws.go:158-343); `out`
+                                     may hold the error response, which the caller
+                                     sends, as protocol.go:31-34 returns (nil, out) */
 };
 
 /* Readable slack the caller must provide after the last byte of a device input
@@ -276,7 +281,12 @@ void gevws_protocol_free(gevws_protocol *p);
  * h + L bytes consumed from `ring`.  GEVWS_NEED_MORE: (nil, nil), nothing
  * consumed.  < 0: logged and (nil, nil), as protocol.go:32-34, 41-45.  When the
  * connection has no queued frames the call decodes its buffered bytes on the
- * device first. */
+ * device first.  On a connection not yet upgraded it runs the handshake
+ * (protocol.go:28-37; needs gevws_protocol_set_upgrader): GEVWS_HANDSHAKE with
+ * (*out, *out_len) = the 101 response, or GEVWS_ERR_HANDSHAKE with the error
+ * response (possibly empty) -- the driver loop (connection.go:208-218) keeps
+ * calling while the status is GEVWS_OK or *out_len != 0, sending every `out`
+ * that is not a frame payload. */
 int gevws_protocol_unpacket(gevws_protocol *p, gevws_conn *c, gevws_ring *ring,
                             gevws_header *ctx_out, const uint8_t **out, uint64_t *out_len);
 
@@ -314,6 +324,109 @@ int64_t gevws_decode_host_stream(gevws_protocol *p, const uint8_t *seg0, uint64_
                                  const uint8_t *seg1, uint64_t n1, gevws_frame *frames,
                                  uint64_t max_frames, uint8_t *payload, uint64_t payload_cap,
                                  gevws_conn_out *conn_out, gevws_summary *summary);
+
+/* ---------------------------------------------------------------- handshake
+ * ws.Upgrader (plugins/websocket/ws/ws.go:49-154) and Upgrader.Upgrade
+ * (ws.go:158-343) with its HTTP helpers (http.go, nonce.go, util.go) -- host
+ * code, once per connection. */
+enum {
+    GEVWS_HS_OK = 0,
+    GEVWS_HS_MALFORMED_REQUEST = 1, /* ErrMalformedRequest (errors.go:60-64); also the
+                                       head not yet complete (ws.go:176-198: nothing read) */
+    GEVWS_HS_BAD_PROTOCOL = 2,      /* ErrHandshakeBadProtocol (errors.go:26-29) */
+    GEVWS_HS_BAD_METHOD = 3,        /* ErrHandshakeBadMethod (errors.go:30-33) */
+    GEVWS_HS_BAD_HOST = 4,          /* errors.go:34-37 */
+    GEVWS_HS_BAD_UPGRADE = 5,       /* errors.go:38-41 */
+    GEVWS_HS_BAD_CONNECTION = 6,    /* errors.go:42-45 */
+    GEVWS_HS_BAD_SEC_ACCEPT = 7,    /* errors.go:46-49 (client side; never produced here) */
+    GEVWS_HS_BAD_SEC_KEY = 8,       /* errors.go:50-53 */
+    GEVWS_HS_BAD_SEC_VERSION = 9,   /* errors.go:54-57 */
+    GEVWS_HS_UPGRADE_REQUIRED = 10, /* ErrHandshakeUpgradeRequired (errors.go:66-79): 426 */
+    GEVWS_HS_HOOK = 11              /* an Upgrader hook returned an error */
+};
+
+/* What a hook returns with a non-zero result: RejectConnectionError(
+ * RejectionStatus(code), RejectionReason(reason), RejectionHeader(header))
+ * (errors.go:81-129), or with plain = 1 an ordinary Go error whose Error() is
+ * `reason` (answered 500 without extra header, ws.go:325-333). */
+typedef struct gevws_reject {
+    int32_t code;            /* 0 -> 500 (ws.go:331-333) */
+    int32_t plain;
+    const char *reason;
+    uint64_t reason_len;
+    const uint8_t *header;   /* raw "Key: value\r\n" lines */
+    uint64_t header_len;
+} gevws_reject;
+
+/* One parameter of a Sec-WebSocket-Extensions option (httphead.Option). */
+typedef struct gevws_ext_param {
+    const uint8_t *key;
+    uint64_t key_len;
+    const uint8_t *value;    /* NULL when the parameter has no value */
+    uint64_t value_len;
+} gevws_ext_param;
+
+/* The Upgrader's function fields (ws.go:51-153); any may be NULL.  Every
+ * argument is valid only until the hook returns.  Hooks returning int: 0 =
+ * accept, non-zero = reject with *rej filled (strings copied before return). */
+typedef struct gevws_upgrader_hooks {
+    void *user;
+    /* Protocol (ws.go:51-56): non-zero selects the offered token. */
+    int (*protocol)(void *user, const uint8_t *token, uint64_t n);
+    /* ProtocolCustom (ws.go:58-61): returns ok; *sel = the selected protocol. */
+    int (*protocol_custom)(void *user, gevws_conn *c, const uint8_t *value, uint64_t n,
+                           const uint8_t **sel, uint64_t *sel_n);
+    /* Extension (ws.go:63-79): non-zero accepts the option. */
+    int (*extension)(void *user, const uint8_t *name, uint64_t n, const gevws_ext_param *params,
+                     uint32_t n_params);
+    /* ExtensionCustom (ws.go:81-84): the header value and the extensions selected
+     * so far (response text form) -> ok, *sel = the new selection's text. */
+    int (*extension_custom)(void *user, gevws_conn *c, const uint8_t *value, uint64_t n,
+                            const uint8_t *cur, uint64_t cur_n, const uint8_t **sel, uint64_t *sel_n);
+    /* OnRequest (ws.go:97-106), OnHost (ws.go:108-121), OnHeader (ws.go:123-133). */
+    int (*on_request)(void *user, gevws_conn *c, const uint8_t *uri, uint64_t n, gevws_reject *rej);
+    int (*on_host)(void *user, gevws_conn *c, const uint8_t *host, uint64_t n, gevws_reject *rej);
+    int (*on_header)(void *user, gevws_conn *c, const uint8_t *key, uint64_t kn, const uint8_t *value,
+                     uint64_t vn, gevws_reject *rej);
+    /* OnBeforeUpgrade (ws.go:135-153): 0 and optionally extra response header
+     * lines in (*hdr, *hdr_len), or non-zero + *rej. */
+    int (*on_before_upgrade)(void *user, gevws_conn *c, const uint8_t **hdr, uint64_t *hdr_len,
+                             gevws_reject *rej);
+} gevws_upgrader_hooks;
+
+/* Upgrade's result: ws.Handshake (ws.go:40-47) plus the error.  Pointers are
+ * owned by the connection and valid until its next handshake call. */
+typedef struct gevws_handshake {
+    const uint8_t *protocol;
+    uint64_t protocol_len;
+    const uint8_t *extensions;   /* as written in Sec-WebSocket-Extensions */
+    uint64_t extensions_len;
+    int32_t error;               /* GEVWS_HS_* */
+    int32_t http_code;           /* 101, the error response status, or 0: nothing written */
+    const char *reason;          /* err.Error(); "" on success */
+} gevws_handshake;
+
+typedef struct gevws_upgrader gevws_upgrader;
+
+/* &ws.Upgrader{} -- immutable once configured, so one upgrader may serve every loop. */
+gevws_upgrader *gevws_upgrader_new(void);
+void gevws_upgrader_free(gevws_upgrader *u);
+/* Upgrader.Header (ws.go:88-95) as raw header lines. */
+void gevws_upgrader_set_header(gevws_upgrader *u, const uint8_t *hdr, uint64_t n);
+void gevws_upgrader_set_hooks(gevws_upgrader *u, const gevws_upgrader_hooks *hooks);
+/* Upgrader.Upgrade(c, in) (ws.go:158-343): consumes the request head from `in`
+ * once it is complete; (*out, *out_len) = the 101 or error response (owned by
+ * `c`; empty when the reference writes none).  GEVWS_OK or GEVWS_ERR_HANDSHAKE. */
+int gevws_upgrader_upgrade(const gevws_upgrader *u, gevws_conn *c, gevws_ring *in, const uint8_t **out,
+                           uint64_t *out_len, gevws_handshake *hs);
+/* The connection's last handshake result (after UnPacket ran the upgrade). */
+int gevws_conn_handshake(const gevws_conn *c, gevws_handshake *hs);
+const char *gevws_handshake_error_string(int hs_error);
+/* initAcceptFromNonce (nonce.go:23-39): 24-byte key -> 28-byte Sec-WebSocket-Accept. */
+void gevws_accept_key(const uint8_t nonce[24], char accept[28]);
+/* websocket.New(u) (protocol.go:22-24): UnPacket on a connection that is not
+ * upgraded runs the handshake (protocol.go:28-37). */
+void gevws_protocol_set_upgrader(gevws_protocol *p, const gevws_upgrader *u);
 
 /* websocket.(*Protocol).Packet (protocol.go:67-69): identity. */
 const uint8_t *gevws_protocol_packet(gevws_protocol *p, gevws_conn *c, const uint8_t *data,

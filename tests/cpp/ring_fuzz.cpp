@@ -20,6 +20,13 @@ int main(int argc, char** argv) {
         for (auto& b : d) b = (uint8_t)rng();
         r.Write(d.data(), d.size());
         model.insert(model.end(), d.begin(), d.end());
+      } else if (rng() % 4 == 0) {
+        std::vector<uint8_t> got(rng() % 300);
+        const uint64_t k = r.Read(got.data(), got.size());
+        if (k != std::min<uint64_t>(got.size(), model.size())) return 5;
+        for (uint64_t i = 0; i < k; ++i)
+          if (got[i] != model[i]) return 6;
+        model.erase(model.begin(), model.begin() + k);
       } else {
         const uint64_t k = rng() % 400;
         r.Retrieve(k);

@@ -174,3 +174,66 @@ def test_decode_host_stream_single_connection(engine):
     for f, fr in zip(frames[:n], want.frames):
         o = int(f["payload_off"])
         assert f.tobytes()[:16] == fr.header.pack() and payload[o:o + fr.header.length].tobytes() == fr.payload
+
+
+XNET_REQUEST = (b"GET / HTTP/1.1\r\nHost: localhost:1834\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+                b"Sec-WebSocket-Key: x3JJHMbDL1EzLkh9GBhXDw==\r\nOrigin: ws://localhost:1834\r\n"
+                b"Sec-WebSocket-Version: 13\r\n\r\n")
+
+
+def _wrap_on_message(got):
+    """HandlerWrap.OnMessage (wrap.go:38-44): a (nil, out) from UnPacket is the
+    handshake response and is sent back as-is; frames are echoed."""
+    def on_message(c, hdr, data):
+        if hdr is None:
+            return data
+        got.append(data)
+        return data
+    return on_message
+
+
+def test_handshake_then_frames_in_chunks(engine):
+    """protocol.go:27-37 end to end: the upgrade request and the first frames
+    arrive together, in small read(2) chunks; the 101 response is the first
+    reply, then every frame is decoded on the device and echoed."""
+    from oracle import ws_handshake as wh
+    rng = np.random.default_rng(33)
+    proto = gev_amd.Protocol(engine, gev_amd.Upgrader())
+    c = gev_amd.Connection(upgraded=False)
+    r = gev_amd.RingBuffer(64)
+    sent = _client_frames(rng, 12)
+    wire = XNET_REQUEST + b"".join(w for _, w in sent)
+    got, replies, pos = [], [], 0
+    on_message = _wrap_on_message(got)
+    while pos < len(wire):
+        n = int(rng.integers(1, 700))
+        r.write(wire[pos:pos + n])
+        pos += n
+        replies += gev_amd.handler_protocol(proto, c, r, on_message)
+    want_101 = wh.upgrade(XNET_REQUEST, b"").out
+    assert replies[0] == want_101 and c.upgraded
+    assert c.handshake().http_code == 101
+    assert got == [d for d, _ in sent] and replies[1:] == got
+    assert r.length() == 0
+
+
+def test_handshake_rejected_then_retried(engine):
+    """A bad request is answered with the error response and the connection
+    stays un-upgraded (protocol.go:31-34 returns (nil, out)); a later good
+    request upgrades it."""
+    from oracle import ws_handshake as wh
+    proto = gev_amd.Protocol(engine, gev_amd.Upgrader())
+    c = gev_amd.Connection(upgraded=False)
+    r = gev_amd.RingBuffer(256)
+    bad = XNET_REQUEST.replace(b"Sec-WebSocket-Version: 13", b"Sec-WebSocket-Version: 8")
+    replies = gev_amd.handler_protocol(proto, c, r, _wrap_on_message([]))
+    assert replies == [] and proto.last_status == gev_amd.ERR_HANDSHAKE   # empty ring: malformed, silent
+    r.write(bad)
+    replies = gev_amd.handler_protocol(proto, c, r, _wrap_on_message([]))
+    assert replies == [wh.upgrade(bad, b"").out] and not c.upgraded and r.length() == 0
+    assert c.handshake().http_code == 426
+    frame = wo.encode_frame(b"hello", wo.OP_TEXT, True, 0, True, b"\x01\x02\x03\x04")
+    r.write(XNET_REQUEST + frame)
+    got = []
+    replies = gev_amd.handler_protocol(proto, c, r, _wrap_on_message(got))
+    assert c.upgraded and got == [b"hello"] and replies[1:] == [b"hello"]

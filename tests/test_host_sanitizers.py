@@ -1,6 +1,7 @@
 """Host code under AddressSanitizer + UndefinedBehaviorSanitizer (CPU only):
 the ring buffer of the C++ host mirror fuzzed against a std::deque model, and
-the C oracle's decode on random hostile byte streams (race /
+the C oracle's decode on random hostile byte streams, and the HTTP upgrade
+(gev_amd/csrc/handshake.cpp) on mutated requests (race /
 sanitizer coverage is host-side; GPU ASan is not available on this pool)."""
 import os
 import shutil
@@ -35,3 +36,14 @@ def test_oracle_decode_fuzz_asan_ubsan(tmp_path):
     assert r.returncode == 0, r.stderr
     r = _run([str(exe)], env={**os.environ, "ASAN_OPTIONS": "detect_leaks=1"})
     assert r.returncode == 0 and "oracle_fuzz ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+def test_handshake_fuzz_asan_ubsan(tmp_path):
+    exe = tmp_path / "handshake_fuzz"
+    r = _run(["g++", "-std=c++17", *SAN, "-I", os.path.join(ROOT, "include"),
+              os.path.join(ROOT, "tests", "cpp", "handshake_fuzz.cpp"),
+              os.path.join(ROOT, "gev_amd", "csrc", "handshake.cpp"), "-o", str(exe)])
+    assert r.returncode == 0, r.stderr
+    r = _run([str(exe)], env={**os.environ, "ASAN_OPTIONS": "detect_leaks=1"})
+    assert r.returncode == 0 and "handshake_fuzz ok" in r.stdout, r.stdout + r.stderr
