@@ -67,6 +67,7 @@ struct Connection {
   std::deque<Delivered> queue;           // decoded, not yet returned by UnPacket
   std::shared_ptr<std::vector<uint8_t>> current;  // keeps the last payload alive
   HandshakeResult hs;                    // last Upgrade's response + Handshake
+  uint64_t tail_len = ~0ull;             // undecodable ring bytes after the last device pass
 };
 
 // ------------------------------------------------------------------ protocol
@@ -95,7 +96,7 @@ class Protocol {
       c->upgraded = true;
       return GEVWS_HANDSHAKE;
     }
-    if (c->queue.empty() && c->poisoned == GEVWS_OK) {
+    if (c->queue.empty() && c->poisoned == GEVWS_OK && ring->Length() != c->tail_len) {
       Connection* cs[1] = {c};
       RingBuffer* rs[1] = {ring};
       int64_t r = UnPacketBatch(cs, rs, 1);
@@ -128,6 +129,7 @@ class Protocol {
     for (uint32_t i = 0; i < n; ++i) {
       if (!conns[i]->upgraded || !conns[i]->queue.empty() || conns[i]->poisoned != GEVWS_OK) continue;
       if (rings[i]->Length() < 6) continue;  // read.go:20-23: nothing can be decoded
+      if (rings[i]->Length() == conns[i]->tail_len) continue;  // no new bytes since the last pass
       gevws_host_conn h;
       rings[i]->PeekAll(&h.seg0, &h.n0, &h.seg1, &h.n1);
       sel.push_back(i);
@@ -154,6 +156,7 @@ class Protocol {
     for (uint32_t j = 0; j < m; ++j) {
       Connection* c = conns[sel[j]];
       const gevws_conn_out& o = cout[j];
+      c->tail_len = cin[j].len - o.consumed;
       uint64_t prev_end = cin[j].off;
       for (uint32_t k = 0; k < o.nframes; ++k) {
         const gevws_frame& f = fr[o.first_frame + k];

@@ -231,7 +231,9 @@ def test_handshake_rejected_then_retried(engine):
     r.write(bad)
     replies = gev_amd.handler_protocol(proto, c, r, _wrap_on_message([]))
     assert replies == [wh.upgrade(bad, b"").out] and not c.upgraded and r.length() == 0
-    assert c.handshake().http_code == 426
+    assert replies[0].startswith(b"HTTP/1.1 426 Upgrade Required\r\n")
+    # the loop's last UnPacket ran the upgrade on the now empty ring: (nil, nil)
+    assert c.handshake().error == gev_amd._abi.HS_MALFORMED_REQUEST
     frame = wo.encode_frame(b"hello", wo.OP_TEXT, True, 0, True, b"\x01\x02\x03\x04")
     r.write(XNET_REQUEST + frame)
     got = []
