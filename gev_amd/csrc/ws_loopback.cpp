@@ -29,6 +29,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -49,7 +50,7 @@
 namespace {
 
 std::atomic<bool> g_stop{false};
-std::atomic<uint64_t> g_batches{0}, g_batch_conns{0}, g_frames{0}, g_bad{0};
+std::atomic<uint64_t> g_batches{0}, g_batch_conns{0}, g_frames{0}, g_bad{0}, g_dev_ns{0};
 
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -177,7 +178,9 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
         br.push_back(s->r);
       }
     if (!bc.empty()) {
+      const double td = now_s();
       const int64_t f = gevws_protocol_unpacket_batch(p, bc.data(), br.data(), (uint32_t)bc.size());
+      g_dev_ns.fetch_add((uint64_t)((now_s() - td) * 1e9), std::memory_order_relaxed);
       if (f < 0) {
         fprintf(stderr, "ws_loopback: unpacket_batch %s\n", gevws_status_string((int)f));
         exit(3);
@@ -257,13 +260,17 @@ void client_thread(int port, int nconn, size_t msg, double t_end, std::atomic<ui
   const int rn = snprintf(req, sizeof(req), req_fmt, port);
   for (int i = 0; i < nconn; ++i) {
     int fd = socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) {
+      perror("ws_loopback: socket");
+      _exit(2);
+    }
     sockaddr_in a{};
     a.sin_family = AF_INET;
     a.sin_port = htons((uint16_t)port);
     a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
     if (connect(fd, (sockaddr*)&a, sizeof(a))) {
       perror("ws_loopback: connect");
-      exit(2);
+      _exit(2);  // other threads are running: no static destructors
     }
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
@@ -335,6 +342,16 @@ int main(int argc, char** argv) {
     else if (k == "--device") device = atoi(v);
   }
   if (port == 0) port = 20000 + (int)(getpid() % 20000);
+  // both ends of every connection live in this process: 2 fds per connection
+  rlimit rl{};
+  getrlimit(RLIMIT_NOFILE, &rl);
+  rl.rlim_cur = rl.rlim_max;
+  setrlimit(RLIMIT_NOFILE, &rl);
+  if ((uint64_t)conns * 2 + 64 > (uint64_t)rl.rlim_cur) {
+    fprintf(stderr, "ws_loopback: %d connections need %d fds, RLIMIT_NOFILE is %llu\n", conns, conns * 2 + 64,
+            (unsigned long long)rl.rlim_cur);
+    return 2;
+  }
   std::atomic<int> ready{0};
   std::vector<std::thread> servers;
   for (int l = 0; l < loops; ++l) servers.emplace_back(server_loop, port, device, &ready);
@@ -352,11 +369,11 @@ int main(int argc, char** argv) {
   }
   // measure the steady state: count frames echoed between warm-up end and t_end
   std::this_thread::sleep_for(std::chrono::duration<double>(warm));
-  const uint64_t f0 = g_frames.load(), b0 = g_batches.load(), c0 = g_batch_conns.load();
+  const uint64_t f0 = g_frames.load(), b0 = g_batches.load(), c0 = g_batch_conns.load(), d0 = g_dev_ns.load();
   const double ts = now_s();
   std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
   const double te = now_s();
-  const uint64_t f1 = g_frames.load(), b1 = g_batches.load(), c1 = g_batch_conns.load();
+  const uint64_t f1 = g_frames.load(), b1 = g_batches.load(), c1 = g_batch_conns.load(), d1 = g_dev_ns.load();
   for (auto& t : clients) t.join();
   g_stop = true;
   for (auto& t : servers) t.join();
@@ -366,9 +383,11 @@ int main(int argc, char** argv) {
          "(gevws_protocol_unpacket_batch) -> UnPacket -> echo\", \"connections\": %d, \"upgraded\": %d, "
          "\"msg_bytes\": %zu, \"loops\": %d, \"client_threads\": %d, \"seconds\": %.3f, "
          "\"echoes_per_s\": %.1f, \"payload_MiBps_each_way\": %.2f, \"device_batches_per_s\": %.1f, "
-         "\"mean_conns_per_batch\": %.1f, \"client_checked_echoes\": %llu, \"errors\": %llu}\n",
+         "\"mean_conns_per_batch\": %.1f, \"device_pass_us_mean\": %.1f, \"device_pass_share_of_loop_time\": %.3f, "
+         "\"client_checked_echoes\": %llu, \"errors\": %llu}\n",
          conns, upgraded.load(), msg, loops, cthreads, dt, mps, mps * (double)msg / 1048576.0,
          (double)(b1 - b0) / dt, b1 > b0 ? (double)(c1 - c0) / (double)(b1 - b0) : 0.0,
+         b1 > b0 ? (double)(d1 - d0) / 1e3 / (double)(b1 - b0) : 0.0, (double)(d1 - d0) / 1e9 / (dt * loops),
          (unsigned long long)total.load(), (unsigned long long)g_bad.load());
   return g_bad.load() == 0 && upgraded.load() == conns ? 0 : 1;
 }
