@@ -142,16 +142,19 @@ class Protocol {
     DeviceScope scope(gevws_ctx_device(ctx_));
     int64_t r = StageDecode(segs.data(), m, &sum, cin);
     if (r < 0) return r;
-    // results back to the host
-    std::vector<gevws_conn_out> cout(m);
-    std::vector<gevws_frame> fr(sum.frames);
-    auto arena = std::make_shared<std::vector<uint8_t>>(sum.payload_bytes ? sum.payload_bytes : 1);
-    if (hipMemcpy(cout.data(), d_cout_, m * sizeof(gevws_conn_out), hipMemcpyDeviceToHost) != hipSuccess ||
-        (sum.frames && hipMemcpy(fr.data(), d_frames_, sum.frames * sizeof(gevws_frame),
-                                 hipMemcpyDeviceToHost) != hipSuccess) ||
-        (sum.payload_bytes && hipMemcpy(arena->data(), d_payload_, sum.payload_bytes,
-                                        hipMemcpyDeviceToHost) != hipSuccess))
+    // frames + payload back in one round trip through pinned memory
+    const uint64_t fb = sum.frames * sizeof(gevws_frame);
+    if (!grow_host(&h_out_, &h_out_cap_, fb + sum.payload_bytes + 16)) return fail();
+    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+    if ((fb && hipMemcpyAsync(h_out_, d_frames_, fb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        (sum.payload_bytes &&
+         hipMemcpyAsync(h_out_ + fb, d_payload_, sum.payload_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess)
       return fail();
+    const gevws_conn_out* cout = reinterpret_cast<const gevws_conn_out*>(h_res_ + sizeof(gevws_summary));
+    const gevws_frame* fr = reinterpret_cast<const gevws_frame*>(h_out_);
+    auto arena = std::make_shared<std::vector<uint8_t>>(h_out_ + fb, h_out_ + fb + sum.payload_bytes);
+    if (arena->empty()) arena->resize(1);
     // hand the frames to their connections in stream order
     for (uint32_t j = 0; j < m; ++j) {
       Connection* c = conns[sel[j]];
@@ -189,11 +192,13 @@ class Protocol {
       sum_out->status = GEVWS_ERR_CAPACITY;
       return GEVWS_ERR_CAPACITY;
     }
-    if (hipMemcpy(conn_out, d_cout_, n * sizeof(gevws_conn_out), hipMemcpyDeviceToHost) != hipSuccess ||
-        (sum.frames && hipMemcpy(frames, d_frames_, sum.frames * sizeof(gevws_frame),
-                                 hipMemcpyDeviceToHost) != hipSuccess) ||
-        (sum.payload_bytes && hipMemcpy(payload, d_payload_, sum.payload_bytes,
-                                        hipMemcpyDeviceToHost) != hipSuccess))
+    memcpy(conn_out, h_res_ + sizeof(gevws_summary), n * sizeof(gevws_conn_out));
+    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+    if ((sum.frames && hipMemcpyAsync(frames, d_frames_, sum.frames * sizeof(gevws_frame), hipMemcpyDeviceToHost,
+                                      st) != hipSuccess) ||
+        (sum.payload_bytes &&
+         hipMemcpyAsync(payload, d_payload_, sum.payload_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess)
       return fail();
     for (uint32_t j = 0; j < n; ++j)
       for (uint32_t k = 0; k < conn_out[j].nframes; ++k) frames[conn_out[j].first_frame + k].src_off -= cin[j].off;
@@ -212,40 +217,51 @@ class Protocol {
     }
   };
 
-  // Join each connection's segments into pinned staging, H2D, decode on the
-  // context's stream; results stay in the device buffers.  Retries once with
-  // the exact sizes on ERR_CAPACITY.
+  // Join each connection's segments into pinned staging behind the connection
+  // table, ONE H2D, decode on the context's stream, ONE D2H of {summary,
+  // conn_out} into pinned h_res_ and one sync.  Frames and payload stay in
+  // the device buffers.  Retries once with the exact sizes on ERR_CAPACITY.
   int64_t StageDecode(const gevws_host_conn* segs, uint32_t m, gevws_summary* sum,
                       std::vector<gevws_conn_in>& cin) {
     uint64_t total = 0;
     for (uint32_t j = 0; j < m; ++j) total += segs[j].n0 + segs[j].n1;
     cin.resize(m);
-    if (!grow_host(&h_in_, &h_in_cap_, total + GEVWS_IN_PAD)) return fail();
+    const uint64_t coff = ((uint64_t)m * sizeof(gevws_conn_in) + 255) & ~255ull;  // input starts here
+    const uint64_t stage = coff + total + GEVWS_IN_PAD;
+    if (!grow_host(&h_in_, &h_in_cap_, stage)) return fail();
+    uint8_t* hin = h_in_ + coff;
     uint64_t off = 0;
     for (uint32_t j = 0; j < m; ++j) {
-      if (segs[j].n0) memcpy(h_in_ + off, segs[j].seg0, segs[j].n0);
-      if (segs[j].n1) memcpy(h_in_ + off + segs[j].n0, segs[j].seg1, segs[j].n1);
+      if (segs[j].n0) memcpy(hin + off, segs[j].seg0, segs[j].n0);
+      if (segs[j].n1) memcpy(hin + off + segs[j].n0, segs[j].seg1, segs[j].n1);
       cin[j] = {off, segs[j].n0 + segs[j].n1};
       off += cin[j].len;
     }
-    memset(h_in_ + off, 0, GEVWS_IN_PAD);
+    memcpy(h_in_, cin.data(), m * sizeof(gevws_conn_in));
+    memset(hin + off, 0, GEVWS_IN_PAD);
+    const uint64_t res = sizeof(gevws_summary) + (uint64_t)m * sizeof(gevws_conn_out);
+    if (!grow_host(&h_res_, &h_res_cap_, res)) return fail();
     uint64_t max_frames = std::min<uint64_t>(total / 2 + 1, 0xFFFFFFFFull);
     uint64_t payload_cap = total + 16 * std::min<uint64_t>(max_frames, total / 64 + 64) + 64;
-    void* st = gevws_ctx_stream(ctx_);
+    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+    if (!grow_dev(&d_in_, &d_in_cap_, stage) || !grow_dev(&d_res_, &d_res_cap_, res) ||
+        hipMemcpyAsync(d_in_, h_in_, stage, hipMemcpyHostToDevice, st) != hipSuccess)
+      return fail();
+    gevws_summary* d_sum = (gevws_summary*)d_res_;
+    gevws_conn_out* d_cout = (gevws_conn_out*)((uint8_t*)d_res_ + sizeof(gevws_summary));
     for (int attempt = 0; attempt < 2; ++attempt) {
-      if (!grow_dev(&d_in_, &d_in_cap_, total + GEVWS_IN_PAD) ||
-          !grow_dev(&d_conns_, &d_conns_cap_, m * sizeof(gevws_conn_in)) ||
-          !grow_dev(&d_cout_, &d_cout_cap_, m * sizeof(gevws_conn_out)) ||
-          !grow_dev(&d_frames_, &d_frames_cap_, max_frames * sizeof(gevws_frame)) ||
+      if (!grow_dev(&d_frames_, &d_frames_cap_, max_frames * sizeof(gevws_frame)) ||
           !grow_dev(&d_payload_, &d_payload_cap_, payload_cap + 16))
         return fail();
-      if (hipMemcpyAsync(d_in_, h_in_, total + GEVWS_IN_PAD, hipMemcpyHostToDevice, (hipStream_t)st) != hipSuccess ||
-          hipMemcpyAsync(d_conns_, cin.data(), m * sizeof(gevws_conn_in), hipMemcpyHostToDevice,
-                         (hipStream_t)st) != hipSuccess)
+      int r = gevws_decode_batch_async(ctx_, st, (const uint8_t*)d_in_ + coff, total, (gevws_conn_in*)d_in_, m,
+                                       (gevws_frame*)d_frames_, max_frames, (uint8_t*)d_payload_, payload_cap,
+                                       d_cout, d_sum);
+      if (r != GEVWS_OK) return r;
+      if (hipMemcpyAsync(h_res_, d_res_, res, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
         return fail();
-      int r = gevws_decode_batch(ctx_, st, (const uint8_t*)d_in_, total, (gevws_conn_in*)d_conns_, m,
-                                 (gevws_frame*)d_frames_, max_frames, (uint8_t*)d_payload_, payload_cap,
-                                 (gevws_conn_out*)d_cout_, sum);
+      memcpy(sum, h_res_, sizeof(gevws_summary));
+      r = sum->status;
       if (r == GEVWS_ERR_CAPACITY && attempt == 0) {
         max_frames = std::max<uint64_t>(sum->frames, 1);
         payload_cap = std::max<uint64_t>(sum->payload_bytes, 16);
@@ -285,17 +301,18 @@ class Protocol {
     return true;
   }
   void release() {
-    if (h_in_) (void)hipHostFree(h_in_);
-    for (void* p : {d_in_, d_conns_, d_cout_, d_frames_, d_payload_})
+    for (uint8_t* p : {h_in_, h_res_, h_out_})
+      if (p) (void)hipHostFree(p);
+    for (void* p : {d_in_, d_res_, d_frames_, d_payload_})
       if (p) (void)hipFree(p);
   }
 
   gevws_ctx* ctx_;
   const Upgrader* upgrader_ = nullptr;
-  uint8_t* h_in_ = nullptr;
-  uint64_t h_in_cap_ = 0;
-  void *d_in_ = nullptr, *d_conns_ = nullptr, *d_cout_ = nullptr, *d_frames_ = nullptr, *d_payload_ = nullptr;
-  uint64_t d_in_cap_ = 0, d_conns_cap_ = 0, d_cout_cap_ = 0, d_frames_cap_ = 0, d_payload_cap_ = 0;
+  uint8_t *h_in_ = nullptr, *h_res_ = nullptr, *h_out_ = nullptr;  // pinned staging
+  uint64_t h_in_cap_ = 0, h_res_cap_ = 0, h_out_cap_ = 0;
+  void *d_in_ = nullptr, *d_res_ = nullptr, *d_frames_ = nullptr, *d_payload_ = nullptr;
+  uint64_t d_in_cap_ = 0, d_res_cap_ = 0, d_frames_cap_ = 0, d_payload_cap_ = 0;
 };
 
 }  // namespace gevws
