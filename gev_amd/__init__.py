@@ -251,6 +251,15 @@ class Engine:
         if st != OK:
             raise RuntimeError(status_string(st))
 
+    def copy_(self, dst, src, nbytes: int, dst_offset: int = 0, src_offset: int = 0, grid: int = 0,
+              stream=None) -> None:
+        """gevws_copy_async: the streaming-copy ceiling kernel (measurement only)."""
+        assert dst_offset + nbytes <= dst.numel() and src_offset + nbytes <= src.numel()
+        st = lib.gevws_copy_async(self._ctx, _stream_handle(stream), dst.data_ptr() + dst_offset,
+                                  src.data_ptr() + src_offset, nbytes, grid)
+        if st != OK:
+            raise RuntimeError(status_string(st))
+
     # -------------------------------------------------------------- synthetic batches
     def synth(self, arena, desc_dev, n_frames: int, seed: int, stream=None) -> None:
         st = lib.gevws_synth_async(self._ctx, _stream_handle(stream), arena.data_ptr(), desc_dev.data_ptr(),

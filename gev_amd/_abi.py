@@ -184,6 +184,7 @@ SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_uint64)]),
     "gevws_protocol_unpacket_batch": (ctypes.c_int64, [P, P, P, ctypes.c_uint32]),
     "gevws_protocol_packet": (U8P, [P, P, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    "gevws_copy_async": (ctypes.c_int, [P, P, P, P, ctypes.c_uint64, ctypes.c_uint32]),
     "gevws_upgrader_new": (P, []),
     "gevws_upgrader_free": (None, [P]),
     "gevws_upgrader_set_header": (None, [P, P, ctypes.c_uint64]),

@@ -580,6 +580,58 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v2(const uint8_t* __res
   }
 }
 
+// Measurement helper (not on the reference path): the unmask kernel's
+// streaming loop with the frame lookup and the XOR taken out -- each workgroup
+// owns a contiguous run of 4 KiB tiles, U unaligned 16-byte loads per lane,
+// aligned non-temporal stores.  bench.py times it over the same bytes as the
+// achievable-bandwidth ceiling beside the 8 TB/s spec peak.
+template <int U, bool INTERLEAVE>
+__global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __restrict__ src,
+                                                              uint8_t* __restrict__ dst, uint64_t n) {
+  const uint64_t ntiles = n / kTile;
+  const uint32_t lane_off = threadIdx.x * 16;
+  if constexpr (INTERLEAVE) {
+    // blocks of U consecutive tiles dealt round-robin over the workgroups
+    const uint64_t nblk = ntiles / U;
+    for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+      const uint64_t base = b * U * kTile + lane_off;
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld16u(src + base + u * kTile);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + base + u * kTile));
+    }
+    for (uint64_t t = nblk * U + blockIdx.x; t < ntiles; t += gridDim.x) {
+      const uint64_t base = t * kTile + lane_off;
+      __builtin_nontemporal_store(ld16u(src + base), reinterpret_cast<u32x4*>(dst + base));
+    }
+  } else {
+    // a contiguous run of tiles per workgroup (the unmask kernel's mapping)
+    const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+    uint64_t t = (uint64_t)blockIdx.x * per;
+    const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+    for (; t + U <= tend; t += U) {
+      const uint64_t base = t * kTile + lane_off;
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld16u(src + base + u * kTile);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + base + u * kTile));
+    }
+    for (; t < tend; ++t) {
+      const uint64_t base = t * kTile + lane_off;
+      __builtin_nontemporal_store(ld16u(src + base), reinterpret_cast<u32x4*>(dst + base));
+    }
+  }
+  // bytes past the last whole tile: 16 per lane, workgroup 0
+  const uint64_t tail = ntiles * kTile;
+  if (blockIdx.x == 0)
+    for (uint64_t p = tail + lane_off; p < n; p += kTile)
+      __builtin_nontemporal_store(ld16u(src + p), reinterpret_cast<u32x4*>(dst + p));
+}
+
 // v3 = v2's streaming fast path + a cooperative small-frame path.  When the
 // next U tiles are not inside the cached frame, the workgroup takes a window
 // of W tiles, loads the records of every frame overlapping it (tile map gives
@@ -1625,6 +1677,22 @@ int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_fram
                                               d_reply_of, d_payload + aux_off);
   GEVWS_HIP(hipGetLastError());
   return mark_last(ctx, st);
+}
+
+int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t* d_src, uint64_t n,
+                     uint32_t grid) {
+  if (!ctx || (n && (!d_dst || !d_src))) return GEVWS_ERR_INVALID;
+  if ((n & 15) || (reinterpret_cast<uint64_t>(d_dst) & 15)) return GEVWS_ERR_INVALID;
+  if (n == 0) return GEVWS_OK;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  if (grid == 0) grid = (uint32_t)ctx->num_cus;
+  if (grid & 0x80000000u)  // high bit: interleaved block mapping (measurement variant)
+    k_copy_stream<16, true><<<grid & 0x7fffffffu, kUnmaskBlock, 0, st>>>(d_src, d_dst, n);
+  else
+    k_copy_stream<16, false><<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst, n);
+  GEVWS_HIP(hipGetLastError());
+  return GEVWS_OK;
 }
 
 int gevws_cipher_async(gevws_ctx* ctx, void* stream, uint8_t* d_p, uint64_t n, const uint8_t mask[4],

@@ -211,6 +211,15 @@ int gevws_dispatch_async(gevws_ctx *ctx, void *stream, const gevws_frame *d_fram
                          uint8_t *d_payload, uint64_t aux_off, uint64_t aux_cap,
                          gevws_out_frame *d_replies, int64_t *d_reply_of, gevws_summary *d_summary);
 
+/* Measurement helper, not on the reference path: n bytes (n % 16 == 0, d_dst
+ * 16-byte aligned, d_src any alignment) copied with the unmask kernel's
+ * streaming access pattern minus the XOR and frame lookup -- the achievable
+ * HBM rate bench.py reports beside the spec peak.  grid 0 = one workgroup per
+ * CU (the unmask kernel's grid for large frames); grid | 0x80000000 deals
+ * 64 KiB blocks round-robin over the workgroups instead of contiguous runs. */
+int gevws_copy_async(gevws_ctx *ctx, void *stream, uint8_t *d_dst, const uint8_t *d_src, uint64_t n,
+                     uint32_t grid);
+
 /* ws.Cipher(payload, mask, offset), plugins/websocket/ws/cipher.go:14-53, on a
  * device buffer in place: p[i] ^= mask[(offset+i) % 4]. */
 int gevws_cipher_async(gevws_ctx *ctx, void *stream, uint8_t *d_p, uint64_t n,
