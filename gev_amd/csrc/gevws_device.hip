@@ -642,7 +642,46 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __r
 constexpr int kWinTiles = 4;
 constexpr int kWinFrames = 1024;
 
-template <int U, bool NTL, bool NTS>
+// Value of `x` in lane+1 (wave-wide shift by one lane; lane 63 gets 0):
+// DPP wave_shl:1, a VALU modifier on gfx9-class waves (no LDS crossbar).
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
+}
+// Value of `x` in lane+1, lane 63 gets lane 0's (DPP wave_rol:1).
+__device__ __forceinline__ u32x4 rot_next_lane(u32x4 x) {
+  return u32x4{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[0], 0x134, 0xf, 0xf, false),
+               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[1], 0x134, 0xf, 0xf, false),
+               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[2], 0x134, 0xf, 0xf, false),
+               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[3], 0x134, 0xf, 0xf, false)};
+}
+
+// Bytes [m, m+16) of the 32-byte concatenation a|b (m in 1..15, wave-uniform).
+__device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t m) {
+  const uint32_t r = m & 3;
+  u32x4 o;
+  switch (m >> 2) {
+    case 0:
+      o = u32x4{__builtin_amdgcn_alignbyte(a[1], a[0], r), __builtin_amdgcn_alignbyte(a[2], a[1], r),
+                __builtin_amdgcn_alignbyte(a[3], a[2], r), __builtin_amdgcn_alignbyte(b[0], a[3], r)};
+      break;
+    case 1:
+      o = u32x4{__builtin_amdgcn_alignbyte(a[2], a[1], r), __builtin_amdgcn_alignbyte(a[3], a[2], r),
+                __builtin_amdgcn_alignbyte(b[0], a[3], r), __builtin_amdgcn_alignbyte(b[1], b[0], r)};
+      break;
+    case 2:
+      o = u32x4{__builtin_amdgcn_alignbyte(a[3], a[2], r), __builtin_amdgcn_alignbyte(b[0], a[3], r),
+                __builtin_amdgcn_alignbyte(b[1], b[0], r), __builtin_amdgcn_alignbyte(b[2], b[1], r)};
+      break;
+    default:
+      o = u32x4{__builtin_amdgcn_alignbyte(b[0], a[3], r), __builtin_amdgcn_alignbyte(b[1], b[0], r),
+                __builtin_amdgcn_alignbyte(b[2], b[1], r), __builtin_amdgcn_alignbyte(b[3], b[2], r)};
+      break;
+  }
+  return o;
+}
+
+
+template <int U, bool NTL, bool NTS, int AL = 0>
 __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __restrict__ in,
                                                             const gevws_frame* __restrict__ frames,
                                                             const uint32_t* __restrict__ tile_first,
@@ -681,6 +720,60 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
       const uint8_t* src = in + f_src + rel0;
       uint8_t* dst = out + base + lane_off;
       u32x4 v[U];
+      const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(src) & 15);  // uniform: lanes 16 B apart
+      if (AL == 2 && mis != 0) {
+        // aligned loads, wave-contiguous mapping: wave w covers U KiB-chunks
+        // [base + w*U KiB, +U KiB) of the step; lane 63's successor chunk at
+        // step u is lane 0's chunk at u+1 (DPP rotate), so only u = U-1 needs
+        // one extra load, by lane 63
+        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const uint64_t wrel = (uint64_t)wave * U * 1024 + lane * 16;  // this lane's offset in the step
+        const uint8_t* a = in + f_src + (base - f_po) + wrel - mis;
+        uint8_t* d = out + base + wrel;
+        const bool last = lane == 63;
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * 1024);
+        u32x4 e = u32x4{0, 0, 0, 0};
+        if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
+        u32x4 r = rot_next_lane(v[0]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const u32x4 rn = u + 1 < U ? rot_next_lane(v[u + 1 < U ? u + 1 : u]) : e;
+          const u32x4 nx = last ? rn : r;
+          u32x4 x = funnel16(v[u], nx, mis) ^ f_key;
+          const int64_t rem = f_len - (int64_t)(base - f_po + wrel + u * 1024);
+          if (rem < 16) x = keep_bytes(x, rem);
+          st16_stream<NTS>(d + u * 1024, x);
+          r = rn;
+        }
+        t += U;
+        continue;
+      }
+      if (AL == 1 && mis != 0) {
+        // aligned loads: this lane's aligned chunk + the next lane's (DPP);
+        // lane 63 loads its successor chunk itself
+        const uint8_t* a = src - mis;
+        const bool last = (threadIdx.x & 63) == 63;
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * kTile);
+        u32x4 e[U];
+        if (last) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) e[u] = *reinterpret_cast<const u32x4*>(a + 16 + u * kTile);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          u32x4 nx = u32x4{from_next_lane(v[u][0]), from_next_lane(v[u][1]), from_next_lane(v[u][2]),
+                           from_next_lane(v[u][3])};
+          if (last) nx = e[u];
+          u32x4 x = funnel16(v[u], nx, mis) ^ f_key;
+          const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
+          if (rem < 16) x = keep_bytes(x, rem);
+          st16_stream<NTS>(dst + u * kTile, x);
+        }
+        t += U;
+        continue;
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = ld16u_stream<NTL>(src + u * kTile);
 #pragma unroll
@@ -1413,13 +1506,16 @@ struct UnmaskVariant {
 // Variant 0 is the default; the others are kept for A/B measurement
 // (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 const UnmaskVariant kUnmaskVariants[] = {
-    {k_unmask_v3<16, false, true>, 16, "v3 U16 + LDS small-frame window, plain-load nt-store"},
+    {k_unmask_v3<16, false, true, 2>, 16,
+     "v3 U16 + LDS small-frame window; streaming path: aligned loads, wave-contiguous 16 KiB spans, DPP rotate"},
     {k_unmask<4>, 4, "v1 U4 grid-stride per-lane lookup"},
     {k_unmask_v2<16, false, true>, 16, "v2 U16 plain-load nt-store"},
     {k_unmask_v2<8, false, true>, 8, "v2 U8 plain-load nt-store"},
     {k_unmask_v2<4, false, true>, 4, "v2 U4 plain-load nt-store"},
     {k_unmask_v3<8, false, true>, 8, "v3 U8 + LDS window"},
     {k_unmask_v3<16, true, true>, 16, "v3 U16 + LDS window, nt-load nt-store"},
+    {k_unmask_v3<16, false, true, 1>, 16, "v3 U16, aligned loads + DPP lane shift + alignbyte funnel"},
+    {k_unmask_v3<16, false, true>, 16, "v3 U16 + LDS small-frame window, unaligned loads (round-1 default before 0)"},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 

@@ -267,3 +267,40 @@ def test_one_context_two_streams_is_ordered(engine):
         want = ref.decode_batch(a, conns[:, 0], conns[:, 1])
         assert out.frames_host().tobytes() == want["frames"].tobytes()
         assert np.array_equal(out.payload_host(), want["payload"])
+
+
+def test_every_unmask_variant_big_frames_all_alignments(engine):
+    """Each unmask variant (the default's aligned-load streaming path included)
+    over frames >= 16 tiles whose payloads start at all 16 source alignments,
+    with odd lengths, unmasked frames and small frames between them, in
+    several connections: bit-exact against the C oracle."""
+    from gev_amd import _abi
+    rng = np.random.default_rng(77)
+    streams, pos = [], 0     # pos: absolute arena offset (the arena starts 256-aligned on the device)
+    for c in range(4):
+        s = b""
+        for k in range(12):
+            masked = k % 5 != 4
+            h = 14 if masked else 10
+            want = (3 * c + 5 * k) % 16        # target source alignment of this payload
+            # a small unmasked frame (2 + n bytes) moves the next payload to `want`
+            n = (want - (pos + len(s) + 2 + h)) % 16 + 16 * int(rng.integers(0, 3))
+            s += wo.encode_frame(bytes(rng.integers(0, 256, n, dtype=np.uint8)), 1, True, 0, False, b"\0" * 4)
+            L = int(rng.integers(16 * 4096, 3 * 16 * 4096)) + int(rng.integers(0, 16))
+            s += wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), 2, True, 0, masked,
+                                 bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+        streams.append(s)
+        pos += len(s)
+    arena, conns = pack_streams(streams)
+    i = 0
+    while engine.variant_name(i) is not None:
+        engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, i)
+        try:
+            got = assert_matches_oracle(engine, arena, conns, f"variant {i}")
+        finally:
+            engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 0)
+        i += 1
+    # the sweep covered every source alignment of a streamed payload
+    f = got["frames"]
+    big = f["length"] >= 16 * 4096
+    assert len(set((f["src_off"][big] % 16).tolist())) == 16
