@@ -43,6 +43,7 @@ HANDLER_ECHO_BINARY = 1
 HANDLER_ECHO_TEXT = 2
 TUNE_UNMASK_VARIANT = 1
 TUNE_UNMASK_GRID = 2
+TUNE_ENCODE_VARIANT = 3
 
 IN_PAD = 64
 PAYLOAD_ALIGN = 16

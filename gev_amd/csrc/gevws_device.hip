@@ -1010,7 +1010,7 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
   return u32x4_of(acc);
 }
 
-template <int U>
+template <int U, bool AL>
 __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
@@ -1045,6 +1045,30 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
     }
     if (t + U <= tend && base >= c_ps && base + U * kTile <= c_pe) {  // inside one payload: stream
       u32x4 v[U];
+      const uint8_t* s0 = payload + (base + c_delta);
+      const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(s0) & 15);  // wave-uniform
+      if (AL && mis != 0) {
+        // as k_unmask_v3's streaming path: wave-contiguous U KiB spans, aligned
+        // loads, neighbour chunk by DPP rotate, lane 63's last successor loaded
+        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const uint64_t wrel = (uint64_t)wave * U * 1024 + lane * 16;
+        const uint8_t* a = s0 + wrel - mis;
+        uint8_t* d = out + base + wrel;
+        const bool last = lane == 63;
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * 1024);
+        u32x4 e = u32x4{0, 0, 0, 0};
+        if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
+        u32x4 r = rot_next_lane(v[0]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const u32x4 rn = u + 1 < U ? rot_next_lane(v[u + 1 < U ? u + 1 : u]) : e;
+          __builtin_nontemporal_store(funnel16(v[u], last ? rn : r, mis), reinterpret_cast<u32x4*>(d + u * 1024));
+          r = rn;
+        }
+        t += U;
+        continue;
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = ld16u(payload + (base + u * kTile + lane_off + c_delta));
 #pragma unroll
@@ -1430,6 +1454,7 @@ struct gevws_ctx {
   gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
+  int encode_variant = 0;  // 0 = aligned-load streaming, 1 = unaligned loads
   // Scratch is per context: calls on a different stream than the previous one
   // first wait for it (one in-flight batch per context; use one context per
   // stream for concurrency).
@@ -1605,6 +1630,10 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       if (value < 0 || value > (1 << 20)) return GEVWS_ERR_INVALID;
       ctx->unmask_grid = (int)value;
       return GEVWS_OK;
+    case GEVWS_TUNE_ENCODE_VARIANT:
+      if (value < 0 || value > 1) return GEVWS_ERR_INVALID;
+      ctx->encode_variant = (int)value;
+      return GEVWS_OK;
     default:
       return GEVWS_ERR_INVALID;
   }
@@ -1744,7 +1773,8 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   // no big-frame grid reduction here: every frame boundary takes the window
   // path, which needs 4 workgroups per CU to hide its latency (C3: 22.6 ms at
   // 4/CU vs 36 ms at 1/CU, profiles/r01_encode_*.json)
-  k_encode<4><<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
+  auto enc = ctx->encode_variant == 1 ? k_encode<4, false> : k_encode<4, true>;
+  enc<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
                                                        0u);
   GEVWS_HIP(hipGetLastError());
   return mark_last(ctx, st);

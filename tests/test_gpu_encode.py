@@ -47,9 +47,21 @@ def test_encode_golden(engine, golden):
     assert np.array_equal(got, g["wire"])
 
 
-def test_encode_random_and_tiny_frames(engine):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_encode_random_and_tiny_frames(engine, variant):
+    """variant 0: aligned-load streaming (default); 1: unaligned loads."""
+    from gev_amd import _abi
+    engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, variant)
+    try:
+        _encode_random(engine)
+    finally:
+        engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, 0)
+
+
+def _encode_random(engine):
     rng = np.random.default_rng(41)
-    for trial, (n, maxlen) in enumerate([(1, 0), (5, 10), (300, 3000), (3000, 0), (5000, 20), (200, 70000)]):
+    for trial, (n, maxlen) in enumerate([(1, 0), (5, 10), (300, 3000), (3000, 0), (5000, 20), (200, 70000),
+                                         (60, 200000)]):
         lens = rng.integers(0, maxlen + 1, n)
         payload = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
         offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)

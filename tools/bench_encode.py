@@ -21,6 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default="0", help="encode variants to A/B, e.g. 0,1 (interleaved rounds)")
+    ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -61,19 +63,38 @@ def main():
         h = 2 if L[g] <= 125 else (4 if L[g] <= 0xFFFF else 10)
         po = int(rep["payload_off"][g])
         assert torch.equal(wire[o + h:o + h + int(L[g])], out.payload[po:po + int(L[g])])
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(args.reps):
-        eng.encode_async(d_rep, lay.n_frames, out.payload, wire, wire_total, off, summ)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / args.reps
-    print(json.dumps({"path": "encode (FrameToBytes of NewBinaryFrame replies)", "workload": lay.name,
-                      "frames": lay.n_frames, "wire_bytes": wire_total, "ms": round(ms, 4),
-                      "payload_GiBps": round(int(L.sum()) / (ms / 1e3) / 2**30, 2),
-                      "frames_per_s": round(lay.n_frames / ms * 1e3, 1),
-                      "algorithmic_GBps": round(alg / ms / 1e6, 1),
-                      "frac_of_8TBps": round(alg / ms / 1e6 / 8000, 4)}))
+    variants = [int(x) for x in args.variants.split(",")]
+    if len(variants) > 1:
+        # every variant's whole wire equals the first one's
+        ref_wire = wire.clone()
+        for v in variants[1:]:
+            eng.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, v)
+            eng.encode_async(d_rep, lay.n_frames, out.payload, wire, wire_total, off, summ)
+            torch.cuda.synchronize()
+            assert torch.equal(wire[:wire_total], ref_wire[:wire_total]), f"encode variant {v} differs"
+        del ref_wire
+        torch.cuda.empty_cache()
+    times = {v: [] for v in variants}
+    for _ in range(args.rounds):
+        for v in variants:
+            eng.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, v)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                eng.encode_async(d_rep, lay.n_frames, out.payload, wire, wire_total, off, summ)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / args.reps)
+    eng.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, 0)
+    for v in variants:
+        ms = sorted(times[v])[len(times[v]) // 2]
+        print(json.dumps({"path": "encode (FrameToBytes of NewBinaryFrame replies)", "variant": v,
+                          "workload": lay.name, "frames": lay.n_frames, "wire_bytes": wire_total,
+                          "ms": round(ms, 4),
+                          "payload_GiBps": round(int(L.sum()) / (ms / 1e3) / 2**30, 2),
+                          "frames_per_s": round(lay.n_frames / ms * 1e3, 1),
+                          "algorithmic_GBps": round(alg / ms / 1e6, 1),
+                          "frac_of_8TBps": round(alg / ms / 1e6 / 8000, 4)}))
 
 
 if __name__ == "__main__":
