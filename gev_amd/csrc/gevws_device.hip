@@ -213,27 +213,38 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_count(const uint8_t* __rest
     load_window(s, lo, hi);
     *sink = WalkEntry{0, 0, 0, 0};
     for (;;) {
+      // parse_header without branches (one exit test per frame): the chain
+      // is latency-bound at about one wave per SIMD, so every instruction
+      // between the header load and the next one counts
       const uint64_t avail = ci.len - pos;
-      if (avail < 6) break;
-      DevHdr h;
-      const int r = parse_header(lo, hi, avail, h);
-      if (r != GEVWS_OK) {
-        if (r < 0) { st = r; err = 1; }
+      const uint32_t b1 = (uint32_t)(lo >> 8) & 0xffu;
+      const uint32_t masked = b1 >> 7, len7 = b1 & 0x7fu;
+      const bool e16 = len7 == 126, e64 = len7 == 127;
+      const uint32_t hlen = 2 + (e64 ? 8u : (e16 ? 2u : 0u)) + 4 * masked;
+      const uint64_t L64 = __builtin_bswap64((lo >> 16) | (hi << 48));
+      const uint64_t L16 = (((lo >> 16) & 0xff) << 8) | ((lo >> 24) & 0xff);
+      const uint64_t L = e64 ? L64 : (e16 ? L16 : (uint64_t)len7);
+      const uint32_t key = (e64 ? (uint32_t)(hi >> 16) : (e16 ? (uint32_t)(lo >> 32) : (uint32_t)(lo >> 16))) &
+                           (0u - masked);
+      const bool have_hdr = avail >= 6 && avail >= hlen;   // read.go:20-23, U1
+      const bool msb = e64 && (L64 >> 63);                  // read.go:71-73
+      if (!have_hdr || msb || avail - hlen < L) {           // protocol.go:47 gate
+        if (have_hdr && msb) { st = GEVWS_ERR_LEN_MSB; err = 1; }
         break;
       }
-      if (avail - h.hlen < h.length) break;  // protocol.go:47 gate
-      const uint64_t next = pos + h.hlen + h.length;
+      const uint64_t next = pos + hlen + L;
+      const uint32_t meta = ((uint32_t)lo & 0xffu) | (masked << 8) | (hlen << 16);  // before lo is reloaded
       load_window(s + next, lo, hi);
       rec = rec && nf < ecap;
       WalkEntry e;
       e.pos = (uint32_t)pos;
-      e.mask = h.mask;
-      e.len = (uint32_t)h.length;
-      e.meta = h.b0 | (h.masked << 8) | (h.hlen << 16);
+      e.mask = key;
+      e.len = (uint32_t)L;
+      e.meta = meta;
       *(rec ? entries + ebase + nf : sink) = e;
       ++nf;
-      pb += round16(h.length);
-      pl += h.length;
+      pb += round16(L);
+      pl += L;
       pos = next;
     }
     gevws_conn_out o;
