@@ -40,38 +40,51 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def build_layout(name: str, rank: int, conns: int | None):
+def build_layout(name: str, rank: int, conns: int | None, world: int = 1, scaling: str = "weak"):
+    """Weak: every rank its own batch of the config's shape (per-rank seed).
+    Strong: one global batch (same seed on every rank), connections assigned to
+    ranks by greedy LPT over stream bytes; this rank decodes its share."""
     from gev_amd import workloads as w
     from gev_amd.dist import rank_seed
+    if scaling == "strong":
+        glob, _ = build_layout(name, 0, conns)
+        return w.shard_lpt(glob, rank, world), glob
     seed = rank_seed(0x67657600, rank)
     if name == "c3":
-        return w.config_c3(seed=seed, n_conns=conns or 16384)
-    if name == "c2":
-        return w.config_c2(seed=seed, n_conns=conns or 4096)
-    if name == "c4":
-        return w.config_c4(total_payload=16 << 30, n_conns=conns or 65536, seed=seed)
-    if name == "c5":
-        return w.config_c5(n_conns=conns or 256, seed=seed)
-    raise SystemExit(f"unknown config {name}")
+        lay = w.config_c3(seed=seed, n_conns=conns or 16384)
+    elif name == "c2":
+        lay = w.config_c2(seed=seed, n_conns=conns or 4096)
+    elif name == "c4":
+        lay = w.config_c4(total_payload=16 << 30, n_conns=conns or 65536, seed=seed)
+    elif name == "c5":
+        lay = w.config_c5(n_conns=conns or 256, seed=seed)
+    else:
+        raise SystemExit(f"unknown config {name}")
+    return lay, lay
 
 
-def cpu_sample_layout(name: str):
-    """A bounded sample of the same workload for the CPU baseline."""
+def cpu_sample_layout(name: str, mib: int = 256):
+    """A bounded sample of the same workload for the CPU baseline: `mib` MiB of
+    payload (>= 64 MiB of input per thread, so the sample is not cache-resident)."""
     from gev_amd import workloads as w
     if name == "c3":
-        return w.uniform(16, 256, 65536, seed=1, name="4096 x 64 KiB masked binary frames (256 MiB payload)")
+        n = mib * 16
+        return w.uniform(16 * mib // 256, 256, 65536, seed=1,
+                         name=f"{n} x 64 KiB masked binary frames ({mib} MiB payload)")
     if name == "c2":
-        return w.uniform(64, 1024, 4096, seed=1, name="65536 x 4 KiB masked binary frames (256 MiB payload)")
+        n = mib * 256
+        return w.uniform(64 * mib // 256, 1024, 4096, seed=1,
+                         name=f"{n} x 4 KiB masked binary frames ({mib} MiB payload)")
     if name == "c4":
-        return w.config_c4(total_payload=256 << 20, n_conns=1024, seed=1)
-    return w.config_c5(n_conns=32, seed=1)
+        return w.config_c4(total_payload=mib << 20, n_conns=4 * mib, seed=1)
+    return w.config_c5(n_conns=mib // 8, seed=1)
 
 
 def cpu_baseline(name: str, seconds: float, threads: int, vectorized: bool = False):
     import numpy as np
     from gev_amd import workloads as w
     from oracle import ref
-    lay = cpu_sample_layout(name)
+    lay = cpu_sample_layout(name, max(256, 64 * threads))
     arena = np.concatenate([w.synth_host(lay), np.zeros(64, np.uint8)])
     secs, pb, nf = ref.bench_pipeline(arena, lay.conns[:, 0], lay.conns[:, 1], threads=threads,
                                       min_seconds=seconds, vectorized=vectorized)
@@ -104,6 +117,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--conns", type=int, default=None)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="weak: each GPU its own batch of the config's shape (default for c2/c3/c5); "
+                         "strong: one global batch sharded over the GPUs by LPT (default for c4)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads-multi", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -115,6 +131,7 @@ def main():
 
     import gev_amd
     from gev_amd import dist
+    from gev_amd.workloads import size_histogram
 
     world, rank, local = dist.env()
     if world != args.gpus:
@@ -126,7 +143,10 @@ def main():
 
     eng = gev_amd.Engine(gpu)
     t_setup = time.time()
-    lay = build_layout(args.config, rank, args.conns)
+    scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
+    lay, glob = build_layout(args.config, rank, args.conns, world, scaling)
+    if lay.n_frames == 0:
+        raise SystemExit(f"rank {rank}: no connections in this rank's share ({glob.n_conns} in the batch)")
     log(f"rank {rank}: {lay.name}: {lay.n_frames} frames, {lay.n_conns} connections, "
         f"{lay.arena_bytes / 2**30:.2f} GiB in, {lay.payload_padded / 2**30:.2f} GiB out")
     arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
@@ -214,13 +234,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: masked frames generated on the device (seeded splitmix64 payloads and keys)",
         "config": {"workload": lay.name, "connections_per_gpu": lay.n_conns, "frames_per_gpu": lay.n_frames,
                    "payload_bytes_per_gpu": lay.payload_len, "input_bytes_per_gpu": lay.arena_bytes,
-                   "parallelism": (f"connections sharded over {world} GPU(s); "
+                   "global_connections": glob.n_conns if scaling == "strong" else glob.n_conns * world,
+                   "global_payload_bytes": glob.payload_len if scaling == "strong" else None,
+                   "parallelism": (f"connections sharded over {world} GPU(s)"
+                                   f"{' by greedy LPT over stream bytes' if scaling == 'strong' else ''}; "
                                    f"{'RCCL' if dist.backend() == 'nccl' else dist.backend()} all-reduce of counts")},
         "frames_per_s": round(frames_step * args.steps / elapsed, 1),
         "errors": errors,
@@ -234,6 +257,7 @@ def main():
                      "copy_ceiling": None if copy_gbps is None else round(copy_gbps, 1),
                      "frac_of_copy_ceiling": None if copy_gbps is None else round(achieved / copy_gbps, 4)},
         "verified_bit_exact": True,
+        "frame_size_histogram": (size_histogram(glob) if args.config in ("c4", "c5") else None),
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu:

@@ -229,6 +229,65 @@ def shard(layout: Layout, rank: int, world: int) -> Layout:
     return Layout(layout.name, desc, conns, off1 - off0, pl, padded, layout.seed)
 
 
+def lpt_assign(conn_lens: np.ndarray, world: int) -> np.ndarray:
+    """Greedy LPT (longest processing time first): connections in descending
+    stream-byte order, each to the rank with the fewest bytes so far (ties to
+    the lowest rank).  Returns the rank of every connection.  The largest
+    rank's load is at most 4/3 of the optimum (Graham's bound)."""
+    n = int(conn_lens.shape[0])
+    owner = np.zeros(n, np.int64)
+    if world <= 1 or n == 0:
+        return owner
+    import heapq
+    heap = [(0, r) for r in range(world)]
+    for c in np.argsort(-conn_lens.astype(np.int64), kind="stable"):
+        load, r = heapq.heappop(heap)
+        owner[c] = r
+        heapq.heappush(heap, (load + int(conn_lens[c]), r))
+    return owner
+
+
+def shard_lpt(layout: Layout, rank: int, world: int) -> Layout:
+    """Connection -> GPU assignment by greedy LPT over stream bytes (SURVEY.md
+    §8d C4 / §8e): rank `rank` takes the connections lpt_assign gives it, in
+    their original order, laid out back to back in its own arena.  Frame
+    descriptors keep their global index order (synth payloads are keyed by the
+    descriptor's position, so each rank's batch is self-consistent)."""
+    if world == 1:
+        return layout
+    lens = layout.conns[:, 1]
+    mine = np.nonzero(lpt_assign(lens, world) == rank)[0]
+    if mine.size == 0:
+        return Layout(layout.name, layout.desc[:0], layout.conns[:0], 0, 0, 0, layout.seed)
+    hdr = layout.desc["hdr_off"].astype(np.int64)
+    # frames of connection c are those with hdr_off in [off_c, off_c + len_c)
+    first = np.searchsorted(hdr, layout.conns[mine, 0], side="left")
+    last = np.searchsorted(hdr, layout.conns[mine, 0] + lens[mine], side="left")
+    counts = last - first
+    idx = np.concatenate([np.arange(a, b) for a, b in zip(first, last)]) if counts.sum() else np.zeros(0, np.int64)
+    new_off = np.concatenate([[0], np.cumsum(lens[mine])])
+    desc = layout.desc[idx].copy()
+    shift = np.repeat(new_off[:-1] - layout.conns[mine, 0], counts)
+    desc["hdr_off"] = (hdr[idx] + shift).astype(np.uint64)
+    conns = np.stack([new_off[:-1], lens[mine]], axis=1).astype(np.int64)
+    pl = int(desc["length"].sum())
+    padded = int(((desc["length"] + np.uint64(15)) // np.uint64(16) * np.uint64(16)).sum())
+    return Layout(layout.name, desc, conns, int(new_off[-1]), pl, padded, layout.seed)
+
+
+def size_histogram(layout: Layout) -> list:
+    """Realised payload-length histogram, power-of-two buckets: [[lo, hi, frames], ...]."""
+    L = layout.desc["length"].astype(np.int64)
+    if L.size == 0:
+        return []
+    b = np.zeros(L.shape, np.int64)
+    nz = L > 0
+    b[nz] = np.floor(np.log2(L[nz])).astype(np.int64) + 1
+    cnt = np.bincount(b)
+    return [[0 if k == 0 else 1 << (k - 1), 0 if k == 0 else (1 << k) - 1, int(c)]
+            for k, c in enumerate(cnt) if c]
+
+
 def synth_host(layout: Layout) -> np.ndarray:
     """Host copy of the device generator's output (gevws_synth_async) for
     small layouts: used for the CPU baseline sample and to pin the device
@@ -255,7 +314,10 @@ def synth_host(layout: Layout) -> np.ndarray:
         arena[off:off + h] = np.frombuffer(bytes(hdr), np.uint8)
         p = np.frombuffer(plaintext(layout.seed, g, L), np.uint8)
         if masked:
-            k = np.frombuffer(key.to_bytes(4, "little"), np.uint8)
-            p = p ^ np.resize(k, L)
+            # key phase 0 at the payload start (ws.Cipher offset 0, protocol.go:54)
+            q = np.zeros((L + 3) // 4 * 4, np.uint8)
+            q[:L] = p
+            q.view("<u4")[:] ^= np.uint32(key)
+            p = q[:L]
         arena[off + h:off + h + L] = p
     return arena

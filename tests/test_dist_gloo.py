@@ -90,3 +90,52 @@ def test_shard_layouts_reassemble():
     assert sum(p.payload_len for p in parts) == lay.payload_len
     assert sum(p.arena_bytes for p in parts) == lay.arena_bytes
     assert np.array_equal(np.concatenate([p.desc["length"] for p in parts]), lay.desc["length"])
+
+
+def test_lpt_shard_partition_and_balance():
+    from gev_amd import workloads as w
+    lay = w.config_c4(total_payload=4 << 20, n_conns=37, seed=11)
+    lens = lay.conns[:, 1]
+    for world in (1, 2, 3, 8):
+        parts = [w.shard_lpt(lay, r, world) for r in range(world)]
+        assert sum(p.n_frames for p in parts) == lay.n_frames
+        assert sum(p.payload_len for p in parts) == lay.payload_len
+        assert sum(p.arena_bytes for p in parts) == lay.arena_bytes
+        assert sorted(np.concatenate([p.conns[:, 1] for p in parts]).tolist()) == sorted(lens.tolist())
+        # Graham's bound for greedy LPT
+        assert max(p.arena_bytes for p in parts) <= 4 / 3 * max(lens.sum() / world, lens.max()) + 1
+        for p in parts:
+            # each rank's arena is a valid back-to-back layout: frames tile every stream exactly
+            h = w.header_len(p.desc["length"].astype(np.int64), p.desc["masked"], p.desc["len_form"].astype(np.int64))
+            end = p.desc["hdr_off"].astype(np.int64) + h + p.desc["length"].astype(np.int64)
+            assert np.array_equal(end[:-1], p.desc["hdr_off"][1:].astype(np.int64))
+            if p.n_conns:
+                assert np.array_equal(p.conns[1:, 0], (p.conns[:, 0] + p.conns[:, 1])[:-1])
+
+
+def test_lpt_shard_decodes_to_global_frames():
+    """The frames every rank decodes (oracle) are exactly the global batch's frames."""
+    from gev_amd import workloads as w
+    from oracle import ref
+    lay = w.config_c5(n_conns=6, messages_per_conn=1, message_bytes=20 * 1024, seed=4)
+    got = []
+    for r in range(3):
+        p = w.shard_lpt(lay, r, 3)
+        if p.n_conns == 0:
+            continue
+        arena = np.concatenate([w.synth_host(p), np.zeros(64, np.uint8)])
+        d = ref.decode_batch(arena, p.conns[:, 0], p.conns[:, 1])
+        assert (d["conn_status"] >= 0).all() and d["frames"].shape[0] == p.n_frames
+        got += list(zip(d["frames"]["length"].tolist(), d["frames"]["opcode"].tolist()))
+    want = list(zip(lay.desc["length"].tolist(), (lay.desc["b0"] & 0xF).tolist()))
+    assert sorted(got) == sorted(want)
+
+
+def test_size_histogram_counts_every_frame():
+    from gev_amd import workloads as w
+    lay = w.config_c5(n_conns=4, messages_per_conn=1, message_bytes=30 * 1024, seed=2)
+    hist = w.size_histogram(lay)
+    assert sum(c for _, _, c in hist) == lay.n_frames
+    for lo, hi, c in hist:
+        m = (lay.desc["length"] >= lo) & (lay.desc["length"] <= hi)
+        assert int(m.sum()) == c
