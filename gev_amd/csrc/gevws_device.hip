@@ -692,6 +692,83 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t m) {
 }
 
 
+// One streaming step: U whole tiles [base, base + U*kTile) of the output
+// arena inside one frame (payload offset f_po, source f_src, length f_len,
+// key f_key).  AL = 2: aligned loads, wave-contiguous spans, realigned in
+// registers (DPP lane rotate + v_alignbyte) when the source is misaligned;
+// AL = 1: aligned loads + DPP lane shift; AL = 0 / aligned source: plain loads.
+template <int U, bool NTL, bool NTS, int AL>
+__device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                            uint64_t base, uint64_t f_po, uint64_t f_src, int64_t f_len,
+                                            uint32_t f_key) {
+  const uint32_t lane_off = threadIdx.x * 16;
+  const uint64_t rel0 = base - f_po + lane_off;
+  const uint8_t* src = in + f_src + rel0;
+  uint8_t* dst = out + base + lane_off;
+  u32x4 v[U];
+  const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(src) & 15);  // uniform: lanes 16 B apart
+  if (AL == 2 && mis != 0) {
+    // aligned loads, wave-contiguous mapping: wave w covers U KiB-chunks
+    // [base + w*U KiB, +U KiB) of the step; lane 63's successor chunk at
+    // step u is lane 0's chunk at u+1 (DPP rotate), so only u = U-1 needs
+    // one extra load, by lane 63
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t wrel = (uint64_t)wave * U * 1024 + lane * 16;  // this lane's offset in the step
+    const uint8_t* a = in + f_src + (base - f_po) + wrel - mis;
+    uint8_t* d = out + base + wrel;
+    const bool last = lane == 63;
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * 1024);
+    u32x4 e = u32x4{0, 0, 0, 0};
+    if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
+    u32x4 r = rot_next_lane(v[0]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u32x4 rn = u + 1 < U ? rot_next_lane(v[u + 1 < U ? u + 1 : u]) : e;
+      const u32x4 nx = last ? rn : r;
+      u32x4 x = funnel16(v[u], nx, mis) ^ f_key;
+      const int64_t rem = f_len - (int64_t)(base - f_po + wrel + u * 1024);
+      if (rem < 16) x = keep_bytes(x, rem);
+      st16_stream<NTS>(d + u * 1024, x);
+      r = rn;
+    }
+    return;
+  }
+  if (AL == 1 && mis != 0) {
+    // aligned loads: this lane's aligned chunk + the next lane's (DPP);
+    // lane 63 loads its successor chunk itself
+    const uint8_t* a = src - mis;
+    const bool last = (threadIdx.x & 63) == 63;
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * kTile);
+    u32x4 e[U];
+    if (last) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) e[u] = *reinterpret_cast<const u32x4*>(a + 16 + u * kTile);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      u32x4 nx = u32x4{from_next_lane(v[u][0]), from_next_lane(v[u][1]), from_next_lane(v[u][2]),
+                       from_next_lane(v[u][3])};
+      if (last) nx = e[u];
+      u32x4 x = funnel16(v[u], nx, mis) ^ f_key;
+      const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
+      if (rem < 16) x = keep_bytes(x, rem);
+      st16_stream<NTS>(dst + u * kTile, x);
+    }
+    return;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = ld16u_stream<NTL>(src + u * kTile);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    u32x4 x = v[u] ^ f_key;
+    const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
+    if (rem < 16) x = keep_bytes(x, rem);
+    st16_stream<NTS>(dst + u * kTile, x);
+  }
+}
+
 template <int U, bool NTL, bool NTS, int AL = 0>
 __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __restrict__ in,
                                                             const gevws_frame* __restrict__ frames,
@@ -727,73 +804,7 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
       f_key = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
     }
     if (t + U <= tend && base + U * kTile <= f_end) {
-      const uint64_t rel0 = base - f_po + lane_off;
-      const uint8_t* src = in + f_src + rel0;
-      uint8_t* dst = out + base + lane_off;
-      u32x4 v[U];
-      const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(src) & 15);  // uniform: lanes 16 B apart
-      if (AL == 2 && mis != 0) {
-        // aligned loads, wave-contiguous mapping: wave w covers U KiB-chunks
-        // [base + w*U KiB, +U KiB) of the step; lane 63's successor chunk at
-        // step u is lane 0's chunk at u+1 (DPP rotate), so only u = U-1 needs
-        // one extra load, by lane 63
-        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        const uint64_t wrel = (uint64_t)wave * U * 1024 + lane * 16;  // this lane's offset in the step
-        const uint8_t* a = in + f_src + (base - f_po) + wrel - mis;
-        uint8_t* d = out + base + wrel;
-        const bool last = lane == 63;
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * 1024);
-        u32x4 e = u32x4{0, 0, 0, 0};
-        if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
-        u32x4 r = rot_next_lane(v[0]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const u32x4 rn = u + 1 < U ? rot_next_lane(v[u + 1 < U ? u + 1 : u]) : e;
-          const u32x4 nx = last ? rn : r;
-          u32x4 x = funnel16(v[u], nx, mis) ^ f_key;
-          const int64_t rem = f_len - (int64_t)(base - f_po + wrel + u * 1024);
-          if (rem < 16) x = keep_bytes(x, rem);
-          st16_stream<NTS>(d + u * 1024, x);
-          r = rn;
-        }
-        t += U;
-        continue;
-      }
-      if (AL == 1 && mis != 0) {
-        // aligned loads: this lane's aligned chunk + the next lane's (DPP);
-        // lane 63 loads its successor chunk itself
-        const uint8_t* a = src - mis;
-        const bool last = (threadIdx.x & 63) == 63;
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * kTile);
-        u32x4 e[U];
-        if (last) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) e[u] = *reinterpret_cast<const u32x4*>(a + 16 + u * kTile);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          u32x4 nx = u32x4{from_next_lane(v[u][0]), from_next_lane(v[u][1]), from_next_lane(v[u][2]),
-                           from_next_lane(v[u][3])};
-          if (last) nx = e[u];
-          u32x4 x = funnel16(v[u], nx, mis) ^ f_key;
-          const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
-          if (rem < 16) x = keep_bytes(x, rem);
-          st16_stream<NTS>(dst + u * kTile, x);
-        }
-        t += U;
-        continue;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16u_stream<NTL>(src + u * kTile);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        u32x4 x = v[u] ^ f_key;
-        const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
-        if (rem < 16) x = keep_bytes(x, rem);
-        st16_stream<NTS>(dst + u * kTile, x);
-      }
+      stream_step<U, NTL, NTS, AL>(in, out, base, f_po, f_src, f_len, f_key);
       t += U;
       continue;
     }
@@ -866,6 +877,193 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
       }
       t += 1;
     }
+  }
+}
+
+// v4 = v3 with the window path software-pipelined.  In v3 every window is one
+// chain of dependent global loads: the tile map and the cached-frame record
+// (scalar) that decide streaming vs window, the window's records, the LDS
+// search, the payload loads.  v4 decides the NEXT step while the current
+// window's payload loads are in flight: it loads the next window's tile-map
+// entries -- first frame a, last frame b and the frame at tile +U, which equals
+// a iff one frame covers the next U tiles (the next step streams) -- and, for a
+// window, its first 256 records into registers (one per lane), which
+// the next iteration writes to LDS without waiting on a fresh load.  WT tiles
+// per window.
+// A value every lane of the wave loaded from the same address, kept in SGPRs
+// (the compiler cannot always prove such loads uniform once the loop stores).
+__device__ __forceinline__ uint32_t uniform32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  return (uint64_t)uniform32((uint32_t)x) | ((uint64_t)uniform32((uint32_t)(x >> 32)) << 32);
+}
+
+constexpr int kWin4Frames = 1024;
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+struct WinRec {
+  u64x2 lo;  // header word (fin, rsv, opcode, masked, mask[4]), length
+  u64x2 hi;  // payload_off, src_off
+};
+
+__device__ __forceinline__ WinRec load_rec(const gevws_frame* __restrict__ frames, uint64_t f) {
+  const u64x2* r = reinterpret_cast<const u64x2*>(frames + f);
+  return WinRec{r[0], r[1]};
+}
+
+// amdgpu_waves_per_eu(4): four workgroups per CU (128 VGPRs; a few loop-
+// invariant lane values spill to scratch).  Three per CU (140 VGPRs, no
+// spills) measured 25-40 % slower on C2/C4/C5.
+template <int U, int WT, bool NTS>
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_v4(const uint8_t* __restrict__ in,
+                                                            const gevws_frame* __restrict__ frames,
+                                                            const uint32_t* __restrict__ tile_first,
+                                                            const gevws_summary* __restrict__ sum,
+                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
+  __shared__ uint32_t s_start[kWin4Frames];   // frame start relative to the window (clamped at 0)
+  __shared__ int32_t s_lend[kWin4Frames];     // payload end relative to the window (clamped)
+  __shared__ uint64_t s_delta[kWin4Frames];   // src_off - payload_off (mod 2^64)
+  __shared__ uint32_t s_key[kWin4Frames];
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t total = sum->payload_bytes;
+  const uint64_t nframes = sum->frames;
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint32_t groups = active_groups(total, nframes, big_grid);
+  if (blockIdx.x >= groups) return;
+  const uint64_t per = (ntiles + groups - 1) / groups;
+  uint64_t t = (uint64_t)blockIdx.x * per;
+  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+  const uint32_t lane_off = threadIdx.x * 16;
+  uint64_t f_po = 0, f_end = 0, f_src = 0;  // the cached (streaming) frame
+  int64_t f_len = 0;
+  uint32_t f_key = 0;
+  // decision for tile pf_t, made during the previous window
+  uint64_t pf_t = ~0ull, pf_a = 0, pf_b = 0;
+  bool pf_stream = false;
+  WinRec r0 = {};  // record pf_a + tid when !pf_stream
+  auto cache_frame = [&](uint64_t f) {  // wave-uniform: SGPRs
+    const uint64_t* rec = reinterpret_cast<const uint64_t*>(frames + f);
+    const uint64_t w0 = uniform64(rec[0]);
+    f_len = (int64_t)uniform64(rec[1]);
+    f_po = uniform64(rec[2]);
+    f_src = uniform64(rec[3]);
+    f_end = f_po + round16((uint64_t)f_len);
+    f_key = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
+  };
+  // step decision for tile x: a = first frame; stream iff one frame covers
+  // [x, x+U) -- the tile map puts frame a at tile x+U-1 too, and its record
+  // (then cached for the streaming step) ends at or past tile x+U; otherwise
+  // b = last frame of the window [x, x+WT)
+  auto decide = [&](uint64_t x, uint64_t& a, uint64_t& b, bool& stream) {
+    a = uniform32(tile_first[x]);
+    stream = false;
+    if (x + U <= tend && uniform32(tile_first[x + U - 1]) == a) {
+      cache_frame(a);
+      stream = x * kTile >= f_po && (x + U) * kTile <= f_end;
+    }
+    const uint64_t wt = (tend - x) < (uint64_t)WT ? (tend - x) : (uint64_t)WT;
+    b = x + wt < ntiles ? (uint64_t)uniform32(tile_first[x + wt]) : nframes - 1;
+  };
+  while (t < tend) {
+    const uint64_t base = t * kTile;
+    if (t + U <= tend && base >= f_po && base + U * kTile <= f_end) {  // still inside the cached frame
+      stream_step<U, false, NTS, 2>(in, out, base, f_po, f_src, f_len, f_key);
+      t += U;
+      pf_t = ~0ull;  // (never t here; redefining r0 keeps it dead across the step)
+      r0 = WinRec{};
+      continue;
+    }
+    uint64_t a, b;
+    bool stream, have = false;
+    if (pf_t == t) {
+      a = pf_a;
+      b = pf_b;
+      stream = pf_stream;
+      have = !pf_stream;
+    } else {
+      decide(t, a, b, stream);
+    }
+    if (stream) {  // decide() cached frame a, which covers [t, t+U)
+      stream_step<U, false, NTS, 2>(in, out, base, f_po, f_src, f_len, f_key);
+      t += U;
+      pf_t = ~0ull;
+      r0 = WinRec{};
+      continue;
+    }
+    // ---- window path
+    const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
+    const uint64_t wend_t = t + wt;
+    const uint64_t wbase = base;
+    const uint64_t F = b - a + 1;
+    if (F > (uint64_t)kWin4Frames) {
+      // too many frames in the window (runs of empty frames): per-lane lookup, one tile
+      const uint64_t p = base + lane_off;
+      if (p < total) {
+        const gevws_frame* fr = frames + find_frame(frames, tile_first, t, ntiles, nframes, p);
+        const uint64_t rel = p - fr->payload_off;
+        uint32_t k;
+        memcpy(&k, fr->hdr.mask, 4);
+        u32x4 x = ld16u(in + fr->src_off + rel) ^ (fr->hdr.masked ? k : 0u);
+        const int64_t r = fr->hdr.length - (int64_t)rel;
+        if (r < 16) x = keep_bytes(x, r);
+        st16_stream<NTS>(out + p, x);
+      }
+      t += 1;
+      continue;
+    }
+    __syncthreads();  // previous window's readers are done with the LDS table
+    auto fill = [&](uint64_t i, const WinRec& q) {
+      const uint64_t L = q.lo[1], po = q.hi[0], so = q.hi[1];
+      s_start[i] = po > wbase ? (uint32_t)(po - wbase) : 0u;
+      const uint64_t lend = po + L;  // end of payload bytes
+      s_lend[i] = lend <= wbase ? 0 : (lend - wbase > 0x7fffffffull ? 0x7fffffff : (int32_t)(lend - wbase));
+      s_delta[i] = so - po;
+      s_key[i] = ((q.lo[0] >> 24) & 0xff) ? (uint32_t)(q.lo[0] >> 32) : 0u;
+    };
+    if (threadIdx.x < F) fill(threadIdx.x, have ? r0 : load_rec(frames, a + threadIdx.x));
+    for (uint64_t i = threadIdx.x + kUnmaskBlock; i < F; i += kUnmaskBlock) fill(i, load_rec(frames, a + i));
+    __syncthreads();
+    u32x4 v[WT];
+    uint32_t key[WT];
+    int32_t rem[WT];
+#pragma unroll
+    for (int u = 0; u < WT; ++u) {
+      const uint32_t rel = (uint32_t)(u * kTile) + lane_off;
+      const uint64_t p = wbase + rel;
+      rem[u] = 0;
+      key[u] = 0;
+      v[u] = u32x4{0, 0, 0, 0};
+      if ((uint64_t)u < wt && p < total) {
+        uint32_t lo = 0, hi = (uint32_t)F - 1;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+        }
+        rem[u] = s_lend[lo] - (int32_t)rel;
+        key[u] = s_key[lo];
+        v[u] = ld16u(in + (p + s_delta[lo]));
+      }
+    }
+    // decide the next step (and fetch the next window's records) while this
+    // window's payload loads are in flight
+    __asm__ volatile("" ::: "memory");
+    pf_t = ~0ull;
+    if (wend_t < tend) {
+      decide(wend_t, pf_a, pf_b, pf_stream);
+      pf_t = wend_t;
+      if (!pf_stream) {
+        const uint64_t nF = pf_b - pf_a + 1;
+        if (threadIdx.x < nF) r0 = load_rec(frames, pf_a + threadIdx.x);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < WT; ++u) {
+      if (rem[u] > 0) {
+        u32x4 x = v[u] ^ key[u];
+        if (rem[u] < 16) x = keep_bytes(x, rem[u]);
+        st16_stream<NTS>(out + wbase + (uint32_t)(u * kTile) + lane_off, x);
+      }
+    }
+    t = wend_t;
   }
 }
 
@@ -1542,8 +1740,11 @@ struct UnmaskVariant {
 // Variant 0 is the default; the others are kept for A/B measurement
 // (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 const UnmaskVariant kUnmaskVariants[] = {
+    {k_unmask_v4<16, 8, true>, 16,
+     "v4 U16 streaming (aligned loads, DPP rotate) + pipelined 8-tile LDS window (next step's tile map and "
+     "records fetched during the current window's payload loads)"},
     {k_unmask_v3<16, false, true, 2>, 16,
-     "v3 U16 + LDS small-frame window; streaming path: aligned loads, wave-contiguous 16 KiB spans, DPP rotate"},
+     "v3 U16 + 4-tile LDS window; streaming path: aligned loads, wave-contiguous 16 KiB spans, DPP rotate"},
     {k_unmask<4>, 4, "v1 U4 grid-stride per-lane lookup"},
     {k_unmask_v2<16, false, true>, 16, "v2 U16 plain-load nt-store"},
     {k_unmask_v2<8, false, true>, 8, "v2 U8 plain-load nt-store"},
@@ -1551,7 +1752,8 @@ const UnmaskVariant kUnmaskVariants[] = {
     {k_unmask_v3<8, false, true>, 8, "v3 U8 + LDS window"},
     {k_unmask_v3<16, true, true>, 16, "v3 U16 + LDS window, nt-load nt-store"},
     {k_unmask_v3<16, false, true, 1>, 16, "v3 U16, aligned loads + DPP lane shift + alignbyte funnel"},
-    {k_unmask_v3<16, false, true>, 16, "v3 U16 + LDS small-frame window, unaligned loads (round-1 default before 0)"},
+    {k_unmask_v3<16, false, true>, 16, "v3 U16 + LDS small-frame window, unaligned loads"},
+    {k_unmask_v4<16, 4, true>, 16, "v4 with a 4-tile window"},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 

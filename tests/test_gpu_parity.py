@@ -304,3 +304,68 @@ def test_every_unmask_variant_big_frames_all_alignments(engine):
     f = got["frames"]
     big = f["length"] >= 16 * 4096
     assert len(set((f["src_off"][big] % 16).tolist())) == 16
+
+
+@pytest.mark.gpu
+def test_every_unmask_variant_small_frame_windows(engine):
+    """Each unmask variant over the window paths: random mixed frames
+    (0-3072 B, every header form, unmasked and masked) in many connections, a
+    run of 3000 empty frames between payloads (more frames per window than the
+    LDS table holds), and 20 000 small frames in one connection, at several
+    grid sizes (so workgroup runs end mid-window): bit-exact against the C
+    oracle."""
+    from gev_amd import _abi
+    rng = np.random.default_rng(4242)
+    streams = [random_stream(rng, int(rng.integers(1, 40)), max_len=3072) for _ in range(120)]
+    empties = b"".join(wo.encode_frame(b"", 2, True, 0, bool(k % 2), b"\x09\x08\x07\x06") for k in range(3000))
+    big = bytes(rng.integers(0, 256, 70000, dtype=np.uint8))
+    streams.append(wo.encode_frame(big, 2, True, 0, True, b"\x01\x02\x03\x04") + empties +
+                   wo.encode_frame(big[:5000], 2, True, 0, True, b"\x05\x06\x07\x08") + empties)
+    streams.append(b"".join(wo.encode_frame(bytes(rng.integers(0, 256, int(n), dtype=np.uint8)), 2, True, 0, True,
+                                            bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+                            for n in rng.integers(1, 200, 20000)))
+    arena, conns = pack_streams(streams)
+    i = 0
+    try:
+        while engine.variant_name(i) is not None:
+            engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, i)
+            for g in (0, 3, 64):
+                engine.set_tuning(_abi.TUNE_UNMASK_GRID, g)
+                assert_matches_oracle(engine, arena, conns, f"variant {i} grid {g}")
+            i += 1
+    finally:
+        engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 0)
+        engine.set_tuning(_abi.TUNE_UNMASK_GRID, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["c4", "c5"])
+def test_every_unmask_variant_device_synth(engine, cfg):
+    """Each unmask variant on a device-generated C4 / C5-shaped batch (a few
+    hundred MiB): decode(mask(P)) == P on every byte via the device verifier."""
+    import torch
+    import gev_amd
+    from gev_amd import _abi, workloads as w
+    lay = (w.config_c4(total_payload=192 << 20, n_conns=768, seed=31) if cfg == "c4"
+           else w.config_c5(n_conns=48, messages_per_conn=2, seed=32))
+    dev = torch.device("cuda", engine.device)
+    arena = torch.zeros(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    desc = torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev)
+    conns = torch.from_numpy(lay.conns.copy()).to(dev)
+    engine.synth(arena, desc, lay.n_frames, lay.seed)
+    out = engine.alloc_batch(lay.n_conns, lay.n_frames, lay.payload_padded)
+    i = 0
+    try:
+        while engine.variant_name(i) is not None:
+            engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, i)
+            out.payload.fill_(0xAB)
+            engine.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, lay.n_frames, lay.payload_padded)
+            mism = torch.zeros(1, dtype=torch.int64, device=dev)
+            engine.verify(desc, lay.n_frames, lay.seed, out, mism)
+            torch.cuda.synchronize()
+            s = out.summary_host()
+            assert int(s["frames"]) == lay.n_frames and int(s["payload_len"]) == lay.payload_len, i
+            assert int(mism.item()) == 0, (i, engine.variant_name(i))
+            i += 1
+    finally:
+        engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 0)

@@ -38,7 +38,7 @@ def main():
 
     dev = torch.device("cuda", 0)
     eng = gev_amd.Engine(0)
-    lay = bench.build_layout(args.config, 0, args.conns)
+    lay, _ = bench.build_layout(args.config, 0, args.conns)
     if args.align_payload:
         # L = 65538 (16-byte multiple frame size with h = 14) and every stream
         # shifted by 2 bytes: payload starts land on 16-byte boundaries

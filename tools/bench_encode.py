@@ -32,7 +32,7 @@ def main():
 
     dev = torch.device("cuda", 0)
     eng = gev_amd.Engine(0)
-    lay = bench.build_layout(args.config, 0, None)
+    lay, _ = bench.build_layout(args.config, 0, None)
     arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
     arena[lay.arena_bytes:] = 0
     eng.synth(arena, torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev), lay.n_frames, lay.seed)

@@ -40,7 +40,7 @@ def main():
     if args.config == "c1":
         lay = w.uniform(65536, 16, 128, opcode=0x1, name="C1-shaped: 1048576 x 128 B masked text frames")
     else:
-        lay = bench.build_layout(args.config, 0, None)
+        lay, _ = bench.build_layout(args.config, 0, None)
     arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
     arena[lay.arena_bytes:] = 0
     eng.synth(arena, torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev), lay.n_frames, lay.seed)

@@ -37,14 +37,15 @@ def main():
     ap.add_argument("--tag", required=True)
     ap.add_argument("--config", required=True)
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--prefix", default="prof", help="gpurun_out/<prefix>_trace, <prefix>_pmc_* (scripts/gpu_profile.sh PREFIX)")
     args = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    stats = os.path.join(args.src, "prof_trace", "bench_kernel_stats.csv")
+    stats = os.path.join(args.src, f"{args.prefix}_trace", "bench_kernel_stats.csv")
     shutil.copy(stats, os.path.join(prof, f"{args.tag}_kernel_stats.csv"))
     per = collections.defaultdict(dict)
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        p = os.path.join(args.src, f"prof_pmc_{c}", "bench_counter_collection.csv")
+        p = os.path.join(args.src, f"{args.prefix}_pmc_{c}", "bench_counter_collection.csv")
         vals = collections.defaultdict(list)
         for r in csv.DictReader(open(p)):
             vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
