@@ -124,6 +124,8 @@ def main():
     ap.add_argument("--cpu-threads-multi", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--copy-reps", type=int, default=5, help="streaming-copy ceiling reps (0 = skip)")
+    ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
+    ap.add_argument("--unmask-variant", type=int, default=None, help="A/B: unmask kernel variant")
     args = ap.parse_args()
 
     import numpy as np
@@ -142,6 +144,11 @@ def main():
     dist.init(dist.backend(), dev)  # RCCL over xGMI when WORLD_SIZE > 1
 
     eng = gev_amd.Engine(gpu)
+    from gev_amd import _abi
+    if args.walk_variant is not None:
+        eng.set_tuning(_abi.TUNE_WALK_VARIANT, args.walk_variant)
+    if args.unmask_variant is not None:
+        eng.set_tuning(_abi.TUNE_UNMASK_VARIANT, args.unmask_variant)
     t_setup = time.time()
     scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
     lay, glob = build_layout(args.config, rank, args.conns, world, scaling)

@@ -44,6 +44,7 @@ HANDLER_ECHO_TEXT = 2
 TUNE_UNMASK_VARIANT = 1
 TUNE_UNMASK_GRID = 2
 TUNE_ENCODE_VARIANT = 3
+TUNE_WALK_VARIANT = 4
 
 IN_PAD = 64
 PAYLOAD_ALIGN = 16

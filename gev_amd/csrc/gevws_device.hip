@@ -38,6 +38,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 namespace {
 
 constexpr int kWalkBlock = 256;
+// The counting walk and the per-connection bases run one wave per workgroup
+// over `cpb` <= 64 connections each: small batches spread their few chains
+// over every CU (one chain's dependent loads share a CU's memory pipeline with
+// fewer others), big ones keep 64 per workgroup.
+constexpr int kCountBlock = 64;
 constexpr int kScanBlock = 1024;
 constexpr int kUnmaskBlock = 256;
 constexpr uint64_t kTile = GEVWS_TILE;
@@ -186,15 +191,44 @@ __device__ __forceinline__ bool entry_slots(const gevws_conn_in* __restrict__ co
   return base + cap <= n_entries;
 }
 
-__global__ __launch_bounds__(kWalkBlock) void k_walk_count(const uint8_t* __restrict__ in,
-                                                           const gevws_conn_in* __restrict__ conns,
-                                                           uint32_t n, gevws_conn_out* __restrict__ cout,
-                                                           uint64_t* __restrict__ blk,
-                                                           WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                           uint32_t gshift) {
-  const uint32_t c = blockIdx.x * kWalkBlock + threadIdx.x;
+// The counting walk's header parse (read.go:19-84 + the protocol.go:47 gate)
+// on the 16-byte window at a frame start with `avail` bytes buffered from it:
+// OK, NEED_MORE (fewer than 6 / header / payload bytes) or ERR_LEN_MSB.
+__device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t avail, uint32_t& meta, uint32_t& hlen,
+                                          uint64_t& L, uint32_t& key) {
+  const uint32_t b1 = (uint32_t)(lo >> 8) & 0xffu;
+  const uint32_t masked = b1 >> 7, len7 = b1 & 0x7fu;
+  const bool e16 = len7 == 126, e64 = len7 == 127;
+  hlen = 2 + (e64 ? 8u : (e16 ? 2u : 0u)) + 4 * masked;
+  const uint64_t L64 = __builtin_bswap64((lo >> 16) | (hi << 48));
+  const uint64_t L16 = (((lo >> 16) & 0xff) << 8) | ((lo >> 24) & 0xff);
+  L = e64 ? L64 : (e16 ? L16 : (uint64_t)len7);
+  key = (e64 ? (uint32_t)(hi >> 16) : (e16 ? (uint32_t)(lo >> 32) : (uint32_t)(lo >> 16))) & (0u - masked);
+  meta = ((uint32_t)lo & 0xffu) | (masked << 8) | (hlen << 16);
+  const bool have_hdr = avail >= 6 && avail >= hlen;
+  if (have_hdr && e64 && (L64 >> 63)) return GEVWS_ERR_LEN_MSB;
+  return (have_hdr && avail - hlen >= L) ? GEVWS_OK : GEVWS_NEED_MORE;
+}
+
+// D > 0: uniform-stream speculation.  After three consecutive frames of equal
+// size F the lane requests the windows at pos, pos + F, ..., pos + (D-1)F
+// (within the stream) at once and parses them in order while the frames keep
+// size F, so a run of equal-size frames costs one memory latency per D frames
+// instead of one per frame.  The first frame of another size ends the batch
+// (the windows after it are dropped) and the walk goes on from the true
+// position, so the result never depends on the guess.  Requiring three equal
+// frames keeps the batch path (and the wave divergence it costs) out of
+// mixed-size traffic.
+template <int D>
+__global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
+                                                            const gevws_conn_in* __restrict__ conns,
+                                                            uint32_t n, gevws_conn_out* __restrict__ cout,
+                                                            uint64_t* __restrict__ blk,
+                                                            WalkEntry* __restrict__ entries, uint64_t n_entries,
+                                                            uint32_t gshift, uint32_t cpb) {
+  const uint32_t c = blockIdx.x * cpb + threadIdx.x;
   uint64_t nf = 0, pb = 0, pl = 0, err = 0;
-  if (c < n) {
+  if (threadIdx.x < cpb && c < n) {
     const gevws_conn_in ci = conns[c];
     const uint8_t* s = in + ci.off;
     uint64_t pos = 0;
@@ -212,6 +246,20 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_count(const uint8_t* __rest
     uint64_t lo, hi;
     load_window(s, lo, hi);
     *sink = WalkEntry{0, 0, 0, 0};
+    uint64_t prev_fsz = 0;  // speculation (D > 0): size of the last frame and the run of equal sizes
+    uint32_t run = 0;
+    auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
+      rec = rec && nf < ecap;
+      WalkEntry e;
+      e.pos = (uint32_t)p;
+      e.mask = key;
+      e.len = (uint32_t)L;
+      e.meta = meta;
+      *(rec ? entries + ebase + nf : sink) = e;
+      ++nf;
+      pb += round16(L);
+      pl += L;
+    };
     for (;;) {
       // parse_header without branches (one exit test per frame): the chain
       // is latency-bound at about one wave per SIMD, so every instruction
@@ -232,20 +280,63 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_count(const uint8_t* __rest
         if (have_hdr && msb) { st = GEVWS_ERR_LEN_MSB; err = 1; }
         break;
       }
-      const uint64_t next = pos + hlen + L;
+      const uint64_t fsz = hlen + L;
+      const uint64_t next = pos + fsz;
       const uint32_t meta = ((uint32_t)lo & 0xffu) | (masked << 8) | (hlen << 16);  // before lo is reloaded
       load_window(s + next, lo, hi);
-      rec = rec && nf < ecap;
-      WalkEntry e;
-      e.pos = (uint32_t)pos;
-      e.mask = key;
-      e.len = (uint32_t)L;
-      e.meta = meta;
-      *(rec ? entries + ebase + nf : sink) = e;
-      ++nf;
-      pb += round16(L);
-      pl += L;
+      put_entry(pos, key, L, meta);
       pos = next;
+      if constexpr (D > 0) {
+        run = fsz == prev_fsz ? run + 1 : 1;
+        prev_fsz = fsz;
+        if (run >= 3 && pos + fsz <= ci.len) {
+          // third equal frame in a row: take the following frames in batches
+          // of D windows at stride fsz while their size stays fsz; (lo, hi),
+          // in flight, is the window at pos
+          bool fail = false;
+          for (;;) {
+            // unconditional loads (addresses clamped to the stream end: 16
+            // bytes at any q <= len stay inside GEVWS_IN_PAD); the first qn
+            // windows are real
+            uint64_t qlo[D], qhi[D];
+#pragma unroll
+            for (int j = 1; j < D; ++j) {
+              const uint64_t q = pos + (uint64_t)j * fsz;
+              load_window(s + (q <= ci.len ? q : ci.len), qlo[j], qhi[j]);
+            }
+            qlo[0] = lo;
+            qhi[0] = hi;
+            const uint64_t room = (ci.len - pos) / fsz + 1;
+            const uint32_t qn = room < (uint64_t)D ? (uint32_t)room : (uint32_t)D;
+            bool stop = false;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+              if (!stop && (uint32_t)j < qn) {
+                uint32_t m2, h2, k2;
+                uint64_t L2;
+                const int r = walk_parse(qlo[j], qhi[j], ci.len - pos, m2, h2, L2, k2);
+                if (r != GEVWS_OK) {
+                  if (r == GEVWS_ERR_LEN_MSB) { st = GEVWS_ERR_LEN_MSB; err = 1; }
+                  fail = stop = true;
+                } else {
+                  put_entry(pos, k2, L2, m2);
+                  pos += h2 + L2;
+                  if (h2 + L2 != fsz) {
+                    stop = true;
+                    run = 1;
+                    prev_fsz = h2 + L2;
+                  }
+                }
+              }
+            }
+            if (fail) break;
+            load_window(s + pos, lo, hi);  // the next batch's first window, or the chain's next header
+            if (stop || qn < (uint32_t)D || pos + fsz > ci.len) break;
+          }
+          if (fail) break;
+          *sink = WalkEntry{0, 0, 0, 0};  // same [load, store] in flight at the loop head as the plain path
+        }
+      }
     }
     gevws_conn_out o;
     o.first_frame = rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
@@ -255,20 +346,12 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_count(const uint8_t* __rest
     o.status = st;
     cout[c] = o;
   }
-  // block partial sums
-  __shared__ uint64_t s_part[kBlkFields][kWalkBlock / 64];
+  // block partial sums (one wave)
   const uint64_t vals[kBlkFields] = {nf, pb, pl, err};
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < kBlkFields; ++k) {
     const uint64_t s = wave_sum(vals[k]);
-    if (lane == 0) s_part[k][w] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x < kBlkFields) {
-    uint64_t s = 0;
-    for (int j = 0; j < kWalkBlock / 64; ++j) s += s_part[threadIdx.x][j];
-    blk[(uint64_t)blockIdx.x * kBlkFields + threadIdx.x] = s;
+    if (threadIdx.x == 0) blk[(uint64_t)blockIdx.x * kBlkFields + k] = s;
   }
 }
 
@@ -306,22 +389,23 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict
 // ------------------------------------------------------------------ 3. walk (emit)
 // 3a. per-connection bases: block-level exclusive scan of (frames, arena bytes)
 // on top of the scanned block partials.
-__global__ __launch_bounds__(kWalkBlock) void k_walk_bases(uint32_t n, gevws_conn_out* __restrict__ cout,
-                                                           const uint64_t* __restrict__ blk,
-                                                           const gevws_summary* __restrict__ sum,
-                                                           uint8_t* __restrict__ rec_flags) {
+__global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_conn_out* __restrict__ cout,
+                                                            const uint64_t* __restrict__ blk,
+                                                            const gevws_summary* __restrict__ sum,
+                                                            uint8_t* __restrict__ rec_flags, uint32_t cpb) {
   if (sum->status != GEVWS_OK) return;  // capacity error: nothing written
-  const uint32_t c = blockIdx.x * kWalkBlock + threadIdx.x;
+  const uint32_t c = blockIdx.x * cpb + threadIdx.x;
+  const bool active = threadIdx.x < cpb && c < n;
   uint64_t v[2] = {0, 0};
   gevws_conn_out o;
-  if (c < n) {
+  if (active) {
     o = cout[c];
     v[0] = o.nframes;
     v[1] = o.payload_base;  // this connection's arena bytes (k_walk_count)
   }
   uint64_t ex[2], tot[2];
-  block_excl_scan<kWalkBlock, 2>(v, ex, tot);
-  if (c >= n) return;
+  block_excl_scan<kCountBlock, 2>(v, ex, tot);
+  if (!active) return;
   rec_flags[c] = o.first_frame != 0 ? 1 : 0;  // k_walk_count's "entries recorded" flag
   o.first_frame = blk[(uint64_t)blockIdx.x * kBlkFields + 0] + ex[0];
   o.payload_base = blk[(uint64_t)blockIdx.x * kBlkFields + 1] + ex[1];
@@ -1664,6 +1748,7 @@ struct gevws_ctx {
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
   int encode_variant = 0;  // 0 = aligned-load streaming, 1 = unaligned loads
+  int walk_variant = 0;    // 0 = uniform-stream speculation (8 windows), 1 = plain chain walk
   // Scratch is per context: calls on a different stream than the previous one
   // first wait for it (one in-flight batch per context; use one context per
   // stream for concurrency).
@@ -1847,6 +1932,10 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       if (value < 0 || value > 1) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
+    case GEVWS_TUNE_WALK_VARIANT:
+      if (value < 0 || value > 1) return GEVWS_ERR_INVALID;
+      ctx->walk_variant = (int)value;
+      return GEVWS_OK;
     default:
       return GEVWS_ERR_INVALID;
   }
@@ -1892,7 +1981,11 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   if (max_frames > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;  // tile map holds 32-bit frame ids
   DeviceGuard g(ctx->device);
   hipStream_t st = pick_stream(ctx, stream);
-  const uint32_t nblk = (n_conns + kWalkBlock - 1) / kWalkBlock;
+  // connections per counting workgroup: 64, or fewer so a small batch covers every CU
+  const uint32_t ncu = (uint32_t)ctx->num_cus;
+  const uint32_t cpb = n_conns >= (uint32_t)kCountBlock * ncu ? (uint32_t)kCountBlock
+                                                              : (n_conns + ncu - 1) / ncu > 0 ? (n_conns + ncu - 1) / ncu : 1;
+  const uint32_t nblk = (n_conns + cpb - 1) / cpb;
   const uint64_t ntiles_cap = (payload_cap + kTile - 1) / kTile + 1;
   const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
   const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
@@ -1921,13 +2014,19 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     ev = ctx->evs[ctx->evs_used++].e;
     GEVWS_HIP(hipEventRecord(ev[0], st));
   }
-  if (nblk)
-    k_walk_count<<<nblk, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, n_entries, gshift);
+  if (nblk) {
+    if (ctx->walk_variant == 0)
+      k_walk_count<8><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, n_entries,
+                                                    gshift, cpb);
+    else
+      k_walk_count<0><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, n_entries,
+                                                    gshift, cpb);
+  }
   if (timed) GEVWS_HIP(hipEventRecord(ev[1], st));
   k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
   if (timed) GEVWS_HIP(hipEventRecord(ev[2], st));
   if (nblk) {
-    k_walk_bases<<<nblk, kWalkBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags);
+    k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb);
     uint64_t egrid = ((uint64_t)n_conns + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
     if (egrid > 8 * (uint64_t)ctx->num_cus) egrid = 8 * (uint64_t)ctx->num_cus;
     k_walk_emit<<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, d_summary, d_frames,

@@ -369,3 +369,61 @@ def test_every_unmask_variant_device_synth(engine, cfg):
             i += 1
     finally:
         engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 0)
+
+
+def _uniform_run_streams(rng, n_conns: int):
+    """Streams built from runs of equal-size frames (the walk's speculation
+    case): run lengths 1-40, frame sizes 2 B-9 KiB, masked/unmasked and long
+    length forms that alias to the same frame size, size changes mid-run,
+    truncated tails inside a run, and a LEN_MSB header inside a run."""
+    streams = []
+    for c in range(n_conns):
+        s = b""
+        for _ in range(int(rng.integers(1, 6))):
+            L = int(rng.choice([0, 1, 10, 14, 64, 125, 126, 300, 4096, 9000]))
+            masked = bool(rng.random() < 0.8)
+            form = None if rng.random() < 0.8 else 64
+            for _k in range(int(rng.integers(1, 41))):
+                s += wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), 2, True, 0, masked,
+                                     bytes(rng.integers(0, 256, 4, dtype=np.uint8)), form)
+            if rng.random() < 0.3:  # same frame size, other header: unmasked L+4 vs masked L
+                s += wo.encode_frame(bytes(rng.integers(0, 256, L + 4, dtype=np.uint8)), 1, True, 0, False,
+                                     b"\0" * 4, form)
+        kind = c % 5
+        if kind == 1:    # truncated frame of the run's size at the end
+            f = wo.encode_frame(bytes(rng.integers(0, 256, 64, dtype=np.uint8)), 2, True, 0, True, b"\1\2\3\4")
+            s += b"".join([f] * 9) + f[: int(rng.integers(1, len(f)))]
+        elif kind == 2:  # 64-bit length with the MSB set inside a run
+            f = wo.encode_frame(b"\x55" * 20, 2, True, 0, True, b"\5\6\7\x08", 64)
+            bad = bytearray(f)
+            bad[2] |= 0x80
+            s += f * 5 + bytes(bad) + f * 3
+        streams.append(s)
+    return streams
+
+
+@pytest.mark.gpu
+def test_walk_variants_uniform_runs(engine):
+    """Both header walks (speculative batches over equal-size runs, and the
+    plain chain walk) bit-exact against the C oracle on uniform-run streams,
+    on random mixes, and on C2-shaped uniform streams."""
+    from gev_amd import _abi
+    rng = np.random.default_rng(9090)
+    cases = [pack_streams(_uniform_run_streams(rng, 150)),
+             pack_streams([random_stream(rng, int(rng.integers(1, 30))) for _ in range(100)]),
+             pack_streams([b"".join(wo.encode_frame(bytes(rng.integers(0, 256, 4096, dtype=np.uint8)), 2, True, 0,
+                                                    True, bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+                                    for _ in range(n)) for n in (1, 2, 3, 8, 9, 16, 17, 64, 65)])]
+    try:
+        for v in (0, 1):
+            engine.set_tuning(_abi.TUNE_WALK_VARIANT, v)
+            for k, (arena, conns) in enumerate(cases):
+                assert_matches_oracle(engine, arena, conns, f"walk variant {v} case {k}")
+    finally:
+        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 0)
+
+
+def test_walk_variant_knob_bounds(engine):
+    from gev_amd import _abi
+    with pytest.raises(ValueError):
+        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 2)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="all")
     ap.add_argument("--grids", default="1024")
+    ap.add_argument("--walk-variants", default="0", help="header walk variants to cross with the unmask variants")
     ap.add_argument("--align-payload", action="store_true",
                     help="experiment: C3-sized frames whose payloads start 16-byte aligned in the input")
     args = ap.parse_args()
@@ -64,18 +65,20 @@ def main():
     if args.variants != "all":
         variants = [int(x) for x in args.variants.split(",")]
     grids = [int(x) for x in args.grids.split(",")]
-    cfgs = [(v, g) for v in variants for g in grids]
+    walks = [int(x) for x in args.walk_variants.split(",")]
+    cfgs = [(v, g, wv) for v in variants for g in grids for wv in walks]
 
     # verify each configuration once
-    for v, g in cfgs:
+    for v, g, wv in cfgs:
         eng.set_tuning(_abi.TUNE_UNMASK_VARIANT, v)
         eng.set_tuning(_abi.TUNE_UNMASK_GRID, g)
+        eng.set_tuning(_abi.TUNE_WALK_VARIANT, wv)
         out.payload.zero_()
         eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, lay.n_frames, lay.payload_padded)
         mism = torch.zeros(1, dtype=torch.int64, device=dev)
         eng.verify(desc, lay.n_frames, lay.seed, out, mism)
         torch.cuda.synchronize()
-        assert int(mism.item()) == 0, (v, g, int(mism.item()))
+        assert int(mism.item()) == 0, (v, g, wv, int(mism.item()))
     print("[ab] all variants verified bit-exact", file=sys.stderr, flush=True)
 
     n_copy = min(lay.payload_padded, lay.arena_bytes)
@@ -92,16 +95,17 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         copy_ms.append(e0.elapsed_time(e1) / args.reps)
-        for v, g in cfgs:
+        for v, g, wv in cfgs:
             eng.set_tuning(_abi.TUNE_UNMASK_VARIANT, v)
             eng.set_tuning(_abi.TUNE_UNMASK_GRID, g)
+            eng.set_tuning(_abi.TUNE_WALK_VARIANT, wv)
             eng.timing()
             eng.set_timing(True)
             for _ in range(args.reps):
                 eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, lay.n_frames, lay.payload_padded)
             eng.set_timing(False)
             ms, calls = eng.timing()
-            res[(v, g)].append([x / calls for x in ms])
+            res[(v, g, wv)].append([x / calls for x in ms])
         print(f"[ab] round {r} done", file=sys.stderr, flush=True)
 
     cm = statistics.median(copy_ms)
@@ -122,11 +126,11 @@ def main():
               "copy_ceiling": {"ms": round(cm, 4), "GBps_rw": round(2 * n_copy / cm / 1e6, 1)},
               "stream_copy_ceiling": {"ms": round(sm, 4), "GBps_rw": round(2 * n2 / sm / 1e6, 1)},
               "variants": []}
-    for (v, g), rows in res.items():
+    for (v, g, wv), rows in res.items():
         um = [row[3] for row in rows]
         med = statistics.median(um)
         report["variants"].append({
-            "variant": v, "name": eng.variant_name(v), "grid": g,
+            "variant": v, "name": eng.variant_name(v), "grid": g, "walk_variant": wv,
             "unmask_ms_median": round(med, 4), "unmask_ms_min": round(min(um), 4),
             "GBps": round(alg / med / 1e6, 1), "frac_of_8TBps": round(alg / med / 1e6 / 8000, 4),
             "walk_count_ms": round(statistics.median(row[0] for row in rows), 4),
