@@ -218,7 +218,11 @@ __device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t ava
 // (the windows after it are dropped) and the walk goes on from the true
 // position, so the result never depends on the guess.  Requiring three equal
 // frames keeps the batch path (and the wave divergence it costs) out of
-// mixed-size traffic.
+// mixed-size traffic.  Measured (profiles/r01_ab_walk_*.json): the walk of
+// fixed-size traffic takes 17-25 % less time (C2, C3), mixed traffic 1-12 %
+// more (C4, C5: the longer loop body sits on a latency-bound chain), so it is
+// opt-in (GEVWS_TUNE_WALK_VARIANT 1) for servers that know their messages have
+// one size.
 template <int D>
 __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
                                                             const gevws_conn_in* __restrict__ conns,
@@ -289,7 +293,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       if constexpr (D > 0) {
         run = fsz == prev_fsz ? run + 1 : 1;
         prev_fsz = fsz;
-        if (run >= 3 && pos + fsz <= ci.len) {
+        if (run >= 3) {
           // third equal frame in a row: take the following frames in batches
           // of D windows at stride fsz while their size stays fsz; (lo, hi),
           // in flight, is the window at pos
@@ -299,15 +303,16 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
             // bytes at any q <= len stay inside GEVWS_IN_PAD); the first qn
             // windows are real
             uint64_t qlo[D], qhi[D];
+            uint32_t qn = 1;  // windows at positions <= len (pos itself is)
 #pragma unroll
             for (int j = 1; j < D; ++j) {
               const uint64_t q = pos + (uint64_t)j * fsz;
-              load_window(s + (q <= ci.len ? q : ci.len), qlo[j], qhi[j]);
+              const bool in = q <= ci.len;
+              qn += in ? 1u : 0u;
+              load_window(s + (in ? q : ci.len), qlo[j], qhi[j]);
             }
             qlo[0] = lo;
             qhi[0] = hi;
-            const uint64_t room = (ci.len - pos) / fsz + 1;
-            const uint32_t qn = room < (uint64_t)D ? (uint32_t)room : (uint32_t)D;
             bool stop = false;
 #pragma unroll
             for (int j = 0; j < D; ++j) {
@@ -454,23 +459,33 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
       uint64_t ebase = 0, ecap = 0;
       entry_slots(conns, n, (uint32_t)c, ci, n_entries, gshift, ebase, ecap);
       uint64_t carry = o.payload_base;
-      for (uint64_t k0 = 0; k0 < cnt; k0 += 64) {
-        const uint64_t k = k0 + lane;
-        const bool valid = k < cnt;
-        WalkEntry q = {0, 0, 0, 0};
-        if (valid) q = entries[ebase + k];
-        const uint64_t padded = valid ? round16(q.len) : 0;
-        const uint64_t incl = wave_incl_scan(padded);
-        if (valid) {
-          DevHdr h;
-          h.b0 = q.meta & 0xff;
-          h.masked = (q.meta >> 8) & 1;
-          h.hlen = q.meta >> 16;
-          h.mask = q.mask;
-          h.length = q.len;
-          emit_record(frames, tile_first, o.first_frame + k, carry + incl - padded, ci.off + q.pos + h.hlen, h);
+      // kEmitU x 64 entries per round: their loads are all in flight before
+      // the first scan waits
+      constexpr int kEmitU = 4;
+      for (uint64_t k0 = 0; k0 < cnt; k0 += 64 * kEmitU) {
+        WalkEntry q[kEmitU];
+#pragma unroll
+        for (int u = 0; u < kEmitU; ++u) {
+          const uint64_t k = k0 + u * 64 + lane;
+          q[u] = k < cnt ? entries[ebase + k] : WalkEntry{0, 0, 0, 0};
         }
-        carry += __shfl(incl, 63, 64);
+#pragma unroll
+        for (int u = 0; u < kEmitU; ++u) {
+          const uint64_t k = k0 + u * 64 + lane;
+          const bool valid = k < cnt;
+          const uint64_t padded = valid ? round16(q[u].len) : 0;
+          const uint64_t incl = wave_incl_scan(padded);
+          if (valid) {
+            DevHdr h;
+            h.b0 = q[u].meta & 0xff;
+            h.masked = (q[u].meta >> 8) & 1;
+            h.hlen = q[u].meta >> 16;
+            h.mask = q[u].mask;
+            h.length = q[u].len;
+            emit_record(frames, tile_first, o.first_frame + k, carry + incl - padded, ci.off + q[u].pos + h.hlen, h);
+          }
+          carry += __shfl(incl, 63, 64);
+        }
       }
     }
   }
@@ -1748,7 +1763,7 @@ struct gevws_ctx {
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
   int encode_variant = 0;  // 0 = aligned-load streaming, 1 = unaligned loads
-  int walk_variant = 0;    // 0 = uniform-stream speculation (8 windows), 1 = plain chain walk
+  int walk_variant = 0;    // 0 = plain chain walk, 1 = with uniform-stream speculation (8 windows)
   // Scratch is per context: calls on a different stream than the previous one
   // first wait for it (one in-flight batch per context; use one context per
   // stream for concurrency).
@@ -2015,7 +2030,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     GEVWS_HIP(hipEventRecord(ev[0], st));
   }
   if (nblk) {
-    if (ctx->walk_variant == 0)
+    if (ctx->walk_variant == 1)
       k_walk_count<8><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, n_entries,
                                                     gshift, cpb);
     else
