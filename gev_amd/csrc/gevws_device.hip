@@ -218,11 +218,10 @@ __device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t ava
 // (the windows after it are dropped) and the walk goes on from the true
 // position, so the result never depends on the guess.  Requiring three equal
 // frames keeps the batch path (and the wave divergence it costs) out of
-// mixed-size traffic.  Measured (profiles/r01_ab_walk_*.json): the walk of
-// fixed-size traffic takes 17-25 % less time (C2, C3), mixed traffic 1-12 %
-// more (C4, C5: the longer loop body sits on a latency-bound chain), so it is
-// opt-in (GEVWS_TUNE_WALK_VARIANT 1) for servers that know their messages have
-// one size.
+// mixed-size traffic.  Interleaved A/B against D = 0
+// (profiles/r01_ab_walk2_*.json): the walk of fixed-size traffic takes 23-28 %
+// less time (C2, C3), mixed traffic 0-5 % more (C4, C5: a longer loop body on
+// a latency-bound chain).  GEVWS_TUNE_WALK_VARIANT 1 selects D = 0.
 template <int D>
 __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
                                                             const gevws_conn_in* __restrict__ conns,
@@ -265,10 +264,10 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       pl += L;
     };
     for (;;) {
-      // parse_header without branches (one exit test per frame): the chain
-      // is latency-bound at about one wave per SIMD, so every instruction
-      // between the header load and the next one counts
-      const uint64_t avail = ci.len - pos;
+      // The chain is latency-bound (one load per frame, few lanes per SIMD):
+      // only the next frame's position is computed before its header load is
+      // issued -- at min(next, len), always inside the stream + GEVWS_IN_PAD
+      // -- and the checks run while that load is in flight.
       const uint32_t b1 = (uint32_t)(lo >> 8) & 0xffu;
       const uint32_t masked = b1 >> 7, len7 = b1 & 0x7fu;
       const bool e16 = len7 == 126, e64 = len7 == 127;
@@ -276,18 +275,20 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       const uint64_t L64 = __builtin_bswap64((lo >> 16) | (hi << 48));
       const uint64_t L16 = (((lo >> 16) & 0xff) << 8) | ((lo >> 24) & 0xff);
       const uint64_t L = e64 ? L64 : (e16 ? L16 : (uint64_t)len7);
-      const uint32_t key = (e64 ? (uint32_t)(hi >> 16) : (e16 ? (uint32_t)(lo >> 32) : (uint32_t)(lo >> 16))) &
-                           (0u - masked);
+      const uint64_t fsz = hlen + L;
+      const uint64_t next = pos + fsz;
+      const uint64_t lo0 = lo, hi0 = hi;
+      load_window(s + (next <= ci.len ? next : ci.len), lo, hi);  // (a wrapped next is <= len or clamped)
+      const uint64_t avail = ci.len - pos;
       const bool have_hdr = avail >= 6 && avail >= hlen;   // read.go:20-23, U1
       const bool msb = e64 && (L64 >> 63);                  // read.go:71-73
       if (!have_hdr || msb || avail - hlen < L) {           // protocol.go:47 gate
         if (have_hdr && msb) { st = GEVWS_ERR_LEN_MSB; err = 1; }
         break;
       }
-      const uint64_t fsz = hlen + L;
-      const uint64_t next = pos + fsz;
-      const uint32_t meta = ((uint32_t)lo & 0xffu) | (masked << 8) | (hlen << 16);  // before lo is reloaded
-      load_window(s + next, lo, hi);
+      const uint32_t key = (e64 ? (uint32_t)(hi0 >> 16) : (e16 ? (uint32_t)(lo0 >> 32) : (uint32_t)(lo0 >> 16))) &
+                           (0u - masked);
+      const uint32_t meta = ((uint32_t)lo0 & 0xffu) | (masked << 8) | (hlen << 16);
       put_entry(pos, key, L, meta);
       pos = next;
       if constexpr (D > 0) {
@@ -1763,7 +1764,7 @@ struct gevws_ctx {
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
   int encode_variant = 0;  // 0 = aligned-load streaming, 1 = unaligned loads
-  int walk_variant = 0;    // 0 = plain chain walk, 1 = with uniform-stream speculation (8 windows)
+  int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk
   // Scratch is per context: calls on a different stream than the previous one
   // first wait for it (one in-flight batch per context; use one context per
   // stream for concurrency).
@@ -2030,7 +2031,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     GEVWS_HIP(hipEventRecord(ev[0], st));
   }
   if (nblk) {
-    if (ctx->walk_variant == 1)
+    if (ctx->walk_variant == 0)
       k_walk_count<8><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, n_entries,
                                                     gshift, cpb);
     else
