@@ -98,7 +98,9 @@ def cpu_baseline(name: str, seconds: float, threads: int, vectorized: bool = Fal
 
 def load_traffic(config_name: str):
     """HBM bytes per unmask launch from a committed rocprofv3 --pmc pass (see
-    profiles/README.md), or None."""
+    profiles/README.md), or None.  The passes are taken at N = 1,
+    so the figure applies to a rank's launch only when that rank runs the same
+    batch (N = 1, or weak scaling)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
@@ -257,7 +259,7 @@ def main():
         "phases_ms": {"walk_count": round(mean_ms[0], 4), "scan": round(mean_ms[1], 4),
                       "walk_emit": round(mean_ms[2], 4), "unmask": round(unmask_ms, 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_traffic(args.config),
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": (load_traffic(args.config) if scaling == "weak" or world == 1 else None),
                      "kernel": "k_unmask", "algorithmic_bytes_per_launch": alg_bytes,
                      "pipeline_achieved": round(pipeline_gbps, 1),
                      "pipeline_frac": round(pipeline_gbps / HBM_PEAK_GBPS, 4),

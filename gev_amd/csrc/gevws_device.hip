@@ -1764,7 +1764,8 @@ struct gevws_ctx {
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
   int encode_variant = 0;  // 0 = aligned-load streaming, 1 = unaligned loads
-  int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk
+  int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
+                           // 2 = plain walk without the entry table (emit re-walks)
   // Scratch is per context: calls on a different stream than the previous one
   // first wait for it (one in-flight batch per context; use one context per
   // stream for concurrency).
@@ -1949,7 +1950,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_WALK_VARIANT:
-      if (value < 0 || value > 1) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 2) return GEVWS_ERR_INVALID;
       ctx->walk_variant = (int)value;
       return GEVWS_OK;
     default:
@@ -2030,13 +2031,16 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     ev = ctx->evs[ctx->evs_used++].e;
     GEVWS_HIP(hipEventRecord(ev[0], st));
   }
+  // walk variant 2 (measurement): no entry table -- the counting walk stores
+  // nothing per frame and the emit pass re-walks every chain
+  const uint64_t ne = ctx->walk_variant == 2 ? 0 : n_entries;
   if (nblk) {
     if (ctx->walk_variant == 0)
-      k_walk_count<8><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, n_entries,
-                                                    gshift, cpb);
+      k_walk_count<8><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
+                                                    cpb);
     else
-      k_walk_count<0><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, n_entries,
-                                                    gshift, cpb);
+      k_walk_count<0><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
+                                                    cpb);
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[1], st));
   k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
@@ -2046,7 +2050,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     uint64_t egrid = ((uint64_t)n_conns + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
     if (egrid > 8 * (uint64_t)ctx->num_cus) egrid = 8 * (uint64_t)ctx->num_cus;
     k_walk_emit<<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, d_summary, d_frames,
-                                                         tile_first, entries, n_entries, gshift, rec_flags);
+                                                         tile_first, entries, ne, gshift, rec_flags);
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[3], st));
   r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);

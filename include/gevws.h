@@ -125,7 +125,8 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto), GEVWS_TUNE_ENCODE_VARIANT
  * the encode kernel's streaming loads (0 = aligned + register realign,
  * 1 = unaligned), GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
- * uniform-stream speculation, 1 = plain chain walk). */
+ * uniform-stream speculation, 1 = plain chain walk, 2 = plain walk that
+ * records no per-frame entries, so the emit pass re-walks every chain). */
 #define GEVWS_TUNE_UNMASK_VARIANT 1
 #define GEVWS_TUNE_UNMASK_GRID 2
 #define GEVWS_TUNE_ENCODE_VARIANT 3
