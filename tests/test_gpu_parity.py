@@ -193,6 +193,34 @@ def test_c3_full_size_property(engine):
     _synth_decode_verify(engine, lay, check_slice_conns=1)
 
 
+def test_stream_over_4gib_and_small_frame_fallback(engine):
+    """A connection whose buffered stream exceeds 4 GiB (32-bit walk entries
+    cannot hold its offsets: the emit pass re-walks it) next to connections of
+    10-byte frames (more frames than entry slots: re-walked too) and ordinary
+    ones, in one batch: decode(mask(P)) == P on every byte."""
+    import numpy as np
+    from gev_amd import workloads as w
+    big = w.uniform(1, 65600, 65536, seed=5)  # 4.3 GB stream, h = 14
+    small = w.uniform(64, 500, 4, seed=6)
+    mid = w.uniform(8, 40, 3000, seed=7)
+    parts = [small, big, mid]
+    desc, conns, off = [], [], 0
+    for lay in parts:
+        d = lay.desc.copy()
+        d["hdr_off"] += np.uint64(off)
+        desc.append(d)
+        c = lay.conns.copy()
+        c[:, 0] += off
+        conns.append(c)
+        off += lay.arena_bytes
+    desc = np.concatenate(desc)
+    desc["mask"] = w.frame_masks(desc.shape[0], 11)
+    lay = w.Layout("4 GiB stream + tiny frames", desc, np.concatenate(conns), off,
+                   sum(p.payload_len for p in parts), sum(p.payload_padded for p in parts), 11)
+    assert lay.conns[64, 1] > 1 << 32
+    _synth_decode_verify(engine, lay, check_slice_conns=8)
+
+
 def test_c4_power_law_property(engine):
     from gev_amd import workloads
     _synth_decode_verify(engine, workloads.config_c4(total_payload=64 << 20, n_conns=512), check_slice_conns=8)
