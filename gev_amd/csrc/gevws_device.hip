@@ -1290,7 +1290,7 @@ __device__ __forceinline__ u128 byte_mask(int k0, int k1) {
 // header bytes from the frame's serialised header, payload bytes from ONE
 // unaligned 16-byte load per frame (all loads independent).
 __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
-                                              const int32_t* s_start, const int32_t* s_pend, const uint32_t* s_hlen,
+                                              const int32_t* s_start, const int32_t* s_pend, const uint8_t* s_hlen,
                                               const uint64_t* s_delta, const uint64_t* s_h0, const uint64_t* s_h1,
                                               const uint8_t* __restrict__ payload) {
   u128 acc = 0;
@@ -1319,7 +1319,11 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
   return u32x4_of(acc);
 }
 
-template <int U, bool AL>
+// COMPACT: a window's chunks that straddle a frame boundary (header bytes or
+// two frames' pieces) are queued in LDS and assembled afterwards by the whole
+// workgroup, one chunk per lane, instead of by the one or two lanes of each
+// wave that meet them while the other lanes of the wave wait.
+template <int U, bool AL, bool COMPACT>
 __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
@@ -1328,7 +1332,9 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
                                                          uint8_t* __restrict__ out, uint32_t big_grid) {
   __shared__ int32_t s_start[kEncWinFrames];  // wire start relative to the window, clamped >= -64
   __shared__ int32_t s_pend[kEncWinFrames];   // payload end relative to the window, clamped
-  __shared__ uint32_t s_hlen[kEncWinFrames];
+  __shared__ uint8_t s_hlen[kEncWinFrames];
+  __shared__ uint32_t s_bnd[COMPACT ? kWinTiles * kUnmaskBlock : 1];  // queued chunk: rel / 16 | frame << 16
+  __shared__ uint32_t s_nb;
   __shared__ uint64_t s_delta[kEncWinFrames];  // payload_off - out_off - hlen (mod 2^64)
   __shared__ uint64_t s_h0[kEncWinFrames];
   __shared__ uint64_t s_h1[kEncWinFrames];
@@ -1406,6 +1412,7 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
         s_h0[i] = lo;
         s_h1[i] = hi;
       }
+      if (COMPACT && threadIdx.x == 0) s_nb = 0;
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < kWinTiles; ++u) {
@@ -1417,12 +1424,27 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
           const uint32_t mid = (lo + hi + 1) >> 1;
           if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
         }
-        u32x4 x;
-        if (rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo])
-          x = ld16u(payload + (a + s_delta[lo]));  // interior of one payload
-        else
-          x = enc_assemble(rel, a, total, lo, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0, s_h1, payload);
-        __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + a));
+        if (rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo]) {  // interior of one payload
+          __builtin_nontemporal_store(ld16u(payload + (a + s_delta[lo])), reinterpret_cast<u32x4*>(out + a));
+        } else if constexpr (COMPACT) {
+          s_bnd[atomicAdd(&s_nb, 1u)] = ((uint32_t)rel >> 4) | (lo << 16);
+        } else {
+          const u32x4 x =
+              enc_assemble(rel, a, total, lo, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0, s_h1, payload);
+          __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + a));
+        }
+      }
+      if constexpr (COMPACT) {
+        __syncthreads();
+        const uint32_t nb = s_nb;
+        for (uint32_t i = threadIdx.x; i < nb; i += kUnmaskBlock) {
+          const uint32_t q = s_bnd[i];
+          const int32_t rel = (int32_t)((q & 0xffffu) << 4);
+          const uint64_t a = wbase + (uint64_t)rel;
+          const u32x4 x = enc_assemble(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
+                                       s_h1, payload);
+          __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + a));
+        }
       }
       t += wt;
       continue;
@@ -1763,7 +1785,8 @@ struct gevws_ctx {
   gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
-  int encode_variant = 0;  // 0 = aligned-load streaming, 1 = unaligned loads
+  int encode_variant = 0;  // 0 = aligned-load streaming + queued boundary chunks, 1 = unaligned loads,
+                           // 2 = aligned loads, per-lane boundary assembly
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
                            // 2 = plain walk without the entry table (emit re-walks)
   // Scratch is per context: calls on a different stream than the previous one
@@ -1946,7 +1969,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->unmask_grid = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_ENCODE_VARIANT:
-      if (value < 0 || value > 1) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 2) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_WALK_VARIANT:
@@ -2105,7 +2128,9 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   // no big-frame grid reduction here: every frame boundary takes the window
   // path, which needs 4 workgroups per CU to hide its latency (C3: 22.6 ms at
   // 4/CU vs 36 ms at 1/CU, profiles/r01_encode_*.json)
-  auto enc = ctx->encode_variant == 1 ? k_encode<4, false> : k_encode<4, true>;
+  auto enc = ctx->encode_variant == 1   ? k_encode<4, false, false>
+             : ctx->encode_variant == 2 ? k_encode<4, true, false>
+                                        : k_encode<4, true, true>;
   enc<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
                                                        0u);
   GEVWS_HIP(hipGetLastError());

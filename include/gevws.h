@@ -123,8 +123,10 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
 /* Tuning knobs for measurement (defaults are the tuned choice):
  * GEVWS_TUNE_UNMASK_VARIANT selects an unmask kernel variant (0 = default),
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto), GEVWS_TUNE_ENCODE_VARIANT
- * the encode kernel's streaming loads (0 = aligned + register realign,
- * 1 = unaligned), GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
+ * the encode kernel (0 = aligned loads + register realign while streaming,
+ * frame-boundary chunks queued and assembled by the whole workgroup;
+ * 1 = unaligned loads, boundary chunks assembled by the lane that meets
+ * them; 2 = aligned loads, per-lane assembly), GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
  * uniform-stream speculation, 1 = plain chain walk, 2 = plain walk that
  * records no per-frame entries, so the emit pass re-walks every chain). */
 #define GEVWS_TUNE_UNMASK_VARIANT 1

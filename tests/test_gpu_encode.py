@@ -47,9 +47,11 @@ def test_encode_golden(engine, golden):
     assert np.array_equal(got, g["wire"])
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_encode_random_and_tiny_frames(engine, variant):
-    """variant 0: aligned-load streaming (default); 1: unaligned loads."""
+    """variant 0: aligned-load streaming + boundary chunks assembled by the
+    whole workgroup (default); 1: unaligned loads, per-lane assembly;
+    2: aligned-load streaming, per-lane assembly."""
     from gev_amd import _abi
     engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, variant)
     try:
