@@ -50,7 +50,10 @@ def build_layout(name: str, rank: int, conns: int | None, world: int = 1, scalin
         glob, _ = build_layout(name, 0, conns)
         return w.shard_lpt(glob, rank, world), glob
     seed = rank_seed(0x67657600, rank)
-    if name == "c3":
+    if name == "c1":  # device-resident batch of the C1 plumbing config's frames (128 B masked text)
+        lay = w.uniform(conns or 65536, 16, 128, opcode=0x1, seed=seed,
+                        name="C1-shaped: 1048576 x 128 B masked text frames")
+    elif name == "c3":
         lay = w.config_c3(seed=seed, n_conns=conns or 16384)
     elif name == "c2":
         lay = w.config_c2(seed=seed, n_conns=conns or 4096)
@@ -77,6 +80,9 @@ def cpu_sample_layout(name: str, mib: int = 256):
                          name=f"{n} x 4 KiB masked binary frames ({mib} MiB payload)")
     if name == "c4":
         return w.config_c4(total_payload=mib << 20, n_conns=4 * mib, seed=1)
+    if name == "c1":
+        n = mib * 8192
+        return w.uniform(n // 16, 16, 128, opcode=0x1, seed=1, name=f"{n} x 128 B masked text frames ({mib} MiB payload)")
     return w.config_c5(n_conns=mib // 8, seed=1)
 
 
@@ -117,7 +123,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--conns", type=int, default=None)
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="weak: each GPU its own batch of the config's shape (default for c2/c3/c5); "

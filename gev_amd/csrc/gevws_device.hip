@@ -460,33 +460,23 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
       uint64_t ebase = 0, ecap = 0;
       entry_slots(conns, n, (uint32_t)c, ci, n_entries, gshift, ebase, ecap);
       uint64_t carry = o.payload_base;
-      // kEmitU x 64 entries per round: their loads are all in flight before
-      // the first scan waits
-      constexpr int kEmitU = 4;
-      for (uint64_t k0 = 0; k0 < cnt; k0 += 64 * kEmitU) {
-        WalkEntry q[kEmitU];
-#pragma unroll
-        for (int u = 0; u < kEmitU; ++u) {
-          const uint64_t k = k0 + u * 64 + lane;
-          q[u] = k < cnt ? entries[ebase + k] : WalkEntry{0, 0, 0, 0};
+      for (uint64_t k0 = 0; k0 < cnt; k0 += 64) {
+        const uint64_t k = k0 + lane;
+        const bool valid = k < cnt;
+        WalkEntry q = {0, 0, 0, 0};
+        if (valid) q = entries[ebase + k];
+        const uint64_t padded = valid ? round16(q.len) : 0;
+        const uint64_t incl = wave_incl_scan(padded);
+        if (valid) {
+          DevHdr h;
+          h.b0 = q.meta & 0xff;
+          h.masked = (q.meta >> 8) & 1;
+          h.hlen = q.meta >> 16;
+          h.mask = q.mask;
+          h.length = q.len;
+          emit_record(frames, tile_first, o.first_frame + k, carry + incl - padded, ci.off + q.pos + h.hlen, h);
         }
-#pragma unroll
-        for (int u = 0; u < kEmitU; ++u) {
-          const uint64_t k = k0 + u * 64 + lane;
-          const bool valid = k < cnt;
-          const uint64_t padded = valid ? round16(q[u].len) : 0;
-          const uint64_t incl = wave_incl_scan(padded);
-          if (valid) {
-            DevHdr h;
-            h.b0 = q[u].meta & 0xff;
-            h.masked = (q[u].meta >> 8) & 1;
-            h.hlen = q[u].meta >> 16;
-            h.mask = q[u].mask;
-            h.length = q[u].len;
-            emit_record(frames, tile_first, o.first_frame + k, carry + incl - padded, ci.off + q[u].pos + h.hlen, h);
-          }
-          carry += __shfl(incl, 63, 64);
-        }
+        carry += __shfl(incl, 63, 64);
       }
     }
   }
@@ -869,7 +859,7 @@ __device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint
   }
 }
 
-template <int U, bool NTL, bool NTS, int AL = 0>
+template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles>
 __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __restrict__ in,
                                                             const gevws_frame* __restrict__ frames,
                                                             const uint32_t* __restrict__ tile_first,
@@ -909,7 +899,7 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
       continue;
     }
     // ---- window path
-    const uint64_t wt = (tend - t) < (uint64_t)kWinTiles ? (tend - t) : (uint64_t)kWinTiles;
+    const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
     const uint64_t wend_t = t + wt;
     const uint64_t wbase = base;
     const uint64_t f_lo = tile_first[t];
@@ -930,11 +920,11 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
         s_key[i] = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
       }
       __syncthreads();
-      u32x4 v[kWinTiles];
-      uint32_t key[kWinTiles];
-      int32_t rem[kWinTiles];
+      u32x4 v[WT];
+      uint32_t key[WT];
+      int32_t rem[WT];
 #pragma unroll
-      for (int u = 0; u < kWinTiles; ++u) {
+      for (int u = 0; u < WT; ++u) {
         const uint32_t rel = (uint32_t)(u * kTile) + lane_off;
         const uint64_t p = wbase + rel;
         rem[u] = 0;
@@ -952,7 +942,7 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
         }
       }
 #pragma unroll
-      for (int u = 0; u < kWinTiles; ++u) {
+      for (int u = 0; u < WT; ++u) {
         if (rem[u] > 0) {
           u32x4 x = v[u] ^ key[u];
           if (rem[u] < 16) x = keep_bytes(x, rem[u]);
@@ -1879,6 +1869,7 @@ const UnmaskVariant kUnmaskVariants[] = {
     {k_unmask_v3<16, false, true, 1>, 16, "v3 U16, aligned loads + DPP lane shift + alignbyte funnel"},
     {k_unmask_v3<16, false, true>, 16, "v3 U16 + LDS small-frame window, unaligned loads"},
     {k_unmask_v4<16, 4, true>, 16, "v4 with a 4-tile window"},
+    {k_unmask_v3<16, false, true, 2, 8>, 16, "v3 with an 8-tile window (no pipelining)"},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 

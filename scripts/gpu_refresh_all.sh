@@ -16,3 +16,10 @@ for c in c2 c4 c5; do
 done
 PREFIX=prof_c3 bash scripts/gpu_profile.sh || exit $?
 PREFIX=prof_c4 BENCH_ARGS="--config c4" STEPS=5 bash scripts/gpu_profile.sh || exit $?
+# outbound encode and the device server step (decode + dispatch + encode)
+for c in c3 c2 c5 c4; do
+  run enc_$c 600 python tools/bench_encode.py --config $c --reps 5 || exit $?
+done
+for c in c1 c2 c5 c3; do
+  run srv_$c 600 python tools/bench_server.py --config $c --reps 5 || exit $?
+done

@@ -27,6 +27,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c1")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default="",
+                    help="A/B: comma list of wW.eE (header walk variant W, encode variant E), interleaved rounds, "
+                         "with per-stage times")
+    ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -97,6 +101,38 @@ def main():
             h = 2 if L <= 125 else (4 if L <= 0xFFFF else 10)
             o, po = int(offs[g]), int(fr["payload_off"][g])
             assert torch.equal(wire[o + h:o + h + L], out.payload[po:po + L])
+    if args.variants:
+        # interleaved A/B with per-stage event times (decode, dispatch, encode)
+        from gev_amd import _abi
+        combos = [tuple(int(x[1:]) for x in v.split(".")) for v in args.variants.split(",")]
+        res = {c: [] for c in combos}
+        for _ in range(args.rounds):
+            for c in combos:
+                eng.set_tuning(_abi.TUNE_WALK_VARIANT, c[0])
+                eng.set_tuning(_abi.TUNE_ENCODE_VARIANT, c[1])
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                acc = [0.0, 0.0, 0.0]
+                for _r in range(args.reps):
+                    ev[0].record()
+                    eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, n, lay.payload_padded)
+                    ev[1].record()
+                    eng.dispatch_async(out.frames, n, gev_amd._abi.HANDLER_ECHO_BINARY, out.payload, aux_off,
+                                       aux_cap, replies, reply_of, dsum)
+                    ev[2].record()
+                    eng.encode_async(replies, n, out.payload, wire, wire_cap, off, esum)
+                    ev[3].record()
+                    torch.cuda.synchronize()
+                    for k in range(3):
+                        acc[k] += ev[k].elapsed_time(ev[k + 1])
+                res[c].append([a / args.reps for a in acc])
+        eng.set_tuning(_abi.TUNE_WALK_VARIANT, 0)
+        eng.set_tuning(_abi.TUNE_ENCODE_VARIANT, 0)
+        for c, rows in res.items():
+            med = [sorted(r[k] for r in rows)[len(rows) // 2] for k in range(3)]
+            print(json.dumps({"workload": lay.name, "walk_variant": c[0], "encode_variant": c[1],
+                              "decode_ms": round(med[0], 4), "dispatch_ms": round(med[1], 4),
+                              "encode_ms": round(med[2], 4), "sum_ms": round(sum(med), 4)}))
+        return
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.reps):
