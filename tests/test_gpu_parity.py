@@ -367,14 +367,15 @@ def test_every_unmask_variant_small_frame_windows(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", ["c4", "c5"])
+@pytest.mark.parametrize("cfg", ["c1", "c4", "c5"])
 def test_every_unmask_variant_device_synth(engine, cfg):
-    """Each unmask variant on a device-generated C4 / C5-shaped batch (a few
-    hundred MiB): decode(mask(P)) == P on every byte via the device verifier."""
+    """Each unmask variant on a device-generated C1 / C4 / C5-shaped batch:
+    decode(mask(P)) == P on every byte via the device verifier."""
     import torch
     import gev_amd
     from gev_amd import _abi, workloads as w
     lay = (w.config_c4(total_payload=192 << 20, n_conns=768, seed=31) if cfg == "c4"
+           else w.uniform(8192, 16, 128, opcode=0x1, seed=33) if cfg == "c1"
            else w.config_c5(n_conns=48, messages_per_conn=2, seed=32))
     dev = torch.device("cuda", engine.device)
     arena = torch.zeros(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
