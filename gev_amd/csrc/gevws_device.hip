@@ -8,20 +8,21 @@
 //
 //   1. k_walk_count  one lane per connection walks its header chain
 //                    (ws.VirtualReadHeader, read.go:19-84, plus the
-//                    completeness gate, protocol.go:47) and counts frames,
-//                    payload bytes and consumed bytes; block partial sums.
+//                    completeness gate, protocol.go:47), counts frames,
+//                    payload bytes and consumed bytes and records a 16-byte
+//                    entry per frame; one wave per workgroup, block sums.
 //   2. k_scan_blocks one workgroup scans the block partials -> batch totals,
 //                    capacity check.
-//   3. k_walk_emit   block-level scan -> per-connection bases; the chain is
-//                    walked again (headers now L2/MALL-resident) writing one
-//                    32-byte record per frame and the output-tile -> first
-//                    frame map.
-//   4. k_unmask      the byte stream: every lane owns one 16-byte chunk of the
-//                    output arena, finds its frame through the tile map, loads
-//                    16 source bytes (unaligned global_load_dwordx4), XORs the
-//                    4-byte key (ws.Cipher, cipher.go:14-53; the payload phase
-//                    restarts at 0 per frame, protocol.go:54) and stores 16
-//                    aligned bytes.  HBM-bound: h + 2L bytes per frame.
+//   3. k_walk_bases  per-connection bases (block-level scan), then
+//      k_walk_emit   one wave per connection turns its entries into 32-byte
+//                    records (wave scan of the padded lengths -> payload
+//                    offsets) and the output-tile -> frame map.
+//   4. k_unmask_v4   the byte stream (ws.Cipher, cipher.go:14-53; the key phase
+//                    restarts at 0 per frame, protocol.go:54): contiguous runs
+//                    of 4 KiB output tiles per workgroup, streamed with aligned
+//                    loads while one frame covers 16 tiles, else an LDS window
+//                    of frame records searched per 16-byte chunk.  HBM-bound:
+//                    h + 2L bytes per frame.
 //
 // No MFMA: this is a byte stream, not a contraction.
 #include <hip/hip_runtime.h>
@@ -538,53 +539,6 @@ __device__ __forceinline__ u32x4 keep_bytes(u32x4 x, int64_t rem) {
   return x;
 }
 
-template <int U>
-__global__ __launch_bounds__(kUnmaskBlock) void k_unmask(const uint8_t* __restrict__ in,
-                                                         const gevws_frame* __restrict__ frames,
-                                                         const uint32_t* __restrict__ tile_first,
-                                                         const gevws_summary* __restrict__ sum,
-                                                         uint8_t* __restrict__ out, uint32_t big_grid) {
-  (void)big_grid;
-  if (sum->status != GEVWS_OK) return;
-  const uint64_t total = sum->payload_bytes;
-  const uint64_t nframes = sum->frames;
-  const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint32_t lane_off = threadIdx.x * 16;
-  for (uint64_t t0 = (uint64_t)blockIdx.x * U; t0 < ntiles; t0 += (uint64_t)gridDim.x * U) {
-    u32x4 v[U];
-    uint32_t key[U];
-    int64_t rem[U];
-    uint64_t p[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t t = t0 + u;
-      p[u] = t * kTile + lane_off;
-      rem[u] = 0;
-      key[u] = 0;
-      v[u] = u32x4{0, 0, 0, 0};
-      if (t < ntiles && p[u] < total) {
-        const uint64_t f = find_frame(frames, tile_first, t, ntiles, nframes, p[u]);
-        const gevws_frame* fr = frames + f;
-        const uint64_t rel = p[u] - fr->payload_off;
-        rem[u] = fr->hdr.length - (int64_t)rel;
-        uint32_t k;
-        memcpy(&k, fr->hdr.mask, 4);
-        key[u] = fr->hdr.masked ? k : 0u;
-        v[u] = ld16u(in + fr->src_off + rel);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (rem[u] > 0) {
-        u32x4 x = v[u] ^ key[u];  // payload phase is 0 mod 4 at every 16-byte chunk
-        if (rem[u] < 16) x = keep_bytes(x, rem[u]);
-        __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + p[u]));
-      }
-    }
-  }
-}
-
-
 template <bool NT>
 __device__ __forceinline__ u32x4 ld16u_stream(const uint8_t* p) {
   if constexpr (NT) {
@@ -601,83 +555,6 @@ __device__ __forceinline__ void st16_stream(uint8_t* p, u32x4 x) {
     __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
   } else {
     *reinterpret_cast<u32x4*>(p) = x;
-  }
-}
-
-// v2: each workgroup owns a contiguous run of output tiles.  The frame covering
-// the current position is cached in wave-uniform registers (scalar loads of
-// tile_first[t] and the 32-byte record), so while U consecutive tiles lie in
-// one frame the loop is pure streaming: U independent 16-byte loads per lane,
-// XOR, U aligned 16-byte stores.  Steps that straddle frames fall back to a
-// per-lane lookup (tile map + binary search) one tile at a time.
-template <int U, bool NTL, bool NTS>
-__global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v2(const uint8_t* __restrict__ in,
-                                                            const gevws_frame* __restrict__ frames,
-                                                            const uint32_t* __restrict__ tile_first,
-                                                            const gevws_summary* __restrict__ sum,
-                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
-  if (sum->status != GEVWS_OK) return;
-  const uint64_t total = sum->payload_bytes;
-  const uint64_t nframes = sum->frames;
-  const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint32_t groups = active_groups(total, nframes, big_grid);
-  if (blockIdx.x >= groups) return;
-  const uint64_t per = (ntiles + groups - 1) / groups;
-  uint64_t t = (uint64_t)blockIdx.x * per;
-  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
-  const uint32_t lane_off = threadIdx.x * 16;
-  uint64_t f_po = 0, f_end = 0, f_src = 0;
-  int64_t f_len = 0;
-  uint32_t f_key = 0;
-  while (t < tend) {
-    const uint64_t base = t * kTile;
-    if (base >= f_end) {  // wave-uniform: refresh the cached frame (scalar loads)
-      const uint64_t* rec = reinterpret_cast<const uint64_t*>(frames + tile_first[t]);
-      const uint64_t w0 = rec[0];  // fin, rsv, opcode, masked, mask[4]
-      f_len = (int64_t)rec[1];
-      f_po = rec[2];
-      f_src = rec[3];
-      f_end = f_po + round16((uint64_t)f_len);
-      f_key = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
-    }
-    if (t + U <= tend && base + U * kTile <= f_end) {
-      const uint64_t rel0 = base - f_po + lane_off;
-      const uint8_t* src = in + f_src + rel0;
-      uint8_t* dst = out + base + lane_off;
-      u32x4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16u_stream<NTL>(src + u * kTile);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        u32x4 x = v[u] ^ f_key;
-        const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
-        if (rem < 16) x = keep_bytes(x, rem);
-        st16_stream<NTS>(dst + u * kTile, x);
-      }
-      t += U;
-    } else {
-      const uint64_t p = base + lane_off;
-      if (p < total) {
-        uint64_t po = f_po, so = f_src;
-        int64_t L = f_len;
-        uint32_t key = f_key;
-        if (p >= f_end) {
-          const gevws_frame* fr = frames + find_frame(frames, tile_first, t, ntiles, nframes, p);
-          po = fr->payload_off;
-          so = fr->src_off;
-          L = fr->hdr.length;
-          uint32_t k;
-          memcpy(&k, fr->hdr.mask, 4);
-          key = fr->hdr.masked ? k : 0u;
-        }
-        const uint64_t rel = p - po;
-        u32x4 x = ld16u_stream<NTL>(in + so + rel) ^ key;
-        const int64_t rem = L - (int64_t)rel;
-        if (rem < 16) x = keep_bytes(x, rem);
-        st16_stream<NTS>(out + p, x);
-      }
-      t += 1;
-    }
   }
 }
 
@@ -743,11 +620,6 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __r
 constexpr int kWinTiles = 4;
 constexpr int kWinFrames = 1024;
 
-// Value of `x` in lane+1 (wave-wide shift by one lane; lane 63 gets 0):
-// DPP wave_shl:1, a VALU modifier on gfx9-class waves (no LDS crossbar).
-__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
-}
 // Value of `x` in lane+1, lane 63 gets lane 0's (DPP wave_rol:1).
 __device__ __forceinline__ u32x4 rot_next_lane(u32x4 x) {
   return u32x4{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[0], 0x134, 0xf, 0xf, false),
@@ -786,7 +658,7 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t m) {
 // arena inside one frame (payload offset f_po, source f_src, length f_len,
 // key f_key).  AL = 2: aligned loads, wave-contiguous spans, realigned in
 // registers (DPP lane rotate + v_alignbyte) when the source is misaligned;
-// AL = 1: aligned loads + DPP lane shift; AL = 0 / aligned source: plain loads.
+// AL = 0 / aligned source: plain (unaligned) loads.
 template <int U, bool NTL, bool NTS, int AL>
 __device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                             uint64_t base, uint64_t f_po, uint64_t f_src, int64_t f_len,
@@ -821,30 +693,6 @@ __device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint
       if (rem < 16) x = keep_bytes(x, rem);
       st16_stream<NTS>(d + u * 1024, x);
       r = rn;
-    }
-    return;
-  }
-  if (AL == 1 && mis != 0) {
-    // aligned loads: this lane's aligned chunk + the next lane's (DPP);
-    // lane 63 loads its successor chunk itself
-    const uint8_t* a = src - mis;
-    const bool last = (threadIdx.x & 63) == 63;
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * kTile);
-    u32x4 e[U];
-    if (last) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) e[u] = *reinterpret_cast<const u32x4*>(a + 16 + u * kTile);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      u32x4 nx = u32x4{from_next_lane(v[u][0]), from_next_lane(v[u][1]), from_next_lane(v[u][2]),
-                       from_next_lane(v[u][3])};
-      if (last) nx = e[u];
-      u32x4 x = funnel16(v[u], nx, mis) ^ f_key;
-      const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
-      if (rem < 16) x = keep_bytes(x, rem);
-      st16_stream<NTS>(dst + u * kTile, x);
     }
     return;
   }
@@ -1860,16 +1708,8 @@ const UnmaskVariant kUnmaskVariants[] = {
      "records fetched during the current window's payload loads)"},
     {k_unmask_v3<16, false, true, 2>, 16,
      "v3 U16 + 4-tile LDS window; streaming path: aligned loads, wave-contiguous 16 KiB spans, DPP rotate"},
-    {k_unmask<4>, 4, "v1 U4 grid-stride per-lane lookup"},
-    {k_unmask_v2<16, false, true>, 16, "v2 U16 plain-load nt-store"},
-    {k_unmask_v2<8, false, true>, 8, "v2 U8 plain-load nt-store"},
-    {k_unmask_v2<4, false, true>, 4, "v2 U4 plain-load nt-store"},
-    {k_unmask_v3<8, false, true>, 8, "v3 U8 + LDS window"},
-    {k_unmask_v3<16, true, true>, 16, "v3 U16 + LDS window, nt-load nt-store"},
-    {k_unmask_v3<16, false, true, 1>, 16, "v3 U16, aligned loads + DPP lane shift + alignbyte funnel"},
-    {k_unmask_v3<16, false, true>, 16, "v3 U16 + LDS small-frame window, unaligned loads"},
-    {k_unmask_v4<16, 4, true>, 16, "v4 with a 4-tile window"},
     {k_unmask_v3<16, false, true, 2, 8>, 16, "v3 with an 8-tile window (no pipelining)"},
+    {k_unmask_v3<16, false, true>, 16, "v3 U16 + 4-tile LDS window, unaligned streaming loads"},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 

@@ -12,7 +12,7 @@ step() {  # step <name> <timeout> <cmd...>
 step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x
 rc=$?; tail -15 $OUT/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
 step smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-step ab 600 python tools/ab_unmask.py --rounds 5 --reps 3 --grids 1024,2048,4096 || exit $?
+step ab 600 python tools/ab_unmask.py --rounds 5 --reps 3 --grids 0 || exit $?
 cat $OUT/ab.log
 step bench 400 python bench.py --steps 20 --warmup 3 || exit $?
 cat $OUT/bench.log
