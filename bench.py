@@ -190,8 +190,9 @@ def main():
 
     def step():
         eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, max_frames, cap)
-        torch.index_select(sum64, 0, sel, out=counts)
-        dist.reduce_counts(counts)  # decoded {frames, payload bytes, errors}, summed over GPUs
+        if world > 1:  # decoded {frames, payload bytes, errors}, summed over GPUs (N = 1: read after the loop)
+            torch.index_select(sum64, 0, sel, out=counts)
+            dist.reduce_counts(counts)
 
     for _ in range(args.warmup):
         step()
@@ -227,6 +228,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         copy_gbps = 2 * n_copy / (e0.elapsed_time(e1) / args.copy_reps / 1e3) / 1e9
+    if world == 1:
+        torch.index_select(sum64, 0, sel, out=counts)
     c = counts.cpu().numpy()
     frames_step, payload_step, errors = int(c[0]), int(c[1]), int(c[2])
     ms_step = elapsed / args.steps * 1e3
