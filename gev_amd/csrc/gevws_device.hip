@@ -229,14 +229,22 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
                                                             uint32_t n, gevws_conn_out* __restrict__ cout,
                                                             uint64_t* __restrict__ blk,
                                                             WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                            uint32_t gshift, uint32_t cpb) {
+                                                            uint32_t gshift, uint32_t cpb, uint64_t in_bytes) {
   const uint32_t c = blockIdx.x * cpb + threadIdx.x;
   uint64_t nf = 0, pb = 0, pl = 0, err = 0;
   if (threadIdx.x < cpb && c < n) {
-    const gevws_conn_in ci = conns[c];
+    gevws_conn_in ci = conns[c];
+    int32_t st = GEVWS_OK;
+    if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
+      // a stream outside the input arena: nothing is read, the connection
+      // reports GEVWS_ERR_INVALID (and counts as an error), the rest decode
+      ci.off = 0;
+      ci.len = 0;
+      st = GEVWS_ERR_INVALID;
+      err = 1;
+    }
     const uint8_t* s = in + ci.off;
     uint64_t pos = 0;
-    int32_t st = GEVWS_OK;
     uint64_t ebase = 0, ecap = 0;
     bool rec = entry_slots(conns, n, c, ci, n_entries, gshift, ebase, ecap);
     // software-pipelined: the next header's 16 bytes are requested before this
@@ -1891,10 +1899,10 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   if (nblk) {
     if (ctx->walk_variant == 0)
       k_walk_count<8><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
-                                                    cpb);
+                                                    cpb, in_bytes);
     else
       k_walk_count<0><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
-                                                    cpb);
+                                                    cpb, in_bytes);
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[1], st));
   k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);

@@ -92,7 +92,9 @@ typedef struct gevws_conn_out {
     uint64_t consumed;      /* bytes of complete frames (sum of h + L) */
     uint64_t payload_base;  /* arena offset of its first payload */
     uint32_t nframes;
-    int32_t status;         /* GEVWS_OK or GEVWS_ERR_LEN_MSB */
+    int32_t status;         /* GEVWS_OK, GEVWS_ERR_LEN_MSB, or GEVWS_ERR_INVALID when
+                               the stream [off, off + len) is not inside d_in[0, in_bytes)
+                               (nothing of it is read) */
 } gevws_conn_out;
 
 /* Batch totals (written on the device). */

@@ -96,6 +96,27 @@ def test_poisoned_connections_isolated(engine):
     assert int(got["summary"]["errors"]) == 2
 
 
+def test_streams_outside_the_arena_are_rejected(engine):
+    """A connection whose [off, off + len) leaves the input arena reads nothing
+    and reports GEVWS_ERR_INVALID; the connections around it decode exactly as
+    the oracle decodes them on their own."""
+    import gev_amd
+    good = [wo.encode_frame(b"abc" * k, 2, True, 0, True, b"\x01\x02\x03\x04") * 3 for k in (1, 50, 400)]
+    arena, conns = pack_streams(good)
+    n = len(arena)
+    bad = np.array([[n - 4, 10], [n + 100, 5], [1 << 62, 1 << 62]], np.int64)
+    table = np.concatenate([conns[:1], bad[:1], conns[1:2], bad[1:], conns[2:]])
+    got = host_result(gpu_decode(engine, arena, table))
+    st = got["conn_out"]["status"]
+    assert list(st) == [0, gev_amd.ERR_INVALID, 0, gev_amd.ERR_INVALID, gev_amd.ERR_INVALID, 0]
+    assert int(got["summary"]["errors"]) == 3
+    assert list(got["conn_out"]["nframes"][[1, 3, 4]]) == [0, 0, 0]
+    assert list(got["conn_out"]["consumed"][[1, 3, 4]]) == [0, 0, 0]
+    want = ref.decode_batch(np.frombuffer(arena, np.uint8).copy(), conns[:, 0], conns[:, 1])
+    assert got["frames"].tobytes() == want["frames"].tobytes()
+    assert np.array_equal(got["payload"], want["payload"])
+
+
 def test_capacity_error_reports_exact_sizes(engine):
     import torch
     rng = np.random.default_rng(14)
