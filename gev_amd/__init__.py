@@ -86,6 +86,52 @@ class Batch:
         return self.payload[:n].cpu().numpy()
 
 
+class _DevAddr:
+    """A bare device address with the one method the launch wrappers read."""
+    __slots__ = ("addr",)
+
+    def __init__(self, addr: int):
+        self.addr = addr
+
+    def data_ptr(self) -> int:
+        return self.addr
+
+
+class PinnedArena:
+    """Page-locked host memory mapped into the device (gevws_pinned_alloc):
+    `host` is a numpy uint8 view for the CPU, `at(off)` a device address a
+    decode can take as its payload arena, so the unmask kernel writes the
+    plaintext straight into host memory (host-ingress helper, not on the
+    reference path)."""
+
+    def __init__(self, nbytes: int):
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        st = lib.gevws_pinned_alloc(nbytes, ctypes.byref(h), ctypes.byref(d))
+        if st != OK:
+            raise RuntimeError(f"gevws_pinned_alloc({nbytes}): {status_string(st)}")
+        self.nbytes = nbytes
+        self._h, self._d = h.value, d.value
+        self.host = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self._h))
+
+    def at(self, offset: int = 0) -> _DevAddr:
+        if not 0 <= offset <= self.nbytes:
+            raise ValueError(f"PinnedArena.at({offset}): outside {self.nbytes} bytes")
+        return _DevAddr(self._d + offset)
+
+    def data_ptr(self) -> int:
+        return self._d
+
+    def close(self) -> None:
+        if self._h:
+            self.host = None
+            lib.gevws_pinned_free(self._h)
+            self._h = self._d = None
+
+    def __del__(self, _free=lib.gevws_pinned_free):  # bound now: module globals are gone at exit
+        if getattr(self, "_h", None):
+            _free(self._h)
+
+
 class Engine:
     """One gevws_ctx (one per event loop / rank) on one GPU."""
 

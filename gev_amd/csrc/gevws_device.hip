@@ -2017,6 +2017,28 @@ int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t
   return GEVWS_OK;
 }
 
+int gevws_pinned_alloc(uint64_t bytes, void** host_ptr, void** dev_ptr) {
+  if (!host_ptr || !dev_ptr || bytes == 0) return GEVWS_ERR_INVALID;
+  *host_ptr = nullptr;
+  *dev_ptr = nullptr;
+  void* h = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess || !h)
+    return GEVWS_ERR_DEVICE;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+    (void)hipHostFree(h);
+    return GEVWS_ERR_DEVICE;
+  }
+  *host_ptr = h;
+  *dev_ptr = d;
+  return GEVWS_OK;
+}
+
+int gevws_pinned_free(void* host_ptr) {
+  if (!host_ptr) return GEVWS_OK;
+  return hipHostFree(host_ptr) == hipSuccess ? GEVWS_OK : GEVWS_ERR_DEVICE;
+}
+
 int gevws_cipher_async(gevws_ctx* ctx, void* stream, uint8_t* d_p, uint64_t n, const uint8_t mask[4],
                        uint64_t offset) {
   if (!ctx || !mask || (n && !d_p)) return GEVWS_ERR_INVALID;

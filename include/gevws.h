@@ -230,6 +230,15 @@ int gevws_dispatch_async(gevws_ctx *ctx, void *stream, const gevws_frame *d_fram
 int gevws_copy_async(gevws_ctx *ctx, void *stream, uint8_t *d_dst, const uint8_t *d_src, uint64_t n,
                      uint32_t grid);
 
+/* Host-ingress helper, not on the reference path: `bytes` of page-locked host
+ * memory mapped into the device address space (hipHostMallocMapped).
+ * *host_ptr is the CPU address, *dev_ptr the address kernels use; passing
+ * *dev_ptr as gevws_decode_batch_async's d_payload makes the unmask kernel
+ * write the decoded payload straight into host memory over PCIe (no D2H copy
+ * of the arena).  GEVWS_ERR_DEVICE when the runtime refuses. */
+int gevws_pinned_alloc(uint64_t bytes, void **host_ptr, void **dev_ptr);
+int gevws_pinned_free(void *host_ptr);
+
 /* ws.Cipher(payload, mask, offset), plugins/websocket/ws/cipher.go:14-53, on a
  * device buffer in place: p[i] ^= mask[(offset+i) % 4]. */
 int gevws_cipher_async(gevws_ctx *ctx, void *stream, uint8_t *d_p, uint64_t n,

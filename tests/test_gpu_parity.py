@@ -117,6 +117,41 @@ def test_streams_outside_the_arena_are_rejected(engine):
     assert np.array_equal(got["payload"], want["payload"])
 
 
+def test_decode_into_mapped_host_arena(engine):
+    """The payload arena may be mapped pinned host memory (gevws_pinned_alloc):
+    the unmask kernel's writes land in host pages, byte-identical to the oracle,
+    and the bytes past the arena stay untouched."""
+    import torch
+    import gev_amd
+    rng = np.random.default_rng(21)
+    s = b"".join(wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), 2, True, 0, True,
+                                 bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+                 for L in (70001, 3, 0, 4096 * 5 + 9, 125, 65536))
+    arena, conns = pack_streams([random_stream(rng, 30), s, s[7:], random_stream(rng, 5)])
+    a = np.frombuffer(arena, np.uint8).copy()
+    want = ref.decode_batch(a, conns[:, 0], conns[:, 1])
+    cap = int(want["total_payload"])
+    dev = torch.device("cuda", engine.device)
+    d_in = torch.zeros(a.size + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    d_in[: a.size] = torch.from_numpy(a).to(dev)
+    d_conns = torch.from_numpy(conns.copy()).to(dev)
+    host = gev_amd.PinnedArena(cap + 4096)
+    try:
+        host.host[:] = 0xA5
+        o = engine.alloc_batch(conns.shape[0], want["frames"].shape[0], 0)
+        out = gev_amd.Batch(frames=o.frames, payload=host.at(0), conn_out=o.conn_out, summary=o.summary,
+                            n_conns=o.n_conns)
+        engine.decode_async(d_in, a.size, d_conns, conns.shape[0], out, want["frames"].shape[0], cap)
+        torch.cuda.synchronize()
+        sm = o.summary.cpu().numpy().view(gev_amd.SUMMARY_DTYPE)[0]
+        assert int(sm["status"]) == 0 and int(sm["payload_bytes"]) == cap
+        assert o.frames.cpu().numpy().tobytes() == want["frames"].tobytes()
+        assert np.array_equal(host.host[:cap], want["payload"])
+        assert (host.host[cap:] == 0xA5).all()
+    finally:
+        host.close()
+
+
 def test_capacity_error_reports_exact_sizes(engine):
     import torch
     rng = np.random.default_rng(14)
