@@ -158,6 +158,13 @@ __device__ __forceinline__ void block_excl_scan(const uint64_t (&v)[NV], uint64_
   __syncthreads();
 }
 
+// A value every lane of the wave loaded from the same address, kept in SGPRs
+// (the compiler cannot always prove such loads uniform once the loop stores).
+__device__ __forceinline__ uint32_t uniform32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  return (uint64_t)uniform32((uint32_t)x) | ((uint64_t)uniform32((uint32_t)(x >> 32)) << 32);
+}
+
 // ------------------------------------------------------------------ 1. walk (count)
 // Frame entries recorded by the counting walk so the emit pass need not
 // re-fetch every header line from HBM: 16 bytes per frame in a per-connection
@@ -178,18 +185,23 @@ struct WalkEntry {
 };
 static_assert(sizeof(WalkEntry) == 16, "one dwordx4 per entry");
 
-__device__ __forceinline__ bool entry_slots(const gevws_conn_in* __restrict__ conns, uint32_t n, uint32_t c,
-                                           const gevws_conn_in& ci, uint64_t n_entries, uint32_t gshift,
-                                           uint64_t& base, uint64_t& cap) {
+__device__ __forceinline__ bool entry_slots_of(const gevws_conn_in& prev, const gevws_conn_in& ci,
+                                              const gevws_conn_in& next, uint32_t n, uint32_t c, uint64_t n_entries,
+                                              uint32_t gshift, uint64_t& base, uint64_t& cap) {
   if (n_entries == 0 || ci.len >= (1ull << 32)) return false;
-  if (c > 0) {
-    const gevws_conn_in p = conns[c - 1];
-    if (p.off + p.len > ci.off) return false;
-  }
-  if (c + 1 < n && ci.off + ci.len > conns[c + 1].off) return false;
+  if (c > 0 && prev.off + prev.len > ci.off) return false;
+  if (c + 1 < n && ci.off + ci.len > next.off) return false;
   base = (ci.off >> gshift) + 2ull * c;
   cap = (ci.len >> gshift) + 2;
   return base + cap <= n_entries;
+}
+
+__device__ __forceinline__ bool entry_slots(const gevws_conn_in* __restrict__ conns, uint32_t n, uint32_t c,
+                                           const gevws_conn_in& ci, uint64_t n_entries, uint32_t gshift,
+                                           uint64_t& base, uint64_t& cap) {
+  const gevws_conn_in prev = conns[c > 0 ? c - 1 : c];
+  const gevws_conn_in next = conns[c + 1 < n ? c + 1 : c];
+  return entry_slots_of(prev, ci, next, n, c, n_entries, gshift, base, cap);
 }
 
 // The counting walk's header parse (read.go:19-84 + the protocol.go:47 gate)
@@ -448,6 +460,13 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
 // time (coalesced), wave prefix sum of their padded lengths -> payload
 // offsets, 64 contiguous 32-byte records per store.  Connections without
 // recorded entries are re-walked afterwards, one lane per connection.
+// U > 1: the entries of up to U rounds (64 each) are requested at once and
+// then turned into records round by round, so a connection of N frames costs
+// ceil(N / 64U) entry-load latencies instead of ceil(N / 64); rounds past the
+// connection's last frame are skipped (wave-uniform), their loads re-read the
+// last entry (one cached line).  Connections of <= 64 frames take one plain
+// round.
+template <int U>
 __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restrict__ in,
                                                           const gevws_conn_in* __restrict__ conns, uint32_t n,
                                                           const gevws_conn_out* __restrict__ cout,
@@ -460,32 +479,55 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
   const int lane = threadIdx.x & 63;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kWalkBlock / 64);
   for (uint64_t c = (uint64_t)blockIdx.x * (kWalkBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
+    // everything the connection needs is requested at once (one latency)
     const gevws_conn_out o = cout[c];
-    const uint64_t cnt = o.nframes;
-    if (cnt == 0) continue;
-    if (!rec_flags[c]) continue;  // second phase below
+    const uint8_t recorded = rec_flags[c];
     const gevws_conn_in ci = conns[c];
-    {
-      uint64_t ebase = 0, ecap = 0;
-      entry_slots(conns, n, (uint32_t)c, ci, n_entries, gshift, ebase, ecap);
-      uint64_t carry = o.payload_base;
+    const gevws_conn_in prev = conns[c > 0 ? c - 1 : c];
+    const gevws_conn_in next = conns[c + 1 < n ? c + 1 : c];
+    const uint64_t cnt = uniform64(o.nframes);  // one connection per wave
+    if (cnt == 0 || !recorded) continue;        // no frames / re-walked below
+    uint64_t ebase = 0, ecap = 0;
+    entry_slots_of(prev, ci, next, n, (uint32_t)c, n_entries, gshift, ebase, ecap);
+    const WalkEntry* ce = entries + ebase;
+    uint64_t carry = o.payload_base;
+    auto round = [&](const WalkEntry& q, uint64_t r0) {
+      const uint64_t k = r0 + lane;
+      const bool valid = k < cnt;
+      const uint64_t padded = valid ? round16(q.len) : 0;
+      const uint64_t incl = wave_incl_scan(padded);
+      if (valid) {
+        DevHdr h;
+        h.b0 = q.meta & 0xff;
+        h.masked = (q.meta >> 8) & 1;
+        h.hlen = q.meta >> 16;
+        h.mask = q.mask;
+        h.length = q.len;
+        emit_record(frames, tile_first, o.first_frame + k, carry + incl - padded, ci.off + q.pos + h.hlen, h);
+      }
+      carry += __shfl(incl, 63, 64);
+    };
+    if (U == 1 || cnt <= 64) {  // wave-uniform
       for (uint64_t k0 = 0; k0 < cnt; k0 += 64) {
-        const uint64_t k = k0 + lane;
-        const bool valid = k < cnt;
         WalkEntry q = {0, 0, 0, 0};
-        if (valid) q = entries[ebase + k];
-        const uint64_t padded = valid ? round16(q.len) : 0;
-        const uint64_t incl = wave_incl_scan(padded);
-        if (valid) {
-          DevHdr h;
-          h.b0 = q.meta & 0xff;
-          h.masked = (q.meta >> 8) & 1;
-          h.hlen = q.meta >> 16;
-          h.mask = q.mask;
-          h.length = q.len;
-          emit_record(frames, tile_first, o.first_frame + k, carry + incl - padded, ci.off + q.pos + h.hlen, h);
+        if (k0 + lane < cnt) q = ce[k0 + lane];
+        round(q, k0);
+      }
+    } else {
+      for (uint64_t k0 = 0; k0 < cnt; k0 += 64 * U) {
+        WalkEntry q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          // unconditional (clamped to the last entry): a branch around the
+          // load would make the compiler wait for it inside the branch
+          const uint64_t k = k0 + (uint64_t)u * 64 + lane;
+          q[u] = ce[k < cnt ? k : cnt - 1];
         }
-        carry += __shfl(incl, 63, 64);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (k0 + (uint64_t)u * 64 >= cnt) break;  // wave-uniform
+          round(q[u], k0 + (uint64_t)u * 64);
+        }
       }
     }
   }
@@ -836,12 +878,6 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
 // window, its first 256 records into registers (one per lane), which
 // the next iteration writes to LDS without waiting on a fresh load.  WT tiles
 // per window.
-// A value every lane of the wave loaded from the same address, kept in SGPRs
-// (the compiler cannot always prove such loads uniform once the loop stores).
-__device__ __forceinline__ uint32_t uniform32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
-__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
-  return (uint64_t)uniform32((uint32_t)x) | ((uint64_t)uniform32((uint32_t)(x >> 32)) << 32);
-}
 
 constexpr int kWin4Frames = 1024;
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -1911,8 +1947,8 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb);
     uint64_t egrid = ((uint64_t)n_conns + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
     if (egrid > 8 * (uint64_t)ctx->num_cus) egrid = 8 * (uint64_t)ctx->num_cus;
-    k_walk_emit<<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, d_summary, d_frames,
-                                                         tile_first, entries, ne, gshift, rec_flags);
+    k_walk_emit<4><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, d_summary, d_frames,
+                                                            tile_first, entries, ne, gshift, rec_flags);
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[3], st));
   r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);
