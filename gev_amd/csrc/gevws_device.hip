@@ -169,12 +169,15 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 // Frame entries recorded by the counting walk so the emit pass need not
 // re-fetch every header line from HBM: 16 bytes per frame in a per-connection
 // slot run whose base derives from the stream's arena offset (no scan needed):
-// base_c = off_c / G + 2c, capacity len_c / G + 2, with the granularity G the
-// smallest power of two >= 64 B that keeps the table within kEntryBudget.  Valid
+// base_c = 4 (off_c / 4G + c), capacity 4 (len_c / 4G + 1), with the
+// granularity G the smallest power of two >= 64 B that keeps the table within
+// kEntryBudget; runs start on 64-byte boundaries, so the walk can store its
+// entries as whole 64-byte groups of four (k_walk_count GRP).  Valid
 // (non-overlapping) when each stream ends before the next one starts, which
 // every connection checks against its neighbours; otherwise, or when a
 // connection's frames outnumber its slots (mean frame < G bytes), or
 // its stream is >= 4 GiB, the emit pass re-walks that connection.
+constexpr uint64_t kGroupedWalkChainsPerCU = 128;  // k_walk_count GRP from n_conns >= this x CUs
 constexpr uint32_t kEntryGranMinShift = 6;        // 64-byte granularity when the table fits
 constexpr uint64_t kEntryBudget = 1ull << 29;     // entries (8 GiB of scratch) at most
 struct WalkEntry {
@@ -191,8 +194,8 @@ __device__ __forceinline__ bool entry_slots_of(const gevws_conn_in& prev, const 
   if (n_entries == 0 || ci.len >= (1ull << 32)) return false;
   if (c > 0 && prev.off + prev.len > ci.off) return false;
   if (c + 1 < n && ci.off + ci.len > next.off) return false;
-  base = (ci.off >> gshift) + 2ull * c;
-  cap = (ci.len >> gshift) + 2;
+  base = 4 * ((ci.off >> (gshift + 2)) + (uint64_t)c);
+  cap = 4 * ((ci.len >> (gshift + 2)) + 1);
   return base + cap <= n_entries;
 }
 
@@ -235,7 +238,17 @@ __device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t ava
 // (profiles/r01_ab_walk2_*.json): the walk of fixed-size traffic takes 23-28 %
 // less time (C2, C3), mixed traffic 0-5 % more (C4, C5: a longer loop body on
 // a latency-bound chain).  GEVWS_TUNE_WALK_VARIANT 1 selects D = 0.
-template <int D>
+// GRP: a lane keeps its last three entries in registers and stores each
+// 64-byte group of four at once.  One lane writes one entry per chain step,
+// ~1 us apart, so with many chains a group's line is evicted from L2 long
+// before single 16-byte stores would fill it: those reach HBM as partial
+// writes (C4: 1.78 GB of writes for 0.70 GB of entries,
+// profiles/r01_c4_pmc.csv).  The cost: on a step that stores a group the next
+// header load waits for three of its stores as well (the store count behind
+// the load depends on the path), which slows latency-bound walks of few
+// chains -- so the host enables GRP only for batches of many connections
+// (profiles/r01_ab_walk_grp.json).
+template <int D, bool GRP>
 __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
                                                             const gevws_conn_in* __restrict__ conns,
                                                             uint32_t n, gevws_conn_out* __restrict__ cout,
@@ -272,6 +285,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
     *sink = WalkEntry{0, 0, 0, 0};
     uint64_t prev_fsz = 0;  // speculation (D > 0): size of the last frame and the run of equal sizes
     uint32_t run = 0;
+    WalkEntry g0 = {0, 0, 0, 0}, g1 = g0, g2 = g0;  // GRP: the last three entries, oldest first
     auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
       rec = rec && nf < ecap;
       WalkEntry e;
@@ -279,7 +293,22 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       e.mask = key;
       e.len = (uint32_t)L;
       e.meta = meta;
-      *(rec ? entries + ebase + nf : sink) = e;
+      if constexpr (GRP) {
+        if (rec && (nf & 3) == 3) {
+          WalkEntry* g = entries + ebase + (nf - 3);  // 64-byte aligned
+          g[0] = g0;
+          g[1] = g1;
+          g[2] = g2;
+          g[3] = e;
+        } else {
+          *sink = e;
+        }
+        g0 = g1;
+        g1 = g2;
+        g2 = e;
+      } else {
+        *(rec ? entries + ebase + nf : sink) = e;
+      }
       ++nf;
       pb += round16(L);
       pl += L;
@@ -363,6 +392,20 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
           if (fail) break;
           *sink = WalkEntry{0, 0, 0, 0};  // same [load, store] in flight at the loop head as the plain path
         }
+      }
+    }
+    if (GRP && rec) {  // the last nf % 4 entries
+      const uint32_t r = (uint32_t)(nf & 3);
+      WalkEntry* g = entries + ebase + (nf - r);
+      if (r == 3) {
+        g[0] = g0;
+        g[1] = g1;
+        g[2] = g2;
+      } else if (r == 2) {
+        g[0] = g1;
+        g[1] = g2;
+      } else if (r == 1) {
+        g[0] = g2;
       }
     }
     gevws_conn_out o;
@@ -1670,7 +1713,9 @@ struct gevws_ctx {
   int encode_variant = 0;  // 0 = aligned-load streaming + queued boundary chunks, 1 = unaligned loads,
                            // 2 = aligned loads, per-lane boundary assembly
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
-                           // 2 = plain walk without the entry table (emit re-walks)
+                           // 2 = plain walk without the entry table (emit re-walks); 0 and 1 store
+                           // entries in 64-byte groups for batches of many connections; 3 / 4 =
+                           // speculation with single / grouped entry stores regardless of the batch
   // Scratch is per context: calls on a different stream than the previous one
   // first wait for it (one in-flight batch per context; use one context per
   // stream for concurrency).
@@ -1848,7 +1893,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_WALK_VARIANT:
-      if (value < 0 || value > 2) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 4) return GEVWS_ERR_INVALID;
       ctx->walk_variant = (int)value;
       return GEVWS_OK;
     default:
@@ -1906,7 +1951,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
   uint32_t gshift = kEntryGranMinShift;
   while ((in_bytes >> gshift) > kEntryBudget) ++gshift;
-  const uint64_t n_entries = (in_bytes >> gshift) + 2ull * n_conns + 2;
+  const uint64_t n_entries = 4 * ((in_bytes >> (gshift + 2)) + (uint64_t)n_conns + 1);
   const size_t flag_bytes = ((size_t)n_conns + 255) & ~size_t(255);
   // + one sink slot per connection after the table (k_walk_count)
   int r = order_after_last(ctx, st);
@@ -1933,12 +1978,25 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   // nothing per frame and the emit pass re-walks every chain
   const uint64_t ne = ctx->walk_variant == 2 ? 0 : n_entries;
   if (nblk) {
-    if (ctx->walk_variant == 0)
-      k_walk_count<8><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
-                                                    cpb, in_bytes);
-    else
-      k_walk_count<0><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
-                                                    cpb, in_bytes);
+    // grouped entry stores pay off when the walk is bound by its line traffic
+    // (many concurrent chains), not by chain latency (few)
+    const int wv = ctx->walk_variant;
+    const bool many = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
+    const bool grp = wv == 4 || ((wv == 0 || wv == 1) && many);
+    if (wv == 1) {
+      if (grp)
+        k_walk_count<0, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
+                                                            gshift, cpb, in_bytes);
+      else
+        k_walk_count<0, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
+                                                             gshift, cpb, in_bytes);
+    } else if (grp) {
+      k_walk_count<8, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
+                                                          gshift, cpb, in_bytes);
+    } else {
+      k_walk_count<8, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
+                                                           gshift, cpb, in_bytes);
+    }
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[1], st));
   k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);

@@ -130,7 +130,10 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * 1 = unaligned loads, boundary chunks assembled by the lane that meets
  * them; 2 = aligned loads, per-lane assembly), GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
  * uniform-stream speculation, 1 = plain chain walk, 2 = plain walk that
- * records no per-frame entries, so the emit pass re-walks every chain). */
+ * records no per-frame entries, so the emit pass re-walks every chain; 0 and
+ * 1 store the per-frame entries in 64-byte groups when the batch has >= 128
+ * connections per CU; 3 / 4 = speculation with single / grouped entry stores
+ * whatever the batch). */
 #define GEVWS_TUNE_UNMASK_VARIANT 1
 #define GEVWS_TUNE_UNMASK_GRID 2
 #define GEVWS_TUNE_ENCODE_VARIANT 3

@@ -500,7 +500,7 @@ def test_walk_variants_uniform_runs(engine):
                                                     True, bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
                                     for _ in range(n)) for n in (1, 2, 3, 8, 9, 16, 17, 64, 65)])]
     try:
-        for v in (0, 1, 2):
+        for v in (0, 1, 2, 3, 4):
             engine.set_tuning(_abi.TUNE_WALK_VARIANT, v)
             for k, (arena, conns) in enumerate(cases):
                 assert_matches_oracle(engine, arena, conns, f"walk variant {v} case {k}")
@@ -511,4 +511,4 @@ def test_walk_variants_uniform_runs(engine):
 def test_walk_variant_knob_bounds(engine):
     from gev_amd import _abi
     with pytest.raises(ValueError):
-        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 3)
+        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 5)
