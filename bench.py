@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--copy-reps", type=int, default=5, help="streaming-copy ceiling reps (0 = skip)")
     ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
     ap.add_argument("--unmask-variant", type=int, default=None, help="A/B: unmask kernel variant")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="batches in flight: M contexts on M streams with M output arenas, step i on slot i %% M "
+                         "(a server loop: one batch's header walk overlaps the previous batch's unmask)")
     args = ap.parse_args()
 
     import numpy as np
@@ -151,12 +154,15 @@ def main():
     dev = torch.device("cuda", gpu)
     dist.init(dist.backend(), dev)  # RCCL over xGMI when WORLD_SIZE > 1
 
-    eng = gev_amd.Engine(gpu)
     from gev_amd import _abi
-    if args.walk_variant is not None:
-        eng.set_tuning(_abi.TUNE_WALK_VARIANT, args.walk_variant)
-    if args.unmask_variant is not None:
-        eng.set_tuning(_abi.TUNE_UNMASK_VARIANT, args.unmask_variant)
+    M = max(1, args.inflight)
+    engs = [gev_amd.Engine(gpu) for _ in range(M)]  # one context (scratch) per stream
+    eng = engs[0]
+    for e in engs:
+        if args.walk_variant is not None:
+            e.set_tuning(_abi.TUNE_WALK_VARIANT, args.walk_variant)
+        if args.unmask_variant is not None:
+            e.set_tuning(_abi.TUNE_UNMASK_VARIANT, args.unmask_variant)
     t_setup = time.time()
     scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
     lay, glob = build_layout(args.config, rank, args.conns, world, scaling)
@@ -181,34 +187,58 @@ def main():
     mismatch = int(mism.item())
     if mismatch or int(s["frames"]) != lay.n_frames or int(s["payload_len"]) != lay.payload_len:
         raise SystemExit(f"verification failed: mismatch={mismatch} frames={int(s['frames'])}")
-    del desc
+    if M == 1:
+        del desc
     log(f"rank {rank}: setup+verify {time.time() - t_setup:.1f}s, bit-exact")
 
     counts = torch.zeros(3, dtype=torch.int64, device=dev)
     sel = torch.tensor([0, 2, 3], dtype=torch.int64, device=dev)
     sum64 = out.summary.view(torch.int64)
+    outs = [out] + [e.alloc_batch(lay.n_conns, max_frames, cap) for e in engs[1:]]
+    streams = [None] if M == 1 else [torch.cuda.Stream(dev) for _ in range(M)]
+    main_stream = torch.cuda.current_stream()
+    n_step = [0]
 
     def step():
-        eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, max_frames, cap)
+        k = n_step[0] % M
+        n_step[0] += 1
+        engs[k].decode_async(arena, lay.arena_bytes, conns, lay.n_conns, outs[k], max_frames, cap,
+                             stream=streams[k])
         if world > 1:  # decoded {frames, payload bytes, errors}, summed over GPUs (N = 1: read after the loop)
-            torch.index_select(sum64, 0, sel, out=counts)
+            if M > 1:
+                main_stream.wait_stream(streams[k])
+            torch.index_select(outs[k].summary.view(torch.int64), 0, sel, out=counts)
             dist.reduce_counts(counts)
 
     for _ in range(args.warmup):
         step()
-    eng.timing()  # drop anything recorded so far
+    for e in engs:
+        e.timing()  # drop anything recorded so far
     dist.barrier()
     torch.cuda.synchronize()
-    eng.set_timing(True)
+    for e in engs:
+        e.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    eng.set_timing(False)
-    phases, calls = eng.timing()
+    phases, calls = [0.0] * 4, 0
+    for e in engs:
+        e.set_timing(False)
+        ph, cl = e.timing()
+        phases = [a + b for a, b in zip(phases, ph)]
+        calls += cl
     elapsed = dist.max_over_ranks(t1 - t0, dev)
+    if M > 1:  # every slot's last batch checked too (outside the timed region)
+        for k in range(1, M):
+            mism.zero_()
+            engs[k].verify(desc, lay.n_frames, lay.seed, outs[k], mism)
+            torch.cuda.synchronize()
+            if int(mism.item()):
+                raise SystemExit(f"verification failed on in-flight slot {k}: mismatch={int(mism.item())}")
+        del desc
 
     # achievable-bandwidth ceiling on this box, after the timed region: the
     # unmask kernel's streaming loop minus XOR / frame lookup (gevws_copy_async)
@@ -262,7 +292,8 @@ def main():
                    "global_payload_bytes": glob.payload_len if scaling == "strong" else None,
                    "parallelism": (f"connections sharded over {world} GPU(s)"
                                    f"{' by greedy LPT over stream bytes' if scaling == 'strong' else ''}; "
-                                   f"{'RCCL' if dist.backend() == 'nccl' else dist.backend()} all-reduce of counts")},
+                                   f"{'RCCL' if dist.backend() == 'nccl' else dist.backend()} all-reduce of counts"),
+                   "batches_in_flight": M},
         "frames_per_s": round(frames_step * args.steps / elapsed, 1),
         "errors": errors,
         "phases_ms": {"walk_count": round(mean_ms[0], 4), "scan": round(mean_ms[1], 4),
