@@ -429,17 +429,31 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
 __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict__ blk, uint32_t nblk,
                                                             uint64_t max_frames, uint64_t payload_cap,
                                                             gevws_summary* __restrict__ sum) {
+  // kScanPer consecutive partials per thread: a batch of per-frame blocks
+  // (encode / dispatch of 43.8 M frames: 171 K partials) takes a few rounds of
+  // the workgroup instead of one round per 1 024 partials
+  constexpr int kScanPer = 8;
   uint64_t carry[kBlkFields] = {0, 0, 0, 0};
-  for (uint32_t base = 0; base < nblk; base += kScanBlock) {
-    const uint32_t i = base + threadIdx.x;
-    uint64_t v[kBlkFields], ex[kBlkFields], tot[kBlkFields];
+  for (uint64_t base = 0; base < nblk; base += (uint64_t)kScanBlock * kScanPer) {
+    const uint64_t i0 = base + (uint64_t)threadIdx.x * kScanPer;
+    uint64_t loc[kBlkFields] = {0, 0, 0, 0}, ex[kBlkFields], tot[kBlkFields];
 #pragma unroll
-    for (int k = 0; k < kBlkFields; ++k) v[k] = (i < nblk) ? blk[(uint64_t)i * kBlkFields + k] : 0;
-    block_excl_scan<kScanBlock, kBlkFields>(v, ex, tot);
-    if (i < nblk) {
-      // fields 0/1 become exclusive bases (frames, arena bytes)
-      blk[(uint64_t)i * kBlkFields + 0] = carry[0] + ex[0];
-      blk[(uint64_t)i * kBlkFields + 1] = carry[1] + ex[1];
+    for (int r = 0; r < kScanPer; ++r)
+#pragma unroll
+      for (int k = 0; k < kBlkFields; ++k) loc[k] += (i0 + r < nblk) ? blk[(i0 + r) * kBlkFields + k] : 0;
+    block_excl_scan<kScanBlock, kBlkFields>(loc, ex, tot);
+    // fields 0/1 become exclusive bases (frames, arena bytes)
+    uint64_t b0 = carry[0] + ex[0], b1 = carry[1] + ex[1];
+#pragma unroll
+    for (int r = 0; r < kScanPer; ++r) {
+      if (i0 + r < nblk) {  // re-read (cached) rather than held across the scan: register budget
+        uint64_t* p = blk + (i0 + r) * kBlkFields;
+        const uint64_t f0 = p[0], f1 = p[1];
+        p[0] = b0;
+        p[1] = b1;
+        b0 += f0;
+        b1 += f1;
+      }
     }
 #pragma unroll
     for (int k = 0; k < kBlkFields; ++k) carry[k] += tot[k];
@@ -1137,15 +1151,25 @@ __device__ __forceinline__ uint32_t enc_hlen(const gevws_header& h) {
   return (L <= 125 ? 2u : (L <= 0xFFFF ? 4u : 10u)) + (h.masked ? 4u : 0u);
 }
 
+// A workgroup sizes kEncSlabs consecutive slabs of kWalkBlock frames (one
+// frame per lane per slab, coalesced), so the batch has one block partial per
+// 4 096 frames and the single-workgroup scan of partials stays short (C4:
+// 10.7 K partials instead of 171 K).
+constexpr int kEncSlabs = 16;
+
 __global__ __launch_bounds__(kWalkBlock) void k_enc_size(const gevws_out_frame* __restrict__ fr, uint64_t n,
                                                          uint64_t* __restrict__ blk) {
-  const uint64_t f = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
+  const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;
   uint64_t one = 0, wire = 0, pl = 0;
-  if (f < n) {
-    const gevws_out_frame o = fr[f];
-    one = 1;
-    pl = o.payload_len;
-    wire = enc_hlen(o.hdr) + o.payload_len;
+#pragma unroll 4
+  for (int j = 0; j < kEncSlabs; ++j) {
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    if (f < n) {
+      const gevws_out_frame o = fr[f];
+      one += 1;
+      pl += o.payload_len;
+      wire += enc_hlen(o.hdr) + o.payload_len;
+    }
   }
   __shared__ uint64_t s_part[3][kWalkBlock / 64];
   const uint64_t vals[3] = {one, wire, pl};
@@ -1170,15 +1194,22 @@ __global__ __launch_bounds__(kWalkBlock) void k_enc_emit(const gevws_out_frame* 
                                                          uint64_t* __restrict__ out_off,
                                                          uint32_t* __restrict__ tile_first) {
   if (sum->status != GEVWS_OK) return;
-  const uint64_t f = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
-  uint64_t v[1] = {0};
-  if (f < n) v[0] = enc_hlen(fr[f].hdr) + fr[f].payload_len;
-  uint64_t ex[1], tot[1];
-  block_excl_scan<kWalkBlock, 1>(v, ex, tot);
-  if (f >= n) return;
-  const uint64_t o = blk[(uint64_t)blockIdx.x * kBlkFields + 1] + ex[0];
-  out_off[f] = o;
-  for (uint64_t t = (o + kTile - 1) / kTile; t * kTile < o + v[0]; ++t) tile_first[t] = (uint32_t)f;
+  const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;
+  uint64_t carry = blk[(uint64_t)blockIdx.x * kBlkFields + 1];
+  for (int j = 0; j < kEncSlabs; ++j) {
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    if (f - threadIdx.x >= n) break;  // workgroup-uniform: slab past the batch
+    uint64_t v[1] = {0};
+    if (f < n) v[0] = enc_hlen(fr[f].hdr) + fr[f].payload_len;
+    uint64_t ex[1], tot[1];
+    block_excl_scan<kWalkBlock, 1>(v, ex, tot);
+    if (f < n) {
+      const uint64_t o = carry + ex[0];
+      out_off[f] = o;
+      for (uint64_t t = (o + kTile - 1) / kTile; t * kTile < o + v[0]; ++t) tile_first[t] = (uint32_t)f;
+    }
+    carry += tot[0];
+  }
 }
 
 // One output byte at absolute position `a` of frame f (global-memory form, used
@@ -1457,14 +1488,18 @@ __device__ __forceinline__ int disp_kind(const gevws_header& h, int policy, uint
 
 __global__ __launch_bounds__(kWalkBlock) void k_disp_count(const gevws_frame* __restrict__ fr, uint64_t n, int policy,
                                                            uint64_t* __restrict__ blk) {
-  const uint64_t f = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
+  const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;  // as k_enc_size
   uint64_t rep = 0, aux = 0, shut = 0;
-  if (f < n) {
-    uint32_t op;
-    const int k = disp_kind(fr[f].hdr, policy, op);
-    rep = k != 0;
-    aux = k == 2;
-    shut = k >= 2;
+#pragma unroll 4
+  for (int j = 0; j < kEncSlabs; ++j) {
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    if (f < n) {
+      uint32_t op;
+      const int k = disp_kind(fr[f].hdr, policy, op);
+      rep += k != 0;
+      aux += k == 2;
+      shut += k >= 2;
+    }
   }
   __shared__ uint64_t s_part[3][kWalkBlock / 64];
   const uint64_t vals[3] = {rep, aux, shut};
@@ -1499,31 +1534,11 @@ __device__ void put_close_error(uint8_t* dst, const char* msg, uint32_t& n) {
   put_close_body(dst, 1002, reinterpret_cast<const uint8_t*>(msg), len, n);  // StatusProtocolError
 }
 
-__global__ __launch_bounds__(kWalkBlock) void k_disp_emit(const gevws_frame* __restrict__ fr, uint64_t n, int policy,
-                                                          const uint8_t* __restrict__ payload, uint64_t aux_off,
-                                                          const uint64_t* __restrict__ blk,
-                                                          const gevws_summary* __restrict__ sum,
-                                                          gevws_out_frame* __restrict__ rep,
-                                                          int64_t* __restrict__ reply_of,
-                                                          uint8_t* __restrict__ aux_base) {
-  if (sum->status != GEVWS_OK) return;
-  const uint64_t f = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
-  uint32_t op = 0;
-  int kind = 0;
-  gevws_frame in;
-  if (f < n) {
-    in = fr[f];
-    kind = disp_kind(in.hdr, policy, op);
-  }
-  uint64_t v[2] = {(uint64_t)(kind != 0), (uint64_t)(kind == 2)};
-  uint64_t ex[2], tot[2];
-  block_excl_scan<kWalkBlock, 2>(v, ex, tot);
-  if (f >= n) return;
-  if (kind == 0) {
-    reply_of[f] = -1;
-    return;
-  }
-  const uint64_t r = blk[(uint64_t)blockIdx.x * kBlkFields + 0] + ex[0];
+// One reply record (and for a close its aux-slot body) for decoded frame f.
+__device__ __forceinline__ void disp_reply(const gevws_frame& in, int kind, uint32_t op, uint64_t f, uint64_t r,
+                                        uint64_t slot, const uint8_t* __restrict__ payload, uint64_t aux_off,
+                                        gevws_out_frame* __restrict__ rep, int64_t* __restrict__ reply_of,
+                                        uint8_t* __restrict__ aux_base) {
   reply_of[f] = (int64_t)r;
   gevws_out_frame o;
   memset(&o, 0, sizeof(o));
@@ -1536,7 +1551,6 @@ __global__ __launch_bounds__(kWalkBlock) void k_disp_emit(const gevws_frame* __r
   } else if (kind == 3) {
     o.hdr.opcode = 0x8;  // WriteHeader(&Header{Fin: true, OpCode: OpClose}), util.go:28-33
   } else {
-    const uint64_t slot = blk[(uint64_t)blockIdx.x * kBlkFields + 1] + ex[1];
     uint8_t* body = aux_base + slot * kAuxSlot;
     const uint8_t* p = payload + in.payload_off;
     const uint64_t L = (uint64_t)in.hdr.length;
@@ -1565,6 +1579,41 @@ __global__ __launch_bounds__(kWalkBlock) void k_disp_emit(const gevws_frame* __r
   }
   rep[r] = o;
 }
+
+__global__ __launch_bounds__(kWalkBlock) void k_disp_emit(const gevws_frame* __restrict__ fr, uint64_t n, int policy,
+                                                          const uint8_t* __restrict__ payload, uint64_t aux_off,
+                                                          const uint64_t* __restrict__ blk,
+                                                          const gevws_summary* __restrict__ sum,
+                                                          gevws_out_frame* __restrict__ rep,
+                                                          int64_t* __restrict__ reply_of,
+                                                          uint8_t* __restrict__ aux_base) {
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;  // as k_enc_emit
+  uint64_t c_rep = blk[(uint64_t)blockIdx.x * kBlkFields + 0], c_aux = blk[(uint64_t)blockIdx.x * kBlkFields + 1];
+  for (int j = 0; j < kEncSlabs; ++j) {
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    if (f - threadIdx.x >= n) break;  // workgroup-uniform: slab past the batch
+    uint32_t op = 0;
+    int kind = 0;
+    gevws_frame in;
+    if (f < n) {
+      in = fr[f];
+      kind = disp_kind(in.hdr, policy, op);
+    }
+    uint64_t v[2] = {(uint64_t)(kind != 0), (uint64_t)(kind == 2)};
+    uint64_t ex[2], tot[2];
+    block_excl_scan<kWalkBlock, 2>(v, ex, tot);
+    if (f < n) {
+      if (kind == 0)
+        reply_of[f] = -1;
+      else
+        disp_reply(in, kind, op, f, c_rep + ex[0], c_aux + ex[1], payload, aux_off, rep, reply_of, aux_base);
+    }
+    c_rep += tot[0];
+    c_aux += tot[1];
+  }
+}
+
 
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
 // p[i] ^= mask[(offset + i) & 3] for i in [0, n): 16-byte aligned chunks of the
@@ -2041,8 +2090,7 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   if (n > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
   DeviceGuard g(ctx->device);
   hipStream_t st = pick_stream(ctx, stream);
-  const uint64_t nblk64 = (n + kWalkBlock - 1) / kWalkBlock;
-  if (nblk64 > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
+  const uint64_t nblk64 = (n + (uint64_t)kWalkBlock * kEncSlabs - 1) / ((uint64_t)kWalkBlock * kEncSlabs);
   const uint32_t nblk = (uint32_t)nblk64;
   const uint64_t ntiles_cap = (out_cap + kTile - 1) / kTile + 1;
   const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
@@ -2077,7 +2125,7 @@ int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_fram
   if (policy < GEVWS_HANDLER_NONE || policy > GEVWS_HANDLER_ECHO_TEXT) return GEVWS_ERR_INVALID;
   DeviceGuard g(ctx->device);
   hipStream_t st = pick_stream(ctx, stream);
-  const uint64_t nblk64 = (n + kWalkBlock - 1) / kWalkBlock;
+  const uint64_t nblk64 = (n + (uint64_t)kWalkBlock * kEncSlabs - 1) / ((uint64_t)kWalkBlock * kEncSlabs);
   if (nblk64 > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
   const uint32_t nblk = (uint32_t)nblk64;
   const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);

@@ -45,18 +45,21 @@ def _client_stream(rng, n):
     return s
 
 
-@pytest.mark.parametrize("policy", [gev_amd._abi.HANDLER_NONE, gev_amd._abi.HANDLER_ECHO_BINARY,
-                                    gev_amd._abi.HANDLER_ECHO_TEXT])
-def test_dispatch_and_encode_replies(engine, policy):
-    rng = np.random.default_rng(50 + policy)
-    streams = [_client_stream(rng, int(rng.integers(1, 60))) for _ in range(30)]
+@pytest.mark.parametrize("policy,n_streams", [(gev_amd._abi.HANDLER_NONE, 30), (gev_amd._abi.HANDLER_ECHO_BINARY, 30),
+                                               (gev_amd._abi.HANDLER_ECHO_TEXT, 30),
+                                               (gev_amd._abi.HANDLER_ECHO_BINARY, 300)])
+def test_dispatch_and_encode_replies(engine, policy, n_streams):
+    """n_streams 300: ~9 000 frames, i.e. several dispatch / encode workgroups
+    of 4 096 frames each and their carried reply / aux-slot / wire offsets."""
+    rng = np.random.default_rng(50 + policy + n_streams)
+    streams = [_client_stream(rng, int(rng.integers(1, 60))) for _ in range(n_streams)]
     arena, conns = pack_streams(streams)
     import torch
     dev = torch.device("cuda", engine.device)
     d_in = torch.zeros(len(arena) + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
     d_in[: len(arena)] = torch.from_numpy(np.frombuffer(arena, np.uint8).copy()).to(dev)
     out = engine.decode(d_in, len(arena), torch.from_numpy(conns.copy()).to(dev), conns.shape[0],
-                        aux_slots=4096)
+                        aux_slots=8192)
     wire, reply_of, ds = engine.serve(out, policy)
     want, shut, reps = b"", 0, []
     k = 0
