@@ -1245,10 +1245,15 @@ __device__ __forceinline__ u128 byte_mask(int k0, int k1) {
 // from the frames overlapping it (at most 8: every frame is >= 2 wire bytes):
 // header bytes from the frame's serialised header, payload bytes from ONE
 // unaligned 16-byte load per frame (all loads independent).
+// LH: the serialised headers are not kept in LDS but rebuilt from the frame's
+// record (an L2 hit: the window just loaded it), which frees 16 KiB of LDS per
+// workgroup for occupancy.
+template <bool LH>
 __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
                                               const int32_t* s_start, const int32_t* s_pend, const uint8_t* s_hlen,
                                               const uint64_t* s_delta, const uint64_t* s_h0, const uint64_t* s_h1,
-                                              const uint8_t* __restrict__ payload) {
+                                              const uint8_t* __restrict__ payload,
+                                              const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
   u128 acc = 0;
   const int kmax = (a + 16 <= total) ? 16 : (int)(total - a);
   for (uint32_t j = lo; j < F && s_start[j] < rel + kmax; ++j) {
@@ -1259,7 +1264,14 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
     const int32_t h0 = hs > rel ? hs : rel;
     const int32_t h1 = ps < rel + kmax ? ps : rel + kmax;
     if (h0 < h1) {
-      const u128 H = (u128)s_h0[j] | ((u128)s_h1[j] << 64);
+      u128 H;
+      if constexpr (LH) {
+        uint64_t hl, hh;
+        enc_header(fr[f_lo + j].hdr, hl, hh);
+        H = (u128)hl | ((u128)hh << 64);
+      } else {
+        H = (u128)s_h0[j] | ((u128)s_h1[j] << 64);
+      }
       const u128 part = (H >> (8 * (h0 - hs))) << (8 * (h0 - rel));
       acc |= part & byte_mask(h0 - rel, h1 - rel);
     }
@@ -1279,7 +1291,7 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
 // two frames' pieces) are queued in LDS and assembled afterwards by the whole
 // workgroup, one chunk per lane, instead of by the one or two lanes of each
 // wave that meet them while the other lanes of the wave wait.
-template <int U, bool AL, bool COMPACT>
+template <int U, bool AL, bool COMPACT, bool LH = false>
 __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
@@ -1292,8 +1304,8 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
   __shared__ uint32_t s_bnd[COMPACT ? kWinTiles * kUnmaskBlock : 1];  // queued chunk: rel / 16 | frame << 16
   __shared__ uint32_t s_nb;
   __shared__ uint64_t s_delta[kEncWinFrames];  // payload_off - out_off - hlen (mod 2^64)
-  __shared__ uint64_t s_h0[kEncWinFrames];
-  __shared__ uint64_t s_h1[kEncWinFrames];
+  __shared__ uint64_t s_h0[LH ? 1 : kEncWinFrames];
+  __shared__ uint64_t s_h1[LH ? 1 : kEncWinFrames];
   if (sum->status != GEVWS_OK) return;
   const uint64_t total = sum->payload_bytes;  // wire bytes
   const uint64_t nframes = sum->frames;
@@ -1365,8 +1377,10 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
         s_pend[i] = pe > 0x7fffffffll ? 0x7fffffff : (int32_t)pe;
         s_hlen[i] = hl;
         s_delta[i] = o.payload_off - oo - hl;
-        s_h0[i] = lo;
-        s_h1[i] = hi;
+        if constexpr (!LH) {
+          s_h0[i] = lo;
+          s_h1[i] = hi;
+        }
       }
       if (COMPACT && threadIdx.x == 0) s_nb = 0;
       __syncthreads();
@@ -1385,8 +1399,8 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
         } else if constexpr (COMPACT) {
           s_bnd[atomicAdd(&s_nb, 1u)] = ((uint32_t)rel >> 4) | (lo << 16);
         } else {
-          const u32x4 x =
-              enc_assemble(rel, a, total, lo, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0, s_h1, payload);
+          const u32x4 x = enc_assemble<LH>(rel, a, total, lo, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
+                                           s_h1, payload, fr, f_lo);
           __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + a));
         }
       }
@@ -1397,8 +1411,8 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* 
           const uint32_t q = s_bnd[i];
           const int32_t rel = (int32_t)((q & 0xffffu) << 4);
           const uint64_t a = wbase + (uint64_t)rel;
-          const u32x4 x = enc_assemble(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
-                                       s_h1, payload);
+          const u32x4 x = enc_assemble<LH>(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta,
+                                           s_h0, s_h1, payload, fr, f_lo);
           __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + a));
         }
       }
@@ -1759,8 +1773,10 @@ struct gevws_ctx {
   gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
-  int encode_variant = 0;  // 0 = aligned-load streaming + queued boundary chunks, 1 = unaligned loads,
-                           // 2 = aligned loads, per-lane boundary assembly
+  int encode_variant = 0;  // 0 = aligned-load streaming + queued boundary chunks, headers rebuilt from
+                           // the records (LDS-light: 6 workgroups per CU), 1 = unaligned loads,
+                           // 2 = aligned loads, per-lane boundary assembly, 3 = as 0 with the headers
+                           // kept in LDS (4 workgroups per CU)
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
                            // 2 = plain walk without the entry table (emit re-walks); 0 and 1 store
                            // entries in 64-byte groups for batches of many connections; 3 / 4 =
@@ -1938,7 +1954,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->unmask_grid = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_ENCODE_VARIANT:
-      if (value < 0 || value > 2) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 3) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_WALK_VARIANT:
@@ -2103,17 +2119,23 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk);
   k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
   if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_summary, d_out_off, tile_first);
+  const uint64_t per_cu = ctx->encode_variant == 0 ? 6 : 4;  // LDS-light kernel: 6 workgroups fit per CU
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
-  if (grid > 4 * (uint64_t)ctx->num_cus) grid = 4 * (uint64_t)ctx->num_cus;
+  if (grid > per_cu * (uint64_t)ctx->num_cus) grid = per_cu * (uint64_t)ctx->num_cus;
   if (grid < 1) grid = 1;
-  // no big-frame grid reduction here: every frame boundary takes the window
-  // path, which needs 4 workgroups per CU to hide its latency (C3: 22.6 ms at
-  // 4/CU vs 36 ms at 1/CU, profiles/r01_encode_*.json)
+  // every frame boundary takes the window path, which needs several
+  // workgroups per CU to hide its latency (C3: 22.6 ms at 4/CU vs 36 ms at
+  // 1/CU); the LDS-light default runs 6 per CU (C2 -14 %, C4 -2 %,
+  // profiles/r01_encode_ab_lds_*.json) and 4 for batches of big frames
   auto enc = ctx->encode_variant == 1   ? k_encode<4, false, false>
              : ctx->encode_variant == 2 ? k_encode<4, true, false>
-                                        : k_encode<4, true, true>;
+             : ctx->encode_variant == 3 ? k_encode<4, true, true>
+                                        : k_encode<4, true, true, true>;
+  // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
+  // workgroups per CU (the rest return at once), the window path gets 6
+  const uint32_t big = per_cu > 4 && grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
   enc<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
-                                                       0u);
+                                                       big);
   GEVWS_HIP(hipGetLastError());
   return mark_last(ctx, st);
 }
