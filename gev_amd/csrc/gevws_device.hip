@@ -1291,8 +1291,12 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
 // two frames' pieces) are queued in LDS and assembled afterwards by the whole
 // workgroup, one chunk per lane, instead of by the one or two lanes of each
 // wave that meet them while the other lanes of the wave wait.
-template <int U, bool AL, bool COMPACT, bool LH = false>
-__global__ __launch_bounds__(kUnmaskBlock) void k_encode(const gevws_out_frame* __restrict__ fr,
+// WPE: waves per SIMD the register allocation must allow (amdgpu_waves_per_eu);
+// the window path is latency-bound, so the default LDS-light kernel is held to
+// 72 VGPRs for 7 workgroups per CU (C2 -4 %, C4 -2 % against 6 per CU; 8 per CU
+// at 64 VGPRs was slower on C5, profiles/r01_encode_ab_occ_*.json).
+template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1>
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
                                                          const uint32_t* __restrict__ tile_first,
@@ -1774,7 +1778,7 @@ struct gevws_ctx {
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
   int encode_variant = 0;  // 0 = aligned-load streaming + queued boundary chunks, headers rebuilt from
-                           // the records (LDS-light: 6 workgroups per CU), 1 = unaligned loads,
+                           // the records (LDS-light: 7 workgroups per CU), 1 = unaligned loads,
                            // 2 = aligned loads, per-lane boundary assembly, 3 = as 0 with the headers
                            // kept in LDS (4 workgroups per CU)
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
@@ -2119,18 +2123,19 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk);
   k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
   if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_summary, d_out_off, tile_first);
-  const uint64_t per_cu = ctx->encode_variant == 0 ? 6 : 4;  // LDS-light kernel: 6 workgroups fit per CU
+  const uint64_t per_cu = ctx->encode_variant == 0 ? 7 : 4;  // LDS-light kernel at <= 72 VGPRs: 7 per CU
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
   if (grid > per_cu * (uint64_t)ctx->num_cus) grid = per_cu * (uint64_t)ctx->num_cus;
   if (grid < 1) grid = 1;
   // every frame boundary takes the window path, which needs several
   // workgroups per CU to hide its latency (C3: 22.6 ms at 4/CU vs 36 ms at
-  // 1/CU); the LDS-light default runs 6 per CU (C2 -14 %, C4 -2 %,
-  // profiles/r01_encode_ab_lds_*.json) and 4 for batches of big frames
+  // 1/CU); the LDS-light default runs 7 per CU (C2 -18 %, C4 -4 % against
+  // 4, profiles/r01_encode_ab_lds_*.json, r01_encode_ab_occ_*.json) and 4 for
+  // batches of big frames
   auto enc = ctx->encode_variant == 1   ? k_encode<4, false, false>
              : ctx->encode_variant == 2 ? k_encode<4, true, false>
              : ctx->encode_variant == 3 ? k_encode<4, true, true>
-                                        : k_encode<4, true, true, true>;
+                                        : k_encode<4, true, true, true, 7>;
   // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
   // workgroups per CU (the rest return at once), the window path gets 6
   const uint32_t big = per_cu > 4 && grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;

@@ -127,7 +127,7 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto), GEVWS_TUNE_ENCODE_VARIANT
  * the encode kernel (0 = aligned loads + register realign while streaming,
  * frame-boundary chunks queued and assembled by the whole workgroup, frame
- * headers rebuilt from the records so 6 workgroups fit per CU;
+ * headers rebuilt from the records so 7 workgroups fit per CU;
  * 1 = unaligned loads, boundary chunks assembled by the lane that meets
  * them; 2 = aligned loads, per-lane assembly; 3 = as 0 with the serialised
  * headers kept in LDS, 4 workgroups per CU), GEVWS_TUNE_WALK_VARIANT the header walk (0 = with

@@ -50,7 +50,7 @@ def test_encode_golden(engine, golden):
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_encode_random_and_tiny_frames(engine, variant):
     """variant 0: aligned-load streaming + boundary chunks assembled by the
-    whole workgroup, headers rebuilt from the records (default, 6 workgroups
+    whole workgroup, headers rebuilt from the records (default, 7 workgroups
     per CU); 1: unaligned loads, per-lane assembly; 2: aligned-load streaming,
     per-lane assembly; 3: as 0 with the headers kept in LDS (4 per CU)."""
     from gev_amd import _abi
