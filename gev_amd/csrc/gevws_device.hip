@@ -2137,7 +2137,7 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
              : ctx->encode_variant == 3 ? k_encode<4, true, true>
                                         : k_encode<4, true, true, true, 7>;
   // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
-  // workgroups per CU (the rest return at once), the window path gets 6
+  // workgroups per CU (the rest return at once), the window path gets 7
   const uint32_t big = per_cu > 4 && grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
   enc<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
                                                        big);
