@@ -1287,6 +1287,70 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
   return u32x4_of(acc);
 }
 
+// enc_assemble with the first two overlapping frames' loads issued together
+// (most boundary chunks hold the end of one payload and the header + start of
+// the next); further frames (frames of a few bytes) continue in the loop.
+// The default encode's assembly: C2 -2.6 %, C5 -1.6 %, C3 / C4 -0.3..-0.5 %
+// (profiles/r01_encode_ab_asm2_*.json).
+template <bool LH>
+__device__ __forceinline__ u32x4 enc_assemble2(int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
+                                               const int32_t* s_start, const int32_t* s_pend, const uint8_t* s_hlen,
+                                               const uint64_t* s_delta, const uint64_t* s_h0, const uint64_t* s_h1,
+                                               const uint8_t* __restrict__ payload,
+                                               const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
+  const int kmax = (a + 16 <= total) ? 16 : (int)(total - a);
+  int32_t hs[2], h0[2], h1[2], p0[2], p1[2];
+  u32x4 pv[2];
+  u64x2 hv[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t j = lo + k;
+    const bool in = j < F && s_start[j < F ? j : lo] < rel + kmax;
+    const uint32_t jj = in ? j : lo;
+    hs[k] = s_start[jj];
+    const int32_t ps = hs[k] + (int32_t)s_hlen[jj];
+    const int32_t pe = s_pend[jj];
+    h0[k] = hs[k] > rel ? hs[k] : rel;
+    h1[k] = in ? (ps < rel + kmax ? ps : rel + kmax) : h0[k];
+    p0[k] = ps > rel ? ps : rel;
+    p1[k] = in ? (pe < rel + kmax ? pe : rel + kmax) : p0[k];
+    pv[k] = u32x4{0, 0, 0, 0};
+    hv[k] = u64x2{0, 0};
+    if (p0[k] < p1[k]) pv[k] = ld16u(payload + (a + (uint64_t)(p0[k] - rel) + s_delta[jj]));
+    if (h0[k] < h1[k]) {
+      if constexpr (LH) hv[k] = *reinterpret_cast<const u64x2*>(fr + f_lo + jj);  // the header half of the record
+      else hv[k] = u64x2{s_h0[jj], s_h1[jj]};
+    }
+  }
+  u128 acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (h0[k] < h1[k]) {
+      u128 H;
+      if constexpr (LH) {
+        gevws_header hd;
+        memcpy(&hd, &hv[k], 16);
+        uint64_t hl, hh;
+        enc_header(hd, hl, hh);
+        H = (u128)hl | ((u128)hh << 64);
+      } else {
+        H = (u128)hv[k][0] | ((u128)hv[k][1] << 64);
+      }
+      acc |= ((H >> (8 * (h0[k] - hs[k]))) << (8 * (h0[k] - rel))) & byte_mask(h0[k] - rel, h1[k] - rel);
+    }
+    if (p0[k] < p1[k]) {
+      const int k0 = p0[k] - rel;
+      acc |= (u128_of(pv[k]) << (8 * k0)) & byte_mask(k0, p1[k] - rel);
+    }
+  }
+  if (lo + 2 < F && s_start[lo + 2] < rel + kmax) {  // more frames in these 16 bytes
+    const u32x4 rest =
+        enc_assemble<LH>(rel, a, total, lo + 2, F, s_start, s_pend, s_hlen, s_delta, s_h0, s_h1, payload, fr, f_lo);
+    acc |= u128_of(rest);
+  }
+  return u32x4_of(acc);
+}
+
 // COMPACT: a window's chunks that straddle a frame boundary (header bytes or
 // two frames' pieces) are queued in LDS and assembled afterwards by the whole
 // workgroup, one chunk per lane, instead of by the one or two lanes of each
@@ -1295,7 +1359,7 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
 // the window path is latency-bound, so the default LDS-light kernel is held to
 // 72 VGPRs for 7 workgroups per CU (C2 -4 %, C4 -2 % against 6 per CU; 8 per CU
 // at 64 VGPRs was slower on C5, profiles/r01_encode_ab_occ_*.json).
-template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1>
+template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
@@ -1415,8 +1479,11 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
           const uint32_t q = s_bnd[i];
           const int32_t rel = (int32_t)((q & 0xffffu) << 4);
           const uint64_t a = wbase + (uint64_t)rel;
-          const u32x4 x = enc_assemble<LH>(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta,
-                                           s_h0, s_h1, payload, fr, f_lo);
+          const u32x4 x =
+              A2 ? enc_assemble2<LH>(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
+                                     s_h1, payload, fr, f_lo)
+                 : enc_assemble<LH>(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
+                                    s_h1, payload, fr, f_lo);
           __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + a));
         }
       }
@@ -2135,7 +2202,7 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   auto enc = ctx->encode_variant == 1   ? k_encode<4, false, false>
              : ctx->encode_variant == 2 ? k_encode<4, true, false>
              : ctx->encode_variant == 3 ? k_encode<4, true, true>
-                                        : k_encode<4, true, true, true, 7>;
+                                        : k_encode<4, true, true, true, 7, true>;
   // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
   // workgroups per CU (the rest return at once), the window path gets 7
   const uint32_t big = per_cu > 4 && grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
