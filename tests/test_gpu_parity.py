@@ -70,6 +70,24 @@ def test_random_batches(engine):
         assert_matches_oracle(engine, arena, conns, f"trial {trial}")
 
 
+def test_random_garbage_streams(engine):
+    """Streams of random bytes (headers parsed from noise: 16- and 64-bit length
+    codes, MSB-set lengths, incomplete payloads, short tails), alone and behind
+    a few valid frames, decode exactly as the oracle decodes them."""
+    rng = np.random.default_rng(14)
+    for trial in range(4):
+        streams = []
+        for _ in range(int(rng.integers(50, 400))):
+            # noise: len7 is <= 125 for most second bytes, so many noise
+            # "frames" complete; 127-codes carry random 64-bit lengths (MSB set
+            # half the time -> ErrHeaderLengthMSB)
+            junk = bytes(rng.integers(0, 256, int(rng.integers(0, 4000)), dtype=np.uint8))
+            lead = random_stream(rng, int(rng.integers(0, 4)), max_len=300, tail=False) if rng.random() < 0.5 else b""
+            streams.append(lead + junk)
+        arena, conns = pack_streams(streams)
+        assert_matches_oracle(engine, arena, conns, f"garbage trial {trial}")
+
+
 def test_big_frames_cross_tiles(engine):
     rng = np.random.default_rng(13)
     s = b""

@@ -236,6 +236,33 @@ def test_python_and_c_oracle_agree_random():
             k += 1
 
 
+def test_python_and_c_oracle_agree_on_noise():
+    """Pure random bytes (the GPU garbage-stream test's input class): headers
+    parsed from noise, ErrHeaderLengthMSB, incomplete tails -- both oracles
+    agree frame by frame."""
+    rng = np.random.default_rng(8)
+    streams = [bytes(rng.integers(0, 256, int(rng.integers(0, 2000)), dtype=np.uint8)) for _ in range(60)]
+    arena = np.frombuffer(b"".join(streams), np.uint8).copy()
+    lens = np.array([len(s) for s in streams])
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    r = ref.decode_batch(arena, offs, lens)
+    k = 0
+    statuses = set()
+    for ci, s in enumerate(streams):
+        res = wo.decode_stream(s)
+        statuses.add(res.status)
+        assert int(r["conn_nframes"][ci]) == len(res.frames)
+        assert int(r["conn_consumed"][ci]) == res.consumed
+        assert int(r["conn_status"][ci]) == res.status
+        for fr in res.frames:
+            f = r["frames"][k]
+            assert f.tobytes()[:16] == fr.header.pack()
+            o = int(f["payload_off"])
+            assert r["payload"][o:o + fr.header.length].tobytes() == fr.payload
+            k += 1
+    assert k > 0 and len(statuses) > 1  # noise produced frames and more than one outcome
+
+
 # --------------------------------------------------------------------------- outbound encode
 def _h(**kw):
     return wo.Header(**kw)
