@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--copy-reps", type=int, default=5, help="streaming-copy ceiling reps (0 = skip)")
     ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
     ap.add_argument("--unmask-variant", type=int, default=None, help="A/B: unmask kernel variant")
+    ap.add_argument("--emulate-shard", default=None, metavar="R/N",
+                    help="projection, not the contract line: decode only rank R's LPT share of an N-way strong "
+                         "split of the global batch, on this one GPU")
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight: M contexts on M streams with M output arenas, step i on slot i %% M "
                          "(a server loop: one batch's header walk overlaps the previous batch's unmask)")
@@ -165,7 +168,15 @@ def main():
             e.set_tuning(_abi.TUNE_UNMASK_VARIANT, args.unmask_variant)
     t_setup = time.time()
     scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
-    lay, glob = build_layout(args.config, rank, args.conns, world, scaling)
+    emulated = None
+    if args.emulate_shard:
+        er, en = (int(x) for x in args.emulate_shard.split("/"))
+        if world != 1 or not 0 <= er < en:
+            raise SystemExit("--emulate-shard R/N: one process, 0 <= R < N")
+        scaling, emulated = "strong", {"rank": er, "world": en}
+        lay, glob = build_layout(args.config, er, args.conns, en, "strong")
+    else:
+        lay, glob = build_layout(args.config, rank, args.conns, world, scaling)
     if lay.n_frames == 0:
         raise SystemExit(f"rank {rank}: no connections in this rank's share ({glob.n_conns} in the batch)")
     log(f"rank {rank}: {lay.name}: {lay.n_frames} frames, {lay.n_conns} connections, "
@@ -293,13 +304,14 @@ def main():
                    "parallelism": (f"connections sharded over {world} GPU(s)"
                                    f"{' by greedy LPT over stream bytes' if scaling == 'strong' else ''}; "
                                    f"{'RCCL' if dist.backend() == 'nccl' else dist.backend()} all-reduce of counts"),
-                   "batches_in_flight": M},
+                   "batches_in_flight": M,
+                   **({"emulated_shard": emulated} if emulated else {})},
         "frames_per_s": round(frames_step * args.steps / elapsed, 1),
         "errors": errors,
         "phases_ms": {"walk_count": round(mean_ms[0], 4), "scan": round(mean_ms[1], 4),
                       "walk_emit": round(mean_ms[2], 4), "unmask": round(unmask_ms, 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": (load_traffic(args.config) if scaling == "weak" or world == 1 else None),
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": (load_traffic(args.config) if (scaling == "weak" or world == 1) and not emulated else None),
                      "kernel": "k_unmask", "algorithmic_bytes_per_launch": alg_bytes,
                      "pipeline_achieved": round(pipeline_gbps, 1),
                      "pipeline_frac": round(pipeline_gbps / HBM_PEAK_GBPS, 4),
