@@ -8,7 +8,12 @@ D2H (payload arena + frame records + per-connection results) on one of S
 streams, so copies in both directions overlap the device work.  Reports payload
 GiB/s host-to-host next to the raw pinned H2D / D2H copy rates on this box.
 
+With --direct-out the payload arena is mapped pinned host memory
+(gevws_pinned_alloc): the unmask kernel writes the plaintext over PCIe and no
+payload D2H copy is issued.
+
     python tools/host_inclusive.py [--gib 8] [--chunk-mib 64] [--streams 2] [--reps 3] [--sweep 64:2,128:3]
+                                   [--direct-out]
 """
 from __future__ import annotations
 
