@@ -4,7 +4,7 @@
 // Hot path: for a batch of connections, the
 // repeated websocket.(*Protocol).UnPacket loop of Connection.handlerProtocol
 // (connection.go:208-218 -> plugins/websocket/protocol.go:38-62) is done as
-// four launches on one stream:
+// four stages (five launches) on one stream:
 //
 //   1. k_walk_count  one lane per connection walks its header chain
 //                    (ws.VirtualReadHeader, read.go:19-84, plus the
