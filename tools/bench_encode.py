@@ -75,8 +75,8 @@ def main():
         del ref_wire
         torch.cuda.empty_cache()
     times = {v: [] for v in variants}
-    for _ in range(args.rounds):
-        for v in variants:
+    for rnd in range(args.rounds):
+        for v in (variants if rnd % 2 == 0 else variants[::-1]):  # alternate the order (position bias)
             eng.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, v)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
