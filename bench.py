@@ -20,6 +20,10 @@ sample of the same workload.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Measurement options (not the contract line's defaults): --inflight M (M
+batches in flight on M streams), --emulate-shard R/N (rank R's LPT share of an
+N-way strong split, on one GPU), --walk-variant / --unmask-variant (A/B).
 """
 from __future__ import annotations
 

@@ -250,7 +250,7 @@ __device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t ava
 // header load waits for three of its stores as well (the store count behind
 // the load depends on the path), which slows latency-bound walks of few
 // chains -- so the host enables GRP only for batches of many connections
-// (profiles/r01_ab_walk_grp.json).
+// (profiles/r01_ab_walk_grp_*.json).
 template <int D, bool GRP>
 __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
                                                             const gevws_conn_in* __restrict__ conns,
