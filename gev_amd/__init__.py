@@ -23,7 +23,7 @@ import numpy as np
 
 from . import _abi
 from ._abi import (ERR_CAPACITY, ERR_DEVICE, ERR_HANDSHAKE, ERR_INVALID, ERR_LEN_MSB, ERR_NOT_UPGRADED,
-                   HANDSHAKE, IN_PAD, NEED_MORE, OK, PAYLOAD_ALIGN, TILE, Header)
+                   HANDSHAKE, IN_PAD, NEED_MORE, OK, PAYLOAD_ALIGN, SUMMARY_UNORDERED, TILE, Header)
 
 lib = _abi.load()
 
@@ -33,7 +33,7 @@ FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked
 CONN_OUT_DTYPE = np.dtype([("first_frame", "<u8"), ("consumed", "<u8"), ("payload_base", "<u8"),
                            ("nframes", "<u4"), ("status", "<i4")])
 SUMMARY_DTYPE = np.dtype([("frames", "<u8"), ("payload_bytes", "<u8"), ("payload_len", "<u8"),
-                          ("errors", "<u8"), ("status", "<i4"), ("reserved0", "<u4"), ("reserved", "<u8", (3,))])
+                          ("errors", "<u8"), ("status", "<i4"), ("flags", "<u4"), ("reserved", "<u8", (3,))])
 OUT_FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked", "u1"),
                             ("mask", "u1", (4,)), ("length", "<i8"),
                             ("payload_off", "<u8"), ("payload_len", "<u8")])
@@ -625,6 +625,13 @@ class Protocol:
             raise RuntimeError(f"unpacket_batch: {status_string(int(r))}")
         return int(r)
 
+    def stats(self) -> dict:
+        """Host-ingress counters (gevws_protocol_get_stats): device passes,
+        connections and bytes staged, UnPacket calls answered by the host gate."""
+        s = _abi.ProtocolStats()
+        lib.gevws_protocol_get_stats(self._p, ctypes.byref(s))
+        return {k: int(getattr(s, k)) for k, _ in _abi.ProtocolStats._fields_}
+
     def decode_host(self, segments: Sequence[Tuple[bytes, bytes]]):
         """gevws_decode_host_batch: [(first, end)] host segments per connection ->
         (frames, payload arena, conn_out, summary) as numpy arrays (the FFI form)."""
@@ -679,4 +686,4 @@ __all__ = ["Engine", "Batch", "RingBuffer", "Connection", "Protocol", "Header", 
            "Upgrader", "RejectError", "HandshakeError", "HandshakeInfo", "accept_key", "HANDSHAKE", "ERR_HANDSHAKE",
            "status_string", "device_count", "lib", "FRAME_DTYPE", "CONN_OUT_DTYPE", "SUMMARY_DTYPE",
            "SYNTH_DTYPE", "OUT_FRAME_DTYPE", "OK", "NEED_MORE", "ERR_LEN_MSB", "ERR_CAPACITY", "ERR_INVALID", "ERR_DEVICE",
-           "ERR_NOT_UPGRADED", "IN_PAD", "PAYLOAD_ALIGN", "TILE"]
+           "ERR_NOT_UPGRADED", "IN_PAD", "PAYLOAD_ALIGN", "TILE", "SUMMARY_UNORDERED"]

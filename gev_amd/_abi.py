@@ -47,6 +47,7 @@ TUNE_ENCODE_VARIANT = 3
 TUNE_WALK_VARIANT = 4
 
 IN_PAD = 64
+SUMMARY_UNORDERED = 1  # summary.flags: connection table not in increasing input order
 PAYLOAD_ALIGN = 16
 TILE = 4096
 
@@ -81,7 +82,12 @@ class ConnOut(ctypes.Structure):
 class Summary(ctypes.Structure):
     _fields_ = [("frames", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64),
                 ("payload_len", ctypes.c_uint64), ("errors", ctypes.c_uint64), ("status", ctypes.c_int32),
-                ("reserved0", ctypes.c_uint32), ("reserved", ctypes.c_uint64 * 3)]
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint64 * 3)]
+
+
+class ProtocolStats(ctypes.Structure):
+    _fields_ = [("device_passes", ctypes.c_uint64), ("conns_staged", ctypes.c_uint64),
+                ("bytes_staged", ctypes.c_uint64), ("gated", ctypes.c_uint64)]
 
 
 class HostConn(ctypes.Structure):
@@ -201,6 +207,11 @@ SIGNATURES = {
     "gevws_protocol_set_upgrader": (None, [P, P]),
     "gevws_decode_host_stream": (ctypes.c_int64, [P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.c_uint64,
                                                   P, ctypes.c_uint64, P, ctypes.POINTER(Summary)]),
+    "gevws_parse_header": (ctypes.c_int, [P, ctypes.c_uint64, ctypes.POINTER(Header), ctypes.POINTER(ctypes.c_uint32)]),
+    "gevws_parse_header_ring": (ctypes.c_int, [P, ctypes.c_uint64, P, ctypes.c_uint64, ctypes.POINTER(Header),
+                                               ctypes.POINTER(ctypes.c_uint32)]),
+    "gevws_cipher": (None, [P, ctypes.c_uint64, P, ctypes.c_uint64]),
+    "gevws_protocol_get_stats": (None, [P, ctypes.POINTER(ProtocolStats)]),
     "gevws_decode_host_batch": (ctypes.c_int64, [P, P, ctypes.c_uint32, P, ctypes.c_uint64, P, ctypes.c_uint64,
                                                  P, ctypes.POINTER(Summary)]),
 }

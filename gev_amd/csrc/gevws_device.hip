@@ -175,11 +175,17 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 // base_c = 4 (off_c / 4G + c), capacity 4 (len_c / 4G + 1), with the
 // granularity G the smallest power of two >= 64 B that keeps the table within
 // kEntryBudget; runs start on 64-byte boundaries, so the walk can store its
-// entries as whole 64-byte groups of four (k_walk_count GRP).  Valid
-// (non-overlapping) when each stream ends before the next one starts, which
-// every connection checks against its neighbours; otherwise, or when a
-// connection's frames outnumber its slots (mean frame < G bytes), or
-// its stream is >= 4 GiB, the emit pass re-walks that connection.
+// entries as whole 64-byte groups of four (k_walk_count GRP).  The runs are
+// disjoint when the whole table is in increasing input order with no overlap
+// (for c < d: base_c + cap_c <= 4 ((off_c + len_c) / 4G + 1 + c) <= base_d);
+// a neighbour check per connection cannot establish that (an
+// unsorted table can pass every local check and still collide), so every
+// workgroup reports whether any of its connections starts before the previous
+// one ends, k_scan_blocks ORs that into summary.flags, and on an unordered
+// table the emit pass ignores the entries and re-walks every chain.  Entries
+// are written either way: base + cap <= n_entries holds for any table, so the
+// stores stay inside the table.  A connection whose frames outnumber its slots
+// (mean frame < G bytes) or whose stream is >= 4 GiB is re-walked too.
 constexpr uint64_t kGroupedWalkChainsPerCU = 128;  // k_walk_count GRP from n_conns >= this x CUs
 constexpr uint32_t kEntryGranMinShift = 6;        // 64-byte granularity when the table fits
 constexpr uint64_t kEntryBudget = 1ull << 29;     // entries (8 GiB of scratch) at most
@@ -191,23 +197,21 @@ struct WalkEntry {
 };
 static_assert(sizeof(WalkEntry) == 16, "one dwordx4 per entry");
 
-__device__ __forceinline__ bool entry_slots_of(const gevws_conn_in& prev, const gevws_conn_in& ci,
-                                              const gevws_conn_in& next, uint32_t n, uint32_t c, uint64_t n_entries,
+__device__ __forceinline__ bool entry_slots_of(const gevws_conn_in& ci, uint32_t c, uint64_t n_entries,
                                               uint32_t gshift, uint64_t& base, uint64_t& cap) {
   if (n_entries == 0 || ci.len >= (1ull << 32)) return false;
-  if (c > 0 && prev.off + prev.len > ci.off) return false;
-  if (c + 1 < n && ci.off + ci.len > next.off) return false;
   base = 4 * ((ci.off >> (gshift + 2)) + (uint64_t)c);
   cap = 4 * ((ci.len >> (gshift + 2)) + 1);
   return base + cap <= n_entries;
 }
 
-__device__ __forceinline__ bool entry_slots(const gevws_conn_in* __restrict__ conns, uint32_t n, uint32_t c,
-                                           const gevws_conn_in& ci, uint64_t n_entries, uint32_t gshift,
-                                           uint64_t& base, uint64_t& cap) {
-  const gevws_conn_in prev = conns[c > 0 ? c - 1 : c];
-  const gevws_conn_in next = conns[c + 1 < n ? c + 1 : c];
-  return entry_slots_of(prev, ci, next, n, c, n_entries, gshift, base, cap);
+// Connection c breaks the increasing, non-overlapping order the slot runs rely
+// on (its stream starts before the previous one ends).
+__device__ __forceinline__ bool out_of_order(const gevws_conn_in* __restrict__ conns, uint32_t c,
+                                             const gevws_conn_in& ci) {
+  if (c == 0) return false;
+  const gevws_conn_in p = conns[c - 1];
+  return ci.off < p.off || ci.off - p.off < p.len;
 }
 
 // The counting walk's header parse (read.go:19-84 + the protocol.go:47 gate)
@@ -262,6 +266,8 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
   uint64_t nf = 0, pb = 0, pl = 0, err = 0;
   if (threadIdx.x < cpb && c < n) {
     gevws_conn_in ci = conns[c];
+    // the order flag rides in the high half of the error count (k_scan_blocks SPLIT)
+    if (out_of_order(conns, c, ci)) err = 1ull << 32;
     int32_t st = GEVWS_OK;
     if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
       // a stream outside the input arena: nothing is read, the connection
@@ -269,12 +275,12 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       ci.off = 0;
       ci.len = 0;
       st = GEVWS_ERR_INVALID;
-      err = 1;
+      err += 1;
     }
     const uint8_t* s = in + ci.off;
     uint64_t pos = 0;
     uint64_t ebase = 0, ecap = 0;
-    bool rec = entry_slots(conns, n, c, ci, n_entries, gshift, ebase, ecap);
+    bool rec = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
     // software-pipelined: the next header's 16 bytes are requested before this
     // frame's entry is stored, so waiting for that load (vmcnt counts loads and
     // stores in issue order) never waits for the store's completion.  Reading
@@ -336,7 +342,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       const bool have_hdr = avail >= 6 && avail >= hlen;   // read.go:20-23, U1
       const bool msb = e64 && (L64 >> 63);                  // read.go:71-73
       if (!have_hdr || msb || avail - hlen < L) {           // protocol.go:47 gate
-        if (have_hdr && msb) { st = GEVWS_ERR_LEN_MSB; err = 1; }
+        if (have_hdr && msb) { st = GEVWS_ERR_LEN_MSB; err += 1; }
         break;
       }
       const uint32_t key = (e64 ? (uint32_t)(hi0 >> 16) : (e16 ? (uint32_t)(lo0 >> 32) : (uint32_t)(lo0 >> 16))) &
@@ -375,7 +381,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
                 uint64_t L2;
                 const int r = walk_parse(qlo[j], qhi[j], ci.len - pos, m2, h2, L2, k2);
                 if (r != GEVWS_OK) {
-                  if (r == GEVWS_ERR_LEN_MSB) { st = GEVWS_ERR_LEN_MSB; err = 1; }
+                  if (r == GEVWS_ERR_LEN_MSB) { st = GEVWS_ERR_LEN_MSB; err += 1; }
                   fail = stop = true;
                 } else {
                   put_entry(pos, k2, L2, m2);
@@ -429,6 +435,10 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
 }
 
 // ------------------------------------------------------------------ 2. scan of block partials
+// SPLIT (decode): field 3 holds errors in its low 32 bits and the count of
+// out-of-order connections in its high 32 (k_walk_count) -> summary.errors and
+// GEVWS_SUMMARY_UNORDERED.
+template <bool SPLIT>
 __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict__ blk, uint32_t nblk,
                                                             uint64_t max_frames, uint64_t payload_cap,
                                                             gevws_summary* __restrict__ sum) {
@@ -467,7 +477,8 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict
     s.frames = carry[0];
     s.payload_bytes = carry[1];
     s.payload_len = carry[2];
-    s.errors = carry[3];
+    s.errors = SPLIT ? (carry[3] & 0xffffffffull) : carry[3];
+    s.flags = (SPLIT && (carry[3] >> 32)) ? GEVWS_SUMMARY_UNORDERED : 0u;
     s.status = (carry[0] > max_frames || carry[1] > payload_cap) ? GEVWS_ERR_CAPACITY : GEVWS_OK;
     *sum = s;
   }
@@ -534,6 +545,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
                                                           const WalkEntry* __restrict__ entries, uint64_t n_entries,
                                                           uint32_t gshift, const uint8_t* __restrict__ rec_flags) {
   if (sum->status != GEVWS_OK) return;
+  const bool unordered = (sum->flags & GEVWS_SUMMARY_UNORDERED) != 0;  // entry runs may collide: unused
   const int lane = threadIdx.x & 63;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kWalkBlock / 64);
   for (uint64_t c = (uint64_t)blockIdx.x * (kWalkBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
@@ -541,12 +553,10 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
     const gevws_conn_out o = cout[c];
     const uint8_t recorded = rec_flags[c];
     const gevws_conn_in ci = conns[c];
-    const gevws_conn_in prev = conns[c > 0 ? c - 1 : c];
-    const gevws_conn_in next = conns[c + 1 < n ? c + 1 : c];
     const uint64_t cnt = uniform64(o.nframes);  // one connection per wave
-    if (cnt == 0 || !recorded) continue;        // no frames / re-walked below
+    if (cnt == 0 || !recorded || unordered) continue;  // no frames / re-walked below
     uint64_t ebase = 0, ecap = 0;
-    entry_slots_of(prev, ci, next, n, (uint32_t)c, n_entries, gshift, ebase, ecap);
+    entry_slots_of(ci, (uint32_t)c, n_entries, gshift, ebase, ecap);
     const WalkEntry* ce = entries + ebase;
     uint64_t carry = o.payload_base;
     auto round = [&](const WalkEntry& q, uint64_t r0) {
@@ -592,7 +602,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
   // connections without recorded entries: one lane per connection re-walks
   const uint64_t nthreads = (uint64_t)gridDim.x * kWalkBlock;
   for (uint64_t c = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x; c < n; c += nthreads) {
-    if (rec_flags[c]) continue;
+    if (rec_flags[c] && !unordered) continue;
     const gevws_conn_out o = cout[c];
     const gevws_conn_in ci = conns[c];
     const uint8_t* s = in + ci.off;
@@ -2136,7 +2146,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     }
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[1], st));
-  k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
+  k_scan_blocks<true><<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
   if (timed) GEVWS_HIP(hipEventRecord(ev[2], st));
   if (nblk) {
     k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb);
@@ -2189,7 +2199,7 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
   uint32_t* tile_first = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes);
   if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk);
-  k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
+  k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
   if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_summary, d_out_off, tile_first);
   const uint64_t per_cu = ctx->encode_variant == 0 ? 7 : 4;  // LDS-light kernel at <= 72 VGPRs: 7 per CU
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
@@ -2230,7 +2240,7 @@ int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_fram
   if (r != GEVWS_OK) return r;
   uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
   if (nblk) k_disp_count<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, blk);
-  k_scan_blocks<<<1, kScanBlock, 0, st>>>(blk, nblk, n, aux_cap / kAuxSlot, d_summary);
+  k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, aux_cap / kAuxSlot, d_summary);
   if (nblk)
     k_disp_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, d_payload, aux_off, blk, d_summary, d_replies,
                                               d_reply_of, d_payload + aux_off);

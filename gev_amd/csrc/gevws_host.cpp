@@ -25,6 +25,7 @@
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "gevws.h"
@@ -53,27 +54,90 @@ static void log_error_text(const char* what, const std::string& text) {
   if (log_errors_enabled()) fprintf(stderr, "[Gev] ERROR %s%s\n", what, text.c_str());
 }
 
+// ------------------------------------------------------------------ pinned arenas
+// The payload arena of a device pass is copied D2H straight into page-locked
+// host memory and handed out from there: every frame a pass delivers holds a
+// reference to its arena, which goes back to the protocol's pool when the last
+// of them is released (no second host copy).  Thread-confined like the
+// protocol (one per event loop); the mutex only guards a release that happens
+// after the protocol is gone.
+class PinnedPool : public std::enable_shared_from_this<PinnedPool> {
+ public:
+  ~PinnedPool() {
+    for (auto& b : free_) (void)hipHostFree(b.p);
+  }
+  // A buffer of at least `need` bytes, or nullptr.
+  std::shared_ptr<uint8_t> Acquire(uint64_t need) {
+    need = std::max<uint64_t>(need, 16);
+    Buf b{nullptr, 0};
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (size_t i = 0; i < free_.size(); ++i)
+        if (free_[i].cap >= need) {
+          b = free_[i];
+          free_.erase(free_.begin() + (long)i);
+          break;
+        }
+    }
+    if (!b.p) {
+      const uint64_t want = std::max<uint64_t>(need + need / 2, 1 << 16);
+      if (hipHostMalloc((void**)&b.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+      b.cap = want;
+    }
+    std::weak_ptr<PinnedPool> pool = shared_from_this();
+    return std::shared_ptr<uint8_t>(b.p, [pool, b](uint8_t*) {
+      if (auto pp = pool.lock()) pp->Release(b);
+      else (void)hipHostFree(b.p);
+    });
+  }
+ private:
+  struct Buf {
+    uint8_t* p;
+    uint64_t cap;
+  };
+  void Release(Buf b) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (free_.size() < kKeep) {
+      free_.push_back(b);
+      return;
+    }
+    (void)hipHostFree(b.p);
+  }
+  static constexpr size_t kKeep = 8;  // arenas kept for reuse
+  std::mutex mu_;
+  std::vector<Buf> free_;
+};
+
 // ------------------------------------------------------------------ connection
 struct Delivered {
   gevws_header hdr;
   uint64_t frame_bytes;  // h + L, consumed from the ring on delivery
-  uint64_t payload_off;  // into the batch's host arena
-  std::shared_ptr<std::vector<uint8_t>> arena;
+  uint64_t payload_off;  // into the pass's pinned arena
+  std::shared_ptr<uint8_t> arena;
 };
 
 struct Connection {
   bool upgraded = false;                 // "gev_ws_upgraded" (protocol.go:12, 36)
   int poisoned = GEVWS_OK;               // sticky ERR_LEN_MSB (Appendix A P9/U3)
   std::deque<Delivered> queue;           // decoded, not yet returned by UnPacket
-  std::shared_ptr<std::vector<uint8_t>> current;  // keeps the last payload alive
+  std::shared_ptr<uint8_t> current;      // keeps the last payload's arena alive
   HandshakeResult hs;                    // last Upgrade's response + Handshake
-  uint64_t tail_len = ~0ull;             // undecodable ring bytes after the last device pass
+  // Completeness carry (protocol.go:47, 59-61): ring bytes, counted from the
+  // ring's read position, that must be buffered before a device pass can
+  // decode anything this connection has not queued yet -- h + L of its first
+  // incomplete frame once its header is known, 6 before that (read.go:20-23).
+  // Valid only while the ring's read position is the one it was derived at
+  // (need_ring / need_at): bytes consumed by anyone else invalidate it.
+  uint64_t need = 0;
+  const RingBuffer* need_ring = nullptr;
+  uint64_t need_at = 0;
+  uint64_t epoch = 0;                    // last UnPacketBatch that took this connection
 };
 
 // ------------------------------------------------------------------ protocol
 class Protocol {
  public:
-  explicit Protocol(gevws_ctx* ctx) : ctx_(ctx) {}
+  explicit Protocol(gevws_ctx* ctx) : ctx_(ctx), pool_(std::make_shared<PinnedPool>()) {}
   void SetUpgrader(const Upgrader* u) { upgrader_ = u; }
   ~Protocol() { release(); }
 
@@ -96,11 +160,15 @@ class Protocol {
       c->upgraded = true;
       return GEVWS_HANDSHAKE;
     }
-    if (c->queue.empty() && c->poisoned == GEVWS_OK && ring->Length() != c->tail_len) {
-      Connection* cs[1] = {c};
-      RingBuffer* rs[1] = {ring};
-      int64_t r = UnPacketBatch(cs, rs, 1);
-      if (r < 0) return (int)r;
+    if (c->queue.empty() && c->poisoned == GEVWS_OK) {
+      if (Ready(c, ring)) {
+        Connection* cs[1] = {c};
+        RingBuffer* rs[1] = {ring};
+        int64_t r = UnPacketBatch(cs, rs, 1);
+        if (r < 0) return (int)r;
+      } else {
+        ++stats_.gated;
+      }
     }
     if (c->queue.empty()) {
       if (c->poisoned != GEVWS_OK) {  // protocol.go:41-45: log and return (nil, nil)
@@ -111,25 +179,34 @@ class Protocol {
     }
     Delivered d = std::move(c->queue.front());
     c->queue.pop_front();
+    const bool carried = c->need_ring == ring && c->need_at == ring->Retrieved();
     ring->Retrieve(d.frame_bytes);  // VirtualFlush + Read (protocol.go:48-51)
-    c->current = d.arena;
+    if (carried) {
+      c->need = c->need > d.frame_bytes ? c->need - d.frame_bytes : 0;
+      c->need_at = ring->Retrieved();
+    }
+    c->current = std::move(d.arena);
     *hdr = d.hdr;
-    *out = d.arena->data() + d.payload_off;
+    *out = c->current.get() + d.payload_off;
     *out_len = (uint64_t)d.hdr.length;
     return GEVWS_OK;
   }
 
-  // One device pass over every listed connection's buffered bytes.
+  // One device pass over every listed connection that can make progress.
   int64_t UnPacketBatch(Connection* const* conns, RingBuffer* const* rings, uint32_t n) {
-    // Connections that already hold undelivered frames (or are poisoned) are
-    // skipped: their ring prefix is already decoded.
+    // Skipped: connections that still hold undelivered frames (their ring
+    // prefix is decoded already), poisoned ones, ones whose first undecoded
+    // frame is not complete yet (the carried gate), and repeats of a
+    // connection already taken by this call.
+    ++epoch_;
     std::vector<uint32_t> sel;
     std::vector<gevws_host_conn> segs;
     sel.reserve(n);
     for (uint32_t i = 0; i < n; ++i) {
-      if (!conns[i]->upgraded || !conns[i]->queue.empty() || conns[i]->poisoned != GEVWS_OK) continue;
-      if (rings[i]->Length() < 6) continue;  // read.go:20-23: nothing can be decoded
-      if (rings[i]->Length() == conns[i]->tail_len) continue;  // no new bytes since the last pass
+      Connection* c = conns[i];
+      if (c->epoch == epoch_ || !c->upgraded || !c->queue.empty() || c->poisoned != GEVWS_OK) continue;
+      if (!Ready(c, rings[i])) continue;
+      c->epoch = epoch_;
       gevws_host_conn h;
       rings[i]->PeekAll(&h.seg0, &h.n0, &h.seg1, &h.n1);
       sel.push_back(i);
@@ -137,30 +214,42 @@ class Protocol {
     }
     if (sel.empty()) return 0;
     const uint32_t m = (uint32_t)sel.size();
-    gevws_summary sum{};
-    std::vector<gevws_conn_in> cin;
     DeviceScope scope(gevws_ctx_device(ctx_));
-    int64_t r = StageDecode(segs.data(), m, &sum, cin);
+    Staged sg;
+    int64_t r = StageDecode(segs.data(), m, &sg);
     if (r < 0) return r;
-    // frames + payload back in one round trip through pinned memory
-    const uint64_t fb = sum.frames * sizeof(gevws_frame);
-    if (!grow_host(&h_out_, &h_out_cap_, fb + sum.payload_bytes + 16)) return fail();
+    // frames + payload land in pinned memory with the summary: one
+    // synchronisation for a pass whose output fits the first estimate
     hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
-    if ((fb && hipMemcpyAsync(h_out_, d_frames_, fb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-        (sum.payload_bytes &&
-         hipMemcpyAsync(h_out_ + fb, d_payload_, sum.payload_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-        hipStreamSynchronize(st) != hipSuccess)
+    const uint64_t est_f = std::min<uint64_t>(sg.max_frames, sg.total / 48 + 2ull * m + 16);
+    const uint64_t est_p = std::min<uint64_t>(sg.payload_cap, sg.total + 16 * est_f + 16);
+    if (!grow_host(&h_out_, &h_out_cap_, est_f * sizeof(gevws_frame))) return fail();
+    std::shared_ptr<uint8_t> arena = pool_->Acquire(est_p);
+    if (!arena) return fail();
+    if (hipMemcpyAsync(h_out_, d_frames_, est_f * sizeof(gevws_frame), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(arena.get(), d_payload_, est_p, hipMemcpyDeviceToHost, st) != hipSuccess)
       return fail();
+    r = Finish(&sg);
+    if (r < 0) return r;
+    const gevws_summary& sum = sg.sum;
+    const uint64_t fb = sum.frames * sizeof(gevws_frame);
+    if (sg.retried || sum.frames > est_f || sum.payload_bytes > est_p) {  // more than estimated: fetch it all
+      if (sum.payload_bytes > est_p && !(arena = pool_->Acquire(sum.payload_bytes))) return fail();
+      if (!grow_host(&h_out_, &h_out_cap_, fb)) return fail();
+      if ((fb && hipMemcpyAsync(h_out_, d_frames_, fb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+          (sum.payload_bytes &&
+           hipMemcpyAsync(arena.get(), d_payload_, sum.payload_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+          hipStreamSynchronize(st) != hipSuccess)
+        return fail();
+    }
     const gevws_conn_out* cout = reinterpret_cast<const gevws_conn_out*>(h_res_ + sizeof(gevws_summary));
     const gevws_frame* fr = reinterpret_cast<const gevws_frame*>(h_out_);
-    auto arena = std::make_shared<std::vector<uint8_t>>(h_out_ + fb, h_out_ + fb + sum.payload_bytes);
-    if (arena->empty()) arena->resize(1);
+    const uint8_t* hin = h_in_ + sg.coff;
     // hand the frames to their connections in stream order
     for (uint32_t j = 0; j < m; ++j) {
       Connection* c = conns[sel[j]];
       const gevws_conn_out& o = cout[j];
-      c->tail_len = cin[j].len - o.consumed;
-      uint64_t prev_end = cin[j].off;
+      uint64_t prev_end = sg.cin[j].off;
       for (uint32_t k = 0; k < o.nframes; ++k) {
         const gevws_frame& f = fr[o.first_frame + k];
         Delivered d;
@@ -171,7 +260,15 @@ class Protocol {
         prev_end = f.src_off + (uint64_t)f.hdr.length;
         c->queue.push_back(std::move(d));
       }
-      if (o.status < 0) c->poisoned = o.status;
+      if (o.status < 0) {
+        c->poisoned = o.status;
+        continue;
+      }
+      // the gate for the next pass: the frame at the end of what was decoded,
+      // read from the staged copy of the ring (still in pinned memory)
+      c->need = o.consumed + Need(hin + sg.cin[j].off + o.consumed, sg.cin[j].len - o.consumed);
+      c->need_ring = rings[sel[j]];
+      c->need_at = rings[sel[j]]->Retrieved();
     }
     return (int64_t)sum.frames;
   }
@@ -179,13 +276,16 @@ class Protocol {
   // Host segments in, caller buffers out (gevws_decode_host_batch).
   int64_t DecodeHost(const gevws_host_conn* segs, uint32_t n, gevws_frame* frames, uint64_t max_frames,
                      uint8_t* payload, uint64_t payload_cap, gevws_conn_out* conn_out, gevws_summary* sum_out) {
-    gevws_summary sum{};
-    *sum_out = sum;
+    gevws_summary zero{};
+    *sum_out = zero;
     if (n == 0) return 0;
-    std::vector<gevws_conn_in> cin;
     DeviceScope scope(gevws_ctx_device(ctx_));
-    int64_t r = StageDecode(segs, n, &sum, cin);
+    Staged sg;
+    int64_t r = StageDecode(segs, n, &sg);
     if (r < 0) return r;
+    r = Finish(&sg);
+    if (r < 0) return r;
+    const gevws_summary& sum = sg.sum;
     // src_off is reported relative to each connection's own stream
     *sum_out = sum;
     if (sum.frames > max_frames || sum.payload_bytes > payload_cap) {
@@ -201,9 +301,11 @@ class Protocol {
         hipStreamSynchronize(st) != hipSuccess)
       return fail();
     for (uint32_t j = 0; j < n; ++j)
-      for (uint32_t k = 0; k < conn_out[j].nframes; ++k) frames[conn_out[j].first_frame + k].src_off -= cin[j].off;
+      for (uint32_t k = 0; k < conn_out[j].nframes; ++k) frames[conn_out[j].first_frame + k].src_off -= sg.cin[j].off;
     return (int64_t)sum.frames;
   }
+
+  void GetStats(gevws_protocol_stats* out) const { *out = stats_; }
 
  private:
   struct DeviceScope {
@@ -217,59 +319,117 @@ class Protocol {
     }
   };
 
+  // Bytes that must be buffered at p for its first frame to be complete
+  // (read.go:20-23, U1 and the protocol.go:47 gate); 0 when the header is
+  // unreadable (ErrHeaderLengthMSB: a pass reports it).
+  static uint64_t Need(const uint8_t* p, uint64_t avail) {
+    gevws_header h;
+    uint32_t hl = 0;
+    const int r = gevws_parse_header(p, avail, &h, &hl);
+    if (r == GEVWS_OK) return (uint64_t)hl + (uint64_t)h.length;
+    if (r == GEVWS_NEED_MORE) return std::max<uint64_t>(6, hl);
+    return 0;
+  }
+
+  // May a device pass decode anything new for this connection (whose queue is
+  // empty, so the ring's read position is its first undecoded frame)?  The
+  // carried count answers most calls; otherwise the frame's header is parsed
+  // on the host, 14 bytes at most.
+  bool Ready(Connection* c, RingBuffer* ring) {
+    const uint64_t len = ring->Length();
+    if (len < 6) return false;  // read.go:20-23
+    if (c->need_ring == ring && c->need_at == ring->Retrieved() && len < c->need) return false;
+    const uint8_t *a, *b;
+    uint64_t na, nb;
+    ring->PeekAll(&a, &na, &b, &nb);
+    gevws_header h;
+    uint32_t hl = 0;
+    const int r = gevws_parse_header_ring(a, na, b, nb, &h, &hl);
+    if (r == GEVWS_OK) c->need = (uint64_t)hl + (uint64_t)h.length;
+    else if (r == GEVWS_NEED_MORE) c->need = std::max<uint64_t>(6, hl);
+    else c->need = 0;  // ErrHeaderLengthMSB: the pass reports and poisons
+    c->need_ring = ring;
+    c->need_at = ring->Retrieved();
+    return len >= c->need;
+  }
+
+  struct Staged {
+    std::vector<gevws_conn_in> cin;
+    uint64_t coff = 0, total = 0, res = 0, max_frames = 0, payload_cap = 0;
+    bool retried = false;  // Finish re-ran the pass: copies enqueued before it are stale
+    gevws_summary sum{};
+  };
+
   // Join each connection's segments into pinned staging behind the connection
-  // table, ONE H2D, decode on the context's stream, ONE D2H of {summary,
-  // conn_out} into pinned h_res_ and one sync.  Frames and payload stay in
-  // the device buffers.  Retries once with the exact sizes on ERR_CAPACITY.
-  int64_t StageDecode(const gevws_host_conn* segs, uint32_t m, gevws_summary* sum,
-                      std::vector<gevws_conn_in>& cin) {
+  // table, ONE H2D, enqueue the decode on the context's stream and the D2H of
+  // {summary, conn_out} into pinned h_res_ (no synchronisation yet: the caller
+  // adds its own copies, then Finish waits).
+  int64_t StageDecode(const gevws_host_conn* segs, uint32_t m, Staged* sg) {
     uint64_t total = 0;
     for (uint32_t j = 0; j < m; ++j) total += segs[j].n0 + segs[j].n1;
-    cin.resize(m);
-    const uint64_t coff = ((uint64_t)m * sizeof(gevws_conn_in) + 255) & ~255ull;  // input starts here
-    const uint64_t stage = coff + total + GEVWS_IN_PAD;
+    sg->cin.resize(m);
+    sg->total = total;
+    sg->coff = ((uint64_t)m * sizeof(gevws_conn_in) + 255) & ~255ull;  // input starts here
+    const uint64_t stage = sg->coff + total + GEVWS_IN_PAD;
     if (!grow_host(&h_in_, &h_in_cap_, stage)) return fail();
-    uint8_t* hin = h_in_ + coff;
+    uint8_t* hin = h_in_ + sg->coff;
     uint64_t off = 0;
     for (uint32_t j = 0; j < m; ++j) {
       if (segs[j].n0) memcpy(hin + off, segs[j].seg0, segs[j].n0);
       if (segs[j].n1) memcpy(hin + off + segs[j].n0, segs[j].seg1, segs[j].n1);
-      cin[j] = {off, segs[j].n0 + segs[j].n1};
-      off += cin[j].len;
+      sg->cin[j] = {off, segs[j].n0 + segs[j].n1};
+      off += sg->cin[j].len;
     }
-    memcpy(h_in_, cin.data(), m * sizeof(gevws_conn_in));
+    memcpy(h_in_, sg->cin.data(), m * sizeof(gevws_conn_in));
     memset(hin + off, 0, GEVWS_IN_PAD);
-    const uint64_t res = sizeof(gevws_summary) + (uint64_t)m * sizeof(gevws_conn_out);
-    if (!grow_host(&h_res_, &h_res_cap_, res)) return fail();
-    uint64_t max_frames = std::min<uint64_t>(total / 2 + 1, 0xFFFFFFFFull);
-    uint64_t payload_cap = total + 16 * std::min<uint64_t>(max_frames, total / 64 + 64) + 64;
+    sg->res = sizeof(gevws_summary) + (uint64_t)m * sizeof(gevws_conn_out);
+    if (!grow_host(&h_res_, &h_res_cap_, sg->res)) return fail();
+    // every frame is >= 2 bytes; the arena bound covers frames of >= 64 bytes
+    // (Finish retries with the exact sizes on GEVWS_ERR_CAPACITY)
+    sg->max_frames = std::min<uint64_t>(total / 2 + 1, 0xFFFFFFFFull);
+    sg->payload_cap = total + 16 * std::min<uint64_t>(sg->max_frames, total / 64 + 64) + 64;
     hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
-    if (!grow_dev(&d_in_, &d_in_cap_, stage) || !grow_dev(&d_res_, &d_res_cap_, res) ||
+    if (!grow_dev(&d_in_, &d_in_cap_, stage) || !grow_dev(&d_res_, &d_res_cap_, sg->res) ||
         hipMemcpyAsync(d_in_, h_in_, stage, hipMemcpyHostToDevice, st) != hipSuccess)
       return fail();
+    ++stats_.device_passes;
+    stats_.conns_staged += m;
+    stats_.bytes_staged += stage;
+    return Launch(sg);
+  }
+
+  int64_t Launch(Staged* sg) {
+    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+    if (!grow_dev(&d_frames_, &d_frames_cap_, sg->max_frames * sizeof(gevws_frame)) ||
+        !grow_dev(&d_payload_, &d_payload_cap_, sg->payload_cap + 16))
+      return fail();
+    const uint32_t m = (uint32_t)sg->cin.size();
     gevws_summary* d_sum = (gevws_summary*)d_res_;
     gevws_conn_out* d_cout = (gevws_conn_out*)((uint8_t*)d_res_ + sizeof(gevws_summary));
-    for (int attempt = 0; attempt < 2; ++attempt) {
-      if (!grow_dev(&d_frames_, &d_frames_cap_, max_frames * sizeof(gevws_frame)) ||
-          !grow_dev(&d_payload_, &d_payload_cap_, payload_cap + 16))
-        return fail();
-      int r = gevws_decode_batch_async(ctx_, st, (const uint8_t*)d_in_ + coff, total, (gevws_conn_in*)d_in_, m,
-                                       (gevws_frame*)d_frames_, max_frames, (uint8_t*)d_payload_, payload_cap,
-                                       d_cout, d_sum);
-      if (r != GEVWS_OK) return r;
-      if (hipMemcpyAsync(h_res_, d_res_, res, hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipStreamSynchronize(st) != hipSuccess)
-        return fail();
-      memcpy(sum, h_res_, sizeof(gevws_summary));
-      r = sum->status;
-      if (r == GEVWS_ERR_CAPACITY && attempt == 0) {
-        max_frames = std::max<uint64_t>(sum->frames, 1);
-        payload_cap = std::max<uint64_t>(sum->payload_bytes, 16);
-        continue;
-      }
-      return r == GEVWS_OK ? (int64_t)sum->frames : (int64_t)r;
+    int r = gevws_decode_batch_async(ctx_, st, (const uint8_t*)d_in_ + sg->coff, sg->total, (gevws_conn_in*)d_in_, m,
+                                     (gevws_frame*)d_frames_, sg->max_frames, (uint8_t*)d_payload_, sg->payload_cap,
+                                     d_cout, d_sum);
+    if (r != GEVWS_OK) return r;
+    if (hipMemcpyAsync(h_res_, d_res_, sg->res, hipMemcpyDeviceToHost, st) != hipSuccess) return fail();
+    return GEVWS_OK;
+  }
+
+  // Waits for the pass (and whatever the caller enqueued after it); on
+  // GEVWS_ERR_CAPACITY runs it once more with the exact sizes.
+  int64_t Finish(Staged* sg) {
+    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail();
+    memcpy(&sg->sum, h_res_, sizeof(gevws_summary));
+    if (sg->sum.status == GEVWS_ERR_CAPACITY) {
+      sg->max_frames = std::max<uint64_t>(sg->sum.frames, 1);
+      sg->payload_cap = std::max<uint64_t>(sg->sum.payload_bytes, 16);
+      sg->retried = true;
+      int64_t r = Launch(sg);
+      if (r < 0) return r;
+      if (hipStreamSynchronize(st) != hipSuccess) return fail();
+      memcpy(&sg->sum, h_res_, sizeof(gevws_summary));
     }
-    return GEVWS_ERR_CAPACITY;
+    return sg->sum.status == GEVWS_OK ? (int64_t)sg->sum.frames : (int64_t)sg->sum.status;
   }
 
   int64_t fail() {
@@ -301,6 +461,7 @@ class Protocol {
     return true;
   }
   void release() {
+    if (ctx_) (void)hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_));
     for (uint8_t* p : {h_in_, h_res_, h_out_})
       if (p) (void)hipHostFree(p);
     for (void* p : {d_in_, d_res_, d_frames_, d_payload_})
@@ -309,10 +470,13 @@ class Protocol {
 
   gevws_ctx* ctx_;
   const Upgrader* upgrader_ = nullptr;
+  std::shared_ptr<PinnedPool> pool_;   // payload arenas handed out with the frames
   uint8_t *h_in_ = nullptr, *h_res_ = nullptr, *h_out_ = nullptr;  // pinned staging
   uint64_t h_in_cap_ = 0, h_res_cap_ = 0, h_out_cap_ = 0;
   void *d_in_ = nullptr, *d_res_ = nullptr, *d_frames_ = nullptr, *d_payload_ = nullptr;
   uint64_t d_in_cap_ = 0, d_res_cap_ = 0, d_frames_cap_ = 0, d_payload_cap_ = 0;
+  uint64_t epoch_ = 0;
+  gevws_protocol_stats stats_{};
 };
 
 }  // namespace gevws
@@ -364,6 +528,15 @@ int64_t gevws_protocol_unpacket_batch(gevws_protocol* p, gevws_conn* const* conn
     rs[i] = rings[i];
   }
   return p->UnPacketBatch(cs.data(), rs.data(), n);
+}
+
+void gevws_protocol_get_stats(const gevws_protocol* p, gevws_protocol_stats* out) {
+  if (!out) return;
+  if (!p) {
+    *out = gevws_protocol_stats{};
+    return;
+  }
+  p->GetStats(out);
 }
 
 int64_t gevws_decode_host_batch(gevws_protocol* p, const gevws_host_conn* conns, uint32_t n,

@@ -67,8 +67,14 @@ class RingBuffer {
     return c1 + c2;
   }
 
+  // Bytes consumed since construction: identifies the read position, so a
+  // value derived from the buffered bytes (the protocol's completeness carry)
+  // can tell whether anyone consumed bytes since it was derived.
+  uint64_t Retrieved() const { return retrieved_; }
+
   void Retrieve(uint64_t n) {
     const uint64_t len = Length();
+    retrieved_ += n < len ? n : len;
     if (n >= len) {
       r_ = w_ = 0;
       empty_ = true;
@@ -98,6 +104,7 @@ class RingBuffer {
   std::vector<uint8_t> buf_;
   uint64_t size_;
   uint64_t r_ = 0, w_ = 0;
+  uint64_t retrieved_ = 0;
   bool empty_ = true;
 };
 

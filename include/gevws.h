@@ -104,9 +104,14 @@ typedef struct gevws_summary {
     uint64_t payload_len;   /* sum of payload lengths */
     uint64_t errors;        /* connections with status < 0 */
     int32_t status;         /* GEVWS_OK or GEVWS_ERR_CAPACITY */
-    uint32_t reserved0;
+    uint32_t flags;         /* GEVWS_SUMMARY_* (decode only; informational) */
     uint64_t reserved[3];
 } gevws_summary;
+
+/* summary.flags: the connection table was not in increasing, non-overlapping
+ * input order, so the header walk's per-connection entry runs were not used and
+ * the record pass re-walked every chain (same result, slower). */
+#define GEVWS_SUMMARY_UNORDERED 1u
 
 typedef struct gevws_ctx gevws_ctx;
 
@@ -249,6 +254,32 @@ int gevws_pinned_free(void *host_ptr);
 int gevws_cipher_async(gevws_ctx *ctx, void *stream, uint8_t *d_p, uint64_t n,
                        const uint8_t mask[4], uint64_t offset);
 
+/* ---------------------------------------------------------------- per-frame host calls
+ * For a host (cgo / C++) that looks at ONE frame at the head of a connection's
+ * buffer -- e.g. to apply the reference's completeness gate (protocol.go:47)
+ * before handing the connection to a device pass.  Plain host memory, no
+ * context, no device work. */
+
+/* ws.VirtualReadHeader (plugins/websocket/ws/read.go:19-84) on the `avail`
+ * buffered bytes at p.  GEVWS_OK: *out = the header (ws.Header layout),
+ * *hdr_len = its length (2..14); the frame is complete iff avail >= *hdr_len +
+ * out->length (protocol.go:47).  GEVWS_NEED_MORE: fewer than 6 bytes
+ * (ErrHeaderNotReady, read.go:20-23 -- even for a complete 2..5-byte frame) or
+ * the extended header is not complete yet (Appendix A U1); *hdr_len = the
+ * header length when at least 2 bytes are buffered, else 0.
+ * GEVWS_ERR_LEN_MSB: ErrHeaderLengthMSB (read.go:71-73).  *out is written only
+ * on GEVWS_OK. */
+int gevws_parse_header(const uint8_t *p, uint64_t avail, gevws_header *out, uint32_t *hdr_len);
+
+/* The same over a ring buffer's PeekAll() segments (first, end): the header may
+ * straddle the wrap, as the virtual reads of read.go:27,63 allow. */
+int gevws_parse_header_ring(const uint8_t *seg0, uint64_t n0, const uint8_t *seg1, uint64_t n1,
+                            gevws_header *out, uint32_t *hdr_len);
+
+/* ws.Cipher(p[:n], mask, offset) (plugins/websocket/ws/cipher.go:14-53) in host
+ * memory, in place: p[i] ^= mask[(offset + i) % 4]. */
+void gevws_cipher(uint8_t *p, uint64_t n, const uint8_t mask[4], uint64_t offset);
+
 /* ---------------------------------------------------------------- synthetic batches
  * Device-side frame generator used by the bench and the full-size property
  * tests (no 64 GiB host buffer is ever built).  d_desc describes each frame:
@@ -329,6 +360,18 @@ int gevws_protocol_unpacket(gevws_protocol *p, gevws_conn *c, gevws_ring *ring,
  * device work.  Returns the number of frames decoded, or < 0. */
 int64_t gevws_protocol_unpacket_batch(gevws_protocol *p, gevws_conn *const *conns,
                                       gevws_ring *const *rings, uint32_t n);
+
+/* Counters of a protocol's host ingress (not on the reference path):
+ * device passes run, connections staged into them, bytes staged (H2D), and
+ * UnPacket calls answered NEED_MORE by the host-side gate without a device pass
+ * (the first frame's h + L is not buffered yet, protocol.go:47). */
+typedef struct gevws_protocol_stats {
+    uint64_t device_passes;
+    uint64_t conns_staged;
+    uint64_t bytes_staged;
+    uint64_t gated;
+} gevws_protocol_stats;
+void gevws_protocol_get_stats(const gevws_protocol *p, gevws_protocol_stats *out);
 
 /* One connection's buffered bytes in host memory, as ringbuffer.PeekAll()
  * returns them (first, end) -- e.g. two Go slices passed through cgo. */

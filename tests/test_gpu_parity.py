@@ -8,6 +8,7 @@ frames (gevws_synth_verify_async), plus an oracle cross-check of a slice."""
 import numpy as np
 import pytest
 
+import gev_amd
 from oracle import ref
 from oracle import ws_oracle as wo
 from tests._helpers import assert_matches_oracle, gpu_decode, host_result, pack_streams, random_stream
@@ -68,6 +69,34 @@ def test_random_batches(engine):
         streams = [random_stream(rng, int(rng.integers(0, 25))) for _ in range(n)]
         arena, conns = pack_streams(streams)
         assert_matches_oracle(engine, arena, conns, f"trial {trial}")
+
+
+def test_unordered_and_overlapping_conn_tables(engine):
+    """the walk's per-connection entry runs are placed by
+    input offset, which is collision-free only for a table in increasing,
+    non-overlapping order.  Tables that break it -- the advisor's example
+    (neighbour checks all pass for conn 0 and conn 3, whose runs collide),
+    shuffled, reversed and overlapping tables -- must decode exactly as the
+    oracle decodes the same table, and report GEVWS_SUMMARY_UNORDERED."""
+    rng = np.random.default_rng(15)
+    s0 = b"".join(wo.encode_frame(bytes(rng.integers(0, 256, 190, dtype=np.uint8)), 2, True, 0, True,
+                                  bytes(rng.integers(0, 256, 4, dtype=np.uint8))) for _ in range(20))
+    arena = s0 + bytes(rng.integers(0, 256, 5010 - len(s0), dtype=np.uint8))
+    conns = np.array([[0, len(s0)], [5000, 10], [50, 10], [60, 30]], np.int64)
+    got = assert_matches_oracle(engine, arena, conns, "advisor example")
+    assert int(got["summary"]["flags"]) & gev_amd.SUMMARY_UNORDERED
+    for trial in range(4):
+        streams = [random_stream(rng, int(rng.integers(0, 30)), max_len=600) for _ in range(int(rng.integers(40, 400)))]
+        arena, conns = pack_streams(streams)
+        got = assert_matches_oracle(engine, arena, conns, f"ordered {trial}")
+        assert int(got["summary"]["flags"]) == 0
+        perm = rng.permutation(conns.shape[0]) if trial % 2 == 0 else np.arange(conns.shape[0])[::-1]
+        got = assert_matches_oracle(engine, arena, conns[perm], f"permuted {trial}")
+        assert int(got["summary"]["flags"]) & gev_amd.SUMMARY_UNORDERED
+    # overlapping streams (the same bytes decoded twice) and a 4-fold repeat
+    arena, conns = pack_streams([random_stream(rng, 25, max_len=900) for _ in range(64)])
+    assert_matches_oracle(engine, arena, np.concatenate([conns, conns[::3]]), "overlap")
+    assert_matches_oracle(engine, arena, np.tile(conns, (4, 1)), "repeat")
 
 
 def test_random_garbage_streams(engine):

@@ -239,3 +239,71 @@ def test_handshake_rejected_then_retried(engine):
     got = []
     replies = gev_amd.handler_protocol(proto, c, r, _wrap_on_message(got))
     assert c.upgraded and got == [b"hello"] and replies[1:] == [b"hello"]
+
+
+def test_large_frame_in_read_sized_chunks_costs_one_pass(engine):
+    """A 1 MiB frame arriving in 64 KiB reads (connection.go:220-251,
+    eventloop.go:15): every UnPacket before the last read is answered by the
+    carried completeness gate (protocol.go:47, 59-61) without a device pass;
+    the read that completes it costs exactly one pass."""
+    rng = np.random.default_rng(31)
+    proto = gev_amd.Protocol(engine)
+    c, r = gev_amd.Connection(), gev_amd.RingBuffer(4096)
+    data = bytes(rng.integers(0, 256, 1 << 20, dtype=np.uint8))
+    w = wo.encode_frame(data, wo.OP_BINARY, True, 0, True, b"\x11\x22\x33\x44")
+    w2 = wo.encode_frame(b"tail", wo.OP_TEXT, True, 0, True, b"\x01\x02\x03\x04")
+    stream = w + w2
+    chunks = [stream[i:i + 65536] for i in range(0, len(stream), 65536)]
+    got = []
+    for ch in chunks:
+        r.write(ch)
+        got += gev_amd.handler_protocol(proto, c, r, lambda cc, h, d: d)
+    st = proto.stats()
+    assert got == [data, b"tail"]
+    assert st["device_passes"] == 1, st
+    assert st["gated"] >= len(chunks) - 1, st
+    assert r.length() == 0
+
+
+def test_carry_survives_deliveries_and_external_consumption(engine):
+    """The carried gate is tied to the ring's read position: frames delivered
+    by UnPacket keep it exact, bytes consumed by anyone else invalidate it."""
+    rng = np.random.default_rng(32)
+    proto = gev_amd.Protocol(engine)
+    c, r = gev_amd.Connection(), gev_amd.RingBuffer(64)
+    frames = [bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) for n in (10, 300, 5000, 0, 70000, 3)]
+    wire = b"".join(wo.encode_frame(d, 2, True, 0, True, bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+                    for d in frames)
+    got, pos = [], 0
+    while pos < len(wire):
+        n = int(rng.integers(1, 9000))
+        r.write(wire[pos:pos + n])
+        pos += n
+        got += gev_amd.handler_protocol(proto, c, r, lambda cc, h, d: d if d else None)
+    assert got == [d for d in frames if d]
+    # external consumption: a partial frame is dropped by the caller, then a
+    # short complete frame follows; the stale carry must not hide it
+    big = wo.encode_frame(bytes(1000), 2, True, 0, True, b"\x01\x02\x03\x04")
+    r.write(big[:500])
+    assert proto.unpacket(c, r) == (None, None)
+    r.retrieve(500)
+    small = wo.encode_frame(b"abc", 1, True, 0, True, b"\x05\x06\x07\x08")
+    r.write(small + bytes(6))
+    h, d = proto.unpacket(c, r)
+    assert d == b"abc" and h.opcode == 1
+
+
+def test_duplicate_connection_in_one_batch(engine):
+    """the same (connection, ring) twice in one UnPacketBatch is
+    decoded once; frames are delivered once and stay aligned."""
+    proto = gev_amd.Protocol(engine)
+    c, r = gev_amd.Connection(), gev_amd.RingBuffer(256)
+    w = [wo.encode_frame(bytes([i]) * (50 + i), 2, True, 0, True, bytes([i, 1, 2, 3])) for i in range(5)]
+    r.write(b"".join(w) + bytes(3))
+    n = proto.unpacket_batch([c, c, c], [r, r, r])
+    assert n == 5 and c.pending() == 5
+    for i in range(5):
+        h, d = proto.unpacket(c, r)
+        assert d == bytes([i]) * (50 + i)
+    assert proto.unpacket(c, r) == (None, None) and r.length() == 3
+    assert proto.stats()["device_passes"] == 1
