@@ -90,16 +90,49 @@ def cpu_sample_layout(name: str, mib: int = 256):
     return w.config_c5(n_conns=mib // 8, seed=1)
 
 
+def host_cpu_info() -> dict:
+    """The host the CPU baseline runs on: model, logical CPUs (nproc), the CPUs
+    this process may run on (affinity) and the cgroup CPU quota, if any."""
+    info = {"model": None, "nproc": os.cpu_count(), "affinity": None, "cgroup_cpu_quota": None}
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                info["model"] = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def all_host_threads() -> int:
+    """One thread per CPU this process may use (nproc unless an affinity mask
+    narrows it) -- SURVEY.md §8d's "all host cores"."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(name: str, seconds: float, threads: int, vectorized: bool = False):
     import numpy as np
     from gev_amd import workloads as w
     from oracle import ref
-    lay = cpu_sample_layout(name, max(256, 64 * threads))
+    # >= 16 MiB of payload per thread (not cache-resident), 256 MiB .. 4 GiB in all
+    lay = cpu_sample_layout(name, min(4096, max(256, 16 * threads)))
     arena = np.concatenate([w.synth_host(lay), np.zeros(64, np.uint8)])
     secs, pb, nf = ref.bench_pipeline(arena, lay.conns[:, 0], lay.conns[:, 1], threads=threads,
                                       min_seconds=seconds, vectorized=vectorized)
     return dict(value=round(pb / secs / 2**30, 4), unit="GiB/s", cores=threads, kind="port",
-                frames_per_s=round(nf / secs, 1),
+                frames_per_s=round(nf / secs, 1), host=host_cpu_info(),
                 sample=(f"{lay.name}, {lay.n_conns} connections round-robin over {threads} thread(s), "
                         f"repeated for >= {seconds:.0f} s; oracle/ws_ref.c per-frame UnPacket pipeline "
                         "(header parse, zero-filled make, ring Read copy, Cipher u64 loop), "
@@ -133,7 +166,8 @@ def main():
                     help="weak: each GPU its own batch of the config's shape (default for c2/c3/c5); "
                          "strong: one global batch sharded over the GPUs by LPT (default for c4)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads-multi", type=int, default=16)
+    ap.add_argument("--cpu-threads-multi", type=int, default=0,
+                    help="threads of the all-cores CPU baseline (0 = every CPU this process may use)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--copy-reps", type=int, default=5, help="streaming-copy ceiling reps (0 = skip)")
     ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
@@ -311,6 +345,8 @@ def main():
                    "batches_in_flight": M,
                    **({"emulated_shard": emulated} if emulated else {})},
         "frames_per_s": round(frames_step * args.steps / elapsed, 1),
+        "decoded_per_step": {"frames": frames_step, "payload_bytes": payload_step, "errors": errors,
+                             "ranks_summed": world},
         "errors": errors,
         "phases_ms": {"walk_count": round(mean_ms[0], 4), "scan": round(mean_ms[1], 4),
                       "walk_emit": round(mean_ms[2], 4), "unmask": round(unmask_ms, 4)},
@@ -328,10 +364,10 @@ def main():
     if world == 1 and not args.no_cpu:
         log("cpu baseline (1 thread)...")
         result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds, 1)
-        if args.cpu_threads_multi > 1:
-            log(f"cpu baseline ({args.cpu_threads_multi} threads)...")
-            result["cpu_baseline_multi"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0),
-                                                        args.cpu_threads_multi)
+        nt = args.cpu_threads_multi or all_host_threads()
+        if nt > 1:
+            log(f"cpu baseline ({nt} threads)...")
+            result["cpu_baseline_multi"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0), nt)
         log("cpu baseline (1 thread, auto-vectorised build)...")
         result["cpu_baseline_vectorized"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0), 1,
                                                          vectorized=True)

@@ -1,393 +1,51 @@
-// ws_loopback.cpp -- live loopback websocket echo server over the C ABI
-// (host ingress) plus the ping-pong client of
-// benchmarks/bench-websocket-pingpong.sh (C1), in one process.
-//
-// Server, shaped like gev: L event loops (eventloop.go), each with its own
-// epoll, SO_REUSEPORT listener, gevws_ctx + gevws_protocol (one context per
-// loop, thread-confined), and per connection a gevws_conn + gevws_ring
-// (connection.go).  One loop iteration = epoll_wait -> one read(2) of <= 64 KiB
-// per readable connection into its ring (handleRead, connection.go:220-251;
-// eventloop.go:15) -> ONE device pass over every readable upgraded connection
-// (gevws_protocol_unpacket_batch: PeekAll segments gathered into pinned
-// staging, H2D, decode, D2H) -> per connection UnPacket until (nil, nil)
-// (handlerProtocol, connection.go:208-218), answering the handshake
-// (gevws_upgrader, ws.go:158-343) and echoing every data frame as a binary
-// frame (benchmarks/websocket/server.go:22-29, ws.NewBinaryFrame +
-// FrameToBytes) -> write(2).  Partial frames stay in the ring for the next
-// pass (the streaming carry across batches).
-//
-// Client: C connections spread over T threads; each does the upgrade, then
-// sends one masked text frame of M random bytes, waits for the echo, checks it
-// byte for byte, repeats for the run time.
-//
-//   ws_loopback [--conns 1000] [--msg 128] [--seconds 5] [--loops 1]
-//               [--client-threads 4] [--port 0] [--device 0]
-// Prints one JSON line.
-#include <arpa/inet.h>
-#include <errno.h>
-#include <fcntl.h>
-#include <netinet/in.h>
-#include <netinet/tcp.h>
-#include <sys/epoll.h>
-#include <sys/resource.h>
-#include <sys/socket.h>
-#include <unistd.h>
-
-#include <atomic>
-#include <chrono>
-#include <cstdint>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <random>
-#include <string>
-#include <thread>
-#include <unordered_map>
-#include <vector>
-
-#include "gevws.h"
+// ws_loopback.cpp -- the live loopback echo server over the C ABI with the
+// device decode (host ingress; C1's plumbing shape).
+// Server/client skeleton: ws_loopback.hpp.  Per loop iteration ONE device pass
+// over every readable upgraded connection (gevws_protocol_unpacket_batch:
+// PeekAll segments gathered into pinned staging, H2D, decode, D2H), then
+// websocket.(*Protocol).UnPacket per connection hands the frames out.
+#include "ws_loopback.hpp"
 
 namespace {
 
-std::atomic<bool> g_stop{false};
-std::atomic<uint64_t> g_batches{0}, g_batch_conns{0}, g_frames{0}, g_bad{0}, g_dev_ns{0};
-
-double now_s() {
-  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
-void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK); }
-
-// ws.WriteHeader (write.go:48-84) for a server frame (unmasked).
-uint32_t write_header(uint8_t* o, uint8_t b0, uint64_t len) {
-  o[0] = b0;
-  if (len <= 125) {
-    o[1] = (uint8_t)len;
-    return 2;
-  }
-  if (len <= 0xFFFF) {
-    o[1] = 126;
-    o[2] = (uint8_t)(len >> 8);
-    o[3] = (uint8_t)len;
-    return 4;
-  }
-  o[1] = 127;
-  for (int i = 0; i < 8; ++i) o[2 + i] = (uint8_t)(len >> (56 - 8 * i));
-  return 10;
-}
-
-bool send_all(int fd, const uint8_t* p, size_t n) {
-  while (n) {
-    ssize_t w = ::send(fd, p, n, MSG_NOSIGNAL);
-    if (w < 0) {
-      if (errno == EAGAIN || errno == EINTR) continue;  // loopback: the peer drains promptly
-      return false;
-    }
-    p += w;
-    n -= (size_t)w;
-  }
-  return true;
-}
-
-// ------------------------------------------------------------------ server
-struct ServerConn {
-  int fd;
-  gevws_conn* c;
-  gevws_ring* r;
-  std::vector<uint8_t> out;
-};
-
-void server_loop(int port, int device, std::atomic<int>* ready) {
-  gevws_ctx* ctx = gevws_ctx_create(device);
-  if (!ctx) {
-    fprintf(stderr, "ws_loopback: no device %d\n", device);
-    exit(2);
-  }
-  gevws_protocol* p = gevws_protocol_new(ctx);
-  gevws_upgrader* u = gevws_upgrader_new();  // &ws.Upgrader{} as benchmarks/websocket/server.go:52
-  gevws_protocol_set_upgrader(p, u);
-
-  int ls = socket(AF_INET, SOCK_STREAM, 0);
-  int one = 1;
-  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-  setsockopt(ls, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
-  sockaddr_in a{};
-  a.sin_family = AF_INET;
-  a.sin_port = htons((uint16_t)port);
-  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-  if (bind(ls, (sockaddr*)&a, sizeof(a)) || listen(ls, 4096)) {
-    perror("ws_loopback: bind/listen");
-    exit(2);
-  }
-  set_nonblock(ls);
-  int ep = epoll_create1(0);
-  epoll_event ev{};
-  ev.events = EPOLLIN;
-  ev.data.fd = ls;
-  epoll_ctl(ep, EPOLL_CTL_ADD, ls, &ev);
-  ready->fetch_add(1);
-
-  std::unordered_map<int, ServerConn> conns;
-  std::vector<epoll_event> evs(4096);
-  std::vector<uint8_t> rbuf(65536);  // the loop's packet buffer (eventloop.go:15)
-  std::vector<ServerConn*> readable;
+struct DeviceDecoder {
+  gevws_ctx* ctx;
+  gevws_protocol* p;
+  gevws_upgrader* u;
   std::vector<gevws_conn*> bc;
   std::vector<gevws_ring*> br;
-  while (!g_stop.load(std::memory_order_relaxed)) {
-    const int n = epoll_wait(ep, evs.data(), (int)evs.size(), 5);
-    readable.clear();
-    for (int i = 0; i < n; ++i) {
-      const int fd = evs[i].data.fd;
-      if (fd == ls) {
-        for (;;) {
-          int cfd = accept4(ls, nullptr, nullptr, SOCK_NONBLOCK);
-          if (cfd < 0) break;
-          setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-          ServerConn sc{cfd, gevws_conn_new(), gevws_ring_new(4096), {}};  // DefaultBufferSize
-          gevws_conn_set_upgraded(sc.c, 0);
-          conns.emplace(cfd, std::move(sc));
-          epoll_event ce{};
-          ce.events = EPOLLIN;
-          ce.data.fd = cfd;
-          epoll_ctl(ep, EPOLL_CTL_ADD, cfd, &ce);
-        }
-        continue;
-      }
-      auto it = conns.find(fd);
-      if (it == conns.end()) continue;
-      const ssize_t k = ::read(fd, rbuf.data(), rbuf.size());  // one read per event (handleRead)
-      if (k <= 0) {
-        if (k < 0 && (errno == EAGAIN || errno == EINTR)) continue;
-        epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
-        close(fd);
-        gevws_conn_free(it->second.c);
-        gevws_ring_free(it->second.r);
-        conns.erase(it);
-        continue;
-      }
-      gevws_ring_write(it->second.r, rbuf.data(), (uint64_t)k);
-      readable.push_back(&it->second);
+
+  explicit DeviceDecoder(int device) {
+    ctx = gevws_ctx_create(device);
+    if (!ctx) {
+      fprintf(stderr, "ws_loopback: no device %d\n", device);
+      exit(2);
     }
-    if (readable.empty()) continue;
-    // one device pass over every readable upgraded connection
+    p = gevws_protocol_new(ctx);
+    u = gevws_upgrader_new();  // &ws.Upgrader{} as benchmarks/websocket/server.go:52
+    gevws_protocol_set_upgrader(p, u);
+  }
+  ~DeviceDecoder() {
+    gevws_protocol_free(p);
+    gevws_upgrader_free(u);
+    gevws_ctx_destroy(ctx);
+  }
+  int64_t pass(wslb::ServerConn* const* conns, uint32_t n) {
     bc.clear();
     br.clear();
-    for (ServerConn* s : readable)
-      if (gevws_conn_upgraded(s->c)) {
-        bc.push_back(s->c);
-        br.push_back(s->r);
-      }
-    if (!bc.empty()) {
-      const double td = now_s();
-      const int64_t f = gevws_protocol_unpacket_batch(p, bc.data(), br.data(), (uint32_t)bc.size());
-      g_dev_ns.fetch_add((uint64_t)((now_s() - td) * 1e9), std::memory_order_relaxed);
-      if (f < 0) {
-        fprintf(stderr, "ws_loopback: unpacket_batch %s\n", gevws_status_string((int)f));
-        exit(3);
-      }
-      g_batches.fetch_add(1, std::memory_order_relaxed);
-      g_batch_conns.fetch_add(bc.size(), std::memory_order_relaxed);
+    for (uint32_t i = 0; i < n; ++i) {
+      bc.push_back(conns[i]->c);
+      br.push_back(conns[i]->r);
     }
-    // handlerProtocol per connection
-    for (ServerConn* s : readable) {
-      s->out.clear();
-      for (;;) {
-        gevws_header h;
-        const uint8_t* data;
-        uint64_t len;
-        const int st = gevws_protocol_unpacket(p, s->c, s->r, &h, &data, &len);
-        if (st == GEVWS_OK) {
-          if (h.opcode & 0x8) continue;  // control frames: not in this workload
-          uint8_t hdr[14];
-          const uint32_t hn = write_header(hdr, 0x82, len);  // NewBinaryFrame + FrameToBytes
-          s->out.insert(s->out.end(), hdr, hdr + hn);
-          s->out.insert(s->out.end(), data, data + len);
-          g_frames.fetch_add(1, std::memory_order_relaxed);
-        } else if (len != 0) {
-          s->out.insert(s->out.end(), data, data + len);  // handshake response (wrap.go:40-42)
-        } else {
-          break;
-        }
-      }
-      if (!s->out.empty() && !send_all(s->fd, s->out.data(), s->out.size())) g_bad.fetch_add(1);
-    }
+    return gevws_protocol_unpacket_batch(p, bc.data(), br.data(), n);
   }
-  for (auto& kv : conns) {
-    close(kv.first);
-    gevws_conn_free(kv.second.c);
-    gevws_ring_free(kv.second.r);
+  int unpacket(wslb::ServerConn* s, gevws_header* h, const uint8_t** data, uint64_t* len) {
+    return gevws_protocol_unpacket(p, s->c, s->r, h, data, len);
   }
-  close(ls);
-  close(ep);
-  gevws_protocol_free(p);
-  gevws_upgrader_free(u);
-  gevws_ctx_destroy(ctx);
-}
-
-// ------------------------------------------------------------------ client
-struct ClientConn {
-  int fd;
-  bool upgraded = false;
-  std::vector<uint8_t> in;
-  std::vector<uint8_t> sent;  // payload of the frame in flight
-  uint64_t done = 0;
+  static const char* name() { return "device"; }
+  static const char* path() { return "batched device decode (gevws_protocol_unpacket_batch) -> UnPacket"; }
 };
-
-void client_send(ClientConn& c, std::mt19937_64& rng, size_t msg) {
-  c.sent.resize(msg);
-  for (auto& b : c.sent) b = (uint8_t)rng();
-  std::vector<uint8_t> f(14 + msg);
-  uint32_t hn = write_header(f.data(), 0x81, msg);  // masked text frame (x/net/websocket client)
-  f[1] |= 0x80;
-  const uint32_t key = (uint32_t)rng();
-  uint8_t m[4];
-  memcpy(m, &key, 4);
-  memcpy(f.data() + hn, m, 4);
-  hn += 4;
-  for (size_t i = 0; i < msg; ++i) f[hn + i] = c.sent[i] ^ m[i & 3];
-  if (!send_all(c.fd, f.data(), hn + msg)) g_bad.fetch_add(1);
-}
-
-void client_thread(int port, int nconn, size_t msg, double t_end, std::atomic<uint64_t>* total,
-                   std::atomic<int>* upgraded_conns, unsigned seed) {
-  std::mt19937_64 rng(seed);
-  int ep = epoll_create1(0);
-  std::vector<ClientConn> cs(nconn);
-  const char req_fmt[] =
-      "GET / HTTP/1.1\r\nHost: 127.0.0.1:%d\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
-      "Sec-WebSocket-Key: dGhlIHNhbXBsZSBub25jZQ==\r\nOrigin: ws://127.0.0.1\r\nSec-WebSocket-Version: 13\r\n\r\n";
-  char req[512];
-  const int rn = snprintf(req, sizeof(req), req_fmt, port);
-  for (int i = 0; i < nconn; ++i) {
-    int fd = socket(AF_INET, SOCK_STREAM, 0);
-    if (fd < 0) {
-      perror("ws_loopback: socket");
-      _exit(2);
-    }
-    sockaddr_in a{};
-    a.sin_family = AF_INET;
-    a.sin_port = htons((uint16_t)port);
-    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-    if (connect(fd, (sockaddr*)&a, sizeof(a))) {
-      perror("ws_loopback: connect");
-      _exit(2);  // other threads are running: no static destructors
-    }
-    int one = 1;
-    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-    set_nonblock(fd);
-    cs[i].fd = fd;
-    epoll_event ev{};
-    ev.events = EPOLLIN;
-    ev.data.u32 = (uint32_t)i;
-    epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
-    send_all(fd, (const uint8_t*)req, (size_t)rn);
-  }
-  std::vector<epoll_event> evs(1024);
-  std::vector<uint8_t> buf(1 << 16);
-  while (now_s() < t_end && !g_stop.load(std::memory_order_relaxed)) {
-    const int n = epoll_wait(ep, evs.data(), (int)evs.size(), 5);
-    for (int e = 0; e < n; ++e) {
-      ClientConn& c = cs[evs[e].data.u32];
-      const ssize_t k = ::read(c.fd, buf.data(), buf.size());
-      if (k <= 0) continue;
-      c.in.insert(c.in.end(), buf.data(), buf.data() + k);
-      if (!c.upgraded) {
-        const std::string s(c.in.begin(), c.in.end());
-        const size_t pos = s.find("\r\n\r\n");
-        if (pos == std::string::npos) continue;
-        if (s.compare(0, 12, "HTTP/1.1 101") != 0 || s.find("s3pPLMBiTxaQ9kYGzzhZRbK+xOo=") == std::string::npos) {
-          g_bad.fetch_add(1);
-          continue;
-        }
-        c.in.erase(c.in.begin(), c.in.begin() + (long)pos + 4);
-        c.upgraded = true;
-        upgraded_conns->fetch_add(1);
-        client_send(c, rng, msg);
-        continue;
-      }
-      // echo: unmasked binary frame carrying the same bytes
-      const size_t hn = msg <= 125 ? 2 : (msg <= 0xFFFF ? 4 : 10);
-      while (c.in.size() >= hn + msg) {
-        if (c.in[0] != 0x82 || memcmp(c.in.data() + hn, c.sent.data(), msg) != 0) g_bad.fetch_add(1);
-        c.in.erase(c.in.begin(), c.in.begin() + (long)(hn + msg));
-        c.done++;
-        client_send(c, rng, msg);
-      }
-    }
-  }
-  uint64_t sum = 0;
-  for (auto& c : cs) {
-    sum += c.done;
-    close(c.fd);
-  }
-  total->fetch_add(sum);
-  close(ep);
-}
 
 }  // namespace
 
-int main(int argc, char** argv) {
-  int conns = 1000, loops = 1, cthreads = 4, port = 0, device = 0;
-  size_t msg = 128;
-  double seconds = 5.0;
-  for (int i = 1; i + 1 < argc; i += 2) {
-    const std::string k = argv[i];
-    const char* v = argv[i + 1];
-    if (k == "--conns") conns = atoi(v);
-    else if (k == "--msg") msg = (size_t)atol(v);
-    else if (k == "--seconds") seconds = atof(v);
-    else if (k == "--loops") loops = atoi(v);
-    else if (k == "--client-threads") cthreads = atoi(v);
-    else if (k == "--port") port = atoi(v);
-    else if (k == "--device") device = atoi(v);
-  }
-  if (port == 0) port = 20000 + (int)(getpid() % 20000);
-  // both ends of every connection live in this process: 2 fds per connection
-  rlimit rl{};
-  getrlimit(RLIMIT_NOFILE, &rl);
-  rl.rlim_cur = rl.rlim_max;
-  setrlimit(RLIMIT_NOFILE, &rl);
-  if ((uint64_t)conns * 2 + 64 > (uint64_t)rl.rlim_cur) {
-    fprintf(stderr, "ws_loopback: %d connections need %d fds, RLIMIT_NOFILE is %llu\n", conns, conns * 2 + 64,
-            (unsigned long long)rl.rlim_cur);
-    return 2;
-  }
-  std::atomic<int> ready{0};
-  std::vector<std::thread> servers;
-  for (int l = 0; l < loops; ++l) servers.emplace_back(server_loop, port, device, &ready);
-  while (ready.load() < loops) std::this_thread::sleep_for(std::chrono::milliseconds(5));
-
-  std::atomic<uint64_t> total{0};
-  std::atomic<int> upgraded{0};
-  const double warm = 1.0;
-  const double t0 = now_s();
-  const double t_end = t0 + warm + seconds;
-  std::vector<std::thread> clients;
-  for (int t = 0; t < cthreads; ++t) {
-    const int n = conns / cthreads + (t < conns % cthreads ? 1 : 0);
-    clients.emplace_back(client_thread, port, n, msg, t_end, &total, &upgraded, 1234u + t);
-  }
-  // measure the steady state: count frames echoed between warm-up end and t_end
-  std::this_thread::sleep_for(std::chrono::duration<double>(warm));
-  const uint64_t f0 = g_frames.load(), b0 = g_batches.load(), c0 = g_batch_conns.load(), d0 = g_dev_ns.load();
-  const double ts = now_s();
-  std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
-  const double te = now_s();
-  const uint64_t f1 = g_frames.load(), b1 = g_batches.load(), c1 = g_batch_conns.load(), d1 = g_dev_ns.load();
-  for (auto& t : clients) t.join();
-  g_stop = true;
-  for (auto& t : servers) t.join();
-  const double dt = te - ts;
-  const double mps = (double)(f1 - f0) / dt;
-  printf("{\"path\": \"loopback websocket echo server: epoll loops -> ring buffers -> batched device decode "
-         "(gevws_protocol_unpacket_batch) -> UnPacket -> echo\", \"connections\": %d, \"upgraded\": %d, "
-         "\"msg_bytes\": %zu, \"loops\": %d, \"client_threads\": %d, \"seconds\": %.3f, "
-         "\"echoes_per_s\": %.1f, \"payload_MiBps_each_way\": %.2f, \"device_batches_per_s\": %.1f, "
-         "\"mean_conns_per_batch\": %.1f, \"device_pass_us_mean\": %.1f, \"device_pass_share_of_loop_time\": %.3f, "
-         "\"client_checked_echoes\": %llu, \"errors\": %llu}\n",
-         conns, upgraded.load(), msg, loops, cthreads, dt, mps, mps * (double)msg / 1048576.0,
-         (double)(b1 - b0) / dt, b1 > b0 ? (double)(c1 - c0) / (double)(b1 - b0) : 0.0,
-         b1 > b0 ? (double)(d1 - d0) / 1e3 / (double)(b1 - b0) : 0.0, (double)(d1 - d0) / 1e9 / (dt * loops),
-         (unsigned long long)total.load(), (unsigned long long)g_bad.load());
-  return g_bad.load() == 0 && upgraded.load() == conns ? 0 : 1;
-}
+int main(int argc, char** argv) { return wslb::loopback_main<DeviceDecoder>(argc, argv); }

@@ -1,0 +1,402 @@
+// ws_loopback.hpp -- live loopback websocket echo server + the ping-pong
+// client of benchmarks/bench-websocket-pingpong.sh (C1), in one process, with
+// the server's frame decoder as a template parameter:
+//
+//   gev_amd/ws_loopback      DeviceDecoder (ws_loopback.cpp): one device pass
+//                            per loop iteration over every readable upgraded
+//                            connection (gevws_protocol_unpacket_batch), then
+//                            UnPacket per connection -- the product path.
+//   tools/ws_loopback_cpu    the CPU baseline beside it: the reference's
+//                            per-frame UnPacket pipeline restated in
+//                            oracle/ws_ref.c (header parse, make, ring Read,
+//                            Cipher) on the loop's own core.  Never linked into
+//                            libgevws.so or gev_amd/ws_loopback.
+//
+// Server, shaped like gev: L event loops (eventloop.go), each with its own
+// epoll, SO_REUSEPORT listener and decoder (one context + protocol per loop,
+// thread-confined), and per connection a gevws_conn + gevws_ring
+// (connection.go).  One loop iteration = epoll_wait -> one read(2) of <= 64 KiB
+// per readable connection into its ring (handleRead, connection.go:220-251;
+// eventloop.go:15) -> decoder pass -> per connection UnPacket until (nil, nil)
+// (handlerProtocol, connection.go:208-218), answering the handshake
+// (gevws_upgrader, ws.go:158-343) and echoing every data frame as a binary
+// frame (benchmarks/websocket/server.go:22-29, ws.NewBinaryFrame +
+// FrameToBytes) -> write(2).  Partial frames stay in the ring for the next
+// pass (the streaming carry across batches).
+//
+// Client: C connections spread over T threads; each does the upgrade, then
+// sends one masked text frame of M random bytes, waits for the echo, checks it
+// byte for byte, repeats for the run time.
+//
+//   [--conns 1000] [--msg 128] [--seconds 5] [--loops 1] [--client-threads 4]
+//   [--port 0] [--device 0]
+// Prints one JSON line.
+#pragma once
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/resource.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "gevws.h"
+
+namespace wslb {
+
+inline std::atomic<bool> g_stop{false};
+inline std::atomic<uint64_t> g_batches{0}, g_batch_conns{0}, g_frames{0}, g_bad{0}, g_dev_ns{0};
+
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+inline void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK); }
+
+// ws.WriteHeader (write.go:48-84) for a server frame (unmasked).
+inline uint32_t write_header(uint8_t* o, uint8_t b0, uint64_t len) {
+  o[0] = b0;
+  if (len <= 125) {
+    o[1] = (uint8_t)len;
+    return 2;
+  }
+  if (len <= 0xFFFF) {
+    o[1] = 126;
+    o[2] = (uint8_t)(len >> 8);
+    o[3] = (uint8_t)len;
+    return 4;
+  }
+  o[1] = 127;
+  for (int i = 0; i < 8; ++i) o[2 + i] = (uint8_t)(len >> (56 - 8 * i));
+  return 10;
+}
+
+inline bool send_all(int fd, const uint8_t* p, size_t n) {
+  while (n) {
+    ssize_t w = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EAGAIN || errno == EINTR) continue;  // loopback: the peer drains promptly
+      return false;
+    }
+    p += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ server
+struct ServerConn {
+  int fd;
+  gevws_conn* c;
+  gevws_ring* r;
+  std::vector<uint8_t> out;
+  std::vector<uint8_t> frame;  // CpuDecoder: the payload slice it returned last (Go's make)
+  int poisoned = 0;
+};
+
+// Decoder concept:
+//   explicit Decoder(int device);
+//   int64_t pass(ServerConn* const* conns, uint32_t n);   // readable upgraded connections
+//   int unpacket(ServerConn* s, gevws_header* h, const uint8_t** data, uint64_t* len);
+//   static const char* name();
+template <class Decoder>
+void server_loop(int port, int device, std::atomic<int>* ready) {
+  Decoder dec(device);
+  int ls = socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  setsockopt(ls, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port);
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  if (bind(ls, (sockaddr*)&a, sizeof(a)) || listen(ls, 4096)) {
+    perror("ws_loopback: bind/listen");
+    exit(2);
+  }
+  set_nonblock(ls);
+  int ep = epoll_create1(0);
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.fd = ls;
+  epoll_ctl(ep, EPOLL_CTL_ADD, ls, &ev);
+  ready->fetch_add(1);
+
+  std::unordered_map<int, ServerConn> conns;
+  std::vector<epoll_event> evs(4096);
+  std::vector<uint8_t> rbuf(65536);  // the loop's packet buffer (eventloop.go:15)
+  std::vector<ServerConn*> readable, upgraded;
+  while (!g_stop.load(std::memory_order_relaxed)) {
+    const int n = epoll_wait(ep, evs.data(), (int)evs.size(), 5);
+    readable.clear();
+    for (int i = 0; i < n; ++i) {
+      const int fd = evs[i].data.fd;
+      if (fd == ls) {
+        for (;;) {
+          int cfd = accept4(ls, nullptr, nullptr, SOCK_NONBLOCK);
+          if (cfd < 0) break;
+          setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+          ServerConn sc{cfd, gevws_conn_new(), gevws_ring_new(4096), {}, {}, 0};  // DefaultBufferSize
+          gevws_conn_set_upgraded(sc.c, 0);
+          conns.emplace(cfd, std::move(sc));
+          epoll_event ce{};
+          ce.events = EPOLLIN;
+          ce.data.fd = cfd;
+          epoll_ctl(ep, EPOLL_CTL_ADD, cfd, &ce);
+        }
+        continue;
+      }
+      auto it = conns.find(fd);
+      if (it == conns.end()) continue;
+      const ssize_t k = ::read(fd, rbuf.data(), rbuf.size());  // one read per event (handleRead)
+      if (k <= 0) {
+        if (k < 0 && (errno == EAGAIN || errno == EINTR)) continue;
+        epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
+        close(fd);
+        gevws_conn_free(it->second.c);
+        gevws_ring_free(it->second.r);
+        conns.erase(it);
+        continue;
+      }
+      gevws_ring_write(it->second.r, rbuf.data(), (uint64_t)k);
+      readable.push_back(&it->second);
+    }
+    if (readable.empty()) continue;
+    upgraded.clear();
+    for (ServerConn* s : readable)
+      if (gevws_conn_upgraded(s->c)) upgraded.push_back(s);
+    // decode time of the iteration: the pass plus the UnPacket calls (the
+    // device decoder's UnPacket only pops queued frames; the CPU decoder's
+    // does the whole per-frame pipeline), not the echo's encode or write(2)
+    double t_dec = 0;
+    if (!upgraded.empty()) {
+      const double td = now_s();
+      const int64_t f = dec.pass(upgraded.data(), (uint32_t)upgraded.size());
+      t_dec += now_s() - td;
+      if (f < 0) {
+        fprintf(stderr, "ws_loopback: decoder pass %s\n", gevws_status_string((int)f));
+        exit(3);
+      }
+      g_batches.fetch_add(1, std::memory_order_relaxed);
+      g_batch_conns.fetch_add(upgraded.size(), std::memory_order_relaxed);
+    }
+    // handlerProtocol per connection
+    for (ServerConn* s : readable) {
+      s->out.clear();
+      for (;;) {
+        gevws_header h;
+        const uint8_t* data = nullptr;
+        uint64_t len = 0;
+        const double tu = now_s();
+        const int st = dec.unpacket(s, &h, &data, &len);
+        t_dec += now_s() - tu;
+        if (st == GEVWS_OK) {
+          if (h.opcode & 0x8) continue;  // control frames: not in this workload
+          uint8_t hdr[14];
+          const uint32_t hn = write_header(hdr, 0x82, len);  // NewBinaryFrame + FrameToBytes
+          s->out.insert(s->out.end(), hdr, hdr + hn);
+          s->out.insert(s->out.end(), data, data + len);
+          g_frames.fetch_add(1, std::memory_order_relaxed);
+        } else if (len != 0) {
+          s->out.insert(s->out.end(), data, data + len);  // handshake response (wrap.go:40-42)
+        } else {
+          break;
+        }
+      }
+      if (!s->out.empty() && !send_all(s->fd, s->out.data(), s->out.size())) g_bad.fetch_add(1);
+    }
+    g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
+  }
+  for (auto& kv : conns) {
+    close(kv.first);
+    gevws_conn_free(kv.second.c);
+    gevws_ring_free(kv.second.r);
+  }
+  close(ls);
+  close(ep);
+}
+
+// ------------------------------------------------------------------ client
+struct ClientConn {
+  int fd;
+  bool upgraded = false;
+  std::vector<uint8_t> in;
+  std::vector<uint8_t> sent;  // payload of the frame in flight
+  uint64_t done = 0;
+};
+
+inline void client_send(ClientConn& c, std::mt19937_64& rng, size_t msg) {
+  c.sent.resize(msg);
+  for (auto& b : c.sent) b = (uint8_t)rng();
+  std::vector<uint8_t> f(14 + msg);
+  uint32_t hn = write_header(f.data(), 0x81, msg);  // masked text frame (x/net/websocket client)
+  f[1] |= 0x80;
+  const uint32_t key = (uint32_t)rng();
+  uint8_t m[4];
+  memcpy(m, &key, 4);
+  memcpy(f.data() + hn, m, 4);
+  hn += 4;
+  for (size_t i = 0; i < msg; ++i) f[hn + i] = c.sent[i] ^ m[i & 3];
+  if (!send_all(c.fd, f.data(), hn + msg)) g_bad.fetch_add(1);
+}
+
+inline void client_thread(int port, int nconn, size_t msg, double t_end, std::atomic<uint64_t>* total,
+                          std::atomic<int>* upgraded_conns, unsigned seed) {
+  std::mt19937_64 rng(seed);
+  int ep = epoll_create1(0);
+  std::vector<ClientConn> cs(nconn);
+  const char req_fmt[] =
+      "GET / HTTP/1.1\r\nHost: 127.0.0.1:%d\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+      "Sec-WebSocket-Key: dGhlIHNhbXBsZSBub25jZQ==\r\nOrigin: ws://127.0.0.1\r\nSec-WebSocket-Version: 13\r\n\r\n";
+  char req[512];
+  const int rn = snprintf(req, sizeof(req), req_fmt, port);
+  for (int i = 0; i < nconn; ++i) {
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) {
+      perror("ws_loopback: socket");
+      _exit(2);
+    }
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (connect(fd, (sockaddr*)&a, sizeof(a))) {
+      perror("ws_loopback: connect");
+      _exit(2);  // other threads are running: no static destructors
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    set_nonblock(fd);
+    cs[i].fd = fd;
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u32 = (uint32_t)i;
+    epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
+    send_all(fd, (const uint8_t*)req, (size_t)rn);
+  }
+  std::vector<epoll_event> evs(1024);
+  std::vector<uint8_t> buf(1 << 16);
+  while (now_s() < t_end && !g_stop.load(std::memory_order_relaxed)) {
+    const int n = epoll_wait(ep, evs.data(), (int)evs.size(), 5);
+    for (int e = 0; e < n; ++e) {
+      ClientConn& c = cs[evs[e].data.u32];
+      const ssize_t k = ::read(c.fd, buf.data(), buf.size());
+      if (k <= 0) continue;
+      c.in.insert(c.in.end(), buf.data(), buf.data() + k);
+      if (!c.upgraded) {
+        const std::string s(c.in.begin(), c.in.end());
+        const size_t pos = s.find("\r\n\r\n");
+        if (pos == std::string::npos) continue;
+        if (s.compare(0, 12, "HTTP/1.1 101") != 0 || s.find("s3pPLMBiTxaQ9kYGzzhZRbK+xOo=") == std::string::npos) {
+          g_bad.fetch_add(1);
+          continue;
+        }
+        c.in.erase(c.in.begin(), c.in.begin() + (long)pos + 4);
+        c.upgraded = true;
+        upgraded_conns->fetch_add(1);
+        client_send(c, rng, msg);
+        continue;
+      }
+      // echo: unmasked binary frame carrying the same bytes
+      const size_t hn = msg <= 125 ? 2 : (msg <= 0xFFFF ? 4 : 10);
+      while (c.in.size() >= hn + msg) {
+        if (c.in[0] != 0x82 || memcmp(c.in.data() + hn, c.sent.data(), msg) != 0) g_bad.fetch_add(1);
+        c.in.erase(c.in.begin(), c.in.begin() + (long)(hn + msg));
+        c.done++;
+        client_send(c, rng, msg);
+      }
+    }
+  }
+  uint64_t sum = 0;
+  for (auto& c : cs) {
+    sum += c.done;
+    close(c.fd);
+  }
+  total->fetch_add(sum);
+  close(ep);
+}
+
+template <class Decoder>
+int loopback_main(int argc, char** argv) {
+  int conns = 1000, loops = 1, cthreads = 4, port = 0, device = 0;
+  size_t msg = 128;
+  double seconds = 5.0;
+  for (int i = 1; i + 1 < argc; i += 2) {
+    const std::string k = argv[i];
+    const char* v = argv[i + 1];
+    if (k == "--conns") conns = atoi(v);
+    else if (k == "--msg") msg = (size_t)atol(v);
+    else if (k == "--seconds") seconds = atof(v);
+    else if (k == "--loops") loops = atoi(v);
+    else if (k == "--client-threads") cthreads = atoi(v);
+    else if (k == "--port") port = atoi(v);
+    else if (k == "--device") device = atoi(v);
+  }
+  if (port == 0) port = 20000 + (int)(getpid() % 20000);
+  // both ends of every connection live in this process: 2 fds per connection
+  rlimit rl{};
+  getrlimit(RLIMIT_NOFILE, &rl);
+  rl.rlim_cur = rl.rlim_max;
+  setrlimit(RLIMIT_NOFILE, &rl);
+  if ((uint64_t)conns * 2 + 64 > (uint64_t)rl.rlim_cur) {
+    fprintf(stderr, "ws_loopback: %d connections need %d fds, RLIMIT_NOFILE is %llu\n", conns, conns * 2 + 64,
+            (unsigned long long)rl.rlim_cur);
+    return 2;
+  }
+  std::atomic<int> ready{0};
+  std::vector<std::thread> servers;
+  for (int l = 0; l < loops; ++l) servers.emplace_back(server_loop<Decoder>, port, device, &ready);
+  while (ready.load() < loops) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+
+  std::atomic<uint64_t> total{0};
+  std::atomic<int> upgraded{0};
+  const double warm = 1.0;
+  const double t0 = now_s();
+  const double t_end = t0 + warm + seconds;
+  std::vector<std::thread> clients;
+  for (int t = 0; t < cthreads; ++t) {
+    const int n = conns / cthreads + (t < conns % cthreads ? 1 : 0);
+    clients.emplace_back(client_thread, port, n, msg, t_end, &total, &upgraded, 1234u + t);
+  }
+  // measure the steady state: count frames echoed between warm-up end and t_end
+  std::this_thread::sleep_for(std::chrono::duration<double>(warm));
+  const uint64_t f0 = g_frames.load(), b0 = g_batches.load(), c0 = g_batch_conns.load(), d0 = g_dev_ns.load();
+  const double ts = now_s();
+  std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+  const double te = now_s();
+  const uint64_t f1 = g_frames.load(), b1 = g_batches.load(), c1 = g_batch_conns.load(), d1 = g_dev_ns.load();
+  for (auto& t : clients) t.join();
+  g_stop = true;
+  for (auto& t : servers) t.join();
+  const double dt = te - ts;
+  const double mps = (double)(f1 - f0) / dt;
+  printf("{\"path\": \"loopback websocket echo server: epoll loops -> ring buffers -> %s -> echo\", "
+         "\"decoder\": \"%s\", \"connections\": %d, \"upgraded\": %d, "
+         "\"msg_bytes\": %zu, \"loops\": %d, \"client_threads\": %d, \"seconds\": %.3f, "
+         "\"echoes_per_s\": %.1f, \"payload_MiBps_each_way\": %.2f, \"decode_passes_per_s\": %.1f, "
+         "\"mean_conns_per_pass\": %.1f, \"decode_us_per_pass\": %.1f, \"decode_share_of_loop_time\": %.3f, "
+         "\"client_checked_echoes\": %llu, \"errors\": %llu}\n",
+         Decoder::path(), Decoder::name(), conns, upgraded.load(), msg, loops, cthreads, dt, mps,
+         mps * (double)msg / 1048576.0, (double)(b1 - b0) / dt,
+         b1 > b0 ? (double)(c1 - c0) / (double)(b1 - b0) : 0.0,
+         b1 > b0 ? (double)(d1 - d0) / 1e3 / (double)(b1 - b0) : 0.0, (double)(d1 - d0) / 1e9 / (dt * loops),
+         (unsigned long long)total.load(), (unsigned long long)g_bad.load());
+  return g_bad.load() == 0 && upgraded.load() == conns ? 0 : 1;
+}
+
+}  // namespace wslb

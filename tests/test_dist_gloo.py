@@ -37,6 +37,17 @@ def _worker(rank, world, port, outdir):
     dist.reduce_counts(counts)
     res["strong"] = counts.tolist()
     res["strong_conns"] = part.n_conns
+    # the bench's C4 strong split: greedy LPT over stream bytes (workloads.shard_lpt)
+    glob4 = w.config_c4(total_payload=3 << 20, n_conns=23, seed=13)
+    part = w.shard_lpt(glob4, rank, world)
+    arena = np.concatenate([w.synth_host(part), np.zeros(64, np.uint8)])
+    r = ref.decode_batch(arena, part.conns[:, 0], part.conns[:, 1])
+    counts = torch.tensor([r["frames"].shape[0], int(r["frames"]["length"].sum()),
+                           int((r["conn_status"] < 0).sum())], dtype=torch.int64)
+    dist.reduce_counts(counts)
+    res["lpt"] = counts.tolist()
+    res["lpt_conns"] = part.n_conns
+    res["lpt_max_bytes"] = dist.max_over_ranks(float(part.arena_bytes), "cpu")
     # weak scaling: every rank its own same-shape batch
     lay = w.uniform(3, 4, 1000, seed=dist.rank_seed(5, rank))
     arena = np.concatenate([w.synth_host(lay), np.zeros(64, np.uint8)])
@@ -58,11 +69,16 @@ def test_gloo_shard_and_count_reduce(tmp_path, world):
     mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
     glob = w.config_c5(n_conns=7, messages_per_conn=1, message_bytes=48 * 1024, seed=3)
+    glob4 = w.config_c4(total_payload=3 << 20, n_conns=23, seed=13)
+    lens4 = glob4.conns[:, 1]
     for r in res:
         assert r["strong"] == [glob.n_frames, glob.payload_len, 0]
+        assert r["lpt"] == [glob4.n_frames, glob4.payload_len, 0]
+        assert r["lpt_max_bytes"] <= 4 / 3 * max(lens4.sum() / world, lens4.max()) + 1  # Graham's bound
         assert r["weak"] == [world * 12, world * 12 * 1000, 0]
         assert r["max"] == float(world)
     assert sum(r["strong_conns"] for r in res) == glob.n_conns
+    assert sum(r["lpt_conns"] for r in res) == glob4.n_conns
 
 
 def test_shard_bounds_partition_and_balance():

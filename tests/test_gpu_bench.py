@@ -41,3 +41,38 @@ def test_bench_line_contract(inflight):
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert r["algorithmic_bytes_per_launch"] == 262144 * (8 + 2 * 4096)
     assert d["cpu_baseline"] is None  # --no-cpu
+
+
+def _bench_2rank(config, port, steps=3):
+    """The driver's N > 1 launch (torch.distributed.run, one process per rank)
+    with 2 ranks sharing this one GPU over gloo (RCCL allows one rank per
+    device): per-rank batches, bit-exact verification on every rank, the count
+    all-reduce, max-over-ranks timing and the rank-0-only JSON line."""
+    env = dict(os.environ, GEV_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--config", config, "--steps", str(steps), "--warmup", "1", "--no-cpu",
+                        "--copy-reps", "0"], cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_weak_c2():
+    d = _bench_2rank("c2", 29611)
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["errors"] == 0
+    c = d["decoded_per_step"]
+    assert c["ranks_summed"] == 2 and c["frames"] == 2 * 262144 and c["payload_bytes"] == 2 * 262144 * 4096
+    assert d["config"]["global_connections"] == 2 * d["config"]["connections_per_gpu"]
+
+
+def test_bench_two_ranks_strong_c4():
+    import bench
+    glob, _ = bench.build_layout("c4", 0, None)
+    d = _bench_2rank("c4", 29612, steps=2)
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["errors"] == 0
+    c = d["decoded_per_step"]
+    # the two LPT shares together are exactly the global batch
+    assert c["frames"] == glob.n_frames and c["payload_bytes"] == glob.payload_len
+    assert d["config"]["global_connections"] == glob.n_conns

@@ -324,6 +324,90 @@ def test_stream_over_4gib_and_small_frame_fallback(engine):
     _synth_decode_verify(engine, lay, check_slice_conns=8)
 
 
+def _oracle_compare_conns(engine, out, arena, layout, idx):
+    """Byte-compare the device result of the connections `idx` (any subset of
+    the batch) with the oracle: their streams are copied to the host, decoded
+    by oracle/ws_ref.c as a batch of their own, and every record / payload
+    byte is compared after rebasing offsets (input offsets by the stream's
+    position, payload offsets by the connection's arena base)."""
+    idx = np.asarray(idx, np.int64)
+    co = out.conn_out_host()
+    streams = [arena[int(layout.conns[c, 0]):int(layout.conns[c, 0] + layout.conns[c, 1])].cpu().numpy() for c in idx]
+    lens = np.array([x.size for x in streams], np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    want = ref.decode_batch(np.concatenate(streams + [np.zeros(64, np.uint8)]), offs, lens)
+    wf = want["frames"]
+    for j, c in enumerate(idx):
+        n = int(co["nframes"][c])
+        assert n == int(want["conn_nframes"][j]) and int(co["consumed"][c]) == int(want["conn_consumed"][j]), c
+        assert int(co["status"][c]) == int(want["conn_status"][j]), c
+        f0, w0 = int(co["first_frame"][c]), int(want["conn_first"][j])
+        g = out.frames[f0:f0 + n].cpu().numpy().reshape(-1).view(wf.dtype)
+        w = wf[w0:w0 + n]
+        assert g.view(np.uint8).reshape(-1, 32)[:, :16].tobytes() == w.view(np.uint8).reshape(-1, 32)[:, :16].tobytes(), c
+        gb, wb = int(co["payload_base"][c]), int(w["payload_off"][0]) if n else 0
+        assert np.array_equal(g["payload_off"] - np.uint64(gb), w["payload_off"] - np.uint64(wb)), c
+        assert np.array_equal(g["src_off"] - np.uint64(layout.conns[c, 0]), w["src_off"] - np.uint64(offs[j])), c
+        if n:
+            end = int(w["payload_off"][-1]) + (int(w["length"][-1]) + 15) // 16 * 16 - wb
+            gp = out.payload[gb:gb + end].cpu().numpy()
+            assert np.array_equal(gp, want["payload"][wb:wb + end]), c
+    return int(wf.shape[0])
+
+
+def _c4_full(engine, lay, n_check: int = 64):
+    """BASELINE config 4 at its configured size (or an LPT share of it): every
+    byte by the generator property, plus >= n_check connections -- the longest
+    chain among them -- byte-compared with the oracle."""
+    import torch
+    import gev_amd
+    dev = torch.device("cuda", engine.device)
+    free, _ = torch.cuda.mem_get_info(engine.device)
+    need = lay.arena_bytes + lay.payload_padded + lay.n_frames * 32 + lay.arena_bytes // 4 + (2 << 30)
+    if free < need:
+        pytest.fail(f"{lay.name}: needs {need / 2**30:.1f} GiB of HBM, {free / 2**30:.1f} GiB free")
+    arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    arena[lay.arena_bytes:] = 0
+    desc = torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev)
+    conns = torch.from_numpy(lay.conns.copy()).to(dev)
+    engine.synth(arena, desc, lay.n_frames, lay.seed)
+    out = engine.decode(arena, lay.arena_bytes, conns, lay.n_conns, max_frames=lay.n_frames,
+                        payload_cap=lay.payload_padded)
+    s = out.summary_host()
+    assert int(s["frames"]) == lay.n_frames and int(s["payload_len"]) == lay.payload_len
+    assert int(s["payload_bytes"]) == lay.payload_padded and int(s["errors"]) == 0 and int(s["flags"]) == 0
+    mism = torch.zeros(1, dtype=torch.int64, device=dev)
+    engine.verify(desc, lay.n_frames, lay.seed, out, mism)
+    torch.cuda.synchronize()
+    assert int(mism.item()) == 0
+    counts = np.diff(np.searchsorted(lay.desc["hdr_off"].astype(np.int64),
+                                     np.concatenate([lay.conns[:, 0], [lay.arena_bytes]])))
+    longest = int(np.argmax(counts))
+    rng = np.random.default_rng(4)
+    idx = np.unique(np.concatenate([[0, longest, lay.n_conns - 1],
+                                    rng.choice(lay.n_conns, min(n_check, lay.n_conns), replace=False)]))
+    nf = _oracle_compare_conns(engine, out, arena, lay, idx)
+    del arena, out, desc
+    torch.cuda.empty_cache()
+    return int(counts[longest]), nf, idx.size
+
+
+def test_c4_full_size_and_lpt_shards(engine):
+    """BASELINE config 4 exactly as bench.py builds it (16 GiB power-law
+    payload over 65 536 connections, 43.8 M frames) on one GPU, then rank 0's
+    and rank 7's greedy-LPT shares of the 8-way strong split."""
+    import bench
+    from gev_amd import workloads as w
+    glob, _ = bench.build_layout("c4", 0, None)
+    assert glob.payload_len >= 16 << 30 and glob.n_conns == 65536
+    longest, nf, k = _c4_full(engine, glob)
+    assert longest > 1000 and k >= 64 and nf > 0
+    for r in (0, 7):
+        part = w.shard_lpt(glob, r, 8)
+        assert part.n_conns == 65536 // 8 or abs(part.n_conns - 65536 // 8) < 65536 // 16
+        _c4_full(engine, part)
+
+
 def test_c4_power_law_property(engine):
     from gev_amd import workloads
     _synth_decode_verify(engine, workloads.config_c4(total_payload=64 << 20, n_conns=512), check_slice_conns=8)
