@@ -172,6 +172,7 @@ def main():
     ap.add_argument("--copy-reps", type=int, default=5, help="streaming-copy ceiling reps (0 = skip)")
     ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
     ap.add_argument("--unmask-variant", type=int, default=None, help="A/B: unmask kernel variant")
+    ap.add_argument("--emit-variant", type=int, default=None, help="A/B: record pass variant (GEVWS_TUNE_EMIT_VARIANT)")
     ap.add_argument("--emulate-shard", default=None, metavar="R/N",
                     help="projection, not the contract line: decode only rank R's LPT share of an N-way strong "
                          "split of the global batch, on this one GPU")
@@ -204,6 +205,8 @@ def main():
             e.set_tuning(_abi.TUNE_WALK_VARIANT, args.walk_variant)
         if args.unmask_variant is not None:
             e.set_tuning(_abi.TUNE_UNMASK_VARIANT, args.unmask_variant)
+        if args.emit_variant is not None:
+            e.set_tuning(_abi.TUNE_EMIT_VARIANT, args.emit_variant)
     t_setup = time.time()
     scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
     emulated = None

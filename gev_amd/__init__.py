@@ -162,9 +162,17 @@ class Engine:
             raise ValueError(f"set_tuning({key}, {value}): {status_string(st)}")
 
     @staticmethod
-    def variant_name(i: int) -> Optional[str]:
-        n = lib.gevws_tuning_name(_abi.TUNE_UNMASK_VARIANT, i)
+    def variant_name(i: int, key: int = _abi.TUNE_UNMASK_VARIANT) -> Optional[str]:
+        n = lib.gevws_tuning_name(key, i)
         return n.decode() if n else None
+
+    @staticmethod
+    def variants(key: int = _abi.TUNE_UNMASK_VARIANT) -> List[int]:
+        """Every valid value of a variant knob (GEVWS_TUNE_UNMASK_VARIANT / _WALK_VARIANT)."""
+        out = []
+        while Engine.variant_name(len(out), key) is not None:
+            out.append(len(out))
+        return out
 
     # -------------------------------------------------------------- timing
     def set_timing(self, enable: bool):

@@ -45,6 +45,8 @@ TUNE_UNMASK_VARIANT = 1
 TUNE_UNMASK_GRID = 2
 TUNE_ENCODE_VARIANT = 3
 TUNE_WALK_VARIANT = 4
+TUNE_SPAN_CONNS_PER_CU = 5
+TUNE_EMIT_VARIANT = 6
 
 IN_PAD = 64
 SUMMARY_UNORDERED = 1  # summary.flags: connection table not in increasing input order

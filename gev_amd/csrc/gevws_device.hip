@@ -109,8 +109,11 @@ __device__ __forceinline__ int parse_header(uint64_t lo, uint64_t hi, uint64_t a
   return GEVWS_OK;
 }
 
+template <bool NT = false>
 __device__ __forceinline__ void load_window(const uint8_t* p, uint64_t& lo, uint64_t& hi) {
-  const u32x4 v = ld16u(p);
+  u32x4 v;
+  if constexpr (NT) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));  // unaligned nt load
+  else v = ld16u(p);
   lo = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
   hi = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
 }
@@ -159,6 +162,15 @@ __device__ __forceinline__ void block_excl_scan(const uint64_t (&v)[NV], uint64_
     tot[k] = all;
   }
   __syncthreads();
+}
+
+// threadIdx.x as a fresh value the compiler cannot hoist or keep live across
+// a loop: addresses derived from it are recomputed where they are used
+// instead of being held in (and spilled from) registers.
+__device__ __forceinline__ uint32_t fresh_tid() {
+  uint32_t t = threadIdx.x;
+  __asm__ volatile("" : "+v"(t));
+  return t;
 }
 
 // A value every lane of the wave loaded from the same address, kept in SGPRs
@@ -255,7 +267,16 @@ __device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t ava
 // the load depends on the path), which slows latency-bound walks of few
 // chains -- so the host enables GRP only for batches of many connections
 // (profiles/r01_ab_walk_grp_*.json).
-template <int D, bool GRP>
+// NTH (measurement): header windows loaded non-temporally -- does the L2
+// then request less than a 128-byte line per header (the walk's reads are
+// 17x the header bytes, profiles/r02_pmc_split_before.json)?
+// PF: with each header load, also touch the PF 128-byte lines after it, so a
+// following small frame's header is an L2 hit (~200 cycles) instead of an HBM
+// miss (~900).  The touches are issued before the header load, so waiting for
+// the header (vmcnt counts loads in issue order) never waits longer for them;
+// they cost bandwidth, which a chain-bound walk of few connections has spare
+// (round 1 measured the same touch 30 % slower on all of C4, which is not).
+template <int D, bool GRP, bool NTH = false, int PF = 0>
 __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
                                                             const gevws_conn_in* __restrict__ conns,
                                                             uint32_t n, gevws_conn_out* __restrict__ cout,
@@ -290,7 +311,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
     // table), so the compiler waits vmcnt(1), not vmcnt(0).
     WalkEntry* sink = entries + n_entries + c;
     uint64_t lo, hi;
-    load_window(s, lo, hi);
+    load_window<NTH>(s, lo, hi);
     *sink = WalkEntry{0, 0, 0, 0};
     uint64_t prev_fsz = 0;  // speculation (D > 0): size of the last frame and the run of equal sizes
     uint32_t run = 0;
@@ -322,7 +343,12 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       pb += round16(L);
       pl += L;
     };
+    uint32_t pfv[PF > 0 ? PF : 1] = {};
     for (;;) {
+      if constexpr (PF > 0) {  // keep the touches' results alive (free: they landed before the header)
+#pragma unroll
+        for (int j = 0; j < PF; ++j) __asm__ volatile("" ::"v"(pfv[j]));
+      }
       // The chain is latency-bound (one load per frame, few lanes per SIMD):
       // only the next frame's position is computed before its header load is
       // issued -- at min(next, len), always inside the stream + GEVWS_IN_PAD
@@ -337,7 +363,16 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       const uint64_t fsz = hlen + L;
       const uint64_t next = pos + fsz;
       const uint64_t lo0 = lo, hi0 = hi;
-      load_window(s + (next <= ci.len ? next : ci.len), lo, hi);  // (a wrapped next is <= len or clamped)
+      if constexpr (PF > 0) {
+        const uint64_t nx = next <= ci.len ? next : ci.len;
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+          const uint64_t q = nx + 128 * (j + 1);
+          pfv[j] = *reinterpret_cast<const uint32_t*>(s + (q <= ci.len ? q : ci.len));
+        }
+        __asm__ volatile("" ::: "memory");  // touches first, then the header load
+      }
+      load_window<NTH>(s + (next <= ci.len ? next : ci.len), lo, hi);  // (a wrapped next is <= len or clamped)
       const uint64_t avail = ci.len - pos;
       const bool have_hdr = avail >= 6 && avail >= hlen;   // read.go:20-23, U1
       const bool msb = e64 && (L64 >> 63);                  // read.go:71-73
@@ -369,7 +404,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
               const uint64_t q = pos + (uint64_t)j * fsz;
               const bool in = q <= ci.len;
               qn += in ? 1u : 0u;
-              load_window(s + (in ? q : ci.len), qlo[j], qhi[j]);
+              load_window<NTH>(s + (in ? q : ci.len), qlo[j], qhi[j]);
             }
             qlo[0] = lo;
             qhi[0] = hi;
@@ -395,7 +430,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
               }
             }
             if (fail) break;
-            load_window(s + pos, lo, hi);  // the next batch's first window, or the chain's next header
+            load_window<NTH>(s + pos, lo, hi);  // the next batch's first window, or the chain's next header
             if (stop || qn < (uint32_t)D || pos + fsz > ci.len) break;
           }
           if (fail) break;
@@ -431,6 +466,215 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
   for (int k = 0; k < kBlkFields; ++k) {
     const uint64_t s = wave_sum(vals[k]);
     if (threadIdx.x == 0) blk[(uint64_t)blockIdx.x * kBlkFields + k] = s;
+  }
+}
+
+// ------------------------------------------------------------------ 1b. walk (count), one wave per connection
+// k_walk_count gives each connection one lane, one dependent header load per
+// frame: right for batches of many connections (C4's 65 536: the memory
+// system is kept busy by the chains' sheer number), but a batch of few
+// connections -- a GPU's LPT share of a strong split, C5 -- is bound by its
+// longest chain (C4: 1 204 frames, ~0.54 us per step on a lightly loaded
+// chip, profiles/r01_c4_strong_projection.jsonl).  Here a whole wave walks one
+// connection and shortens the chain's critical path two ways:
+//
+//  * ring mode: the wave streams the stream through a per-wave LDS ring of
+//    two K KiB halves (coalesced 16-byte loads, one chunk per lane per KiB);
+//    frames whose header lies in the ring are parsed out of LDS (a few LDS
+//    reads per frame instead of an HBM round trip), the next contiguous half
+//    is in flight while the wave walks the current one, and a frame that
+//    jumps past the ring (a big payload) reloads the ring at its end;
+//  * ballot mode: after three frames of equal size F, lane j loads the
+//    16-byte window at pos + j F and parses it; a ballot of "a complete frame
+//    of size F" gives the run's length -- up to 64 frames per memory latency,
+//    exactly the frames the serial chain would have found (each candidate is
+//    checked, the first non-matching one ends the batch and the walk goes on
+//    from the true position).
+//
+// Entries (the same WalkEntry slot runs as k_walk_count, so k_walk_emit is
+// shared) are gathered one per lane and stored 64 at a time (1 KiB coalesced).
+// Results are identical to k_walk_count's by construction: the chain is the
+// same serial chain, only where its header bytes come from differs.
+constexpr int kSpanWaves = 4;  // connections (waves) per workgroup
+
+template <int K>
+__global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __restrict__ in,
+                                                             const gevws_conn_in* __restrict__ conns, uint32_t n,
+                                                             gevws_conn_out* __restrict__ cout,
+                                                             uint64_t* __restrict__ blk,
+                                                             WalkEntry* __restrict__ entries, uint64_t n_entries,
+                                                             uint32_t gshift, uint64_t in_bytes) {
+  constexpr uint64_t S = (uint64_t)K * 1024;  // bytes per ring half
+  constexpr uint32_t RW = (uint32_t)(2 * S / 8);  // ring words (u64) per wave
+  __shared__ uint64_t s_ring[kSpanWaves][RW];
+  __shared__ uint64_t s_part[kSpanWaves][kBlkFields];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t c = blockIdx.x * kSpanWaves + wave;
+  uint64_t nf = 0, pb = 0, pl = 0, err = 0;  // wave-uniform
+  if (c < n) {
+    gevws_conn_in ci = conns[c];
+    ci.off = uniform64(ci.off);
+    ci.len = uniform64(ci.len);
+    if (out_of_order(conns, c, ci)) err = 1ull << 32;  // as k_walk_count (k_scan_blocks SPLIT)
+    int32_t st = GEVWS_OK;
+    if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
+      ci.off = 0;
+      ci.len = 0;
+      st = GEVWS_ERR_INVALID;
+      err += 1;
+    }
+    uint64_t ebase = 0, ecap = 0;
+    bool rec = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
+    uint64_t* ring = s_ring[wave];
+    const uint64_t sbeg = reinterpret_cast<uint64_t>(in) + ci.off;  // stream bytes [sbeg, send)
+    const uint64_t send = sbeg + ci.len;
+    // one K KiB half: chunk k * 64 + lane, loaded only where it holds stream bytes
+    auto issue = [&](uint64_t b, u32x4 (&v)[K]) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint64_t a = b + (uint64_t)(k * 64 + lane) * 16;
+        v[k] = a < send ? *reinterpret_cast<const u32x4*>(a) : u32x4{0, 0, 0, 0};
+      }
+    };
+    auto put = [&](uint64_t b, const u32x4 (&v)[K]) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint32_t w = (uint32_t)(((b >> 3) + 2ull * (k * 64 + lane)) % RW);  // even: b is 16-aligned
+        ring[w] = (uint64_t)v[k][0] | ((uint64_t)v[k][1] << 32);
+        ring[w + 1] = (uint64_t)v[k][2] | ((uint64_t)v[k][3] << 32);
+      }
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave reads other lanes' words next
+    };
+    // entries: entry i sits in lane i % 64 until its group of 64 is stored
+    WalkEntry my = {0, 0, 0, 0};
+    uint64_t flushed = 0;  // entries [0, flushed) are stored
+    auto flush = [&]() {
+      if (rec && nf > flushed) {
+        const uint64_t g = (nf - 1) & ~63ull;  // the group of the unstored entries
+        const uint64_t i = g + lane;
+        if (i >= flushed && i < nf) entries[ebase + i] = my;
+      }
+      flushed = nf;
+    };
+    auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
+      rec = rec && nf < ecap;
+      if (lane == (uint32_t)(nf & 63)) my = WalkEntry{(uint32_t)p, key, (uint32_t)L, meta};
+      ++nf;
+      pb += round16(L);
+      pl += L;
+      if ((nf & 63) == 0) flush();
+    };
+    uint64_t pos = 0, prev_fsz = 0;
+    uint32_t run = 0;
+    // ring state: [rb, rb + S) is written; [rb + S, rb + 2S) is in `nv` (in flight) until hi_ready
+    uint64_t rb = sbeg & ~15ull;
+    bool hi_ready = false;
+    u32x4 nv[K];
+    {
+      u32x4 v0[K];
+      issue(rb, v0);
+      issue(rb + S, nv);
+      put(rb, v0);
+    }
+    for (;;) {
+      const uint64_t x = sbeg + pos;
+      const uint64_t avail = ci.len - pos;
+      if (avail < 6) break;  // read.go:20-23
+      if (run >= 3) {
+        // ---- ballot mode: lane j checks the frame at pos + j F
+        const uint64_t F = prev_fsz;
+        const uint64_t q = pos + (uint64_t)lane * F;
+        const bool inside = q < ci.len;
+        uint64_t lo, hi;
+        load_window(reinterpret_cast<const uint8_t*>(sbeg + (inside ? q : ci.len)), lo, hi);
+        uint32_t m2 = 0, h2 = 0, k2 = 0;
+        uint64_t L2 = 0;
+        const int r = walk_parse(lo, hi, inside ? ci.len - q : 0, m2, h2, L2, k2);
+        const bool ok = inside && r == GEVWS_OK && h2 + L2 == F;
+        const uint64_t okm = __ballot(ok);
+        const uint32_t k = okm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);  // leading run of matches
+        if (k > 0) {
+          flush();  // the buffered group goes out before the direct stores
+          rec = rec && nf + k <= ecap;
+          if (rec && lane < k) entries[ebase + nf + lane] = WalkEntry{(uint32_t)q, k2, (uint32_t)L2, m2};
+          const uint64_t add_pb = wave_sum(lane < k ? round16(L2) : 0);
+          const uint64_t add_pl = wave_sum(lane < k ? L2 : 0);
+          nf += k;
+          pb += add_pb;
+          pl += add_pl;
+          flushed = nf;
+          pos += (uint64_t)k * F;
+        }
+        if (k < 64) run = 0;  // the frame at pos differs (or the stream ends there): ring mode
+        continue;
+      }
+      // ---- ring mode: bring the header window [x, x + 16) into the ring
+      if (x >= rb + S) {
+        if (x < rb + 2 * S) {  // into the upper half: slide by one half, prefetch the next
+          if (!hi_ready) put(rb + S, nv);
+          rb += S;
+          issue(rb + S, nv);
+        } else {  // past the ring: reload it at the header
+          rb = x & ~15ull;
+          u32x4 v0[K];
+          issue(rb, v0);
+          issue(rb + S, nv);
+          put(rb, v0);
+        }
+        hi_ready = false;
+      }
+      if (x + 16 > rb + S && !hi_ready) {  // the window reaches into the upper half
+        put(rb + S, nv);
+        hi_ready = true;
+      }
+      // the chain is serial and wave-uniform: read the words once into SGPRs
+      // so the parse runs on the scalar unit (as VALU work it is repeated by
+      // all 64 lanes and, with 32 waves per CU, bound by VALU issue)
+      const uint64_t qw = x >> 3;
+      const uint32_t sh = (uint32_t)(x & 7) * 8;
+      const uint64_t w0 = uniform64(ring[qw % RW]), w1 = uniform64(ring[(qw + 1) % RW]),
+                     w2 = uniform64(ring[(qw + 2) % RW]);
+      const uint64_t lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+      const uint64_t hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+      uint32_t meta, hlen, key;
+      uint64_t L;
+      const int r = walk_parse(lo, hi, avail, meta, hlen, L, key);
+      if (r != GEVWS_OK) {
+        if (r == GEVWS_ERR_LEN_MSB) {
+          st = GEVWS_ERR_LEN_MSB;
+          err += 1;
+        }
+        break;
+      }
+      put_entry(pos, key, L, meta);
+      const uint64_t fsz = hlen + L;
+      run = fsz == prev_fsz ? run + 1 : 1;
+      prev_fsz = fsz;
+      pos += fsz;
+    }
+    flush();
+    if (lane == 0) {
+      gevws_conn_out o;
+      o.first_frame = rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
+      o.consumed = pos;
+      o.payload_base = pb;
+      o.nframes = (uint32_t)nf;
+      o.status = st;
+      cout[c] = o;
+    }
+  }
+  if (lane == 0) {
+    s_part[wave][0] = nf;
+    s_part[wave][1] = pb;
+    s_part[wave][2] = pl;
+    s_part[wave][3] = err;
+  }
+  __syncthreads();
+  if (threadIdx.x < kBlkFields) {
+    uint64_t sm = 0;
+#pragma unroll
+    for (int w = 0; w < kSpanWaves; ++w) sm += s_part[w][threadIdx.x];
+    blk[(uint64_t)blockIdx.x * kBlkFields + threadIdx.x] = sm;
   }
 }
 
@@ -535,7 +779,19 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
 // connection's last frame are skipped (wave-uniform), their loads re-read the
 // last entry (one cached line).  Connections of <= 64 frames take one plain
 // round.
-template <int U>
+//
+// G > 0 (grouped): a wave takes G consecutive connections at a time, their
+// metadata in one coalesced load (lane j = connection j).  When their
+// recorded frames number at most 64 R, the group's frames are enumerated
+// across connection boundaries -- lane l of round r takes the group's frame
+// r*64 + l, finds its connection by a binary search over the lanes' frame
+// prefix sums (__shfl), and the payload offsets come from a segmented wave
+// scan plus a per-connection carry kept in lane j -- so connections of a few
+// frames (C1: 16 frames of 136 B) fill whole waves instead of 16 lanes of
+// one, and all R rounds' entries are requested at once.  Longer groups take
+// the per-connection rounds above, connection by connection.
+constexpr int kEmitGroup = 16;
+template <int U, int G = 0>
 __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restrict__ in,
                                                           const gevws_conn_in* __restrict__ conns, uint32_t n,
                                                           const gevws_conn_out* __restrict__ cout,
@@ -548,31 +804,25 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
   const bool unordered = (sum->flags & GEVWS_SUMMARY_UNORDERED) != 0;  // entry runs may collide: unused
   const int lane = threadIdx.x & 63;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kWalkBlock / 64);
-  for (uint64_t c = (uint64_t)blockIdx.x * (kWalkBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
-    // everything the connection needs is requested at once (one latency)
-    const gevws_conn_out o = cout[c];
-    const uint8_t recorded = rec_flags[c];
-    const gevws_conn_in ci = conns[c];
-    const uint64_t cnt = uniform64(o.nframes);  // one connection per wave
-    if (cnt == 0 || !recorded || unordered) continue;  // no frames / re-walked below
-    uint64_t ebase = 0, ecap = 0;
-    entry_slots_of(ci, (uint32_t)c, n_entries, gshift, ebase, ecap);
+  auto record = [&](const WalkEntry& q, uint64_t f, uint64_t poff, uint64_t coff) {
+    DevHdr h;
+    h.b0 = q.meta & 0xff;
+    h.masked = (q.meta >> 8) & 1;
+    h.hlen = q.meta >> 16;
+    h.mask = q.mask;
+    h.length = q.len;
+    emit_record(frames, tile_first, f, poff, coff + q.pos + h.hlen, h);
+  };
+  // the per-connection rounds (64 entries per round, U rounds per load)
+  auto one_conn = [&](uint64_t cnt, uint64_t first_frame, uint64_t payload_base, uint64_t coff, uint64_t ebase) {
     const WalkEntry* ce = entries + ebase;
-    uint64_t carry = o.payload_base;
+    uint64_t carry = payload_base;
     auto round = [&](const WalkEntry& q, uint64_t r0) {
       const uint64_t k = r0 + lane;
       const bool valid = k < cnt;
       const uint64_t padded = valid ? round16(q.len) : 0;
       const uint64_t incl = wave_incl_scan(padded);
-      if (valid) {
-        DevHdr h;
-        h.b0 = q.meta & 0xff;
-        h.masked = (q.meta >> 8) & 1;
-        h.hlen = q.meta >> 16;
-        h.mask = q.mask;
-        h.length = q.len;
-        emit_record(frames, tile_first, o.first_frame + k, carry + incl - padded, ci.off + q.pos + h.hlen, h);
-      }
+      if (valid) record(q, first_frame + k, carry + incl - padded, coff);
       carry += __shfl(incl, 63, 64);
     };
     if (U == 1 || cnt <= 64) {  // wave-uniform
@@ -598,6 +848,124 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
         }
       }
     }
+  };
+  if constexpr (G > 0) {
+    // phase 1: groups of G connections, their short connections (<= kShort
+    // frames, so a group has at most 64 R) enumerated across boundaries
+    constexpr int R = 4;
+    constexpr uint64_t kShort = 64ull * R / G;
+    const uint64_t ngroups = ((uint64_t)n + G - 1) / G;
+    for (uint64_t g = (uint64_t)blockIdx.x * (kWalkBlock / 64) + (threadIdx.x >> 6); g < ngroups; g += nwaves) {
+      const uint64_t c = g * G + lane;
+      uint64_t nf = 0, ff = 0, pbase = 0, coff = 0, ebase = 0;
+      if (lane < G && c < n) {
+        const gevws_conn_out o = cout[c];
+        const gevws_conn_in ci = conns[c];
+        uint64_t ecap = 0;
+        const bool rec = rec_flags[c] && !unordered && entry_slots_of(ci, (uint32_t)c, n_entries, gshift, ebase, ecap);
+        nf = (rec && o.nframes <= kShort) ? o.nframes : 0;  // long: phase 2; unrecorded: re-walked below
+        ff = o.first_frame;
+        pbase = o.payload_base;
+        coff = ci.off;
+      }
+      const uint64_t inc = wave_incl_scan(nf);
+      const uint64_t T = uniform64(__shfl(inc, 63, 64));  // <= 64 R
+      if (T == 0) continue;
+      const uint64_t tstart = inc - nf;  // lane j: group index of its connection's first frame
+      WalkEntry q[R];
+      uint32_t jr[R];
+      uint64_t kr[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint64_t t = (uint64_t)r * 64 + lane;
+        static_assert((G & (G - 1)) == 0, "G: a power of two");
+        uint32_t lo = 0, hi = G - 1;  // smallest j with inc_j > t
+#pragma unroll
+        for (int it = 0; (1 << it) < G; ++it) {  // fixed trip count: the __shfl sees every lane
+          const uint32_t mid = (lo + hi) >> 1;
+          if (__shfl(inc, (int)mid, 64) > t) hi = mid; else lo = mid + 1;
+        }
+        jr[r] = lo;
+        kr[r] = t - __shfl(tstart, (int)lo, 64);
+        const uint64_t eb = __shfl(ebase, (int)lo, 64);  // (outside the t < T branch: see below)
+        q[r] = WalkEntry{0, 0, 0, 0};
+        if (t < T) q[r] = entries[eb + kr[r]];
+      }
+      uint64_t carry = 0;  // lane j: its connection's padded bytes already placed
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if ((uint64_t)r * 64 >= T) break;  // wave-uniform
+        const uint64_t t = (uint64_t)r * 64 + lane;
+        const bool valid = t < T;
+        const uint32_t j = jr[r];
+        const uint64_t padded = valid ? round16(q[r].len) : 0;
+        // segmented inclusive scan: a segment starts at a connection's first
+        // frame and at lane 0
+        uint64_t v = padded;
+        bool head = kr[r] == 0 || lane == 0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint64_t vu = __shfl_up(v, d, 64);
+          const bool hu = __shfl_up((int)head, d, 64) != 0;
+          if (lane >= d && !head) {
+            v += vu;
+            head = hu;
+          }
+        }
+        // every __shfl runs with the whole wave active: a ds_bpermute reads
+        // nothing from a lane masked off by a branch (here: lane j of a
+        // connection whose frames are all taken, in a round's short tail)
+        const uint64_t cj = __shfl(carry, (int)j, 64);
+        const uint64_t fj = __shfl(ff, (int)j, 64), pj = __shfl(pbase, (int)j, 64), oj = __shfl(coff, (int)j, 64);
+        if (valid) record(q[r], fj + kr[r], pj + cj + v - padded, oj);
+        // lane j adds its connection's bytes in this round (from the lane of its last frame here)
+        const uint64_t r0 = (uint64_t)r * 64, r1 = r0 + 64;
+        const uint64_t a = tstart > r0 ? tstart : r0, b = inc < r1 ? inc : r1;
+        const uint64_t got = __shfl(v, (int)((b > a ? b - 1 : r0) - r0), 64);
+        if (lane < G && b > a) carry += got;
+      }
+    }
+    // phase 2: connections of more than kShort frames, one wave per
+    // connection, GL consecutive connections per wave (their metadata in one
+    // load) when the batch has more connections than the grid has waves
+    // (half the grid's waves busy: C4's 65 536 connections 0.43 ms in groups of
+    // 16 vs 0.53 ms in groups of 8 over every wave -- fewer record streams
+    // interleave in DRAM; profiles/r02_emit_ab.jsonl)
+    const uint64_t per = (2 * (uint64_t)n + nwaves - 1) / nwaves;
+    const uint64_t GL = per < 1 ? 1 : (per > 16 ? 16 : per);
+    const uint64_t nl = ((uint64_t)n + GL - 1) / GL;
+    for (uint64_t g = (uint64_t)blockIdx.x * (kWalkBlock / 64) + (threadIdx.x >> 6); g < nl; g += nwaves) {
+      const uint64_t c = g * GL + lane;
+      uint64_t nf = 0, ff = 0, pbase = 0, coff = 0, ebase = 0;
+      if (lane < GL && c < n) {
+        const gevws_conn_out o = cout[c];
+        const gevws_conn_in ci = conns[c];
+        uint64_t ecap = 0;
+        const bool rec = rec_flags[c] && !unordered && entry_slots_of(ci, (uint32_t)c, n_entries, gshift, ebase, ecap);
+        nf = (rec && o.nframes > kShort) ? o.nframes : 0;
+        ff = o.first_frame;
+        pbase = o.payload_base;
+        coff = ci.off;
+      }
+      for (uint64_t j = 0; j < GL; ++j) {  // wave-uniform
+        const uint64_t cnt = uniform64(__shfl(nf, (int)j, 64));
+        const uint64_t fj = uniform64(__shfl(ff, (int)j, 64)), pj = uniform64(__shfl(pbase, (int)j, 64));
+        const uint64_t oj = uniform64(__shfl(coff, (int)j, 64)), ej = uniform64(__shfl(ebase, (int)j, 64));
+        if (cnt) one_conn(cnt, fj, pj, oj, ej);
+      }
+    }
+  } else {
+  for (uint64_t c = (uint64_t)blockIdx.x * (kWalkBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
+    // everything the connection needs is requested at once (one latency)
+    const gevws_conn_out o = cout[c];
+    const uint8_t recorded = rec_flags[c];
+    const gevws_conn_in ci = conns[c];
+    const uint64_t cnt = uniform64(o.nframes);  // one connection per wave
+    if (cnt == 0 || !recorded || unordered) continue;  // no frames / re-walked below
+    uint64_t ebase = 0, ecap = 0;
+    entry_slots_of(ci, (uint32_t)c, n_entries, gshift, ebase, ecap);
+    one_conn(cnt, o.first_frame, o.payload_base, ci.off, ebase);
+  }
   }
   // connections without recorded entries: one lane per connection re-walks
   const uint64_t nthreads = (uint64_t)gridDim.x * kWalkBlock;
@@ -825,6 +1193,67 @@ __device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint
   }
 }
 
+// A run of streaming steps inside one frame, software-pipelined: the loads of
+// step i+1 (U2 tiles, wave-contiguous U2 KiB per wave, aligned + register
+// realign as stream_step AL = 2) are issued before step i is realigned, XORed
+// and stored, so a wave always has a step's loads in flight -- with one
+// workgroup per CU for big frames a CU runs only 4 waves, and stream_step's
+// load-all / store-all leaves each wave's read queue empty while it stores.
+// Returns the tile after the run (it takes every whole step that fits in
+// [t, tend) and inside the frame's padded end f_end).
+template <int U2, bool NTS>
+__device__ __forceinline__ uint64_t stream_run(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t t,
+                                               uint64_t tend, uint64_t f_po, uint64_t f_src, int64_t f_len,
+                                               uint32_t f_key, uint64_t f_end) {
+  const uint64_t n1 = (tend - t) / U2, n2 = (f_end - t * kTile) / ((uint64_t)U2 * kTile);
+  const uint64_t n = n1 < n2 ? n1 : n2;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t wrel = (uint64_t)wave * U2 * 1024 + lane * 16;
+  const uint8_t* src0 = in + f_src + (t * kTile - f_po);  // the run's first source byte (wave-uniform)
+  const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(src0) & 15);
+  const uint8_t* a0 = src0 - mis + wrel;
+  uint8_t* d0 = out + t * kTile + wrel;
+  const int64_t rem0 = f_len - (int64_t)(t * kTile - f_po + wrel);  // payload bytes from this lane's chunk, step 0
+  const bool last = lane == 63;
+  constexpr uint64_t kStep = (uint64_t)U2 * kTile;
+  auto load = [&](u32x4 (&v)[U2], u32x4& e, uint64_t i) {
+    const uint8_t* a = a0 + i * kStep;
+#pragma unroll
+    for (int u = 0; u < U2; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * 1024);
+    e = u32x4{0, 0, 0, 0};
+    if (last && mis) e = *reinterpret_cast<const u32x4*>(a + (U2 - 1) * 1024 + 16);
+  };
+  auto emit = [&](const u32x4 (&v)[U2], const u32x4& e, uint64_t i) {
+    uint8_t* d = d0 + i * kStep;
+    const int64_t rem = rem0 - (int64_t)(i * kStep);
+    u32x4 r = rot_next_lane(v[0]);
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      u32x4 x = v[u];
+      if (mis) {
+        const u32x4 rn = u + 1 < U2 ? rot_next_lane(v[u + 1 < U2 ? u + 1 : u]) : e;
+        x = funnel16(v[u], last ? rn : r, mis);
+        r = rn;
+      }
+      x ^= f_key;
+      const int64_t rr = rem - (int64_t)u * 1024;
+      if (rr < 16) x = keep_bytes(x, rr);
+      st16_stream<NTS>(d + u * 1024, x);
+    }
+  };
+  u32x4 va[U2], vb[U2], ea, eb;
+  load(va, ea, 0);
+  uint64_t i = 0;
+  for (; i + 2 <= n; i += 2) {  // unrolled by two: va / vb alternate, no register copies
+    load(vb, eb, i + 1);
+    emit(va, ea, i);
+    if (i + 2 < n) load(va, ea, i + 2);
+    emit(vb, eb, i + 1);
+  }
+  if (i < n) emit(va, ea, i);
+  return t + n * U2;
+}
+
 template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles>
 __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __restrict__ in,
                                                             const gevws_frame* __restrict__ frames,
@@ -963,7 +1392,19 @@ __device__ __forceinline__ WinRec load_rec(const gevws_frame* __restrict__ frame
 // amdgpu_waves_per_eu(4): four workgroups per CU (128 VGPRs; a few loop-
 // invariant lane values spill to scratch).  Three per CU (140 VGPRs, no
 // spills) measured 25-40 % slower on C2/C4/C5.
-template <int U, int WT, bool NTS>
+// WC (wave-contiguous window mapping): in the window path wave w takes the
+// contiguous WT KiB [w*WT KiB, (w+1)*WT KiB) of the window, 1 KiB per step,
+// instead of 1 KiB of every tile.  The chunk loads are unaligned (the source
+// shifts by the header lengths), so each wave instruction touches 9 lines for
+// 8 lines of data; with tile-strided spans the 9th line is the first line of
+// ANOTHER wave's span, which runs skewed and finds it evicted -- the C4 window
+// path read 10 % more than its bytes (profiles/r02_pmc_split_before.json:
+// 22.87 GB of 128-byte requests for 20.84 GB).  Wave-contiguous, the shared
+// line belongs to the same wave's next instruction, issued right behind it.
+// FT (measurement switch): false re-creates the round-1 kernel whose fill
+// addresses were spilled (threadIdx.x used directly).
+// SP: streaming steps as software-pipelined runs (stream_run, U / 2 tiles per step).
+template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_v4(const uint8_t* __restrict__ in,
                                                             const gevws_frame* __restrict__ frames,
                                                             const uint32_t* __restrict__ tile_first,
@@ -1016,8 +1457,11 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   while (t < tend) {
     const uint64_t base = t * kTile;
     if (t + U <= tend && base >= f_po && base + U * kTile <= f_end) {  // still inside the cached frame
-      stream_step<U, false, NTS, 2>(in, out, base, f_po, f_src, f_len, f_key);
-      t += U;
+      if constexpr (SP) t = stream_run<U / 2, NTS>(in, out, t, tend, f_po, f_src, f_len, f_key, f_end);
+      else {
+        stream_step<U, false, NTS, 2>(in, out, base, f_po, f_src, f_len, f_key);
+        t += U;
+      }
       pf_t = ~0ull;  // (never t here; redefining r0 keeps it dead across the step)
       r0 = WinRec{};
       continue;
@@ -1033,8 +1477,11 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
       decide(t, a, b, stream);
     }
     if (stream) {  // decide() cached frame a, which covers [t, t+U)
-      stream_step<U, false, NTS, 2>(in, out, base, f_po, f_src, f_len, f_key);
-      t += U;
+      if constexpr (SP) t = stream_run<U / 2, NTS>(in, out, t, tend, f_po, f_src, f_len, f_key, f_end);
+      else {
+        stream_step<U, false, NTS, 2>(in, out, base, f_po, f_src, f_len, f_key);
+        t += U;
+      }
       pf_t = ~0ull;
       r0 = WinRec{};
       continue;
@@ -1069,20 +1516,27 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
       s_delta[i] = so - po;
       s_key[i] = ((q.lo[0] >> 24) & 0xff) ? (uint32_t)(q.lo[0] >> 32) : 0u;
     };
-    if (threadIdx.x < F) fill(threadIdx.x, have ? r0 : load_rec(frames, a + threadIdx.x));
-    for (uint64_t i = threadIdx.x + kUnmaskBlock; i < F; i += kUnmaskBlock) fill(i, load_rec(frames, a + i));
+    // threadIdx.x re-read here (fresh_tid): otherwise the compiler keeps the
+    // fill's per-lane LDS / record addresses live across the whole loop and
+    // spills them; their reloads are scratch loads that queue behind the
+    // window's global loads (vmcnt is in order) and miss in L2 under the
+    // stream (C4: 2 GB of the 22.9 GB read per launch)
+    const uint32_t tid = FT ? fresh_tid() : threadIdx.x;
+    if (tid < F) fill(tid, have ? r0 : load_rec(frames, a + tid));
+    for (uint64_t i = tid + kUnmaskBlock; i < F; i += kUnmaskBlock) fill(i, load_rec(frames, a + i));
     __syncthreads();
     u32x4 v[WT];
     uint32_t key[WT];
     int32_t rem[WT];
 #pragma unroll
     for (int u = 0; u < WT; ++u) {
-      const uint32_t rel = (uint32_t)(u * kTile) + lane_off;
+      const uint32_t rel = WC ? (threadIdx.x >> 6) * (uint32_t)(WT * 1024) + (uint32_t)u * 1024 + (threadIdx.x & 63) * 16
+                              : (uint32_t)(u * kTile) + lane_off;
       const uint64_t p = wbase + rel;
       rem[u] = 0;
       key[u] = 0;
       v[u] = u32x4{0, 0, 0, 0};
-      if ((uint64_t)u < wt && p < total) {
+      if ((WC ? (uint64_t)rel < wt * kTile : (uint64_t)u < wt) && p < total) {
         uint32_t lo = 0, hi = (uint32_t)F - 1;
         while (lo < hi) {
           const uint32_t mid = (lo + hi + 1) >> 1;
@@ -1102,7 +1556,8 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
       pf_t = wend_t;
       if (!pf_stream) {
         const uint64_t nF = pf_b - pf_a + 1;
-        if (threadIdx.x < nF) r0 = load_rec(frames, pf_a + threadIdx.x);
+        const uint32_t tid = FT ? fresh_tid() : threadIdx.x;  // (a spilled frames + tid * 32 would wait vmcnt(0) on its reload)
+        if (tid < nF) r0 = load_rec(frames, pf_a + tid);
       }
     }
 #pragma unroll
@@ -1110,7 +1565,9 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
       if (rem[u] > 0) {
         u32x4 x = v[u] ^ key[u];
         if (rem[u] < 16) x = keep_bytes(x, rem[u]);
-        st16_stream<NTS>(out + wbase + (uint32_t)(u * kTile) + lane_off, x);
+        const uint32_t rel = WC ? (threadIdx.x >> 6) * (uint32_t)(WT * 1024) + (uint32_t)u * 1024 + (threadIdx.x & 63) * 16
+                                : (uint32_t)(u * kTile) + lane_off;
+        st16_stream<NTS>(out + wbase + rel, x);
       }
     }
     t = wend_t;
@@ -1394,9 +1851,9 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
   const uint64_t per = (ntiles + groups - 1) / groups;
   uint64_t t = (uint64_t)blockIdx.x * per;
   const uint64_t tend = t + per < ntiles ? t + per : ntiles;
-  const uint32_t lane_off = threadIdx.x * 16;
   uint64_t c_ps = 0, c_pe = 0, c_delta = 0;  // cached frame: payload [c_ps, c_pe) in wire coordinates
   while (t < tend) {
+    const uint32_t lane_off = fresh_tid() * 16;  // recomputed per step: held, it was spilled
     const uint64_t base = t * kTile;
     if (base >= c_pe) {  // workgroup-uniform refresh (scalar loads)
       const uint64_t f = tile_first[t];
@@ -1445,7 +1902,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
     const uint64_t F = f_hi - f_lo + 1;
     if (F <= (uint64_t)kEncWinFrames) {
       __syncthreads();
-      for (uint64_t i = threadIdx.x; i < F; i += kUnmaskBlock) {
+      for (uint64_t i = fresh_tid(); i < F; i += kUnmaskBlock) {  // (fresh_tid: see k_unmask_v4's fill)
         const gevws_out_frame o = fr[f_lo + i];
         uint64_t lo, hi;
         const uint32_t hl = enc_header(o.hdr, lo, hi);
@@ -1486,7 +1943,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
       if constexpr (COMPACT) {
         __syncthreads();
         const uint32_t nb = s_nb;
-        for (uint32_t i = threadIdx.x; i < nb; i += kUnmaskBlock) {
+        for (uint32_t i = fresh_tid(); i < nb; i += kUnmaskBlock) {
           const uint32_t q = s_bnd[i];
           const int32_t rel = (int32_t)((q & 0xffffu) << 4);
           const uint64_t a = wbase + (uint64_t)rel;
@@ -1859,6 +2316,8 @@ struct gevws_ctx {
                            // the records (LDS-light: 7 workgroups per CU), 1 = unaligned loads,
                            // 2 = aligned loads, per-lane boundary assembly, 3 = as 0 with the headers
                            // kept in LDS (4 workgroups per CU)
+  int emit_variant = 0;    // 0 = grouped record pass (k_walk_emit G = 16), 1 = one wave per connection
+  uint32_t span_conns_per_cu = 0;  // walk variant 0: one wave per connection up to this many per CU
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
                            // 2 = plain walk without the entry table (emit re-walks); 0 and 1 store
                            // entries in 64-byte groups for batches of many connections; 3 / 4 =
@@ -1946,8 +2405,34 @@ const UnmaskVariant kUnmaskVariants[] = {
      "v3 U16 + 4-tile LDS window; streaming path: aligned loads, wave-contiguous 16 KiB spans, DPP rotate"},
     {k_unmask_v3<16, false, true, 2, 8>, 16, "v3 with an 8-tile window (no pipelining)"},
     {k_unmask_v3<16, false, true>, 16, "v3 U16 + 4-tile LDS window, unaligned streaming loads"},
+    {k_unmask_v4<16, 8, true, true>, 16,
+     "v4 with a wave-contiguous window mapping (each wave 8 contiguous KiB of the 32 KiB window)"},
+    {k_unmask_v4<16, 4, true, true>, 16, "v4 with a 4-tile wave-contiguous window"},
+    {k_unmask_v4<16, 8, true, false, false>, 16, "v4 as in round 1 (fill addresses spilled to scratch)"},
+    {k_unmask_v4<16, 4, true>, 16, "v4 with a 4-tile pipelined window"},
+    {k_unmask_v4<16, 8, true, false, true, true>, 16,
+     "v4 with software-pipelined streaming runs (8-tile steps, next step's loads before this step's stores)"},
+    {k_unmask_v4<8, 8, true, false, true, true>, 8,
+     "v4, pipelined streaming runs of 4-tile steps (streams from 8 tiles inside a frame)"},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
+
+// GEVWS_TUNE_WALK_VARIANT values (0 = the default choice per batch).
+const char* const kWalkVariants[] = {
+    "default: one wave per connection (k_walk_span, K = 1) up to GEVWS_TUNE_SPAN_CONNS_PER_CU connections per CU, "
+    "else one lane per connection with uniform-stream speculation (k_walk_count D = 8; 64-byte entry groups from "
+    "128 connections per CU)",
+    "one lane per connection, plain chain walk (D = 0)",
+    "one lane per connection, no entry table (the record pass re-walks every chain)",
+    "one lane per connection, speculation, single entry stores",
+    "one lane per connection, speculation, grouped entry stores",
+    "one lane per connection, speculation, non-temporal header loads",
+    "one wave per connection: LDS ring of 2 x 1 KiB + ballot over equal-size runs",
+    "one wave per connection: LDS ring of 2 x 2 KiB + ballot over equal-size runs",
+    "one lane per connection, plain chain walk, each header load also touches the next 128-byte line",
+    "one lane per connection, plain chain walk, each header load also touches the next two 128-byte lines",
+};
+constexpr int kNumWalkVariants = sizeof(kWalkVariants) / sizeof(kWalkVariants[0]);
 
 }  // namespace
 
@@ -2039,8 +2524,16 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       if (value < 0 || value > 3) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
+    case GEVWS_TUNE_EMIT_VARIANT:
+      if (value < 0 || value > 1) return GEVWS_ERR_INVALID;
+      ctx->emit_variant = (int)value;
+      return GEVWS_OK;
+    case GEVWS_TUNE_SPAN_CONNS_PER_CU:
+      if (value < 0 || value > (1 << 20)) return GEVWS_ERR_INVALID;
+      ctx->span_conns_per_cu = (uint32_t)value;
+      return GEVWS_OK;
     case GEVWS_TUNE_WALK_VARIANT:
-      if (value < 0 || value > 4) return GEVWS_ERR_INVALID;
+      if (value < 0 || value >= kNumWalkVariants) return GEVWS_ERR_INVALID;
       ctx->walk_variant = (int)value;
       return GEVWS_OK;
     default:
@@ -2051,6 +2544,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
 const char* gevws_tuning_name(int key, int64_t value) {
   if (key == GEVWS_TUNE_UNMASK_VARIANT && value >= 0 && value < kNumUnmaskVariants)
     return kUnmaskVariants[value].name;
+  if (key == GEVWS_TUNE_WALK_VARIANT && value >= 0 && value < kNumWalkVariants) return kWalkVariants[value];
   return nullptr;
 }
 
@@ -2090,8 +2584,16 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   hipStream_t st = pick_stream(ctx, stream);
   // connections per counting workgroup: 64, or fewer so a small batch covers every CU
   const uint32_t ncu = (uint32_t)ctx->num_cus;
-  const uint32_t cpb = n_conns >= (uint32_t)kCountBlock * ncu ? (uint32_t)kCountBlock
-                                                              : (n_conns + ncu - 1) / ncu > 0 ? (n_conns + ncu - 1) / ncu : 1;
+  // header walk: one wave per connection (k_walk_span) when the batch has few
+  // connections for the chip -- its chains, not the memory system, bound the
+  // walk -- else one lane per connection (k_walk_count)
+  const int wv = ctx->walk_variant;
+  const bool span = wv == 6 || wv == 7 ||
+                    (wv == 0 && (uint64_t)n_conns <= (uint64_t)ctx->span_conns_per_cu * ncu);
+  const uint32_t cpb = span ? (uint32_t)kSpanWaves
+                            : n_conns >= (uint32_t)kCountBlock * ncu
+                                  ? (uint32_t)kCountBlock
+                                  : (n_conns + ncu - 1) / ncu > 0 ? (n_conns + ncu - 1) / ncu : 1;
   const uint32_t nblk = (n_conns + cpb - 1) / cpb;
   const uint64_t ntiles_cap = (payload_cap + kTile - 1) / kTile + 1;
   const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
@@ -2124,13 +2626,39 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   // walk variant 2 (measurement): no entry table -- the counting walk stores
   // nothing per frame and the emit pass re-walks every chain
   const uint64_t ne = ctx->walk_variant == 2 ? 0 : n_entries;
-  if (nblk) {
+  if (nblk && span) {
+    if (wv == 7)
+      k_walk_span<2><<<nblk, kSpanWaves * 64, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
+                                                       in_bytes);
+    else
+      k_walk_span<1><<<nblk, kSpanWaves * 64, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
+                                                       in_bytes);
+  } else if (nblk) {
     // grouped entry stores pay off when the walk is bound by its line traffic
     // (many concurrent chains), not by chain latency (few)
-    const int wv = ctx->walk_variant;
     const bool many = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
-    const bool grp = wv == 4 || ((wv == 0 || wv == 1) && many);
-    if (wv == 1) {
+    const bool grp = wv == 4 || ((wv == 0 || wv == 1 || wv == 5 || wv == 8 || wv == 9) && many);
+    if (wv == 8 || wv == 9) {
+      if (grp && wv == 8)
+        k_walk_count<0, true, false, 1><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
+                                                                     entries, ne, gshift, cpb, in_bytes);
+      else if (wv == 8)
+        k_walk_count<0, false, false, 1><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
+                                                                      entries, ne, gshift, cpb, in_bytes);
+      else if (grp)
+        k_walk_count<0, true, false, 2><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
+                                                                     entries, ne, gshift, cpb, in_bytes);
+      else
+        k_walk_count<0, false, false, 2><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
+                                                                      entries, ne, gshift, cpb, in_bytes);
+    } else if (wv == 5) {
+      if (grp)
+        k_walk_count<8, true, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries,
+                                                                  ne, gshift, cpb, in_bytes);
+      else
+        k_walk_count<8, false, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries,
+                                                                   ne, gshift, cpb, in_bytes);
+    } else if (wv == 1) {
       if (grp)
         k_walk_count<0, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
                                                             gshift, cpb, in_bytes);
@@ -2152,8 +2680,13 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb);
     uint64_t egrid = ((uint64_t)n_conns + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
     if (egrid > 8 * (uint64_t)ctx->num_cus) egrid = 8 * (uint64_t)ctx->num_cus;
-    k_walk_emit<4><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, d_summary, d_frames,
-                                                            tile_first, entries, ne, gshift, rec_flags);
+    if (ctx->emit_variant == 1)
+      k_walk_emit<4><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, d_summary,
+                                                              d_frames, tile_first, entries, ne, gshift, rec_flags);
+    else
+      k_walk_emit<4, kEmitGroup><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out,
+                                                                          d_summary, d_frames, tile_first, entries,
+                                                                          ne, gshift, rec_flags);
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[3], st));
   r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);

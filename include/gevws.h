@@ -140,13 +140,21 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * records no per-frame entries, so the emit pass re-walks every chain; 0 and
  * 1 store the per-frame entries in 64-byte groups when the batch has >= 128
  * connections per CU; 3 / 4 = speculation with single / grouped entry stores
- * whatever the batch). */
+ * whatever the batch; gevws_tuning_name lists them all, 0 being the per-batch
+ * default), GEVWS_TUNE_SPAN_CONNS_PER_CU the batch size (connections per CU)
+ * up to which the default walk takes one wave per connection (0 = never, the
+ * default: k_walk_span is issue-bound), GEVWS_TUNE_EMIT_VARIANT
+ * the record pass (0 = groups of 16 connections with few frames enumerated
+ * across connection boundaries, 1 = one wave per connection). */
 #define GEVWS_TUNE_UNMASK_VARIANT 1
 #define GEVWS_TUNE_UNMASK_GRID 2
 #define GEVWS_TUNE_ENCODE_VARIANT 3
 #define GEVWS_TUNE_WALK_VARIANT 4
+#define GEVWS_TUNE_SPAN_CONNS_PER_CU 5
+#define GEVWS_TUNE_EMIT_VARIANT 6
 int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
-/* Human-readable name of a tuning value, or NULL. */
+/* Human-readable name of a variant (GEVWS_TUNE_UNMASK_VARIANT or
+ * GEVWS_TUNE_WALK_VARIANT), or NULL past the last one. */
 const char *gevws_tuning_name(int key, int64_t value);
 /* Per-phase HIP-event timing of the following decode calls (0 = off). */
 int gevws_ctx_set_timing(gevws_ctx *ctx, int enable);

@@ -630,16 +630,77 @@ def test_walk_variants_uniform_runs(engine):
              pack_streams([b"".join(wo.encode_frame(bytes(rng.integers(0, 256, 4096, dtype=np.uint8)), 2, True, 0,
                                                     True, bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
                                     for _ in range(n)) for n in (1, 2, 3, 8, 9, 16, 17, 64, 65)])]
+    # noise streams (headers parsed from random bytes, MSB-set lengths), long
+    # streams of small frames crossing the span walk's LDS ring many times,
+    # frames straddling its halves, and an unordered table
+    noise = [random_stream(rng, int(rng.integers(0, 4)), max_len=300, tail=False)
+             + bytes(rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8)) for _ in range(120)]
+    cases.append(pack_streams(noise))
+    smalls = [b"".join(wo.encode_frame(bytes(rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8)),
+                                       int(rng.integers(0, 16)), True, 0, bool(rng.random() < .9),
+                                       bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+                       for _ in range(int(rng.integers(200, 900)))) + bytes(int(rng.integers(0, 9)))
+              for _ in range(24)]
+    smalls += [b"".join(wo.encode_frame(bytes(L), 2, True, 0, True, b"\1\2\3\4") for L in
+                        list(range(0, 2100, 7)) + [70000, 3, 5, 1 << 20, 0, 0, 125, 126, 65535, 65536])]
+    cases.append(pack_streams(smalls))
+    arena, conns = pack_streams([random_stream(rng, int(rng.integers(1, 40))) for _ in range(90)])
+    cases.append((arena, conns[rng.permutation(conns.shape[0])]))
+    walks = engine.variants(_abi.TUNE_WALK_VARIANT)
+    assert len(walks) >= 8
     try:
-        for v in (0, 1, 2, 3, 4):
+        for v in walks:
             engine.set_tuning(_abi.TUNE_WALK_VARIANT, v)
             for k, (arena, conns) in enumerate(cases):
                 assert_matches_oracle(engine, arena, conns, f"walk variant {v} case {k}")
+        # the default's choice of walk by batch size, both sides of the threshold
+        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 0)
+        for per_cu in (0, 1 << 20):
+            engine.set_tuning(_abi.TUNE_SPAN_CONNS_PER_CU, per_cu)  # never / always
+            for k, (arena, conns) in enumerate(cases):
+                assert_matches_oracle(engine, arena, conns, f"span threshold {per_cu} case {k}")
     finally:
         engine.set_tuning(_abi.TUNE_WALK_VARIANT, 0)
+        engine.set_tuning(_abi.TUNE_SPAN_CONNS_PER_CU, 0)
+
+
+def test_emit_variants(engine):
+    """Both record passes (grouped: frames of up to 16 short connections
+    enumerated across connection boundaries; per connection) bit-exact on
+    batches of short, long, empty, unrecorded and mixed connections."""
+    from gev_amd import _abi
+    rng = np.random.default_rng(9191)
+    cases = []
+    for trial in range(3):
+        streams = []
+        for _ in range(int(rng.integers(50, 700))):
+            kind = rng.random()
+            if kind < 0.5:    # a few small frames (groups take the enumerated path)
+                streams.append(random_stream(rng, int(rng.integers(0, 6)), max_len=200))
+            elif kind < 0.7:  # long chains (groups of these go connection by connection)
+                streams.append(random_stream(rng, int(rng.integers(60, 200)), max_len=100, tail=False))
+            elif kind < 0.8:  # 10-byte frames: more frames than entry slots -> re-walked
+                streams.append(b"".join(wo.encode_frame(b"abcd", 1, True, 0, True, b"\1\2\3\4")
+                                        for _ in range(int(rng.integers(1, 40)))))
+            else:
+                streams.append(b"")
+        cases.append(pack_streams(streams))
+    # exactly 64 x 4 frames in a group, and one more
+    for nfr in (16, 17):
+        cases.append(pack_streams([b"".join(wo.encode_frame(bytes(20), 2, True, 0, True, b"\1\2\3\4")
+                                            for _ in range(nfr)) for _ in range(40)]))
+    try:
+        for v in (0, 1):
+            engine.set_tuning(_abi.TUNE_EMIT_VARIANT, v)
+            for k, (arena, conns) in enumerate(cases):
+                assert_matches_oracle(engine, arena, conns, f"emit variant {v} case {k}")
+    finally:
+        engine.set_tuning(_abi.TUNE_EMIT_VARIANT, 0)
 
 
 def test_walk_variant_knob_bounds(engine):
     from gev_amd import _abi
     with pytest.raises(ValueError):
-        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 5)
+        engine.set_tuning(_abi.TUNE_WALK_VARIANT, len(engine.variants(_abi.TUNE_WALK_VARIANT)))
+    with pytest.raises(ValueError):
+        engine.set_tuning(_abi.TUNE_WALK_VARIANT, -1)
