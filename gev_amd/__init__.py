@@ -33,7 +33,8 @@ FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked
 CONN_OUT_DTYPE = np.dtype([("first_frame", "<u8"), ("consumed", "<u8"), ("payload_base", "<u8"),
                            ("nframes", "<u4"), ("status", "<i4")])
 SUMMARY_DTYPE = np.dtype([("frames", "<u8"), ("payload_bytes", "<u8"), ("payload_len", "<u8"),
-                          ("errors", "<u8"), ("status", "<i4"), ("flags", "<u4"), ("reserved", "<u8", (3,))])
+                          ("errors", "<u8"), ("status", "<i4"), ("flags", "<u4"), ("run_frames", "<u8"),
+                          ("reserved", "<u8", (2,))])
 OUT_FRAME_DTYPE = np.dtype([("fin", "u1"), ("rsv", "u1"), ("opcode", "u1"), ("masked", "u1"),
                             ("mask", "u1", (4,)), ("length", "<i8"),
                             ("payload_off", "<u8"), ("payload_len", "<u8")])

@@ -84,7 +84,7 @@ class ConnOut(ctypes.Structure):
 class Summary(ctypes.Structure):
     _fields_ = [("frames", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64),
                 ("payload_len", ctypes.c_uint64), ("errors", ctypes.c_uint64), ("status", ctypes.c_int32),
-                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint64 * 3)]
+                ("flags", ctypes.c_uint32), ("run_frames", ctypes.c_uint64), ("reserved", ctypes.c_uint64 * 2)]
 
 
 class ProtocolStats(ctypes.Structure):

@@ -49,6 +49,16 @@ constexpr int kUnmaskBlock = 256;
 constexpr uint64_t kTile = GEVWS_TILE;
 static_assert(kTile == kUnmaskBlock * 16, "one tile = one 16-byte chunk per lane");
 constexpr int kBlkFields = 4;  // frames, padded payload bytes, payload length, errors
+// decode partials: the four above + frames of a connection's equal-size runs
+// (the size of the frame before them on the connection) -> summary.run_frames
+constexpr int kDecFields = 5;
+// up to this many walk blocks the last one to finish scans the partials
+// (no separate k_scan_blocks launch); more take the scan kernel: every block
+// counts itself with an atomic on one address, and 1 024 of them serialise
+// for longer than the launch they save (C1-shaped batch: walk + scan 46 ->
+// 54 us fused; 256 blocks -- C2, C3, C5, an 8-way C4 share -- save 4-8 us)
+constexpr uint32_t kFusedScanMaxBlocks = 256;
+constexpr bool kFusedScan = true;  // see gevws_decode_batch_async
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ u32x4 ld16u(const uint8_t* p) {
@@ -150,16 +160,14 @@ __device__ __forceinline__ void block_excl_scan(const uint64_t (&v)[NV], uint64_
     if (lane == 63) s_w[k][w] = inc[k];
   }
   __syncthreads();
+  // lane j reads wave j's total: one LDS load per field instead of NW
+  // (unrolled over NV x NW it took 160 VGPRs at NV = 5 and spilled)
+  static_assert(NW <= 64, "one lane per wave total");
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    uint64_t base = 0, all = 0;
-    for (int j = 0; j < NW; ++j) {
-      const uint64_t s = s_w[k][j];
-      base += (j < w) ? s : 0;
-      all += s;
-    }
-    ex[k] = base + inc[k] - v[k];
-    tot[k] = all;
+    const uint64_t sj = lane < NW ? s_w[k][lane] : 0;
+    ex[k] = wave_sum(lane < w ? sj : 0) + inc[k] - v[k];
+    tot[k] = wave_sum(sj);
   }
   __syncthreads();
 }
@@ -178,6 +186,88 @@ __device__ __forceinline__ uint32_t fresh_tid() {
 __device__ __forceinline__ uint32_t uniform32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
   return (uint64_t)uniform32((uint32_t)x) | ((uint64_t)uniform32((uint32_t)(x >> 32)) << 32);
+}
+
+// The decode's partials scan by ONE wave (the walk's last block, see
+// walk_block_done): per round each lane takes 8 consecutive block partials,
+// fields 0/1 become exclusive bases (frames, arena bytes) for k_walk_bases,
+// every field is totalled into the summary, with the capacity check.
+__device__ void scan_partials_wave(uint64_t* __restrict__ blk, uint32_t nblk, uint64_t max_frames,
+                                   uint64_t payload_cap, gevws_summary* __restrict__ sum) {
+  constexpr int P = 8;
+  const int lane = threadIdx.x & 63;
+  uint64_t carry[kDecFields] = {0, 0, 0, 0, 0};
+  for (uint64_t base = 0; base < nblk; base += 64 * P) {  // wave-uniform
+    const uint64_t i0 = base + (uint64_t)lane * P;
+    uint64_t loc[kDecFields] = {0, 0, 0, 0, 0};
+    uint64_t loc0[P], loc1[P];  // this lane's partials of fields 0 / 1, for the bases
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      loc0[r] = (i0 + r < nblk) ? __hip_atomic_load(blk + (i0 + r) * kDecFields, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) : 0;
+      loc1[r] = (i0 + r < nblk) ? __hip_atomic_load(blk + (i0 + r) * kDecFields + 1, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < P; ++r)
+#pragma unroll
+      for (int k = 0; k < kDecFields; ++k)
+        loc[k] += (i0 + r < nblk) ? __hip_atomic_load(blk + (i0 + r) * kDecFields + k, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0;
+    const uint64_t inc0 = wave_incl_scan(loc[0]), inc1 = wave_incl_scan(loc[1]);
+    uint64_t b0 = carry[0] + inc0 - loc[0], b1 = carry[1] + inc1 - loc[1];
+#pragma unroll
+    for (int r = 0; r < P; ++r) {
+      if (i0 + r < nblk) {
+        uint64_t* q = blk + (i0 + r) * kDecFields;
+        const uint64_t f0 = loc0[r], f1 = loc1[r];
+        q[0] = b0;
+        q[1] = b1;
+        b0 += f0;
+        b1 += f1;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kDecFields; ++k) carry[k] += wave_sum(loc[k]);
+  }
+  if (lane == 0) {
+    gevws_summary sm;
+    memset(&sm, 0, sizeof(sm));
+    sm.frames = carry[0];
+    sm.payload_bytes = carry[1];
+    sm.payload_len = carry[2];
+    sm.errors = carry[3] & 0xffffffffull;
+    sm.flags = (carry[3] >> 32) ? GEVWS_SUMMARY_UNORDERED : 0u;
+    sm.run_frames = carry[4];
+    sm.status = (carry[0] > max_frames || carry[1] > payload_cap) ? GEVWS_ERR_CAPACITY : GEVWS_OK;
+    *sum = sm;
+  }
+}
+
+// The last of the walk's workgroups to finish (a device-scope counter) scans
+// the partials, so the decode needs no k_scan_blocks launch.  L2 is per XCD
+// and not coherent, and a release fence would write back the whole L2 (the
+// walk's entry stores: measured 2x slower), so only the partials travel
+// coherently: they are stored and loaded as agent-scope atomics (write-through
+// / L2-bypassing), each writer waits for its stores before its workgroup counts
+// itself, and the last workgroup resets the counter for the context's next call.
+__device__ __forceinline__ void put_partial(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uint32_t nblk, uint64_t* __restrict__ blk,
+                                                uint64_t max_frames, uint64_t payload_cap,
+                                                gevws_summary* __restrict__ sum, bool wrote) {
+  __shared__ uint32_t s_last;
+  if (wrote) __builtin_amdgcn_s_waitcnt(0);  // the partials' write-through stores are done
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1 ? 1u : 0u;
+  __syncthreads();
+  if (s_last) {
+    if (threadIdx.x < 64) scan_partials_wave(blk, nblk, max_frames, payload_cap, sum);
+    if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ------------------------------------------------------------------ 1. walk (count)
@@ -282,9 +372,11 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
                                                             uint32_t n, gevws_conn_out* __restrict__ cout,
                                                             uint64_t* __restrict__ blk,
                                                             WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                            uint32_t gshift, uint32_t cpb, uint64_t in_bytes) {
+                                                            uint32_t gshift, uint32_t cpb, uint64_t in_bytes,
+                                                            uint32_t* __restrict__ done, uint64_t max_frames,
+                                                            uint64_t payload_cap, gevws_summary* __restrict__ sum) {
   const uint32_t c = blockIdx.x * cpb + threadIdx.x;
-  uint64_t nf = 0, pb = 0, pl = 0, err = 0;
+  uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0, lastf = ~0ull;
   if (threadIdx.x < cpb && c < n) {
     gevws_conn_in ci = conns[c];
     // the order flag rides in the high half of the error count (k_scan_blocks SPLIT)
@@ -342,6 +434,9 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       ++nf;
       pb += round16(L);
       pl += L;
+      const uint64_t f = (uint64_t)(meta >> 16) + L;  // frame size (hlen + L)
+      same += f == lastf;
+      lastf = f;
     };
     uint32_t pfv[PF > 0 ? PF : 1] = {};
     for (;;) {
@@ -461,12 +556,16 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
     cout[c] = o;
   }
   // block partial sums (one wave)
-  const uint64_t vals[kBlkFields] = {nf, pb, pl, err};
+  const uint64_t vals[kDecFields] = {nf, pb, pl, err, same};
 #pragma unroll
-  for (int k = 0; k < kBlkFields; ++k) {
+  for (int k = 0; k < kDecFields; ++k) {
     const uint64_t s = wave_sum(vals[k]);
-    if (threadIdx.x == 0) blk[(uint64_t)blockIdx.x * kBlkFields + k] = s;
+    if (threadIdx.x == 0) {
+      if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + k, s);
+      else blk[(uint64_t)blockIdx.x * kDecFields + k] = s;
+    }
   }
+  if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
 }
 
 // ------------------------------------------------------------------ 1b. walk (count), one wave per connection
@@ -503,14 +602,16 @@ __global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __
                                                              gevws_conn_out* __restrict__ cout,
                                                              uint64_t* __restrict__ blk,
                                                              WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                             uint32_t gshift, uint64_t in_bytes) {
+                                                             uint32_t gshift, uint64_t in_bytes,
+                                                             uint32_t* __restrict__ done, uint64_t max_frames,
+                                                             uint64_t payload_cap, gevws_summary* __restrict__ sum) {
   constexpr uint64_t S = (uint64_t)K * 1024;  // bytes per ring half
   constexpr uint32_t RW = (uint32_t)(2 * S / 8);  // ring words (u64) per wave
   __shared__ uint64_t s_ring[kSpanWaves][RW];
-  __shared__ uint64_t s_part[kSpanWaves][kBlkFields];
+  __shared__ uint64_t s_part[kSpanWaves][kDecFields];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t c = blockIdx.x * kSpanWaves + wave;
-  uint64_t nf = 0, pb = 0, pl = 0, err = 0;  // wave-uniform
+  uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0;  // wave-uniform
   if (c < n) {
     gevws_conn_in ci = conns[c];
     ci.off = uniform64(ci.off);
@@ -602,6 +703,7 @@ __global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __
           nf += k;
           pb += add_pb;
           pl += add_pl;
+          same += k;  // each frame of the batch has the run's size F
           flushed = nf;
           pos += (uint64_t)k * F;
         }
@@ -648,6 +750,7 @@ __global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __
       }
       put_entry(pos, key, L, meta);
       const uint64_t fsz = hlen + L;
+      same += fsz == prev_fsz;
       run = fsz == prev_fsz ? run + 1 : 1;
       prev_fsz = fsz;
       pos += fsz;
@@ -668,21 +771,24 @@ __global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __
     s_part[wave][1] = pb;
     s_part[wave][2] = pl;
     s_part[wave][3] = err;
+    s_part[wave][4] = same;
   }
   __syncthreads();
-  if (threadIdx.x < kBlkFields) {
+  if (threadIdx.x < kDecFields) {
     uint64_t sm = 0;
 #pragma unroll
     for (int w = 0; w < kSpanWaves; ++w) sm += s_part[w][threadIdx.x];
-    blk[(uint64_t)blockIdx.x * kBlkFields + threadIdx.x] = sm;
+    if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + threadIdx.x, sm);
+    else blk[(uint64_t)blockIdx.x * kDecFields + threadIdx.x] = sm;
   }
+  if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x < kDecFields);
 }
 
 // ------------------------------------------------------------------ 2. scan of block partials
 // SPLIT (decode): field 3 holds errors in its low 32 bits and the count of
 // out-of-order connections in its high 32 (k_walk_count) -> summary.errors and
 // GEVWS_SUMMARY_UNORDERED.
-template <bool SPLIT>
+template <bool SPLIT, int NF = kBlkFields>
 __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict__ blk, uint32_t nblk,
                                                             uint64_t max_frames, uint64_t payload_cap,
                                                             gevws_summary* __restrict__ sum) {
@@ -690,21 +796,21 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict
   // (encode / dispatch of 43.8 M frames: 171 K partials) takes a few rounds of
   // the workgroup instead of one round per 1 024 partials
   constexpr int kScanPer = 8;
-  uint64_t carry[kBlkFields] = {0, 0, 0, 0};
+  uint64_t carry[NF] = {};
   for (uint64_t base = 0; base < nblk; base += (uint64_t)kScanBlock * kScanPer) {
     const uint64_t i0 = base + (uint64_t)threadIdx.x * kScanPer;
-    uint64_t loc[kBlkFields] = {0, 0, 0, 0}, ex[kBlkFields], tot[kBlkFields];
+    uint64_t loc[NF] = {}, ex[NF], tot[NF];
 #pragma unroll
     for (int r = 0; r < kScanPer; ++r)
 #pragma unroll
-      for (int k = 0; k < kBlkFields; ++k) loc[k] += (i0 + r < nblk) ? blk[(i0 + r) * kBlkFields + k] : 0;
-    block_excl_scan<kScanBlock, kBlkFields>(loc, ex, tot);
+      for (int k = 0; k < NF; ++k) loc[k] += (i0 + r < nblk) ? blk[(i0 + r) * NF + k] : 0;
+    block_excl_scan<kScanBlock, NF>(loc, ex, tot);
     // fields 0/1 become exclusive bases (frames, arena bytes)
     uint64_t b0 = carry[0] + ex[0], b1 = carry[1] + ex[1];
 #pragma unroll
     for (int r = 0; r < kScanPer; ++r) {
       if (i0 + r < nblk) {  // re-read (cached) rather than held across the scan: register budget
-        uint64_t* p = blk + (i0 + r) * kBlkFields;
+        uint64_t* p = blk + (i0 + r) * NF;
         const uint64_t f0 = p[0], f1 = p[1];
         p[0] = b0;
         p[1] = b1;
@@ -713,7 +819,7 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict
       }
     }
 #pragma unroll
-    for (int k = 0; k < kBlkFields; ++k) carry[k] += tot[k];
+    for (int k = 0; k < NF; ++k) carry[k] += tot[k];
   }
   if (threadIdx.x == 0) {
     gevws_summary s;
@@ -723,6 +829,7 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict
     s.payload_len = carry[2];
     s.errors = SPLIT ? (carry[3] & 0xffffffffull) : carry[3];
     s.flags = (SPLIT && (carry[3] >> 32)) ? GEVWS_SUMMARY_UNORDERED : 0u;
+    if constexpr (NF > 4) s.run_frames = carry[4];
     s.status = (carry[0] > max_frames || carry[1] > payload_cap) ? GEVWS_ERR_CAPACITY : GEVWS_OK;
     *sum = s;
   }
@@ -749,8 +856,8 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_co
   block_excl_scan<kCountBlock, 2>(v, ex, tot);
   if (!active) return;
   rec_flags[c] = o.first_frame != 0 ? 1 : 0;  // k_walk_count's "entries recorded" flag
-  o.first_frame = blk[(uint64_t)blockIdx.x * kBlkFields + 0] + ex[0];
-  o.payload_base = blk[(uint64_t)blockIdx.x * kBlkFields + 1] + ex[1];
+  o.first_frame = blk[(uint64_t)blockIdx.x * kDecFields + 0] + ex[0];
+  o.payload_base = blk[(uint64_t)blockIdx.x * kDecFields + 1] + ex[1];
   cout[c] = o;
 }
 
@@ -1254,16 +1361,23 @@ __device__ __forceinline__ uint64_t stream_run(const uint8_t* __restrict__ in, u
   return t + n * U2;
 }
 
+// The LDS frame table of a window (kWinFrames entries each).
+struct WinLds {
+  uint32_t* start;   // frame start relative to the window (clamped at 0)
+  int32_t* lend;     // payload end relative to the window (clamped)
+  uint64_t* delta;   // src_off - payload_off (mod 2^64)
+  uint32_t* key;
+};
+
 template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles>
-__global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __restrict__ in,
-                                                            const gevws_frame* __restrict__ frames,
-                                                            const uint32_t* __restrict__ tile_first,
-                                                            const gevws_summary* __restrict__ sum,
-                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
-  __shared__ uint32_t s_start[kWinFrames];   // frame start relative to the window (clamped at 0)
-  __shared__ int32_t s_lend[kWinFrames];     // payload end relative to the window (clamped)
-  __shared__ uint64_t s_delta[kWinFrames];   // src_off - payload_off (mod 2^64)
-  __shared__ uint32_t s_key[kWinFrames];
+__device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
+                                               const uint32_t* __restrict__ tile_first,
+                                               const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
+                                               uint32_t big_grid, const WinLds& L) {
+  uint32_t* const s_start = L.start;
+  int32_t* const s_lend = L.lend;
+  uint64_t* const s_delta = L.delta;
+  uint32_t* const s_key = L.key;
   if (sum->status != GEVWS_OK) return;
   const uint64_t total = sum->payload_bytes;
   const uint64_t nframes = sum->frames;
@@ -1365,6 +1479,19 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __res
   }
 }
 
+template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles>
+__global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __restrict__ in,
+                                                            const gevws_frame* __restrict__ frames,
+                                                            const uint32_t* __restrict__ tile_first,
+                                                            const gevws_summary* __restrict__ sum,
+                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
+  __shared__ uint32_t s_start[kWinFrames];   // frame start relative to the window (clamped at 0)
+  __shared__ int32_t s_lend[kWinFrames];     // payload end relative to the window (clamped)
+  __shared__ uint64_t s_delta[kWinFrames];   // src_off - payload_off (mod 2^64)
+  __shared__ uint32_t s_key[kWinFrames];
+  unmask_v3_body<U, NTL, NTS, AL, WT>(in, frames, tile_first, sum, out, big_grid, WinLds{s_start, s_lend, s_delta, s_key});
+}
+
 // v4 = v3 with the window path software-pipelined.  In v3 every window is one
 // chain of dependent global loads: the tile map and the cached-frame record
 // (scalar) that decide streaming vs window, the window's records, the LDS
@@ -1405,15 +1532,14 @@ __device__ __forceinline__ WinRec load_rec(const gevws_frame* __restrict__ frame
 // addresses were spilled (threadIdx.x used directly).
 // SP: streaming steps as software-pipelined runs (stream_run, U / 2 tiles per step).
 template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false>
-__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_v4(const uint8_t* __restrict__ in,
-                                                            const gevws_frame* __restrict__ frames,
-                                                            const uint32_t* __restrict__ tile_first,
-                                                            const gevws_summary* __restrict__ sum,
-                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
-  __shared__ uint32_t s_start[kWin4Frames];   // frame start relative to the window (clamped at 0)
-  __shared__ int32_t s_lend[kWin4Frames];     // payload end relative to the window (clamped)
-  __shared__ uint64_t s_delta[kWin4Frames];   // src_off - payload_off (mod 2^64)
-  __shared__ uint32_t s_key[kWin4Frames];
+__device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
+                                               const uint32_t* __restrict__ tile_first,
+                                               const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
+                                               uint32_t big_grid, const WinLds& L) {
+  uint32_t* const s_start = L.start;
+  int32_t* const s_lend = L.lend;
+  uint64_t* const s_delta = L.delta;
+  uint32_t* const s_key = L.key;
   if (sum->status != GEVWS_OK) return;
   const uint64_t total = sum->payload_bytes;
   const uint64_t nframes = sum->frames;
@@ -1572,6 +1698,42 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
     }
     t = wend_t;
   }
+}
+
+template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false>
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_v4(const uint8_t* __restrict__ in,
+                                                            const gevws_frame* __restrict__ frames,
+                                                            const uint32_t* __restrict__ tile_first,
+                                                            const gevws_summary* __restrict__ sum,
+                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
+  __shared__ uint32_t s_start[kWin4Frames];
+  __shared__ int32_t s_lend[kWin4Frames];
+  __shared__ uint64_t s_delta[kWin4Frames];
+  __shared__ uint32_t s_key[kWin4Frames];
+  unmask_v4_body<U, WT, NTS, WC, FT, SP>(in, frames, tile_first, sum, out, big_grid,
+                                         WinLds{s_start, s_lend, s_delta, s_key});
+}
+
+// The default unmask: the batch's own statistics pick the window scheme --
+// batches of equal-size frames (at least half of the frames the size of the
+// one before them on the connection: C1, C2, C3) take v3's 4-tile windows,
+// mixed ones (C4, C5) v4's pipelined 8-tile windows (interleaved A/B:
+// v3-4 -5 % on C1-shaped and -2.4 % on C2 batches, v4-8 -3 % on C4 and -2 % on
+// C5, equal on C3; profiles/r02_ab2.log).  One kernel, one LDS table, the
+// choice is a uniform branch on the summary the walk wrote.
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto(
+    const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
+  __shared__ uint32_t s_start[kWin4Frames];
+  __shared__ int32_t s_lend[kWin4Frames];
+  __shared__ uint64_t s_delta[kWin4Frames];
+  __shared__ uint32_t s_key[kWin4Frames];
+  static_assert(kWinFrames == kWin4Frames, "one LDS table for both bodies");
+  const WinLds L{s_start, s_lend, s_delta, s_key};
+  if (2 * sum->run_frames >= sum->frames)  // frames the size of their predecessor on the connection
+    unmask_v3_body<16, false, true, 2>(in, frames, tile_first, sum, out, big_grid, L);
+  else
+    unmask_v4_body<16, 8, true>(in, frames, tile_first, sum, out, big_grid, L);
 }
 
 // ------------------------------------------------------------------ outbound encode (§8f row 1)
@@ -2329,6 +2491,7 @@ struct gevws_ctx {
   hipStream_t last_stream = nullptr;
   bool has_last = false;
   int num_cus = 256;
+  uint32_t* d_done = nullptr;  // the decode walk's finished-workgroup counter (zero between calls)
 };
 
 namespace {
@@ -2398,6 +2561,9 @@ struct UnmaskVariant {
 // Variant 0 is the default; the others are kept for A/B measurement
 // (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 const UnmaskVariant kUnmaskVariants[] = {
+    {k_unmask_auto, 16,
+     "auto: v3 4-tile windows for batches of equal-size frames, v4 pipelined 8-tile windows otherwise (summary "
+     "statistics of the walk)"},
     {k_unmask_v4<16, 8, true>, 16,
      "v4 U16 streaming (aligned loads, DPP rotate) + pipelined 8-tile LDS window (next step's tile map and "
      "records fetched during the current window's payload loads)"},
@@ -2485,7 +2651,9 @@ gevws_ctx* gevws_ctx_create(int device) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
-  if (hipMalloc(reinterpret_cast<void**>(&ctx->d_sum), sizeof(gevws_summary)) != hipSuccess) {
+  if (hipMalloc(reinterpret_cast<void**>(&ctx->d_sum), sizeof(gevws_summary)) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&ctx->d_done), 256) != hipSuccess ||
+      hipMemset(ctx->d_done, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     gevws_ctx_destroy(ctx);
     return nullptr;
   }
@@ -2498,6 +2666,7 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->d_sum) (void)hipFree(ctx->d_sum);
+  if (ctx->d_done) (void)hipFree(ctx->d_done);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
   for (auto& set : ctx->evs)
     for (auto& e : set.e) (void)hipEventDestroy(e);
@@ -2596,7 +2765,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
                                   : (n_conns + ncu - 1) / ncu > 0 ? (n_conns + ncu - 1) / ncu : 1;
   const uint32_t nblk = (n_conns + cpb - 1) / cpb;
   const uint64_t ntiles_cap = (payload_cap + kTile - 1) / kTile + 1;
-  const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
+  const size_t blk_bytes = ((size_t)nblk * kDecFields * sizeof(uint64_t) + 255) & ~size_t(255);
   const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
   uint32_t gshift = kEntryGranMinShift;
   while ((in_bytes >> gshift) > kEntryBudget) ++gshift;
@@ -2626,13 +2795,19 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   // walk variant 2 (measurement): no entry table -- the counting walk stores
   // nothing per frame and the emit pass re-walks every chain
   const uint64_t ne = ctx->walk_variant == 2 ? 0 : n_entries;
+  // The walk's last workgroup scans the partials itself (walk_block_done) and
+  // saves the k_scan_blocks launch (with release / acquire fences instead of
+  // coherent partials it was slower: C1-shaped walk 0.034 -> 0.074 ms,
+  // profiles/r02_steps_fused.jsonl).
+  const bool fused = kFusedScan && nblk > 0 && nblk <= kFusedScanMaxBlocks;
+  uint32_t* done = fused ? ctx->d_done : nullptr;
   if (nblk && span) {
     if (wv == 7)
       k_walk_span<2><<<nblk, kSpanWaves * 64, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
-                                                       in_bytes);
+                                                       in_bytes, done, max_frames, payload_cap, d_summary);
     else
       k_walk_span<1><<<nblk, kSpanWaves * 64, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
-                                                       in_bytes);
+                                                       in_bytes, done, max_frames, payload_cap, d_summary);
   } else if (nblk) {
     // grouped entry stores pay off when the walk is bound by its line traffic
     // (many concurrent chains), not by chain latency (few)
@@ -2641,40 +2816,50 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     if (wv == 8 || wv == 9) {
       if (grp && wv == 8)
         k_walk_count<0, true, false, 1><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
-                                                                     entries, ne, gshift, cpb, in_bytes);
+                                                                     entries, ne, gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
       else if (wv == 8)
         k_walk_count<0, false, false, 1><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
-                                                                      entries, ne, gshift, cpb, in_bytes);
+                                                                      entries, ne, gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
       else if (grp)
         k_walk_count<0, true, false, 2><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
-                                                                     entries, ne, gshift, cpb, in_bytes);
+                                                                     entries, ne, gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
       else
         k_walk_count<0, false, false, 2><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
-                                                                      entries, ne, gshift, cpb, in_bytes);
+                                                                      entries, ne, gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
     } else if (wv == 5) {
       if (grp)
         k_walk_count<8, true, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries,
-                                                                  ne, gshift, cpb, in_bytes);
+                                                                  ne, gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
       else
         k_walk_count<8, false, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries,
-                                                                   ne, gshift, cpb, in_bytes);
+                                                                   ne, gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
     } else if (wv == 1) {
       if (grp)
         k_walk_count<0, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                            gshift, cpb, in_bytes);
+                                                            gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
       else
         k_walk_count<0, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                             gshift, cpb, in_bytes);
+                                                             gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
     } else if (grp) {
       k_walk_count<8, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                          gshift, cpb, in_bytes);
+                                                          gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
     } else {
       k_walk_count<8, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                           gshift, cpb, in_bytes);
+                                                           gshift, cpb, in_bytes, done, max_frames,
+                                                            payload_cap, d_summary);
     }
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[1], st));
-  k_scan_blocks<true><<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
+  if (!fused) k_scan_blocks<true, kDecFields><<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
   if (timed) GEVWS_HIP(hipEventRecord(ev[2], st));
   if (nblk) {
     k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb);

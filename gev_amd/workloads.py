@@ -275,6 +275,20 @@ def shard_lpt(layout: Layout, rank: int, world: int) -> Layout:
     return Layout(layout.name, desc, conns, int(new_off[-1]), pl, padded, layout.seed)
 
 
+def run_frames(layout: Layout) -> int:
+    """summary.run_frames of a decode of the whole layout: frames whose size
+    (h + L) equals the size of the frame before them on the same connection."""
+    d = layout.desc
+    if d.shape[0] == 0:
+        return 0
+    size = header_len(d["length"].astype(np.int64), d["masked"], d["len_form"].astype(np.int64)) + \
+        d["length"].astype(np.int64)
+    first = np.zeros(d.shape[0], bool)
+    starts = np.searchsorted(d["hdr_off"].astype(np.int64), layout.conns[:, 0], side="left")
+    first[starts[starts < d.shape[0]]] = True
+    return int(((size[1:] == size[:-1]) & ~first[1:]).sum())
+
+
 def size_histogram(layout: Layout) -> list:
     """Realised payload-length histogram, power-of-two buckets: [[lo, hi, frames], ...]."""
     L = layout.desc["length"].astype(np.int64)

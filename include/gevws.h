@@ -105,7 +105,10 @@ typedef struct gevws_summary {
     uint64_t errors;        /* connections with status < 0 */
     int32_t status;         /* GEVWS_OK or GEVWS_ERR_CAPACITY */
     uint32_t flags;         /* GEVWS_SUMMARY_* (decode only; informational) */
-    uint64_t reserved[3];
+    uint64_t run_frames;    /* decode: frames the size (h + L) of the frame before them on
+                               their connection -- the batch's uniformity, which picks the
+                               unmask kernel's window scheme */
+    uint64_t reserved[2];
 } gevws_summary;
 
 /* summary.flags: the connection table was not in increasing, non-overlapping

@@ -46,8 +46,25 @@ def assert_matches_oracle(engine, arena: bytes | np.ndarray, conns: np.ndarray, 
     assert int(s["errors"]) == int((want["conn_status"] < 0).sum()), tag
     assert int(s["payload_len"]) == int(want["frames"]["length"].sum()), tag
     assert got["frames"].tobytes() == want["frames"].tobytes(), tag
+    assert int(s["run_frames"]) == oracle_run_frames(want, conns), tag
     assert np.array_equal(got["payload"], want["payload"]), tag
     return got
+
+
+def oracle_run_frames(want, conns) -> int:
+    """summary.run_frames from the oracle's records: frames whose size (h + L)
+    equals the size of the frame before them on the same connection."""
+    fr = want["frames"]
+    n = 0
+    for c in range(conns.shape[0]):
+        f0, k = int(want["conn_first"][c]), int(want["conn_nframes"][c])
+        prev_end, prev = int(conns[c, 0]), None
+        for i in range(f0, f0 + k):
+            end = int(fr["src_off"][i]) + int(fr["length"][i])
+            size = end - prev_end
+            n += size == prev
+            prev, prev_end = size, end
+    return n
 
 
 def random_stream(rng, n_frames: int, max_len: int = 3072, tail: bool = True) -> bytes:

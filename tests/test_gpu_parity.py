@@ -255,6 +255,8 @@ def _synth_decode_verify(engine, layout, check_slice_conns: int = 2):
     s = out.summary_host()
     assert int(s["frames"]) == layout.n_frames
     assert int(s["payload_len"]) == layout.payload_len
+    from gev_amd import workloads as wl
+    assert int(s["run_frames"]) == wl.run_frames(layout)
     assert int(s["payload_bytes"]) == layout.payload_padded
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
     engine.verify(desc, layout.n_frames, layout.seed, out, mism)
@@ -376,6 +378,8 @@ def _c4_full(engine, lay, n_check: int = 64):
     s = out.summary_host()
     assert int(s["frames"]) == lay.n_frames and int(s["payload_len"]) == lay.payload_len
     assert int(s["payload_bytes"]) == lay.payload_padded and int(s["errors"]) == 0 and int(s["flags"]) == 0
+    from gev_amd import workloads as wl
+    assert int(s["run_frames"]) == wl.run_frames(lay)
     mism = torch.zeros(1, dtype=torch.int64, device=dev)
     engine.verify(desc, lay.n_frames, lay.seed, out, mism)
     torch.cuda.synchronize()
