@@ -75,8 +75,26 @@ def main():
     ap.add_argument("--prefix", default="split")
     ap.add_argument("--configs", nargs="+", default=["c4"])
     ap.add_argument("--out", default=None)
+    ap.add_argument("--traffic", action="store_true",
+                    help="also record the unmask kernel's bytes per launch in profiles/pmc_traffic.json "
+                         "(bench.py's roofline.traffic)")
+    ap.add_argument("--source", default=None, help="profile file named as the source in pmc_traffic.json")
     args = ap.parse_args()
     res = {cfg: table(args.src, args.prefix, cfg) for cfg in args.configs}
+    if args.traffic:
+        tj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        tab = json.load(open(tj)) if os.path.exists(tj) else {}
+        for cfg, t in res.items():
+            um = [k for k in t if k.startswith("k_unmask")]
+            if not um:
+                continue
+            d = t[um[0]]
+            tab[cfg] = {"kernel": um[0], "hbm_bytes_per_launch": int(d["read_bytes"] + d["write_bytes"]),
+                        "read_bytes": int(d["read_bytes"]), "write_bytes": int(d["write_bytes"]),
+                        "method": "TCC_EA0_RDREQ_{32B,64B,128B} x size + TCC_EA0_WRREQ(_64B) x size, per launch "
+                                  "(exact for any access width; FETCH_SIZE tallies 128-B reads at 64 B on gfx950)",
+                        "source": args.source or f"gpurun_out/{args.prefix}_{cfg}_rd,_wr"}
+        json.dump(tab, open(tj, "w"), indent=1)
     for cfg, t in res.items():
         print(f"== {cfg}")
         for k, d in sorted(t.items(), key=lambda kv: -kv[1]["hbm_bytes"]):
