@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -126,8 +127,9 @@ def cpu_baseline(name: str, seconds: float, threads: int, vectorized: bool = Fal
     import numpy as np
     from gev_amd import workloads as w
     from oracle import ref
-    # >= 16 MiB of payload per thread (not cache-resident), 256 MiB .. 4 GiB in all
-    lay = cpu_sample_layout(name, min(4096, max(256, 16 * threads)))
+    # 64 MiB of payload per thread up to 4 GiB in all (>= 16 MiB per thread at
+    # 256 threads), at least 256 MiB: never cache-resident
+    lay = cpu_sample_layout(name, min(4096, max(256, 64 * threads)))
     arena = np.concatenate([w.synth_host(lay), np.zeros(64, np.uint8)])
     secs, pb, nf = ref.bench_pipeline(arena, lay.conns[:, 0], lay.conns[:, 1], threads=threads,
                                       min_seconds=seconds, vectorized=vectorized)
@@ -371,6 +373,13 @@ def main():
         if nt > 1:
             log(f"cpu baseline ({nt} threads)...")
             result["cpu_baseline_multi"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0), nt)
+        quota = host_cpu_info()["cgroup_cpu_quota"]
+        if not args.cpu_threads_multi and quota and 1 < math.ceil(quota) < nt:
+            # the job's CPU share is capped below its visible threads: also time
+            # one thread per CPU of the quota (no time-sharing between threads)
+            nq = math.ceil(quota)
+            log(f"cpu baseline ({nq} threads = cgroup quota)...")
+            result["cpu_baseline_quota"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0), nq)
         log("cpu baseline (1 thread, auto-vectorised build)...")
         result["cpu_baseline_vectorized"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0), 1,
                                                          vectorized=True)
