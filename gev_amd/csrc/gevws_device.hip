@@ -1981,6 +1981,13 @@ __device__ __forceinline__ u32x4 enc_assemble2(int32_t rel, uint64_t a, uint64_t
   return u32x4_of(acc);
 }
 
+// A 16-byte store of the encode's window path, non-temporal or plain.
+template <bool NT>
+__device__ __forceinline__ void win_store(u32x4 v, u32x4* p) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // COMPACT: a window's chunks that straddle a frame boundary (header bytes or
 // two frames' pieces) are queued in LDS and assembled afterwards by the whole
 // workgroup, one chunk per lane, instead of by the one or two lanes of each
@@ -1989,21 +1996,36 @@ __device__ __forceinline__ u32x4 enc_assemble2(int32_t rel, uint64_t a, uint64_t
 // the window path is latency-bound, so the default LDS-light kernel is held to
 // 72 VGPRs for 7 workgroups per CU (C2 -4 %, C4 -2 % against 6 per CU; 8 per CU
 // at 64 VGPRs was slower on C5, profiles/r01_encode_ab_occ_*.json).
-template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false>
+// HL: the window's payload loads are all issued before its stores (as the
+// decode's window path does); without it each chunk's store waited for its
+// own load.  Alone it changed nothing measurable (C4 11.46 vs 11.47 ms).
+// WNT: the window path's stores are non-temporal (false: plain stores).
+// G64 (with HL): a 64-byte group of chunks holding a frame boundary is
+// written whole by the queue pass -- its interior chunks are queued with it,
+// four consecutive queue slots, so one store instruction writes the group's
+// 64 bytes.  Without it every frame boundary left its line to HBM as two
+// partial writes (the interior chunks, then the queued boundary chunk): C4
+// 46 M 32-byte write requests per launch, 0 with it, and the whole C4 encode
+// 10.70 -> 9.11 ms (profiles/r02_encode_pmc_split_c4*.json,
+// r02_encode_ab_g64_*.json); plain stores recovered part of it by merging
+// the pieces in L2 (10.24 ms) at 2 GB more reads.
+template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false, bool HL = false,
+          bool WNT = true, bool G64 = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
                                                          const uint32_t* __restrict__ tile_first,
                                                          const gevws_summary* __restrict__ sum,
                                                          uint8_t* __restrict__ out, uint32_t big_grid) {
-  __shared__ int32_t s_start[kEncWinFrames];  // wire start relative to the window, clamped >= -64
-  __shared__ int32_t s_pend[kEncWinFrames];   // payload end relative to the window, clamped
-  __shared__ uint8_t s_hlen[kEncWinFrames];
+  constexpr int WF = kEncWinFrames;  // frames per window held in LDS
+  __shared__ int32_t s_start[WF];  // wire start relative to the window, clamped >= -64
+  __shared__ int32_t s_pend[WF];   // payload end relative to the window, clamped
+  __shared__ uint8_t s_hlen[WF];
   __shared__ uint32_t s_bnd[COMPACT ? kWinTiles * kUnmaskBlock : 1];  // queued chunk: rel / 16 | frame << 16
   __shared__ uint32_t s_nb;
-  __shared__ uint64_t s_delta[kEncWinFrames];  // payload_off - out_off - hlen (mod 2^64)
-  __shared__ uint64_t s_h0[LH ? 1 : kEncWinFrames];
-  __shared__ uint64_t s_h1[LH ? 1 : kEncWinFrames];
+  __shared__ uint64_t s_delta[WF];  // payload_off - out_off - hlen (mod 2^64)
+  __shared__ uint64_t s_h0[LH ? 1 : WF];
+  __shared__ uint64_t s_h1[LH ? 1 : WF];
   if (sum->status != GEVWS_OK) return;
   const uint64_t total = sum->payload_bytes;  // wire bytes
   const uint64_t nframes = sum->frames;
@@ -2062,7 +2084,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
     const uint64_t f_lo = tile_first[t];
     const uint64_t f_hi = (t + wt) < ntiles ? (uint64_t)tile_first[t + wt] : nframes - 1;
     const uint64_t F = f_hi - f_lo + 1;
-    if (F <= (uint64_t)kEncWinFrames) {
+    if (F <= (uint64_t)WF) {
       __syncthreads();
       for (uint64_t i = fresh_tid(); i < F; i += kUnmaskBlock) {  // (fresh_tid: see k_unmask_v4's fill)
         const gevws_out_frame o = fr[f_lo + i];
@@ -2082,6 +2104,57 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
       }
       if (COMPACT && threadIdx.x == 0) s_nb = 0;
       __syncthreads();
+      if constexpr (HL && COMPACT) {
+        // loads first, the queue entries after them.  Every valid chunk
+        // loads (a boundary chunk from payload[0], always readable, result
+        // unused): a load inside the interior/boundary branch made the
+        // compiler wait for it at the branch's join
+        u32x4 v[kWinTiles];
+        uint32_t interior = 0, queued = 0;
+        uint32_t qlo[kWinTiles];
+#pragma unroll
+        for (int u = 0; u < kWinTiles; ++u) {
+          const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
+          const uint64_t a = wbase + (uint64_t)rel;
+          const bool valid = (uint64_t)u < wt && a < total;
+          uint32_t lo = 0, hi = valid ? (uint32_t)F - 1 : 0u;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+          }
+          const bool in = valid && rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo];
+          v[u] = ld16u(payload + (in ? a + s_delta[lo] : 0ull));
+          qlo[u] = lo;
+          interior |= (in ? 1u : 0u) << u;
+          queued |= (valid && !in ? 1u : 0u) << u;
+        }
+        if constexpr (G64) {
+          const uint32_t lane = threadIdx.x & 63, g0 = lane & ~3u;
+#pragma unroll
+          for (int u = 0; u < kWinTiles; ++u) {
+            const uint64_t bal = __ballot((queued >> u) & 1u);  // whole wave active
+            const bool defer = ((bal >> g0) & 0xFull) != 0;     // (group-uniform)
+            uint32_t slot = 0;
+            if (defer && (lane & 3u) == 0) slot = atomicAdd(&s_nb, 4u);
+            slot = __shfl(slot, (int)g0);
+            if (defer) {
+              const bool valid = (interior | queued) & (1u << u);
+              s_bnd[slot + (lane & 3u)] =
+                  valid ? ((uint32_t)(u * (int32_t)kTile + (int32_t)lane_off) >> 4) | (qlo[u] << 16) : 0xffffffffu;
+              interior &= ~(1u << u);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < kWinTiles; ++u)
+            if (queued & (1u << u))
+              s_bnd[atomicAdd(&s_nb, 1u)] = ((uint32_t)(u * (int32_t)kTile + (int32_t)lane_off) >> 4) | (qlo[u] << 16);
+        }
+#pragma unroll
+        for (int u = 0; u < kWinTiles; ++u)
+          if (interior & (1u << u))
+            win_store<WNT>(v[u], reinterpret_cast<u32x4*>(out + wbase + u * kTile + fresh_tid() * 16));
+      } else
 #pragma unroll
       for (int u = 0; u < kWinTiles; ++u) {
         const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
@@ -2093,13 +2166,13 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
           if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
         }
         if (rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo]) {  // interior of one payload
-          __builtin_nontemporal_store(ld16u(payload + (a + s_delta[lo])), reinterpret_cast<u32x4*>(out + a));
+          win_store<WNT>(ld16u(payload + (a + s_delta[lo])), reinterpret_cast<u32x4*>(out + a));
         } else if constexpr (COMPACT) {
           s_bnd[atomicAdd(&s_nb, 1u)] = ((uint32_t)rel >> 4) | (lo << 16);
         } else {
           const u32x4 x = enc_assemble<LH>(rel, a, total, lo, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
                                            s_h1, payload, fr, f_lo);
-          __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + a));
+          win_store<WNT>(x, reinterpret_cast<u32x4*>(out + a));
         }
       }
       if constexpr (COMPACT) {
@@ -2107,6 +2180,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
         const uint32_t nb = s_nb;
         for (uint32_t i = fresh_tid(); i < nb; i += kUnmaskBlock) {
           const uint32_t q = s_bnd[i];
+          if (G64 && q == 0xffffffffu) continue;  // a group's slot past the batch's end
           const int32_t rel = (int32_t)((q & 0xffffu) << 4);
           const uint64_t a = wbase + (uint64_t)rel;
           const u32x4 x =
@@ -2114,7 +2188,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
                                      s_h1, payload, fr, f_lo)
                  : enc_assemble<LH>(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
                                     s_h1, payload, fr, f_lo);
-          __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(out + a));
+          win_store<WNT>(x, reinterpret_cast<u32x4*>(out + a));
         }
       }
       t += wt;
@@ -2474,10 +2548,13 @@ struct gevws_ctx {
   gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
   int unmask_variant = 0;
   int unmask_grid = 0;  // 0 = auto
-  int encode_variant = 0;  // 0 = aligned-load streaming + queued boundary chunks, headers rebuilt from
-                           // the records (LDS-light: 7 workgroups per CU), 1 = unaligned loads,
-                           // 2 = aligned loads, per-lane boundary assembly, 3 = as 0 with the headers
-                           // kept in LDS (4 workgroups per CU)
+  int encode_variant = 0;  // 0 = aligned-load streaming + window loads before stores + boundary
+                           // 64-byte groups queued whole, headers rebuilt from the records (7
+                           // workgroups per CU); 1 = unaligned loads, per-lane assembly; 2 = aligned
+                           // loads, per-lane assembly; 3 = queued boundary chunks, headers in LDS (4
+                           // per CU); 4 = queued boundary chunks, LDS-light (round-1 default);
+                           // 5 = 4 + loads before stores; 6 = 5 with plain window stores; 7 = 0 with
+                           // plain window stores
   int emit_variant = 0;    // 0 = grouped record pass (k_walk_emit G = 16), 1 = one wave per connection
   uint32_t span_conns_per_cu = 0;  // walk variant 0: one wave per connection up to this many per CU
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
@@ -2690,7 +2767,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->unmask_grid = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_ENCODE_VARIANT:
-      if (value < 0 || value > 3) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 7) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_EMIT_VARIANT:
@@ -2919,7 +2996,7 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk);
   k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
   if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_summary, d_out_off, tile_first);
-  const uint64_t per_cu = ctx->encode_variant == 0 ? 7 : 4;  // LDS-light kernel at <= 72 VGPRs: 7 per CU
+  const uint64_t per_cu = (ctx->encode_variant == 0 || ctx->encode_variant >= 4) ? 7 : 4;  // LDS-light: 7 per CU
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
   if (grid > per_cu * (uint64_t)ctx->num_cus) grid = per_cu * (uint64_t)ctx->num_cus;
   if (grid < 1) grid = 1;
@@ -2931,7 +3008,11 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   auto enc = ctx->encode_variant == 1   ? k_encode<4, false, false>
              : ctx->encode_variant == 2 ? k_encode<4, true, false>
              : ctx->encode_variant == 3 ? k_encode<4, true, true>
-                                        : k_encode<4, true, true, true, 7, true>;
+             : ctx->encode_variant == 4 ? k_encode<4, true, true, true, 7, true>  // round-1 default
+             : ctx->encode_variant == 5 ? k_encode<4, true, true, true, 7, true, true>
+             : ctx->encode_variant == 6 ? k_encode<4, true, true, true, 7, true, true, false>
+             : ctx->encode_variant == 7 ? k_encode<4, true, true, true, 7, true, true, false, true>
+                                        : k_encode<4, true, true, true, 7, true, true, true, true>;
   // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
   // workgroups per CU (the rest return at once), the window path gets 7
   const uint32_t big = per_cu > 4 && grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;

@@ -133,12 +133,17 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
 /* Tuning knobs for measurement (defaults are the tuned choice):
  * GEVWS_TUNE_UNMASK_VARIANT selects an unmask kernel variant (0 = default),
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto), GEVWS_TUNE_ENCODE_VARIANT
- * the encode kernel (0 = aligned loads + register realign while streaming,
- * frame-boundary chunks queued and assembled by the whole workgroup, frame
- * headers rebuilt from the records so 7 workgroups fit per CU;
- * 1 = unaligned loads, boundary chunks assembled by the lane that meets
- * them; 2 = aligned loads, per-lane assembly; 3 = as 0 with the serialised
- * headers kept in LDS, 4 workgroups per CU), GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
+ * the encode kernel (0 = aligned loads + register realign while streaming;
+ * in frame windows all payload loads issued before the stores, and every
+ * 64-byte group that holds a frame boundary queued whole and written by one
+ * store instruction of the workgroup's assembly pass; frame headers rebuilt
+ * from the records so 7 workgroups fit per CU; 1 = unaligned loads, boundary
+ * chunks assembled by the lane that meets them; 2 = aligned loads, per-lane
+ * assembly; 3 = boundary chunks queued alone, serialised headers kept in
+ * LDS, 4 workgroups per CU; 4 = boundary chunks queued alone, LDS-light (the
+ * round-1 default); 5 = 4 with the loads before the stores; 6 = 5 with plain
+ * (not non-temporal) window stores; 7 = 0 with plain window stores),
+ * GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
  * uniform-stream speculation, 1 = plain chain walk, 2 = plain walk that
  * records no per-frame entries, so the emit pass re-walks every chain; 0 and
  * 1 store the per-frame entries in 64-byte groups when the batch has >= 128

@@ -47,12 +47,19 @@ def test_encode_golden(engine, golden):
     assert np.array_equal(got, g["wire"])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+ENC_VARIANTS = list(range(8))
+
+
+@pytest.mark.parametrize("variant", ENC_VARIANTS)
 def test_encode_random_and_tiny_frames(engine, variant):
-    """variant 0: aligned-load streaming + boundary chunks assembled by the
-    whole workgroup, headers rebuilt from the records (default, 7 workgroups
-    per CU); 1: unaligned loads, per-lane assembly; 2: aligned-load streaming,
-    per-lane assembly; 3: as 0 with the headers kept in LDS (4 per CU)."""
+    """variant 0 (default): aligned-load streaming; frame windows issue their
+    loads before their stores and queue every 64-byte group holding a frame
+    boundary whole for the workgroup's assembly pass, headers rebuilt from the
+    records (7 workgroups per CU); 1: unaligned loads, per-lane assembly; 2:
+    aligned-load streaming, per-lane assembly; 3: boundary chunks queued
+    alone, headers in LDS (4 per CU); 4: boundary chunks queued alone,
+    LDS-light (round-1 default); 5: 4 + loads before stores; 6: 5 with plain
+    window stores; 7: 0 with plain window stores."""
     from gev_amd import _abi
     engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, variant)
     try:
@@ -78,6 +85,46 @@ def _encode_random(engine):
             hd.append(np.frombuffer(h.pack(), np.uint8))
         fr = _records(np.array(hd), offs[perm], lens[perm])
         _encode_check(engine, fr, payload, f"trial {trial}")
+
+
+def _uniform_frames(wire_len: int, n: int, rng):
+    """n unmasked binary frames of `wire_len` wire bytes each (2-byte header)."""
+    L = wire_len - 2
+    payload = rng.integers(0, 256, n * L + 1, dtype=np.uint8)
+    hd = np.array([np.frombuffer(wo.Header(True, 0, 2, False, b"\0\0\0\0", L).pack(), np.uint8)
+                   for _ in range(n)])
+    offs = (np.arange(n, dtype=np.uint64) * np.uint64(L))
+    return _records(hd, offs, np.full(n, L)), payload
+
+
+@pytest.mark.parametrize("variant", ENC_VARIANTS)
+def test_encode_window_queue_at_capacity(engine, variant):
+    """Windows whose boundary queues are as full as they get: 1 024 frames
+    of 16 wire bytes in one 4-tile window (every chunk holds a header, so the
+    workgroup queue takes all 1 024 chunks -- as single chunks or as 256
+    whole 64-byte groups -- and F = the window's frame capacity); one frame
+    more (the per-lane fallback); frames of 32 B (every other 64-byte group
+    half header); frames of 17 / 24 / 33 B (boundaries at every phase, groups
+    with one to four boundaries); and runs of tiny frames between big ones
+    (three or more frames per chunk).  Regression test for the queue's
+    capacity and for groups cut by the batch's end (sentinel slots)."""
+    from gev_amd import _abi
+    rng = np.random.default_rng(1234 + variant)
+    engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, variant)
+    try:
+        for wl, n in [(16, 1024), (16, 1025), (32, 512), (32, 513), (17, 963), (24, 682), (33, 1000),
+                      (16, 1024 * 3), (32, 512 * 5)]:
+            fr, pay = _uniform_frames(wl, n, rng)
+            _encode_check(engine, fr, pay, f"v{variant} {wl}B x {n}")
+        lens = np.concatenate([rng.integers(0, 4, 200), [20000], rng.integers(0, 14, 700), [9000],
+                               rng.integers(0, 40, 400)])
+        payload = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+        hd = np.array([np.frombuffer(wo.Header(True, 0, 2, False, b"\0\0\0\0", int(L)).pack(), np.uint8)
+                       for L in lens])
+        _encode_check(engine, _records(hd, offs, lens), payload, f"v{variant} tiny runs")
+    finally:
+        engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, 0)
 
 
 def test_encode_empty_batch(engine):
