@@ -15,6 +15,7 @@ gev uses it), ``Connection`` (gev.Connection's websocket context keys),
 from __future__ import annotations
 
 import ctypes
+import atexit
 import weakref
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
@@ -133,6 +134,25 @@ class PinnedArena:
             _free(self._h)
 
 
+# Objects still alive at interpreter exit (e.g. held by a failed test's
+# traceback) are freed in dependency order -- protocols, then engines -- from
+# an atexit hook, while the HIP runtime is still up; the garbage collector's
+# order at shutdown is arbitrary, and a protocol freed after its engine would
+# synchronise a destroyed stream.
+_LIVE_PROTOCOLS: "weakref.WeakSet" = weakref.WeakSet()
+_LIVE_ENGINES: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def _close_live() -> None:
+    for p in list(_LIVE_PROTOCOLS):
+        p.close()
+    for e in list(_LIVE_ENGINES):
+        e.close()
+
+
+atexit.register(_close_live)
+
+
 class Engine:
     """One gevws_ctx (one per event loop / rank) on one GPU."""
 
@@ -144,6 +164,7 @@ class Engine:
         self._ctx = lib.gevws_ctx_create(device)
         if not self._ctx:
             raise RuntimeError("gevws_ctx_create failed")
+        _LIVE_ENGINES.add(self)
 
     def close(self):
         if self._ctx:
@@ -599,6 +620,7 @@ class Protocol:
     def __init__(self, engine: Engine, upgrader: Optional[Upgrader] = None):
         self.engine = engine
         self._p = lib.gevws_protocol_new(engine._ctx)
+        _LIVE_PROTOCOLS.add(self)
         self.upgrader = upgrader
         if upgrader is not None:
             lib.gevws_protocol_set_upgrader(self._p, upgrader._p)
@@ -606,6 +628,13 @@ class Protocol:
     def __del__(self, _free=lib.gevws_protocol_free):  # bound now: module globals are gone at exit
         if getattr(self, "_p", None):
             _free(self._p)
+            self._p = None
+
+    def close(self) -> None:
+        """Free the protocol (it synchronises its engine's stream, so it must go
+        before the engine: _close_live does protocols first at exit)."""
+        if getattr(self, "_p", None):
+            lib.gevws_protocol_free(self._p)
             self._p = None
 
     def unpacket(self, c: Connection, buffer: RingBuffer) -> Tuple[Optional[Header], Optional[bytes]]:
@@ -634,9 +663,15 @@ class Protocol:
             raise RuntimeError(f"unpacket_batch: {status_string(int(r))}")
         return int(r)
 
+    def set_zero_copy_max(self, nbytes: int) -> None:
+        """gevws_protocol_set_zero_copy_max: batched passes over at most
+        `nbytes` of input run on mapped host memory with no copies (0 = never)."""
+        lib.gevws_protocol_set_zero_copy_max(self._p, int(nbytes))
+
     def stats(self) -> dict:
         """Host-ingress counters (gevws_protocol_get_stats): device passes,
-        connections and bytes staged, UnPacket calls answered by the host gate."""
+        connections and bytes staged, UnPacket calls answered by the host gate,
+        passes run zero-copy."""
         s = _abi.ProtocolStats()
         lib.gevws_protocol_get_stats(self._p, ctypes.byref(s))
         return {k: int(getattr(s, k)) for k, _ in _abi.ProtocolStats._fields_}

@@ -87,9 +87,13 @@ class Summary(ctypes.Structure):
                 ("flags", ctypes.c_uint32), ("run_frames", ctypes.c_uint64), ("reserved", ctypes.c_uint64 * 2)]
 
 
+ZERO_COPY_MAX_DEFAULT = 256 * 1024  # GEVWS_ZERO_COPY_MAX_DEFAULT
+
+
 class ProtocolStats(ctypes.Structure):
     _fields_ = [("device_passes", ctypes.c_uint64), ("conns_staged", ctypes.c_uint64),
-                ("bytes_staged", ctypes.c_uint64), ("gated", ctypes.c_uint64)]
+                ("bytes_staged", ctypes.c_uint64), ("gated", ctypes.c_uint64),
+                ("zero_copy_passes", ctypes.c_uint64)]
 
 
 class HostConn(ctypes.Structure):
@@ -214,6 +218,7 @@ SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_uint32)]),
     "gevws_cipher": (None, [P, ctypes.c_uint64, P, ctypes.c_uint64]),
     "gevws_protocol_get_stats": (None, [P, ctypes.POINTER(ProtocolStats)]),
+    "gevws_protocol_set_zero_copy_max": (None, [P, ctypes.c_uint64]),
     "gevws_decode_host_batch": (ctypes.c_int64, [P, P, ctypes.c_uint32, P, ctypes.c_uint64, P, ctypes.c_uint64,
                                                  P, ctypes.POINTER(Summary)]),
 }

@@ -61,6 +61,18 @@ static void log_error_text(const char* what, const std::string& text) {
 // of them is released (no second host copy).  Thread-confined like the
 // protocol (one per event loop); the mutex only guards a release that happens
 // after the protocol is gone.
+// Page-locked host memory mapped into the device address space and coherent
+// (fine-grained: device accesses go to host memory, never stale in a device
+// cache), so a small pass's kernels can read the staged input and write their
+// results in place (Protocol::kZeroCopyMax).
+constexpr unsigned kHostFlags = hipHostMallocMapped | hipHostMallocCoherent;
+
+// The device address of mapped host memory, or nullptr.
+inline void* device_of(void* h) {
+  void* d = nullptr;
+  return hipHostGetDevicePointer(&d, h, 0) == hipSuccess ? d : nullptr;
+}
+
 class PinnedPool : public std::enable_shared_from_this<PinnedPool> {
  public:
   ~PinnedPool() {
@@ -81,7 +93,7 @@ class PinnedPool : public std::enable_shared_from_this<PinnedPool> {
     }
     if (!b.p) {
       const uint64_t want = std::max<uint64_t>(need + need / 2, 1 << 16);
-      if (hipHostMalloc((void**)&b.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+      if (hipHostMalloc((void**)&b.p, want, kHostFlags) != hipSuccess) return nullptr;
       b.cap = want;
     }
     std::weak_ptr<PinnedPool> pool = shared_from_this();
@@ -136,6 +148,8 @@ struct Connection {
 
 // ------------------------------------------------------------------ protocol
 class Protocol {
+  struct Staged;  // a pass in flight (below)
+
  public:
   explicit Protocol(gevws_ctx* ctx) : ctx_(ctx), pool_(std::make_shared<PinnedPool>()) {}
   void SetUpgrader(const Upgrader* u) { upgrader_ = u; }
@@ -216,15 +230,22 @@ class Protocol {
     const uint32_t m = (uint32_t)sel.size();
     DeviceScope scope(gevws_ctx_device(ctx_));
     Staged sg;
-    int64_t r = StageDecode(segs.data(), m, &sg);
+    int64_t r = StageDecode(segs.data(), m, &sg, true);
     if (r < 0) return r;
+    std::shared_ptr<uint8_t> arena;
+    if (sg.zc) {
+      r = Finish(&sg);
+      if (r < 0) return r;
+      arena = sg.arena;
+      return Deliver(conns, rings, sel, sg, arena);
+    }
     // frames + payload land in pinned memory with the summary: one
     // synchronisation for a pass whose output fits the first estimate
     hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
     const uint64_t est_f = std::min<uint64_t>(sg.max_frames, sg.total / 48 + 2ull * m + 16);
     const uint64_t est_p = std::min<uint64_t>(sg.payload_cap, sg.total + 16 * est_f + 16);
     if (!grow_host(&h_out_, &h_out_cap_, est_f * sizeof(gevws_frame))) return fail();
-    std::shared_ptr<uint8_t> arena = pool_->Acquire(est_p);
+    arena = pool_->Acquire(est_p);
     if (!arena) return fail();
     if (hipMemcpyAsync(h_out_, d_frames_, est_f * sizeof(gevws_frame), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(arena.get(), d_payload_, est_p, hipMemcpyDeviceToHost, st) != hipSuccess)
@@ -242,6 +263,15 @@ class Protocol {
           hipStreamSynchronize(st) != hipSuccess)
         return fail();
     }
+    return Deliver(conns, rings, sel, sg, arena);
+  }
+
+  // Hands a finished pass's frames to their connections in stream order and
+  // carries each connection's completeness gate to the next pass.
+  int64_t Deliver(Connection* const* conns, RingBuffer* const* rings, const std::vector<uint32_t>& sel,
+                  const Staged& sg, const std::shared_ptr<uint8_t>& arena) {
+    const uint32_t m = (uint32_t)sel.size();
+    const gevws_summary& sum = sg.sum;
     const gevws_conn_out* cout = reinterpret_cast<const gevws_conn_out*>(h_res_ + sizeof(gevws_summary));
     const gevws_frame* fr = reinterpret_cast<const gevws_frame*>(h_out_);
     const uint8_t* hin = h_in_ + sg.coff;
@@ -306,6 +336,7 @@ class Protocol {
   }
 
   void GetStats(gevws_protocol_stats* out) const { *out = stats_; }
+  void SetZeroCopyMax(uint64_t bytes) { zc_max_ = bytes; }
 
  private:
   struct DeviceScope {
@@ -357,6 +388,9 @@ class Protocol {
     std::vector<gevws_conn_in> cin;
     uint64_t coff = 0, total = 0, res = 0, max_frames = 0, payload_cap = 0;
     bool retried = false;  // Finish re-ran the pass: copies enqueued before it are stale
+    bool zc = false;       // zero-copy pass: kernels on the pinned buffers themselves
+    std::shared_ptr<uint8_t> arena;  // zero-copy: the payload arena the kernels write
+    uint64_t arena_cap = 0;
     gevws_summary sum{};
   };
 
@@ -364,7 +398,7 @@ class Protocol {
   // table, ONE H2D, enqueue the decode on the context's stream and the D2H of
   // {summary, conn_out} into pinned h_res_ (no synchronisation yet: the caller
   // adds its own copies, then Finish waits).
-  int64_t StageDecode(const gevws_host_conn* segs, uint32_t m, Staged* sg) {
+  int64_t StageDecode(const gevws_host_conn* segs, uint32_t m, Staged* sg, bool allow_zc = false) {
     uint64_t total = 0;
     for (uint32_t j = 0; j < m; ++j) total += segs[j].n0 + segs[j].n1;
     sg->cin.resize(m);
@@ -389,9 +423,18 @@ class Protocol {
     sg->max_frames = std::min<uint64_t>(total / 2 + 1, 0xFFFFFFFFull);
     sg->payload_cap = total + 16 * std::min<uint64_t>(sg->max_frames, total / 64 + 64) + 64;
     hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
-    if (!grow_dev(&d_in_, &d_in_cap_, stage) || !grow_dev(&d_res_, &d_res_cap_, sg->res) ||
-        hipMemcpyAsync(d_in_, h_in_, stage, hipMemcpyHostToDevice, st) != hipSuccess)
+    sg->zc = allow_zc && total <= zc_max_;
+    if (sg->zc) {
+      // small pass: no copies -- the kernels read the staged bytes and write
+      // records, payload and results into mapped host memory (a pass is then
+      // its launches and one synchronisation, no H2D / D2H on the way)
+      sg->max_frames = std::min<uint64_t>(sg->max_frames, total / 48 + 2ull * m + 16);
+      sg->payload_cap = std::min<uint64_t>(sg->payload_cap, total + 16 * sg->max_frames + 16);
+      ++stats_.zero_copy_passes;
+    } else if (!grow_dev(&d_in_, &d_in_cap_, stage) || !grow_dev(&d_res_, &d_res_cap_, sg->res) ||
+               hipMemcpyAsync(d_in_, h_in_, stage, hipMemcpyHostToDevice, st) != hipSuccess) {
       return fail();
+    }
     ++stats_.device_passes;
     stats_.conns_staged += m;
     stats_.bytes_staged += stage;
@@ -400,6 +443,23 @@ class Protocol {
 
   int64_t Launch(Staged* sg) {
     hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+    if (sg->zc) {
+      const uint32_t m = (uint32_t)sg->cin.size();
+      if (!grow_host(&h_out_, &h_out_cap_, std::max<uint64_t>(sg->max_frames, 1) * sizeof(gevws_frame)))
+        return fail();
+      if (!sg->arena || sg->arena_cap < sg->payload_cap + 16) {
+        sg->arena = pool_->Acquire(sg->payload_cap + 16);
+        sg->arena_cap = sg->payload_cap + 16;
+      }
+      uint8_t* din = (uint8_t*)device_of(h_in_);
+      uint8_t* dres = (uint8_t*)device_of(h_res_);
+      void* dfr = sg->arena ? device_of(h_out_) : nullptr;
+      void* dpay = sg->arena ? device_of(sg->arena.get()) : nullptr;
+      if (!din || !dres || !dfr || !dpay) return fail();
+      return gevws_decode_batch_async(ctx_, st, din + sg->coff, sg->total, (gevws_conn_in*)din, m,
+                                      (gevws_frame*)dfr, sg->max_frames, (uint8_t*)dpay, sg->payload_cap,
+                                      (gevws_conn_out*)(dres + sizeof(gevws_summary)), (gevws_summary*)dres);
+    }
     if (!grow_dev(&d_frames_, &d_frames_cap_, sg->max_frames * sizeof(gevws_frame)) ||
         !grow_dev(&d_payload_, &d_payload_cap_, sg->payload_cap + 16))
       return fail();
@@ -441,7 +501,7 @@ class Protocol {
     if (*p) (void)hipHostFree(*p);
     *p = nullptr;
     uint64_t want = std::max<uint64_t>(need + need / 2, 1 << 16);
-    if (hipHostMalloc((void**)p, want, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void**)p, want, kHostFlags) != hipSuccess) {
       *cap = 0;
       return false;
     }
@@ -476,6 +536,7 @@ class Protocol {
   void *d_in_ = nullptr, *d_res_ = nullptr, *d_frames_ = nullptr, *d_payload_ = nullptr;
   uint64_t d_in_cap_ = 0, d_res_cap_ = 0, d_frames_cap_ = 0, d_payload_cap_ = 0;
   uint64_t epoch_ = 0;
+  uint64_t zc_max_ = GEVWS_ZERO_COPY_MAX_DEFAULT;
   gevws_protocol_stats stats_{};
 };
 
@@ -537,6 +598,10 @@ void gevws_protocol_get_stats(const gevws_protocol* p, gevws_protocol_stats* out
     return;
   }
   p->GetStats(out);
+}
+
+void gevws_protocol_set_zero_copy_max(gevws_protocol* p, uint64_t bytes) {
+  if (p) p->SetZeroCopyMax(bytes);
 }
 
 int64_t gevws_decode_host_batch(gevws_protocol* p, const gevws_host_conn* conns, uint32_t n,

@@ -3,7 +3,9 @@
 // Server/client skeleton: ws_loopback.hpp.  Per loop iteration ONE device pass
 // over every readable upgraded connection (gevws_protocol_unpacket_batch:
 // PeekAll segments gathered into pinned staging, H2D, decode, D2H), then
-// websocket.(*Protocol).UnPacket per connection hands the frames out.
+// websocket.(*Protocol).UnPacket per connection hands the frames out.  Small
+// passes run zero-copy on mapped host memory (gevws_protocol_set_zero_copy_max;
+// env GEVWS_LB_ZERO_COPY_MAX overrides the default for an A/B).
 #include "ws_loopback.hpp"
 
 namespace {
@@ -22,6 +24,8 @@ struct DeviceDecoder {
       exit(2);
     }
     p = gevws_protocol_new(ctx);
+    if (const char* zc = getenv("GEVWS_LB_ZERO_COPY_MAX"))  // A/B: 0 = copy every pass in and out
+      gevws_protocol_set_zero_copy_max(p, strtoull(zc, nullptr, 10));
     u = gevws_upgrader_new();  // &ws.Upgrader{} as benchmarks/websocket/server.go:52
     gevws_protocol_set_upgrader(p, u);
   }

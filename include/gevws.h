@@ -378,16 +378,27 @@ int64_t gevws_protocol_unpacket_batch(gevws_protocol *p, gevws_conn *const *conn
                                       gevws_ring *const *rings, uint32_t n);
 
 /* Counters of a protocol's host ingress (not on the reference path):
- * device passes run, connections staged into them, bytes staged (H2D), and
- * UnPacket calls answered NEED_MORE by the host-side gate without a device pass
- * (the first frame's h + L is not buffered yet, protocol.go:47). */
+ * device passes run, connections staged into them, bytes staged, UnPacket
+ * calls answered NEED_MORE by the host-side gate without a device pass (the
+ * first frame's h + L is not buffered yet, protocol.go:47), and the passes run
+ * zero-copy (below). */
 typedef struct gevws_protocol_stats {
     uint64_t device_passes;
     uint64_t conns_staged;
     uint64_t bytes_staged;
     uint64_t gated;
+    uint64_t zero_copy_passes;
 } gevws_protocol_stats;
 void gevws_protocol_get_stats(const gevws_protocol *p, gevws_protocol_stats *out);
+
+/* Batched passes over at most `bytes` of buffered input (default
+ * GEVWS_ZERO_COPY_MAX_DEFAULT; 0 = never) run zero-copy: the kernels read the
+ * pinned staging block and write records, payload and results into mapped
+ * pinned host memory, so the pass is its launches and one synchronisation
+ * with no H2D / D2H copies (a small pass is latency, not bytes).  Larger
+ * passes copy in and out (DMA at the PCIe rate). */
+#define GEVWS_ZERO_COPY_MAX_DEFAULT (256u * 1024u)
+void gevws_protocol_set_zero_copy_max(gevws_protocol *p, uint64_t bytes);
 
 /* One connection's buffered bytes in host memory, as ringbuffer.PeekAll()
  * returns them (first, end) -- e.g. two Go slices passed through cgo. */

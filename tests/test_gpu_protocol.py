@@ -57,9 +57,13 @@ def test_echo_over_ring_buffers(engine):
         assert rings[i].length() == 0
 
 
-def test_batched_driver_matches_oracle(engine):
+@pytest.mark.parametrize("zero_copy_max", [0, 1 << 30])
+def test_batched_driver_matches_oracle(engine, zero_copy_max):
+    """zero_copy_max 0: the pass copies in and out; 1 GiB: the kernels run on
+    the mapped pinned staging and write into mapped host memory."""
     rng = np.random.default_rng(22)
     proto = gev_amd.Protocol(engine)
+    proto.set_zero_copy_max(zero_copy_max)
     streams = []
     for _ in range(64):
         s = b""
@@ -92,6 +96,25 @@ def test_batched_driver_matches_oracle(engine):
         assert proto.unpacket(c, r) == (None, None)
         assert proto.last_status == gev_amd.NEED_MORE
         assert r.length() == len(s) - want.consumed
+    st = proto.stats()
+    assert st["zero_copy_passes"] == (st["device_passes"] if zero_copy_max else 0), st
+
+
+def test_zero_copy_capacity_retry(engine):
+    """A zero-copy pass sizes its host outputs from an estimate (~1 frame per
+    48 input bytes); a run of empty frames (6 bytes each) exceeds it, the pass
+    reports GEVWS_ERR_CAPACITY and is re-run once with the exact sizes."""
+    proto = gev_amd.Protocol(engine)
+    c, r = gev_amd.Connection(), gev_amd.RingBuffer(1 << 16)
+    w = b"".join(wo.encode_frame(b"", 2, True, 0, True, bytes([i & 255, 1, 2, 3])) for i in range(3000))
+    tail = bytes([0x82, 0x7F, 0, 0, 0])  # 5 bytes of a 64-bit-length header: (nil, nil), read.go:20-23
+    w += wo.encode_frame(b"end", 1, True, 0, True, b"\x09\x08\x07\x06") + tail
+    r.write(w)
+    got = gev_amd.handler_protocol(proto, c, r, lambda cc, h, d: (h.opcode, d))
+    assert got == [(2, b"")] * 3000 + [(1, b"end")]
+    st = proto.stats()
+    assert st["device_passes"] == 1 and st["zero_copy_passes"] == 1, st
+    assert r.length() == len(tail)
 
 
 def test_not_upgraded_and_poison(engine):
