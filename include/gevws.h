@@ -212,7 +212,8 @@ typedef struct gevws_out_frame {
  * handlerProtocol appends to its send buffer, connection.go:208-218).
  * d_out_off[f] receives frame f's wire offset; d_summary->payload_bytes the
  * wire total, ->payload_len the payload total, ->status GEVWS_ERR_CAPACITY if
- * the total exceeds out_cap (nothing written).  Payload bytes are read as
+ * the total exceeds out_cap (nothing written to d_out; d_out_off[f] then holds
+ * frame f's wire size h + L).  Payload bytes are read as
  * 16-byte vectors: d_payload needs 16 readable bytes past its last payload
  * byte (a decode's payload arena has them).  Device pointers; enqueued on
  * `stream`. */
