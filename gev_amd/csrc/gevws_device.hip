@@ -128,6 +128,15 @@ __device__ __forceinline__ void load_window(const uint8_t* p, uint64_t& lo, uint
   hi = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
 }
 
+typedef unsigned __int128 u128;
+
+__device__ __forceinline__ u128 u128_of(u32x4 v) {
+  return (u128)v[0] | ((u128)v[1] << 32) | ((u128)v[2] << 64) | ((u128)v[3] << 96);
+}
+__device__ __forceinline__ u32x4 u32x4_of(u128 x) {
+  return u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+}
+
 // Wave-level (64 lanes) inclusive scan of a u64.
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
   const int lane = threadIdx.x & 63;
@@ -563,6 +572,156 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
     if (threadIdx.x == 0) {
       if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + k, s);
       else blk[(uint64_t)blockIdx.x * kDecFields + k] = s;
+    }
+  }
+  if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
+}
+
+// ------------------------------------------------------------------ 1a'. walk (count), buffered
+// k_walk_count's chain costs one memory round trip per frame, and a wave
+// waits for its slowest lane at every step, so a C4-sized walk takes about
+// (longest chain) x (loaded latency) -- 1 132-1 204 frames x ~1.3 us.  Half of
+// C4's frames are under 128 bytes, so the next header is often within a few
+// hundred bytes of the current one.  Here each lane reads WB bytes of its
+// stream at once into its own LDS row and walks every frame whose 16-byte
+// header window lies inside that row (an inner loop of LDS reads and parses,
+// no memory wait); only then do the lanes that ran out of row reload, all in
+// the same round trip.  A wave's round trips per chain are the row reloads of
+// its worst lane instead of its frames.  Entries, per-connection results and
+// block partials are exactly k_walk_count's (D = 0).
+template <int WB, bool GRP>
+__global__ __launch_bounds__(kCountBlock) void k_walk_buf(const uint8_t* __restrict__ in,
+                                                          const gevws_conn_in* __restrict__ conns, uint32_t n,
+                                                          gevws_conn_out* __restrict__ cout,
+                                                          uint64_t* __restrict__ blk,
+                                                          WalkEntry* __restrict__ entries, uint64_t n_entries,
+                                                          uint32_t gshift, uint32_t cpb, uint64_t in_bytes,
+                                                          uint32_t* __restrict__ done, uint64_t max_frames,
+                                                          uint64_t payload_cap, gevws_summary* __restrict__ sum) {
+  constexpr int NC = WB / 16;
+  static_assert(WB % 16 == 0 && NC >= 2, "whole 16-byte chunks, at least two");
+  __shared__ u32x4 s_row[kCountBlock][NC + 1];  // chunk NC: read (shift 0, unused) by a window at the row's end
+  const uint32_t c = blockIdx.x * cpb + threadIdx.x;
+  uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0, lastf = ~0ull;
+  if (threadIdx.x < cpb && c < n) {
+    gevws_conn_in ci = conns[c];
+    if (out_of_order(conns, c, ci)) err = 1ull << 32;  // as k_walk_count
+    int32_t st = GEVWS_OK;
+    if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
+      ci.off = 0;
+      ci.len = 0;
+      st = GEVWS_ERR_INVALID;
+      err += 1;
+    }
+    const uint8_t* s = in + ci.off;
+    u32x4* row = s_row[threadIdx.x];
+    uint64_t pos = 0, wb = 0;  // row[k] = stream bytes [wb + 16k, wb + 16k + 16)
+    uint64_t ebase = 0, ecap = 0;
+    bool rec = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
+    WalkEntry* sink = entries + n_entries + c;
+    WalkEntry g0 = {0, 0, 0, 0}, g1 = g0, g2 = g0;
+    auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
+      rec = rec && nf < ecap;
+      WalkEntry e;
+      e.pos = (uint32_t)p;
+      e.mask = key;
+      e.len = (uint32_t)L;
+      e.meta = meta;
+      if constexpr (GRP) {
+        if (rec && (nf & 3) == 3) {
+          WalkEntry* g = entries + ebase + (nf - 3);
+          g[0] = g0;
+          g[1] = g1;
+          g[2] = g2;
+          g[3] = e;
+        }
+        g0 = g1;
+        g1 = g2;
+        g2 = e;
+      } else if (rec) {
+        entries[ebase + nf] = e;
+      }
+      ++nf;
+      pb += round16(L);
+      pl += L;
+      const uint64_t f = (uint64_t)(meta >> 16) + L;
+      same += f == lastf;
+      lastf = f;
+    };
+    // the row at stream offset p & ~15: chunks starting past the stream end
+    // are loaded from its end instead (only bytes < len + 16 are ever parsed,
+    // and 16 bytes at any offset <= len stay inside GEVWS_IN_PAD)
+    auto reload = [&](uint64_t p) {
+      wb = p & ~15ull;
+      u32x4 v[NC];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        const uint64_t a = wb + 16ull * k;
+        v[k] = ld16u(s + (a <= ci.len ? a : ci.len));
+      }
+#pragma unroll
+      for (int k = 0; k < NC; ++k) row[k] = v[k];
+    };
+    reload(0);
+    bool fin = false;
+    for (;;) {
+      while (pos + 16 <= wb + WB) {  // the frame's 16-byte window is in the row
+        const uint32_t o = (uint32_t)(pos - wb), k = o >> 4, r = o & 15u;
+        const u128 x = (u128_of(row[k]) >> (8 * r)) | (r ? u128_of(row[k + 1]) << (128 - 8 * r) : (u128)0);
+        const uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);
+        const uint32_t b1 = (uint32_t)(lo >> 8) & 0xffu;
+        const uint32_t masked = b1 >> 7, len7 = b1 & 0x7fu;
+        const bool e16 = len7 == 126, e64 = len7 == 127;
+        const uint32_t hlen = 2 + (e64 ? 8u : (e16 ? 2u : 0u)) + 4 * masked;
+        const uint64_t L64 = __builtin_bswap64((lo >> 16) | (hi << 48));
+        const uint64_t L16 = (((lo >> 16) & 0xff) << 8) | ((lo >> 24) & 0xff);
+        const uint64_t L = e64 ? L64 : (e16 ? L16 : (uint64_t)len7);
+        const uint64_t avail = ci.len - pos;
+        const bool have_hdr = avail >= 6 && avail >= hlen;  // read.go:20-23, U1
+        const bool msb = e64 && (L64 >> 63);                 // read.go:71-73
+        if (!have_hdr || msb || avail - hlen < L) {          // protocol.go:47 gate
+          if (have_hdr && msb) { st = GEVWS_ERR_LEN_MSB; err += 1; }
+          fin = true;
+          break;
+        }
+        const uint32_t key = (e64 ? (uint32_t)(hi >> 16) : (e16 ? (uint32_t)(lo >> 32) : (uint32_t)(lo >> 16))) &
+                             (0u - masked);
+        put_entry(pos, key, L, ((uint32_t)lo & 0xffu) | (masked << 8) | (hlen << 16));
+        pos += hlen + L;
+      }
+      if (fin) break;
+      reload(pos);
+    }
+    (void)sink;
+    if (GRP && rec) {  // the last nf % 4 entries
+      const uint32_t r = (uint32_t)(nf & 3);
+      WalkEntry* g = entries + ebase + (nf - r);
+      if (r == 3) {
+        g[0] = g0;
+        g[1] = g1;
+        g[2] = g2;
+      } else if (r == 2) {
+        g[0] = g1;
+        g[1] = g2;
+      } else if (r == 1) {
+        g[0] = g2;
+      }
+    }
+    gevws_conn_out o;
+    o.first_frame = rec ? 1 : 0;
+    o.consumed = pos;
+    o.payload_base = pb;
+    o.nframes = (uint32_t)nf;
+    o.status = st;
+    cout[c] = o;
+  }
+  const uint64_t vals[kDecFields] = {nf, pb, pl, err, same};
+#pragma unroll
+  for (int k = 0; k < kDecFields; ++k) {
+    const uint64_t sm = wave_sum(vals[k]);
+    if (threadIdx.x == 0) {
+      if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + k, sm);
+      else blk[(uint64_t)blockIdx.x * kDecFields + k] = sm;
     }
   }
   if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
@@ -1861,14 +2020,6 @@ __device__ __forceinline__ uint8_t enc_byte_global(const gevws_out_frame* __rest
 }
 
 constexpr int kEncWinFrames = 1024;
-typedef unsigned __int128 u128;
-
-__device__ __forceinline__ u128 u128_of(u32x4 v) {
-  return (u128)v[0] | ((u128)v[1] << 32) | ((u128)v[2] << 64) | ((u128)v[3] << 96);
-}
-__device__ __forceinline__ u32x4 u32x4_of(u128 x) {
-  return u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
-}
 // bytes [k0, k1) of a 16-byte lane (0 <= k0 < k1 <= 16)
 __device__ __forceinline__ u128 byte_mask(int k0, int k1) {
   const u128 hi = (k1 >= 16) ? ~(u128)0 : (((u128)1 << (8 * k1)) - 1);
@@ -2687,6 +2838,8 @@ const char* const kWalkVariants[] = {
     "one wave per connection: LDS ring of 2 x 2 KiB + ballot over equal-size runs",
     "one lane per connection, plain chain walk, each header load also touches the next 128-byte line",
     "one lane per connection, plain chain walk, each header load also touches the next two 128-byte lines",
+    "one lane per connection, 128-byte LDS row per lane: every header inside it walked before the next load",
+    "one lane per connection, 256-byte LDS row per lane: every header inside it walked before the next load",
 };
 constexpr int kNumWalkVariants = sizeof(kWalkVariants) / sizeof(kWalkVariants[0]);
 
@@ -2902,8 +3055,13 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     // grouped entry stores pay off when the walk is bound by its line traffic
     // (many concurrent chains), not by chain latency (few)
     const bool many = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
-    const bool grp = wv == 4 || ((wv == 0 || wv == 1 || wv == 5 || wv == 8 || wv == 9) && many);
-    if (wv == 8 || wv == 9) {
+    const bool grp = wv == 4 || ((wv == 0 || wv == 1 || wv == 5 || wv == 8 || wv == 9 || wv >= 10) && many);
+    if (wv == 10 || wv == 11) {
+      auto kb = wv == 10 ? (grp ? k_walk_buf<128, true> : k_walk_buf<128, false>)
+                         : (grp ? k_walk_buf<256, true> : k_walk_buf<256, false>);
+      kb<<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes,
+                                       done, max_frames, payload_cap, d_summary);
+    } else if (wv == 8 || wv == 9) {
       if (grp && wv == 8)
         k_walk_count<0, true, false, 1><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
                                                                      entries, ne, gshift, cpb, in_bytes, done, max_frames,
