@@ -1528,7 +1528,25 @@ struct WinLds {
   uint32_t* key;
 };
 
-template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles>
+// For each of a lane's WT window chunks at once: the largest frame j < F with
+// s_start[j] <= rel[u] (s_start is non-decreasing, s_start[0] <= every rel).
+// Binary lifting with a wave-uniform step count, the WT LDS reads of a step
+// issued together: the per-chunk bisection loops ran one after another, WT x
+// log2(F) dependent LDS round trips per window instead of log2(F).
+template <int WT, typename T>
+__device__ __forceinline__ void window_search(const T* s_start, uint32_t F, const T (&rel)[WT], uint32_t (&lo)[WT]) {
+#pragma unroll
+  for (int u = 0; u < WT; ++u) lo[u] = 0;
+  for (uint32_t step = F > 1 ? 1u << (31 - __builtin_clz(F - 1)) : 0u; step; step >>= 1) {
+    T st[WT];
+#pragma unroll
+    for (int u = 0; u < WT; ++u) st[u] = lo[u] + step < F ? s_start[lo[u] + step] : rel[u] + 1;
+#pragma unroll
+    for (int u = 0; u < WT; ++u) lo[u] += st[u] <= rel[u] ? step : 0u;
+  }
+}
+
+template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles, bool IS = false>
 __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
@@ -1591,6 +1609,12 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
       u32x4 v[WT];
       uint32_t key[WT];
       int32_t rem[WT];
+      uint32_t relv[WT], lov[WT];
+      if constexpr (IS) {
+#pragma unroll
+        for (int u = 0; u < WT; ++u) relv[u] = (uint32_t)(u * kTile) + lane_off;
+        window_search<WT>(s_start, (uint32_t)F, relv, lov);
+      }
 #pragma unroll
       for (int u = 0; u < WT; ++u) {
         const uint32_t rel = (uint32_t)(u * kTile) + lane_off;
@@ -1600,9 +1624,13 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
         v[u] = u32x4{0, 0, 0, 0};
         if ((uint64_t)u < wt && p < total) {
           uint32_t lo = 0, hi = (uint32_t)F - 1;
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+          if constexpr (IS) {
+            lo = lov[u];
+          } else {
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi + 1) >> 1;
+              if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+            }
           }
           rem[u] = s_lend[lo] - (int32_t)rel;
           key[u] = s_key[lo];
@@ -1690,7 +1718,7 @@ __device__ __forceinline__ WinRec load_rec(const gevws_frame* __restrict__ frame
 // FT (measurement switch): false re-creates the round-1 kernel whose fill
 // addresses were spilled (threadIdx.x used directly).
 // SP: streaming steps as software-pipelined runs (stream_run, U / 2 tiles per step).
-template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false>
+template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false, bool IS = false>
 __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
@@ -1813,6 +1841,14 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
     u32x4 v[WT];
     uint32_t key[WT];
     int32_t rem[WT];
+    uint32_t relv[WT], lov[WT];
+    if constexpr (IS) {
+#pragma unroll
+      for (int u = 0; u < WT; ++u)
+        relv[u] = WC ? (threadIdx.x >> 6) * (uint32_t)(WT * 1024) + (uint32_t)u * 1024 + (threadIdx.x & 63) * 16
+                     : (uint32_t)(u * kTile) + lane_off;
+      window_search<WT>(s_start, (uint32_t)F, relv, lov);
+    }
 #pragma unroll
     for (int u = 0; u < WT; ++u) {
       const uint32_t rel = WC ? (threadIdx.x >> 6) * (uint32_t)(WT * 1024) + (uint32_t)u * 1024 + (threadIdx.x & 63) * 16
@@ -1823,9 +1859,13 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
       v[u] = u32x4{0, 0, 0, 0};
       if ((WC ? (uint64_t)rel < wt * kTile : (uint64_t)u < wt) && p < total) {
         uint32_t lo = 0, hi = (uint32_t)F - 1;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi + 1) >> 1;
-          if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+        if constexpr (IS) {
+          lo = lov[u];
+        } else {
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+          }
         }
         rem[u] = s_lend[lo] - (int32_t)rel;
         key[u] = s_key[lo];
@@ -1880,6 +1920,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
 // v3-4 -5 % on C1-shaped and -2.4 % on C2 batches, v4-8 -3 % on C4 and -2 % on
 // C5, equal on C3; profiles/r02_ab2.log).  One kernel, one LDS table, the
 // choice is a uniform branch on the summary the walk wrote.
+template <bool IS>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
     const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
@@ -1890,9 +1931,9 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   static_assert(kWinFrames == kWin4Frames, "one LDS table for both bodies");
   const WinLds L{s_start, s_lend, s_delta, s_key};
   if (2 * sum->run_frames >= sum->frames)  // frames the size of their predecessor on the connection
-    unmask_v3_body<16, false, true, 2>(in, frames, tile_first, sum, out, big_grid, L);
+    unmask_v3_body<16, false, true, 2, kWinTiles, IS>(in, frames, tile_first, sum, out, big_grid, L);
   else
-    unmask_v4_body<16, 8, true>(in, frames, tile_first, sum, out, big_grid, L);
+    unmask_v4_body<16, 8, true, false, true, false, IS>(in, frames, tile_first, sum, out, big_grid, L);
 }
 
 // ------------------------------------------------------------------ outbound encode (§8f row 1)
@@ -2802,7 +2843,7 @@ struct UnmaskVariant {
 // Variant 0 is the default; the others are kept for A/B measurement
 // (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 const UnmaskVariant kUnmaskVariants[] = {
-    {k_unmask_auto, 16,
+    {k_unmask_auto<false>, 16,
      "auto: v3 4-tile windows for batches of equal-size frames, v4 pipelined 8-tile windows otherwise (summary "
      "statistics of the walk)"},
     {k_unmask_v4<16, 8, true>, 16,
@@ -2821,6 +2862,9 @@ const UnmaskVariant kUnmaskVariants[] = {
      "v4 with software-pipelined streaming runs (8-tile steps, next step's loads before this step's stores)"},
     {k_unmask_v4<8, 8, true, false, true, true>, 8,
      "v4, pipelined streaming runs of 4-tile steps (streams from 8 tiles inside a frame)"},
+    {k_unmask_auto<true>, 16,
+     "auto with the window chunks' frame searches interleaved (binary lifting, one LDS round trip per step for "
+     "all chunks of a lane)"},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
