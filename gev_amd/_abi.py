@@ -47,6 +47,7 @@ TUNE_ENCODE_VARIANT = 3
 TUNE_WALK_VARIANT = 4
 TUNE_SPAN_CONNS_PER_CU = 5
 TUNE_EMIT_VARIANT = 6
+TUNE_SMALL_BATCH = 7  # one-launch decode up to this many input bytes (0 = never)
 
 IN_PAD = 64
 SUMMARY_UNORDERED = 1  # summary.flags: connection table not in increasing input order

@@ -69,6 +69,17 @@ __device__ __forceinline__ u32x4 ld16u(const uint8_t* p) {
 
 __device__ __forceinline__ uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
+__device__ __forceinline__ u32x4 keep_bytes(u32x4 x, int64_t rem) {
+  // zero bytes at positions >= rem (rem in 1..15): Go's make() zero-fill of the pad
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t valid = rem - 4 * j;
+    const uint32_t m = valid >= 4 ? 0xffffffffu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
+    x[j] &= m;
+  }
+  return x;
+}
+
 // 32-bit field starting at byte `off` (0..12) of the 16-byte window lo|hi.
 __device__ __forceinline__ uint32_t window32(uint64_t lo, uint64_t hi, uint32_t off) {
   const uint32_t sh = off * 8;
@@ -1253,6 +1264,143 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
   }
 }
 
+// ------------------------------------------------------------------ 3c. small batches, one launch
+// A live server's pass is small (C1: ~100 connections x 136 B per loop
+// iteration) and pays per launch, not per byte: four kernels cost ~5 us each
+// of GPU time whatever their size (profiles/r02_loopback_*), plus their host
+// launch costs.  Batches of at most kSmallConns connections and
+// GEVWS_TUNE_SMALL_BATCH bytes (default kSmallBytes) run the whole decode in
+// ONE workgroup: each lane walks its connection (k_walk_count's rules), a
+// block scan gives the bases and the summary, each lane re-walks its chain
+// writing the records and unmasking payloads of up to kSmallLaneBytes itself
+// (all its chunk loads at once), and the workgroup unmasks the larger ones
+// together.  Output identical to the multi-kernel decode.
+constexpr uint32_t kSmallConns = 256;
+constexpr uint64_t kSmallBytes = 64 * 1024;
+constexpr uint32_t kSmallLaneBytes = 256;
+constexpr uint32_t kSmallBig = kSmallBytes / kSmallLaneBytes;  // larger payloads fit in the input at most this often
+
+__global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __restrict__ in, uint64_t in_bytes,
+                                                              const gevws_conn_in* __restrict__ conns, uint32_t n,
+                                                              gevws_frame* __restrict__ frames, uint64_t max_frames,
+                                                              uint8_t* __restrict__ payload, uint64_t payload_cap,
+                                                              gevws_conn_out* __restrict__ cout,
+                                                              gevws_summary* __restrict__ sum) {
+  __shared__ uint64_t s_big[kSmallBig][3];  // {src_off, payload_off, length} of the larger payloads
+  __shared__ uint32_t s_bkey[kSmallBig];
+  __shared__ uint32_t s_nbig;
+  const uint32_t c = threadIdx.x;
+  if (c == 0) s_nbig = 0;
+  gevws_conn_in ci{0, 0};
+  uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0, lastf = ~0ull, pos = 0;
+  int32_t st = GEVWS_OK;
+  if (c < n) {
+    ci = conns[c];
+    if (out_of_order(conns, c, ci)) err = 1ull << 32;  // informational, as k_walk_count
+    if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
+      ci.off = 0;
+      ci.len = 0;
+      st = GEVWS_ERR_INVALID;
+      err += 1;
+    }
+    const uint8_t* s = in + ci.off;
+    for (;;) {  // read.go:19-84 + the protocol.go:47 gate, frame after frame
+      uint64_t lo, hi;
+      load_window(s + pos, lo, hi);
+      DevHdr h;
+      const int r = parse_header(lo, hi, ci.len - pos, h);
+      if (r == GEVWS_ERR_LEN_MSB) {
+        st = GEVWS_ERR_LEN_MSB;
+        err += 1;
+      }
+      if (r != GEVWS_OK || ci.len - pos - h.hlen < h.length) break;
+      ++nf;
+      pb += round16(h.length);
+      pl += h.length;
+      const uint64_t f = h.hlen + h.length;
+      same += f == lastf;
+      lastf = f;
+      pos += f;
+    }
+  }
+  const uint64_t v[kDecFields] = {nf, pb, pl, err, same};
+  uint64_t ex[kDecFields], tot[kDecFields];
+  block_excl_scan<kSmallConns, kDecFields>(v, ex, tot);
+  const bool ok = tot[0] <= max_frames && tot[1] <= payload_cap;
+  if (c == 0) {
+    gevws_summary sm;
+    memset(&sm, 0, sizeof(sm));
+    sm.frames = tot[0];
+    sm.payload_bytes = tot[1];
+    sm.payload_len = tot[2];
+    sm.errors = tot[3] & 0xffffffffull;
+    sm.flags = (tot[3] >> 32) ? GEVWS_SUMMARY_UNORDERED : 0u;
+    sm.run_frames = tot[4];
+    sm.status = ok ? GEVWS_OK : GEVWS_ERR_CAPACITY;
+    *sum = sm;
+  }
+  if (!ok) return;  // capacity error: nothing written (uniform)
+  if (c < n) {
+    gevws_conn_out o;
+    o.first_frame = ex[0];
+    o.consumed = pos;
+    o.payload_base = ex[1];
+    o.nframes = (uint32_t)nf;
+    o.status = st;
+    cout[c] = o;
+    // records + the lane's own payloads
+    const uint8_t* s = in + ci.off;
+    uint64_t q = 0, poff = ex[1];
+    for (uint64_t k = 0; k < nf; ++k) {
+      uint64_t lo, hi;
+      load_window(s + q, lo, hi);
+      DevHdr h;
+      parse_header(lo, hi, ci.len - q, h);  // succeeded in the walk above
+      const uint64_t src = ci.off + q + h.hlen;
+      const uint32_t flags = (h.b0 >> 7) | (((h.b0 & 0x70) >> 4) << 8) | ((h.b0 & 0x0f) << 16) | ((h.masked & 1) << 24);
+      u32x4* rp = reinterpret_cast<u32x4*>(frames + ex[0] + k);
+      rp[0] = u32x4{flags, h.mask, (uint32_t)h.length, (uint32_t)(h.length >> 32)};
+      rp[1] = u32x4{(uint32_t)poff, (uint32_t)(poff >> 32), (uint32_t)src, (uint32_t)(src >> 32)};
+      if (h.length <= kSmallLaneBytes) {
+        constexpr int NCH = kSmallLaneBytes / 16;
+        const uint32_t nch = (uint32_t)((h.length + 15) >> 4);
+        u32x4 x[NCH];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j)
+          if ((uint32_t)j < nch) x[j] = ld16u(in + src + 16ull * j);
+#pragma unroll
+        for (int j = 0; j < NCH; ++j)
+          if ((uint32_t)j < nch) {
+            u32x4 y = x[j] ^ h.mask;
+            const int64_t rem = (int64_t)h.length - 16 * j;
+            if (rem < 16) y = keep_bytes(y, rem);
+            *reinterpret_cast<u32x4*>(payload + poff + 16ull * j) = y;
+          }
+      } else {
+        const uint32_t b = atomicAdd(&s_nbig, 1u);
+        s_big[b][0] = src;
+        s_big[b][1] = poff;
+        s_big[b][2] = h.length;
+        s_bkey[b] = h.mask;
+      }
+      poff += round16(h.length);
+      q += h.hlen + h.length;
+    }
+  }
+  __syncthreads();
+  const uint32_t nbig = s_nbig;
+  for (uint32_t b = 0; b < nbig; ++b) {  // the larger payloads, by the whole workgroup
+    const uint64_t src = s_big[b][0], poff = s_big[b][1], L = s_big[b][2];
+    const uint32_t key = s_bkey[b];
+    for (uint64_t j = c; 16 * j < L; j += kSmallConns) {
+      u32x4 y = ld16u(in + src + 16 * j) ^ key;
+      const int64_t rem = (int64_t)L - (int64_t)(16 * j);
+      if (rem < 16) y = keep_bytes(y, rem);
+      *reinterpret_cast<u32x4*>(payload + poff + 16 * j) = y;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ 4. unmask / compact
 // Streams of big frames run fastest with one workgroup per CU (fewer
 // concurrent streams: better DRAM row locality); small frames need more
@@ -1278,17 +1426,6 @@ __device__ __forceinline__ uint64_t find_frame(const gevws_frame* __restrict__ f
     if (frames[mid].payload_off <= p) lo = mid; else hi = mid - 1;
   }
   return lo;
-}
-
-__device__ __forceinline__ u32x4 keep_bytes(u32x4 x, int64_t rem) {
-  // zero bytes at positions >= rem (rem in 1..15): Go's make() zero-fill of the pad
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t valid = rem - 4 * j;
-    const uint32_t m = valid >= 4 ? 0xffffffffu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
-    x[j] &= m;
-  }
-  return x;
 }
 
 template <bool NT>
@@ -2761,6 +2898,7 @@ struct gevws_ctx {
                            // 5 = 4 + loads before stores; 6 = 5 with plain window stores; 7 = 0 with
                            // plain window stores
   int emit_variant = 0;    // 0 = grouped record pass (k_walk_emit G = 16), 1 = one wave per connection
+  uint64_t small_bytes = kSmallBytes;  // one-launch decode (k_decode_small) up to this many input bytes
   uint32_t span_conns_per_cu = 0;  // walk variant 0: one wave per connection up to this many per CU
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
                            // 2 = plain walk without the entry table (emit re-walks); 0 and 1 store
@@ -2984,6 +3122,10 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       if (value < 0 || value > 1) return GEVWS_ERR_INVALID;
       ctx->emit_variant = (int)value;
       return GEVWS_OK;
+    case GEVWS_TUNE_SMALL_BATCH:
+      if (value < 0 || (uint64_t)value > kSmallBytes) return GEVWS_ERR_INVALID;
+      ctx->small_bytes = (uint64_t)value;
+      return GEVWS_OK;
     case GEVWS_TUNE_SPAN_CONNS_PER_CU:
       if (value < 0 || value > (1 << 20)) return GEVWS_ERR_INVALID;
       ctx->span_conns_per_cu = (uint32_t)value;
@@ -3038,6 +3180,17 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   if (max_frames > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;  // tile map holds 32-bit frame ids
   DeviceGuard g(ctx->device);
   hipStream_t st = pick_stream(ctx, stream);
+  // a small batch with the default kernels: the whole decode in one launch
+  // (per-phase timing and the variant knobs keep the multi-kernel path)
+  if (n_conns <= kSmallConns && in_bytes <= ctx->small_bytes && !ctx->timing && ctx->walk_variant == 0 &&
+      ctx->unmask_variant == 0 && ctx->emit_variant == 0 && ctx->span_conns_per_cu == 0 && ctx->unmask_grid == 0) {
+    int r = order_after_last(ctx, st);
+    if (r != GEVWS_OK) return r;
+    k_decode_small<<<1, kSmallConns, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
+                                               payload_cap, d_conn_out, d_summary);
+    GEVWS_HIP(hipGetLastError());
+    return mark_last(ctx, st);
+  }
   // connections per counting workgroup: 64, or fewer so a small batch covers every CU
   const uint32_t ncu = (uint32_t)ctx->num_cus;
   // header walk: one wave per connection (k_walk_span) when the batch has few

@@ -26,6 +26,8 @@ struct DeviceDecoder {
     p = gevws_protocol_new(ctx);
     if (const char* zc = getenv("GEVWS_LB_ZERO_COPY_MAX"))  // A/B: 0 = copy every pass in and out
       gevws_protocol_set_zero_copy_max(p, strtoull(zc, nullptr, 10));
+    if (const char* sb = getenv("GEVWS_LB_SMALL_BATCH"))  // A/B: 0 = multi-kernel decode for small passes
+      gevws_ctx_set_tuning(ctx, GEVWS_TUNE_SMALL_BATCH, (int64_t)strtoll(sb, nullptr, 10));
     u = gevws_upgrader_new();  // &ws.Upgrader{} as benchmarks/websocket/server.go:52
     gevws_protocol_set_upgrader(p, u);
   }

@@ -153,13 +153,18 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * up to which the default walk takes one wave per connection (0 = never, the
  * default: k_walk_span is issue-bound), GEVWS_TUNE_EMIT_VARIANT
  * the record pass (0 = groups of 16 connections with few frames enumerated
- * across connection boundaries, 1 = one wave per connection). */
+ * across connection boundaries, 1 = one wave per connection),
+ * GEVWS_TUNE_SMALL_BATCH the input size in bytes (default and maximum 65 536;
+ * 0 = never) up to which a batch of at most 256 connections is decoded by ONE
+ * kernel launch -- walk, scan, records and unmask in a single workgroup --
+ * when every other knob is at its default and per-phase timing is off. */
 #define GEVWS_TUNE_UNMASK_VARIANT 1
 #define GEVWS_TUNE_UNMASK_GRID 2
 #define GEVWS_TUNE_ENCODE_VARIANT 3
 #define GEVWS_TUNE_WALK_VARIANT 4
 #define GEVWS_TUNE_SPAN_CONNS_PER_CU 5
 #define GEVWS_TUNE_EMIT_VARIANT 6
+#define GEVWS_TUNE_SMALL_BATCH 7
 int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
 /* Human-readable name of a variant (GEVWS_TUNE_UNMASK_VARIANT or
  * GEVWS_TUNE_WALK_VARIANT), or NULL past the last one. */

@@ -16,8 +16,19 @@ from tests._helpers import assert_matches_oracle, gpu_decode, host_result, pack_
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["one_launch", "multi_kernel"])
+def small_path(engine, request):
+    """Small batches run the one-launch decode (k_decode_small) by default;
+    the multi-kernel path (walk, scan, records, unmask) must give the same
+    bytes, so the core parity tests run both."""
+    from gev_amd import _abi
+    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536 if request.param == "one_launch" else 0)
+    yield request.param
+    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+
+
 # --------------------------------------------------------------------------- golden vectors
-def test_golden_vectors(engine, golden):
+def test_golden_vectors(engine, golden, small_path):
     for name, g in golden.items():
         if name == "encode":
             continue  # tests/test_gpu_encode.py
@@ -35,7 +46,7 @@ def test_golden_vectors(engine, golden):
         assert_matches_oracle(engine, g["in"], g["conns"], name)
 
 
-def test_rfc6455_kats_on_device(engine):
+def test_rfc6455_kats_on_device(engine, small_path):
     arena = b"".join(k[0] for k in wo.RFC6455_KATS)
     got = host_result(gpu_decode(engine, arena, np.array([[0, len(arena)]])))
     assert int(got["summary"]["frames"]) == len(wo.RFC6455_KATS)
@@ -45,7 +56,7 @@ def test_rfc6455_kats_on_device(engine):
 
 
 # --------------------------------------------------------------------------- alignment / edge sweeps
-def test_alignment_and_length_sweep(engine):
+def test_alignment_and_length_sweep(engine, small_path):
     """Every payload start mod 16 x every length class near the 16-byte chunk edges."""
     rng = np.random.default_rng(11)
     streams = []
@@ -62,7 +73,7 @@ def test_alignment_and_length_sweep(engine):
     assert_matches_oracle(engine, arena, conns, "alignment sweep")
 
 
-def test_random_batches(engine):
+def test_random_batches(engine, small_path):
     rng = np.random.default_rng(12)
     for trial in range(6):
         n = int(rng.integers(1, 300))
@@ -71,7 +82,7 @@ def test_random_batches(engine):
         assert_matches_oracle(engine, arena, conns, f"trial {trial}")
 
 
-def test_unordered_and_overlapping_conn_tables(engine):
+def test_unordered_and_overlapping_conn_tables(engine, small_path):
     """the walk's per-connection entry runs are placed by
     input offset, which is collision-free only for a table in increasing,
     non-overlapping order.  Tables that break it -- the advisor's example
@@ -99,7 +110,7 @@ def test_unordered_and_overlapping_conn_tables(engine):
     assert_matches_oracle(engine, arena, np.tile(conns, (4, 1)), "repeat")
 
 
-def test_random_garbage_streams(engine):
+def test_random_garbage_streams(engine, small_path):
     """Streams of random bytes (headers parsed from noise: 16- and 64-bit length
     codes, MSB-set lengths, incomplete payloads, short tails), alone and behind
     a few valid frames, decode exactly as the oracle decodes them."""
@@ -117,7 +128,7 @@ def test_random_garbage_streams(engine):
         assert_matches_oracle(engine, arena, conns, f"garbage trial {trial}")
 
 
-def test_big_frames_cross_tiles(engine):
+def test_big_frames_cross_tiles(engine, small_path):
     rng = np.random.default_rng(13)
     s = b""
     for L in (1 << 20, 65536, 70001, 4096 * 3 + 5, 1, 0, (1 << 20) + 17):
@@ -127,14 +138,14 @@ def test_big_frames_cross_tiles(engine):
     assert_matches_oracle(engine, arena, conns, "big frames")
 
 
-def test_empty_and_tiny_batches(engine):
+def test_empty_and_tiny_batches(engine, small_path):
     assert_matches_oracle(engine, b"", np.zeros((0, 2), np.int64), "no conns")
     assert_matches_oracle(engine, b"\x81", np.array([[0, 1], [1, 0]]), "1 byte + empty")
     arena, conns = pack_streams([b"", b"\x81\x00", b"\x81\x80\x01\x02\x03\x04"])
     assert_matches_oracle(engine, arena, conns, "tiny")
 
 
-def test_poisoned_connections_isolated(engine):
+def test_poisoned_connections_isolated(engine, small_path):
     good = wo.encode_frame(b"fine", 1, True, 0, True, b"\x01\x02\x03\x04")
     bad = bytes([0x82, 0xFF, 0x80, 0, 0, 0, 0, 0, 0, 5, 1, 2, 3, 4]) + b"hello"
     arena, conns = pack_streams([good + bad + good, good * 3, bad, good])
@@ -143,7 +154,7 @@ def test_poisoned_connections_isolated(engine):
     assert int(got["summary"]["errors"]) == 2
 
 
-def test_streams_outside_the_arena_are_rejected(engine):
+def test_streams_outside_the_arena_are_rejected(engine, small_path):
     """A connection whose [off, off + len) leaves the input arena reads nothing
     and reports GEVWS_ERR_INVALID; the connections around it decode exactly as
     the oracle decodes them on their own."""
@@ -164,7 +175,7 @@ def test_streams_outside_the_arena_are_rejected(engine):
     assert np.array_equal(got["payload"], want["payload"])
 
 
-def test_decode_into_mapped_host_arena(engine):
+def test_decode_into_mapped_host_arena(engine, small_path):
     """The payload arena may be mapped pinned host memory (gevws_pinned_alloc):
     the unmask kernel's writes land in host pages, byte-identical to the oracle,
     and the bytes past the arena stay untouched."""
@@ -199,7 +210,7 @@ def test_decode_into_mapped_host_arena(engine):
         host.close()
 
 
-def test_capacity_error_reports_exact_sizes(engine):
+def test_capacity_error_reports_exact_sizes(engine, small_path):
     import torch
     rng = np.random.default_rng(14)
     arena, conns = pack_streams([random_stream(rng, 20, tail=False) for _ in range(10)])
