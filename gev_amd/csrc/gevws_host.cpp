@@ -311,7 +311,7 @@ class Protocol {
     if (n == 0) return 0;
     DeviceScope scope(gevws_ctx_device(ctx_));
     Staged sg;
-    int64_t r = StageDecode(segs, n, &sg);
+    int64_t r = StageDecode(segs, n, &sg, true);
     if (r < 0) return r;
     r = Finish(&sg);
     if (r < 0) return r;
@@ -323,13 +323,18 @@ class Protocol {
       return GEVWS_ERR_CAPACITY;
     }
     memcpy(conn_out, h_res_ + sizeof(gevws_summary), n * sizeof(gevws_conn_out));
-    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
-    if ((sum.frames && hipMemcpyAsync(frames, d_frames_, sum.frames * sizeof(gevws_frame), hipMemcpyDeviceToHost,
-                                      st) != hipSuccess) ||
-        (sum.payload_bytes &&
-         hipMemcpyAsync(payload, d_payload_, sum.payload_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return fail();
+    if (sg.zc) {  // the results are in mapped host memory already: the caller's buffers are host memory too
+      if (sum.frames) memcpy(frames, h_out_, sum.frames * sizeof(gevws_frame));
+      if (sum.payload_bytes) memcpy(payload, sg.arena.get(), sum.payload_bytes);
+    } else {
+      hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+      if ((sum.frames && hipMemcpyAsync(frames, d_frames_, sum.frames * sizeof(gevws_frame),
+                                        hipMemcpyDeviceToHost, st) != hipSuccess) ||
+          (sum.payload_bytes &&
+           hipMemcpyAsync(payload, d_payload_, sum.payload_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+          hipStreamSynchronize(st) != hipSuccess)
+        return fail();
+    }
     for (uint32_t j = 0; j < n; ++j)
       for (uint32_t k = 0; k < conn_out[j].nframes; ++k) frames[conn_out[j].first_frame + k].src_off -= sg.cin[j].off;
     return (int64_t)sum.frames;

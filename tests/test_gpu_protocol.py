@@ -149,12 +149,16 @@ def test_need_more_then_complete(engine):
     assert d == bytes(range(200)) and h.length == 200 and r.length() == 0
 
 
-def test_decode_host_batch_two_segments(engine):
+@pytest.mark.parametrize("zero_copy_max", [0, 1 << 30])
+def test_decode_host_batch_two_segments(engine, zero_copy_max):
     """gevws_decode_host_batch (the cgo entry point): each connection's bytes
-    arrive as the two PeekAll segments of a wrapped ring (connection.go:237-244)."""
+    arrive as the two PeekAll segments of a wrapped ring (connection.go:237-244).
+    Both pass forms: copies in and out, and zero-copy on mapped pinned memory
+    with a CPU copy into the caller's buffers."""
     from tests._helpers import random_stream
     rng = np.random.default_rng(23)
     proto = gev_amd.Protocol(engine)
+    proto.set_zero_copy_max(zero_copy_max)
     streams = [random_stream(rng, int(rng.integers(0, 20))) for _ in range(50)]
     segs = []
     for s in streams:
@@ -173,6 +177,7 @@ def test_decode_host_batch_two_segments(engine):
             o = int(f["payload_off"])
             assert payload[o:o + fr.header.length].tobytes() == fr.payload
     assert summ.frames == sum(len(wo.decode_stream(s).frames) for s in streams)
+    assert proto.stats()["zero_copy_passes"] == (1 if zero_copy_max else 0)
 
 
 def test_decode_host_stream_single_connection(engine):
