@@ -1452,7 +1452,15 @@ __device__ __forceinline__ void st16_stream(uint8_t* p, u32x4 x) {
 // owns a contiguous run of 4 KiB tiles, U unaligned 16-byte loads per lane,
 // aligned non-temporal stores.  bench.py times it over the same bytes as the
 // achievable-bandwidth ceiling beside the 8 TB/s spec peak.
-template <int U, bool INTERLEAVE>
+// Loads of the copy ceiling: non-temporal like the unmask's streaming loads
+// (NTL), or plain (measurement).
+template <bool NT>
+__device__ __forceinline__ u32x4 copy_ld(const uint8_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));  // unaligned nt load
+  else return ld16u(p);
+}
+
+template <int U, bool INTERLEAVE, bool NTL = true>
 __global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __restrict__ src,
                                                               uint8_t* __restrict__ dst, uint64_t n) {
   const uint64_t ntiles = n / kTile;
@@ -1464,14 +1472,14 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __r
       const uint64_t base = b * U * kTile + lane_off;
       u32x4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16u(src + base + u * kTile);
+      for (int u = 0; u < U; ++u) v[u] = copy_ld<NTL>(src + base + u * kTile);
 #pragma unroll
       for (int u = 0; u < U; ++u)
         __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + base + u * kTile));
     }
     for (uint64_t t = nblk * U + blockIdx.x; t < ntiles; t += gridDim.x) {
       const uint64_t base = t * kTile + lane_off;
-      __builtin_nontemporal_store(ld16u(src + base), reinterpret_cast<u32x4*>(dst + base));
+      __builtin_nontemporal_store(copy_ld<NTL>(src + base), reinterpret_cast<u32x4*>(dst + base));
     }
   } else {
     // a contiguous run of tiles per workgroup (the unmask kernel's mapping)
@@ -1482,21 +1490,21 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __r
       const uint64_t base = t * kTile + lane_off;
       u32x4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16u(src + base + u * kTile);
+      for (int u = 0; u < U; ++u) v[u] = copy_ld<NTL>(src + base + u * kTile);
 #pragma unroll
       for (int u = 0; u < U; ++u)
         __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + base + u * kTile));
     }
     for (; t < tend; ++t) {
       const uint64_t base = t * kTile + lane_off;
-      __builtin_nontemporal_store(ld16u(src + base), reinterpret_cast<u32x4*>(dst + base));
+      __builtin_nontemporal_store(copy_ld<NTL>(src + base), reinterpret_cast<u32x4*>(dst + base));
     }
   }
   // bytes past the last whole tile: 16 per lane, workgroup 0
   const uint64_t tail = ntiles * kTile;
   if (blockIdx.x == 0)
     for (uint64_t p = tail + lane_off; p < n; p += kTile)
-      __builtin_nontemporal_store(ld16u(src + p), reinterpret_cast<u32x4*>(dst + p));
+      __builtin_nontemporal_store(copy_ld<NTL>(src + p), reinterpret_cast<u32x4*>(dst + p));
 }
 
 // v3 = v2's streaming fast path + a cooperative small-frame path.  When the
@@ -1548,7 +1556,8 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t m) {
 // key f_key).  AL = 2: aligned loads, wave-contiguous spans, realigned in
 // registers (DPP lane rotate + v_alignbyte) when the source is misaligned;
 // AL = 0 / aligned source: plain (unaligned) loads.
-template <int U, bool NTL, bool NTS, int AL>
+// NTA (measurement): the aligned streaming loads non-temporal.
+template <int U, bool NTL, bool NTS, int AL, bool NTA = false>
 __device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                             uint64_t base, uint64_t f_po, uint64_t f_src, int64_t f_len,
                                             uint32_t f_key) {
@@ -1569,7 +1578,10 @@ __device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint
     uint8_t* d = out + base + wrel;
     const bool last = lane == 63;
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * 1024);
+    for (int u = 0; u < U; ++u) {
+      const u32x4* q = reinterpret_cast<const u32x4*>(a + u * 1024);
+      v[u] = NTA ? __builtin_nontemporal_load(q) : *q;
+    }
     u32x4 e = u32x4{0, 0, 0, 0};
     if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
     u32x4 r = rot_next_lane(v[0]);
@@ -1683,7 +1695,7 @@ __device__ __forceinline__ void window_search(const T* s_start, uint32_t F, cons
   }
 }
 
-template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles, bool IS = false>
+template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles, bool IS = false, bool NTA = false>
 __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
@@ -1717,7 +1729,7 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
       f_key = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
     }
     if (t + U <= tend && base + U * kTile <= f_end) {
-      stream_step<U, NTL, NTS, AL>(in, out, base, f_po, f_src, f_len, f_key);
+      stream_step<U, NTL, NTS, AL, NTA>(in, out, base, f_po, f_src, f_len, f_key);
       t += U;
       continue;
     }
@@ -1855,7 +1867,8 @@ __device__ __forceinline__ WinRec load_rec(const gevws_frame* __restrict__ frame
 // FT (measurement switch): false re-creates the round-1 kernel whose fill
 // addresses were spilled (threadIdx.x used directly).
 // SP: streaming steps as software-pipelined runs (stream_run, U / 2 tiles per step).
-template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false, bool IS = false>
+template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false, bool IS = false,
+          bool NTA = false>
 __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
@@ -1909,7 +1922,7 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
     if (t + U <= tend && base >= f_po && base + U * kTile <= f_end) {  // still inside the cached frame
       if constexpr (SP) t = stream_run<U / 2, NTS>(in, out, t, tend, f_po, f_src, f_len, f_key, f_end);
       else {
-        stream_step<U, false, NTS, 2>(in, out, base, f_po, f_src, f_len, f_key);
+        stream_step<U, false, NTS, 2, NTA>(in, out, base, f_po, f_src, f_len, f_key);
         t += U;
       }
       pf_t = ~0ull;  // (never t here; redefining r0 keeps it dead across the step)
@@ -1929,7 +1942,7 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
     if (stream) {  // decide() cached frame a, which covers [t, t+U)
       if constexpr (SP) t = stream_run<U / 2, NTS>(in, out, t, tend, f_po, f_src, f_len, f_key, f_end);
       else {
-        stream_step<U, false, NTS, 2>(in, out, base, f_po, f_src, f_len, f_key);
+        stream_step<U, false, NTS, 2, NTA>(in, out, base, f_po, f_src, f_len, f_key);
         t += U;
       }
       pf_t = ~0ull;
@@ -2057,7 +2070,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
 // v3-4 -5 % on C1-shaped and -2.4 % on C2 batches, v4-8 -3 % on C4 and -2 % on
 // C5, equal on C3; profiles/r02_ab2.log).  One kernel, one LDS table, the
 // choice is a uniform branch on the summary the walk wrote.
-template <bool IS>
+template <bool IS, bool NTA = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
     const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
@@ -2068,9 +2081,9 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   static_assert(kWinFrames == kWin4Frames, "one LDS table for both bodies");
   const WinLds L{s_start, s_lend, s_delta, s_key};
   if (2 * sum->run_frames >= sum->frames)  // frames the size of their predecessor on the connection
-    unmask_v3_body<16, false, true, 2, kWinTiles, IS>(in, frames, tile_first, sum, out, big_grid, L);
+    unmask_v3_body<16, false, true, 2, kWinTiles, IS, NTA>(in, frames, tile_first, sum, out, big_grid, L);
   else
-    unmask_v4_body<16, 8, true, false, true, false, IS>(in, frames, tile_first, sum, out, big_grid, L);
+    unmask_v4_body<16, 8, true, false, true, false, IS, NTA>(in, frames, tile_first, sum, out, big_grid, L);
 }
 
 // ------------------------------------------------------------------ outbound encode (§8f row 1)
@@ -2344,7 +2357,7 @@ __device__ __forceinline__ void win_store(u32x4 v, u32x4* p) {
 // r02_encode_ab_g64_*.json); plain stores recovered part of it by merging
 // the pieces in L2 (10.24 ms) at 2 GB more reads.
 template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false, bool HL = false,
-          bool WNT = true, bool G64 = false>
+          bool WNT = true, bool G64 = false, bool NTA = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
@@ -2393,7 +2406,10 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
         uint8_t* d = out + base + wrel;
         const bool last = lane == 63;
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * 1024);
+        for (int u = 0; u < U; ++u) {
+          const u32x4* q = reinterpret_cast<const u32x4*>(a + u * 1024);
+          v[u] = NTA ? __builtin_nontemporal_load(q) : *q;
+        }
         u32x4 e = u32x4{0, 0, 0, 0};
         if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
         u32x4 r = rot_next_lane(v[0]);
@@ -2896,7 +2912,7 @@ struct gevws_ctx {
                            // loads, per-lane assembly; 3 = queued boundary chunks, headers in LDS (4
                            // per CU); 4 = queued boundary chunks, LDS-light (round-1 default);
                            // 5 = 4 + loads before stores; 6 = 5 with plain window stores; 7 = 0 with
-                           // plain window stores
+                           // plain window stores; 8 = 0 with plain (not non-temporal) streaming loads
   int emit_variant = 0;    // 0 = grouped record pass (k_walk_emit G = 16), 1 = one wave per connection
   uint64_t small_bytes = kSmallBytes;  // one-launch decode (k_decode_small) up to this many input bytes
   uint32_t span_conns_per_cu = 0;  // walk variant 0: one wave per connection up to this many per CU
@@ -2981,9 +2997,9 @@ struct UnmaskVariant {
 // Variant 0 is the default; the others are kept for A/B measurement
 // (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 const UnmaskVariant kUnmaskVariants[] = {
-    {k_unmask_auto<false>, 16,
+    {k_unmask_auto<false, true>, 16,
      "auto: v3 4-tile windows for batches of equal-size frames, v4 pipelined 8-tile windows otherwise (summary "
-     "statistics of the walk)"},
+     "statistics of the walk); non-temporal aligned streaming loads"},
     {k_unmask_v4<16, 8, true>, 16,
      "v4 U16 streaming (aligned loads, DPP rotate) + pipelined 8-tile LDS window (next step's tile map and "
      "records fetched during the current window's payload loads)"},
@@ -3003,6 +3019,7 @@ const UnmaskVariant kUnmaskVariants[] = {
     {k_unmask_auto<true>, 16,
      "auto with the window chunks' frame searches interleaved (binary lifting, one LDS round trip per step for "
      "all chunks of a lane)"},
+    {k_unmask_auto<false>, 16, "auto with plain (temporal) streaming loads (the default until round 2's end)"},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
@@ -3115,7 +3132,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->unmask_grid = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_ENCODE_VARIANT:
-      if (value < 0 || value > 7) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 8) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_EMIT_VARIANT:
@@ -3380,7 +3397,8 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
              : ctx->encode_variant == 5 ? k_encode<4, true, true, true, 7, true, true>
              : ctx->encode_variant == 6 ? k_encode<4, true, true, true, 7, true, true, false>
              : ctx->encode_variant == 7 ? k_encode<4, true, true, true, 7, true, true, false, true>
-                                        : k_encode<4, true, true, true, 7, true, true, true, true>;
+             : ctx->encode_variant == 8 ? k_encode<4, true, true, true, 7, true, true, true, true>
+                                        : k_encode<4, true, true, true, 7, true, true, true, true, true>;
   // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
   // workgroups per CU (the rest return at once), the window path gets 7
   const uint32_t big = per_cu > 4 && grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
@@ -3422,11 +3440,15 @@ int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t
   if (n == 0) return GEVWS_OK;
   DeviceGuard g(ctx->device);
   hipStream_t st = pick_stream(ctx, stream);
+  // high bit: interleaved block mapping; next bit: plain loads (measurement variants)
+  const bool inter = grid & 0x80000000u, plain = grid & 0x40000000u;
+  grid &= 0x3fffffffu;
   if (grid == 0) grid = (uint32_t)ctx->num_cus;
-  if (grid & 0x80000000u)  // high bit: interleaved block mapping (measurement variant)
-    k_copy_stream<16, true><<<grid & 0x7fffffffu, kUnmaskBlock, 0, st>>>(d_src, d_dst, n);
+  if (inter)
+    (plain ? k_copy_stream<16, true, false> : k_copy_stream<16, true>)<<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst, n);
   else
-    k_copy_stream<16, false><<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst, n);
+    (plain ? k_copy_stream<16, false, false> : k_copy_stream<16, false>)<<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst,
+                                                                                                        n);
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;
 }

@@ -133,7 +133,7 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
 /* Tuning knobs for measurement (defaults are the tuned choice):
  * GEVWS_TUNE_UNMASK_VARIANT selects an unmask kernel variant (0 = default),
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto), GEVWS_TUNE_ENCODE_VARIANT
- * the encode kernel (0 = aligned loads + register realign while streaming;
+ * the encode kernel (0 = aligned non-temporal loads + register realign while streaming;
  * in frame windows all payload loads issued before the stores, and every
  * 64-byte group that holds a frame boundary queued whole and written by one
  * store instruction of the workgroup's assembly pass; frame headers rebuilt
@@ -142,7 +142,8 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * assembly; 3 = boundary chunks queued alone, serialised headers kept in
  * LDS, 4 workgroups per CU; 4 = boundary chunks queued alone, LDS-light (the
  * round-1 default); 5 = 4 with the loads before the stores; 6 = 5 with plain
- * (not non-temporal) window stores; 7 = 0 with plain window stores),
+ * (not non-temporal) window stores; 7 = 0 with plain window stores; 8 = 0 with
+ * plain streaming loads -- the default's are non-temporal),
  * GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
  * uniform-stream speculation, 1 = plain chain walk, 2 = plain walk that
  * records no per-frame entries, so the emit pass re-walks every chain; 0 and
@@ -258,7 +259,9 @@ int gevws_dispatch_async(gevws_ctx *ctx, void *stream, const gevws_frame *d_fram
  * streaming access pattern minus the XOR and frame lookup -- the achievable
  * HBM rate bench.py reports beside the spec peak.  grid 0 = one workgroup per
  * CU (the unmask kernel's grid for large frames); grid | 0x80000000 deals
- * 64 KiB blocks round-robin over the workgroups instead of contiguous runs. */
+ * 64 KiB blocks round-robin over the workgroups instead of contiguous runs;
+ * grid | 0x40000000 uses plain loads instead of the non-temporal ones the
+ * unmask kernel's streaming path uses. */
 int gevws_copy_async(gevws_ctx *ctx, void *stream, uint8_t *d_dst, const uint8_t *d_src, uint64_t n,
                      uint32_t grid);
 
