@@ -1695,7 +1695,8 @@ __device__ __forceinline__ void window_search(const T* s_start, uint32_t F, cons
   }
 }
 
-template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles, bool IS = false, bool NTA = false>
+template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles, bool IS = false, bool NTA = false,
+          bool NTW = false>
 __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
@@ -1783,7 +1784,7 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
           }
           rem[u] = s_lend[lo] - (int32_t)rel;
           key[u] = s_key[lo];
-          v[u] = ld16u_stream<NTL>(in + (p + s_delta[lo]));
+          v[u] = ld16u_stream<NTL || NTW>(in + (p + s_delta[lo]));
         }
       }
 #pragma unroll
@@ -1868,7 +1869,7 @@ __device__ __forceinline__ WinRec load_rec(const gevws_frame* __restrict__ frame
 // addresses were spilled (threadIdx.x used directly).
 // SP: streaming steps as software-pipelined runs (stream_run, U / 2 tiles per step).
 template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false, bool IS = false,
-          bool NTA = false>
+          bool NTA = false, bool NTW = false>
 __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
@@ -2019,7 +2020,7 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
         }
         rem[u] = s_lend[lo] - (int32_t)rel;
         key[u] = s_key[lo];
-        v[u] = ld16u(in + (p + s_delta[lo]));
+        v[u] = ld16u_stream<NTW>(in + (p + s_delta[lo]));
       }
     }
     // decide the next step (and fetch the next window's records) while this
@@ -2070,7 +2071,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
 // v3-4 -5 % on C1-shaped and -2.4 % on C2 batches, v4-8 -3 % on C4 and -2 % on
 // C5, equal on C3; profiles/r02_ab2.log).  One kernel, one LDS table, the
 // choice is a uniform branch on the summary the walk wrote.
-template <bool IS, bool NTA = false>
+template <bool IS, bool NTA = false, bool NTW = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
     const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
@@ -2081,9 +2082,9 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   static_assert(kWinFrames == kWin4Frames, "one LDS table for both bodies");
   const WinLds L{s_start, s_lend, s_delta, s_key};
   if (2 * sum->run_frames >= sum->frames)  // frames the size of their predecessor on the connection
-    unmask_v3_body<16, false, true, 2, kWinTiles, IS, NTA>(in, frames, tile_first, sum, out, big_grid, L);
+    unmask_v3_body<16, false, true, 2, kWinTiles, IS, NTA, NTW>(in, frames, tile_first, sum, out, big_grid, L);
   else
-    unmask_v4_body<16, 8, true, false, true, false, IS, NTA>(in, frames, tile_first, sum, out, big_grid, L);
+    unmask_v4_body<16, 8, true, false, true, false, IS, NTA, NTW>(in, frames, tile_first, sum, out, big_grid, L);
 }
 
 // ------------------------------------------------------------------ outbound encode (§8f row 1)
@@ -2357,7 +2358,7 @@ __device__ __forceinline__ void win_store(u32x4 v, u32x4* p) {
 // r02_encode_ab_g64_*.json); plain stores recovered part of it by merging
 // the pieces in L2 (10.24 ms) at 2 GB more reads.
 template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false, bool HL = false,
-          bool WNT = true, bool G64 = false, bool NTA = false>
+          bool WNT = true, bool G64 = false, bool NTA = false, bool NTW = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
@@ -2473,7 +2474,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
             if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
           }
           const bool in = valid && rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo];
-          if constexpr (!G64) v[u] = ld16u(payload + (in ? a + s_delta[lo] : 0ull));  // (G64: below)
+          if constexpr (!G64) v[u] = ld16u_stream<NTW>(payload + (in ? a + s_delta[lo] : 0ull));  // (G64: below)
           qlo[u] = lo;
           interior |= (in ? 1u : 0u) << u;
           queued |= (valid && !in ? 1u : 0u) << u;
@@ -2500,7 +2501,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
           for (int u = 0; u < kWinTiles; ++u) {
             const bool in = (interior >> u) & 1u;
             const uint64_t a = wbase + (uint64_t)(u * (int32_t)kTile + (int32_t)lane_off);
-            v[u] = ld16u(payload + (in ? a + s_delta[qlo[u]] : 0ull));
+            v[u] = ld16u_stream<NTW>(payload + (in ? a + s_delta[qlo[u]] : 0ull));
           }
         } else {
 #pragma unroll
@@ -2524,7 +2525,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
           if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
         }
         if (rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo]) {  // interior of one payload
-          win_store<WNT>(ld16u(payload + (a + s_delta[lo])), reinterpret_cast<u32x4*>(out + a));
+          win_store<WNT>(ld16u_stream<NTW>(payload + (a + s_delta[lo])), reinterpret_cast<u32x4*>(out + a));
         } else if constexpr (COMPACT) {
           s_bnd[atomicAdd(&s_nb, 1u)] = ((uint32_t)rel >> 4) | (lo << 16);
         } else {
@@ -2997,9 +2998,9 @@ struct UnmaskVariant {
 // Variant 0 is the default; the others are kept for A/B measurement
 // (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 const UnmaskVariant kUnmaskVariants[] = {
-    {k_unmask_auto<false, true>, 16,
+    {k_unmask_auto<false, true, true>, 16,
      "auto: v3 4-tile windows for batches of equal-size frames, v4 pipelined 8-tile windows otherwise (summary "
-     "statistics of the walk); non-temporal aligned streaming loads"},
+     "statistics of the walk); non-temporal streaming and window loads"},
     {k_unmask_v4<16, 8, true>, 16,
      "v4 U16 streaming (aligned loads, DPP rotate) + pipelined 8-tile LDS window (next step's tile map and "
      "records fetched during the current window's payload loads)"},
@@ -3020,6 +3021,7 @@ const UnmaskVariant kUnmaskVariants[] = {
      "auto with the window chunks' frame searches interleaved (binary lifting, one LDS round trip per step for "
      "all chunks of a lane)"},
     {k_unmask_auto<false>, 16, "auto with plain (temporal) streaming loads (the default until round 2's end)"},
+    {k_unmask_auto<false, true>, 16, "auto with non-temporal streaming loads, plain window loads"},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
@@ -3132,7 +3134,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->unmask_grid = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_ENCODE_VARIANT:
-      if (value < 0 || value > 8) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 9) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_EMIT_VARIANT:
@@ -3398,6 +3400,7 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
              : ctx->encode_variant == 6 ? k_encode<4, true, true, true, 7, true, true, false>
              : ctx->encode_variant == 7 ? k_encode<4, true, true, true, 7, true, true, false, true>
              : ctx->encode_variant == 8 ? k_encode<4, true, true, true, 7, true, true, true, true>
+             : ctx->encode_variant == 9 ? k_encode<4, true, true, true, 7, true, true, true, true, true, true>
                                         : k_encode<4, true, true, true, 7, true, true, true, true, true>;
   // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
   // workgroups per CU (the rest return at once), the window path gets 7

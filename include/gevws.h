@@ -143,7 +143,8 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * LDS, 4 workgroups per CU; 4 = boundary chunks queued alone, LDS-light (the
  * round-1 default); 5 = 4 with the loads before the stores; 6 = 5 with plain
  * (not non-temporal) window stores; 7 = 0 with plain window stores; 8 = 0 with
- * plain streaming loads -- the default's are non-temporal),
+ * plain streaming loads -- the default's are non-temporal; 9 = 0 with
+ * non-temporal window loads as well),
  * GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
  * uniform-stream speculation, 1 = plain chain walk, 2 = plain walk that
  * records no per-frame entries, so the emit pass re-walks every chain; 0 and

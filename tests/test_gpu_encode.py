@@ -47,7 +47,7 @@ def test_encode_golden(engine, golden):
     assert np.array_equal(got, g["wire"])
 
 
-ENC_VARIANTS = list(range(9))
+ENC_VARIANTS = list(range(10))
 
 
 @pytest.mark.parametrize("variant", ENC_VARIANTS)
@@ -60,7 +60,8 @@ def test_encode_random_and_tiny_frames(engine, variant):
     alone, headers in LDS (4 per CU); 4: boundary chunks queued alone,
     LDS-light (round-1 default); 5: 4 + loads before stores; 6: 5 with plain
     window stores; 7: 0 with plain window stores; 8: 0 with plain streaming
-    loads (the default's are non-temporal)."""
+    loads (the default's are non-temporal); 9: 0 with non-temporal window
+    loads."""
     from gev_amd import _abi
     engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, variant)
     try:
