@@ -1031,6 +1031,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_co
   cout[c] = o;
 }
 
+template <bool NT = false>
 __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, uint32_t* __restrict__ tile_first,
                                             uint64_t f, uint64_t poff, uint64_t src_off, const DevHdr& h) {
   // the 32-byte record as two 16-byte stores: {fin, rsv, opcode, masked,
@@ -1039,8 +1040,15 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
   // compiled to three stores of 8 + 16 + 8 bytes; profiles/r01_ab_emit_store_*.json)
   const uint32_t flags = (h.b0 >> 7) | (((h.b0 & 0x70) >> 4) << 8) | ((h.b0 & 0x0f) << 16) | ((h.masked & 1) << 24);
   u32x4* r = reinterpret_cast<u32x4*>(frames + f);
-  r[0] = u32x4{flags, h.mask, (uint32_t)h.length, (uint32_t)(h.length >> 32)};
-  r[1] = u32x4{(uint32_t)poff, (uint32_t)(poff >> 32), (uint32_t)src_off, (uint32_t)(src_off >> 32)};
+  const u32x4 r0 = u32x4{flags, h.mask, (uint32_t)h.length, (uint32_t)(h.length >> 32)};
+  const u32x4 r1 = u32x4{(uint32_t)poff, (uint32_t)(poff >> 32), (uint32_t)src_off, (uint32_t)(src_off >> 32)};
+  if constexpr (NT) {
+    __builtin_nontemporal_store(r0, r);
+    __builtin_nontemporal_store(r1, r + 1);
+  } else {
+    r[0] = r0;
+    r[1] = r1;
+  }
   const uint64_t padded = round16(h.length);
   // output tiles whose first byte lies in [poff, poff + padded)
   for (uint64_t t = (poff + kTile - 1) / kTile; t * kTile < poff + padded; ++t) tile_first[t] = (uint32_t)f;
@@ -1067,8 +1075,19 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
 // frames (C1: 16 frames of 136 B) fill whole waves instead of 16 lanes of
 // one, and all R rounds' entries are requested at once.  Longer groups take
 // the per-connection rounds above, connection by connection.
+template <bool NT>
+__device__ __forceinline__ WalkEntry ld_entry(const WalkEntry* p) {
+  if constexpr (NT) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return WalkEntry{v[0], v[1], v[2], v[3]};
+  } else {
+    return *p;
+  }
+}
+
 constexpr int kEmitGroup = 16;
-template <int U, int G = 0>
+// NTR (measurement): the entry loads and record stores non-temporal.
+template <int U, int G = 0, bool NTR = false>
 __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restrict__ in,
                                                           const gevws_conn_in* __restrict__ conns, uint32_t n,
                                                           const gevws_conn_out* __restrict__ cout,
@@ -1088,7 +1107,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
     h.hlen = q.meta >> 16;
     h.mask = q.mask;
     h.length = q.len;
-    emit_record(frames, tile_first, f, poff, coff + q.pos + h.hlen, h);
+    emit_record<NTR>(frames, tile_first, f, poff, coff + q.pos + h.hlen, h);
   };
   // the per-connection rounds (64 entries per round, U rounds per load)
   auto one_conn = [&](uint64_t cnt, uint64_t first_frame, uint64_t payload_base, uint64_t coff, uint64_t ebase) {
@@ -1105,7 +1124,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
     if (U == 1 || cnt <= 64) {  // wave-uniform
       for (uint64_t k0 = 0; k0 < cnt; k0 += 64) {
         WalkEntry q = {0, 0, 0, 0};
-        if (k0 + lane < cnt) q = ce[k0 + lane];
+        if (k0 + lane < cnt) q = ld_entry<NTR>(ce + k0 + lane);
         round(q, k0);
       }
     } else {
@@ -1116,7 +1135,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
           // unconditional (clamped to the last entry): a branch around the
           // load would make the compiler wait for it inside the branch
           const uint64_t k = k0 + (uint64_t)u * 64 + lane;
-          q[u] = ce[k < cnt ? k : cnt - 1];
+          q[u] = ld_entry<NTR>(ce + (k < cnt ? k : cnt - 1));
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1166,7 +1185,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
         kr[r] = t - __shfl(tstart, (int)lo, 64);
         const uint64_t eb = __shfl(ebase, (int)lo, 64);  // (outside the t < T branch: see below)
         q[r] = WalkEntry{0, 0, 0, 0};
-        if (t < T) q[r] = entries[eb + kr[r]];
+        if (t < T) q[r] = ld_entry<NTR>(entries + eb + kr[r]);
       }
       uint64_t carry = 0;  // lane j: its connection's padded bytes already placed
 #pragma unroll
@@ -3138,7 +3157,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_EMIT_VARIANT:
-      if (value < 0 || value > 1) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 2) return GEVWS_ERR_INVALID;
       ctx->emit_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_SMALL_BATCH:
@@ -3332,6 +3351,9 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     if (ctx->emit_variant == 1)
       k_walk_emit<4><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, d_summary,
                                                               d_frames, tile_first, entries, ne, gshift, rec_flags);
+    else if (ctx->emit_variant == 2)
+      k_walk_emit<4, kEmitGroup, true><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(
+          d_in, d_conns, n_conns, d_conn_out, d_summary, d_frames, tile_first, entries, ne, gshift, rec_flags);
     else
       k_walk_emit<4, kEmitGroup><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out,
                                                                           d_summary, d_frames, tile_first, entries,

@@ -8,7 +8,7 @@ run pytest_emit 600 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cac
 : > $OUT/emit_ab.jsonl
 for spec_ in ${SPECS:-c1 c2 c4 c4_--emulate-shard_0/8 c5 c3}; do
   spec=${spec_//_/ }
-  for ev in 0 1 0 1; do
+  for ev in ${EMITS:-0 1 0 1}; do
     run eab 300 python bench.py --steps 10 --warmup 2 --no-cpu --copy-reps 0 --config $spec --emit-variant $ev || exit $?
     python -c "
 import json; d=json.loads(open('$OUT/eab.log').read().strip().splitlines()[-1])

@@ -680,9 +680,10 @@ def test_walk_variants_uniform_runs(engine):
 
 
 def test_emit_variants(engine):
-    """Both record passes (grouped: frames of up to 16 short connections
-    enumerated across connection boundaries; per connection) bit-exact on
-    batches of short, long, empty, unrecorded and mixed connections."""
+    """Every record pass (grouped: frames of up to 16 short connections
+    enumerated across connection boundaries; per connection; grouped with
+    non-temporal entry loads / record stores) bit-exact on batches of short,
+    long, empty, unrecorded and mixed connections."""
     from gev_amd import _abi
     rng = np.random.default_rng(9191)
     cases = []
@@ -705,7 +706,7 @@ def test_emit_variants(engine):
         cases.append(pack_streams([b"".join(wo.encode_frame(bytes(20), 2, True, 0, True, b"\1\2\3\4")
                                             for _ in range(nfr)) for _ in range(40)]))
     try:
-        for v in (0, 1):
+        for v in (0, 1, 2):
             engine.set_tuning(_abi.TUNE_EMIT_VARIANT, v)
             for k, (arena, conns) in enumerate(cases):
                 assert_matches_oracle(engine, arena, conns, f"emit variant {v} case {k}")
