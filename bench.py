@@ -175,6 +175,9 @@ def main():
     ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
     ap.add_argument("--unmask-variant", type=int, default=None, help="A/B: unmask kernel variant")
     ap.add_argument("--emit-variant", type=int, default=None, help="A/B: record pass variant (GEVWS_TUNE_EMIT_VARIANT)")
+    ap.add_argument("--split-lanes", type=int, default=None,
+                    help="A/B: split header walk lanes per connection (GEVWS_TUNE_SPLIT_LANES; 0 = auto, 1 = off)")
+    ap.add_argument("--split-mode", type=int, default=0, help="measurement: GEVWS_TUNE_SPLIT_MODE")
     ap.add_argument("--emulate-shard", default=None, metavar="R/N",
                     help="projection, not the contract line: decode only rank R's LPT share of an N-way strong "
                          "split of the global batch, on this one GPU")
@@ -209,6 +212,10 @@ def main():
             e.set_tuning(_abi.TUNE_UNMASK_VARIANT, args.unmask_variant)
         if args.emit_variant is not None:
             e.set_tuning(_abi.TUNE_EMIT_VARIANT, args.emit_variant)
+        if args.split_lanes is not None:
+            e.set_tuning(_abi.TUNE_SPLIT_LANES, args.split_lanes)
+        if args.split_mode:
+            e.set_tuning(_abi.TUNE_SPLIT_MODE, args.split_mode)
     t_setup = time.time()
     scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
     emulated = None

@@ -183,6 +183,11 @@ class Engine:
         if st != OK:
             raise ValueError(f"set_tuning({key}, {value}): {status_string(st)}")
 
+    @property
+    def last_split_lanes(self) -> int:
+        """Lanes per connection of the last multi-kernel decode's header walk (1 = not split)."""
+        return int(lib.gevws_ctx_last_split_lanes(self._ctx))
+
     @staticmethod
     def variant_name(i: int, key: int = _abi.TUNE_UNMASK_VARIANT) -> Optional[str]:
         n = lib.gevws_tuning_name(key, i)

@@ -48,6 +48,8 @@ TUNE_WALK_VARIANT = 4
 TUNE_SPAN_CONNS_PER_CU = 5
 TUNE_EMIT_VARIANT = 6
 TUNE_SMALL_BATCH = 7  # one-launch decode up to this many input bytes (0 = never)
+TUNE_SPLIT_MODE = 9  # measurement: 1 = split guesses made then dropped, 2 = none made
+TUNE_SPLIT_LANES = 8  # split header walk: lanes per connection (0 = auto, 1 = never, 2/4/8/16)
 
 IN_PAD = 64
 SUMMARY_UNORDERED = 1  # summary.flags: connection table not in increasing input order
@@ -167,6 +169,7 @@ SIGNATURES = {
     "gevws_ctx_stream": (P, [P]),
     "gevws_ctx_set_timing": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_ctx_set_tuning": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
+    "gevws_ctx_last_split_lanes": (ctypes.c_int, [P]),
     "gevws_tuning_name": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32)]),
     "gevws_decode_batch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,

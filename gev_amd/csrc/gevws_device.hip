@@ -386,34 +386,23 @@ __device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t ava
 // the header (vmcnt counts loads in issue order) never waits longer for them;
 // they cost bandwidth, which a chain-bound walk of few connections has spare
 // (round 1 measured the same touch 30 % slower on all of C4, which is not).
+// The chain walk of one stream (k_walk_count's loop; also each segment of
+// k_walk_split): entries into [ebase, ebase + ecap) while rec, per-frame
+// counts into R (R.err / R.st carry in the caller's values).
+struct WalkRes {
+  uint64_t pos, nf, pb, pl, same, lastf, firstf, err;
+  int32_t st;
+  bool rec;
+};
+
 template <int D, bool GRP, bool NTH = false, int PF = 0>
-__global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
-                                                            const gevws_conn_in* __restrict__ conns,
-                                                            uint32_t n, gevws_conn_out* __restrict__ cout,
-                                                            uint64_t* __restrict__ blk,
-                                                            WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                            uint32_t gshift, uint32_t cpb, uint64_t in_bytes,
-                                                            uint32_t* __restrict__ done, uint64_t max_frames,
-                                                            uint64_t payload_cap, gevws_summary* __restrict__ sum) {
-  const uint32_t c = blockIdx.x * cpb + threadIdx.x;
-  uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0, lastf = ~0ull;
-  if (threadIdx.x < cpb && c < n) {
-    gevws_conn_in ci = conns[c];
-    // the order flag rides in the high half of the error count (k_scan_blocks SPLIT)
-    if (out_of_order(conns, c, ci)) err = 1ull << 32;
-    int32_t st = GEVWS_OK;
-    if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
-      // a stream outside the input arena: nothing is read, the connection
-      // reports GEVWS_ERR_INVALID (and counts as an error), the rest decode
-      ci.off = 0;
-      ci.len = 0;
-      st = GEVWS_ERR_INVALID;
-      err += 1;
-    }
-    const uint8_t* s = in + ci.off;
+__device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const uint64_t len, bool rec,
+                                           const uint64_t ebase, const uint64_t ecap,
+                                           WalkEntry* __restrict__ entries, WalkEntry* __restrict__ sink,
+                                           WalkRes& R) {
+    uint64_t nf = 0, pb = 0, pl = 0, same = 0, lastf = ~0ull, firstf = 0, err = R.err;
+    int32_t st = R.st;
     uint64_t pos = 0;
-    uint64_t ebase = 0, ecap = 0;
-    bool rec = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
     // software-pipelined: the next header's 16 bytes are requested before this
     // frame's entry is stored, so waiting for that load (vmcnt counts loads and
     // stores in issue order) never waits for the store's completion.  Reading
@@ -421,7 +410,6 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
     // Every path into the loop head has exactly [header load, entry store]
     // outstanding (lanes not recording store to their own sink slot past the
     // table), so the compiler waits vmcnt(1), not vmcnt(0).
-    WalkEntry* sink = entries + n_entries + c;
     uint64_t lo, hi;
     load_window<NTH>(s, lo, hi);
     *sink = WalkEntry{0, 0, 0, 0};
@@ -456,6 +444,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       pl += L;
       const uint64_t f = (uint64_t)(meta >> 16) + L;  // frame size (hlen + L)
       same += f == lastf;
+      firstf = lastf == ~0ull ? f : firstf;
       lastf = f;
     };
     uint32_t pfv[PF > 0 ? PF : 1] = {};
@@ -479,16 +468,16 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       const uint64_t next = pos + fsz;
       const uint64_t lo0 = lo, hi0 = hi;
       if constexpr (PF > 0) {
-        const uint64_t nx = next <= ci.len ? next : ci.len;
+        const uint64_t nx = next <= len ? next : len;
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
           const uint64_t q = nx + 128 * (j + 1);
-          pfv[j] = *reinterpret_cast<const uint32_t*>(s + (q <= ci.len ? q : ci.len));
+          pfv[j] = *reinterpret_cast<const uint32_t*>(s + (q <= len ? q : len));
         }
         __asm__ volatile("" ::: "memory");  // touches first, then the header load
       }
-      load_window<NTH>(s + (next <= ci.len ? next : ci.len), lo, hi);  // (a wrapped next is <= len or clamped)
-      const uint64_t avail = ci.len - pos;
+      load_window<NTH>(s + (next <= len ? next : len), lo, hi);  // (a wrapped next is <= len or clamped)
+      const uint64_t avail = len - pos;
       const bool have_hdr = avail >= 6 && avail >= hlen;   // read.go:20-23, U1
       const bool msb = e64 && (L64 >> 63);                  // read.go:71-73
       if (!have_hdr || msb || avail - hlen < L) {           // protocol.go:47 gate
@@ -517,9 +506,9 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
 #pragma unroll
             for (int j = 1; j < D; ++j) {
               const uint64_t q = pos + (uint64_t)j * fsz;
-              const bool in = q <= ci.len;
+              const bool in = q <= len;
               qn += in ? 1u : 0u;
-              load_window<NTH>(s + (in ? q : ci.len), qlo[j], qhi[j]);
+              load_window<NTH>(s + (in ? q : len), qlo[j], qhi[j]);
             }
             qlo[0] = lo;
             qhi[0] = hi;
@@ -529,7 +518,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
               if (!stop && (uint32_t)j < qn) {
                 uint32_t m2, h2, k2;
                 uint64_t L2;
-                const int r = walk_parse(qlo[j], qhi[j], ci.len - pos, m2, h2, L2, k2);
+                const int r = walk_parse(qlo[j], qhi[j], len - pos, m2, h2, L2, k2);
                 if (r != GEVWS_OK) {
                   if (r == GEVWS_ERR_LEN_MSB) { st = GEVWS_ERR_LEN_MSB; err += 1; }
                   fail = stop = true;
@@ -546,7 +535,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
             }
             if (fail) break;
             load_window<NTH>(s + pos, lo, hi);  // the next batch's first window, or the chain's next header
-            if (stop || qn < (uint32_t)D || pos + fsz > ci.len) break;
+            if (stop || qn < (uint32_t)D || pos + fsz > len) break;
           }
           if (fail) break;
           *sink = WalkEntry{0, 0, 0, 0};  // same [load, store] in flight at the loop head as the plain path
@@ -567,12 +556,59 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
         g[0] = g2;
       }
     }
+    R.pos = pos;
+    R.nf = nf;
+    R.pb = pb;
+    R.pl = pl;
+    R.same = same;
+    R.lastf = lastf;
+    R.firstf = firstf;
+    R.err = err;
+    R.st = st;
+    R.rec = rec;
+}
+
+template <int D, bool GRP, bool NTH = false, int PF = 0>
+__global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
+                                                            const gevws_conn_in* __restrict__ conns,
+                                                            uint32_t n, gevws_conn_out* __restrict__ cout,
+                                                            uint64_t* __restrict__ blk,
+                                                            WalkEntry* __restrict__ entries, uint64_t n_entries,
+                                                            uint32_t gshift, uint32_t cpb, uint64_t in_bytes,
+                                                            uint32_t* __restrict__ done, uint64_t max_frames,
+                                                            uint64_t payload_cap, gevws_summary* __restrict__ sum) {
+  const uint32_t c = blockIdx.x * cpb + threadIdx.x;
+  uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0;
+  if (threadIdx.x < cpb && c < n) {
+    gevws_conn_in ci = conns[c];
+    // the order flag rides in the high half of the error count (k_scan_blocks SPLIT)
+    if (out_of_order(conns, c, ci)) err = 1ull << 32;
+    int32_t st = GEVWS_OK;
+    if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
+      // a stream outside the input arena: nothing is read, the connection
+      // reports GEVWS_ERR_INVALID (and counts as an error), the rest decode
+      ci.off = 0;
+      ci.len = 0;
+      st = GEVWS_ERR_INVALID;
+      err += 1;
+    }
+    uint64_t ebase = 0, ecap = 0;
+    const bool rec0 = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
+    WalkRes R;
+    R.err = err;
+    R.st = st;
+    walk_chain<D, GRP, NTH, PF>(in + ci.off, ci.len, rec0, ebase, ecap, entries, entries + n_entries + c, R);
+    nf = R.nf;
+    pb = R.pb;
+    pl = R.pl;
+    err = R.err;
+    same = R.same;
     gevws_conn_out o;
-    o.first_frame = rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
-    o.consumed = pos;
+    o.first_frame = R.rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
+    o.consumed = R.pos;
     o.payload_base = pb;  // per-connection arena bytes; k_walk_emit turns it into a base
     o.nframes = (uint32_t)nf;
-    o.status = st;
+    o.status = R.st;
     cout[c] = o;
   }
   // block partial sums (one wave)
@@ -583,6 +619,366 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
     if (threadIdx.x == 0) {
       if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + k, s);
       else blk[(uint64_t)blockIdx.x * kDecFields + k] = s;
+    }
+  }
+  if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
+}
+
+// ------------------------------------------------------------------ 1a''. walk (count), split
+// A chain costs one memory round trip per frame, so a batch of few, long
+// chains (an 8-way C4 share: 8 192 connections, 1 100+ frames on the longest)
+// walks for (longest chain) x (latency) with most of the chip idle.
+// k_walk_split gives each connection KS lanes.  Lane i > 0 guesses a frame
+// start near i/KS of the stream: it searches kSyncWin bytes from there for a
+// position whose header and the kSyncDepth - 1 headers its chain reaches are
+// all plausible (sync_frame: RSV clear, a defined opcode, control frames final
+// and short, the mask bit of the connection's first frame, minimal length
+// encodings, frames inside the stream), and guesses the chain's last header
+// (sync_search).  WebSocket headers are not
+// self-synchronising, so a guess is only a guess: each lane walks its segment
+// [its guess, the next lane's guess) with k_walk_count's rules, and the
+// connection's result is accepted only when every segment but the last ends
+// exactly on its end (consumed == segment length, status OK) -- segment 0
+// starts at a true frame start, so by induction every accepted guess is one,
+// and the segments' frames, in order, are exactly the serial chain's.  If any
+// segment misses, lane 0 re-walks the whole connection serially (a guess can
+// cost time, never a different result).  The segments become the rows of a
+// virtual connection table (segs / sout / srec) that the record pass walks
+// like connections, with each segment's frame / payload offsets relative to
+// its connection (k_walk_emit adds the connection's bases); per-connection
+// results, block partials and summary are exactly k_walk_count's (the
+// equal-size run count is stitched across segment boundaries).
+constexpr uint32_t kSyncWin = 256;                // bytes searched after a split point
+constexpr uint32_t kSyncRow = kSyncWin / 4 + 5;   // dwords per lane's LDS row (window + 16 B; odd stride)
+constexpr int kSyncDepth = 5;                     // consecutive plausible headers confirm a guess
+constexpr uint64_t kSplitMinBytes = 16384;        // a connection's segments are at least this long
+constexpr uint32_t kSplitMaxLanes = 16;
+constexpr uint64_t kSplitLanesPerCU = 512;        // auto: split while the walk has fewer lanes per CU
+// auto: split only after a decode on this context whose connections averaged
+// this many frames of at most this many payload bytes (the long chains of
+// small frames splitting shortens; a batch of big frames -- C2, C3, C5 --
+// pays the guesses for nothing)
+constexpr uint64_t kSplitMinFramesPerConn = 256;
+constexpr uint64_t kSplitMaxConnsPerCU = 32;  // more chains keep the walk busy unsplit (C4 1/4 share: +5 %)
+constexpr uint64_t kSplitMaxFrameBytes = 4096;
+
+__device__ __forceinline__ bool sync_plausible1(uint32_t b0, uint32_t b1, uint32_t m0) {
+  const uint32_t op = b0 & 0x0fu;
+  const bool data = op <= 2, ctrl = op >= 8 && op <= 10;
+  return (b0 & 0x70u) == 0 && (b1 >> 7) == m0 && (data || (ctrl && (b0 & 0x80u) && (b1 & 0x7fu) <= 125));
+}
+
+// The frame size of a plausible header in the 16 bytes lo|hi with rem stream
+// bytes from it, else 0.
+__device__ __forceinline__ uint64_t sync_frame(uint64_t lo, uint64_t hi, uint64_t rem, uint32_t m0) {
+  const uint32_t b0 = (uint32_t)lo & 0xffu, b1 = (uint32_t)(lo >> 8) & 0xffu;
+  if (!sync_plausible1(b0, b1, m0)) return 0;
+  const uint32_t len7 = b1 & 0x7fu;
+  const uint32_t hlen = 2 + (len7 == 127 ? 8u : (len7 == 126 ? 2u : 0u)) + 4 * (b1 >> 7);
+  uint64_t L = len7;
+  if (len7 == 126) {
+    L = (((lo >> 16) & 0xff) << 8) | ((lo >> 24) & 0xff);
+    if (L < 126) return 0;
+  } else if (len7 == 127) {
+    L = __builtin_bswap64((lo >> 16) | (hi << 48));
+    if ((L >> 63) || L < 65536) return 0;
+  }
+  if (rem < hlen || rem - hlen < L) return 0;
+  return hlen + L;
+}
+
+// The guess is the LAST header of a confirmed chain of kSyncDepth, not its
+// first: chains converge (a false start inside a payload often hops onto a
+// true header and from there follows the true chain), so a chain's far end is
+// a frame start far more often than its first header -- for the last header
+// to be a false start the chain must have stayed inside payload bytes for
+// every hop.  (16-byte loads at q < len stay inside the stream + GEVWS_IN_PAD.)
+// 16 bytes at byte x of an LDS row
+__device__ __forceinline__ void row_window(const uint32_t* __restrict__ row, uint32_t x, uint64_t& lo, uint64_t& hi) {
+  const uint32_t k = x >> 2, e = x & 3;
+  const uint32_t w0 = row[k], w1 = row[k + 1], w2 = row[k + 2], w3 = row[k + 3], w4 = row[k + 4];
+  lo = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, e) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, e) << 32);
+  hi = (uint64_t)__builtin_amdgcn_alignbyte(w3, w2, e) | ((uint64_t)__builtin_amdgcn_alignbyte(w4, w3, e) << 32);
+}
+
+// Level-1 candidates among the 4 byte positions of dword w (wn: the next
+// dword): bit e set when byte e could open a frame -- RSV clear, opcode & 7
+// <= 2 (0-2, 8-10), the next byte's mask bit == m0 (mpat: m0 in every byte's
+// bit 7).  SWAR, so a window's 256 positions cost 64 such steps on every lane
+// alike instead of a divergent test per position.
+__device__ __forceinline__ uint32_t sync_l1_mask4(uint32_t w, uint32_t wn, uint32_t mpat) {
+  const uint32_t w1 = __builtin_amdgcn_alignbyte(wn, w, 1);  // byte p + 1 of every position p
+  const uint32_t bad = (w & 0x74747474u) | (w & (w >> 1) & 0x01010101u) | ((w1 ^ mpat) & 0x80808080u);
+  const uint32_t z = ~(((bad & 0x7f7f7f7fu) + 0x7f7f7f7fu) | bad | 0x7f7f7f7fu);  // 0x80 where bad's byte is 0
+  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+// A confirmed frame start reached from one of kSyncWindows windows of
+// kSyncWin bytes at t, t + step, ..., below qmax (every window inside the
+// stream).  Per window: (1) the window into this lane's LDS row and a bitmask
+// of its level-1 candidates (sync_l1_mask4); (2) the lane's candidates in
+// order -- a loop over set bits, so the wave iterates as often as its busiest
+// lane has candidates, not once per position -- until the first whose chain
+// stays plausible for every hop inside the window; (3) all lanes at once
+// continue that candidate's chain with global loads to kSyncDepth headers.
+constexpr int kSyncWindows = 4;
+// headers a candidate's chain must show inside the window before its global
+// confirmation (a lone plausible header is common in payload bytes, and
+// confirming it costs the whole wave memory round trips; 2 finds fewer guesses)
+constexpr int kSyncMinInWindow = 1;
+__device__ __forceinline__ bool sync_search(const uint8_t* __restrict__ s, uint64_t len, uint64_t t, uint64_t step,
+                                            uint64_t qmax, uint32_t m0, uint32_t* __restrict__ row, uint64_t& b) {
+  const uint32_t mpat = m0 ? 0x80808080u : 0u;
+  for (int win = 0; win < kSyncWindows; ++win, t += step) {
+    if (t + kSyncWin + 16 > len || t >= qmax) return false;
+    uint32_t wv[kSyncRow - 1];
+#pragma unroll
+    for (uint32_t j = 0; j < (kSyncWin + 16) / 16; ++j) {
+      const u32x4 v = ld16u(s + t + 16 * j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wv[4 * j + e] = v[e];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kSyncRow - 1; ++k) row[k] = wv[k];
+    row[kSyncRow - 1] = 0;
+    uint64_t cm[kSyncWin / 64];
+#pragma unroll
+    for (uint32_t j = 0; j < kSyncWin / 64; ++j) {
+      uint64_t m = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 16; ++k) m |= (uint64_t)sync_l1_mask4(wv[16 * j + k], wv[16 * j + k + 1], mpat) << (4 * k);
+      cm[j] = m;
+    }
+    // (2) the first candidate whose in-window hops are all plausible
+    bool have = false;
+    uint64_t q = 0, lb = 0;
+    int h = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kSyncWin / 64; ++j) {
+      uint64_t m = have ? 0 : cm[j];
+      while (m) {
+        uint32_t x = 64 * j + (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        uint64_t lo, hi;
+        row_window(row, x, lo, hi);
+        uint64_t f = sync_frame(lo, hi, len - (t + x), m0);
+        if (f == 0) continue;
+        int hh = 1;
+        uint32_t last = x;
+        while (hh < kSyncDepth && x + f < kSyncWin) {
+          x += (uint32_t)f;
+          row_window(row, x, lo, hi);
+          f = sync_frame(lo, hi, len - (t + x), m0);
+          if (f == 0) break;
+          last = x;
+          ++hh;
+        }
+        if (f == 0 || (hh < kSyncMinInWindow && t + x + f < len)) continue;
+        have = true;
+        q = t + x + f;
+        lb = t + last;
+        h = hh;
+        m = 0;
+      }
+    }
+    if (!have) continue;
+    // (3) the rest of its chain from memory
+    bool ok = true;
+    while (h < kSyncDepth) {
+      if (q >= qmax || q >= len) {
+        ok = false;
+        break;
+      }
+      uint64_t lo, hi;
+      load_window(s + q, lo, hi);
+      const uint64_t g = sync_frame(lo, hi, len - q, m0);
+      if (g == 0) {
+        ok = false;
+        break;
+      }
+      lb = q;
+      q += g;
+      ++h;
+    }
+    if (ok && lb < qmax) {
+      b = lb;
+      return true;
+    }
+  }
+  return false;
+}
+
+template <int KS, int D, bool GRP>
+__global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __restrict__ in,
+                                                            const gevws_conn_in* __restrict__ conns, uint32_t n,
+                                                            gevws_conn_out* __restrict__ cout,
+                                                            uint64_t* __restrict__ blk,
+                                                            WalkEntry* __restrict__ entries, uint64_t n_entries,
+                                                            uint32_t gshift, uint32_t cpb, uint64_t in_bytes,
+                                                            uint32_t* __restrict__ done, uint64_t max_frames,
+                                                            uint64_t payload_cap, gevws_summary* __restrict__ sum,
+                                                            gevws_conn_in* __restrict__ segs,
+                                                            gevws_conn_out* __restrict__ sout,
+                                                            uint8_t* __restrict__ srec, int mode) {
+  static_assert(KS >= 2 && KS <= (int)kSplitMaxLanes && (KS & (KS - 1)) == 0, "KS: a power of two");
+  __shared__ uint32_t s_row[kCountBlock * kSyncRow];
+  const uint32_t lane = threadIdx.x & 63, i = lane % KS;
+  const uint32_t c = blockIdx.x * cpb + threadIdx.x / KS;
+  const bool active = threadIdx.x / KS < cpb && c < n;
+  const uint64_t v = (uint64_t)c * KS + i;
+  gevws_conn_in ci = {0, 0};
+  bool oob = false;
+  if (active) {
+    ci = conns[c];
+    oob = ci.off > in_bytes || ci.len > in_bytes - ci.off;
+    if (oob) ci = gevws_conn_in{0, 0};  // nothing of it is read (k_walk_count's rule)
+  }
+  const uint8_t* s = in + ci.off;
+  // 1. guesses: lane 0 starts at 0; lane i at the first confirmed frame start
+  // after i/kc of the stream (kc: segments of >= kSplitMinBytes)
+  bool found = active && i == 0;
+  uint64_t b = 0;
+  if (active && i > 0 && mode != 2) {  // mode 2 (measurement): no guesses
+    const uint64_t kc = ci.len / kSplitMinBytes < KS ? ci.len / kSplitMinBytes : KS;
+    if (i < kc) {
+      // windows spread over the first half of the segment; guesses below
+      // 3/4 of it, so they stay in increasing lane order
+      const uint64_t seg = ci.len / kc, t = ci.len * i / kc;
+      const uint64_t step = seg / (2 * kSyncWindows) > kSyncWin ? seg / (2 * kSyncWindows) : kSyncWin;
+      const uint32_t m0 = (uint32_t)s[1] >> 7;  // the first frame's mask bit (len >= 2 x kSplitMinBytes)
+      found = sync_search(s, ci.len, t, step, t + seg * 3 / 4, m0, s_row + (threadIdx.x) * kSyncRow, b);
+    }
+  }
+  if (mode == 1 && i > 0) found = false;  // mode 1 (measurement): guesses made, then dropped
+  // 2. a segment ends at the next lane's guess (or the stream's end);
+  // lanes without a guess hold an empty segment there
+  const uint64_t mine = found ? b : ~0ull;
+  uint64_t end = ci.len;
+#pragma unroll
+  for (int j = KS - 1; j >= 1; --j) {
+    const uint64_t y = __shfl(mine, (int)((lane + j) & 63), 64);
+    if ((int)i + j < KS && y != ~0ull) end = y;
+  }
+  const uint64_t sb = found ? b : end;
+  const uint64_t slen = found ? end - b : 0;
+  gevws_conn_in sg = {ci.off + sb, slen};
+  // 3. walk the segment (entries in its own slot run)
+  uint64_t ebase = 0, ecap = 0;
+  const bool rec0 = active && entry_slots_of(sg, (uint32_t)v, n_entries, gshift, ebase, ecap);
+  WalkRes R;
+  R.err = 0;
+  R.st = GEVWS_OK;
+  R.pos = R.nf = R.pb = R.pl = R.same = R.firstf = 0;
+  R.lastf = ~0ull;
+  R.rec = false;
+  if (active) walk_chain<D, GRP>(in + sg.off, sg.len, rec0, ebase, ecap, entries, entries + n_entries + v, R);
+  // 4. stitch the group's KS lanes (every lane takes part in the shuffles)
+  const bool last = found && end == ci.len;
+  const bool ok = !found || last || (R.st == GEVWS_OK && R.pos == slen);
+  uint64_t prevlast = ~0ull;
+  bool got = false;
+#pragma unroll
+  for (int d = 1; d < KS; ++d) {
+    const uint64_t ynf = __shfl_up(R.nf, d, 64), ylast = __shfl_up(R.lastf, d, 64);
+    if (!got && (int)i >= d && ynf > 0) {
+      prevlast = ylast;
+      got = true;
+    }
+  }
+  const uint64_t same = R.same + ((R.nf > 0 && got && R.firstf == prevlast) ? 1 : 0);
+  uint64_t inf = R.nf, ipb = R.pb;  // inclusive prefixes within the group
+#pragma unroll
+  for (int d = 1; d < KS; d <<= 1) {
+    const uint64_t a = __shfl_up(inf, d, 64), q = __shfl_up(ipb, d, 64);
+    if ((int)i >= d) {
+      inf += a;
+      ipb += q;
+    }
+  }
+  uint64_t t_nf = R.nf, t_pb = R.pb, t_pl = R.pl, t_same = same;
+  uint64_t t_cons = last ? sb + R.pos : 0;
+  int32_t t_st = last ? R.st : 0;
+  int t_ok = ok ? 1 : 0;
+#pragma unroll
+  for (int d = KS / 2; d >= 1; d >>= 1) {
+    t_nf += __shfl_xor(t_nf, d, 64);
+    t_pb += __shfl_xor(t_pb, d, 64);
+    t_pl += __shfl_xor(t_pl, d, 64);
+    t_same += __shfl_xor(t_same, d, 64);
+    t_cons += __shfl_xor(t_cons, d, 64);
+    t_st += __shfl_xor(t_st, d, 64);
+    t_ok &= __shfl_xor(t_ok, d, 64);
+  }
+  const bool valid = t_ok != 0 && !oob;
+  uint64_t nf = 0, pb = 0, pl = 0, err = 0, rs = 0;
+  if (active) {
+    if (valid) {
+      segs[v] = sg;
+      gevws_conn_out so;
+      so.first_frame = inf - R.nf;  // relative to the connection's first frame
+      so.consumed = R.pos;
+      so.payload_base = ipb - R.pb;  // relative to the connection's payload base
+      so.nframes = (uint32_t)R.nf;
+      so.status = R.st;
+      sout[v] = so;
+      srec[v] = R.rec ? 1 : 0;
+    }
+    if (i == 0) {
+      gevws_conn_out o;
+      o.first_frame = 0;
+      if (oob) {
+        o.consumed = 0;
+        o.payload_base = 0;
+        o.nframes = 0;
+        o.status = GEVWS_ERR_INVALID;
+      } else if (valid) {
+        nf = t_nf;
+        pb = t_pb;
+        pl = t_pl;
+        rs = t_same;
+        o.consumed = t_cons;
+        o.payload_base = pb;
+        o.nframes = (uint32_t)nf;
+        o.status = t_st;
+      } else {
+        // a guess missed: the whole chain, serially (no entries: the record
+        // pass re-walks it as one segment)
+        WalkRes S;
+        S.err = 0;
+        S.st = GEVWS_OK;
+        walk_chain<0, false>(s, ci.len, false, 0, 0, entries, entries + n_entries + v, S);
+        nf = S.nf;
+        pb = S.pb;
+        pl = S.pl;
+        rs = S.same;
+        o.consumed = S.pos;
+        o.payload_base = pb;
+        o.nframes = (uint32_t)nf;
+        o.status = S.st;
+      }
+      err = (o.status < 0 ? 1ull : 0ull) + (out_of_order(conns, c, conns[c]) ? (1ull << 32) : 0ull);
+      cout[c] = o;
+    }
+    if (!valid) {  // one segment: the whole connection, re-walked by the record pass
+      segs[v] = i == 0 ? ci : gevws_conn_in{ci.off + ci.len, 0};
+      gevws_conn_out so;
+      so.first_frame = 0;
+      so.consumed = 0;
+      so.payload_base = 0;
+      so.nframes = (uint32_t)(i == 0 ? nf : 0);
+      so.status = GEVWS_OK;
+      sout[v] = so;
+      srec[v] = 0;
+    }
+  }
+  // block partials (one wave), as k_walk_count
+  const uint64_t vals[kDecFields] = {nf, pb, pl, err, rs};
+#pragma unroll
+  for (int k = 0; k < kDecFields; ++k) {
+    const uint64_t x = wave_sum(vals[k]);
+    if (threadIdx.x == 0) {
+      if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + k, x);
+      else blk[(uint64_t)blockIdx.x * kDecFields + k] = x;
     }
   }
   if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
@@ -1011,7 +1407,12 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict
 __global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_conn_out* __restrict__ cout,
                                                             const uint64_t* __restrict__ blk,
                                                             const gevws_summary* __restrict__ sum,
-                                                            uint8_t* __restrict__ rec_flags, uint32_t cpb) {
+                                                            uint8_t* __restrict__ rec_flags, uint32_t cpb,
+                                                            uint64_t* __restrict__ stats = nullptr) {
+  if (stats && blockIdx.x == 0 && threadIdx.x == 0) {  // the split walk's history (see decode_split_lanes)
+    stats[0] = sum->frames;
+    stats[1] = sum->payload_len;
+  }
   if (sum->status != GEVWS_OK) return;  // capacity error: nothing written
   const uint32_t c = blockIdx.x * cpb + threadIdx.x;
   const bool active = threadIdx.x < cpb && c < n;
@@ -1095,8 +1496,20 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
                                                           gevws_frame* __restrict__ frames,
                                                           uint32_t* __restrict__ tile_first,
                                                           const WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                          uint32_t gshift, const uint8_t* __restrict__ rec_flags) {
+                                                          uint32_t gshift, const uint8_t* __restrict__ rec_flags,
+                                                          const gevws_conn_out* __restrict__ pout = nullptr,
+                                                          uint32_t ks = 0) {
   if (sum->status != GEVWS_OK) return;
+  // k_walk_split's segments: frame / payload offsets relative to connection c / ks
+  auto out_of = [&](uint64_t c) {
+    gevws_conn_out o = cout[c];
+    if (ks) {
+      const gevws_conn_out p = pout[c / ks];
+      o.first_frame += p.first_frame;
+      o.payload_base += p.payload_base;
+    }
+    return o;
+  };
   const bool unordered = (sum->flags & GEVWS_SUMMARY_UNORDERED) != 0;  // entry runs may collide: unused
   const int lane = threadIdx.x & 63;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kWalkBlock / 64);
@@ -1155,7 +1568,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
       const uint64_t c = g * G + lane;
       uint64_t nf = 0, ff = 0, pbase = 0, coff = 0, ebase = 0;
       if (lane < G && c < n) {
-        const gevws_conn_out o = cout[c];
+        const gevws_conn_out o = out_of(c);
         const gevws_conn_in ci = conns[c];
         uint64_t ecap = 0;
         const bool rec = rec_flags[c] && !unordered && entry_slots_of(ci, (uint32_t)c, n_entries, gshift, ebase, ecap);
@@ -1234,7 +1647,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
       const uint64_t c = g * GL + lane;
       uint64_t nf = 0, ff = 0, pbase = 0, coff = 0, ebase = 0;
       if (lane < GL && c < n) {
-        const gevws_conn_out o = cout[c];
+        const gevws_conn_out o = out_of(c);
         const gevws_conn_in ci = conns[c];
         uint64_t ecap = 0;
         const bool rec = rec_flags[c] && !unordered && entry_slots_of(ci, (uint32_t)c, n_entries, gshift, ebase, ecap);
@@ -1253,7 +1666,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
   } else {
   for (uint64_t c = (uint64_t)blockIdx.x * (kWalkBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
     // everything the connection needs is requested at once (one latency)
-    const gevws_conn_out o = cout[c];
+    const gevws_conn_out o = out_of(c);
     const uint8_t recorded = rec_flags[c];
     const gevws_conn_in ci = conns[c];
     const uint64_t cnt = uniform64(o.nframes);  // one connection per wave
@@ -1267,7 +1680,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
   const uint64_t nthreads = (uint64_t)gridDim.x * kWalkBlock;
   for (uint64_t c = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x; c < n; c += nthreads) {
     if (rec_flags[c] && !unordered) continue;
-    const gevws_conn_out o = cout[c];
+    const gevws_conn_out o = out_of(c);
     const gevws_conn_in ci = conns[c];
     const uint8_t* s = in + ci.off;
     uint64_t pos = 0, poff = o.payload_base;
@@ -2936,6 +3349,16 @@ struct gevws_ctx {
   int emit_variant = 0;    // 0 = grouped record pass (k_walk_emit G = 16), 1 = one wave per connection
   uint64_t small_bytes = kSmallBytes;  // one-launch decode (k_decode_small) up to this many input bytes
   uint32_t span_conns_per_cu = 0;  // walk variant 0: one wave per connection up to this many per CU
+  // the split walk's history: the last multi-kernel decode's frame / payload
+  // totals (written by k_walk_bases into mapped host memory) and its
+  // connection count, read once that decode has finished
+  uint64_t* h_stats = nullptr;
+  uint64_t* d_stats = nullptr;
+  bool stats_pending = false, stats_known = false;
+  uint64_t stats_conns = 0, prev_frames_per_conn = 0, prev_frame_bytes = 0;
+  uint32_t last_ks = 1;    // lanes per connection of the last multi-kernel decode's walk
+  int split_mode = 0;       // measurement: 1 = guesses made then dropped, 2 = no guesses
+  uint32_t split_lanes = 0;  // walk variant 0: lanes per connection (k_walk_split); 0 = auto, 1 = off
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
                            // 2 = plain walk without the entry table (emit re-walks); 0 and 1 store
                            // entries in 64-byte groups for batches of many connections; 3 / 4 =
@@ -3116,7 +3539,11 @@ gevws_ctx* gevws_ctx_create(int device) {
     ctx->num_cus = prop.multiProcessorCount;
   if (hipMalloc(reinterpret_cast<void**>(&ctx->d_sum), sizeof(gevws_summary)) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&ctx->d_done), 256) != hipSuccess ||
-      hipMemset(ctx->d_done, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      hipMemset(ctx->d_done, 0, 256) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&ctx->h_stats), 64, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_stats), ctx->h_stats, 0) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
     gevws_ctx_destroy(ctx);
     return nullptr;
   }
@@ -3130,6 +3557,7 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->d_sum) (void)hipFree(ctx->d_sum);
   if (ctx->d_done) (void)hipFree(ctx->d_done);
+  if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
   for (auto& set : ctx->evs)
     for (auto& e : set.e) (void)hipEventDestroy(e);
@@ -3168,6 +3596,14 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       if (value < 0 || value > (1 << 20)) return GEVWS_ERR_INVALID;
       ctx->span_conns_per_cu = (uint32_t)value;
       return GEVWS_OK;
+    case GEVWS_TUNE_SPLIT_LANES:
+      if (value < 0 || value > kSplitMaxLanes || (value > 1 && (value & (value - 1)))) return GEVWS_ERR_INVALID;
+      ctx->split_lanes = (uint32_t)value;
+      return GEVWS_OK;
+    case GEVWS_TUNE_SPLIT_MODE:
+      if (value < 0 || value > 2) return GEVWS_ERR_INVALID;
+      ctx->split_mode = (int)value;
+      return GEVWS_OK;
     case GEVWS_TUNE_WALK_VARIANT:
       if (value < 0 || value >= kNumWalkVariants) return GEVWS_ERR_INVALID;
       ctx->walk_variant = (int)value;
@@ -3183,6 +3619,8 @@ const char* gevws_tuning_name(int key, int64_t value) {
   if (key == GEVWS_TUNE_WALK_VARIANT && value >= 0 && value < kNumWalkVariants) return kWalkVariants[value];
   return nullptr;
 }
+
+int gevws_ctx_last_split_lanes(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_ks : -1; }
 
 int gevws_ctx_set_timing(gevws_ctx* ctx, int enable) {
   if (!ctx) return GEVWS_ERR_INVALID;
@@ -3241,24 +3679,53 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
                             : n_conns >= (uint32_t)kCountBlock * ncu
                                   ? (uint32_t)kCountBlock
                                   : (n_conns + ncu - 1) / ncu > 0 ? (n_conns + ncu - 1) / ncu : 1;
-  const uint32_t nblk = (n_conns + cpb - 1) / cpb;
+  // split walk (k_walk_split): ks lanes per connection when the batch has too
+  // few connections to keep kSplitLanesPerCU lanes per CU walking, and they
+  // are long enough to split
+  uint32_t ks = 1;
+  if (ctx->stats_pending && hipEventQuery(ctx->last_done) == hipSuccess) {
+    ctx->stats_pending = false;
+    ctx->stats_known = true;
+    const uint64_t fr = ctx->h_stats[0], pl = ctx->h_stats[1];
+    ctx->prev_frames_per_conn = ctx->stats_conns ? fr / ctx->stats_conns : 0;
+    ctx->prev_frame_bytes = fr ? pl / fr : 0;
+  }
+  if (!span && wv == 0 && n_conns) {
+    if (ctx->split_lanes >= 2) {
+      ks = ctx->split_lanes;
+    } else if (ctx->split_lanes == 0 && in_bytes / n_conns >= 2 * kSplitMinBytes && ctx->stats_known &&
+               ctx->prev_frames_per_conn >= kSplitMinFramesPerConn && ctx->prev_frame_bytes <= kSplitMaxFrameBytes) {
+      if ((uint64_t)n_conns <= kSplitMaxConnsPerCU * ncu)
+        while (ks < kSplitMaxLanes && (uint64_t)n_conns * ks * 2 <= (uint64_t)kSplitLanesPerCU * ncu) ks *= 2;
+    }
+  }
+  if ((uint64_t)n_conns * ks > 0xFFFFFFFFull) ks = 1;
+  ctx->last_ks = ks;
+  const uint32_t cpb_w = ks > 1 ? (kCountBlock / ks < cpb ? kCountBlock / ks : cpb) : cpb;
+  const uint32_t nblk = (n_conns + cpb_w - 1) / cpb_w;
+  const uint64_t n_v = (uint64_t)n_conns * ks;  // rows of the record pass's connection table
   const uint64_t ntiles_cap = (payload_cap + kTile - 1) / kTile + 1;
   const size_t blk_bytes = ((size_t)nblk * kDecFields * sizeof(uint64_t) + 255) & ~size_t(255);
   const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
   uint32_t gshift = kEntryGranMinShift;
   while ((in_bytes >> gshift) > kEntryBudget) ++gshift;
-  const uint64_t n_entries = 4 * ((in_bytes >> (gshift + 2)) + (uint64_t)n_conns + 1);
+  const uint64_t n_entries = 4 * ((in_bytes >> (gshift + 2)) + n_v + 1);
   const size_t flag_bytes = ((size_t)n_conns + 255) & ~size_t(255);
-  // + one sink slot per connection after the table (k_walk_count)
+  const size_t seg_bytes = ks > 1 ? ((n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out) + 1) + 1023) & ~size_t(255)) : 0;
+  // + one sink slot per walk lane after the table (k_walk_count / k_walk_split)
   int r = order_after_last(ctx, st);
   if (r != GEVWS_OK) return r;
-  r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + (n_entries + n_conns) * sizeof(WalkEntry));
+  r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + seg_bytes + (n_entries + n_v) * sizeof(WalkEntry));
   if (r != GEVWS_OK) return r;
   char* sp = reinterpret_cast<char*>(ctx->scratch);
   uint64_t* blk = reinterpret_cast<uint64_t*>(sp);
   uint32_t* tile_first = reinterpret_cast<uint32_t*>(sp + blk_bytes);
   uint8_t* rec_flags = reinterpret_cast<uint8_t*>(sp + blk_bytes + tile_bytes);
-  WalkEntry* entries = reinterpret_cast<WalkEntry*>(sp + blk_bytes + tile_bytes + flag_bytes);
+  char* segp = sp + blk_bytes + tile_bytes + flag_bytes;
+  gevws_conn_in* segs = reinterpret_cast<gevws_conn_in*>(segp);
+  gevws_conn_out* sout = reinterpret_cast<gevws_conn_out*>(segp + n_v * sizeof(gevws_conn_in));
+  uint8_t* srec = reinterpret_cast<uint8_t*>(segp + n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out)));
+  WalkEntry* entries = reinterpret_cast<WalkEntry*>(segp + seg_bytes);
   const bool timed = ctx->timing;
   hipEvent_t* ev = nullptr;
   if (timed) {
@@ -3279,7 +3746,20 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   // profiles/r02_steps_fused.jsonl).
   const bool fused = kFusedScan && nblk > 0 && nblk <= kFusedScanMaxBlocks;
   uint32_t* done = fused ? ctx->d_done : nullptr;
-  if (nblk && span) {
+  if (nblk && ks > 1) {
+    // (entry groups by the real connection count: the segments of one
+    // connection are one chain's worth of line traffic)
+    const bool grp = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
+#define GEVWS_SPLIT(K)                                                                                            \
+  (grp ? k_walk_split<K, 8, true> : k_walk_split<K, 8, false>)<<<nblk, kCountBlock, 0, st>>>(                     \
+      d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb_w, in_bytes, done, max_frames, payload_cap, \
+      d_summary, segs, sout, srec, ctx->split_mode)
+    if (ks == 2) GEVWS_SPLIT(2);
+    else if (ks == 4) GEVWS_SPLIT(4);
+    else if (ks == 8) GEVWS_SPLIT(8);
+    else GEVWS_SPLIT(16);
+#undef GEVWS_SPLIT
+  } else if (nblk && span) {
     if (wv == 7)
       k_walk_span<2><<<nblk, kSpanWaves * 64, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
                                                        in_bytes, done, max_frames, payload_cap, d_summary);
@@ -3345,19 +3825,29 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   if (!fused) k_scan_blocks<true, kDecFields><<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
   if (timed) GEVWS_HIP(hipEventRecord(ev[2], st));
   if (nblk) {
-    k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb);
-    uint64_t egrid = ((uint64_t)n_conns + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
+    k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb_w, ctx->d_stats);
+    ctx->stats_pending = true;
+    ctx->stats_conns = n_conns;
+    // the record pass walks the segments when the walk was split
+    const gevws_conn_in* e_conns = ks > 1 ? segs : d_conns;
+    const gevws_conn_out* e_out = ks > 1 ? sout : d_conn_out;
+    const uint8_t* e_rec = ks > 1 ? srec : rec_flags;
+    const gevws_conn_out* e_parent = ks > 1 ? d_conn_out : nullptr;
+    const uint32_t e_ks = ks > 1 ? ks : 0;
+    uint64_t egrid = (n_v + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
     if (egrid > 8 * (uint64_t)ctx->num_cus) egrid = 8 * (uint64_t)ctx->num_cus;
     if (ctx->emit_variant == 1)
-      k_walk_emit<4><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, d_summary,
-                                                              d_frames, tile_first, entries, ne, gshift, rec_flags);
+      k_walk_emit<4><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out, d_summary,
+                                                              d_frames, tile_first, entries, ne, gshift, e_rec,
+                                                              e_parent, e_ks);
     else if (ctx->emit_variant == 2)
       k_walk_emit<4, kEmitGroup, true><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(
-          d_in, d_conns, n_conns, d_conn_out, d_summary, d_frames, tile_first, entries, ne, gshift, rec_flags);
+          d_in, e_conns, (uint32_t)n_v, e_out, d_summary, d_frames, tile_first, entries, ne, gshift, e_rec, e_parent,
+          e_ks);
     else
-      k_walk_emit<4, kEmitGroup><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out,
+      k_walk_emit<4, kEmitGroup><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out,
                                                                           d_summary, d_frames, tile_first, entries,
-                                                                          ne, gshift, rec_flags);
+                                                                          ne, gshift, e_rec, e_parent, e_ks);
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[3], st));
   r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);

@@ -160,7 +160,13 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * GEVWS_TUNE_SMALL_BATCH the input size in bytes (default and maximum 65 536;
  * 0 = never) up to which a batch of at most 256 connections is decoded by ONE
  * kernel launch -- walk, scan, records and unmask in a single workgroup --
- * when every other knob is at its default and per-phase timing is off. */
+ * when every other knob is at its default and per-phase timing is off,
+ * GEVWS_TUNE_SPLIT_LANES the lanes per connection of the default walk's split
+ * form (k_walk_split: lanes guess frame starts inside the stream and walk
+ * the segments between the guesses; a connection whose guesses do not all
+ * line up is re-walked serially, so the output never depends on them): 0 =
+ * auto (the batch's connections x lanes up to 256 per CU, streams of >= 32 KiB
+ * mean), 1 = never, 2 / 4 / 8 / 16 = always. */
 #define GEVWS_TUNE_UNMASK_VARIANT 1
 #define GEVWS_TUNE_UNMASK_GRID 2
 #define GEVWS_TUNE_ENCODE_VARIANT 3
@@ -168,7 +174,15 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
 #define GEVWS_TUNE_SPAN_CONNS_PER_CU 5
 #define GEVWS_TUNE_EMIT_VARIANT 6
 #define GEVWS_TUNE_SMALL_BATCH 7
+#define GEVWS_TUNE_SPLIT_LANES 8
+#define GEVWS_TUNE_SPLIT_MODE 9  /* measurement: 1 = split guesses made then dropped, 2 = none made */
 int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
+/* Lanes per connection the last multi-kernel decode's header walk used (1 =
+ * not split; GEVWS_TUNE_SPLIT_LANES), -1 for a null context.  The auto choice
+ * splits a batch of few connections once an earlier decode on this context
+ * has shown long chains of small frames (>= 256 frames per connection of <= 4
+ * KiB each). */
+int gevws_ctx_last_split_lanes(const gevws_ctx *ctx);
 /* Human-readable name of a variant (GEVWS_TUNE_UNMASK_VARIANT or
  * GEVWS_TUNE_WALK_VARIANT), or NULL past the last one. */
 const char *gevws_tuning_name(int key, int64_t value);

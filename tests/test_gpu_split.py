@@ -1,0 +1,174 @@
+"""Split header walk (k_walk_split, GEVWS_TUNE_SPLIT_LANES): lanes guess frame
+starts inside long streams and walk the segments between guesses; a
+connection is accepted only when every segment ends exactly on the next
+guess, else it is re-walked serially.  Whatever the guesses, the output must
+be the serial chain's: every case below is compared with the oracle
+(oracle/ws_ref.c) record by record, byte by byte, per connection and in the
+summary (run_frames included), for every lane count and the auto choice.
+
+The cases aim at each way a guess can go: small frames (guesses confirmed),
+big frames (no header near a split point), a payload that carries a
+plausible embedded frame chain (a confirmed guess that is NOT a frame start),
+noise, an ERR_LEN_MSB header mid-stream, 2-5 byte frames (the avail < 6
+rule at a segment's end), uniform frames (run_frames stitched across
+segments), partial tails, unordered tables and streams outside the arena."""
+import numpy as np
+import pytest
+
+from oracle import ref
+from oracle import ws_oracle as wo
+from tests._helpers import assert_matches_oracle, gpu_decode, host_result, pack_streams
+
+pytestmark = pytest.mark.gpu
+
+KEY = b"\x11\x22\x33\x44"
+
+
+def _frames(rng, nbytes, lens, masked=True, opcode=2):
+    """Frames with payload lengths drawn by lens(rng) until nbytes of stream."""
+    out, tot = [], 0
+    while tot < nbytes:
+        L = int(lens(rng))
+        f = wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), opcode, True, 0, masked,
+                            bytes(rng.integers(0, 256, 4, dtype=np.uint8)) if masked else KEY)
+        out.append(f)
+        tot += len(f)
+    return b"".join(out)
+
+
+def _power(rng):
+    u = rng.random()
+    return min(int(64 * (1 - u * (1 - (64 / (1 << 20)) ** 1.1)) ** (-1 / 1.1)), 1 << 20)
+
+
+def _tail(rng):
+    t = wo.encode_frame(bytes(300), 2, True, 0, True, KEY)
+    return t[: int(rng.integers(1, len(t)))]
+
+
+def _cases():
+    rng = np.random.default_rng(0x5911)
+    cases = {}
+    # long chains of small frames, some with a partial last frame
+    small = [_frames(rng, int(rng.integers(40_000, 300_000)), lambda r: r.integers(0, 200))
+             + (_tail(rng) if k % 3 == 0 else b"") for k in range(48)]
+    cases["small"] = pack_streams(small)
+    # power-law frames 64 B .. 1 MiB (C4's mix)
+    cases["power"] = pack_streams([_frames(rng, int(rng.integers(100_000, 1_500_000)), _power) for _ in range(24)])
+    # an unmasked first frame whose payload is itself a plausible stream of
+    # unmasked frames: split points inside it confirm guesses that are not
+    # frame starts
+    fake = []
+    for k in range(12):
+        inner = _frames(rng, int(rng.integers(60_000, 120_000)), lambda r: r.integers(0, 120), masked=False)
+        outer = wo.encode_frame(inner, 2, True, 0, False, KEY)
+        fake.append(outer + _frames(rng, int(rng.integers(0, 80_000)), lambda r: r.integers(0, 120), masked=False))
+    cases["embedded_chain"] = pack_streams(fake)
+    # noise: headers parsed from random bytes
+    cases["noise"] = pack_streams([bytes(rng.integers(0, 256, int(rng.integers(33_000, 200_000)), dtype=np.uint8))
+                                   for _ in range(16)])
+    # ERR_LEN_MSB header in the middle of a long small-frame chain
+    msb = bytes([0x82, 0xFF, 0x80, 0, 0, 0, 0, 0, 0, 5, 1, 2, 3, 4]) + b"hello"
+    errs = []
+    for _ in range(8):
+        a = _frames(rng, int(rng.integers(30_000, 150_000)), lambda r: r.integers(0, 150))
+        b = _frames(rng, int(rng.integers(30_000, 150_000)), lambda r: r.integers(0, 150))
+        errs.append(a + msb + b)
+    cases["len_msb"] = pack_streams(errs)
+    # 2..5-byte unmasked frames: a segment's last frames meet avail < 6
+    tiny = [_frames(rng, int(rng.integers(33_000, 90_000)), lambda r: r.integers(0, 4), masked=False)
+            for _ in range(10)]
+    cases["tiny"] = pack_streams(tiny)
+    # uniform frames (run_frames counts pairs across segment boundaries)
+    cases["uniform"] = pack_streams([_frames(rng, 200_000, lambda r: 100) for _ in range(20)]
+                                    + [_frames(rng, 300_000, lambda r: 4096) for _ in range(8)])
+    # mixed: short and empty connections between long ones
+    mixed = []
+    for k in range(60):
+        if k % 4 == 0:
+            mixed.append(b"")
+        elif k % 4 == 1:
+            mixed.append(_frames(rng, int(rng.integers(1, 3000)), lambda r: r.integers(0, 300)))
+        else:
+            mixed.append(_frames(rng, int(rng.integers(32_768, 250_000)), lambda r: r.integers(0, 500)))
+    cases["mixed"] = pack_streams(mixed)
+    arena, conns = cases["small"]
+    cases["unordered"] = (arena, conns[rng.permutation(conns.shape[0])])
+    return cases
+
+
+@pytest.fixture(scope="module")
+def split_cases():
+    return _cases()
+
+
+@pytest.mark.parametrize("lanes", [0, 2, 4, 8, 16])
+def test_split_walk_matches_oracle(engine, split_cases, lanes):
+    from gev_amd import _abi
+    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 0)
+    engine.set_tuning(_abi.TUNE_SPLIT_LANES, lanes)
+    try:
+        for name, (arena, conns) in split_cases.items():
+            assert_matches_oracle(engine, arena, conns, f"split lanes {lanes}: {name}")
+    finally:
+        engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+
+
+def test_split_walk_streams_outside_the_arena(engine, split_cases):
+    """Out-of-arena rows in a split batch: GEVWS_ERR_INVALID, nothing read,
+    the long connections around them exact."""
+    import gev_amd
+    from gev_amd import _abi
+    arena, conns = split_cases["small"]
+    n = len(arena)
+    bad = np.array([[n - 4, 10], [n + 100, 70_000], [1 << 62, 1 << 62]], np.int64)
+    table = np.concatenate([conns[:3], bad[:1], conns[3:5], bad[1:], conns[5:]])
+    engine.set_tuning(_abi.TUNE_SPLIT_LANES, 8)
+    try:
+        got = host_result(gpu_decode(engine, arena, table))
+    finally:
+        engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
+    st = got["conn_out"]["status"]
+    assert list(st[[3, 6, 7]]) == [gev_amd.ERR_INVALID] * 3
+    assert int(got["summary"]["errors"]) == 3
+    want = ref.decode_batch(np.frombuffer(arena, np.uint8).copy(), conns[:, 0], conns[:, 1])
+    assert got["frames"].tobytes() == want["frames"].tobytes()
+    assert np.array_equal(got["payload"], want["payload"])
+
+
+def test_split_lanes_knob_bounds(engine):
+    from gev_amd import _abi
+    for bad in (-1, 3, 6, 32):
+        with pytest.raises(ValueError):
+            engine.set_tuning(_abi.TUNE_SPLIT_LANES, bad)
+    engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
+
+
+def test_split_walk_auto_choice(engine, split_cases):
+    """Auto (GEVWS_TUNE_SPLIT_LANES 0): a context splits a batch of few long
+    connections once a finished decode on it showed long chains of small
+    frames -- not on its first batch, not after big frames -- and the split
+    decode is exact."""
+    import torch
+    from gev_amd import _abi
+    rng = np.random.default_rng(77)
+    longs = pack_streams([_frames(rng, 300_000, lambda r: r.integers(0, 200)) for _ in range(64)])
+    bigs = pack_streams([_frames(rng, 300_000, lambda r: 8192) for _ in range(64)])
+    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 0)
+    try:
+        assert_matches_oracle(engine, *bigs, "auto: big frames")
+        torch.cuda.synchronize()
+        assert_matches_oracle(engine, *longs, "auto: after big frames")
+        assert engine.last_split_lanes == 1
+        torch.cuda.synchronize()
+        assert_matches_oracle(engine, *longs, "auto: after long chains")
+        assert engine.last_split_lanes == 16
+        torch.cuda.synchronize()
+        assert_matches_oracle(engine, *bigs, "auto: big frames after long chains")
+        assert engine.last_split_lanes == 16  # the previous batch decides
+        torch.cuda.synchronize()
+        assert_matches_oracle(engine, *bigs, "auto: big frames again")
+        assert engine.last_split_lanes == 1
+    finally:
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
