@@ -368,7 +368,7 @@ def _oracle_compare_conns(engine, out, arena, layout, idx):
     return int(wf.shape[0])
 
 
-def _c4_full(engine, lay, n_check: int = 64):
+def _c4_full(engine, lay, n_check: int = 64, expect_split=None):
     """BASELINE config 4 at its configured size (or an LPT share of it): every
     byte by the generator property, plus >= n_check connections -- the longest
     chain among them -- byte-compared with the oracle."""
@@ -387,6 +387,8 @@ def _c4_full(engine, lay, n_check: int = 64):
     out = engine.decode(arena, lay.arena_bytes, conns, lay.n_conns, max_frames=lay.n_frames,
                         payload_cap=lay.payload_padded)
     s = out.summary_host()
+    if expect_split is not None:  # which header walk ran (k_walk_split: lanes per connection)
+        assert engine.last_split_lanes == expect_split, (lay.name, engine.last_split_lanes)
     assert int(s["frames"]) == lay.n_frames and int(s["payload_len"]) == lay.payload_len
     assert int(s["payload_bytes"]) == lay.payload_padded and int(s["errors"]) == 0 and int(s["flags"]) == 0
     from gev_amd import workloads as wl
@@ -411,16 +413,20 @@ def test_c4_full_size_and_lpt_shards(engine):
     """BASELINE config 4 exactly as bench.py builds it (16 GiB power-law
     payload over 65 536 connections, 43.8 M frames) on one GPU, then rank 0's
     and rank 7's greedy-LPT shares of the 8-way strong split."""
+    import torch
     import bench
     from gev_amd import workloads as w
     glob, _ = bench.build_layout("c4", 0, None)
     assert glob.payload_len >= 16 << 30 and glob.n_conns == 65536
-    longest, nf, k = _c4_full(engine, glob)
+    longest, nf, k = _c4_full(engine, glob, expect_split=1)
     assert longest > 1000 and k >= 64 and nf > 0
+    # the 8-way shares after the full batch: the auto choice splits their walk
+    # (16 lanes per connection, k_walk_split) on the full batch's history
     for r in (0, 7):
         part = w.shard_lpt(glob, r, 8)
         assert part.n_conns == 65536 // 8 or abs(part.n_conns - 65536 // 8) < 65536 // 16
-        _c4_full(engine, part)
+        ncu = torch.cuda.get_device_properties(engine.device).multi_processor_count
+        _c4_full(engine, part, expect_split=16 if part.n_conns <= 32 * ncu else None)
 
 
 def test_c4_power_law_property(engine):
