@@ -341,6 +341,15 @@ class Engine:
         if st != OK:
             raise RuntimeError(status_string(st))
 
+    def gather_(self, src, nbytes: int, lanes: int, per_lane: int, dependent: bool, sink, seed: int = 1,
+                stream=None) -> None:
+        """gevws_gather_async: the header walk's random-line fetch ceiling (measurement only)."""
+        assert nbytes <= src.numel() and sink.numel() >= lanes
+        st = lib.gevws_gather_async(self._ctx, _stream_handle(stream), src.data_ptr(), nbytes, lanes, per_lane,
+                                    1 if dependent else 0, seed, sink.data_ptr())
+        if st != OK:
+            raise RuntimeError(status_string(st))
+
     # -------------------------------------------------------------- synthetic batches
     def synth(self, arena, desc_dev, n_frames: int, seed: int, stream=None) -> None:
         st = lib.gevws_synth_async(self._ctx, _stream_handle(stream), arena.data_ptr(), desc_dev.data_ptr(),

@@ -203,6 +203,8 @@ SIGNATURES = {
     "gevws_protocol_unpacket_batch": (ctypes.c_int64, [P, P, P, ctypes.c_uint32]),
     "gevws_protocol_packet": (U8P, [P, P, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "gevws_copy_async": (ctypes.c_int, [P, P, P, P, ctypes.c_uint64, ctypes.c_uint32]),
+    "gevws_gather_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                          ctypes.c_uint64, P]),
     "gevws_pinned_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(P), ctypes.POINTER(P)]),
     "gevws_pinned_free": (ctypes.c_int, [P]),
     "gevws_upgrader_new": (P, []),

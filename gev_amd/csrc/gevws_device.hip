@@ -1350,6 +1350,43 @@ __global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __
   if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x < kDecFields);
 }
 
+// ------------------------------------------------------------------ 1b. gather ceiling (measurement)
+// The header walk's access pattern without its parsing: every lane fetches
+// `per_lane` 16-byte windows at random 128-byte lines of an n-byte buffer.
+// DEP: each address depends on the previous load's data (a chain, one load in
+// flight per lane, like the walk); else the lane issues 8 independent loads
+// at a time -- the random-line fetch rate of HBM, the walk's roofline.
+template <bool DEP>
+__global__ __launch_bounds__(kCountBlock) void k_gather(const uint8_t* __restrict__ in, uint64_t lines,
+                                                        uint32_t per_lane, uint64_t seed, uint64_t* __restrict__ sink) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t x = seed ^ (g * 0x9E3779B97F4A7C15ull), acc = 0;
+  auto mix = [](uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  if constexpr (DEP) {
+    for (uint32_t k = 0; k < per_lane; ++k) {
+      x = mix(x + acc);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(in + (x % lines) * 128 + ((x >> 60) & 7) * 16);
+      acc = (uint64_t)(v[0] & 1u);  // the next address waits for this load's data
+    }
+  } else {
+    for (uint32_t k = 0; k < per_lane; k += 8) {
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t z = mix(x + k + j);
+        v[j] = *reinterpret_cast<const u32x4*>(in + (z % lines) * 128 + ((z >> 60) & 7) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += v[j][0];
+    }
+  }
+  sink[g] = acc;
+}
+
 // ------------------------------------------------------------------ 2. scan of block partials
 // SPLIT (decode): field 3 holds errors in its low 32 bits and the count of
 // out-of-order connections in its high 32 (k_walk_count) -> summary.errors and
@@ -3964,6 +4001,18 @@ int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t
   else
     (plain ? k_copy_stream<16, false, false> : k_copy_stream<16, false>)<<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst,
                                                                                                         n);
+  GEVWS_HIP(hipGetLastError());
+  return GEVWS_OK;
+}
+
+int gevws_gather_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64_t in_bytes, uint32_t lanes,
+                       uint32_t per_lane, int dependent, uint64_t seed, uint64_t* d_sink) {
+  if (!ctx || !d_in || !d_sink || in_bytes < 128 || lanes == 0 || (lanes % kCountBlock) || (per_lane % 8))
+    return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  (dependent ? k_gather<true> : k_gather<false>)<<<lanes / kCountBlock, kCountBlock, 0, st>>>(
+      d_in, in_bytes / 128, per_lane, seed, d_sink);
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;
 }

@@ -281,6 +281,17 @@ int gevws_dispatch_async(gevws_ctx *ctx, void *stream, const gevws_frame *d_fram
 int gevws_copy_async(gevws_ctx *ctx, void *stream, uint8_t *d_dst, const uint8_t *d_src, uint64_t n,
                      uint32_t grid);
 
+/* Measurement helper, not on the reference path: the header walk's access
+ * pattern without its parsing -- `lanes` lanes (a multiple of 64), each
+ * fetching `per_lane` (a multiple of 8) 16-byte windows at random 128-byte
+ * lines of d_in[0, in_bytes); `dependent` != 0 makes each address depend on
+ * the previous load's data (one load in flight per lane, as in the walk),
+ * else 8 independent loads are in flight per lane.  One u64 per lane is
+ * written to d_sink.  bench / tools use it as the walk's random-line fetch
+ * ceiling. */
+int gevws_gather_async(gevws_ctx *ctx, void *stream, const uint8_t *d_in, uint64_t in_bytes, uint32_t lanes,
+                       uint32_t per_lane, int dependent, uint64_t seed, uint64_t *d_sink);
+
 /* Host-ingress helper, not on the reference path: `bytes` of page-locked host
  * memory mapped into the device address space (hipHostMallocMapped).
  * *host_ptr is the CPU address, *dev_ptr the address kernels use; passing
