@@ -23,7 +23,12 @@ sample of the same workload.
 
 Measurement options (not the contract line's defaults): --inflight M (M
 batches in flight on M streams), --emulate-shard R/N (rank R's LPT share of an
-N-way strong split, on one GPU), --walk-variant / --unmask-variant (A/B).
+N-way strong split, on one GPU), --walk-variant / --unmask-variant /
+--emit-variant / --split-lanes (A/B), --split-mode (split-walk cost breakdown).
+The split header walk's auto choice (GEVWS_TUNE_SPLIT_LANES 0) looks at the
+previous finished decode on the context: the untimed verify decode walks
+unsplit, the warmup and timed steps split when that decode showed long chains
+of small frames on few connections (C4's 8-way share).
 """
 from __future__ import annotations
 
