@@ -184,6 +184,11 @@ class Engine:
             raise ValueError(f"set_tuning({key}, {value}): {status_string(st)}")
 
     @property
+    def last_unmask_grid(self) -> int:
+        """Workgroups of the last multi-kernel decode's unmask launch."""
+        return int(lib.gevws_ctx_last_unmask_grid(self._ctx))
+
+    @property
     def last_split_lanes(self) -> int:
         """Lanes per connection of the last multi-kernel decode's header walk (1 = not split)."""
         return int(lib.gevws_ctx_last_split_lanes(self._ctx))

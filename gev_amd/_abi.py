@@ -170,6 +170,7 @@ SIGNATURES = {
     "gevws_ctx_set_timing": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_ctx_set_tuning": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_last_split_lanes": (ctypes.c_int, [P]),
+    "gevws_ctx_last_unmask_grid": (ctypes.c_int, [P]),
     "gevws_tuning_name": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32)]),
     "gevws_decode_batch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,

@@ -1449,6 +1449,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_co
   if (stats && blockIdx.x == 0 && threadIdx.x == 0) {  // the split walk's history (see decode_split_lanes)
     stats[0] = sum->frames;
     stats[1] = sum->payload_len;
+    stats[2] = sum->run_frames;
   }
   if (sum->status != GEVWS_OK) return;  // capacity error: nothing written
   const uint32_t c = blockIdx.x * cpb + threadIdx.x;
@@ -1878,10 +1879,27 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
 // with 4 workgroups per CU and, for big frames, all but the first `big_grid`
 // return at once.  big_grid = 0 disables the adaptation (explicit grid).
 constexpr uint64_t kBigFrameBytes = 48 * 1024;
+// k_unmask_auto's wide grid (kWideGridPerCU workgroups per CU instead of 4),
+// launched when the context's previous decode was a batch of mixed frame
+// sizes (v4) below kWideGridTiles output tiles: there the contiguous runs of
+// 4 workgroups per CU finish unevenly (the window path's cost follows the
+// local frame density) and more, shorter runs balance -- C4's 8-way share
+// (590 K tiles) 1.15 -> 0.99 ms, its 4-way share (1.2 M) 2.15 -> 2.09; the
+// 2-way share (2.4 M), the full C4 (4.7 M tiles), C2, C3, C5 are best at 4
+// per CU (profiles/r02_grid_sweep.jsonl)
+constexpr uint32_t kWideGridPerCU = 32;
+constexpr uint64_t kWideGridTiles = 2ull << 20;
 
-__device__ __forceinline__ uint32_t active_groups(uint64_t total, uint64_t nframes, uint32_t big_grid) {
-  if (big_grid == 0 || gridDim.x <= big_grid || nframes == 0) return gridDim.x;
-  return total / nframes >= kBigFrameBytes ? big_grid : gridDim.x;
+// Workgroups that take a run of the output: big_grid (low 16 bits: one per CU)
+// for batches of big frames, else the whole grid -- or, when the host
+// launched a wide grid (k_unmask_auto; high 16 bits: the usual grid), the
+// usual grid unless the caller asks for the wide one.
+__device__ __forceinline__ uint32_t active_groups(uint64_t total, uint64_t nframes, uint32_t big_grid,
+                                                  bool wide = false) {
+  const uint32_t ncu = big_grid & 0xffffu, norm = big_grid >> 16;
+  if (ncu == 0 || gridDim.x <= ncu || nframes == 0) return gridDim.x;
+  if (total / nframes >= kBigFrameBytes) return ncu;
+  return (norm == 0 || wide || gridDim.x <= norm) ? gridDim.x : norm;
 }
 
 // Largest frame index f in [tile_first[t], tile_first[t+1]] with payload_off <= p.
@@ -2169,7 +2187,7 @@ template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles, bool IS = f
 __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
-                                               uint32_t big_grid, const WinLds& L) {
+                                               uint32_t big_grid, const WinLds& L, bool wide = false) {
   uint32_t* const s_start = L.start;
   int32_t* const s_lend = L.lend;
   uint64_t* const s_delta = L.delta;
@@ -2178,7 +2196,7 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
   const uint64_t total = sum->payload_bytes;
   const uint64_t nframes = sum->frames;
   const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint32_t groups = active_groups(total, nframes, big_grid);
+  const uint32_t groups = active_groups(total, nframes, big_grid, wide);
   if (blockIdx.x >= groups) return;
   const uint64_t per = (ntiles + groups - 1) / groups;
   uint64_t t = (uint64_t)blockIdx.x * per;
@@ -2342,7 +2360,7 @@ template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = fa
 __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
-                                               uint32_t big_grid, const WinLds& L) {
+                                               uint32_t big_grid, const WinLds& L, bool wide = false) {
   uint32_t* const s_start = L.start;
   int32_t* const s_lend = L.lend;
   uint64_t* const s_delta = L.delta;
@@ -2351,7 +2369,7 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
   const uint64_t total = sum->payload_bytes;
   const uint64_t nframes = sum->frames;
   const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint32_t groups = active_groups(total, nframes, big_grid);
+  const uint32_t groups = active_groups(total, nframes, big_grid, wide);
   if (blockIdx.x >= groups) return;
   const uint64_t per = (ntiles + groups - 1) / groups;
   uint64_t t = (uint64_t)blockIdx.x * per;
@@ -2552,8 +2570,9 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   const WinLds L{s_start, s_lend, s_delta, s_key};
   if (2 * sum->run_frames >= sum->frames)  // frames the size of their predecessor on the connection
     unmask_v3_body<16, false, true, 2, kWinTiles, IS, NTA, NTW>(in, frames, tile_first, sum, out, big_grid, L);
-  else
-    unmask_v4_body<16, 8, true, false, true, false, IS, NTA, NTW>(in, frames, tile_first, sum, out, big_grid, L);
+  else  // mixed sizes: the whole (wide) grid for a batch of fewer than kWideGridTiles tiles
+    unmask_v4_body<16, 8, true, false, true, false, IS, NTA, NTW>(in, frames, tile_first, sum, out, big_grid, L,
+                                                                   sum->payload_bytes / kTile < kWideGridTiles);
 }
 
 // ------------------------------------------------------------------ outbound encode (§8f row 1)
@@ -3393,6 +3412,8 @@ struct gevws_ctx {
   uint64_t* d_stats = nullptr;
   bool stats_pending = false, stats_known = false;
   uint64_t stats_conns = 0, prev_frames_per_conn = 0, prev_frame_bytes = 0;
+  bool prev_mixed = false;
+  uint32_t last_unmask_grid = 0;  // workgroups of the last decode's unmask launch
   uint32_t last_ks = 1;    // lanes per connection of the last multi-kernel decode's walk
   int split_mode = 0;       // measurement: 1 = guesses made then dropped, 2 = no guesses
   uint32_t split_lanes = 0;  // walk variant 0: lanes per connection (k_walk_split); 0 = auto, 1 = off
@@ -3473,13 +3494,15 @@ struct UnmaskVariant {
   UnmaskFn fn;
   int unroll;
   const char* name;
+  bool wide = false;  // may launch the wide grid (k_unmask_auto)
 };
 // Variant 0 is the default; the others are kept for A/B measurement
 // (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 const UnmaskVariant kUnmaskVariants[] = {
     {k_unmask_auto<false, true, true>, 16,
      "auto: v3 4-tile windows for batches of equal-size frames, v4 pipelined 8-tile windows otherwise (summary "
-     "statistics of the walk); non-temporal streaming and window loads"},
+     "statistics of the walk); non-temporal streaming and window loads; a wide grid for a smaller batch of "
+     "mixed sizes after one on this context", true},
     {k_unmask_v4<16, 8, true>, 16,
      "v4 U16 streaming (aligned loads, DPP rotate) + pipelined 8-tile LDS window (next step's tile map and "
      "records fetched during the current window's payload loads)"},
@@ -3659,6 +3682,8 @@ const char* gevws_tuning_name(int key, int64_t value) {
 
 int gevws_ctx_last_split_lanes(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_ks : -1; }
 
+int gevws_ctx_last_unmask_grid(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_unmask_grid : -1; }
+
 int gevws_ctx_set_timing(gevws_ctx* ctx, int enable) {
   if (!ctx) return GEVWS_ERR_INVALID;
   ctx->timing = enable != 0;
@@ -3726,6 +3751,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     const uint64_t fr = ctx->h_stats[0], pl = ctx->h_stats[1];
     ctx->prev_frames_per_conn = ctx->stats_conns ? fr / ctx->stats_conns : 0;
     ctx->prev_frame_bytes = fr ? pl / fr : 0;
+    ctx->prev_mixed = 2 * ctx->h_stats[2] < fr;  // k_unmask_auto's v4 choice
   }
   if (!span && wv == 0 && n_conns) {
     if (ctx->split_lanes >= 2) {
@@ -4089,11 +4115,20 @@ static int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, c
                   uint8_t* d_payload) {
   const UnmaskVariant& v = kUnmaskVariants[ctx->unmask_variant];
   const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
-  uint64_t grid = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : 4 * (uint64_t)ctx->num_cus;
+  const uint64_t norm = 4 * (uint64_t)ctx->num_cus;
+  // the wide grid (kWideGridPerCU per CU) when the previous decode on this
+  // context was a batch of mixed sizes (run frames < half) below
+  // kWideGridTiles; the kernel still uses `norm` workgroups unless this
+  // batch is one too
+  const bool wide = v.wide && !ctx->unmask_grid && ctx->stats_known && ctx->prev_mixed &&
+                    ntiles < kWideGridTiles && norm <= 0xffffu;
+  uint64_t grid = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : wide ? kWideGridPerCU * (uint64_t)ctx->num_cus : norm;
   const uint64_t useful = (ntiles + v.unroll - 1) / v.unroll;
   if (grid > useful) grid = useful;
   if (grid < 1) grid = 1;
+  ctx->last_unmask_grid = (uint32_t)grid;
   v.fn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary, d_payload,
-                                                ctx->unmask_grid ? 0u : (uint32_t)ctx->num_cus);
+                                                ctx->unmask_grid ? 0u
+                                                                 : (uint32_t)ctx->num_cus | (wide ? (uint32_t)norm << 16 : 0u));
   return GEVWS_OK;
 }

@@ -183,6 +183,11 @@ int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
  * has shown long chains of small frames (>= 256 frames per connection of <= 4
  * KiB each). */
 int gevws_ctx_last_split_lanes(const gevws_ctx *ctx);
+/* Workgroups of the last multi-kernel decode's unmask launch (-1 for a null
+ * context): 4 per CU, or 32 per CU after a decode on this context of a batch
+ * of mixed frame sizes below 8 GiB of output (the kernel then uses the wide
+ * grid if this batch is one too). */
+int gevws_ctx_last_unmask_grid(const gevws_ctx *ctx);
 /* Human-readable name of a variant (GEVWS_TUNE_UNMASK_VARIANT or
  * GEVWS_TUNE_WALK_VARIANT), or NULL past the last one. */
 const char *gevws_tuning_name(int key, int64_t value);

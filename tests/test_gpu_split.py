@@ -172,3 +172,26 @@ def test_split_walk_auto_choice(engine, split_cases):
         assert engine.last_split_lanes == 1
     finally:
         engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+
+
+def test_wide_unmask_grid_after_mixed_batch(engine):
+    """The unmask's wide grid (32 workgroups per CU) is launched after a
+    finished decode of a mixed-size batch below 8 GiB of output, and the
+    kernel uses it only when this batch is mixed as well: both cases exact
+    (every byte by the generator property, leading connections against the
+    oracle)."""
+    import torch
+    from gev_amd import workloads as w
+    from tests.test_gpu_parity import _synth_decode_verify
+    mixed = w.config_c4(total_payload=512 << 20, n_conns=1024, seed=5)       # 131 K output tiles, v4
+    uniform = w.uniform(1024, 128, 4096, seed=6)                             # 512 MiB of 4 KiB frames, v3
+    ncu = torch.cuda.get_device_properties(engine.device).multi_processor_count
+    _synth_decode_verify(engine, uniform, check_slice_conns=4)
+    _synth_decode_verify(engine, mixed, check_slice_conns=4)
+    assert engine.last_unmask_grid <= 4 * ncu
+    _synth_decode_verify(engine, mixed, check_slice_conns=4)   # after a mixed batch: wide grid, used
+    assert engine.last_unmask_grid > 4 * ncu, engine.last_unmask_grid
+    _synth_decode_verify(engine, uniform, check_slice_conns=4)  # wide launch, the usual grid used
+    assert engine.last_unmask_grid > 4 * ncu
+    _synth_decode_verify(engine, uniform, check_slice_conns=4)
+    assert engine.last_unmask_grid <= 4 * ncu

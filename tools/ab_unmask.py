@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="all")
     ap.add_argument("--grids", default="1024")
+    ap.add_argument("--emulate-shard", default=None, metavar="R/N", help="rank R's LPT share of an N-way split")
     ap.add_argument("--walk-variants", default="0", help="header walk variants to cross with the unmask variants")
     ap.add_argument("--align-payload", action="store_true",
                     help="experiment: C3-sized frames whose payloads start 16-byte aligned in the input")
@@ -40,6 +41,10 @@ def main():
     dev = torch.device("cuda", 0)
     eng = gev_amd.Engine(0)
     lay, _ = bench.build_layout(args.config, 0, args.conns)
+    if args.emulate_shard:  # rank R's LPT share of an N-way strong split (bench.py --emulate-shard)
+        from gev_amd import workloads as w
+        r, n = (int(x) for x in args.emulate_shard.split("/"))
+        lay = w.shard_lpt(lay, r, n)
     if args.align_payload:
         # L = 65538 (16-byte multiple frame size with h = 14) and every stream
         # shifted by 2 bytes: payload starts land on 16-byte boundaries
