@@ -1525,6 +1525,7 @@ __device__ __forceinline__ WalkEntry ld_entry(const WalkEntry* p) {
 }
 
 constexpr int kEmitGroup = 16;
+constexpr uint64_t kEmitSplitPerCU = 32;  // record-pass workgroups per CU over k_walk_split's rows
 // NTR (measurement): the entry loads and record stores non-temporal.
 template <int U, int G = 0, bool NTR = false>
 __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restrict__ in,
@@ -3898,7 +3899,10 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     const gevws_conn_out* e_parent = ks > 1 ? d_conn_out : nullptr;
     const uint32_t e_ks = ks > 1 ? ks : 0;
     uint64_t egrid = (n_v + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
-    if (egrid > 8 * (uint64_t)ctx->num_cus) egrid = 8 * (uint64_t)ctx->num_cus;
+    // (split rows: each row is a chain of ~100 frames whose entries cost a
+    // load round trip, so more waves share them out)
+    const uint64_t ecap = (ks > 1 ? kEmitSplitPerCU : 8) * (uint64_t)ctx->num_cus;
+    if (egrid > ecap) egrid = ecap;
     if (ctx->emit_variant == 1)
       k_walk_emit<4><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out, d_summary,
                                                               d_frames, tile_first, entries, ne, gshift, e_rec,
