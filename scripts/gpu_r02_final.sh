@@ -10,4 +10,4 @@ bash scripts/gpu_r02_full.sh || exit 1
 run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 run bench 600 python bench.py || exit 1
 tail -c 1500 $OUT/bench.log
-CONFIGS="c3 c4" PREFIX=r02f STEPS=5 bash scripts/gpu_pmc_split.sh || exit 1
+CONFIGS="c3 c4" PREFIX=${PREFIX:-r02f} STEPS=5 bash scripts/gpu_pmc_split.sh || exit 1
