@@ -3964,7 +3964,9 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(n, blk, d_summary, d_out_off, tile_first);
   const uint64_t per_cu = (ctx->encode_variant == 0 || ctx->encode_variant >= 4) ? 7 : 4;  // LDS-light: 7 per CU
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
-  if (grid > per_cu * (uint64_t)ctx->num_cus) grid = per_cu * (uint64_t)ctx->num_cus;
+  // (GEVWS_TUNE_UNMASK_GRID, when set, caps the encode's grid too: measurement)
+  const uint64_t gcap = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : per_cu * (uint64_t)ctx->num_cus;
+  if (grid > gcap) grid = gcap;
   if (grid < 1) grid = 1;
   // every frame boundary takes the window path, which needs several
   // workgroups per CU to hide its latency (C3: 22.6 ms at 4/CU vs 36 ms at

@@ -132,7 +132,8 @@ int gevws_ctx_device(const gevws_ctx *ctx);
 void *gevws_ctx_stream(const gevws_ctx *ctx);
 /* Tuning knobs for measurement (defaults are the tuned choice):
  * GEVWS_TUNE_UNMASK_VARIANT selects an unmask kernel variant (0 = default),
- * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto), GEVWS_TUNE_ENCODE_VARIANT
+ * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto; when set it caps the
+ * encode's grid too), GEVWS_TUNE_ENCODE_VARIANT
  * the encode kernel (0 = aligned non-temporal loads + register realign while streaming;
  * in frame windows all payload loads issued before the stores, and every
  * 64-byte group that holds a frame boundary queued whole and written by one

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="0", help="encode variants to A/B, e.g. 0,1 (interleaved rounds)")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--grids", default="0", help="encode grid caps to A/B (GEVWS_TUNE_UNMASK_GRID; 0 = the default)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -74,21 +75,25 @@ def main():
             assert torch.equal(wire[:wire_total], ref_wire[:wire_total]), f"encode variant {v} differs"
         del ref_wire
         torch.cuda.empty_cache()
-    times = {v: [] for v in variants}
+    grids = [int(x) for x in args.grids.split(",")]
+    cfgs = [(v, g) for v in variants for g in grids]
+    times = {c: [] for c in cfgs}
     for rnd in range(args.rounds):
-        for v in (variants if rnd % 2 == 0 else variants[::-1]):  # alternate the order (position bias)
+        for v, g in (cfgs if rnd % 2 == 0 else cfgs[::-1]):  # alternate the order (position bias)
             eng.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, v)
+            eng.set_tuning(gev_amd._abi.TUNE_UNMASK_GRID, g)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(args.reps):
                 eng.encode_async(d_rep, lay.n_frames, out.payload, wire, wire_total, off, summ)
             e1.record()
             torch.cuda.synchronize()
-            times[v].append(e0.elapsed_time(e1) / args.reps)
+            times[(v, g)].append(e0.elapsed_time(e1) / args.reps)
     eng.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, 0)
-    for v in variants:
-        ms = sorted(times[v])[len(times[v]) // 2]
-        print(json.dumps({"path": "encode (FrameToBytes of NewBinaryFrame replies)", "variant": v,
+    eng.set_tuning(gev_amd._abi.TUNE_UNMASK_GRID, 0)
+    for v, g in cfgs:
+        ms = sorted(times[(v, g)])[len(times[(v, g)]) // 2]
+        print(json.dumps({"path": "encode (FrameToBytes of NewBinaryFrame replies)", "variant": v, "grid": g,
                           "workload": lay.name, "frames": lay.n_frames, "wire_bytes": wire_total,
                           "ms": round(ms, 4),
                           "payload_GiBps": round(int(L.sum()) / (ms / 1e3) / 2**30, 2),
