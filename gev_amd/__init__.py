@@ -682,6 +682,26 @@ class Protocol:
             raise RuntimeError(f"unpacket_batch: {status_string(int(r))}")
         return int(r)
 
+    def unpacket_batch_begin(self, conns: Sequence[Connection], buffers: Sequence[RingBuffer]) -> int:
+        """gevws_protocol_unpacket_batch_begin: stage and enqueue the pass, do not wait;
+        returns the connections in it."""
+        n = len(conns)
+        cs = (ctypes.c_void_p * n)(*[c._p for c in conns])
+        rs = (ctypes.c_void_p * n)(*[b._p for b in buffers])
+        self._pending = (cs, rs)  # the C side keeps the pointers until _end
+        r = lib.gevws_protocol_unpacket_batch_begin(self._p, cs, rs, n)
+        if r < 0:
+            raise RuntimeError(f"unpacket_batch_begin: {status_string(int(r))}")
+        return int(r)
+
+    def unpacket_batch_end(self) -> int:
+        """gevws_protocol_unpacket_batch_end: wait for the pass in flight and queue its frames."""
+        r = lib.gevws_protocol_unpacket_batch_end(self._p)
+        self._pending = None
+        if r < 0:
+            raise RuntimeError(f"unpacket_batch_end: {status_string(int(r))}")
+        return int(r)
+
     def set_zero_copy_max(self, nbytes: int) -> None:
         """gevws_protocol_set_zero_copy_max: batched passes over at most
         `nbytes` of input run on mapped host memory with no copies (0 = never)."""

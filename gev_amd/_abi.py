@@ -202,6 +202,8 @@ SIGNATURES = {
     "gevws_protocol_unpacket": (ctypes.c_int, [P, P, P, ctypes.POINTER(Header), ctypes.POINTER(U8P),
                                                ctypes.POINTER(ctypes.c_uint64)]),
     "gevws_protocol_unpacket_batch": (ctypes.c_int64, [P, P, P, ctypes.c_uint32]),
+    "gevws_protocol_unpacket_batch_begin": (ctypes.c_int64, [P, P, P, ctypes.c_uint32]),
+    "gevws_protocol_unpacket_batch_end": (ctypes.c_int64, [P]),
     "gevws_protocol_packet": (U8P, [P, P, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "gevws_copy_async": (ctypes.c_int, [P, P, P, P, ctypes.c_uint64, ctypes.c_uint32]),
     "gevws_gather_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,

@@ -174,6 +174,10 @@ class Protocol {
       c->upgraded = true;
       return GEVWS_HANDSHAKE;
     }
+    if (pend_.active) {  // a pass begun by BeginBatch finishes first
+      const int64_t r = EndBatch();
+      if (r < 0) return (int)r;
+    }
     if (c->queue.empty() && c->poisoned == GEVWS_OK) {
       if (Ready(c, ring)) {
         Connection* cs[1] = {c};
@@ -208,13 +212,28 @@ class Protocol {
 
   // One device pass over every listed connection that can make progress.
   int64_t UnPacketBatch(Connection* const* conns, RingBuffer* const* rings, uint32_t n) {
+    const int64_t r = BeginBatch(conns, rings, n);
+    if (r <= 0) return r;
+    return EndBatch();
+  }
+
+  // The pass of UnPacketBatch in two halves, so an event loop can read its
+  // sockets while the device decodes: BeginBatch selects, stages and enqueues
+  // the pass and its copies (no synchronisation) and returns the number of
+  // connections in it (0: nothing to do); EndBatch waits for it and queues the
+  // frames on their connections.  One pass in flight per protocol; between
+  // the two, the rings may take new bytes (the pass decodes its staged copy)
+  // but are not read; UnPacket ends a pass in flight first.
+  int64_t BeginBatch(Connection* const* conns, RingBuffer* const* rings, uint32_t n) {
+    if (pend_.active) return GEVWS_ERR_INVALID;
     // Skipped: connections that still hold undelivered frames (their ring
     // prefix is decoded already), poisoned ones, ones whose first undecoded
     // frame is not complete yet (the carried gate), and repeats of a
     // connection already taken by this call.
     ++epoch_;
-    std::vector<uint32_t> sel;
+    std::vector<uint32_t>& sel = pend_.sel;
     std::vector<gevws_host_conn> segs;
+    sel.clear();
     sel.reserve(n);
     for (uint32_t i = 0; i < n; ++i) {
       Connection* c = conns[i];
@@ -229,41 +248,57 @@ class Protocol {
     if (sel.empty()) return 0;
     const uint32_t m = (uint32_t)sel.size();
     DeviceScope scope(gevws_ctx_device(ctx_));
-    Staged sg;
+    pend_.sg = Staged{};
+    Staged& sg = pend_.sg;
     int64_t r = StageDecode(segs.data(), m, &sg, true);
     if (r < 0) return r;
-    std::shared_ptr<uint8_t> arena;
+    pend_.conns.assign(conns, conns + n);
+    pend_.rings.assign(rings, rings + n);
     if (sg.zc) {
-      r = Finish(&sg);
-      if (r < 0) return r;
-      arena = sg.arena;
-      return Deliver(conns, rings, sel, sg, arena);
-    }
-    // frames + payload land in pinned memory with the summary: one
-    // synchronisation for a pass whose output fits the first estimate
-    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
-    const uint64_t est_f = std::min<uint64_t>(sg.max_frames, sg.total / 48 + 2ull * m + 16);
-    const uint64_t est_p = std::min<uint64_t>(sg.payload_cap, sg.total + 16 * est_f + 16);
-    if (!grow_host(&h_out_, &h_out_cap_, est_f * sizeof(gevws_frame))) return fail();
-    arena = pool_->Acquire(est_p);
-    if (!arena) return fail();
-    if (hipMemcpyAsync(h_out_, d_frames_, est_f * sizeof(gevws_frame), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(arena.get(), d_payload_, est_p, hipMemcpyDeviceToHost, st) != hipSuccess)
-      return fail();
-    r = Finish(&sg);
-    if (r < 0) return r;
-    const gevws_summary& sum = sg.sum;
-    const uint64_t fb = sum.frames * sizeof(gevws_frame);
-    if (sg.retried || sum.frames > est_f || sum.payload_bytes > est_p) {  // more than estimated: fetch it all
-      if (sum.payload_bytes > est_p && !(arena = pool_->Acquire(sum.payload_bytes))) return fail();
-      if (!grow_host(&h_out_, &h_out_cap_, fb)) return fail();
-      if ((fb && hipMemcpyAsync(h_out_, d_frames_, fb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-          (sum.payload_bytes &&
-           hipMemcpyAsync(arena.get(), d_payload_, sum.payload_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-          hipStreamSynchronize(st) != hipSuccess)
+      pend_.arena = sg.arena;
+    } else {
+      // frames + payload land in pinned memory with the summary: one
+      // synchronisation for a pass whose output fits the first estimate
+      hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+      pend_.est_f = std::min<uint64_t>(sg.max_frames, sg.total / 48 + 2ull * m + 16);
+      pend_.est_p = std::min<uint64_t>(sg.payload_cap, sg.total + 16 * pend_.est_f + 16);
+      if (!grow_host(&h_out_, &h_out_cap_, pend_.est_f * sizeof(gevws_frame))) return fail();
+      pend_.arena = pool_->Acquire(pend_.est_p);
+      if (!pend_.arena) return fail();
+      if (hipMemcpyAsync(h_out_, d_frames_, pend_.est_f * sizeof(gevws_frame), hipMemcpyDeviceToHost, st) !=
+              hipSuccess ||
+          hipMemcpyAsync(pend_.arena.get(), d_payload_, pend_.est_p, hipMemcpyDeviceToHost, st) != hipSuccess)
         return fail();
     }
-    return Deliver(conns, rings, sel, sg, arena);
+    pend_.active = true;
+    return (int64_t)m;
+  }
+
+  int64_t EndBatch() {
+    if (!pend_.active) return 0;
+    pend_.active = false;
+    DeviceScope scope(gevws_ctx_device(ctx_));
+    Staged& sg = pend_.sg;
+    std::shared_ptr<uint8_t> arena = std::move(pend_.arena);
+    int64_t r = Finish(&sg);
+    if (r < 0) return r;
+    if (sg.zc) {
+      arena = sg.arena;
+    } else {
+      hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+      const gevws_summary& sum = sg.sum;
+      const uint64_t fb = sum.frames * sizeof(gevws_frame);
+      if (sg.retried || sum.frames > pend_.est_f || sum.payload_bytes > pend_.est_p) {  // more than estimated
+        if (sum.payload_bytes > pend_.est_p && !(arena = pool_->Acquire(sum.payload_bytes))) return fail();
+        if (!grow_host(&h_out_, &h_out_cap_, fb)) return fail();
+        if ((fb && hipMemcpyAsync(h_out_, d_frames_, fb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+            (sum.payload_bytes &&
+             hipMemcpyAsync(arena.get(), d_payload_, sum.payload_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+            hipStreamSynchronize(st) != hipSuccess)
+          return fail();
+      }
+    }
+    return Deliver(pend_.conns.data(), pend_.rings.data(), pend_.sel, sg, arena);
   }
 
   // Hands a finished pass's frames to their connections in stream order and
@@ -534,6 +569,16 @@ class Protocol {
   }
 
   gevws_ctx* ctx_;
+  struct Pending {  // the pass between BeginBatch and EndBatch
+    bool active = false;
+    std::vector<Connection*> conns;
+    std::vector<RingBuffer*> rings;
+    std::vector<uint32_t> sel;
+    Staged sg;
+    std::shared_ptr<uint8_t> arena;
+    uint64_t est_f = 0, est_p = 0;
+  };
+  Pending pend_;
   const Upgrader* upgrader_ = nullptr;
   std::shared_ptr<PinnedPool> pool_;   // payload arenas handed out with the frames
   uint8_t *h_in_ = nullptr, *h_res_ = nullptr, *h_out_ = nullptr;  // pinned staging
@@ -594,6 +639,23 @@ int64_t gevws_protocol_unpacket_batch(gevws_protocol* p, gevws_conn* const* conn
     rs[i] = rings[i];
   }
   return p->UnPacketBatch(cs.data(), rs.data(), n);
+}
+
+int64_t gevws_protocol_unpacket_batch_begin(gevws_protocol* p, gevws_conn* const* conns, gevws_ring* const* rings,
+                                            uint32_t n) {
+  if (!p || (n && (!conns || !rings))) return GEVWS_ERR_INVALID;
+  std::vector<gevws::Connection*> cs(n);
+  std::vector<gevws::RingBuffer*> rs(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    cs[i] = conns[i];
+    rs[i] = rings[i];
+  }
+  return p->BeginBatch(cs.data(), rs.data(), n);
+}
+
+int64_t gevws_protocol_unpacket_batch_end(gevws_protocol* p) {
+  if (!p) return GEVWS_ERR_INVALID;
+  return p->EndBatch();
 }
 
 void gevws_protocol_get_stats(const gevws_protocol* p, gevws_protocol_stats* out) {

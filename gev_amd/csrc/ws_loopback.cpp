@@ -45,6 +45,18 @@ struct DeviceDecoder {
     }
     return gevws_protocol_unpacket_batch(p, bc.data(), br.data(), n);
   }
+  // the pass in two halves (gevws_protocol_unpacket_batch_begin / _end)
+  static constexpr bool kPipelined = true;
+  int64_t begin(wslb::ServerConn* const* conns, uint32_t n) {
+    bc.clear();
+    br.clear();
+    for (uint32_t i = 0; i < n; ++i) {
+      bc.push_back(conns[i]->c);
+      br.push_back(conns[i]->r);
+    }
+    return gevws_protocol_unpacket_batch_begin(p, bc.data(), br.data(), n);
+  }
+  int64_t end() { return gevws_protocol_unpacket_batch_end(p); }
   int unpacket(wslb::ServerConn* s, gevws_header* h, const uint8_t** data, uint64_t* len) {
     return gevws_protocol_unpacket(p, s->c, s->r, h, data, len);
   }

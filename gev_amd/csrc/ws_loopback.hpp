@@ -140,9 +140,59 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
   std::unordered_map<int, ServerConn> conns;
   std::vector<epoll_event> evs(4096);
   std::vector<uint8_t> rbuf(65536);  // the loop's packet buffer (eventloop.go:15)
-  std::vector<ServerConn*> readable, upgraded;
+  std::vector<ServerConn*> readable, upgraded, inflight;
+  // GEVWS_LB_PIPELINE=1 with a pipelined decoder (Decoder::kPipelined): the
+  // device pass of iteration k runs while iteration k+1 waits on epoll and
+  // reads its sockets, and its frames are echoed after those reads.  Measured
+  // slower than the serial loop (pass, then echo) with closed-loop clients
+  // (profiles/r02_loopback_pipeline_ab.jsonl): a connection only sends again
+  // once echoed, so the overlap splits the connections into two alternating
+  // passes of half the size, twice the fixed cost per pass -- default off.
+  const char* pe = getenv("GEVWS_LB_PIPELINE");
+  const bool pipeline = Decoder::kPipelined && pe && atoi(pe) == 1;
+  bool pending = false;
+  // handlerProtocol for one connection: UnPacket until (nil, nil), echo
+  auto handle = [&](ServerConn* s, double& t_dec) {
+    s->out.clear();
+    for (;;) {
+      gevws_header h;
+      const uint8_t* data = nullptr;
+      uint64_t len = 0;
+      const double tu = now_s();
+      const int st = dec.unpacket(s, &h, &data, &len);
+      t_dec += now_s() - tu;
+      if (st == GEVWS_OK) {
+        if (h.opcode & 0x8) continue;  // control frames: not in this workload
+        uint8_t hdr[14];
+        const uint32_t hn = write_header(hdr, 0x82, len);  // NewBinaryFrame + FrameToBytes
+        s->out.insert(s->out.end(), hdr, hdr + hn);
+        s->out.insert(s->out.end(), data, data + len);
+        g_frames.fetch_add(1, std::memory_order_relaxed);
+      } else if (len != 0) {
+        s->out.insert(s->out.end(), data, data + len);  // handshake response (wrap.go:40-42)
+      } else {
+        break;
+      }
+    }
+    if (!s->out.empty() && !send_all(s->fd, s->out.data(), s->out.size())) g_bad.fetch_add(1);
+  };
+  // the pass in flight, ended and its frames handed out (also before a
+  // connection it holds is closed: the protocol writes to its rings' owners)
+  auto finish = [&](double& t_dec) {
+    if (!pending) return;
+    const double td = now_s();
+    const int64_t f = dec.end();
+    t_dec += now_s() - td;
+    if (f < 0) {
+      fprintf(stderr, "ws_loopback: decoder pass %s\n", gevws_status_string((int)f));
+      exit(3);
+    }
+    pending = false;
+    for (ServerConn* s : inflight) handle(s, t_dec);
+  };
+  double t_close = 0;
   while (!g_stop.load(std::memory_order_relaxed)) {
-    const int n = epoll_wait(ep, evs.data(), (int)evs.size(), 5);
+    const int n = epoll_wait(ep, evs.data(), (int)evs.size(), pending ? 0 : 5);
     readable.clear();
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
@@ -166,6 +216,7 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
       const ssize_t k = ::read(fd, rbuf.data(), rbuf.size());  // one read per event (handleRead)
       if (k <= 0) {
         if (k < 0 && (errno == EAGAIN || errno == EINTR)) continue;
+        finish(t_close);
         epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
         close(fd);
         gevws_conn_free(it->second.c);
@@ -176,17 +227,25 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
       gevws_ring_write(it->second.r, rbuf.data(), (uint64_t)k);
       readable.push_back(&it->second);
     }
-    if (readable.empty()) continue;
-    upgraded.clear();
-    for (ServerConn* s : readable)
-      if (gevws_conn_upgraded(s->c)) upgraded.push_back(s);
     // decode time of the iteration: the pass plus the UnPacket calls (the
     // device decoder's UnPacket only pops queued frames; the CPU decoder's
     // does the whole per-frame pipeline), not the echo's encode or write(2)
-    double t_dec = 0;
+    double t_dec = t_close;
+    t_close = 0;
+    finish(t_dec);  // the pass begun last iteration: its frames go out now
+    if (readable.empty()) {
+      g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
+      continue;
+    }
+    upgraded.clear();
+    for (ServerConn* s : readable) {
+      if (gevws_conn_upgraded(s->c)) upgraded.push_back(s);
+      else if (pipeline) handle(s, t_dec);  // the handshake: no device pass involved
+    }
     if (!upgraded.empty()) {
       const double td = now_s();
-      const int64_t f = dec.pass(upgraded.data(), (uint32_t)upgraded.size());
+      const int64_t f = pipeline ? dec.begin(upgraded.data(), (uint32_t)upgraded.size())
+                                 : dec.pass(upgraded.data(), (uint32_t)upgraded.size());
       t_dec += now_s() - td;
       if (f < 0) {
         fprintf(stderr, "ws_loopback: decoder pass %s\n", gevws_status_string((int)f));
@@ -194,34 +253,16 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
       }
       g_batches.fetch_add(1, std::memory_order_relaxed);
       g_batch_conns.fetch_add(upgraded.size(), std::memory_order_relaxed);
-    }
-    // handlerProtocol per connection
-    for (ServerConn* s : readable) {
-      s->out.clear();
-      for (;;) {
-        gevws_header h;
-        const uint8_t* data = nullptr;
-        uint64_t len = 0;
-        const double tu = now_s();
-        const int st = dec.unpacket(s, &h, &data, &len);
-        t_dec += now_s() - tu;
-        if (st == GEVWS_OK) {
-          if (h.opcode & 0x8) continue;  // control frames: not in this workload
-          uint8_t hdr[14];
-          const uint32_t hn = write_header(hdr, 0x82, len);  // NewBinaryFrame + FrameToBytes
-          s->out.insert(s->out.end(), hdr, hdr + hn);
-          s->out.insert(s->out.end(), data, data + len);
-          g_frames.fetch_add(1, std::memory_order_relaxed);
-        } else if (len != 0) {
-          s->out.insert(s->out.end(), data, data + len);  // handshake response (wrap.go:40-42)
-        } else {
-          break;
-        }
+      if (pipeline && f > 0) {  // in flight: the next iteration reads its sockets meanwhile
+        pending = true;
+        inflight = upgraded;
       }
-      if (!s->out.empty() && !send_all(s->fd, s->out.data(), s->out.size())) g_bad.fetch_add(1);
     }
+    if (!pipeline)
+      for (ServerConn* s : readable) handle(s, t_dec);  // handlerProtocol per connection
     g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
   }
+  if (pending) (void)dec.end();
   for (auto& kv : conns) {
     close(kv.first);
     gevws_conn_free(kv.second.c);

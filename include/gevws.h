@@ -419,6 +419,21 @@ int gevws_protocol_unpacket(gevws_protocol *p, gevws_conn *c, gevws_ring *ring,
 int64_t gevws_protocol_unpacket_batch(gevws_protocol *p, gevws_conn *const *conns,
                                       gevws_ring *const *rings, uint32_t n);
 
+/* gevws_protocol_unpacket_batch in two halves, so an event loop can read its
+ * sockets while the device decodes (connection.go:208-251 runs read and
+ * decode back to back; this overlaps them): _begin selects the connections
+ * that can make progress, stages their buffered bytes and enqueues the pass
+ * without waiting -- it returns the number of connections in the pass (0:
+ * nothing to do) or < 0 (GEVWS_ERR_INVALID while a pass is in flight); _end
+ * waits for that pass and queues its frames, returning the number of frames
+ * decoded (0 when none is in flight) or < 0.  Between the two the rings may
+ * take new bytes (gevws_ring_write; the pass decodes its staged copy) but must
+ * not be read or retrieved; gevws_protocol_unpacket ends a pass in flight
+ * first. */
+int64_t gevws_protocol_unpacket_batch_begin(gevws_protocol *p, gevws_conn *const *conns,
+                                            gevws_ring *const *rings, uint32_t n);
+int64_t gevws_protocol_unpacket_batch_end(gevws_protocol *p);
+
 /* Counters of a protocol's host ingress (not on the reference path):
  * device passes run, connections staged into them, bytes staged, UnPacket
  * calls answered NEED_MORE by the host-side gate without a device pass (the

@@ -18,11 +18,12 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(binary, conns=100, seconds=2.0, msg=128, loops=1, threads=2):
+def _run(binary, conns=100, seconds=2.0, msg=128, loops=1, threads=2, env=None):
     path = os.path.join(ROOT, binary)
     assert os.path.exists(path), f"{binary} not built (python -c 'import __graft_entry__ as g; g.build()')"
     r = subprocess.run([path, "--conns", str(conns), "--seconds", str(seconds), "--msg", str(msg), "--loops",
-                        str(loops), "--client-threads", str(threads)], capture_output=True, text=True, timeout=120)
+                        str(loops), "--client-threads", str(threads)], capture_output=True, text=True, timeout=120,
+                       env={**os.environ, **(env or {})})
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert r.returncode == 0 and len(lines) == 1, (r.returncode, r.stdout[-1500:], r.stderr[-1500:])
     d = json.loads(lines[0])
@@ -49,3 +50,13 @@ def test_c1_loopback_large_frames_span_reads():
     wait in the ring for the next pass (the completeness carry)."""
     d = _run("gev_amd/ws_loopback", conns=16, seconds=1.5, msg=65536)
     assert d["client_checked_echoes"] > 0
+
+
+@pytest.mark.parametrize("msg", [128, 65536])
+def test_c1_loopback_pipelined_loop(msg):
+    """GEVWS_LB_PIPELINE=1: the device pass of one loop iteration in flight
+    (gevws_protocol_unpacket_batch_begin) while the next reads its sockets,
+    ended (_end) before its frames are echoed and before any connection it
+    holds is closed; every echo still checked byte for byte."""
+    _run("gev_amd/ws_loopback", conns=100 if msg == 128 else 16, seconds=1.5, msg=msg,
+         env={"GEVWS_LB_PIPELINE": "1"})

@@ -100,6 +100,54 @@ def test_batched_driver_matches_oracle(engine, zero_copy_max):
     assert st["zero_copy_passes"] == (st["device_passes"] if zero_copy_max else 0), st
 
 
+@pytest.mark.parametrize("zero_copy_max", [0, 1 << 30])
+def test_batch_begin_end_with_ring_writes_in_flight(engine, zero_copy_max):
+    """gevws_protocol_unpacket_batch_begin / _end: the pass decodes the bytes
+    buffered at _begin while the rings take more (an event loop reading its
+    sockets during the pass); a second _begin in flight is refused; the
+    frames come out exactly as the oracle decodes each part, and UnPacket
+    ends a pass in flight before it answers."""
+    rng = np.random.default_rng(23)
+    proto = gev_amd.Protocol(engine)
+    proto.set_zero_copy_max(zero_copy_max)
+
+    def part():
+        s = b""
+        for _ in range(int(rng.integers(1, 8))):
+            L = int(rng.integers(0, 3000))
+            s += wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), 2, True, 0, True,
+                                 bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+        return s
+    first = [part() for _ in range(40)]
+    second = [part() for _ in range(40)]
+    conns = [gev_amd.Connection() for _ in first]
+    rings = [gev_amd.RingBuffer(64) for _ in first]
+    for r, s in zip(rings, first):
+        r.write(s)
+    assert proto.unpacket_batch_begin(conns, rings) == len(conns)
+    for r, s in zip(rings, second):  # bytes arriving while the pass runs
+        r.write(s)
+    with pytest.raises(RuntimeError):
+        proto.unpacket_batch_begin(conns, rings)
+    n = proto.unpacket_batch_end()
+    assert n == sum(len(wo.decode_stream(s).frames) for s in first)
+    assert proto.unpacket_batch_end() == 0
+    for c, r, s1, s2 in zip(conns, rings, first, second):
+        want = wo.decode_stream(s1).frames + wo.decode_stream(s2).frames
+        for fr in want:  # the first part from the pass, the second from UnPacket's own passes
+            h, data = proto.unpacket(c, r)
+            assert h is not None and h.length == fr.header.length and data == fr.payload
+        assert proto.unpacket(c, r) == (None, None)
+        assert r.length() == 0
+    # UnPacket with a pass in flight: it ends the pass first
+    for r, s in zip(rings, first):
+        r.write(s)
+    assert proto.unpacket_batch_begin(conns, rings) == len(conns)
+    h, data = proto.unpacket(conns[0], rings[0])
+    assert data == wo.decode_stream(first[0]).frames[0].payload
+    assert conns[1].pending() == len(wo.decode_stream(first[1]).frames)
+
+
 def test_zero_copy_capacity_retry(engine):
     """A zero-copy pass sizes its host outputs from an estimate (~1 frame per
     48 input bytes); a run of empty frames (6 bytes each) exceeds it, the pass

@@ -33,6 +33,9 @@ struct CpuDecoder {
   explicit CpuDecoder(int) { u = gevws_upgrader_new(); }
   ~CpuDecoder() { gevws_upgrader_free(u); }
   int64_t pass(wslb::ServerConn* const*, uint32_t) { return 0; }  // per-frame decode happens in unpacket
+  static constexpr bool kPipelined = false;  // nothing to overlap: the decode runs in unpacket
+  int64_t begin(wslb::ServerConn* const*, uint32_t) { return 0; }
+  int64_t end() { return 0; }
 
   int unpacket(wslb::ServerConn* s, gevws_header* h, const uint8_t** data, uint64_t* len) {
     *data = nullptr;
