@@ -3646,7 +3646,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_EMIT_VARIANT:
-      if (value < 0 || value > 2) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 3) return GEVWS_ERR_INVALID;
       ctx->emit_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_SMALL_BATCH:
@@ -3911,6 +3911,10 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
       k_walk_emit<4, kEmitGroup, true><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(
           d_in, e_conns, (uint32_t)n_v, e_out, d_summary, d_frames, tile_first, entries, ne, gshift, e_rec, e_parent,
           e_ks);
+    else if (ctx->emit_variant == 3)
+      k_walk_emit<8, kEmitGroup><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out,
+                                                                          d_summary, d_frames, tile_first, entries,
+                                                                          ne, gshift, e_rec, e_parent, e_ks);
     else
       k_walk_emit<4, kEmitGroup><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out,
                                                                           d_summary, d_frames, tile_first, entries,

@@ -157,7 +157,8 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * default: k_walk_span is issue-bound), GEVWS_TUNE_EMIT_VARIANT
  * the record pass (0 = groups of 16 connections with few frames enumerated
  * across connection boundaries, 1 = one wave per connection, 2 = 0 with
- * non-temporal entry loads and record stores),
+ * non-temporal entry loads and record stores, 3 = 0 with 8 rounds of 64
+ * entries per load instead of 4),
  * GEVWS_TUNE_SMALL_BATCH the input size in bytes (default and maximum 65 536;
  * 0 = never) up to which a batch of at most 256 connections is decoded by ONE
  * kernel launch -- walk, scan, records and unmask in a single workgroup --

@@ -712,7 +712,7 @@ def test_emit_variants(engine):
         cases.append(pack_streams([b"".join(wo.encode_frame(bytes(20), 2, True, 0, True, b"\1\2\3\4")
                                             for _ in range(nfr)) for _ in range(40)]))
     try:
-        for v in (0, 1, 2):
+        for v in (0, 1, 2, 3):
             engine.set_tuning(_abi.TUNE_EMIT_VARIANT, v)
             for k, (arena, conns) in enumerate(cases):
                 assert_matches_oracle(engine, arena, conns, f"emit variant {v} case {k}")
