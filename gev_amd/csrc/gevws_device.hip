@@ -629,7 +629,8 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
 // chains (an 8-way C4 share: 8 192 connections, 1 100+ frames on the longest)
 // walks for (longest chain) x (latency) with most of the chip idle.
 // k_walk_split gives each connection KS lanes.  Lane i > 0 guesses a frame
-// start near i/KS of the stream: it searches kSyncWin bytes from there for a
+// start near i/KS of the stream: it searches up to kSyncWindows windows of
+// kSyncWin bytes spread over the first half of its segment for a
 // position whose header and the kSyncDepth - 1 headers its chain reaches are
 // all plausible (sync_frame: RSV clear, a defined opcode, control frames final
 // and short, the mask bit of the connection's first frame, minimal length
