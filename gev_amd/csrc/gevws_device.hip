@@ -3417,7 +3417,8 @@ struct gevws_ctx {
   bool prev_mixed = false;
   uint32_t last_unmask_grid = 0;  // workgroups of the last decode's unmask launch
   uint32_t last_ks = 1;    // lanes per connection of the last multi-kernel decode's walk
-  int split_mode = 0;       // measurement: 1 = guesses made then dropped, 2 = no guesses
+  int split_mode = 0;       // measurement: 1 = guesses made then dropped, 2 = no guesses, 3 = the
+                            // default walk keeps its speculation (D = 8) whatever the history
   uint32_t split_lanes = 0;  // walk variant 0: lanes per connection (k_walk_split); 0 = auto, 1 = off
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
                            // 2 = plain walk without the entry table (emit re-walks); 0 and 1 store
@@ -3663,7 +3664,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->split_lanes = (uint32_t)value;
       return GEVWS_OK;
     case GEVWS_TUNE_SPLIT_MODE:
-      if (value < 0 || value > 2) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 3) return GEVWS_ERR_INVALID;
       ctx->split_mode = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_WALK_VARIANT:
@@ -3811,12 +3812,19 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   // profiles/r02_steps_fused.jsonl).
   const bool fused = kFusedScan && nblk > 0 && nblk <= kFusedScanMaxBlocks;
   uint32_t* done = fused ? ctx->d_done : nullptr;
+  // the default walk's uniform-stream speculation (D = 8) pays on long runs of
+  // equal frames (C2, C3: -23..-28 %) and costs 2-7 % elsewhere (C1, C4,
+  // profiles/r02_walk_store_count_ab.jsonl); after a decode on this context
+  // whose frames were mostly NOT the size of their predecessor the plain
+  // chain walk (D = 0) runs instead
+  const bool plain = wv == 0 && ctx->split_mode != 3 && ctx->stats_known && ctx->prev_mixed;
   if (nblk && ks > 1) {
     // (entry groups by the real connection count: the segments of one
     // connection are one chain's worth of line traffic)
     const bool grp = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
 #define GEVWS_SPLIT(K)                                                                                            \
-  (grp ? k_walk_split<K, 8, true> : k_walk_split<K, 8, false>)<<<nblk, kCountBlock, 0, st>>>(                     \
+  (grp ? k_walk_split<K, 8, true> : plain ? k_walk_split<K, 0, false> : k_walk_split<K, 8, false>)               \
+      <<<nblk, kCountBlock, 0, st>>>(                                                                             \
       d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb_w, in_bytes, done, max_frames, payload_cap, \
       d_summary, segs, sout, srec, ctx->split_mode)
     if (ks == 2) GEVWS_SPLIT(2);
@@ -3876,6 +3884,14 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
         k_walk_count<0, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
                                                              gshift, cpb, in_bytes, done, max_frames,
                                                             payload_cap, d_summary);
+    } else if (grp && plain) {
+      k_walk_count<0, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
+                                                          gshift, cpb, in_bytes, done, max_frames, payload_cap,
+                                                          d_summary);
+    } else if (plain) {
+      k_walk_count<0, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
+                                                           gshift, cpb, in_bytes, done, max_frames, payload_cap,
+                                                           d_summary);
     } else if (grp) {
       k_walk_count<8, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
                                                           gshift, cpb, in_bytes, done, max_frames,

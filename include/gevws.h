@@ -177,7 +177,8 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
 #define GEVWS_TUNE_EMIT_VARIANT 6
 #define GEVWS_TUNE_SMALL_BATCH 7
 #define GEVWS_TUNE_SPLIT_LANES 8
-#define GEVWS_TUNE_SPLIT_MODE 9  /* measurement: 1 = split guesses made then dropped, 2 = none made */
+#define GEVWS_TUNE_SPLIT_MODE 9  /* measurement: 1 = split guesses made then dropped, 2 = none made, \
+                                    3 = keep the walk's speculation after a mixed-size batch */
 int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
 /* Lanes per connection the last multi-kernel decode's header walk used (1 =
  * not split; GEVWS_TUNE_SPLIT_LANES), -1 for a null context.  The auto choice
