@@ -183,6 +183,10 @@ def main():
     ap.add_argument("--split-lanes", type=int, default=None,
                     help="A/B: split header walk lanes per connection (GEVWS_TUNE_SPLIT_LANES; 0 = auto, 1 = off)")
     ap.add_argument("--split-mode", type=int, default=0, help="measurement: GEVWS_TUNE_SPLIT_MODE")
+    ap.add_argument("--walk-budget", type=int, default=None,
+                    help="A/B: budgeted header walk, frames per lane (GEVWS_TUNE_WALK_BUDGET; 0 = auto, -1 = off)")
+    ap.add_argument("--resume-lanes", type=int, default=None, help="A/B: lanes per resumed connection")
+    ap.add_argument("--budget-frac", type=int, default=None, help="A/B: auto budget in 16ths of the mean chain")
     ap.add_argument("--emulate-shard", default=None, metavar="R/N",
                     help="projection, not the contract line: decode only rank R's LPT share of an N-way strong "
                          "split of the global batch, on this one GPU")
@@ -221,6 +225,12 @@ def main():
             e.set_tuning(_abi.TUNE_SPLIT_LANES, args.split_lanes)
         if args.split_mode:
             e.set_tuning(_abi.TUNE_SPLIT_MODE, args.split_mode)
+        if args.walk_budget is not None:
+            e.set_tuning(_abi.TUNE_WALK_BUDGET, args.walk_budget)
+        if args.resume_lanes is not None:
+            e.set_tuning(_abi.TUNE_RESUME_LANES, args.resume_lanes)
+        if args.budget_frac is not None:
+            e.set_tuning(_abi.TUNE_BUDGET_FRAC, args.budget_frac)
     t_setup = time.time()
     scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
     emulated = None
@@ -306,25 +316,32 @@ def main():
                 raise SystemExit(f"verification failed on in-flight slot {k}: mismatch={int(mism.item())}")
         del desc
 
+    walk_info = {"split_lanes": eng.last_split_lanes, "budget": eng.last_walk_budget,
+                 "resumed_connections": eng.last_resumed}
     # achievable-bandwidth ceiling on this box, after the timed region: the
     # unmask kernel's streaming loop minus XOR / frame lookup (gevws_copy_async)
-    # over the same byte count, from the same unaligned source offset (the
-    # first payload byte) into the payload arena
-    # -- with non-temporal loads (as the unmask's streaming path) and with plain
-    # loads; the faster of the two is the ceiling
+    # over the same byte count into the payload arena -- from the payload's
+    # unaligned source offset (the first payload byte) and from an aligned one
+    # (offset 0: a float4 copy, the chip's copy rate), each with non-temporal
+    # loads (as the unmask's streaming path) and with plain loads; the fastest
+    # of the four is the ceiling
     copy_gbps = None
     copy_by_load = {}
     if args.copy_reps > 0:
         from gev_amd.workloads import header_len
         src_off = int(header_len(lay.desc["length"][:1], lay.desc["masked"][:1], lay.desc["len_form"][:1])[0])
         n_copy = min(lay.payload_padded, lay.arena_bytes - src_off) // 16 * 16
-        for name, flag in (("nt", 0), ("plain", 0x40000000)):
-            eng.copy_(out.payload, arena, n_copy, src_offset=src_off, grid=flag)
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        span = 0x20000000 | (4 * ncu)  # the unmask's layout: wave-contiguous 16 KiB spans, 4 workgroups per CU
+        for name, flag, so in (("nt", 0, src_off), ("plain", 0x40000000, src_off),
+                               ("nt_aligned", 0, 0), ("plain_aligned", 0x40000000, 0),
+                               ("nt_aligned_wavespan", span, 0), ("plain_aligned_wavespan", span | 0x40000000, 0)):
+            eng.copy_(out.payload, arena, n_copy, src_offset=so, grid=flag)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             e0.record()
             for _ in range(args.copy_reps):
-                eng.copy_(out.payload, arena, n_copy, src_offset=src_off, grid=flag)
+                eng.copy_(out.payload, arena, n_copy, src_offset=so, grid=flag)
             e1.record()
             torch.cuda.synchronize()
             copy_by_load[name] = round(2 * n_copy / (e0.elapsed_time(e1) / args.copy_reps / 1e3) / 1e9, 1)
@@ -370,6 +387,7 @@ def main():
         "decoded_per_step": {"frames": frames_step, "payload_bytes": payload_step, "errors": errors,
                              "ranks_summed": world},
         "errors": errors,
+        "walk": walk_info,
         "phases_ms": {"walk_count": round(mean_ms[0], 4), "scan": round(mean_ms[1], 4),
                       "walk_emit": round(mean_ms[2], 4), "unmask": round(unmask_ms, 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

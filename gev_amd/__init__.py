@@ -193,6 +193,19 @@ class Engine:
         """Lanes per connection of the last multi-kernel decode's header walk (1 = not split)."""
         return int(lib.gevws_ctx_last_split_lanes(self._ctx))
 
+    @property
+    def last_walk_budget(self) -> int:
+        """Frames per lane of the last multi-kernel decode's budgeted walk (0 = not budgeted)."""
+        return int(lib.gevws_ctx_last_walk_budget(self._ctx))
+
+    @property
+    def last_resumed(self) -> int:
+        """Connections the last decode's budgeted walk resumed (waits for it)."""
+        r = int(lib.gevws_ctx_last_resumed(self._ctx))
+        if r < 0:
+            raise RuntimeError(f"last_resumed: {status_string(r)}")
+        return r
+
     @staticmethod
     def variant_name(i: int, key: int = _abi.TUNE_UNMASK_VARIANT) -> Optional[str]:
         n = lib.gevws_tuning_name(key, i)
@@ -688,7 +701,9 @@ class Protocol:
         n = len(conns)
         cs = (ctypes.c_void_p * n)(*[c._p for c in conns])
         rs = (ctypes.c_void_p * n)(*[b._p for b in buffers])
-        self._pending = (cs, rs)  # the C side keeps the pointers until _end
+        # the C side keeps the raw pointers until _end: hold the Python objects
+        # too, so no Connection / RingBuffer is freed under a pass in flight
+        self._pending = (cs, rs, list(conns), list(buffers))
         r = lib.gevws_protocol_unpacket_batch_begin(self._p, cs, rs, n)
         if r < 0:
             raise RuntimeError(f"unpacket_batch_begin: {status_string(int(r))}")
@@ -701,6 +716,24 @@ class Protocol:
         if r < 0:
             raise RuntimeError(f"unpacket_batch_end: {status_string(int(r))}")
         return int(r)
+
+    def set_handler(self, policy: int) -> None:
+        """gevws_protocol_set_handler: HandlerWrap.OnMessage on the device for
+        every frame a pass decodes (GEVWS_HANDLER_*; -1 = off)."""
+        st = lib.gevws_protocol_set_handler(self._p, int(policy))
+        if st != OK:
+            raise ValueError(f"set_handler({policy}): {status_string(st)}")
+
+    def reply(self, c: Connection) -> Tuple[Optional[bytes], bool]:
+        """gevws_protocol_reply: (reply wire bytes or None, ShutdownWrite) -- the
+        device handler's answer for the frame unpacket() last returned on c."""
+        out = _abi.U8P()
+        n = ctypes.c_uint64()
+        sh = ctypes.c_int()
+        st = lib.gevws_protocol_reply(self._p, c._p, ctypes.byref(out), ctypes.byref(n), ctypes.byref(sh))
+        if st != OK:
+            raise RuntimeError(f"reply: {status_string(st)}")
+        return (ctypes.string_at(out, n.value) if n.value else None), bool(sh.value)
 
     def set_zero_copy_max(self, nbytes: int) -> None:
         """gevws_protocol_set_zero_copy_max: batched passes over at most

@@ -50,6 +50,9 @@ TUNE_EMIT_VARIANT = 6
 TUNE_SMALL_BATCH = 7  # one-launch decode up to this many input bytes (0 = never)
 TUNE_SPLIT_MODE = 9  # measurement: 1 = split guesses made then dropped, 2 = none made
 TUNE_SPLIT_LANES = 8  # split header walk: lanes per connection (0 = auto, 1 = never, 2/4/8/16)
+TUNE_WALK_BUDGET = 10  # budgeted walk: frames per lane (0 = auto, -1 = never, > 0 = always)
+TUNE_RESUME_LANES = 11  # lanes per resumed connection (0 = default 8, 2/4/8/16)
+TUNE_BUDGET_FRAC = 12  # auto budget in 16ths of the previous mean chain
 
 IN_PAD = 64
 SUMMARY_UNORDERED = 1  # summary.flags: connection table not in increasing input order
@@ -96,7 +99,7 @@ ZERO_COPY_MAX_DEFAULT = 256 * 1024  # GEVWS_ZERO_COPY_MAX_DEFAULT
 class ProtocolStats(ctypes.Structure):
     _fields_ = [("device_passes", ctypes.c_uint64), ("conns_staged", ctypes.c_uint64),
                 ("bytes_staged", ctypes.c_uint64), ("gated", ctypes.c_uint64),
-                ("zero_copy_passes", ctypes.c_uint64)]
+                ("zero_copy_passes", ctypes.c_uint64), ("handler_passes", ctypes.c_uint64)]
 
 
 class HostConn(ctypes.Structure):
@@ -171,6 +174,8 @@ SIGNATURES = {
     "gevws_ctx_set_tuning": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_last_split_lanes": (ctypes.c_int, [P]),
     "gevws_ctx_last_unmask_grid": (ctypes.c_int, [P]),
+    "gevws_ctx_last_walk_budget": (ctypes.c_int64, [P]),
+    "gevws_ctx_last_resumed": (ctypes.c_int64, [P]),
     "gevws_tuning_name": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32)]),
     "gevws_decode_batch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,
@@ -178,6 +183,9 @@ SIGNATURES = {
     "gevws_decode_batch": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,
                                           ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.POINTER(Summary)]),
     "gevws_encode_batch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, P, ctypes.c_uint64, P, P]),
+    "gevws_encode_replies_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, P, P, ctypes.c_uint64, P, P]),
+    "gevws_dispatch_decoded_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_int, P, ctypes.c_uint64,
+                                                    ctypes.c_uint64, P, P, P]),
     "gevws_dispatch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_int, P, ctypes.c_uint64,
                                             ctypes.c_uint64, P, P, P]),
     "gevws_cipher_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint64]),
@@ -228,6 +236,9 @@ SIGNATURES = {
     "gevws_cipher": (None, [P, ctypes.c_uint64, P, ctypes.c_uint64]),
     "gevws_protocol_get_stats": (None, [P, ctypes.POINTER(ProtocolStats)]),
     "gevws_protocol_set_zero_copy_max": (None, [P, ctypes.c_uint64]),
+    "gevws_protocol_set_handler": (ctypes.c_int, [P, ctypes.c_int]),
+    "gevws_protocol_reply": (ctypes.c_int, [P, P, ctypes.POINTER(U8P), ctypes.POINTER(ctypes.c_uint64),
+                                            ctypes.POINTER(ctypes.c_int)]),
     "gevws_decode_host_batch": (ctypes.c_int64, [P, P, ctypes.c_uint32, P, ctypes.c_uint64, P, ctypes.c_uint64,
                                                  P, ctypes.POINTER(Summary)]),
 }

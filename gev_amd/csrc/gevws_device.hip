@@ -389,20 +389,34 @@ __device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t ava
 // The chain walk of one stream (k_walk_count's loop; also each segment of
 // k_walk_split): entries into [ebase, ebase + ecap) while rec, per-frame
 // counts into R (R.err / R.st carry in the caller's values).
+// The walk starts from the state in R (a fresh chain: walk_res_fresh; the
+// budgeted walk's resumption: the state it stopped in) and stops after
+// `budget` frames in all (R.more: the header at R.pos is not parsed yet).
 struct WalkRes {
   uint64_t pos, nf, pb, pl, same, lastf, firstf, err;
   int32_t st;
-  bool rec;
+  bool rec, more;
 };
+__device__ __forceinline__ WalkRes walk_res_fresh(uint64_t err = 0, int32_t st = GEVWS_OK) {
+  WalkRes R;
+  R.pos = R.nf = R.pb = R.pl = R.same = R.firstf = 0;
+  R.lastf = ~0ull;
+  R.err = err;
+  R.st = st;
+  R.rec = R.more = false;
+  return R;
+}
 
 template <int D, bool GRP, bool NTH = false, int PF = 0>
 __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const uint64_t len, bool rec,
                                            const uint64_t ebase, const uint64_t ecap,
                                            WalkEntry* __restrict__ entries, WalkEntry* __restrict__ sink,
-                                           WalkRes& R) {
-    uint64_t nf = 0, pb = 0, pl = 0, same = 0, lastf = ~0ull, firstf = 0, err = R.err;
+                                           WalkRes& R, const uint64_t budget = ~0ull) {
+    // (GRP keeps the group's earlier entries in registers: a fresh chain only)
+    uint64_t nf = R.nf, pb = R.pb, pl = R.pl, same = R.same, lastf = R.lastf, firstf = R.firstf, err = R.err;
     int32_t st = R.st;
-    uint64_t pos = 0;
+    uint64_t pos = R.pos;
+    bool more = false;
     // software-pipelined: the next header's 16 bytes are requested before this
     // frame's entry is stored, so waiting for that load (vmcnt counts loads and
     // stores in issue order) never waits for the store's completion.  Reading
@@ -411,7 +425,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
     // outstanding (lanes not recording store to their own sink slot past the
     // table), so the compiler waits vmcnt(1), not vmcnt(0).
     uint64_t lo, hi;
-    load_window<NTH>(s, lo, hi);
+    load_window<NTH>(s + pos, lo, hi);
     *sink = WalkEntry{0, 0, 0, 0};
     uint64_t prev_fsz = 0;  // speculation (D > 0): size of the last frame and the run of equal sizes
     uint32_t run = 0;
@@ -449,6 +463,10 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
     };
     uint32_t pfv[PF > 0 ? PF : 1] = {};
     for (;;) {
+      if (nf >= budget) {  // the budgeted walk stops here; k_walk_resume goes on from pos
+        more = true;
+        break;
+      }
       if constexpr (PF > 0) {  // keep the touches' results alive (free: they landed before the header)
 #pragma unroll
         for (int j = 0; j < PF; ++j) __asm__ volatile("" ::"v"(pfv[j]));
@@ -566,9 +584,27 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
     R.err = err;
     R.st = st;
     R.rec = rec;
+    R.more = more;
 }
 
-template <int D, bool GRP, bool NTH = false, int PF = 0>
+// Budgeted walk (BUD, with k_walk_resume): a C4-sized batch (65 536 chains,
+// mean 668 frames, longest 1 204) walks for its LONGEST chain, and the last
+// few hundred steps run on a chip that is otherwise done.
+// With BUD every lane stops after `budget` frames (~ the mean chain, from the
+// context's history); the connections that finished write their results and
+// the record-pass rows of a split walk (row c*ks = the whole stream, rows
+// c*ks+1.. empty), the others append their state to a resume list that
+// k_walk_resume walks KS-wide from where they stopped.  Entries go to row
+// c*ks's slot run, so the resumption's row 0 continues them in place.  An
+// unfinished connection adds nothing to its block partial but the order flag;
+// k_walk_resume adds its totals.
+struct WalkResume {
+  uint32_t c, rec;
+  uint64_t pos, nf, pb, pl, same, lastf, firstf;
+};
+static_assert(sizeof(WalkResume) == 64, "one resume record per 64 bytes");
+
+template <int D, bool GRP, bool NTH = false, int PF = 0, bool BUD = false>
 __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
                                                             const gevws_conn_in* __restrict__ conns,
                                                             uint32_t n, gevws_conn_out* __restrict__ cout,
@@ -576,9 +612,17 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
                                                             WalkEntry* __restrict__ entries, uint64_t n_entries,
                                                             uint32_t gshift, uint32_t cpb, uint64_t in_bytes,
                                                             uint32_t* __restrict__ done, uint64_t max_frames,
-                                                            uint64_t payload_cap, gevws_summary* __restrict__ sum) {
+                                                            uint64_t payload_cap, gevws_summary* __restrict__ sum,
+                                                            uint64_t budget = ~0ull, uint32_t ks = 1,
+                                                            gevws_conn_in* __restrict__ segs = nullptr,
+                                                            gevws_conn_out* __restrict__ sout = nullptr,
+                                                            uint8_t* __restrict__ srec = nullptr,
+                                                            WalkResume* __restrict__ rlist = nullptr,
+                                                            uint32_t* __restrict__ rcount = nullptr) {
   const uint32_t c = blockIdx.x * cpb + threadIdx.x;
   uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0;
+  bool more = false;
+  WalkRes R = walk_res_fresh();
   if (threadIdx.x < cpb && c < n) {
     gevws_conn_in ci = conns[c];
     // the order flag rides in the high half of the error count (k_scan_blocks SPLIT)
@@ -592,24 +636,69 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       st = GEVWS_ERR_INVALID;
       err += 1;
     }
+    const uint64_t v0 = BUD ? (uint64_t)c * ks : c;  // entry slot run / sink of the connection's first row
     uint64_t ebase = 0, ecap = 0;
-    const bool rec0 = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
-    WalkRes R;
-    R.err = err;
-    R.st = st;
-    walk_chain<D, GRP, NTH, PF>(in + ci.off, ci.len, rec0, ebase, ecap, entries, entries + n_entries + c, R);
-    nf = R.nf;
-    pb = R.pb;
-    pl = R.pl;
-    err = R.err;
-    same = R.same;
-    gevws_conn_out o;
-    o.first_frame = R.rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
-    o.consumed = R.pos;
-    o.payload_base = pb;  // per-connection arena bytes; k_walk_emit turns it into a base
-    o.nframes = (uint32_t)nf;
-    o.status = R.st;
-    cout[c] = o;
+    const bool rec0 = entry_slots_of(ci, (uint32_t)v0, n_entries, gshift, ebase, ecap);
+    R = walk_res_fresh(err, st);
+    walk_chain<D, GRP, NTH, PF>(in + ci.off, ci.len, rec0, ebase, ecap, entries, entries + n_entries + v0, R,
+                                BUD ? budget : ~0ull);
+    more = BUD && R.more;
+    if (!more) {
+      nf = R.nf;
+      pb = R.pb;
+      pl = R.pl;
+      err = R.err;
+      same = R.same;
+      gevws_conn_out o;
+      o.first_frame = R.rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
+      o.consumed = R.pos;
+      o.payload_base = pb;  // per-connection arena bytes; k_walk_emit turns it into a base
+      o.nframes = (uint32_t)nf;
+      o.status = R.st;
+      cout[c] = o;
+      if constexpr (BUD) {  // the record pass's rows: the whole stream, then empty rows
+        segs[v0] = ci;
+        gevws_conn_out so;
+        so.first_frame = 0;
+        so.consumed = R.pos;
+        so.payload_base = 0;
+        so.nframes = (uint32_t)nf;
+        so.status = R.st;
+        sout[v0] = so;
+        srec[v0] = R.rec ? 1 : 0;
+        so.consumed = 0;
+        so.nframes = 0;
+        so.status = GEVWS_OK;
+        for (uint32_t k = 1; k < ks; ++k) {
+          segs[v0 + k] = gevws_conn_in{ci.off + ci.len, 0};
+          sout[v0 + k] = so;
+          srec[v0 + k] = 0;
+        }
+      }
+    }
+  }
+  if constexpr (BUD) {
+    // append the unfinished connections to the resume list (one atomic per wave)
+    const uint64_t m = __ballot(more);
+    if (m) {
+      const uint32_t lane = threadIdx.x & 63;
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(rcount, (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, 0, 64);
+      if (more) {
+        WalkResume w;
+        w.c = c;
+        w.rec = R.rec ? 1u : 0u;
+        w.pos = R.pos;
+        w.nf = R.nf;
+        w.pb = R.pb;
+        w.pl = R.pl;
+        w.same = R.same;
+        w.lastf = R.lastf;
+        w.firstf = R.firstf;
+        rlist[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = w;
+      }
+    }
   }
   // block partial sums (one wave)
   const uint64_t vals[kDecFields] = {nf, pb, pl, err, same};
@@ -866,12 +955,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
   // 3. walk the segment (entries in its own slot run)
   uint64_t ebase = 0, ecap = 0;
   const bool rec0 = active && entry_slots_of(sg, (uint32_t)v, n_entries, gshift, ebase, ecap);
-  WalkRes R;
-  R.err = 0;
-  R.st = GEVWS_OK;
-  R.pos = R.nf = R.pb = R.pl = R.same = R.firstf = 0;
-  R.lastf = ~0ull;
-  R.rec = false;
+  WalkRes R = walk_res_fresh();
   if (active) walk_chain<D, GRP>(in + sg.off, sg.len, rec0, ebase, ecap, entries, entries + n_entries + v, R);
   // 4. stitch the group's KS lanes (every lane takes part in the shuffles)
   const bool last = found && end == ci.len;
@@ -944,9 +1028,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
       } else {
         // a guess missed: the whole chain, serially (no entries: the record
         // pass re-walks it as one segment)
-        WalkRes S;
-        S.err = 0;
-        S.st = GEVWS_OK;
+        WalkRes S = walk_res_fresh();
         walk_chain<0, false>(s, ci.len, false, 0, 0, entries, entries + n_entries + v, S);
         nf = S.nf;
         pb = S.pb;
@@ -983,6 +1065,183 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
     }
   }
   if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
+}
+
+// ------------------------------------------------------------------ 1b. walk (count), resumed
+// The budgeted walk's unfinished connections (k_walk_count BUD), KS lanes
+// each, k_walk_split's way from where the chain stopped: lane 0 goes on from
+// the saved position in row 0 (its entries continue the ones already in that
+// row's slot run), lane i > 0 guesses a frame start near i/KS of the REST of
+// the stream and walks [its guess, the next guess) as row i; the rows are
+// accepted when every one but the last ends exactly on its end (induction
+// from lane 0's true position), else lane 0 walks the rest serially and the
+// record pass re-walks the connection as one row.  Persistent grid over the
+// list (its length is known only on the device).  Each connection's totals go
+// into its walk block's partials (atomics; the scan runs after this launch).
+constexpr uint32_t kResumeLanes = 8;       // default lanes per resumed connection
+constexpr uint64_t kResumeBlocksPerCU = 16;
+constexpr uint32_t kBudgetFrac16 = 18;     // default budget: 18/16 of the previous batch's mean chain
+template <int KS, int D>
+__global__ __launch_bounds__(kCountBlock) void k_walk_resume(const uint8_t* __restrict__ in,
+                                                             const gevws_conn_in* __restrict__ conns,
+                                                             gevws_conn_out* __restrict__ cout,
+                                                             uint64_t* __restrict__ blk,
+                                                             WalkEntry* __restrict__ entries, uint64_t n_entries,
+                                                             uint32_t gshift, uint32_t cpb,
+                                                             const WalkResume* __restrict__ rlist,
+                                                             const uint32_t* __restrict__ rcount,
+                                                             gevws_conn_in* __restrict__ segs,
+                                                             gevws_conn_out* __restrict__ sout,
+                                                             uint8_t* __restrict__ srec) {
+  static_assert(KS >= 2 && KS <= (int)kSplitMaxLanes && (KS & (KS - 1)) == 0, "KS: a power of two");
+  __shared__ uint32_t s_row[kCountBlock * kSyncRow];
+  constexpr uint32_t G = kCountBlock / KS;  // connections per workgroup per round
+  const uint32_t lane = threadIdx.x & 63, i = lane % KS;
+  const uint32_t cnt = uniform32(__hip_atomic_load(rcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (uint32_t base = blockIdx.x * G; base < cnt; base += gridDim.x * G) {  // wave-uniform
+    const uint32_t r = base + threadIdx.x / KS;
+    const bool active = r < cnt;
+    WalkResume w = {0, 0, 0, 0, 0, 0, 0, ~0ull, 0};
+    gevws_conn_in ci = {0, 0};
+    if (active) {
+      w = rlist[r];
+      ci = conns[w.c];
+    }
+    const uint8_t* s = in + ci.off;
+    const uint64_t v = (uint64_t)w.c * KS + i;
+    // 1. guesses in the rest of the stream [w.pos, len)
+    bool found = active && i == 0;
+    uint64_t b = 0;
+    if (active && i > 0) {
+      const uint64_t rem = ci.len - w.pos;
+      const uint64_t kc = rem / kSplitMinBytes < KS ? rem / kSplitMinBytes : KS;
+      if (i < kc) {
+        const uint64_t seg = rem / kc, t = w.pos + rem * i / kc;
+        const uint64_t step = seg / (2 * kSyncWindows) > kSyncWin ? seg / (2 * kSyncWindows) : kSyncWin;
+        const uint32_t m0 = (uint32_t)s[1] >> 7;  // the first frame's mask bit
+        found = sync_search(s, ci.len, t, step, t + seg * 3 / 4, m0, s_row + threadIdx.x * kSyncRow, b);
+      }
+    }
+    // 2. a row ends at the next lane's guess (or the stream's end)
+    const uint64_t mine = found ? b : ~0ull;
+    uint64_t end = ci.len;
+#pragma unroll
+    for (int j = KS - 1; j >= 1; --j) {
+      const uint64_t y = __shfl(mine, (int)((lane + j) & 63), 64);
+      if ((int)i + j < KS && y != ~0ull) end = y;
+    }
+    // row 0 is the stream's start to the first guess (walked from w.pos on)
+    const uint64_t rb = i == 0 ? 0 : (found ? b : end);
+    const gevws_conn_in sg = {ci.off + rb, found ? end - rb : 0};
+    uint64_t ebase = 0, ecap = 0;
+    bool rec0 = active && entry_slots_of(sg, (uint32_t)v, n_entries, gshift, ebase, ecap);
+    WalkRes R = walk_res_fresh();
+    if (i == 0) {
+      R.pos = w.pos;
+      R.nf = w.nf;
+      R.pb = w.pb;
+      R.pl = w.pl;
+      R.same = w.same;
+      R.lastf = w.lastf;
+      R.firstf = w.firstf;
+      // the entries already stored must fit row 0's (shorter) slot run
+      rec0 = rec0 && w.rec && w.nf <= ecap;
+    }
+    if (active) walk_chain<D, false>(in + sg.off, sg.len, rec0, ebase, ecap, entries, entries + n_entries + v, R);
+    // 3. stitch the group's KS lanes (every lane takes part in the shuffles)
+    const bool last = found && end == ci.len;
+    const bool ok = !found || last || (R.st == GEVWS_OK && R.pos == sg.len);
+    uint64_t prevlast = ~0ull;
+    bool got = false;
+#pragma unroll
+    for (int d = 1; d < KS; ++d) {
+      const uint64_t ynf = __shfl_up(R.nf, d, 64), ylast = __shfl_up(R.lastf, d, 64);
+      if (!got && (int)i >= d && ynf > 0) {
+        prevlast = ylast;
+        got = true;
+      }
+    }
+    // (row 0's own count already runs across the budget boundary)
+    const uint64_t same = R.same + ((i > 0 && R.nf > 0 && got && R.firstf == prevlast) ? 1 : 0);
+    uint64_t inf = R.nf, ipb = R.pb;
+#pragma unroll
+    for (int d = 1; d < KS; d <<= 1) {
+      const uint64_t a = __shfl_up(inf, d, 64), q = __shfl_up(ipb, d, 64);
+      if ((int)i >= d) {
+        inf += a;
+        ipb += q;
+      }
+    }
+    uint64_t t_nf = R.nf, t_pb = R.pb, t_pl = R.pl, t_same = same;
+    uint64_t t_cons = last ? rb + R.pos : 0;
+    int32_t t_st = last ? R.st : 0;
+    int t_ok = ok ? 1 : 0;
+#pragma unroll
+    for (int d = KS / 2; d >= 1; d >>= 1) {
+      t_nf += __shfl_xor(t_nf, d, 64);
+      t_pb += __shfl_xor(t_pb, d, 64);
+      t_pl += __shfl_xor(t_pl, d, 64);
+      t_same += __shfl_xor(t_same, d, 64);
+      t_cons += __shfl_xor(t_cons, d, 64);
+      t_st += __shfl_xor(t_st, d, 64);
+      t_ok &= __shfl_xor(t_ok, d, 64);
+    }
+    if (!active) continue;
+    const bool valid = t_ok != 0;
+    if (!valid && i == 0) {
+      // a guess missed: the rest of the chain serially from where the budget
+      // stopped it (no entries: the record pass re-walks the connection)
+      WalkRes S = walk_res_fresh();
+      S.pos = w.pos;
+      S.nf = w.nf;
+      S.pb = w.pb;
+      S.pl = w.pl;
+      S.same = w.same;
+      S.lastf = w.lastf;
+      S.firstf = w.firstf;
+      walk_chain<0, false>(s, ci.len, false, 0, 0, entries, entries + n_entries + v, S);
+      t_nf = S.nf;
+      t_pb = S.pb;
+      t_pl = S.pl;
+      t_same = S.same;
+      t_cons = S.pos;
+      t_st = S.st;
+    }
+    gevws_conn_out so;
+    if (valid) {
+      segs[v] = sg;
+      so.first_frame = inf - R.nf;  // relative to the connection's first frame
+      so.consumed = R.pos;
+      so.payload_base = ipb - R.pb;  // relative to the connection's payload base
+      so.nframes = (uint32_t)R.nf;
+      so.status = R.st;
+      srec[v] = R.rec ? 1 : 0;
+    } else {  // one row: the whole connection, re-walked by the record pass
+      segs[v] = i == 0 ? ci : gevws_conn_in{ci.off + ci.len, 0};
+      so.first_frame = 0;
+      so.consumed = 0;
+      so.payload_base = 0;
+      so.nframes = i == 0 ? (uint32_t)t_nf : 0u;
+      so.status = GEVWS_OK;
+      srec[v] = 0;
+    }
+    sout[v] = so;
+    if (i == 0) {
+      gevws_conn_out o;
+      o.first_frame = 0;
+      o.consumed = t_cons;
+      o.payload_base = t_pb;
+      o.nframes = (uint32_t)t_nf;
+      o.status = t_st;
+      cout[w.c] = o;
+      unsigned long long* bp = reinterpret_cast<unsigned long long*>(blk + (uint64_t)(w.c / cpb) * kDecFields);
+      atomicAdd(bp + 0, (unsigned long long)t_nf);
+      atomicAdd(bp + 1, (unsigned long long)t_pb);
+      atomicAdd(bp + 2, (unsigned long long)t_pl);
+      if (t_st < 0) atomicAdd(bp + 3, 1ull);
+      atomicAdd(bp + 4, (unsigned long long)t_same);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ 1a'. walk (count), buffered
@@ -1446,11 +1705,13 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_co
                                                             const uint64_t* __restrict__ blk,
                                                             const gevws_summary* __restrict__ sum,
                                                             uint8_t* __restrict__ rec_flags, uint32_t cpb,
-                                                            uint64_t* __restrict__ stats = nullptr) {
+                                                            uint64_t* __restrict__ stats = nullptr,
+                                                            const uint32_t* __restrict__ rcount = nullptr) {
   if (stats && blockIdx.x == 0 && threadIdx.x == 0) {  // the split walk's history (see decode_split_lanes)
     stats[0] = sum->frames;
     stats[1] = sum->payload_len;
     stats[2] = sum->run_frames;
+    stats[3] = rcount ? *rcount : 0;  // connections the budgeted walk resumed
   }
   if (sum->status != GEVWS_OK) return;  // capacity error: nothing written
   const uint32_t c = blockIdx.x * cpb + threadIdx.x;
@@ -1949,12 +2210,33 @@ __device__ __forceinline__ u32x4 copy_ld(const uint8_t* p) {
   else return ld16u(p);
 }
 
-template <int U, bool INTERLEAVE, bool NTL = true>
+// WSPAN: the unmask's streaming layout -- a contiguous run of tiles per
+// workgroup, in steps of U tiles of which wave w copies the contiguous
+// U KiB at w * U KiB (16 aligned bytes per lane per KiB).
+template <int U, bool INTERLEAVE, bool NTL = true, bool WSPAN = false>
 __global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __restrict__ src,
                                                               uint8_t* __restrict__ dst, uint64_t n) {
   const uint64_t ntiles = n / kTile;
   const uint32_t lane_off = threadIdx.x * 16;
-  if constexpr (INTERLEAVE) {
+  if constexpr (WSPAN) {
+    const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+    uint64_t t = (uint64_t)blockIdx.x * per;
+    const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+    const uint64_t wrel = (uint64_t)(threadIdx.x >> 6) * U * 1024 + (threadIdx.x & 63) * 16;
+    for (; t + U <= tend; t += U) {
+      const uint64_t base = t * kTile + wrel;
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = copy_ld<NTL>(src + base + u * 1024);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + base + u * 1024));
+    }
+    for (; t < tend; ++t) {
+      const uint64_t base = t * kTile + lane_off;
+      __builtin_nontemporal_store(copy_ld<NTL>(src + base), reinterpret_cast<u32x4*>(dst + base));
+    }
+  } else if constexpr (INTERLEAVE) {
     // blocks of U consecutive tiles dealt round-robin over the workgroups
     const uint64_t nblk = ntiles / U;
     for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
@@ -2627,12 +2909,22 @@ __device__ __forceinline__ uint32_t enc_hlen(const gevws_header& h) {
 // 4 096 frames and the single-workgroup scan of partials stays short (C4:
 // 10.7 K partials instead of 171 K).
 constexpr int kEncSlabs = 16;
+// The frame count of a chained pass (decode -> dispatch -> encode with no host
+// round trip): the producing step's summary gates the consumer -- its frames,
+// or none when it failed (a capacity error leaves stale records behind).
+__device__ __forceinline__ uint64_t gated_count(uint64_t n, const gevws_summary* __restrict__ gate) {
+  if (!gate) return n;
+  const gevws_summary g = *gate;
+  return g.status != GEVWS_OK ? 0 : (g.frames < n ? g.frames : n);
+}
 
 // Also writes each frame's wire size (h + L) into out_off[f], which k_enc_emit
 // turns into the offset in place: the emit pass reads 8 bytes per frame
 // instead of the 32-byte record again (C4: 0.35 instead of 1.4 GB).
 __global__ __launch_bounds__(kWalkBlock) void k_enc_size(const gevws_out_frame* __restrict__ fr, uint64_t n,
-                                                         uint64_t* __restrict__ blk, uint64_t* __restrict__ out_off) {
+                                                         uint64_t* __restrict__ blk, uint64_t* __restrict__ out_off,
+                                                         const gevws_summary* __restrict__ gate = nullptr) {
+  n = gated_count(n, gate);
   const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;
   uint64_t one = 0, wire = 0, pl = 0;
 #pragma unroll 4
@@ -2668,8 +2960,10 @@ __global__ __launch_bounds__(kWalkBlock) void k_enc_emit(uint64_t n,
                                                          const uint64_t* __restrict__ blk,
                                                          const gevws_summary* __restrict__ sum,
                                                          uint64_t* __restrict__ out_off,
-                                                         uint32_t* __restrict__ tile_first) {
+                                                         uint32_t* __restrict__ tile_first,
+                                                         const gevws_summary* __restrict__ gate = nullptr) {
   if (sum->status != GEVWS_OK) return;
+  n = gated_count(n, gate);
   const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;
   uint64_t carry = blk[(uint64_t)blockIdx.x * kBlkFields + 1];
   for (int j = 0; j < kEncSlabs; ++j) {
@@ -3125,7 +3419,9 @@ __device__ __forceinline__ int disp_kind(const gevws_header& h, int policy, uint
 }
 
 __global__ __launch_bounds__(kWalkBlock) void k_disp_count(const gevws_frame* __restrict__ fr, uint64_t n, int policy,
-                                                           uint64_t* __restrict__ blk) {
+                                                           uint64_t* __restrict__ blk,
+                                                           const gevws_summary* __restrict__ gate = nullptr) {
+  n = gated_count(n, gate);
   const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;  // as k_enc_size
   uint64_t rep = 0, aux = 0, shut = 0;
 #pragma unroll 4
@@ -3224,8 +3520,10 @@ __global__ __launch_bounds__(kWalkBlock) void k_disp_emit(const gevws_frame* __r
                                                           const gevws_summary* __restrict__ sum,
                                                           gevws_out_frame* __restrict__ rep,
                                                           int64_t* __restrict__ reply_of,
-                                                          uint8_t* __restrict__ aux_base) {
+                                                          uint8_t* __restrict__ aux_base,
+                                                          const gevws_summary* __restrict__ gate = nullptr) {
   if (sum->status != GEVWS_OK) return;
+  n = gated_count(n, gate);
   const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;  // as k_enc_emit
   uint64_t c_rep = blk[(uint64_t)blockIdx.x * kBlkFields + 0], c_aux = blk[(uint64_t)blockIdx.x * kBlkFields + 1];
   for (int j = 0; j < kEncSlabs; ++j) {
@@ -3420,6 +3718,10 @@ struct gevws_ctx {
   int split_mode = 0;       // measurement: 1 = guesses made then dropped, 2 = no guesses, 3 = the
                             // default walk keeps its speculation (D = 8) whatever the history
   uint32_t split_lanes = 0;  // walk variant 0: lanes per connection (k_walk_split); 0 = auto, 1 = off
+  int64_t walk_budget = 0;   // frames per lane of the budgeted walk: 0 = auto, -1 = never, > 0 = always
+  uint32_t resume_lanes = 0;  // lanes per resumed connection (k_walk_resume): 0 = kResumeLanes
+  uint32_t budget_frac16 = kBudgetFrac16;  // auto budget: this many 16ths of the previous mean chain
+  uint64_t last_budget = 0;  // budget of the last multi-kernel decode's walk (0 = not budgeted)
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
                            // 2 = plain walk without the entry table (emit re-walks); 0 and 1 store
                            // entries in 64-byte groups for batches of many connections; 3 / 4 =
@@ -3671,6 +3973,18 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       if (value < 0 || value >= kNumWalkVariants) return GEVWS_ERR_INVALID;
       ctx->walk_variant = (int)value;
       return GEVWS_OK;
+    case GEVWS_TUNE_WALK_BUDGET:
+      if (value < -1 || value > 0xFFFFFFFFll) return GEVWS_ERR_INVALID;
+      ctx->walk_budget = value;
+      return GEVWS_OK;
+    case GEVWS_TUNE_RESUME_LANES:
+      if (value < 0 || value == 1 || value > kSplitMaxLanes || (value & (value - 1))) return GEVWS_ERR_INVALID;
+      ctx->resume_lanes = (uint32_t)value;
+      return GEVWS_OK;
+    case GEVWS_TUNE_BUDGET_FRAC:
+      if (value < 1 || value > 64) return GEVWS_ERR_INVALID;
+      ctx->budget_frac16 = (uint32_t)value;
+      return GEVWS_OK;
     default:
       return GEVWS_ERR_INVALID;
   }
@@ -3684,6 +3998,15 @@ const char* gevws_tuning_name(int key, int64_t value) {
 }
 
 int gevws_ctx_last_split_lanes(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_ks : -1; }
+
+int64_t gevws_ctx_last_walk_budget(const gevws_ctx* ctx) { return ctx ? (int64_t)ctx->last_budget : -1; }
+
+int64_t gevws_ctx_last_resumed(gevws_ctx* ctx) {
+  if (!ctx) return -1;
+  DeviceGuard g(ctx->device);
+  if (ctx->has_last && hipEventSynchronize(ctx->last_done) != hipSuccess) return GEVWS_ERR_DEVICE;
+  return (int64_t)ctx->h_stats[3];
+}
 
 int gevws_ctx_last_unmask_grid(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_unmask_grid : -1; }
 
@@ -3759,7 +4082,8 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   if (!span && wv == 0 && n_conns) {
     if (ctx->split_lanes >= 2) {
       ks = ctx->split_lanes;
-    } else if (ctx->split_lanes == 0 && in_bytes / n_conns >= 2 * kSplitMinBytes && ctx->stats_known &&
+    } else if (ctx->split_lanes == 0 && ctx->walk_budget <= 0 && in_bytes / n_conns >= 2 * kSplitMinBytes &&
+               ctx->stats_known &&
                ctx->prev_frames_per_conn >= kSplitMinFramesPerConn && ctx->prev_frame_bytes <= kSplitMaxFrameBytes) {
       if ((uint64_t)n_conns <= kSplitMaxConnsPerCU * ncu)
         while (ks < kSplitMaxLanes && (uint64_t)n_conns * ks * 2 <= (uint64_t)kSplitLanesPerCU * ncu) ks *= 2;
@@ -3767,9 +4091,31 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   }
   if ((uint64_t)n_conns * ks > 0xFFFFFFFFull) ks = 1;
   ctx->last_ks = ks;
+  // budgeted walk (k_walk_count BUD + k_walk_resume): a batch of many long
+  // chains of small frames -- too many connections for the split walk --
+  // walks each chain for ~ the previous batch's mean chain length, then the
+  // unfinished ones rks lanes wide from where they stopped
+  uint64_t budget = 0;
+  uint32_t rks = 1;
+  if (!span && wv == 0 && n_conns && ks == 1 && ctx->walk_budget >= 0) {
+    if (ctx->walk_budget > 0) {
+      budget = (uint64_t)ctx->walk_budget;
+    } else if (ctx->stats_known && ctx->prev_frames_per_conn >= kSplitMinFramesPerConn &&
+               ctx->prev_frame_bytes <= kSplitMaxFrameBytes && in_bytes / n_conns >= 2 * kSplitMinBytes) {
+      budget = ctx->prev_frames_per_conn * ctx->budget_frac16 / 16;
+      if (budget < 1) budget = 1;
+    }
+    if (budget) rks = ctx->resume_lanes ? ctx->resume_lanes : kResumeLanes;
+    if ((uint64_t)n_conns * rks > 0xFFFFFFFFull) {
+      budget = 0;
+      rks = 1;
+    }
+  }
+  ctx->last_budget = budget;
+  const uint32_t rows = ks > 1 ? ks : rks;  // record-pass rows per connection
   const uint32_t cpb_w = ks > 1 ? (kCountBlock / ks < cpb ? kCountBlock / ks : cpb) : cpb;
   const uint32_t nblk = (n_conns + cpb_w - 1) / cpb_w;
-  const uint64_t n_v = (uint64_t)n_conns * ks;  // rows of the record pass's connection table
+  const uint64_t n_v = (uint64_t)n_conns * rows;  // rows of the record pass's connection table
   const uint64_t ntiles_cap = (payload_cap + kTile - 1) / kTile + 1;
   const size_t blk_bytes = ((size_t)nblk * kDecFields * sizeof(uint64_t) + 255) & ~size_t(255);
   const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
@@ -3777,11 +4123,14 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   while ((in_bytes >> gshift) > kEntryBudget) ++gshift;
   const uint64_t n_entries = 4 * ((in_bytes >> (gshift + 2)) + n_v + 1);
   const size_t flag_bytes = ((size_t)n_conns + 255) & ~size_t(255);
-  const size_t seg_bytes = ks > 1 ? ((n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out) + 1) + 1023) & ~size_t(255)) : 0;
+  const size_t seg_bytes = rows > 1 ? ((n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out) + 1) + 1023) & ~size_t(255)) : 0;
+  // the budgeted walk's resume list + its length
+  const size_t res_bytes = budget ? (size_t)n_conns * sizeof(WalkResume) + 256 : 0;
   // + one sink slot per walk lane after the table (k_walk_count / k_walk_split)
   int r = order_after_last(ctx, st);
   if (r != GEVWS_OK) return r;
-  r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + seg_bytes + (n_entries + n_v) * sizeof(WalkEntry));
+  r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + seg_bytes + res_bytes +
+                              (n_entries + n_v) * sizeof(WalkEntry));
   if (r != GEVWS_OK) return r;
   char* sp = reinterpret_cast<char*>(ctx->scratch);
   uint64_t* blk = reinterpret_cast<uint64_t*>(sp);
@@ -3791,7 +4140,9 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   gevws_conn_in* segs = reinterpret_cast<gevws_conn_in*>(segp);
   gevws_conn_out* sout = reinterpret_cast<gevws_conn_out*>(segp + n_v * sizeof(gevws_conn_in));
   uint8_t* srec = reinterpret_cast<uint8_t*>(segp + n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out)));
-  WalkEntry* entries = reinterpret_cast<WalkEntry*>(segp + seg_bytes);
+  WalkResume* rlist = reinterpret_cast<WalkResume*>(segp + seg_bytes);
+  uint32_t* rcount = reinterpret_cast<uint32_t*>(segp + seg_bytes + res_bytes - 256);
+  WalkEntry* entries = reinterpret_cast<WalkEntry*>(segp + seg_bytes + res_bytes);
   const bool timed = ctx->timing;
   hipEvent_t* ev = nullptr;
   if (timed) {
@@ -3810,7 +4161,8 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   // saves the k_scan_blocks launch (with release / acquire fences instead of
   // coherent partials it was slower: C1-shaped walk 0.034 -> 0.074 ms,
   // profiles/r02_steps_fused.jsonl).
-  const bool fused = kFusedScan && nblk > 0 && nblk <= kFusedScanMaxBlocks;
+  // (the budgeted walk's partials are complete only after k_walk_resume)
+  const bool fused = kFusedScan && nblk > 0 && nblk <= kFusedScanMaxBlocks && !budget;
   uint32_t* done = fused ? ctx->d_done : nullptr;
   // the default walk's uniform-stream speculation (D = 8) pays on long runs of
   // equal frames (C2, C3: -23..-28 %) and costs 2-7 % elsewhere (C1, C4,
@@ -3818,7 +4170,25 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   // whose frames were mostly NOT the size of their predecessor the plain
   // chain walk (D = 0) runs instead
   const bool plain = wv == 0 && ctx->split_mode != 3 && ctx->stats_known && ctx->prev_mixed;
-  if (nblk && ks > 1) {
+  if (nblk && budget) {
+    const bool grp = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
+    GEVWS_HIP(hipMemsetAsync(rcount, 0, sizeof(uint32_t), st));
+    auto kc = grp ? (plain ? k_walk_count<0, true, false, 0, true> : k_walk_count<8, true, false, 0, true>)
+                  : (plain ? k_walk_count<0, false, false, 0, true> : k_walk_count<8, false, false, 0, true>);
+    kc<<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes,
+                                     nullptr, max_frames, payload_cap, d_summary, budget, rks, segs, sout, srec, rlist,
+                                     rcount);
+    uint64_t rgrid = ((uint64_t)n_conns * rks + kCountBlock - 1) / kCountBlock;
+    if (rgrid > kResumeBlocksPerCU * ncu) rgrid = kResumeBlocksPerCU * ncu;
+#define GEVWS_RESUME(K)                                                                                  \
+  (plain ? k_walk_resume<K, 0> : k_walk_resume<K, 8>)<<<(uint32_t)rgrid, kCountBlock, 0, st>>>(        \
+      d_in, d_conns, d_conn_out, blk, entries, ne, gshift, cpb, rlist, rcount, segs, sout, srec)
+    if (rks == 2) GEVWS_RESUME(2);
+    else if (rks == 4) GEVWS_RESUME(4);
+    else if (rks == 8) GEVWS_RESUME(8);
+    else GEVWS_RESUME(16);
+#undef GEVWS_RESUME
+  } else if (nblk && ks > 1) {
     // (entry groups by the real connection count: the segments of one
     // connection are one chain's worth of line traffic)
     const bool grp = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
@@ -3906,15 +4276,16 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   if (!fused) k_scan_blocks<true, kDecFields><<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
   if (timed) GEVWS_HIP(hipEventRecord(ev[2], st));
   if (nblk) {
-    k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb_w, ctx->d_stats);
+    k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb_w, ctx->d_stats,
+                                               budget ? rcount : nullptr);
     ctx->stats_pending = true;
     ctx->stats_conns = n_conns;
     // the record pass walks the segments when the walk was split
-    const gevws_conn_in* e_conns = ks > 1 ? segs : d_conns;
-    const gevws_conn_out* e_out = ks > 1 ? sout : d_conn_out;
-    const uint8_t* e_rec = ks > 1 ? srec : rec_flags;
-    const gevws_conn_out* e_parent = ks > 1 ? d_conn_out : nullptr;
-    const uint32_t e_ks = ks > 1 ? ks : 0;
+    const gevws_conn_in* e_conns = rows > 1 ? segs : d_conns;
+    const gevws_conn_out* e_out = rows > 1 ? sout : d_conn_out;
+    const uint8_t* e_rec = rows > 1 ? srec : rec_flags;
+    const gevws_conn_out* e_parent = rows > 1 ? d_conn_out : nullptr;
+    const uint32_t e_ks = rows > 1 ? rows : 0;
     uint64_t egrid = (n_v + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
     // (split rows: each row is a chain of ~100 frames whose entries cost a
     // load round trip, so more waves share them out)
@@ -3963,9 +4334,9 @@ int gevws_decode_batch(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64
   return r;
 }
 
-int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_frames, uint64_t n,
-                             const uint8_t* d_payload, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
-                             gevws_summary* d_summary) {
+static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_frames, uint64_t n,
+                       const gevws_summary* gate, const uint8_t* d_payload, uint8_t* d_out, uint64_t out_cap,
+                       uint64_t* d_out_off, gevws_summary* d_summary) {
   if (!ctx || !d_summary || (n && (!d_frames || !d_out || !d_out_off))) return GEVWS_ERR_INVALID;
   if (n > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
   DeviceGuard g(ctx->device);
@@ -3980,9 +4351,9 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   if (r != GEVWS_OK) return r;
   uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
   uint32_t* tile_first = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes);
-  if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_out_off);
+  if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_out_off, gate);
   k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
-  if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(n, blk, d_summary, d_out_off, tile_first);
+  if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(n, blk, d_summary, d_out_off, tile_first, gate);
   const uint64_t per_cu = (ctx->encode_variant == 0 || ctx->encode_variant >= 4) ? 7 : 4;  // LDS-light: 7 per CU
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
   // (GEVWS_TUNE_UNMASK_GRID, when set, caps the encode's grid too: measurement)
@@ -4013,9 +4384,24 @@ int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame
   return mark_last(ctx, st);
 }
 
-int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t n, int policy,
-                         uint8_t* d_payload, uint64_t aux_off, uint64_t aux_cap, gevws_out_frame* d_replies,
-                         int64_t* d_reply_of, gevws_summary* d_summary) {
+int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_frames, uint64_t n,
+                             const uint8_t* d_payload, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                             gevws_summary* d_summary) {
+  return encode_impl(ctx, stream, d_frames, n, nullptr, d_payload, d_out, out_cap, d_out_off, d_summary);
+}
+
+int gevws_encode_replies_async(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_replies,
+                               uint64_t max_replies, const gevws_summary* d_dispatched, const uint8_t* d_payload,
+                               uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off, gevws_summary* d_summary) {
+  if (!d_dispatched) return GEVWS_ERR_INVALID;
+  return encode_impl(ctx, stream, d_replies, max_replies, d_dispatched, d_payload, d_out, out_cap, d_out_off,
+                     d_summary);
+}
+
+static int dispatch_impl(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t n,
+                         const gevws_summary* gate, int policy, uint8_t* d_payload, uint64_t aux_off,
+                         uint64_t aux_cap, gevws_out_frame* d_replies, int64_t* d_reply_of,
+                         gevws_summary* d_summary) {
   if (!ctx || !d_summary || (n && (!d_frames || !d_payload || !d_replies || !d_reply_of))) return GEVWS_ERR_INVALID;
   if (policy < GEVWS_HANDLER_NONE || policy > GEVWS_HANDLER_ECHO_TEXT) return GEVWS_ERR_INVALID;
   DeviceGuard g(ctx->device);
@@ -4029,13 +4415,29 @@ int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_fram
   r = ensure_scratch(ctx, blk_bytes);
   if (r != GEVWS_OK) return r;
   uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
-  if (nblk) k_disp_count<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, blk);
+  if (nblk) k_disp_count<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, blk, gate);
   k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, aux_cap / kAuxSlot, d_summary);
   if (nblk)
     k_disp_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, d_payload, aux_off, blk, d_summary, d_replies,
-                                              d_reply_of, d_payload + aux_off);
+                                              d_reply_of, d_payload + aux_off, gate);
   GEVWS_HIP(hipGetLastError());
   return mark_last(ctx, st);
+}
+
+int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t n, int policy,
+                         uint8_t* d_payload, uint64_t aux_off, uint64_t aux_cap, gevws_out_frame* d_replies,
+                         int64_t* d_reply_of, gevws_summary* d_summary) {
+  return dispatch_impl(ctx, stream, d_frames, n, nullptr, policy, d_payload, aux_off, aux_cap, d_replies,
+                       d_reply_of, d_summary);
+}
+
+int gevws_dispatch_decoded_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t max_frames,
+                                 const gevws_summary* d_decoded, int policy, uint8_t* d_payload, uint64_t aux_off,
+                                 uint64_t aux_cap, gevws_out_frame* d_replies, int64_t* d_reply_of,
+                                 gevws_summary* d_summary) {
+  if (!d_decoded) return GEVWS_ERR_INVALID;
+  return dispatch_impl(ctx, stream, d_frames, max_frames, d_decoded, policy, d_payload, aux_off, aux_cap, d_replies,
+                       d_reply_of, d_summary);
 }
 
 int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t* d_src, uint64_t n,
@@ -4045,11 +4447,15 @@ int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t
   if (n == 0) return GEVWS_OK;
   DeviceGuard g(ctx->device);
   hipStream_t st = pick_stream(ctx, stream);
-  // high bit: interleaved block mapping; next bit: plain loads (measurement variants)
-  const bool inter = grid & 0x80000000u, plain = grid & 0x40000000u;
-  grid &= 0x3fffffffu;
+  // high bit: interleaved block mapping; next bit: plain loads; next: the
+  // unmask's wave-contiguous spans (measurement variants)
+  const bool inter = grid & 0x80000000u, plain = grid & 0x40000000u, wspan = grid & 0x20000000u;
+  grid &= 0x1fffffffu;
   if (grid == 0) grid = (uint32_t)ctx->num_cus;
-  if (inter)
+  if (wspan)
+    (plain ? k_copy_stream<16, false, false, true> : k_copy_stream<16, false, true, true>)<<<grid, kUnmaskBlock, 0,
+                                                                                            st>>>(d_src, d_dst, n);
+  else if (inter)
     (plain ? k_copy_stream<16, true, false> : k_copy_stream<16, true>)<<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst, n);
   else
     (plain ? k_copy_stream<16, false, false> : k_copy_stream<16, false>)<<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst,

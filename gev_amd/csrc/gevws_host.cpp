@@ -83,13 +83,16 @@ class PinnedPool : public std::enable_shared_from_this<PinnedPool> {
     need = std::max<uint64_t>(need, 16);
     Buf b{nullptr, 0};
     {
+      // the smallest kept buffer that fits (first-fit let one big
+      // pass's arena serve every later tiny one)
       std::lock_guard<std::mutex> g(mu_);
+      size_t best = free_.size();
       for (size_t i = 0; i < free_.size(); ++i)
-        if (free_[i].cap >= need) {
-          b = free_[i];
-          free_.erase(free_.begin() + (long)i);
-          break;
-        }
+        if (free_[i].cap >= need && (best == free_.size() || free_[i].cap < free_[best].cap)) best = i;
+      if (best < free_.size()) {
+        b = free_[best];
+        free_.erase(free_.begin() + (long)best);
+      }
     }
     if (!b.p) {
       const uint64_t want = std::max<uint64_t>(need + need / 2, 1 << 16);
@@ -109,13 +112,17 @@ class PinnedPool : public std::enable_shared_from_this<PinnedPool> {
   };
   void Release(Buf b) {
     std::lock_guard<std::mutex> g(mu_);
-    if (free_.size() < kKeep) {
+    if (free_.size() < kKeep && b.cap <= kKeepMaxBytes) {
       free_.push_back(b);
       return;
     }
     (void)hipHostFree(b.p);
   }
   static constexpr size_t kKeep = 8;  // arenas kept for reuse
+  // page-locked memory is a system-wide resource: an arena bigger than this
+  // (a bulk pass's) goes back to the OS instead of staying pinned for the
+  // protocol's life
+  static constexpr uint64_t kKeepMaxBytes = 64ull << 20;
   std::mutex mu_;
   std::vector<Buf> free_;
 };
@@ -126,6 +133,12 @@ struct Delivered {
   uint64_t frame_bytes;  // h + L, consumed from the ring on delivery
   uint64_t payload_off;  // into the pass's pinned arena
   std::shared_ptr<uint8_t> arena;
+  // the device handler's answer (HandlerWrap.OnMessage, wrap.go:38-90): the
+  // wire bytes of the reply frame (none: len 0) in the pass's reply buffer and
+  // whether the frame was a close (c.ShutdownWrite(), wrap.go:56)
+  std::shared_ptr<uint8_t> replies;
+  uint64_t reply_off = 0, reply_len = 0;
+  bool shutdown = false;
 };
 
 struct Connection {
@@ -133,6 +146,9 @@ struct Connection {
   int poisoned = GEVWS_OK;               // sticky ERR_LEN_MSB (Appendix A P9/U3)
   std::deque<Delivered> queue;           // decoded, not yet returned by UnPacket
   std::shared_ptr<uint8_t> current;      // keeps the last payload's arena alive
+  std::shared_ptr<uint8_t> current_replies;  // ... and its reply buffer (device handler)
+  uint64_t reply_off = 0, reply_len = 0;
+  bool reply_valid = false, shutdown = false;
   HandshakeResult hs;                    // last Upgrade's response + Handshake
   // Completeness carry (protocol.go:47, 59-61): ring bytes, counted from the
   // ring's read position, that must be buffered before a device pass can
@@ -204,6 +220,11 @@ class Protocol {
       c->need_at = ring->Retrieved();
     }
     c->current = std::move(d.arena);
+    c->current_replies = std::move(d.replies);
+    c->reply_off = d.reply_off;
+    c->reply_len = d.reply_len;
+    c->shutdown = d.shutdown;
+    c->reply_valid = handler_ >= 0;
     *hdr = d.hdr;
     *out = c->current.get() + d.payload_off;
     *out_len = (uint64_t)d.hdr.length;
@@ -212,6 +233,10 @@ class Protocol {
 
   // One device pass over every listed connection that can make progress.
   int64_t UnPacketBatch(Connection* const* conns, RingBuffer* const* rings, uint32_t n) {
+    if (pend_.active) {  // a pass begun by BeginBatch finishes first, as in UnPacket
+      const int64_t e = EndBatch();
+      if (e < 0) return e;
+    }
     const int64_t r = BeginBatch(conns, rings, n);
     if (r <= 0) return r;
     return EndBatch();
@@ -298,6 +323,10 @@ class Protocol {
           return fail();
       }
     }
+    if (handler_ >= 0) {
+      const int64_t h = RunHandler(&sg, arena);
+      if (h < 0) return h;
+    }
     return Deliver(pend_.conns.data(), pend_.rings.data(), pend_.sel, sg, arena);
   }
 
@@ -310,6 +339,10 @@ class Protocol {
     const gevws_conn_out* cout = reinterpret_cast<const gevws_conn_out*>(h_res_ + sizeof(gevws_summary));
     const gevws_frame* fr = reinterpret_cast<const gevws_frame*>(h_out_);
     const uint8_t* hin = h_in_ + sg.coff;
+    const bool handled = handler_ >= 0 && sg.hd.done;
+    const int64_t* rof = reinterpret_cast<const int64_t*>(h_rof_);
+    const uint64_t* roff = reinterpret_cast<const uint64_t*>(h_roff_);
+    const uint64_t nrep = handled ? sg.hd.disp.frames : 0, wire = handled ? sg.hd.enc.payload_bytes : 0;
     // hand the frames to their connections in stream order
     for (uint32_t j = 0; j < m; ++j) {
       Connection* c = conns[sel[j]];
@@ -322,6 +355,15 @@ class Protocol {
         d.frame_bytes = f.src_off + (uint64_t)f.hdr.length - prev_end;
         d.payload_off = f.payload_off;
         d.arena = arena;
+        if (handled) {
+          const int64_t r = rof[o.first_frame + k];
+          if (r >= 0) {
+            d.replies = sg.hd.rbuf;
+            d.reply_off = roff[r];
+            d.reply_len = ((uint64_t)r + 1 < nrep ? roff[r + 1] : wire) - roff[r];
+          }
+          d.shutdown = f.hdr.opcode == 0x8;  // ws.OpClose: ShutdownWrite after the reply (wrap.go:52-56)
+        }
         prev_end = f.src_off + (uint64_t)f.hdr.length;
         c->queue.push_back(std::move(d));
       }
@@ -343,6 +385,10 @@ class Protocol {
                      uint8_t* payload, uint64_t payload_cap, gevws_conn_out* conn_out, gevws_summary* sum_out) {
     gevws_summary zero{};
     *sum_out = zero;
+    if (pend_.active) {  // the pass in flight shares the staging buffers: deliver it first
+      const int64_t e = EndBatch();
+      if (e < 0) return e;
+    }
     if (n == 0) return 0;
     DeviceScope scope(gevws_ctx_device(ctx_));
     Staged sg;
@@ -376,6 +422,22 @@ class Protocol {
   }
 
   void GetStats(gevws_protocol_stats* out) const { *out = stats_; }
+  int SetHandler(int policy) {
+    if (policy < -1 || policy > GEVWS_HANDLER_ECHO_TEXT) return GEVWS_ERR_INVALID;
+    handler_ = policy;
+    return GEVWS_OK;
+  }
+  // The device handler's answer for the frame UnPacket last returned on c.
+  int Reply(Connection* c, const uint8_t** reply, uint64_t* len, int* shutdown) const {
+    *reply = nullptr;
+    *len = 0;
+    *shutdown = 0;
+    if (!c->reply_valid) return GEVWS_ERR_INVALID;
+    if (c->reply_len) *reply = c->current_replies.get() + c->reply_off;
+    *len = c->reply_len;
+    *shutdown = c->shutdown ? 1 : 0;
+    return GEVWS_OK;
+  }
   void SetZeroCopyMax(uint64_t bytes) { zc_max_ = bytes; }
 
  private:
@@ -389,6 +451,81 @@ class Protocol {
       if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
     }
   };
+
+  // After the decode of sg finished (its frames in the pass's outputs: device
+  // memory, or mapped host memory for a zero-copy pass): the handler step,
+  // sized exactly from the decode's summary, then one synchronisation.  The
+  // close bodies go to an aux region behind the payloads in the pass's
+  // payload arena; a capacity miss (more closes than the first guess of aux
+  // slots) re-runs the step once with the exact count.
+  int64_t RunHandler(Staged* sg, std::shared_ptr<uint8_t>& arena) {
+    const uint64_t n = sg->sum.frames;
+    sg->hd = Handled{};
+    sg->hd.done = true;
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+    const uint64_t aux_off = (sg->sum.payload_bytes + 15) & ~15ull;
+    uint64_t aux_slots = std::min<uint64_t>(n, 4096);
+    // reply wire bytes: <= L + 10 per echo / pong / ping, <= 131 per close
+    const uint64_t rcap = sg->sum.payload_len + 141 * n + 16;
+    if (!grow_host(&h_rof_, &h_rof_cap_, 8 * n) || !grow_host(&h_roff_, &h_roff_cap_, 8 * n) ||
+        !grow_host(&h_hs_, &h_hs_cap_, 2 * sizeof(gevws_summary)) || !grow_dev(&d_rep_, &d_rep_cap_, 32 * n))
+      return fail();
+    sg->hd.rbuf = pool_->Acquire(rcap + GEVWS_OUT_PAD);
+    if (!sg->hd.rbuf) return fail();
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      // the aux region lives in the payload arena the decode wrote
+      uint8_t* dpay = nullptr;
+      const uint64_t need = aux_off + 128 * aux_slots + 32;
+      if (sg->zc) {
+        if (sg->arena_cap < need) {  // a bigger mapped arena holding the decoded payloads
+          std::shared_ptr<uint8_t> a = pool_->Acquire(need);
+          if (!a) return fail();
+          memcpy(a.get(), sg->arena.get(), sg->sum.payload_bytes);
+          sg->arena = a;
+          sg->arena_cap = need;
+          arena = a;
+        }
+        dpay = (uint8_t*)device_of(sg->arena.get());
+      } else {
+        if (d_payload_cap_ < need) {  // keep the decoded payloads while growing
+          void* np = nullptr;
+          if (hipStreamSynchronize(st) != hipSuccess || hipMalloc(&np, need + need / 2) != hipSuccess ||
+              hipMemcpy(np, d_payload_, sg->sum.payload_bytes, hipMemcpyDeviceToDevice) != hipSuccess)
+            return fail();
+          (void)hipFree(d_payload_);
+          d_payload_ = np;
+          d_payload_cap_ = need + need / 2;
+        }
+        dpay = (uint8_t*)d_payload_;
+      }
+      const gevws_frame* dfr = sg->zc ? (const gevws_frame*)device_of(h_out_) : (const gevws_frame*)d_frames_;
+      gevws_summary* dhs = (gevws_summary*)device_of(h_hs_);
+      int64_t* drof = (int64_t*)device_of(h_rof_);
+      uint64_t* droff = (uint64_t*)device_of(h_roff_);
+      uint8_t* drb = (uint8_t*)device_of(sg->hd.rbuf.get());
+      if (!dpay || !dfr || !dhs || !drof || !droff || !drb) return fail();
+      if (gevws_dispatch_async(ctx_, st, dfr, n, handler_, dpay, aux_off, 128 * aux_slots, (gevws_out_frame*)d_rep_,
+                               drof, dhs) != GEVWS_OK ||
+          gevws_encode_replies_async(ctx_, st, (const gevws_out_frame*)d_rep_, n, dhs, dpay, drb, rcap, droff,
+                                     dhs + 1) != GEVWS_OK ||
+          hipStreamSynchronize(st) != hipSuccess)
+        return fail();
+      memcpy(&sg->hd.disp, h_hs_, sizeof(gevws_summary));
+      memcpy(&sg->hd.enc, h_hs_ + sizeof(gevws_summary), sizeof(gevws_summary));
+      if (sg->hd.disp.status == GEVWS_ERR_CAPACITY && attempt == 0) {
+        aux_slots = std::max<uint64_t>(sg->hd.disp.payload_bytes, 1);  // aux slots the closes need
+        continue;
+      }
+      break;
+    }
+    if (sg->hd.disp.status != GEVWS_OK || sg->hd.enc.status != GEVWS_OK) {
+      log_error("handler: ", sg->hd.disp.status != GEVWS_OK ? sg->hd.disp.status : sg->hd.enc.status);
+      return GEVWS_ERR_DEVICE;
+    }
+    ++stats_.handler_passes;
+    return 0;
+  }
 
   // Bytes that must be buffered at p for its first frame to be complete
   // (read.go:20-23, U1 and the protocol.go:47 gate); 0 when the header is
@@ -424,7 +561,19 @@ class Protocol {
     return len >= c->need;
   }
 
+  // The device handler's step of a pass: HandlerWrap.OnMessage over every
+  // decoded frame (gevws_dispatch_decoded_async: close -> HandleClose reply,
+  // ping -> pong, pong -> ping, data -> the policy's echo) and FrameToBytes of
+  // the replies (gevws_encode_replies_async), written into mapped pinned host
+  // memory -- reply_of / wire offsets / summaries in the protocol's buffers,
+  // the reply bytes in a pool buffer the delivered frames hold.
+  struct Handled {
+    bool done = false;
+    gevws_summary disp{}, enc{};
+    std::shared_ptr<uint8_t> rbuf;
+  };
   struct Staged {
+    Handled hd;
     std::vector<gevws_conn_in> cin;
     uint64_t coff = 0, total = 0, res = 0, max_frames = 0, payload_cap = 0;
     bool retried = false;  // Finish re-ran the pass: copies enqueued before it are stale
@@ -532,7 +681,11 @@ class Protocol {
     return sg->sum.status == GEVWS_OK ? (int64_t)sg->sum.frames : (int64_t)sg->sum.status;
   }
 
+  // Every failure waits for the context's stream first: a failing step may
+  // follow an enqueued H2D copy or a zero-copy kernel still reading the
+  // pinned staging, which the next pass would overwrite.
   int64_t fail() {
+    if (ctx_) (void)hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_));
     log_error("device: ", GEVWS_ERR_DEVICE);
     return GEVWS_ERR_DEVICE;
   }
@@ -562,9 +715,9 @@ class Protocol {
   }
   void release() {
     if (ctx_) (void)hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_));
-    for (uint8_t* p : {h_in_, h_res_, h_out_})
+    for (uint8_t* p : {h_in_, h_res_, h_out_, h_rof_, h_roff_, h_hs_})
       if (p) (void)hipHostFree(p);
-    for (void* p : {d_in_, d_res_, d_frames_, d_payload_})
+    for (void* p : {d_in_, d_res_, d_frames_, d_payload_, d_rep_})
       if (p) (void)hipFree(p);
   }
 
@@ -587,6 +740,11 @@ class Protocol {
   uint64_t d_in_cap_ = 0, d_res_cap_ = 0, d_frames_cap_ = 0, d_payload_cap_ = 0;
   uint64_t epoch_ = 0;
   uint64_t zc_max_ = GEVWS_ZERO_COPY_MAX_DEFAULT;
+  int handler_ = -1;  // device handler policy (GEVWS_HANDLER_*), -1 = none
+  uint8_t *h_rof_ = nullptr, *h_roff_ = nullptr, *h_hs_ = nullptr;  // handler outputs (mapped pinned)
+  uint64_t h_rof_cap_ = 0, h_roff_cap_ = 0, h_hs_cap_ = 0;
+  void* d_rep_ = nullptr;  // reply records (gevws_out_frame)
+  uint64_t d_rep_cap_ = 0;
   gevws_protocol_stats stats_{};
 };
 
@@ -669,6 +827,17 @@ void gevws_protocol_get_stats(const gevws_protocol* p, gevws_protocol_stats* out
 
 void gevws_protocol_set_zero_copy_max(gevws_protocol* p, uint64_t bytes) {
   if (p) p->SetZeroCopyMax(bytes);
+}
+
+int gevws_protocol_set_handler(gevws_protocol* p, int policy) {
+  if (!p) return GEVWS_ERR_INVALID;
+  return p->SetHandler(policy);
+}
+
+int gevws_protocol_reply(const gevws_protocol* p, const gevws_conn* c, const uint8_t** reply, uint64_t* len,
+                         int* shutdown_write) {
+  if (!p || !c || !reply || !len || !shutdown_write) return GEVWS_ERR_INVALID;
+  return p->Reply(const_cast<gevws_conn*>(c), reply, len, shutdown_write);
 }
 
 int64_t gevws_decode_host_batch(gevws_protocol* p, const gevws_host_conn* conns, uint32_t n,

@@ -60,6 +60,12 @@ struct DeviceDecoder {
   int unpacket(wslb::ServerConn* s, gevws_header* h, const uint8_t** data, uint64_t* len) {
     return gevws_protocol_unpacket(p, s->c, s->r, h, data, len);
   }
+  // HandlerWrap.OnMessage on the device (the protocol's handler step)
+  static constexpr bool kHandler = true;
+  void set_handler(int policy) { gevws_protocol_set_handler(p, policy); }
+  int reply(wslb::ServerConn* s, const uint8_t** out, uint64_t* len, int* shutdown_write) {
+    return gevws_protocol_reply(p, s->c, out, len, shutdown_write);
+  }
   static const char* name() { return "device"; }
   static const char* path() { return "batched device decode (gevws_protocol_unpacket_batch) -> UnPacket"; }
 };

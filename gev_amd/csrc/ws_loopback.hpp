@@ -28,8 +28,28 @@
 // sends one masked text frame of M random bytes, waits for the echo, checks it
 // byte for byte, repeats for the run time.
 //
+// --mode wsserver mirrors the reference's own end-to-end test,
+// example/websocket/wsserver_test.go:73-133 with wsExample (:22-70): every
+// client sends masked text frames of random 1..3072 bytes and reads the same
+// number of bytes back (io.ReadFull + bytes.Equal); the server's OnMessage
+// answers (MessageText, data) either by return value or by c.Send(PackData)
+// at random (:47-63) -- here every frame's reply is computed on the device by
+// the protocol's handler step (HandlerWrap.OnMessage + FrameToBytes,
+// gevws_protocol_set_handler(GEVWS_HANDLER_ECHO_TEXT)) and routed either into
+// the returned `out` (sent after the connection's handlerProtocol) or into a
+// queue sent after the loop iteration (c.Send -> QueueInLoop).  --ctrl P
+// precedes a message with a masked ping (or pong) with probability P; the
+// device's control reply (pong / the reference's ping-for-pong) is returned
+// inline; --close-end 1 ends every client with a close frame (valid, reserved,
+// unknown and application codes; UTF-8 and invalid reasons; empty bodies),
+// answered by util.HandleClose's reply plus ShutdownWrite (wrap.go:45-68), so
+// the client must see the reply and then EOF.  --transcript FILE writes every
+// (control frame sent, reply received) pair as hex for the oracle check
+// (tests/test_gpu_loopback.py against oracle/ws_oracle.on_message).
+//
 //   [--conns 1000] [--msg 128] [--seconds 5] [--loops 1] [--client-threads 4]
-//   [--port 0] [--device 0]
+//   [--port 0] [--device 0] [--mode echo|wsserver] [--ctrl 0] [--close-end 0]
+//   [--transcript FILE] [--seed 1]
 // Prints one JSON line.
 #pragma once
 
@@ -45,6 +65,8 @@
 
 #include <atomic>
 #include <chrono>
+#include <deque>
+#include <mutex>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -61,6 +83,19 @@ namespace wslb {
 
 inline std::atomic<bool> g_stop{false};
 inline std::atomic<uint64_t> g_batches{0}, g_batch_conns{0}, g_frames{0}, g_bad{0}, g_dev_ns{0};
+inline std::atomic<uint64_t> g_ctrl{0}, g_closed{0}, g_sent_async{0}, g_payload{0};
+
+enum { kModeEcho = 0, kModeWsServer = 1 };
+struct Config {
+  int mode = kModeEcho;
+  double ctrl_prob = 0.0;  // wsserver: a control frame before a message with this probability
+  bool close_end = false;  // wsserver: every client ends with a close frame
+  std::string transcript;  // wsserver: (control frame sent, reply) pairs, hex
+  unsigned seed = 1;
+};
+inline Config g_cfg;
+inline std::mutex g_tr_mu;
+inline std::vector<std::pair<std::vector<uint8_t>, std::vector<uint8_t>>> g_transcript;
 
 inline double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -107,6 +142,8 @@ struct ServerConn {
   std::vector<uint8_t> out;
   std::vector<uint8_t> frame;  // CpuDecoder: the payload slice it returned last (Go's make)
   int poisoned = 0;
+  std::vector<uint8_t> queued;  // wsserver: c.Send(PackData(...)) output, sent after the loop iteration
+  bool shut = false;            // wsserver: ShutdownWrite done (a close was answered)
 };
 
 // Decoder concept:
@@ -114,9 +151,15 @@ struct ServerConn {
 //   int64_t pass(ServerConn* const* conns, uint32_t n);   // readable upgraded connections
 //   int unpacket(ServerConn* s, gevws_header* h, const uint8_t** data, uint64_t* len);
 //   static const char* name();
+//   static constexpr bool kHandler;  // reply(): HandlerWrap.OnMessage's answer for the last frame
+//   void set_handler(int policy);
+//   int reply(ServerConn* s, const uint8_t** out, uint64_t* len, int* shutdown_write);
 template <class Decoder>
-void server_loop(int port, int device, std::atomic<int>* ready) {
+void server_loop(int port, int device, std::atomic<int>* ready, int index) {
   Decoder dec(device);
+  const bool wss = g_cfg.mode == kModeWsServer;
+  if (wss) dec.set_handler(GEVWS_HANDLER_ECHO_TEXT);  // wsExample.OnMessage returns (MessageText, data)
+  std::mt19937_64 route(g_cfg.seed * 1000003u + (unsigned)index);  // wsserver_test.go:47: rand.Int() % 2
   int ls = socket(AF_INET, SOCK_STREAM, 0);
   int one = 1;
   setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
@@ -152,8 +195,10 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
   const bool pipeline = Decoder::kPipelined && pe && atoi(pe) == 1;
   bool pending = false;
   // handlerProtocol for one connection: UnPacket until (nil, nil), echo
+  std::vector<ServerConn*> queued_conns;
   auto handle = [&](ServerConn* s, double& t_dec) {
     s->out.clear();
+    bool shut = false;
     for (;;) {
       gevws_header h;
       const uint8_t* data = nullptr;
@@ -161,20 +206,65 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
       const double tu = now_s();
       const int st = dec.unpacket(s, &h, &data, &len);
       t_dec += now_s() - tu;
-      if (st == GEVWS_OK) {
+      if (st == GEVWS_OK && wss) {
+        // HandlerWrap.OnMessage (wrap.go:38-90): the device handler's reply
+        const uint8_t* rp = nullptr;
+        uint64_t rl = 0;
+        int sh = 0;
+        std::vector<uint8_t> host_reply;
+        if constexpr (Decoder::kHandler) {
+          if (dec.reply(s, &rp, &rl, &sh) != GEVWS_OK) g_bad.fetch_add(1);
+        } else if (!(h.opcode & 0x8) && len) {  // CPU twin: data frames only, echoed as text on the host
+          uint8_t hdr[14];
+          const uint32_t hn = write_header(hdr, 0x81, len);
+          host_reply.assign(hdr, hdr + hn);
+          host_reply.insert(host_reply.end(), data, data + len);
+          rp = host_reply.data();
+          rl = host_reply.size();
+        }
+        if (h.opcode & 0x8) {  // control: HandlerWrap returns the reply (sent with handlerProtocol's out)
+          s->out.insert(s->out.end(), rp, rp + rl);
+          shut = shut || sh;
+          g_ctrl.fetch_add(1, std::memory_order_relaxed);
+        } else {
+          if (route() & 1) {  // case 1: c.Send(util.PackData(ws.MessageText, data)) -> QueueInLoop
+            if (s->queued.empty()) queued_conns.push_back(s);
+            s->queued.insert(s->queued.end(), rp, rp + rl);
+            g_sent_async.fetch_add(1, std::memory_order_relaxed);
+          } else {  // case 0: out = data, framed by HandlerWrap (NewTextFrame + FrameToBytes)
+            s->out.insert(s->out.end(), rp, rp + rl);
+          }
+          g_frames.fetch_add(1, std::memory_order_relaxed);
+          g_payload.fetch_add(len, std::memory_order_relaxed);
+        }
+      } else if (st == GEVWS_OK) {
         if (h.opcode & 0x8) continue;  // control frames: not in this workload
         uint8_t hdr[14];
         const uint32_t hn = write_header(hdr, 0x82, len);  // NewBinaryFrame + FrameToBytes
         s->out.insert(s->out.end(), hdr, hdr + hn);
         s->out.insert(s->out.end(), data, data + len);
         g_frames.fetch_add(1, std::memory_order_relaxed);
+        g_payload.fetch_add(len, std::memory_order_relaxed);
       } else if (len != 0) {
         s->out.insert(s->out.end(), data, data + len);  // handshake response (wrap.go:40-42)
       } else {
         break;
       }
     }
-    if (!s->out.empty() && !send_all(s->fd, s->out.data(), s->out.size())) g_bad.fetch_add(1);
+    if (!s->out.empty() && !s->shut && !send_all(s->fd, s->out.data(), s->out.size())) g_bad.fetch_add(1);
+    if (shut && !s->shut) {  // c.ShutdownWrite() after the close reply (wrap.go:56)
+      ::shutdown(s->fd, SHUT_WR);
+      s->shut = true;
+      g_closed.fetch_add(1, std::memory_order_relaxed);
+    }
+  };
+  // the loop's pending functions (doPendingFunc): the c.Send calls of this iteration
+  auto flush_queued = [&]() {
+    for (ServerConn* s : queued_conns) {
+      if (!s->shut && !s->queued.empty() && !send_all(s->fd, s->queued.data(), s->queued.size())) g_bad.fetch_add(1);
+      s->queued.clear();
+    }
+    queued_conns.clear();
   };
   // the pass in flight, ended and its frames handed out (also before a
   // connection it holds is closed: the protocol writes to its rings' owners)
@@ -217,6 +307,7 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
       if (k <= 0) {
         if (k < 0 && (errno == EAGAIN || errno == EINTR)) continue;
         finish(t_close);
+        flush_queued();
         epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
         close(fd);
         gevws_conn_free(it->second.c);
@@ -234,6 +325,7 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
     t_close = 0;
     finish(t_dec);  // the pass begun last iteration: its frames go out now
     if (readable.empty()) {
+      flush_queued();
       g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
       continue;
     }
@@ -260,6 +352,7 @@ void server_loop(int port, int device, std::atomic<int>* ready) {
     }
     if (!pipeline)
       for (ServerConn* s : readable) handle(s, t_dec);  // handlerProtocol per connection
+    flush_queued();
     g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
   }
   if (pending) (void)dec.end();
@@ -372,6 +465,195 @@ inline void client_thread(int port, int nconn, size_t msg, double t_end, std::at
   close(ep);
 }
 
+// ------------------------------------------------------------------ wsserver_test.go client
+// startWebSocketClient (wsserver_test.go:101-133): masked text frames of
+// 1..3072 random bytes, the echo read back in full and compared; optional
+// control frames (--ctrl) before a message and a closing handshake at the end
+// (--close-end).  Server frames are parsed as they arrive: text payload bytes
+// accumulate until the message's length (io.ReadFull), control frames are
+// paired with the control frame they answer (in order) for the transcript.
+struct WsClient {
+  int fd = -1;
+  bool upgraded = false;
+  int state = 0;  // 0 running, 1 close sent (reply + EOF expected), 2 done
+  std::vector<uint8_t> in, data, got;
+  std::deque<std::vector<uint8_t>> ctrl_sent;  // control frames awaiting their reply
+  uint64_t done = 0;
+};
+
+inline std::vector<uint8_t> masked_frame(std::mt19937_64& rng, uint8_t b0, const uint8_t* p, size_t n) {
+  std::vector<uint8_t> f(14 + n);
+  uint32_t hn = write_header(f.data(), b0, n);
+  f[1] |= 0x80;
+  const uint32_t key = (uint32_t)rng();
+  memcpy(f.data() + hn, &key, 4);
+  const uint8_t* m = f.data() + hn;
+  hn += 4;
+  for (size_t i = 0; i < n; ++i) f[hn + i] = p[i] ^ m[i & 3];
+  f.resize(hn + n);
+  return f;
+}
+
+inline void ws_client_next(WsClient& c, std::mt19937_64& rng) {
+  std::uniform_real_distribution<double> u(0.0, 1.0);
+  if (g_cfg.ctrl_prob > 0 && u(rng) < g_cfg.ctrl_prob) {  // a ping (or a pong) before the message
+    std::vector<uint8_t> p(rng() % 126);
+    for (auto& b : p) b = (uint8_t)rng();
+    auto f = masked_frame(rng, u(rng) < 0.8 ? 0x89 : 0x8A, p.data(), p.size());
+    if (!send_all(c.fd, f.data(), f.size())) g_bad.fetch_add(1);
+    c.ctrl_sent.push_back(std::move(f));
+  }
+  c.data.resize(rng() % (1024 * 3) + 1);  // wsserver_test.go:112
+  for (auto& b : c.data) b = (uint8_t)rng();
+  c.got.clear();
+  auto f = masked_frame(rng, 0x81, c.data.data(), c.data.size());  // x/net/websocket: text frames
+  if (!send_all(c.fd, f.data(), f.size())) g_bad.fetch_add(1);
+}
+
+inline void ws_client_close(WsClient& c, std::mt19937_64& rng) {
+  static const uint16_t kCodes[] = {1000, 1001, 1002, 1003, 1005, 1006, 1007, 1011, 1015, 1016, 2999, 3000, 4999, 999};
+  static const char* kReasons[] = {"", "bye", "normal closure", "\xc3\x28", "caf\xc3\xa9", "\xff"};
+  std::vector<uint8_t> body;
+  if (rng() % 8) {
+    const uint16_t code = kCodes[rng() % (sizeof(kCodes) / sizeof(kCodes[0]))];
+    body.push_back((uint8_t)(code >> 8));
+    body.push_back((uint8_t)code);
+    const char* r = kReasons[rng() % (sizeof(kReasons) / sizeof(kReasons[0]))];
+    body.insert(body.end(), r, r + strlen(r));
+  }
+  auto f = masked_frame(rng, 0x88, body.data(), body.size());
+  if (!send_all(c.fd, f.data(), f.size())) g_bad.fetch_add(1);
+  c.ctrl_sent.push_back(std::move(f));
+  c.state = 1;
+}
+
+inline void ws_client_thread(int port, int nconn, double t_end, std::atomic<uint64_t>* total,
+                             std::atomic<int>* upgraded_conns, unsigned seed) {
+  std::mt19937_64 rng(seed);
+  int ep = epoll_create1(0);
+  std::vector<WsClient> cs(nconn);
+  std::vector<std::pair<std::vector<uint8_t>, std::vector<uint8_t>>> tr;
+  const char req_fmt[] =
+      "GET / HTTP/1.1\r\nHost: 127.0.0.1:%d\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+      "Sec-WebSocket-Key: dGhlIHNhbXBsZSBub25jZQ==\r\nOrigin: ws://127.0.0.1\r\nSec-WebSocket-Version: 13\r\n\r\n";
+  char req[512];
+  const int rn = snprintf(req, sizeof(req), req_fmt, port);
+  for (int i = 0; i < nconn; ++i) {
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (fd < 0 || connect(fd, (sockaddr*)&a, sizeof(a))) {
+      perror("ws_loopback: connect");
+      _exit(2);
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    set_nonblock(fd);
+    cs[i].fd = fd;
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u32 = (uint32_t)i;
+    epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
+    send_all(fd, (const uint8_t*)req, (size_t)rn);
+  }
+  std::vector<epoll_event> evs(1024);
+  std::vector<uint8_t> buf(1 << 16);
+  const double t_hard = t_end + 5.0;  // closing handshakes must finish by then
+  int finished = 0;
+  while (!g_stop.load(std::memory_order_relaxed)) {
+    const double now = now_s();
+    if (now >= t_hard || (now >= t_end && (!g_cfg.close_end || finished == nconn))) break;
+    const int n = epoll_wait(ep, evs.data(), (int)evs.size(), 5);
+    for (int e = 0; e < n; ++e) {
+      WsClient& c = cs[evs[e].data.u32];
+      if (c.state == 2) continue;
+      const ssize_t k = ::read(c.fd, buf.data(), buf.size());
+      if (k == 0) {  // EOF: only after the close reply (the server's ShutdownWrite)
+        if (c.state == 1 && c.ctrl_sent.empty()) {
+          c.state = 2;
+          ++finished;
+          epoll_ctl(ep, EPOLL_CTL_DEL, c.fd, nullptr);
+        } else {
+          g_bad.fetch_add(1);
+          c.state = 2;
+          ++finished;
+          epoll_ctl(ep, EPOLL_CTL_DEL, c.fd, nullptr);
+        }
+        continue;
+      }
+      if (k < 0) continue;
+      c.in.insert(c.in.end(), buf.data(), buf.data() + k);
+      if (!c.upgraded) {
+        const std::string s(c.in.begin(), c.in.end());
+        const size_t pos = s.find("\r\n\r\n");
+        if (pos == std::string::npos) continue;
+        if (s.compare(0, 12, "HTTP/1.1 101") != 0 || s.find("s3pPLMBiTxaQ9kYGzzhZRbK+xOo=") == std::string::npos) {
+          g_bad.fetch_add(1);
+          continue;
+        }
+        c.in.erase(c.in.begin(), c.in.begin() + (long)pos + 4);
+        c.upgraded = true;
+        upgraded_conns->fetch_add(1);
+        ws_client_next(c, rng);
+      }
+      // server frames (unmasked)
+      size_t off = 0;
+      for (;;) {
+        const size_t avail = c.in.size() - off;
+        if (avail < 2) break;
+        const uint8_t* f = c.in.data() + off;
+        const uint32_t len7 = f[1] & 0x7f;
+        const size_t hn = len7 < 126 ? 2 : (len7 == 126 ? 4 : 10);
+        if (avail < hn) break;
+        uint64_t L = len7;
+        if (len7 == 126) L = ((uint64_t)f[2] << 8) | f[3];
+        if (len7 == 127) {
+          L = 0;
+          for (int i = 0; i < 8; ++i) L = (L << 8) | f[2 + i];
+        }
+        if ((f[1] & 0x80) || avail - hn < L) {
+          if (f[1] & 0x80) g_bad.fetch_add(1);  // a server frame must not be masked
+          break;
+        }
+        if (f[0] & 0x08) {  // a control reply: pair it with the oldest unanswered control frame
+          if (c.ctrl_sent.empty()) {
+            g_bad.fetch_add(1);
+          } else {
+            tr.emplace_back(std::move(c.ctrl_sent.front()), std::vector<uint8_t>(f, f + hn + L));
+            c.ctrl_sent.pop_front();
+          }
+        } else {
+          if (f[0] != 0x81) g_bad.fetch_add(1);  // wsExample answers MessageText, FIN
+          c.got.insert(c.got.end(), f + hn, f + hn + L);
+        }
+        off += hn + L;
+      }
+      c.in.erase(c.in.begin(), c.in.begin() + (long)off);
+      if (c.state == 0 && c.ctrl_sent.empty() && c.got.size() >= c.data.size()) {
+        if (c.got != c.data) g_bad.fetch_add(1);  // bytes.Equal (wsserver_test.go:128-130)
+        c.done++;
+        if (now_s() >= t_end) {
+          if (g_cfg.close_end) ws_client_close(c, rng);
+        } else {
+          ws_client_next(c, rng);
+        }
+      }
+    }
+  }
+  uint64_t sum = 0;
+  for (auto& c : cs) {
+    sum += c.done;
+    if (g_cfg.close_end && c.state != 2) g_bad.fetch_add(1);  // closing handshake unfinished
+    close(c.fd);
+  }
+  total->fetch_add(sum);
+  close(ep);
+  std::lock_guard<std::mutex> g(g_tr_mu);
+  for (auto& p : tr) g_transcript.push_back(std::move(p));
+}
+
 template <class Decoder>
 int loopback_main(int argc, char** argv) {
   int conns = 1000, loops = 1, cthreads = 4, port = 0, device = 0;
@@ -387,6 +669,16 @@ int loopback_main(int argc, char** argv) {
     else if (k == "--client-threads") cthreads = atoi(v);
     else if (k == "--port") port = atoi(v);
     else if (k == "--device") device = atoi(v);
+    else if (k == "--mode") g_cfg.mode = std::string(v) == "wsserver" ? kModeWsServer : kModeEcho;
+    else if (k == "--ctrl") g_cfg.ctrl_prob = atof(v);
+    else if (k == "--close-end") g_cfg.close_end = atoi(v) != 0;
+    else if (k == "--transcript") g_cfg.transcript = v;
+    else if (k == "--seed") g_cfg.seed = (unsigned)atoi(v);
+  }
+  const bool wss = g_cfg.mode == kModeWsServer;
+  if (wss && !Decoder::kHandler && (g_cfg.ctrl_prob > 0 || g_cfg.close_end)) {
+    fprintf(stderr, "ws_loopback: control frames need the device handler (%s has none)\n", Decoder::name());
+    return 2;
   }
   if (port == 0) port = 20000 + (int)(getpid() % 20000);
   // both ends of every connection live in this process: 2 fds per connection
@@ -401,7 +693,7 @@ int loopback_main(int argc, char** argv) {
   }
   std::atomic<int> ready{0};
   std::vector<std::thread> servers;
-  for (int l = 0; l < loops; ++l) servers.emplace_back(server_loop<Decoder>, port, device, &ready);
+  for (int l = 0; l < loops; ++l) servers.emplace_back(server_loop<Decoder>, port, device, &ready, l);
   while (ready.load() < loops) std::this_thread::sleep_for(std::chrono::milliseconds(5));
 
   std::atomic<uint64_t> total{0};
@@ -412,31 +704,53 @@ int loopback_main(int argc, char** argv) {
   std::vector<std::thread> clients;
   for (int t = 0; t < cthreads; ++t) {
     const int n = conns / cthreads + (t < conns % cthreads ? 1 : 0);
-    clients.emplace_back(client_thread, port, n, msg, t_end, &total, &upgraded, 1234u + t);
+    if (wss)
+      clients.emplace_back(ws_client_thread, port, n, t_end, &total, &upgraded, 1234u * g_cfg.seed + t);
+    else
+      clients.emplace_back(client_thread, port, n, msg, t_end, &total, &upgraded, 1234u + t);
   }
   // measure the steady state: count frames echoed between warm-up end and t_end
   std::this_thread::sleep_for(std::chrono::duration<double>(warm));
   const uint64_t f0 = g_frames.load(), b0 = g_batches.load(), c0 = g_batch_conns.load(), d0 = g_dev_ns.load();
+  const uint64_t p0 = g_payload.load();
   const double ts = now_s();
   std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
   const double te = now_s();
   const uint64_t f1 = g_frames.load(), b1 = g_batches.load(), c1 = g_batch_conns.load(), d1 = g_dev_ns.load();
+  const uint64_t p1 = g_payload.load();
   for (auto& t : clients) t.join();
   g_stop = true;
   for (auto& t : servers) t.join();
   const double dt = te - ts;
   const double mps = (double)(f1 - f0) / dt;
+  if (!g_cfg.transcript.empty()) {
+    FILE* tf = fopen(g_cfg.transcript.c_str(), "w");
+    if (!tf) {
+      perror("ws_loopback: transcript");
+      return 2;
+    }
+    for (auto& p : g_transcript) {
+      for (uint8_t b : p.first) fprintf(tf, "%02x", b);
+      fputc(' ', tf);
+      for (uint8_t b : p.second) fprintf(tf, "%02x", b);
+      fputc('\n', tf);
+    }
+    fclose(tf);
+  }
   printf("{\"path\": \"loopback websocket echo server: epoll loops -> ring buffers -> %s -> echo\", "
          "\"decoder\": \"%s\", \"connections\": %d, \"upgraded\": %d, "
          "\"msg_bytes\": %zu, \"loops\": %d, \"client_threads\": %d, \"seconds\": %.3f, "
          "\"echoes_per_s\": %.1f, \"payload_MiBps_each_way\": %.2f, \"decode_passes_per_s\": %.1f, "
          "\"mean_conns_per_pass\": %.1f, \"decode_us_per_pass\": %.1f, \"decode_share_of_loop_time\": %.3f, "
-         "\"client_checked_echoes\": %llu, \"errors\": %llu}\n",
-         Decoder::path(), Decoder::name(), conns, upgraded.load(), msg, loops, cthreads, dt, mps,
-         mps * (double)msg / 1048576.0, (double)(b1 - b0) / dt,
+         "\"client_checked_echoes\": %llu, \"mode\": \"%s\", \"control_frames\": %llu, "
+         "\"async_sends\": %llu, \"closes_answered\": %llu, \"transcript_pairs\": %zu, \"errors\": %llu}\n",
+         Decoder::path(), Decoder::name(), conns, upgraded.load(), wss ? (size_t)0 : msg, loops, cthreads, dt, mps,
+         (double)(p1 - p0) / dt / 1048576.0, (double)(b1 - b0) / dt,
          b1 > b0 ? (double)(c1 - c0) / (double)(b1 - b0) : 0.0,
          b1 > b0 ? (double)(d1 - d0) / 1e3 / (double)(b1 - b0) : 0.0, (double)(d1 - d0) / 1e9 / (dt * loops),
-         (unsigned long long)total.load(), (unsigned long long)g_bad.load());
+         (unsigned long long)total.load(), wss ? "wsserver" : "echo", (unsigned long long)g_ctrl.load(),
+         (unsigned long long)g_sent_async.load(), (unsigned long long)g_closed.load(), g_transcript.size(),
+         (unsigned long long)g_bad.load());
   return g_bad.load() == 0 && upgraded.load() == conns ? 0 : 1;
 }
 

@@ -179,6 +179,18 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
 #define GEVWS_TUNE_SPLIT_LANES 8
 #define GEVWS_TUNE_SPLIT_MODE 9  /* measurement: 1 = split guesses made then dropped, 2 = none made, \
                                     3 = keep the walk's speculation after a mixed-size batch */
+/* Budgeted header walk (a batch of many long chains of small frames): every
+ * lane walks its connection for at most this many frames, then the
+ * connections not finished are walked on from where they stopped with
+ * GEVWS_TUNE_RESUME_LANES lanes each (k_walk_split's guesses, checked by the
+ * chain itself, over the rest of the stream).  0 = auto (after a decode on
+ * this context whose connections averaged >= 256 frames of <= 4 KiB, when the
+ * split walk is not chosen: GEVWS_TUNE_BUDGET_FRAC 16ths of that mean), -1 =
+ * never, > 0 = this budget for every multi-kernel decode (instead of the
+ * split walk's auto choice; GEVWS_TUNE_SPLIT_LANES >= 2 still splits). */
+#define GEVWS_TUNE_WALK_BUDGET 10
+#define GEVWS_TUNE_RESUME_LANES 11  /* 0 = default (8), else 2 / 4 / 8 / 16 */
+#define GEVWS_TUNE_BUDGET_FRAC 12   /* auto budget in 16ths of the previous mean chain (default 18) */
 int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
 /* Lanes per connection the last multi-kernel decode's header walk used (1 =
  * not split; GEVWS_TUNE_SPLIT_LANES), -1 for a null context.  The auto choice
@@ -186,6 +198,11 @@ int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
  * has shown long chains of small frames (>= 256 frames per connection of <= 4
  * KiB each). */
 int gevws_ctx_last_split_lanes(const gevws_ctx *ctx);
+/* Frames per lane of the last multi-kernel decode's budgeted walk (0 = not
+ * budgeted; -1 for a null context), and the connections it resumed (waits for
+ * the context's last call; < 0 on error). */
+int64_t gevws_ctx_last_walk_budget(const gevws_ctx *ctx);
+int64_t gevws_ctx_last_resumed(gevws_ctx *ctx);
 /* Workgroups of the last multi-kernel decode's unmask launch (-1 for a null
  * context): 4 per CU, or 32 per CU after a decode on this context of a batch
  * of mixed frame sizes below 8 GiB of output (the kernel then uses the wide
@@ -278,6 +295,21 @@ int gevws_dispatch_async(gevws_ctx *ctx, void *stream, const gevws_frame *d_fram
                          uint8_t *d_payload, uint64_t aux_off, uint64_t aux_cap,
                          gevws_out_frame *d_replies, int64_t *d_reply_of, gevws_summary *d_summary);
 
+/* The same two steps chained after a decode with no host round trip (a live
+ * pass: decode -> HandlerWrap.OnMessage -> FrameToBytes on the device): the
+ * frame / reply count is read on the device from the previous step's summary
+ * (d_decoded: the decode's; d_dispatched: the dispatch's), none when that
+ * step failed; max_frames / max_replies only bound the launch and the
+ * buffers (d_reply_of: max_frames entries, d_replies / d_out_off:
+ * max_replies). */
+int gevws_dispatch_decoded_async(gevws_ctx *ctx, void *stream, const gevws_frame *d_frames, uint64_t max_frames,
+                                 const gevws_summary *d_decoded, int policy, uint8_t *d_payload, uint64_t aux_off,
+                                 uint64_t aux_cap, gevws_out_frame *d_replies, int64_t *d_reply_of,
+                                 gevws_summary *d_summary);
+int gevws_encode_replies_async(gevws_ctx *ctx, void *stream, const gevws_out_frame *d_replies,
+                               uint64_t max_replies, const gevws_summary *d_dispatched, const uint8_t *d_payload,
+                               uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off, gevws_summary *d_summary);
+
 /* Measurement helper, not on the reference path: n bytes (n % 16 == 0, d_dst
  * 16-byte aligned, d_src any alignment) copied with the unmask kernel's
  * streaming access pattern minus the XOR and frame lookup -- the achievable
@@ -285,7 +317,8 @@ int gevws_dispatch_async(gevws_ctx *ctx, void *stream, const gevws_frame *d_fram
  * CU (the unmask kernel's grid for large frames); grid | 0x80000000 deals
  * 64 KiB blocks round-robin over the workgroups instead of contiguous runs;
  * grid | 0x40000000 uses plain loads instead of the non-temporal ones the
- * unmask kernel's streaming path uses. */
+ * unmask kernel's streaming path uses; grid | 0x20000000 copies in the
+ * unmask's wave layout (each wave a contiguous 16 KiB span per step). */
 int gevws_copy_async(gevws_ctx *ctx, void *stream, uint8_t *d_dst, const uint8_t *d_src, uint64_t n,
                      uint32_t grid);
 
@@ -417,7 +450,9 @@ int gevws_protocol_unpacket(gevws_protocol *p, gevws_conn *c, gevws_ring *ring,
 /* Batched driver for an event loop: one device pass over the buffered bytes of
  * n connections (stage -> H2D -> decode -> D2H); afterwards
  * gevws_protocol_unpacket returns their frames in stream order with no further
- * device work.  Returns the number of frames decoded, or < 0. */
+ * device work.  A pass still in flight from _begin below is finished (its
+ * frames queued) first, as gevws_protocol_unpacket does.  Returns the number
+ * of frames decoded, or < 0. */
 int64_t gevws_protocol_unpacket_batch(gevws_protocol *p, gevws_conn *const *conns,
                                       gevws_ring *const *rings, uint32_t n);
 
@@ -430,8 +465,10 @@ int64_t gevws_protocol_unpacket_batch(gevws_protocol *p, gevws_conn *const *conn
  * waits for that pass and queues its frames, returning the number of frames
  * decoded (0 when none is in flight) or < 0.  Between the two the rings may
  * take new bytes (gevws_ring_write; the pass decodes its staged copy) but must
- * not be read or retrieved; gevws_protocol_unpacket ends a pass in flight
- * first. */
+ * not be read or retrieved; gevws_protocol_unpacket, _unpacket_batch and
+ * gevws_decode_host_batch end a pass in flight first.  The protocol keeps the
+ * `conns` and `rings` pointers (not the arrays) until _end: every connection
+ * and ring listed must stay alive until then. */
 int64_t gevws_protocol_unpacket_batch_begin(gevws_protocol *p, gevws_conn *const *conns,
                                             gevws_ring *const *rings, uint32_t n);
 int64_t gevws_protocol_unpacket_batch_end(gevws_protocol *p);
@@ -447,6 +484,7 @@ typedef struct gevws_protocol_stats {
     uint64_t bytes_staged;
     uint64_t gated;
     uint64_t zero_copy_passes;
+    uint64_t handler_passes;  /* passes that ran the device handler step */
 } gevws_protocol_stats;
 void gevws_protocol_get_stats(const gevws_protocol *p, gevws_protocol_stats *out);
 
@@ -457,6 +495,21 @@ void gevws_protocol_get_stats(const gevws_protocol *p, gevws_protocol_stats *out
  * with no H2D / D2H copies (a small pass is latency, not bytes).  Larger
  * passes copy in and out (DMA at the PCIe rate). */
 #define GEVWS_ZERO_COPY_MAX_DEFAULT (256u * 1024u)
+
+/* websocket.HandlerWrap.OnMessage (plugins/websocket/wrap.go:38-90) on the
+ * device for every frame a pass decodes: policy GEVWS_HANDLER_* (-1 = off, the
+ * default).  Each pass then also runs gevws_dispatch_async + encode over its
+ * frames (close -> util.HandleClose reply, ping -> pong, pong -> ping, data ->
+ * the policy's echo as a binary / text frame; FrameToBytes of each) and one
+ * more synchronisation; gevws_protocol_reply hands out the answer. */
+int gevws_protocol_set_handler(gevws_protocol *p, int policy);
+/* The handler's answer for the frame gevws_protocol_unpacket last returned on
+ * c: *reply / *len = the reply frame's wire bytes (the `out` OnMessage returns;
+ * len 0 = none), *shutdown_write = 1 for a close frame (c.ShutdownWrite() after
+ * sending the reply, wrap.go:52-56).  Valid until the next UnPacket on c.
+ * GEVWS_ERR_INVALID when no handler is set or no frame was returned yet. */
+int gevws_protocol_reply(const gevws_protocol *p, const gevws_conn *c, const uint8_t **reply, uint64_t *len,
+                         int *shutdown_write);
 void gevws_protocol_set_zero_copy_max(gevws_protocol *p, uint64_t bytes);
 
 /* One connection's buffered bytes in host memory, as ringbuffer.PeekAll()

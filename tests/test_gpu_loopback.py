@@ -18,12 +18,12 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(binary, conns=100, seconds=2.0, msg=128, loops=1, threads=2, env=None):
+def _run(binary, conns=100, seconds=2.0, msg=128, loops=1, threads=2, env=None, extra=()):
     path = os.path.join(ROOT, binary)
     assert os.path.exists(path), f"{binary} not built (python -c 'import __graft_entry__ as g; g.build()')"
     r = subprocess.run([path, "--conns", str(conns), "--seconds", str(seconds), "--msg", str(msg), "--loops",
-                        str(loops), "--client-threads", str(threads)], capture_output=True, text=True, timeout=120,
-                       env={**os.environ, **(env or {})})
+                        str(loops), "--client-threads", str(threads), *extra], capture_output=True, text=True,
+                       timeout=120, env={**os.environ, **(env or {})})
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert r.returncode == 0 and len(lines) == 1, (r.returncode, r.stdout[-1500:], r.stderr[-1500:])
     d = json.loads(lines[0])
@@ -60,3 +60,53 @@ def test_c1_loopback_pipelined_loop(msg):
     holds is closed; every echo still checked byte for byte."""
     _run("gev_amd/ws_loopback", conns=100 if msg == 128 else 16, seconds=1.5, msg=msg,
          env={"GEVWS_LB_PIPELINE": "1"})
+
+
+# ---------------------------------------------------------------- wsserver_test.go on the live server
+def test_wsserver_test_mirror_8_loops_100_clients():
+    """example/websocket/wsserver_test.go:73-133, the reference's own hot-path
+    test: 8 loops, 100 clients for 2 s, each sending masked text frames of
+    random 1..3072 bytes and reading the echo back in full (bytes.Equal); the
+    server answers (MessageText, data) by return value or by c.Send(PackData)
+    at random (:47-63).  Here the answer of every frame is computed on the
+    device (the protocol's handler step: HandlerWrap.OnMessage + FrameToBytes)
+    and both routes are taken; zero mismatches."""
+    d = _run("gev_amd/ws_loopback", conns=100, seconds=2.0, loops=8, threads=4, extra=("--mode", "wsserver"))
+    assert d["mode"] == "wsserver" and d["decoder"] == "device"
+    assert d["client_checked_echoes"] > 1000
+    assert d["async_sends"] > 0  # both reply routes taken
+
+
+def test_wsserver_mirror_cpu_twin_beside():
+    """The same mirror on the CPU-decode twin (host-framed text echo): the
+    baseline server passes the reference test's checks too."""
+    d = _run("tools/ws_loopback_cpu", conns=100, seconds=2.0, loops=8, threads=4, extra=("--mode", "wsserver"))
+    assert d["client_checked_echoes"] > 1000
+
+
+def test_wsserver_control_frames_match_oracle(tmp_path):
+    """Control frames on the live server, answered by the device dispatch
+    inside the loop: clients put a masked ping (or pong) before 30 % of their
+    messages and end with a close frame (valid / reserved / unknown /
+    application codes, UTF-8 and invalid reasons, empty bodies).  Every reply
+    the clients received -- pong for ping, the reference's ping for pong
+    (util.go:54-56), util.HandleClose's close reply -- is compared byte for
+    byte with oracle/ws_oracle.on_message for the frame they sent, and every
+    close is followed by the server's ShutdownWrite (the client sees EOF)."""
+    from oracle import ws_oracle as wo
+    tr = tmp_path / "transcript.txt"
+    d = _run("gev_amd/ws_loopback", conns=100, seconds=1.5, loops=8, threads=4,
+             extra=("--mode", "wsserver", "--ctrl", "0.3", "--close-end", "1", "--transcript", str(tr)))
+    assert d["closes_answered"] == 100
+    pairs = [ln.split() for ln in tr.read_text().splitlines() if ln.strip()]
+    assert len(pairs) == d["transcript_pairs"] and len(pairs) >= 100 + 50
+    kinds = set()
+    for sent_hex, reply_hex in pairs:
+        sent = bytes.fromhex(sent_hex)
+        fr = wo.decode_stream(sent).frames
+        assert len(fr) == 1
+        want, shut = wo.on_message(fr[0].header, fr[0].payload, wo.HANDLER_ECHO_TEXT)
+        assert bytes.fromhex(reply_hex) == want, (fr[0].header, fr[0].payload)
+        assert shut == (fr[0].header.opcode == wo.OP_CLOSE)
+        kinds.add(fr[0].header.opcode)
+    assert kinds == {wo.OP_PING, wo.OP_PONG, wo.OP_CLOSE}

@@ -148,6 +148,59 @@ def test_batch_begin_end_with_ring_writes_in_flight(engine, zero_copy_max):
     assert conns[1].pending() == len(wo.decode_stream(first[1]).frames)
 
 
+@pytest.mark.parametrize("zero_copy_max", [0, 1 << 30])
+def test_pass_in_flight_then_decode_host_and_batch(engine, zero_copy_max):
+    """gevws_decode_host_batch and gevws_protocol_unpacket_batch
+    share the staging buffers with a pass begun by _begin; both finish that
+    pass (its frames queued on its connections) before they stage their own,
+    so begin -> decode_host -> end and begin -> unpacket_batch deliver every
+    frame to the right connection."""
+    rng = np.random.default_rng(29)
+    proto = gev_amd.Protocol(engine)
+    proto.set_zero_copy_max(zero_copy_max)
+
+    def stream(k):
+        return b"".join(wo.encode_frame(bytes(rng.integers(0, 256, int(rng.integers(0, 2000)), dtype=np.uint8)),
+                                        2, True, 0, True, bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+                        for _ in range(k))
+    first = [stream(int(rng.integers(1, 6))) for _ in range(24)]
+    conns = [gev_amd.Connection() for _ in first]
+    rings = [gev_amd.RingBuffer(64) for _ in first]
+    for r, s in zip(rings, first):
+        r.write(s)
+    assert proto.unpacket_batch_begin(conns, rings) == len(conns)
+    # a host decode in between: its own output is the oracle's ...
+    other = [stream(3) + b"\x82\xfe", stream(1)]
+    frames, payload, cout, summ = proto.decode_host([(s, b"") for s in other])
+    want = [wo.decode_stream(s) for s in other]
+    assert int(summ.frames) == sum(len(w.frames) for w in want)
+    for j, w in enumerate(want):
+        assert int(cout[j]["nframes"]) == len(w.frames)
+        for k, fr in enumerate(w.frames):
+            rec = frames[int(cout[j]["first_frame"]) + k]
+            off = int(rec["payload_off"])
+            assert bytes(payload[off:off + fr.header.length]) == fr.payload
+    # ... and the pass in flight was delivered to its own connections
+    assert proto.unpacket_batch_end() == 0
+    for c, s in zip(conns, first):
+        assert c.pending() == len(wo.decode_stream(s).frames)
+    for c, r, s in zip(conns, rings, first):
+        for fr in wo.decode_stream(s).frames:
+            h, data = proto.unpacket(c, r)
+            assert h is not None and data == fr.payload
+        assert proto.unpacket(c, r) == (None, None)
+    # begin -> unpacket_batch: the batch call ends the pass first instead of failing
+    second = [stream(2) for _ in first]
+    for r, s in zip(rings, second):
+        r.write(s)
+    assert proto.unpacket_batch_begin(conns[:12], rings[:12]) == 12
+    proto.unpacket_batch(conns, rings)  # the first 12 hold frames now: the other 12 are decoded
+    for c, r, s in zip(conns, rings, second):
+        got = [proto.unpacket(c, r)[1] for _ in wo.decode_stream(s).frames]
+        assert got == [fr.payload for fr in wo.decode_stream(s).frames]
+        assert proto.unpacket(c, r) == (None, None)
+
+
 def test_zero_copy_capacity_retry(engine):
     """A zero-copy pass sizes its host outputs from an estimate (~1 frame per
     48 input bytes); a run of empty frames (6 bytes each) exceeds it, the pass
@@ -383,3 +436,86 @@ def test_duplicate_connection_in_one_batch(engine):
         assert d == bytes([i]) * (50 + i)
     assert proto.unpacket(c, r) == (None, None) and r.length() == 3
     assert proto.stats()["device_passes"] == 1
+
+
+def _control_mix(rng, n):
+    """Client frames of the wsserver_test.go shape (masked text, 1-3072 random
+    bytes) with masked control frames between them: pings and pongs (0-125
+    bytes), and closes with valid, reserved, unknown and application codes,
+    UTF-8 and non-UTF-8 reasons, and empty bodies (util.go:27-85)."""
+    out = []
+    codes = [1000, 1001, 1002, 1003, 1005, 1006, 1007, 1011, 1015, 1016, 2999, 3000, 4999, 999, 5000]
+    for _ in range(n):
+        r = rng.random()
+        key = bytes(rng.integers(0, 256, 4, dtype=np.uint8))
+        if r < 0.55:
+            p = bytes(rng.integers(0, 256, int(rng.integers(1, 3073)), dtype=np.uint8))
+            out.append(wo.encode_frame(p, wo.OP_TEXT, True, 0, True, key))
+        elif r < 0.75:
+            p = bytes(rng.integers(0, 256, int(rng.integers(0, 126)), dtype=np.uint8))
+            out.append(wo.encode_frame(p, wo.OP_PING, True, 0, True, key))
+        elif r < 0.85:
+            p = bytes(rng.integers(0, 256, int(rng.integers(0, 126)), dtype=np.uint8))
+            out.append(wo.encode_frame(p, wo.OP_PONG, True, 0, True, key))
+        else:
+            k = rng.random()
+            if k < 0.15:
+                body = b""
+            else:
+                reason = "bye ü".encode() if k < 0.6 else bytes([0xC3, 0x28, 0x41])
+                body = int(rng.choice(codes)).to_bytes(2, "big") + reason[: int(rng.integers(0, 6))]
+            out.append(wo.encode_frame(body, wo.OP_CLOSE, True, 0, True, key))
+    return out
+
+
+@pytest.mark.parametrize("policy", [wo.HANDLER_ECHO_TEXT, wo.HANDLER_ECHO_BINARY, wo.HANDLER_NONE])
+@pytest.mark.parametrize("zero_copy_max", [0, 1 << 30])
+def test_device_handler_replies_match_oracle(engine, policy, zero_copy_max):
+    """gevws_protocol_set_handler: every pass runs HandlerWrap.OnMessage
+    (wrap.go:38-90) on the device -- close -> HandleClose reply + ShutdownWrite,
+    ping -> pong, pong -> ping, data -> the policy's echo -- and each frame's
+    reply (gevws_protocol_reply) equals oracle/ws_oracle.on_message's, byte for
+    byte, over many connections fed in read(2)-sized chunks."""
+    rng = np.random.default_rng(31 + policy)
+    proto = gev_amd.Protocol(engine)
+    proto.set_zero_copy_max(zero_copy_max)
+    proto.set_handler(policy)
+    streams = [b"".join(_control_mix(rng, int(rng.integers(1, 30)))) for _ in range(64)]
+    conns = [gev_amd.Connection() for _ in streams]
+    rings = [gev_amd.RingBuffer(4096) for _ in streams]
+    pos = [0] * len(streams)
+    got = [[] for _ in streams]
+    while any(p < len(s) for p, s in zip(pos, streams)):
+        for i, s in enumerate(streams):
+            k = int(rng.integers(1, 9000))
+            rings[i].write(s[pos[i]:pos[i] + k])
+            pos[i] = min(len(s), pos[i] + k)
+        proto.unpacket_batch(conns, rings)
+        for i in range(len(streams)):
+            h, data = proto.unpacket(conns[i], rings[i])
+            while h is not None:
+                got[i].append((h.opcode, data, proto.reply(conns[i])))
+                h, data = proto.unpacket(conns[i], rings[i])
+    n = 0
+    for s, g in zip(streams, got):
+        want = wo.decode_stream(s).frames
+        assert len(g) == len(want)
+        for (op, data, (rep, shut)), fr in zip(g, want):
+            assert op == fr.header.opcode and data == fr.payload
+            wrep, wshut = wo.on_message(fr.header, fr.payload, policy)
+            assert rep == wrep and shut == wshut, (fr.header, fr.payload[:16], rep, wrep)
+            n += 1
+    assert n > 500
+    assert proto.stats()["handler_passes"] > 0
+
+
+def test_device_handler_off_by_default(engine):
+    proto = gev_amd.Protocol(engine)
+    c, r = gev_amd.Connection(), gev_amd.RingBuffer(4096)
+    r.write(wo.encode_frame(b"ping", wo.OP_PING, True, 0, True, b"\x01\x02\x03\x04"))
+    h, data = proto.unpacket(c, r)
+    assert h is not None and data == b"ping"
+    with pytest.raises(RuntimeError):
+        proto.reply(c)
+    with pytest.raises(ValueError):
+        proto.set_handler(7)

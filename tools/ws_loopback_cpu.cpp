@@ -36,6 +36,10 @@ struct CpuDecoder {
   static constexpr bool kPipelined = false;  // nothing to overlap: the decode runs in unpacket
   int64_t begin(wslb::ServerConn* const*, uint32_t) { return 0; }
   int64_t end() { return 0; }
+  // no device handler: the wsserver mode's text echo is framed on the host
+  static constexpr bool kHandler = false;
+  void set_handler(int) {}
+  int reply(wslb::ServerConn*, const uint8_t**, uint64_t*, int*) { return GEVWS_ERR_INVALID; }
 
   int unpacket(wslb::ServerConn* s, gevws_header* h, const uint8_t** data, uint64_t* len) {
     *data = nullptr;
