@@ -646,6 +646,48 @@ class Upgrader:
         return data, info, err
 
 
+class Comm:
+    """gevws_comm: an RCCL communicator over several GPUs of ONE process (a gev
+    server whose event loops are placed on the node's devices round-robin) and
+    the decode path's one collective, the all-reduce(sum) of every device's
+    decoded {frames, payload bytes, errors}."""
+
+    def __init__(self, devices: Sequence[int]):
+        arr = (ctypes.c_int * len(devices))(*devices)
+        self._p = lib.gevws_comm_create(arr, len(devices))
+        if not self._p:
+            raise RuntimeError(f"gevws_comm_create({list(devices)}) failed (RCCL missing or device not visible)")
+        self.devices = list(devices)
+
+    def __del__(self, _free=lib.gevws_comm_destroy):
+        if getattr(self, "_p", None):
+            _free(self._p)
+            self._p = None
+
+    def size(self) -> int:
+        return int(lib.gevws_comm_size(self._p))
+
+    def allreduce_counts(self, engines: Sequence["Engine"], batches: Sequence["Batch"]) -> Tuple[int, int, int]:
+        """gevws_counts_allreduce over each device's last decode summary; every
+        device's batch gets the totals in `counts` (int64[3] on its device);
+        returns (frames, payload_len, errors) summed over the devices."""
+        import torch
+        n = len(self.devices)
+        if len(engines) != n or len(batches) != n:
+            raise ValueError("one engine and one batch per device of the communicator")
+        counts = [torch.zeros(3, dtype=torch.int64, device=torch.device("cuda", e.device)) for e in engines]
+        ctxs = (ctypes.c_void_p * n)(*[e._ctx for e in engines])
+        sums = (ctypes.c_void_p * n)(*[b.summary.data_ptr() for b in batches])
+        cnts = (ctypes.c_void_p * n)(*[c.data_ptr() for c in counts])
+        tot = (ctypes.c_int64 * 3)()
+        st = lib.gevws_counts_allreduce(self._p, ctxs, sums, cnts, tot)
+        if st != OK:
+            raise RuntimeError(f"gevws_counts_allreduce: {status_string(st)}")
+        for b, c in zip(batches, counts):
+            b.counts = c
+        return int(tot[0]), int(tot[1]), int(tot[2])
+
+
 class Protocol:
     """websocket.Protocol (plugins/websocket/protocol.go:16-69) over the device engine."""
 
@@ -798,7 +840,7 @@ def handler_protocol(protocol: Protocol, c: Connection, buffer: RingBuffer,
     return replies
 
 
-__all__ = ["Engine", "Batch", "RingBuffer", "Connection", "Protocol", "Header", "handler_protocol",
+__all__ = ["Engine", "Batch", "Comm", "RingBuffer", "Connection", "Protocol", "Header", "handler_protocol",
            "Upgrader", "RejectError", "HandshakeError", "HandshakeInfo", "accept_key", "HANDSHAKE", "ERR_HANDSHAKE",
            "status_string", "device_count", "lib", "FRAME_DTYPE", "CONN_OUT_DTYPE", "SUMMARY_DTYPE",
            "SYNTH_DTYPE", "OUT_FRAME_DTYPE", "OK", "NEED_MORE", "ERR_LEN_MSB", "ERR_CAPACITY", "ERR_INVALID", "ERR_DEVICE",

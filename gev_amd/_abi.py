@@ -237,6 +237,12 @@ SIGNATURES = {
     "gevws_protocol_get_stats": (None, [P, ctypes.POINTER(ProtocolStats)]),
     "gevws_protocol_set_zero_copy_max": (None, [P, ctypes.c_uint64]),
     "gevws_protocol_set_handler": (ctypes.c_int, [P, ctypes.c_int]),
+    "gevws_comm_create": (P, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "gevws_comm_destroy": (None, [P]),
+    "gevws_comm_size": (ctypes.c_int, [P]),
+    "gevws_counts_allreduce_async": (ctypes.c_int, [P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P)]),
+    "gevws_counts_allreduce": (ctypes.c_int, [P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P),
+                                              ctypes.POINTER(ctypes.c_int64)]),
     "gevws_protocol_reply": (ctypes.c_int, [P, P, ctypes.POINTER(U8P), ctypes.POINTER(ctypes.c_uint64),
                                             ctypes.POINTER(ctypes.c_int)]),
     "gevws_decode_host_batch": (ctypes.c_int64, [P, P, ctypes.c_uint32, P, ctypes.c_uint64, P, ctypes.c_uint64,

@@ -311,6 +311,10 @@ __device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uin
 constexpr uint64_t kGroupedWalkChainsPerCU = 128;  // k_walk_count GRP from n_conns >= this x CUs
 constexpr uint32_t kEntryGranMinShift = 6;        // 64-byte granularity when the table fits
 constexpr uint64_t kEntryBudget = 1ull << 29;     // entries (8 GiB of scratch) at most
+// slot runs start on 16-entry (256-byte) boundaries: the writer wave of the
+// LDS-ring walk stores whole 256-byte groups (k_walk_count ST 2)
+constexpr uint32_t kSlotShift = 4;
+constexpr uint64_t kSlotAlign = 1ull << kSlotShift;
 struct WalkEntry {
   uint32_t pos;   // header offset in the connection stream
   uint32_t mask;
@@ -322,8 +326,8 @@ static_assert(sizeof(WalkEntry) == 16, "one dwordx4 per entry");
 __device__ __forceinline__ bool entry_slots_of(const gevws_conn_in& ci, uint32_t c, uint64_t n_entries,
                                               uint32_t gshift, uint64_t& base, uint64_t& cap) {
   if (n_entries == 0 || ci.len >= (1ull << 32)) return false;
-  base = 4 * ((ci.off >> (gshift + 2)) + (uint64_t)c);
-  cap = 4 * ((ci.len >> (gshift + 2)) + 1);
+  base = kSlotAlign * ((ci.off >> (gshift + kSlotShift)) + (uint64_t)c);
+  cap = kSlotAlign * ((ci.len >> (gshift + kSlotShift)) + 1);
   return base + cap <= n_entries;
 }
 
@@ -407,11 +411,36 @@ __device__ __forceinline__ WalkRes walk_res_fresh(uint64_t err = 0, int32_t st =
   return R;
 }
 
-template <int D, bool GRP, bool NTH = false, int PF = 0>
+// ST: where entries go.  0 = global memory from the walking lane (GRP: in
+// 64-byte groups of four); 1 = nowhere (measurement); 2 = this lane's LDS ring
+// (WalkRing), drained to global memory by the workgroup's writer wave
+// (k_walk_count ST 2): the walker then issues no global stores at all, so
+// waiting for its header load (vmcnt counts loads and stores in order) never
+// waits for an entry store.
+constexpr uint32_t kRingDone = 0x80000000u;   // head flag: the chain is finished
+// entries per lane's LDS ring for a writer group of WGS entries
+template <int WGS>
+constexpr uint32_t ring_size() { return WGS >= 16 ? 32u : 16u; }
+struct WalkRing {
+  WalkEntry* e;    // ring_size entries (LDS)
+  uint32_t mask;   // ring_size - 1
+  uint32_t* head;  // entries published (whole groups of 4; | kRingDone with the count at the end)
+  uint32_t* tail;  // entries the writer has taken
+};
+__device__ __forceinline__ uint32_t lds_ld(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int D, bool GRP, bool NTH = false, int PF = 0, int UNR = 2, int ST = 0>
 __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const uint64_t len, bool rec,
                                            const uint64_t ebase, const uint64_t ecap,
                                            WalkEntry* __restrict__ entries, WalkEntry* __restrict__ sink,
-                                           WalkRes& R, const uint64_t budget = ~0ull) {
+                                           WalkRes& R, const uint64_t budget = ~0ull,
+                                           WalkRing ring = WalkRing{nullptr, 0, nullptr, nullptr}) {
+    constexpr bool NST = ST != 0;  // no global entry stores from this lane
     // (GRP keeps the group's earlier entries in registers: a fresh chain only)
     uint64_t nf = R.nf, pb = R.pb, pl = R.pl, same = R.same, lastf = R.lastf, firstf = R.firstf, err = R.err;
     int32_t st = R.st;
@@ -426,7 +455,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
     // table), so the compiler waits vmcnt(1), not vmcnt(0).
     uint64_t lo, hi;
     load_window<NTH>(s + pos, lo, hi);
-    *sink = WalkEntry{0, 0, 0, 0};
+    if constexpr (!NST) *sink = WalkEntry{0, 0, 0, 0};
     uint64_t prev_fsz = 0;  // speculation (D > 0): size of the last frame and the run of equal sizes
     uint32_t run = 0;
     WalkEntry g0 = {0, 0, 0, 0}, g1 = g0, g2 = g0;  // GRP: the last three entries, oldest first
@@ -437,7 +466,17 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
       e.mask = key;
       e.len = (uint32_t)L;
       e.meta = meta;
-      if constexpr (GRP) {
+      if constexpr (ST == 1) {  // measurement: no stores at all (the walk's pure chain cost)
+        rec = false;
+      } else if constexpr (ST == 2) {
+        // room for this group in the ring? (the writer is normally far ahead:
+        // it copies a group in a few hundred cycles, a step takes ~1 us)
+        if ((nf & 3) == 0)
+          while ((uint32_t)nf + 4 - lds_ld(ring.tail) > ring.mask + 1) __builtin_amdgcn_s_sleep(1);
+        ring.e[nf & ring.mask] = e;
+        __asm__ volatile("" ::: "memory");  // the entry before the head that publishes it (DS ops run in order)
+        if ((nf & 3) == 3) lds_st(ring.head, (uint32_t)nf + 1);
+      } else if constexpr (GRP) {
         if (rec && (nf & 3) == 3) {
           WalkEntry* g = entries + ebase + (nf - 3);  // 64-byte aligned
           g[0] = g0;
@@ -462,10 +501,12 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
       lastf = f;
     };
     uint32_t pfv[PF > 0 ? PF : 1] = {};
-    for (;;) {
+    // One chain step on the window (clo, chi) at pos; the next header's window
+    // is loaded into (nlo, nhi).  false: the chain ends here.
+    auto step = [&](const uint64_t clo, const uint64_t chi, uint64_t& nlo, uint64_t& nhi) -> bool {
       if (nf >= budget) {  // the budgeted walk stops here; k_walk_resume goes on from pos
         more = true;
-        break;
+        return false;
       }
       if constexpr (PF > 0) {  // keep the touches' results alive (free: they landed before the header)
 #pragma unroll
@@ -475,16 +516,15 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
       // only the next frame's position is computed before its header load is
       // issued -- at min(next, len), always inside the stream + GEVWS_IN_PAD
       // -- and the checks run while that load is in flight.
-      const uint32_t b1 = (uint32_t)(lo >> 8) & 0xffu;
+      const uint32_t b1 = (uint32_t)(clo >> 8) & 0xffu;
       const uint32_t masked = b1 >> 7, len7 = b1 & 0x7fu;
       const bool e16 = len7 == 126, e64 = len7 == 127;
       const uint32_t hlen = 2 + (e64 ? 8u : (e16 ? 2u : 0u)) + 4 * masked;
-      const uint64_t L64 = __builtin_bswap64((lo >> 16) | (hi << 48));
-      const uint64_t L16 = (((lo >> 16) & 0xff) << 8) | ((lo >> 24) & 0xff);
+      const uint64_t L64 = __builtin_bswap64((clo >> 16) | (chi << 48));
+      const uint64_t L16 = (((clo >> 16) & 0xff) << 8) | ((clo >> 24) & 0xff);
       const uint64_t L = e64 ? L64 : (e16 ? L16 : (uint64_t)len7);
       const uint64_t fsz = hlen + L;
       const uint64_t next = pos + fsz;
-      const uint64_t lo0 = lo, hi0 = hi;
       if constexpr (PF > 0) {
         const uint64_t nx = next <= len ? next : len;
 #pragma unroll
@@ -494,17 +534,17 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
         }
         __asm__ volatile("" ::: "memory");  // touches first, then the header load
       }
-      load_window<NTH>(s + (next <= len ? next : len), lo, hi);  // (a wrapped next is <= len or clamped)
+      load_window<NTH>(s + (next <= len ? next : len), nlo, nhi);  // (a wrapped next is <= len or clamped)
       const uint64_t avail = len - pos;
       const bool have_hdr = avail >= 6 && avail >= hlen;   // read.go:20-23, U1
       const bool msb = e64 && (L64 >> 63);                  // read.go:71-73
       if (!have_hdr || msb || avail - hlen < L) {           // protocol.go:47 gate
         if (have_hdr && msb) { st = GEVWS_ERR_LEN_MSB; err += 1; }
-        break;
+        return false;
       }
-      const uint32_t key = (e64 ? (uint32_t)(hi0 >> 16) : (e16 ? (uint32_t)(lo0 >> 32) : (uint32_t)(lo0 >> 16))) &
+      const uint32_t key = (e64 ? (uint32_t)(chi >> 16) : (e16 ? (uint32_t)(clo >> 32) : (uint32_t)(clo >> 16))) &
                            (0u - masked);
-      const uint32_t meta = ((uint32_t)lo0 & 0xffu) | (masked << 8) | (hlen << 16);
+      const uint32_t meta = ((uint32_t)clo & 0xffu) | (masked << 8) | (hlen << 16);
       put_entry(pos, key, L, meta);
       pos = next;
       if constexpr (D > 0) {
@@ -512,7 +552,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
         prev_fsz = fsz;
         if (run >= 3) {
           // third equal frame in a row: take the following frames in batches
-          // of D windows at stride fsz while their size stays fsz; (lo, hi),
+          // of D windows at stride fsz while their size stays fsz; (nlo, nhi),
           // in flight, is the window at pos
           bool fail = false;
           for (;;) {
@@ -528,8 +568,8 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
               qn += in ? 1u : 0u;
               load_window<NTH>(s + (in ? q : len), qlo[j], qhi[j]);
             }
-            qlo[0] = lo;
-            qhi[0] = hi;
+            qlo[0] = nlo;
+            qhi[0] = nhi;
             bool stop = false;
 #pragma unroll
             for (int j = 0; j < D; ++j) {
@@ -552,15 +592,36 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
               }
             }
             if (fail) break;
-            load_window<NTH>(s + pos, lo, hi);  // the next batch's first window, or the chain's next header
+            load_window<NTH>(s + pos, nlo, nhi);  // the next batch's first window, or the chain's next header
             if (stop || qn < (uint32_t)D || pos + fsz > len) break;
           }
-          if (fail) break;
-          *sink = WalkEntry{0, 0, 0, 0};  // same [load, store] in flight at the loop head as the plain path
+          if (fail) return false;
+          if constexpr (!NST) *sink = WalkEntry{0, 0, 0, 0};  // same [load, store] in flight as the plain path
         }
       }
+      return true;
+    };
+    if constexpr (UNR == 2) {
+      // two window buffers in turn: the window a step loads is the next
+      // step's current one in the same registers.  (With one buffer the
+      // compiler copies the loaded window into the loop-carried registers at
+      // the back edge -- a copy that waits for the load and, vmcnt being in
+      // order, for every entry store after it: each step then paid the load
+      // AND the stores' latency instead of overlapping them with the checks.)
+      uint64_t lo2 = 0, hi2 = 0;
+      for (;;) {
+        if (!step(lo, hi, lo2, hi2)) break;
+        if (!step(lo2, hi2, lo, hi)) break;
+      }
+    } else {
+      for (;;) {
+        uint64_t nlo, nhi;
+        if (!step(lo, hi, nlo, nhi)) break;
+        lo = nlo;
+        hi = nhi;
+      }
     }
-    if (GRP && rec) {  // the last nf % 4 entries
+    if (GRP && !NST && rec) {  // the last nf % 4 entries
       const uint32_t r = (uint32_t)(nf & 3);
       WalkEntry* g = entries + ebase + (nf - r);
       if (r == 3) {
@@ -585,6 +646,59 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
     R.st = st;
     R.rec = rec;
     R.more = more;
+    if constexpr (ST == 2) {  // the rest of the entries, and the end of the chain
+      __asm__ volatile("" ::: "memory");
+      lds_st(ring.head, (uint32_t)nf | kRingDone);
+    }
+}
+
+// The writer wave of k_walk_count ST 2: lane j copies walker lane j's ring to
+// its entry slots (ebase ~0: none) in groups of WGS entries (WGS x 16 bytes,
+// aligned: slot runs start on kSlotAlign entries) as they are published, the
+// last partial group when the chain is done; every slot below ecap only.
+// Whole groups: a 64-byte group is half an L2 line, and scattered half-line
+// writes among the walk's random line reads cost far more than their bytes
+// (C4: 0.7 GB of 64-byte entry groups made the walk 1.50 ms, 1.00 without).
+// NTW: the group stores non-temporal.
+template <int WGS, bool NTW = false>
+__device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries, WalkRing ring, uint64_t ebase,
+                                                 uint64_t ecap) {
+  static_assert(WGS == 4 || WGS == 8 || WGS == 16, "group of 4, 8 or 16 entries");
+  uint32_t t = 0;
+  bool fin = false;
+  for (;;) {
+    if (!fin) {
+      const uint32_t hv = lds_ld(ring.head);
+      __asm__ volatile("" ::: "memory");  // the entries after the head that published them
+      const uint32_t h = hv & ~kRingDone;
+      while (h - t >= (uint32_t)WGS) {
+        WalkEntry g[WGS];
+#pragma unroll
+        for (int k = 0; k < WGS; ++k) g[k] = ring.e[(t + k) & ring.mask];
+        if (ebase != ~0ull && t + WGS <= ecap) {
+          WalkEntry* d = entries + ebase + t;  // WGS x 16-byte aligned
+#pragma unroll
+          for (int k = 0; k < WGS; ++k) {
+            if constexpr (NTW)
+              __builtin_nontemporal_store(u32x4{g[k].pos, g[k].mask, g[k].len, g[k].meta},
+                                          reinterpret_cast<u32x4*>(d + k));
+            else
+              d[k] = g[k];
+          }
+        }
+        t += WGS;
+        __asm__ volatile("" ::: "memory");
+        lds_st(ring.tail, t);
+      }
+      if (hv & kRingDone) {
+        for (; t < h; ++t)
+          if (ebase != ~0ull && t < ecap) entries[ebase + t] = ring.e[t & ring.mask];
+        fin = true;
+      }
+    }
+    if (__all(fin)) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
 }
 
 // Budgeted walk (BUD, with k_walk_resume): a C4-sized batch (65 536 chains,
@@ -604,30 +718,37 @@ struct WalkResume {
 };
 static_assert(sizeof(WalkResume) == 64, "one resume record per 64 bytes");
 
-template <int D, bool GRP, bool NTH = false, int PF = 0, bool BUD = false>
-__global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __restrict__ in,
-                                                            const gevws_conn_in* __restrict__ conns,
-                                                            uint32_t n, gevws_conn_out* __restrict__ cout,
-                                                            uint64_t* __restrict__ blk,
-                                                            WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                            uint32_t gshift, uint32_t cpb, uint64_t in_bytes,
-                                                            uint32_t* __restrict__ done, uint64_t max_frames,
-                                                            uint64_t payload_cap, gevws_summary* __restrict__ sum,
-                                                            uint64_t budget = ~0ull, uint32_t ks = 1,
-                                                            gevws_conn_in* __restrict__ segs = nullptr,
-                                                            gevws_conn_out* __restrict__ sout = nullptr,
-                                                            uint8_t* __restrict__ srec = nullptr,
-                                                            WalkResume* __restrict__ rlist = nullptr,
-                                                            uint32_t* __restrict__ rcount = nullptr) {
-  const uint32_t c = blockIdx.x * cpb + threadIdx.x;
+template <int D, bool GRP, bool NTH = false, int PF = 0, bool BUD = false, int UNR = 2, int ST = 0, int WGS = 16,
+          int WM = 0>
+__global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_walk_count(
+    const uint8_t* __restrict__ in, const gevws_conn_in* __restrict__ conns, uint32_t n,
+    gevws_conn_out* __restrict__ cout, uint64_t* __restrict__ blk, WalkEntry* __restrict__ entries, uint64_t n_entries,
+    uint32_t gshift, uint32_t cpb, uint64_t in_bytes, uint32_t* __restrict__ done, uint64_t max_frames,
+    uint64_t payload_cap, gevws_summary* __restrict__ sum, uint64_t budget = ~0ull, uint32_t ks = 1,
+    gevws_conn_in* __restrict__ segs = nullptr, gevws_conn_out* __restrict__ sout = nullptr,
+    uint8_t* __restrict__ srec = nullptr, WalkResume* __restrict__ rlist = nullptr,
+    uint32_t* __restrict__ rcount = nullptr) {
+  // ST 2: wave 0 walks (lane = connection), wave 1 writes its entries
+  constexpr uint32_t kRing = ring_size<WGS>();
+  __shared__ WalkEntry s_ring[ST == 2 ? kCountBlock * kRing : 1];
+  __shared__ uint32_t s_head[ST == 2 ? kCountBlock : 1], s_tail[ST == 2 ? kCountBlock : 1];
+  __shared__ uint64_t s_ebase[ST == 2 ? kCountBlock : 1], s_ecap[ST == 2 ? kCountBlock : 1];
+  const uint32_t lane = threadIdx.x & 63;
+  const bool walker = ST != 2 || threadIdx.x < 64;
+  const uint32_t c = blockIdx.x * cpb + lane;
+  const bool active = walker && lane < cpb && c < n;
   uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0;
   bool more = false;
   WalkRes R = walk_res_fresh();
-  if (threadIdx.x < cpb && c < n) {
-    gevws_conn_in ci = conns[c];
+  gevws_conn_in ci = {0, 0};
+  int32_t st = GEVWS_OK;
+  const uint64_t v0 = BUD ? (uint64_t)c * ks : c;  // entry slot run / sink of the connection's first row
+  uint64_t ebase = 0, ecap = 0;
+  bool rec0 = false;
+  if (active) {
+    ci = conns[c];
     // the order flag rides in the high half of the error count (k_scan_blocks SPLIT)
     if (out_of_order(conns, c, ci)) err = 1ull << 32;
-    int32_t st = GEVWS_OK;
     if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
       // a stream outside the input arena: nothing is read, the connection
       // reports GEVWS_ERR_INVALID (and counts as an error), the rest decode
@@ -636,12 +757,26 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
       st = GEVWS_ERR_INVALID;
       err += 1;
     }
-    const uint64_t v0 = BUD ? (uint64_t)c * ks : c;  // entry slot run / sink of the connection's first row
-    uint64_t ebase = 0, ecap = 0;
-    const bool rec0 = entry_slots_of(ci, (uint32_t)v0, n_entries, gshift, ebase, ecap);
+    rec0 = entry_slots_of(ci, (uint32_t)v0, n_entries, gshift, ebase, ecap);
+  }
+  const WalkRing ring = {s_ring + lane * kRing, kRing - 1, s_head + lane, s_tail + lane};
+  if constexpr (ST == 2) {
+    if (walker) {
+      s_head[lane] = active ? 0u : kRingDone;
+      s_tail[lane] = 0;
+      s_ebase[lane] = rec0 ? ebase : ~0ull;
+      s_ecap[lane] = ecap;
+    }
+    __syncthreads();
+    // WM (measurement): 1 = the writer drains the ring but stores nothing (the
+    // record pass re-walks); 2 = non-temporal group stores
+    if (!walker) walk_ring_writer<WGS, WM == 2>(entries, ring, WM == 1 ? ~0ull : s_ebase[lane], s_ecap[lane]);
+  }
+  if (active) {
     R = walk_res_fresh(err, st);
-    walk_chain<D, GRP, NTH, PF>(in + ci.off, ci.len, rec0, ebase, ecap, entries, entries + n_entries + v0, R,
-                                BUD ? budget : ~0ull);
+    walk_chain<D, GRP, NTH, PF, UNR, ST>(in + ci.off, ci.len, rec0 && WM != 1, ebase, ecap, entries,
+                                         entries + n_entries + v0, R,
+                                         BUD ? budget : ~0ull, ring);
     more = BUD && R.more;
     if (!more) {
       nf = R.nf;
@@ -681,7 +816,6 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_count(const uint8_t* __res
     // append the unfinished connections to the resume list (one atomic per wave)
     const uint64_t m = __ballot(more);
     if (m) {
-      const uint32_t lane = threadIdx.x & 63;
       uint32_t base = 0;
       if (lane == 0) base = atomicAdd(rcount, (uint32_t)__popcll(m));
       base = (uint32_t)__shfl((int)base, 0, 64);
@@ -3718,7 +3852,10 @@ struct gevws_ctx {
   int split_mode = 0;       // measurement: 1 = guesses made then dropped, 2 = no guesses, 3 = the
                             // default walk keeps its speculation (D = 8) whatever the history
   uint32_t split_lanes = 0;  // walk variant 0: lanes per connection (k_walk_split); 0 = auto, 1 = off
-  int64_t walk_budget = 0;   // frames per lane of the budgeted walk: 0 = auto, -1 = never, > 0 = always
+  // frames per lane of the budgeted walk: 0 = auto, -1 = never (the default:
+  // measured slower than the plain walk on C4 and its shares,
+  // profiles/r03_budget_ab.jsonl), > 0 = always
+  int64_t walk_budget = -1;
   uint32_t resume_lanes = 0;  // lanes per resumed connection (k_walk_resume): 0 = kResumeLanes
   uint32_t budget_frac16 = kBudgetFrac16;  // auto budget: this many 16ths of the previous mean chain
   uint64_t last_budget = 0;  // budget of the last multi-kernel decode's walk (0 = not budgeted)
@@ -3835,8 +3972,8 @@ constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVaria
 // GEVWS_TUNE_WALK_VARIANT values (0 = the default choice per batch).
 const char* const kWalkVariants[] = {
     "default: one wave per connection (k_walk_span, K = 1) up to GEVWS_TUNE_SPAN_CONNS_PER_CU connections per CU, "
-    "else one lane per connection with uniform-stream speculation (k_walk_count D = 8; 64-byte entry groups from "
-    "128 connections per CU)",
+    "else one lane per connection with uniform-stream speculation (k_walk_count D = 8; from 128 connections per CU "
+    "the entries go through an LDS ring to a writer wave, 256-byte groups)",
     "one lane per connection, plain chain walk (D = 0)",
     "one lane per connection, no entry table (the record pass re-walks every chain)",
     "one lane per connection, speculation, single entry stores",
@@ -3848,6 +3985,15 @@ const char* const kWalkVariants[] = {
     "one lane per connection, plain chain walk, each header load also touches the next two 128-byte lines",
     "one lane per connection, 128-byte LDS row per lane: every header inside it walked before the next load",
     "one lane per connection, 256-byte LDS row per lane: every header inside it walked before the next load",
+    "as 0 (speculating lane walk) with one window buffer (the round-2 loop: the back edge copies the loaded window)",
+    "as 1 (plain lane walk) with one window buffer (the round-2 loop)",
+    "measurement: plain lane walk storing nothing (no entries, no sink; the record pass re-walks every chain)",
+    "plain lane walk, entries through an LDS ring per lane drained to HBM by a writer wave in 256-byte groups",
+    "as 15 with uniform-stream speculation",
+    "as 15 with 64-byte groups",
+    "as 15 with 128-byte groups",
+    "measurement: as 15 with the writer storing nothing (the record pass re-walks every chain)",
+    "as 15 with non-temporal group stores",
 };
 constexpr int kNumWalkVariants = sizeof(kWalkVariants) / sizeof(kWalkVariants[0]);
 
@@ -4121,7 +4267,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
   uint32_t gshift = kEntryGranMinShift;
   while ((in_bytes >> gshift) > kEntryBudget) ++gshift;
-  const uint64_t n_entries = 4 * ((in_bytes >> (gshift + 2)) + n_v + 1);
+  const uint64_t n_entries = kSlotAlign * ((in_bytes >> (gshift + kSlotShift)) + n_v + 1);
   const size_t flag_bytes = ((size_t)n_conns + 255) & ~size_t(255);
   const size_t seg_bytes = rows > 1 ? ((n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out) + 1) + 1023) & ~size_t(255)) : 0;
   // the budgeted walk's resume list + its length
@@ -4214,7 +4360,27 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     // (many concurrent chains), not by chain latency (few)
     const bool many = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
     const bool grp = wv == 4 || ((wv == 0 || wv == 1 || wv == 5 || wv == 8 || wv == 9 || wv >= 10) && many);
-    if (wv == 10 || wv == 11) {
+    if (wv >= 15 && wv <= 20) {
+      (wv == 15   ? k_walk_count<0, false, false, 0, false, 2, 2, 16>
+       : wv == 16 ? k_walk_count<8, false, false, 0, false, 2, 2, 16>
+       : wv == 17 ? k_walk_count<0, false, false, 0, false, 2, 2, 4>
+       : wv == 18 ? k_walk_count<0, false, false, 0, false, 2, 2, 8>
+       : wv == 19 ? k_walk_count<0, false, false, 0, false, 2, 2, 16, 1>
+                  : k_walk_count<0, false, false, 0, false, 2, 2, 16, 2>)
+          <<<nblk, 2 * kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb,
+                                             in_bytes, done, max_frames, payload_cap, d_summary, ~0ull, 1u, nullptr,
+                                             nullptr, nullptr, nullptr, nullptr);
+    } else if (wv == 14) {
+      k_walk_count<0, false, false, 0, false, 2, 1><<<nblk, kCountBlock, 0, st>>>(
+          d_in, d_conns, n_conns, d_conn_out, blk, entries, 0, gshift, cpb, in_bytes, done, max_frames, payload_cap,
+          d_summary);
+    } else if (wv == 12 || wv == 13) {
+      auto k1 = wv == 12 ? (grp ? k_walk_count<8, true, false, 0, false, 1> : k_walk_count<8, false, false, 0, false, 1>)
+                         : (grp ? k_walk_count<0, true, false, 0, false, 1> : k_walk_count<0, false, false, 0, false, 1>);
+      k1<<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes,
+                                       done, max_frames, payload_cap, d_summary, ~0ull, 1u, nullptr, nullptr, nullptr,
+                                       nullptr, nullptr);
+    } else if (wv == 10 || wv == 11) {
       auto kb = wv == 10 ? (grp ? k_walk_buf<128, true> : k_walk_buf<128, false>)
                          : (grp ? k_walk_buf<256, true> : k_walk_buf<256, false>);
       kb<<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes,
@@ -4254,6 +4420,18 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
         k_walk_count<0, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
                                                              gshift, cpb, in_bytes, done, max_frames,
                                                             payload_cap, d_summary);
+    } else if (wv == 0 && grp) {
+      // many chains: the walk is bound by its line traffic, and entry stores
+      // from the walking lanes -- half-line groups scattered among the random
+      // header reads -- cost far more than their bytes (C4: 1.60 ms against
+      // 1.00 without entries); a writer wave per workgroup drains each lane's
+      // LDS ring in whole 256-byte groups instead (C4 1.41 ms, its 2-way
+      // share 0.94 -> 0.87, C1-shaped 0.042 -> 0.038;
+      // profiles/r03_walk_writer_grp_ab.jsonl)
+      (plain ? k_walk_count<0, false, false, 0, false, 2, 2, 16> : k_walk_count<8, false, false, 0, false, 2, 2, 16>)
+          <<<nblk, 2 * kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb,
+                                             in_bytes, done, max_frames, payload_cap, d_summary, ~0ull, 1u, nullptr,
+                                             nullptr, nullptr, nullptr, nullptr);
     } else if (grp && plain) {
       k_walk_count<0, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
                                                           gshift, cpb, in_bytes, done, max_frames, payload_cap,

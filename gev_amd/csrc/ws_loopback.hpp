@@ -49,7 +49,10 @@
 //
 //   [--conns 1000] [--msg 128] [--seconds 5] [--loops 1] [--client-threads 4]
 //   [--port 0] [--device 0] [--mode echo|wsserver] [--ctrl 0] [--close-end 0]
-//   [--transcript FILE] [--seed 1]
+//   [--transcript FILE] [--seed 1] [--devices 1]
+// --devices N places loop l on device (--device + l % N): the loops of one
+// server process spread over the node's GPUs round-robin, each with its own
+// context and protocol (a connection stays on its loop's GPU).
 // Prints one JSON line.
 #pragma once
 
@@ -656,7 +659,7 @@ inline void ws_client_thread(int port, int nconn, double t_end, std::atomic<uint
 
 template <class Decoder>
 int loopback_main(int argc, char** argv) {
-  int conns = 1000, loops = 1, cthreads = 4, port = 0, device = 0;
+  int conns = 1000, loops = 1, cthreads = 4, port = 0, device = 0, ndev = 1;
   size_t msg = 128;
   double seconds = 5.0;
   for (int i = 1; i + 1 < argc; i += 2) {
@@ -669,6 +672,7 @@ int loopback_main(int argc, char** argv) {
     else if (k == "--client-threads") cthreads = atoi(v);
     else if (k == "--port") port = atoi(v);
     else if (k == "--device") device = atoi(v);
+    else if (k == "--devices") ndev = atoi(v) > 0 ? atoi(v) : 1;
     else if (k == "--mode") g_cfg.mode = std::string(v) == "wsserver" ? kModeWsServer : kModeEcho;
     else if (k == "--ctrl") g_cfg.ctrl_prob = atof(v);
     else if (k == "--close-end") g_cfg.close_end = atoi(v) != 0;
@@ -693,7 +697,7 @@ int loopback_main(int argc, char** argv) {
   }
   std::atomic<int> ready{0};
   std::vector<std::thread> servers;
-  for (int l = 0; l < loops; ++l) servers.emplace_back(server_loop<Decoder>, port, device, &ready, l);
+  for (int l = 0; l < loops; ++l) servers.emplace_back(server_loop<Decoder>, port, device + l % ndev, &ready, l);
   while (ready.load() < loops) std::this_thread::sleep_for(std::chrono::milliseconds(5));
 
   std::atomic<uint64_t> total{0};
@@ -743,13 +747,14 @@ int loopback_main(int argc, char** argv) {
          "\"echoes_per_s\": %.1f, \"payload_MiBps_each_way\": %.2f, \"decode_passes_per_s\": %.1f, "
          "\"mean_conns_per_pass\": %.1f, \"decode_us_per_pass\": %.1f, \"decode_share_of_loop_time\": %.3f, "
          "\"client_checked_echoes\": %llu, \"mode\": \"%s\", \"control_frames\": %llu, "
-         "\"async_sends\": %llu, \"closes_answered\": %llu, \"transcript_pairs\": %zu, \"errors\": %llu}\n",
+         "\"async_sends\": %llu, \"closes_answered\": %llu, \"transcript_pairs\": %zu, \"devices\": %d, "
+         "\"errors\": %llu}\n",
          Decoder::path(), Decoder::name(), conns, upgraded.load(), wss ? (size_t)0 : msg, loops, cthreads, dt, mps,
          (double)(p1 - p0) / dt / 1048576.0, (double)(b1 - b0) / dt,
          b1 > b0 ? (double)(c1 - c0) / (double)(b1 - b0) : 0.0,
          b1 > b0 ? (double)(d1 - d0) / 1e3 / (double)(b1 - b0) : 0.0, (double)(d1 - d0) / 1e9 / (dt * loops),
          (unsigned long long)total.load(), wss ? "wsserver" : "echo", (unsigned long long)g_ctrl.load(),
-         (unsigned long long)g_sent_async.load(), (unsigned long long)g_closed.load(), g_transcript.size(),
+         (unsigned long long)g_sent_async.load(), (unsigned long long)g_closed.load(), g_transcript.size(), ndev,
          (unsigned long long)g_bad.load());
   return g_bad.load() == 0 && upgraded.load() == conns ? 0 : 1;
 }

@@ -186,8 +186,9 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * chain itself, over the rest of the stream).  0 = auto (after a decode on
  * this context whose connections averaged >= 256 frames of <= 4 KiB, when the
  * split walk is not chosen: GEVWS_TUNE_BUDGET_FRAC 16ths of that mean), -1 =
- * never, > 0 = this budget for every multi-kernel decode (instead of the
- * split walk's auto choice; GEVWS_TUNE_SPLIT_LANES >= 2 still splits). */
+ * never (the default: measured slower than the plain walk),
+ * > 0 = this budget for every multi-kernel decode (instead of the split walk's
+ * auto choice; GEVWS_TUNE_SPLIT_LANES >= 2 still splits). */
 #define GEVWS_TUNE_WALK_BUDGET 10
 #define GEVWS_TUNE_RESUME_LANES 11  /* 0 = default (8), else 2 / 4 / 8 / 16 */
 #define GEVWS_TUNE_BUDGET_FRAC 12   /* auto budget in 16ths of the previous mean chain (default 18) */
@@ -648,6 +649,30 @@ const uint8_t *gevws_protocol_packet(gevws_protocol *p, gevws_conn *c, const uin
                                      uint64_t n, uint64_t *out_len);
 
 #if defined(__GNUC__)
+/* ---------------------------------------------------------------- multi-GPU in one process
+ * A gev server drives all its event loops from one process (server.go:80-91):
+ * with NumLoops loops placed on the node's GPUs round-robin (loop l on device
+ * devices[l % n], one gevws_ctx per loop, load_balance.go:7-14 deals
+ * connections to loops), each device decodes only its own loops' connections
+ * and the one collective is the all-reduce(sum) of the decoded counts
+ *  over RCCL / xGMI -- payloads never cross GPUs.
+ * gevws_comm_create: ncclCommInitAll over `devices` (RCCL is loaded on first
+ * use; NULL when it is absent or a device is not visible). */
+typedef struct gevws_comm gevws_comm;
+gevws_comm *gevws_comm_create(const int *devices, int n);
+void gevws_comm_destroy(gevws_comm *comm);
+int gevws_comm_size(const gevws_comm *comm);
+/* For every device i of the communicator: d_counts[i] (int64[3], device
+ * memory on device i) = the sum over all devices of {frames, payload_len,
+ * errors} of their decode summaries d_summaries[i], enqueued on ctxs[i]'s
+ * stream after whatever it holds (one RCCL group, ncclAllReduce in place).
+ * ctxs[i] must be on the communicator's device i.  The synchronous form
+ * waits and also returns the totals in h_total. */
+int gevws_counts_allreduce_async(gevws_comm *comm, gevws_ctx *const *ctxs, const gevws_summary *const *d_summaries,
+                                 int64_t *const *d_counts);
+int gevws_counts_allreduce(gevws_comm *comm, gevws_ctx *const *ctxs, const gevws_summary *const *d_summaries,
+                           int64_t *const *d_counts, int64_t h_total[3]);
+
 #pragma GCC visibility pop
 #endif
 #ifdef __cplusplus

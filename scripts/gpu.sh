@@ -58,7 +58,7 @@ PY
       fi ;;
     prof)
       tag=$1; shift
-      timeout -k 10 $to rocprofv3 --kernel-trace --stats -d $OUT/prof_$tag -o $tag -- \
+      timeout -k 10 $to rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$tag -o $tag -- \
         python -u bench.py --no-cpu --copy-reps 0 "$@" > $log 2> $err; rc=$?
       [ $rc -eq 0 ] && tail -c 600 $log ;;
     pmc)
@@ -70,7 +70,7 @@ PY
       tail -c 1500 $log ;;
     pyprof)
       tag=$1; shift
-      timeout -k 10 $to rocprofv3 --kernel-trace --stats -d $OUT/prof_$tag -o $tag -- python -u "$@" > $log 2> $err
+      timeout -k 10 $to rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$tag -o $tag -- python -u "$@" > $log 2> $err
       rc=$?
       [ $rc -eq 0 ] && tail -c 600 $log ;;
     *)

@@ -110,3 +110,14 @@ def test_wsserver_control_frames_match_oracle(tmp_path):
         assert shut == (fr[0].header.opcode == wo.OP_CLOSE)
         kinds.add(fr[0].header.opcode)
     assert kinds == {wo.OP_PING, wo.OP_PONG, wo.OP_CLOSE}
+
+
+def test_wsserver_loops_placed_on_devices_round_robin():
+    """--devices N places loop l on device l % N (one context + protocol per
+    loop); on a one-GPU box N = the visible devices (1), the mapping still goes
+    through the flag."""
+    import gev_amd
+    n = max(1, gev_amd.device_count())
+    d = _run("gev_amd/ws_loopback", conns=64, seconds=1.0, loops=4, threads=2,
+             extra=("--mode", "wsserver", "--devices", str(n)))
+    assert d["devices"] == n and d["client_checked_echoes"] > 0

@@ -218,7 +218,7 @@ def test_budgeted_walk_matches_oracle(engine, split_cases, budget, lanes):
             # a connection is resumed when the budget stopped it (>= budget frames seen)
             assert engine.last_resumed >= int((nf > budget).sum()), name
     finally:
-        engine.set_tuning(_abi.TUNE_WALK_BUDGET, 0)
+        engine.set_tuning(_abi.TUNE_WALK_BUDGET, -1)
         engine.set_tuning(_abi.TUNE_RESUME_LANES, 0)
         engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
 
@@ -247,7 +247,7 @@ def test_budgeted_walk_streams_outside_the_arena_and_random(engine):
             assert got["frames"].tobytes() == want["frames"].tobytes()
             assert np.array_equal(got["payload"], want["payload"])
     finally:
-        engine.set_tuning(_abi.TUNE_WALK_BUDGET, 0)
+        engine.set_tuning(_abi.TUNE_WALK_BUDGET, -1)
         engine.set_tuning(_abi.TUNE_RESUME_LANES, 0)
         engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
 
@@ -258,7 +258,7 @@ def test_budget_knob_bounds(engine):
                      (_abi.TUNE_RESUME_LANES, 32), (_abi.TUNE_BUDGET_FRAC, 0)):
         with pytest.raises(ValueError):
             engine.set_tuning(key, bad)
-    engine.set_tuning(_abi.TUNE_WALK_BUDGET, 0)
+    engine.set_tuning(_abi.TUNE_WALK_BUDGET, -1)
     engine.set_tuning(_abi.TUNE_RESUME_LANES, 0)
 
 
@@ -274,6 +274,7 @@ def test_budgeted_walk_auto_choice(engine):
     from gev_amd import workloads as w
     from tests.test_gpu_parity import _synth_decode_verify
     ncu = torch.cuda.get_device_properties(engine.device).multi_processor_count
+    engine.set_tuning(_abi.TUNE_WALK_BUDGET, 0)  # auto (the default is off)
     n = 33 * ncu
     mixed = w.config_c4(total_payload=n * 160_000, n_conns=n, alpha=1.1, lo=64, hi=4096, seed=11)
     big = w.uniform(n, 8, 64 << 10, seed=12)
@@ -290,4 +291,4 @@ def test_budgeted_walk_auto_choice(engine):
         _synth_decode_verify(engine, mixed, check_slice_conns=2)
         assert engine.last_walk_budget == 0
     finally:
-        engine.set_tuning(_abi.TUNE_WALK_BUDGET, 0)
+        engine.set_tuning(_abi.TUNE_WALK_BUDGET, -1)

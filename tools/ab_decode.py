@@ -25,7 +25,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULTS = {"WALK_BUDGET": 0, "RESUME_LANES": 0, "BUDGET_FRAC": 18, "SPLIT_LANES": 0, "WALK_VARIANT": 0,
+DEFAULTS = {"WALK_BUDGET": -1, "RESUME_LANES": 0, "BUDGET_FRAC": 18, "SPLIT_LANES": 0, "WALK_VARIANT": 0,
             "UNMASK_VARIANT": 0, "UNMASK_GRID": 0, "EMIT_VARIANT": 0, "SPLIT_MODE": 0}
 
 

@@ -10,10 +10,13 @@ GiB/s host-to-host next to the raw pinned H2D / D2H copy rates on this box.
 
 With --direct-out the payload arena is mapped pinned host memory
 (gevws_pinned_alloc): the unmask kernel writes the plaintext over PCIe and no
-payload D2H copy is issued.
+payload D2H copy is issued.  With --zero-copy-in the input frames sit in
+mapped pinned host memory too and the kernels read them over PCIe (no H2D
+copy): with both, a chunk is its launches only -- the large-chunk form of the
+live server's zero-copy pass.
 
     python tools/host_inclusive.py [--gib 8] [--chunk-mib 64] [--streams 2] [--reps 3] [--sweep 64:2,128:3]
-                                   [--direct-out]
+                                   [--direct-out] [--zero-copy-in]
 """
 from __future__ import annotations
 
@@ -38,6 +41,8 @@ def main():
     ap.add_argument("--direct-out", action="store_true",
                     help="the unmask kernel writes the payload straight into mapped pinned host memory "
                          "(gevws_pinned_alloc) instead of a device arena + D2H copy")
+    ap.add_argument("--zero-copy-in", action="store_true",
+                    help="the kernels read the input frames straight from mapped pinned host memory (no H2D copy)")
     args = ap.parse_args()
 
     import numpy as np
@@ -56,7 +61,11 @@ def main():
     d_all = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
     d_all[lay.arena_bytes:] = 0
     eng.synth(d_all, torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev), lay.n_frames, lay.seed)
-    h_in = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, pin_memory=True)
+    if args.zero_copy_in:
+        in_arena = gev_amd.PinnedArena(lay.arena_bytes + gev_amd.IN_PAD)
+        h_in = torch.from_numpy(in_arena.host)  # CPU view of the mapped pages
+    else:
+        h_in = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, pin_memory=True)
     h_in.copy_(d_all)
     del d_all
     torch.cuda.empty_cache()
@@ -77,7 +86,8 @@ def main():
         chunk_pay = chunk_frames * pay_frame
         streams = [torch.cuda.Stream(dev) for _ in range(S)]
         engs = [gev_amd.Engine(0) for _ in range(S)]  # one context (scratch) per stream
-        d_in = [torch.zeros(chunk_in + gev_amd.IN_PAD, dtype=torch.uint8, device=dev) for _ in range(S)]
+        d_in = [None if args.zero_copy_in else torch.zeros(chunk_in + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+                for _ in range(S)]
         outs = [eng.alloc_batch(cpc, chunk_frames, 0 if args.direct_out else chunk_pay) for _ in range(S)]
         conn_tab = np.stack([np.arange(cpc, dtype=np.int64) * stream_bytes,
                              np.full(cpc, stream_bytes, np.int64)], 1)
@@ -90,16 +100,20 @@ def main():
                 nconn = min(cpc, lay.n_conns - c * cpc)
                 nin, nfr = nconn * stream_bytes, nconn * fpc
                 with torch.cuda.stream(s):
-                    d_in[k][:nin].copy_(h_in[c * chunk_in:c * chunk_in + nin], non_blocking=True)
+                    if args.zero_copy_in:
+                        src = in_arena.at(c * chunk_in)  # the kernels read the mapped host pages
+                    else:
+                        d_in[k][:nin].copy_(h_in[c * chunk_in:c * chunk_in + nin], non_blocking=True)
+                        src = d_in[k]
                     f0 = c * chunk_frames
                     if args.direct_out:
                         o = outs[k]
                         direct = gev_amd.Batch(frames=o.frames, payload=arena.at(f0 * pay_frame),
                                                conn_out=o.conn_out, summary=o.summary, n_conns=o.n_conns)
-                        engs[k].decode_async(d_in[k], nin, d_conns, nconn, direct, chunk_frames,
+                        engs[k].decode_async(src, nin, d_conns, nconn, direct, chunk_frames,
                                              nfr * pay_frame, stream=s)
                     else:
-                        engs[k].decode_async(d_in[k], nin, d_conns, nconn, outs[k], chunk_frames, chunk_pay,
+                        engs[k].decode_async(src, nin, d_conns, nconn, outs[k], chunk_frames, chunk_pay,
                                              stream=s)
                         h_pay[f0 * pay_frame:(f0 + nfr) * pay_frame].copy_(outs[k].payload[:nfr * pay_frame],
                                                                            non_blocking=True)
@@ -148,8 +162,9 @@ def main():
         configs = [tuple(int(x) for x in item.split(":")) for item in args.sweep.split(",")]
     runs = [run(cm, S) for cm, S in configs]
     best = max(runs, key=lambda r: r["payload_GiBps"])
-    mode = ("host-inclusive (pinned H2D -> decode writing the payload into mapped host memory)" if args.direct_out
-            else "host-inclusive (pinned H2D -> decode -> D2H, overlapped)")
+    src_mode = "decode reading mapped host memory" if args.zero_copy_in else "pinned H2D -> decode"
+    dst_mode = "writing the payload into mapped host memory" if args.direct_out else "-> D2H, overlapped"
+    mode = f"host-inclusive ({src_mode} {dst_mode})"
     res = {"mode": mode,
            "workload": lay.name, "payload_bytes": lay.payload_len, "input_bytes": lay.arena_bytes,
            "payload_GiBps": best["payload_GiBps"], "frames_per_s": best["frames_per_s"], "best": best,

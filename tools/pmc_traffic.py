@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--tag", required=True)
     ap.add_argument("--config", required=True)
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
-    ap.add_argument("--prefix", default="prof", help="gpurun_out/<prefix>_trace, <prefix>_pmc_* (scripts/gpu_profile.sh PREFIX)")
+    ap.add_argument("--prefix", default="prof", help="gpurun_out/<prefix>_trace, <prefix>_pmc_* (scripts/archive/gpu_profile.sh PREFIX)")
     args = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
