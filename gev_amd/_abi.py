@@ -175,6 +175,7 @@ SIGNATURES = {
     "gevws_ctx_last_split_lanes": (ctypes.c_int, [P]),
     "gevws_ctx_last_unmask_grid": (ctypes.c_int, [P]),
     "gevws_ctx_last_walk_budget": (ctypes.c_int64, [P]),
+    "gevws_unmask_profile": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "gevws_ctx_last_resumed": (ctypes.c_int64, [P]),
     "gevws_tuning_name": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32)]),

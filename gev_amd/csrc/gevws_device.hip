@@ -2773,12 +2773,49 @@ __device__ __forceinline__ WinRec load_rec(const gevws_frame* __restrict__ frame
 // FT (measurement switch): false re-creates the round-1 kernel whose fill
 // addresses were spilled (threadIdx.x used directly).
 // SP: streaming steps as software-pipelined runs (stream_run, U / 2 tiles per step).
+// PROF (measurement): thread 0 of every workgroup stamps the phases of its
+// loop with s_memtime and adds the cycle counts into g_uprof (gevws_unmask_profile):
+//   0 kernel, 1 streaming steps, 2 window first barrier, 3 fill, 4 second
+//   barrier, 5 search + payload load issue, 6 next-step decision + record
+//   prefetch, 7 wait for the payload + XOR + stores, 8 windows, 9 windows of
+//   more than 256 frames, 10 frames over all windows, 11 streaming steps,
+//   12 workgroups, 13 fallback (per-lane lookup) tiles; PROF 2 waits for the
+//   window's payload loads right after issuing them (phase 14: the loads'
+//   own latency, then decision and stores run on landed data).
+__device__ unsigned long long g_uprof[16];
+__device__ __forceinline__ uint64_t stamp() {
+  __asm__ volatile("" ::: "memory");
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  __asm__ volatile("" ::: "memory");
+  return t;
+}
+
 template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false, bool IS = false,
-          bool NTA = false, bool NTW = false>
+          bool NTA = false, bool NTW = false, int PROF = 0>
 __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
                                                uint32_t big_grid, const WinLds& L, bool wide = false) {
+  uint64_t pr[16] = {};
+  uint64_t tk0 = 0, tp = 0;
+  if constexpr (PROF) tk0 = stamp();
+  auto lap = [&](int k) {  // time since the previous stamp into phase k
+    if constexpr (PROF) {
+      const uint64_t t = stamp();
+      pr[k] += t - tp;
+      tp = t;
+    }
+  };
+  auto prof_flush = [&]() {
+    if constexpr (PROF) {
+      pr[0] = stamp() - tk0;
+      pr[12] = 1;
+      if (fresh_tid() == 0)
+        for (int k = 0; k < 16; ++k)
+          if (pr[k]) __hip_atomic_fetch_add(&g_uprof[k], (unsigned long long)pr[k], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
   uint32_t* const s_start = L.start;
   int32_t* const s_lend = L.lend;
   uint64_t* const s_delta = L.delta;
@@ -2793,6 +2830,7 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
   uint64_t t = (uint64_t)blockIdx.x * per;
   const uint64_t tend = t + per < ntiles ? t + per : ntiles;
   const uint32_t lane_off = threadIdx.x * 16;
+  if constexpr (PROF) tp = stamp();
   uint64_t f_po = 0, f_end = 0, f_src = 0;  // the cached (streaming) frame
   int64_t f_len = 0;
   uint32_t f_key = 0;
@@ -2833,6 +2871,8 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
       }
       pf_t = ~0ull;  // (never t here; redefining r0 keeps it dead across the step)
       r0 = WinRec{};
+      lap(1);
+      if constexpr (PROF) ++pr[11];
       continue;
     }
     uint64_t a, b;
@@ -2853,6 +2893,8 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
       }
       pf_t = ~0ull;
       r0 = WinRec{};
+      lap(1);
+      if constexpr (PROF) ++pr[11];
       continue;
     }
     // ---- window path
@@ -2874,9 +2916,13 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
         st16_stream<NTS>(out + p, x);
       }
       t += 1;
+      lap(7);
+      if constexpr (PROF) ++pr[13];
       continue;
     }
+    lap(6);
     __syncthreads();  // previous window's readers are done with the LDS table
+    lap(2);
     auto fill = [&](uint64_t i, const WinRec& q) {
       const uint64_t L = q.lo[1], po = q.hi[0], so = q.hi[1];
       s_start[i] = po > wbase ? (uint32_t)(po - wbase) : 0u;
@@ -2893,7 +2939,9 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
     const uint32_t tid = FT ? fresh_tid() : threadIdx.x;
     if (tid < F) fill(tid, have ? r0 : load_rec(frames, a + tid));
     for (uint64_t i = tid + kUnmaskBlock; i < F; i += kUnmaskBlock) fill(i, load_rec(frames, a + i));
+    lap(3);
     __syncthreads();
+    lap(4);
     u32x4 v[WT];
     uint32_t key[WT];
     int32_t rem[WT];
@@ -2930,6 +2978,11 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
     }
     // decide the next step (and fetch the next window's records) while this
     // window's payload loads are in flight
+    lap(5);
+    if constexpr (PROF == 2) {
+      __builtin_amdgcn_s_waitcnt(0);  // (measurement) every load of this wave landed
+      lap(14);
+    }
     __asm__ volatile("" ::: "memory");
     pf_t = ~0ull;
     if (wend_t < tend) {
@@ -2941,6 +2994,7 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
         if (tid < nF) r0 = load_rec(frames, pf_a + tid);
       }
     }
+    lap(6);
 #pragma unroll
     for (int u = 0; u < WT; ++u) {
       if (rem[u] > 0) {
@@ -2952,7 +3006,14 @@ __device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, c
       }
     }
     t = wend_t;
+    lap(7);
+    if constexpr (PROF) {
+      ++pr[8];
+      pr[9] += F > 256 ? 1 : 0;
+      pr[10] += F;
+    }
   }
+  prof_flush();
 }
 
 template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false>
@@ -2976,7 +3037,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
 // v3-4 -5 % on C1-shaped and -2.4 % on C2 batches, v4-8 -3 % on C4 and -2 % on
 // C5, equal on C3; profiles/r02_ab2.log).  One kernel, one LDS table, the
 // choice is a uniform branch on the summary the walk wrote.
-template <bool IS, bool NTA = false, bool NTW = false>
+template <bool IS, bool NTA = false, bool NTW = false, int PROF = 0>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
     const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
@@ -2989,8 +3050,326 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   if (2 * sum->run_frames >= sum->frames)  // frames the size of their predecessor on the connection
     unmask_v3_body<16, false, true, 2, kWinTiles, IS, NTA, NTW>(in, frames, tile_first, sum, out, big_grid, L);
   else  // mixed sizes: the whole (wide) grid for a batch of fewer than kWideGridTiles tiles
-    unmask_v4_body<16, 8, true, false, true, false, IS, NTA, NTW>(in, frames, tile_first, sum, out, big_grid, L,
-                                                                   sum->payload_bytes / kTile < kWideGridTiles);
+    unmask_v4_body<16, 8, true, false, true, false, IS, NTA, NTW, PROF>(in, frames, tile_first, sum, out, big_grid,
+                                                                         L, sum->payload_bytes / kTile < kWideGridTiles);
+}
+
+// v5 = v4 with the two latency chains of a window taken out of the critical
+// path (profiled with the PROF variant: per 8-tile window ~37 K cycles, a
+// quarter in the per-chunk searches -- eight binary searches one after the
+// other, each ~7 dependent LDS reads, before the chunk's payload load can
+// issue -- and a third in the next-step decision -- a chain of scalar loads of
+// the tile map and a record; profiles/r03_unmask_profile*.jsonl):
+//  * chunk -> frame by a map instead of a search: every non-empty frame marks
+//    its first 16-byte chunk in the window (payloads are 16-aligned and
+//    contiguous, so each chunk belongs to exactly one frame: the last one
+//    starting at or before it), and a workgroup prefix-max over the 2 048
+//    chunk slots turns the marks into the owner of every chunk; a lane then
+//    reads its 8 owners and their attributes in two LDS round trips, all
+//    chunks at once.  The map is double-buffered: window k clears the buffer
+//    window k+1 fills.
+//  * the tile map through an LDS cache of kTmapN entries (refilled by the
+//    whole workgroup every ~60 windows): a decision is LDS reads, not global.
+constexpr uint32_t kWinChunks = 8 * (uint32_t)kTile / 16;  // 2 048 chunks in an 8-tile window
+constexpr uint32_t kQuarter = kWinChunks / (kUnmaskBlock / 64);  // chunks per wave
+constexpr uint32_t kTmapN = 512;
+
+struct WinLds5 {
+  int32_t* lend;    // [kWin4Frames] payload end relative to the window (clamped)
+  uint64_t* delta;  // [kWin4Frames] src_off - payload_off
+  uint32_t* key;    // [kWin4Frames]
+  uint16_t* own;    // [2][kWinChunks] window chunk -> frame index + 1 (marks, then their prefix max)
+  uint32_t* wtot;   // [2][kUnmaskBlock / 64] per map: frame index + 1 covering each wave quarter's first chunk
+  uint32_t* tmap;   // [kTmapN] tile_first[tm0 ...]
+};
+
+template <int U, bool NTS, int PROF = 0>
+__device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
+                                               const uint32_t* __restrict__ tile_first,
+                                               const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
+                                               uint32_t big_grid, const WinLds5& L, bool wide = false) {
+  constexpr int WT = 8;
+  static_assert(WT * kTile / 16 == kWinChunks && kWinChunks == 8 * kUnmaskBlock, "8 chunks per thread");
+  uint64_t pr[16] = {};
+  uint64_t tk0 = 0, tp = 0;
+  if constexpr (PROF) tk0 = stamp();
+  auto lap = [&](int k) {
+    if constexpr (PROF) {
+      const uint64_t t = stamp();
+      pr[k] += t - tp;
+      tp = t;
+    }
+  };
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t total = sum->payload_bytes;
+  const uint64_t nframes = sum->frames;
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint32_t groups = active_groups(total, nframes, big_grid, wide);
+  if (blockIdx.x >= groups) return;
+  const uint64_t per = (ntiles + groups - 1) / groups;
+  uint64_t t = (uint64_t)blockIdx.x * per;
+  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+  {  // both chunk maps (and their wave seeds) start empty
+    const uint32_t tid = fresh_tid();
+    reinterpret_cast<u32x4*>(L.own)[tid] = u32x4{0, 0, 0, 0};
+    reinterpret_cast<u32x4*>(L.own + kWinChunks)[tid] = u32x4{0, 0, 0, 0};
+    if (tid < 2 * (kUnmaskBlock / 64)) L.wtot[tid] = 0;
+  }
+  __syncthreads();
+  if constexpr (PROF) tp = stamp();
+  uint64_t f_po = 0, f_end = 0, f_src = 0;  // the cached (streaming) frame
+  int64_t f_len = 0;
+  uint32_t f_key = 0;
+  uint64_t pf_t = ~0ull, pf_a = 0, pf_b = 0;
+  bool pf_stream = false;
+  WinRec r0 = {};
+  uint32_t buf = 0;          // chunk map of this window
+  uint64_t tm0 = ~0ull;      // first tile of the cached tile map
+  auto cache_frame = [&](uint64_t f) {
+    const uint64_t* rec = reinterpret_cast<const uint64_t*>(frames + f);
+    const uint64_t w0 = uniform64(rec[0]);
+    f_len = (int64_t)uniform64(rec[1]);
+    f_po = uniform64(rec[2]);
+    f_src = uniform64(rec[3]);
+    f_end = f_po + round16((uint64_t)f_len);
+    f_key = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
+  };
+  // tile_first[x] for x < ntiles from the LDS cache, which holds [x, x + 16]
+  // after the call (a refill is a workgroup step: callers are uniform)
+  auto tmap_at = [&](uint64_t x) -> uint64_t {
+    if (tm0 == ~0ull || x < tm0 || x + 16 >= tm0 + kTmapN) {
+      __syncthreads();  // every wave done with the old entries
+      tm0 = x;
+      for (uint32_t i = fresh_tid(); i < kTmapN; i += kUnmaskBlock) {
+        const uint64_t y = x + i;
+        L.tmap[i] = y < ntiles ? tile_first[y] : 0u;
+      }
+      __syncthreads();
+    }
+    return uniform32(L.tmap[x - tm0]);
+  };
+  auto decide = [&](uint64_t x, uint64_t& a, uint64_t& b, bool& stream) {
+    a = tmap_at(x);
+    stream = false;
+    if (x + U <= tend && tmap_at(x + U - 1) == a) {
+      cache_frame(a);
+      stream = x * kTile >= f_po && (x + U) * kTile <= f_end;
+    }
+    const uint64_t wt = (tend - x) < (uint64_t)WT ? (tend - x) : (uint64_t)WT;
+    b = x + wt < ntiles ? tmap_at(x + wt) : nframes - 1;
+  };
+  while (t < tend) {
+    const uint64_t base = t * kTile;
+    if (t + U <= tend && base >= f_po && base + U * kTile <= f_end) {
+      stream_step<U, false, NTS, 2, true>(in, out, base, f_po, f_src, f_len, f_key);
+      t += U;
+      pf_t = ~0ull;
+      r0 = WinRec{};
+      lap(1);
+      if constexpr (PROF) ++pr[11];
+      continue;
+    }
+    uint64_t a, b;
+    bool stream, have = false;
+    if (pf_t == t) {
+      a = pf_a;
+      b = pf_b;
+      stream = pf_stream;
+      have = !pf_stream;
+    } else {
+      decide(t, a, b, stream);
+    }
+    if (stream) {
+      stream_step<U, false, NTS, 2, true>(in, out, base, f_po, f_src, f_len, f_key);
+      t += U;
+      pf_t = ~0ull;
+      r0 = WinRec{};
+      lap(1);
+      if constexpr (PROF) ++pr[11];
+      continue;
+    }
+    const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
+    const uint64_t wend_t = t + wt;
+    const uint64_t wbase = base;
+    const uint64_t F = b - a + 1;
+    if (F > (uint64_t)kWin4Frames) {  // runs of empty frames: per-lane lookup, one tile
+      const uint64_t p = base + fresh_tid() * 16;
+      if (p < total) {
+        const gevws_frame* fr = frames + find_frame(frames, tile_first, t, ntiles, nframes, p);
+        const uint64_t rel = p - fr->payload_off;
+        uint32_t k;
+        memcpy(&k, fr->hdr.mask, 4);
+        u32x4 x = ld16u(in + fr->src_off + rel) ^ (fr->hdr.masked ? k : 0u);
+        const int64_t r = fr->hdr.length - (int64_t)rel;
+        if (r < 16) x = keep_bytes(x, r);
+        st16_stream<NTS>(out + p, x);
+      }
+      t += 1;
+      pf_t = ~0ull;
+      r0 = WinRec{};
+      lap(7);
+      if constexpr (PROF) ++pr[13];
+      continue;
+    }
+    uint16_t* const own = L.own + buf * kWinChunks;
+    uint32_t* const carry = L.wtot + buf * (kUnmaskBlock / 64);
+    lap(6);
+    __syncthreads();  // previous window's readers are done with the frame table
+    lap(2);
+    auto fill = [&](uint64_t i, const WinRec& q) {
+      const uint64_t Ln = q.lo[1], po = q.hi[0], so = q.hi[1];
+      const uint64_t lend = po + Ln;
+      L.lend[i] = lend <= wbase ? 0 : (lend - wbase > 0x7fffffffull ? 0x7fffffff : (int32_t)(lend - wbase));
+      L.delta[i] = so - po;
+      L.key[i] = ((q.lo[0] >> 24) & 0xff) ? (uint32_t)(q.lo[0] >> 32) : 0u;
+      if (Ln) {  // the frame's first chunk in the window (frame a's is chunk 0)
+        const uint64_t sc = po > wbase ? (po - wbase) >> 4 : 0;
+        if (sc < kWinChunks) own[sc] = (uint16_t)(i + 1);
+        // the frame covering the first chunk of wave w's quarter (w > 0)
+        // seeds that wave's scan: no cross-wave step
+        const uint64_t ec = (po + round16(Ln) - wbase) >> 4;  // one past its last chunk
+#pragma unroll
+        for (uint32_t w = 1; w < kUnmaskBlock / 64; ++w)
+          if (sc < w * kQuarter && w * kQuarter < ec) carry[w] = (uint32_t)(i + 1);
+      }
+    };
+    const uint32_t tid = fresh_tid();
+    if (tid < F) fill(tid, have ? r0 : load_rec(frames, a + tid));
+    for (uint64_t i = tid + kUnmaskBlock; i < F; i += kUnmaskBlock) fill(i, load_rec(frames, a + i));
+    lap(3);
+    __syncthreads();
+    lap(4);
+    // prefix max over the chunk marks, per wave over its own quarter of the
+    // window (wave w: chunks [512 w, 512 (w + 1)), lane l the 8 from 512 w + 8 l),
+    // seeded with the frame covering the quarter's first chunk; the wave then
+    // reads only its quarter's owners, so no barrier follows
+    {
+      const uint32_t j = fresh_tid(), lane = j & 63, w = j >> 6;
+      u32x4 m = reinterpret_cast<const u32x4*>(own)[j];
+      uint32_t run[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        run[2 * k] = m[k] & 0xffffu;
+        run[2 * k + 1] = m[k] >> 16;
+      }
+#pragma unroll
+      for (int k = 1; k < 8; ++k) run[k] = run[k] > run[k - 1] ? run[k] : run[k - 1];
+      uint32_t inc = run[7];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= (uint32_t)d) inc = inc > y ? inc : y;
+      }
+      uint32_t exc = (uint32_t)__shfl_up((int)inc, 1, 64);
+      const uint32_t seed = w ? carry[w] : 0u;
+      if (lane == 0) exc = 0;
+      exc = exc > seed ? exc : seed;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t lo16 = run[2 * k] > exc ? run[2 * k] : exc;
+        const uint32_t hi16 = run[2 * k + 1] > exc ? run[2 * k + 1] : exc;
+        m[k] = lo16 | (hi16 << 16);
+      }
+      reinterpret_cast<u32x4*>(own)[j] = m;
+      // the next window's map and seeds start empty (their last readers
+      // finished before this window's first barrier)
+      reinterpret_cast<u32x4*>(L.own + (buf ^ 1) * kWinChunks)[j] = u32x4{0, 0, 0, 0};
+      if (lane == 0) L.wtot[(buf ^ 1) * (kUnmaskBlock / 64) + w] = 0;
+    }
+    lap(5);
+    u32x4 v[WT];
+    uint32_t key[WT];
+    int32_t rem[WT];
+    uint32_t lov[WT];
+    // wave w, step u: the 64 contiguous chunks 512 w + 64 u + lane (1 KiB)
+#pragma unroll
+    for (int u = 0; u < WT; ++u) {
+      const uint32_t tq = fresh_tid();
+      const uint32_t c = (tq >> 6) * kQuarter + (uint32_t)u * 64 + (tq & 63);
+      const uint32_t o = own[c];
+      lov[u] = o ? o - 1 : 0;
+    }
+    // (the lane's chunk offsets re-derived from a fresh threadIdx.x: kept live
+    // across the loop they spill, and each reload -- a scratch load queued
+    // behind the payload loads, vmcnt being in order -- serialises them)
+    const uint32_t tl = fresh_tid();
+    const uint32_t loff = (tl >> 6) * kQuarter * 16 + (tl & 63) * 16;
+#pragma unroll
+    for (int u = 0; u < WT; ++u) {
+      const uint32_t rel = (uint32_t)u * 1024 + loff;
+      const uint64_t p = wbase + rel;
+      rem[u] = 0;
+      key[u] = 0;
+      v[u] = u32x4{0, 0, 0, 0};
+      if ((uint64_t)rel < wt * kTile && p < total) {
+        const uint32_t lo = lov[u];
+        rem[u] = L.lend[lo] - (int32_t)rel;
+        key[u] = L.key[lo];
+        v[u] = ld16u_stream<true>(in + (p + L.delta[lo]));
+      }
+    }
+    lap(5);
+    __asm__ volatile("" ::: "memory");
+    pf_t = ~0ull;
+    if (wend_t < tend) {
+      decide(wend_t, pf_a, pf_b, pf_stream);
+      pf_t = wend_t;
+      if (!pf_stream) {
+        const uint64_t nF = pf_b - pf_a + 1;
+        const uint32_t tid2 = fresh_tid();
+        if (tid2 < nF) r0 = load_rec(frames, pf_a + tid2);
+      }
+    }
+    lap(6);
+    const uint32_t ts = fresh_tid();
+    const uint32_t soff = (ts >> 6) * kQuarter * 16 + (ts & 63) * 16;
+#pragma unroll
+    for (int u = 0; u < WT; ++u) {
+      if (rem[u] > 0) {
+        u32x4 x = v[u] ^ key[u];
+        if (rem[u] < 16) x = keep_bytes(x, rem[u]);
+        st16_stream<NTS>(out + wbase + (uint32_t)u * 1024 + soff, x);
+      }
+    }
+    buf ^= 1;
+    t = wend_t;
+    lap(7);
+    if constexpr (PROF) {
+      ++pr[8];
+      pr[9] += F > 256 ? 1 : 0;
+      pr[10] += F;
+    }
+  }
+  if constexpr (PROF) {
+    pr[0] = stamp() - tk0;
+    pr[12] = 1;
+    if (fresh_tid() == 0)
+      for (int k = 0; k < 16; ++k)
+        if (pr[k]) __hip_atomic_fetch_add(&g_uprof[k], (unsigned long long)pr[k], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// The default unmask with v5 for mixed batches (v3's 4-tile windows for
+// batches of equal-size frames, as k_unmask_auto).
+template <int PROF = 0>
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto5(
+    const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
+  __shared__ uint32_t s_start[kWin4Frames];
+  __shared__ int32_t s_lend[kWin4Frames];
+  __shared__ uint64_t s_delta[kWin4Frames];
+  __shared__ uint32_t s_key[kWin4Frames];
+  __shared__ __attribute__((aligned(16))) uint16_t s_own[2 * kWinChunks];
+  __shared__ uint32_t s_wtot[2 * (kUnmaskBlock / 64)];
+  __shared__ uint32_t s_tmap[kTmapN];
+  if (2 * sum->run_frames >= sum->frames)
+    unmask_v3_body<16, false, true, 2, kWinTiles, false, true, true>(in, frames, tile_first, sum, out, big_grid,
+                                                                     WinLds{s_start, s_lend, s_delta, s_key});
+  else
+    unmask_v5_body<16, true, PROF>(in, frames, tile_first, sum, out, big_grid,
+                                   WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap},
+                                   sum->payload_bytes / kTile < kWideGridTiles);
 }
 
 // ------------------------------------------------------------------ outbound encode (§8f row 1)
@@ -3941,10 +4320,10 @@ struct UnmaskVariant {
 // Variant 0 is the default; the others are kept for A/B measurement
 // (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 const UnmaskVariant kUnmaskVariants[] = {
-    {k_unmask_auto<false, true, true>, 16,
-     "auto: v3 4-tile windows for batches of equal-size frames, v4 pipelined 8-tile windows otherwise (summary "
-     "statistics of the walk); non-temporal streaming and window loads; a wide grid for a smaller batch of "
-     "mixed sizes after one on this context", true},
+    {k_unmask_auto5<0>, 16,
+     "auto: v3 4-tile windows for batches of equal-size frames, v5 (v4's pipelined 8-tile windows with a chunk -> "
+     "frame map instead of per-chunk searches and the tile map cached in LDS) otherwise; non-temporal streaming "
+     "and window loads; a wide grid for a smaller batch of mixed sizes after one on this context", true},
     {k_unmask_v4<16, 8, true>, 16,
      "v4 U16 streaming (aligned loads, DPP rotate) + pipelined 8-tile LDS window (next step's tile map and "
      "records fetched during the current window's payload loads)"},
@@ -3966,6 +4345,16 @@ const UnmaskVariant kUnmaskVariants[] = {
      "all chunks of a lane)"},
     {k_unmask_auto<false>, 16, "auto with plain (temporal) streaming loads (the default until round 2's end)"},
     {k_unmask_auto<false, true>, 16, "auto with non-temporal streaming loads, plain window loads"},
+    {k_unmask_auto<false, true, true, 1>, 16,
+     "measurement: the default with v4's phases timed per workgroup (gevws_unmask_profile)", true},
+    {k_unmask_auto<true, true, true, 1>, 16,
+     "measurement: 14 with the window searches interleaved (binary lifting, as 11)", true},
+    {k_unmask_auto<false, true, true, 2>, 16,
+     "measurement: 14 waiting for each window's payload loads right after issuing them (their latency)", true},
+    {k_unmask_auto<false, true, true>, 16,
+     "auto with v4 for mixed batches (the default until round 3: per-chunk binary searches in LDS, tile map read "
+     "with scalar loads)", true},
+    {k_unmask_auto5<1>, 16, "measurement: the default (v5) with its phases timed (gevws_unmask_profile)", true},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
@@ -4155,6 +4544,18 @@ int64_t gevws_ctx_last_resumed(gevws_ctx* ctx) {
 }
 
 int gevws_ctx_last_unmask_grid(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_unmask_grid : -1; }
+
+int gevws_unmask_profile(gevws_ctx* ctx, uint64_t out[16], int reset) {
+  if (!ctx || !out) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  GEVWS_HIP(hipDeviceSynchronize());
+  GEVWS_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_uprof), 16 * sizeof(uint64_t)));
+  if (reset) {
+    const uint64_t z[16] = {};
+    GEVWS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_uprof), z, sizeof(z)));
+  }
+  return GEVWS_OK;
+}
 
 int gevws_ctx_set_timing(gevws_ctx* ctx, int enable) {
   if (!ctx) return GEVWS_ERR_INVALID;

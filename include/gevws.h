@@ -209,6 +209,15 @@ int64_t gevws_ctx_last_resumed(gevws_ctx *ctx);
  * of mixed frame sizes below 8 GiB of output (the kernel then uses the wide
  * grid if this batch is one too). */
 int gevws_ctx_last_unmask_grid(const gevws_ctx *ctx);
+/* Measurement: the phase cycle counts the profiled unmask variants
+ * (GEVWS_TUNE_UNMASK_VARIANT 14 -- v4 -- and 18 -- v5, the default) accumulated on ctx's device since the last
+ * reset -- 0 kernel, 1 streaming steps, 2 window first barrier, 3 window fill,
+ * 4 second barrier, 5 search + payload load issue, 6 next-step decision, 7
+ * payload wait + XOR + stores, 8 windows, 9 windows of > 256 frames, 10 frames
+ * over the windows, 11 streaming steps, 12 workgroups, 13 per-lane fallback
+ * tiles (cycles summed over workgroups, thread 0's view) -- then zeroes them
+ * when reset != 0.  Waits for the device. */
+int gevws_unmask_profile(gevws_ctx *ctx, uint64_t out[16], int reset);
 /* Human-readable name of a variant (GEVWS_TUNE_UNMASK_VARIANT or
  * GEVWS_TUNE_WALK_VARIANT), or NULL past the last one. */
 const char *gevws_tuning_name(int key, int64_t value);
