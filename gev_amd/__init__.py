@@ -360,11 +360,13 @@ class Engine:
             raise RuntimeError(status_string(st))
 
     def gather_(self, src, nbytes: int, lanes: int, per_lane: int, dependent: bool, sink, seed: int = 1,
-                stream=None) -> None:
-        """gevws_gather_async: the header walk's random-line fetch ceiling (measurement only)."""
-        assert nbytes <= src.numel() and sink.numel() >= lanes
+                stream=None, load_kind: int = 0) -> None:
+        """gevws_gather_async: the header walk's random-line fetch ceiling (measurement only).
+        load_kind: 0 plain 16-byte loads, 1 / 2 two 8-byte system- / agent-scope loads, 3 one 4-byte
+        system-scope load."""
+        assert nbytes <= src.numel() and sink.numel() >= lanes and 0 <= load_kind < 4
         st = lib.gevws_gather_async(self._ctx, _stream_handle(stream), src.data_ptr(), nbytes, lanes, per_lane,
-                                    1 if dependent else 0, seed, sink.data_ptr())
+                                    (1 if dependent else 0) | (load_kind << 1), seed, sink.data_ptr())
         if st != OK:
             raise RuntimeError(status_string(st))
 

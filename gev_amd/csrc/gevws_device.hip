@@ -1750,7 +1750,25 @@ __global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __
 // DEP: each address depends on the previous load's data (a chain, one load in
 // flight per lane, like the walk); else the lane issues 8 independent loads
 // at a time -- the random-line fetch rate of HBM, the walk's roofline.
-template <bool DEP>
+template <int LK>
+__device__ __forceinline__ uint64_t gather_load(const uint8_t* p) {
+  // LK 0: one plain 16-byte load; 1 / 2: two aligned 8-byte relaxed atomic
+  // loads at system / agent scope (gfx950: sc0 sc1 / sc1 -- miss L2 and
+  // fetch from memory); 3: one 4-byte system-scope load
+  if constexpr (LK == 0) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+    return (uint64_t)v[0] ^ v[2];
+  } else if constexpr (LK == 3) {
+    return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    constexpr int sc = LK == 1 ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
+    const uint64_t a = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, sc);
+    const uint64_t b = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p + 8), __ATOMIC_RELAXED, sc);
+    return a ^ b;
+  }
+}
+
+template <bool DEP, int LK = 0>
 __global__ __launch_bounds__(kCountBlock) void k_gather(const uint8_t* __restrict__ in, uint64_t lines,
                                                         uint32_t per_lane, uint64_t seed, uint64_t* __restrict__ sink) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1763,19 +1781,19 @@ __global__ __launch_bounds__(kCountBlock) void k_gather(const uint8_t* __restric
   if constexpr (DEP) {
     for (uint32_t k = 0; k < per_lane; ++k) {
       x = mix(x + acc);
-      const u32x4 v = *reinterpret_cast<const u32x4*>(in + (x % lines) * 128 + ((x >> 60) & 7) * 16);
-      acc = (uint64_t)(v[0] & 1u);  // the next address waits for this load's data
+      const uint64_t v = gather_load<LK>(in + (x % lines) * 128 + ((x >> 60) & 7) * 16);
+      acc = v & 1u;  // the next address waits for this load's data
     }
   } else {
     for (uint32_t k = 0; k < per_lane; k += 8) {
-      u32x4 v[8];
+      uint64_t v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint64_t z = mix(x + k + j);
-        v[j] = *reinterpret_cast<const u32x4*>(in + (z % lines) * 128 + ((z >> 60) & 7) * 16);
+        v[j] = gather_load<LK>(in + (z % lines) * 128 + ((z >> 60) & 7) * 16);
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc += v[j][0];
+      for (int j = 0; j < 8; ++j) acc += v[j];
     }
   }
   sink[g] = acc;
@@ -3081,6 +3099,7 @@ struct WinLds5 {
   uint16_t* own;    // [2][kWinChunks] window chunk -> frame index + 1 (marks, then their prefix max)
   uint32_t* wtot;   // [2][kUnmaskBlock / 64] per map: frame index + 1 covering each wave quarter's first chunk
   uint32_t* tmap;   // [kTmapN] tile_first[tm0 ...]
+  uint64_t* prof;   // [16] PROF counters
 };
 
 template <int U, bool NTS, int PROF = 0>
@@ -3090,13 +3109,19 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
                                                uint32_t big_grid, const WinLds5& L, bool wide = false) {
   constexpr int WT = 8;
   static_assert(WT * kTile / 16 == kWinChunks && kWinChunks == 8 * kUnmaskBlock, "8 chunks per thread");
-  uint64_t pr[16] = {};
+  // (PROF: the counters live in LDS, updated by thread 0 -- registers for
+  // them made the kernel spill, and the spill reloads distorted the phases)
   uint64_t tk0 = 0, tp = 0;
   if constexpr (PROF) tk0 = stamp();
+  auto pr_add = [&](int k, uint64_t v) {
+    if constexpr (PROF) {
+      if (fresh_tid() == 0) L.prof[k] += v;
+    }
+  };
   auto lap = [&](int k) {
     if constexpr (PROF) {
       const uint64_t t = stamp();
-      pr[k] += t - tp;
+      pr_add(k, t - tp);
       tp = t;
     }
   };
@@ -3111,6 +3136,7 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
   const uint64_t tend = t + per < ntiles ? t + per : ntiles;
   {  // both chunk maps (and their wave seeds) start empty
     const uint32_t tid = fresh_tid();
+    if (PROF && tid < 16) L.prof[tid] = 0;
     reinterpret_cast<u32x4*>(L.own)[tid] = u32x4{0, 0, 0, 0};
     reinterpret_cast<u32x4*>(L.own + kWinChunks)[tid] = u32x4{0, 0, 0, 0};
     if (tid < 2 * (kUnmaskBlock / 64)) L.wtot[tid] = 0;
@@ -3166,7 +3192,7 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
       pf_t = ~0ull;
       r0 = WinRec{};
       lap(1);
-      if constexpr (PROF) ++pr[11];
+      pr_add(11, 1);
       continue;
     }
     uint64_t a, b;
@@ -3185,7 +3211,7 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
       pf_t = ~0ull;
       r0 = WinRec{};
       lap(1);
-      if constexpr (PROF) ++pr[11];
+      pr_add(11, 1);
       continue;
     }
     const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
@@ -3208,7 +3234,7 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
       pf_t = ~0ull;
       r0 = WinRec{};
       lap(7);
-      if constexpr (PROF) ++pr[13];
+      pr_add(13, 1);
       continue;
     }
     uint16_t* const own = L.own + buf * kWinChunks;
@@ -3334,19 +3360,17 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
     buf ^= 1;
     t = wend_t;
     lap(7);
-    if constexpr (PROF) {
-      ++pr[8];
-      pr[9] += F > 256 ? 1 : 0;
-      pr[10] += F;
-    }
+    pr_add(8, 1);
+    pr_add(9, F > 256 ? 1 : 0);
+    pr_add(10, F);
   }
   if constexpr (PROF) {
-    pr[0] = stamp() - tk0;
-    pr[12] = 1;
+    pr_add(0, stamp() - tk0);
+    pr_add(12, 1);
     if (fresh_tid() == 0)
       for (int k = 0; k < 16; ++k)
-        if (pr[k]) __hip_atomic_fetch_add(&g_uprof[k], (unsigned long long)pr[k], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+        if (L.prof[k]) __hip_atomic_fetch_add(&g_uprof[k], (unsigned long long)L.prof[k], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -3363,12 +3387,13 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   __shared__ __attribute__((aligned(16))) uint16_t s_own[2 * kWinChunks];
   __shared__ uint32_t s_wtot[2 * (kUnmaskBlock / 64)];
   __shared__ uint32_t s_tmap[kTmapN];
+  __shared__ uint64_t s_prof[PROF ? 16 : 1];
   if (2 * sum->run_frames >= sum->frames)
     unmask_v3_body<16, false, true, 2, kWinTiles, false, true, true>(in, frames, tile_first, sum, out, big_grid,
                                                                      WinLds{s_start, s_lend, s_delta, s_key});
   else
     unmask_v5_body<16, true, PROF>(in, frames, tile_first, sum, out, big_grid,
-                                   WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap},
+                                   WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap, s_prof},
                                    sum->payload_bytes / kTile < kWideGridTiles);
 }
 
@@ -5049,8 +5074,11 @@ int gevws_gather_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64
     return GEVWS_ERR_INVALID;
   DeviceGuard g(ctx->device);
   hipStream_t st = pick_stream(ctx, stream);
-  (dependent ? k_gather<true> : k_gather<false>)<<<lanes / kCountBlock, kCountBlock, 0, st>>>(
-      d_in, in_bytes / 128, per_lane, seed, d_sink);
+  // dependent: bit 0 = chain; bits 1-2 = load kind (gather_load)
+  using K = void (*)(const uint8_t*, uint64_t, uint32_t, uint64_t, uint64_t*);
+  static const K ks[8] = {k_gather<false, 0>, k_gather<true, 0>, k_gather<false, 1>, k_gather<true, 1>,
+                          k_gather<false, 2>, k_gather<true, 2>, k_gather<false, 3>, k_gather<true, 3>};
+  ks[dependent & 7]<<<lanes / kCountBlock, kCountBlock, 0, st>>>(d_in, in_bytes / 128, per_lane, seed, d_sink);
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;
 }

@@ -26,6 +26,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=int, default=16)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--load-kinds", default="0", help="comma list: 0 plain 16 B, 1 / 2 two 8-B system / agent "
+                    "scope loads (miss L2), 3 one 4-B system-scope load")
+    ap.add_argument("--cases", default="", help="lanes:per_lane:dep,... (default: the C4 set)")
     args = ap.parse_args()
     import torch
     import gev_amd
@@ -39,21 +42,25 @@ def main():
     # same loads issued independently
     cases = [(65536, 672, True), (65536, 672, False), (262144, 168, False), (8192, 672, True), (8192, 1104, True),
              (8192, 672, False), (131072, 336, True)]
+    if args.cases:
+        cases = [(int(a), int(b), bool(int(c))) for a, b, c in (x.split(":") for x in args.cases.split(","))]
+    kinds = [int(k) for k in args.load_kinds.split(",")]
+    cases = [c + (k,) for k in kinds for c in cases]
     sink = torch.empty(max(c[0] for c in cases), dtype=torch.int64, device=dev)
     out = []
-    for lanes, per, dep in cases:
+    for lanes, per, dep, lk in cases:
         ts = []
         for r in range(args.reps + 1):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            eng.gather_(buf, n, lanes, per, dep, sink, seed=r + 1)
+            eng.gather_(buf, n, lanes, per, dep, sink, seed=r + 1, load_kind=lk)
             e1.record()
             torch.cuda.synchronize()
             if r:
                 ts.append(e0.elapsed_time(e1))
         ms = statistics.median(ts)
         loads = lanes * per
-        rec = {"lanes": lanes, "per_lane": per, "dependent": dep, "ms": round(ms, 4),
+        rec = {"lanes": lanes, "per_lane": per, "dependent": dep, "load_kind": lk, "ms": round(ms, 4),
                "Gloads_per_s": round(loads / ms / 1e6, 2), "line_GBps": round(loads * 128 / ms / 1e6, 1),
                "us_per_step": round(ms * 1e3 / per, 3) if dep else None}
         print(json.dumps(rec), flush=True)
