@@ -292,14 +292,15 @@ __device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uin
 
 // ------------------------------------------------------------------ 1. walk (count)
 // Frame entries recorded by the counting walk so the emit pass need not
-// re-fetch every header line from HBM: 16 bytes per frame in a per-connection
+// re-fetch every header line from HBM: 8 bytes per frame in a per-connection
 // slot run whose base derives from the stream's arena offset (no scan needed):
-// base_c = 4 (off_c / 4G + c), capacity 4 (len_c / 4G + 1), with the
-// granularity G the smallest power of two >= 64 B that keeps the table within
-// kEntryBudget; runs start on 64-byte boundaries, so the walk can store its
-// entries as whole 64-byte groups of four (k_walk_count GRP).  The runs are
+// base_c = S (off_c / SG + c), capacity S (len_c / SG + 1) with S = kSlotAlign
+// = 32, the granularity G the smallest power of two >= 64 B that keeps the
+// table within kEntryBudget; runs start on 256-byte boundaries, so the walk can
+// store its entries as whole groups (k_walk_count GRP: 32 bytes of four; the
+// LDS-ring writer: 256 bytes of 32).  The runs are
 // disjoint when the whole table is in increasing input order with no overlap
-// (for c < d: base_c + cap_c <= 4 ((off_c + len_c) / 4G + 1 + c) <= base_d);
+// (for c < d: base_c + cap_c <= S ((off_c + len_c) / SG + 1 + c) <= base_d);
 // a neighbour check per connection cannot establish that (an
 // unsorted table can pass every local check and still collide), so every
 // workgroup reports whether any of its connections starts before the previous
@@ -311,17 +312,38 @@ __device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uin
 constexpr uint64_t kGroupedWalkChainsPerCU = 128;  // k_walk_count GRP from n_conns >= this x CUs
 constexpr uint32_t kEntryGranMinShift = 6;        // 64-byte granularity when the table fits
 constexpr uint64_t kEntryBudget = 1ull << 29;     // entries (8 GiB of scratch) at most
-// slot runs start on 16-entry (256-byte) boundaries: the writer wave of the
+// slot runs start on 32-entry (256-byte) boundaries: the writer wave of the
 // LDS-ring walk stores whole 256-byte groups (k_walk_count ST 2)
-constexpr uint32_t kSlotShift = 4;
+constexpr uint32_t kSlotShift = 5;
 constexpr uint64_t kSlotAlign = 1ull << kSlotShift;
+// 8-byte entry: the key, and b0 | masked << 8 | length form << 9 | payload
+// length << 11.  The header's position is not stored: a row's frames are
+// contiguous from its start, so the record pass recomputes each position as
+// the prefix sum of the frame sizes before it (hlen + L).  A payload length
+// >= kLenEsc is stored as kLenEsc and re-read from the header by the record
+// pass, where the prefix sum gives its position (rare: frames of 2 MiB and
+// more, whose unmask dwarfs one header load).  Round 2's 16-byte entry
+// (position, key, length, meta) cost the walk 0.71 GB of C4's writes and the
+// record pass as many reads (profiles/r03_pmc_split.json).
+constexpr uint32_t kLenEsc = (1u << 21) - 1;
 struct WalkEntry {
-  uint32_t pos;   // header offset in the connection stream
   uint32_t mask;
-  uint32_t len;   // payload length (< 2^32: the stream is)
-  uint32_t meta;  // b0 | masked << 8 | hlen << 16
+  uint32_t w;
 };
-static_assert(sizeof(WalkEntry) == 16, "one dwordx4 per entry");
+static_assert(sizeof(WalkEntry) == 8, "one dwordx2 per entry");
+// meta: b0 | masked << 8 | hlen << 16 (walk_parse / walk_chain)
+__device__ __forceinline__ WalkEntry make_entry(uint32_t key, uint64_t L, uint32_t meta) {
+  const uint32_t hlen = meta >> 16, masked = (meta >> 8) & 1u;
+  const uint32_t ext = hlen - 2 - 4 * masked;  // 0, 2 or 8 length bytes
+  const uint32_t form = ext == 0 ? 0u : (ext == 2 ? 1u : 2u);
+  const uint32_t l21 = L < kLenEsc ? (uint32_t)L : kLenEsc;
+  return WalkEntry{key, (meta & 0x1ffu) | (form << 9) | (l21 << 11)};
+}
+__device__ __forceinline__ uint32_t entry_hlen(const WalkEntry& e) {
+  const uint32_t form = (e.w >> 9) & 3u;
+  return 2 + (form == 2 ? 8u : 2u * form) + 4 * ((e.w >> 8) & 1u);
+}
+__device__ __forceinline__ uint32_t entry_len21(const WalkEntry& e) { return e.w >> 11; }
 
 __device__ __forceinline__ bool entry_slots_of(const gevws_conn_in& ci, uint32_t c, uint64_t n_entries,
                                               uint32_t gshift, uint64_t& base, uint64_t& cap) {
@@ -420,7 +442,7 @@ __device__ __forceinline__ WalkRes walk_res_fresh(uint64_t err = 0, int32_t st =
 constexpr uint32_t kRingDone = 0x80000000u;   // head flag: the chain is finished
 // entries per lane's LDS ring for a writer group of WGS entries
 template <int WGS>
-constexpr uint32_t ring_size() { return WGS >= 16 ? 32u : 16u; }
+constexpr uint32_t ring_size() { return WGS >= 8 ? 2u * WGS : 16u; }
 struct WalkRing {
   WalkEntry* e;    // ring_size entries (LDS)
   uint32_t mask;   // ring_size - 1
@@ -455,17 +477,14 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
     // table), so the compiler waits vmcnt(1), not vmcnt(0).
     uint64_t lo, hi;
     load_window<NTH>(s + pos, lo, hi);
-    if constexpr (!NST) *sink = WalkEntry{0, 0, 0, 0};
+    if constexpr (!NST) *sink = WalkEntry{0, 0};
     uint64_t prev_fsz = 0;  // speculation (D > 0): size of the last frame and the run of equal sizes
     uint32_t run = 0;
-    WalkEntry g0 = {0, 0, 0, 0}, g1 = g0, g2 = g0;  // GRP: the last three entries, oldest first
+    WalkEntry g0 = {0, 0}, g1 = g0, g2 = g0;  // GRP: the last three entries, oldest first
     auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
+      (void)p;  // positions are recomputed by the record pass
       rec = rec && nf < ecap;
-      WalkEntry e;
-      e.pos = (uint32_t)p;
-      e.mask = key;
-      e.len = (uint32_t)L;
-      e.meta = meta;
+      const WalkEntry e = make_entry(key, L, meta);
       if constexpr (ST == 1) {  // measurement: no stores at all (the walk's pure chain cost)
         rec = false;
       } else if constexpr (ST == 2) {
@@ -596,7 +615,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
             if (stop || qn < (uint32_t)D || pos + fsz > len) break;
           }
           if (fail) return false;
-          if constexpr (!NST) *sink = WalkEntry{0, 0, 0, 0};  // same [load, store] in flight as the plain path
+          if constexpr (!NST) *sink = WalkEntry{0, 0};  // same [load, store] in flight as the plain path
         }
       }
       return true;
@@ -653,7 +672,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
 }
 
 // The writer wave of k_walk_count ST 2: lane j copies walker lane j's ring to
-// its entry slots (ebase ~0: none) in groups of WGS entries (WGS x 16 bytes,
+// its entry slots (ebase ~0: none) in groups of WGS entries (WGS x 8 bytes,
 // aligned: slot runs start on kSlotAlign entries) as they are published, the
 // last partial group when the chain is done; every slot below ecap only.
 // Whole groups: a 64-byte group is half an L2 line, and scattered half-line
@@ -663,7 +682,8 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
 template <int WGS, bool NTW = false>
 __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries, WalkRing ring, uint64_t ebase,
                                                  uint64_t ecap) {
-  static_assert(WGS == 4 || WGS == 8 || WGS == 16, "group of 4, 8 or 16 entries");
+  static_assert(WGS == 8 || WGS == 16 || WGS == 32, "group of 8, 16 or 32 entries");
+  static_assert(WGS <= (int)kSlotAlign, "groups aligned by the slot runs");
   uint32_t t = 0;
   bool fin = false;
   for (;;) {
@@ -676,14 +696,14 @@ __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries
 #pragma unroll
         for (int k = 0; k < WGS; ++k) g[k] = ring.e[(t + k) & ring.mask];
         if (ebase != ~0ull && t + WGS <= ecap) {
-          WalkEntry* d = entries + ebase + t;  // WGS x 16-byte aligned
+          u32x4* d = reinterpret_cast<u32x4*>(entries + ebase + t);  // WGS x 8-byte aligned
 #pragma unroll
-          for (int k = 0; k < WGS; ++k) {
+          for (int k = 0; k < WGS / 2; ++k) {
+            const u32x4 v = {g[2 * k].mask, g[2 * k].w, g[2 * k + 1].mask, g[2 * k + 1].w};
             if constexpr (NTW)
-              __builtin_nontemporal_store(u32x4{g[k].pos, g[k].mask, g[k].len, g[k].meta},
-                                          reinterpret_cast<u32x4*>(d + k));
+              __builtin_nontemporal_store(v, d + k);
             else
-              d[k] = g[k];
+              d[k] = v;
           }
         }
         t += WGS;
@@ -718,7 +738,7 @@ struct WalkResume {
 };
 static_assert(sizeof(WalkResume) == 64, "one resume record per 64 bytes");
 
-template <int D, bool GRP, bool NTH = false, int PF = 0, bool BUD = false, int UNR = 2, int ST = 0, int WGS = 16,
+template <int D, bool GRP, bool NTH = false, int PF = 0, bool BUD = false, int UNR = 2, int ST = 0, int WGS = 32,
           int WM = 0>
 __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_walk_count(
     const uint8_t* __restrict__ in, const gevws_conn_in* __restrict__ conns, uint32_t n,
@@ -1420,14 +1440,11 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_buf(const uint8_t* __restr
     uint64_t ebase = 0, ecap = 0;
     bool rec = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
     WalkEntry* sink = entries + n_entries + c;
-    WalkEntry g0 = {0, 0, 0, 0}, g1 = g0, g2 = g0;
+    WalkEntry g0 = {0, 0}, g1 = g0, g2 = g0;
     auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
+      (void)p;
       rec = rec && nf < ecap;
-      WalkEntry e;
-      e.pos = (uint32_t)p;
-      e.mask = key;
-      e.len = (uint32_t)L;
-      e.meta = meta;
+      const WalkEntry e = make_entry(key, L, meta);
       if constexpr (GRP) {
         if (rec && (nf & 3) == 3) {
           WalkEntry* g = entries + ebase + (nf - 3);
@@ -1607,7 +1624,7 @@ __global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __
       __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave reads other lanes' words next
     };
     // entries: entry i sits in lane i % 64 until its group of 64 is stored
-    WalkEntry my = {0, 0, 0, 0};
+    WalkEntry my = {0, 0};
     uint64_t flushed = 0;  // entries [0, flushed) are stored
     auto flush = [&]() {
       if (rec && nf > flushed) {
@@ -1619,7 +1636,8 @@ __global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __
     };
     auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
       rec = rec && nf < ecap;
-      if (lane == (uint32_t)(nf & 63)) my = WalkEntry{(uint32_t)p, key, (uint32_t)L, meta};
+      (void)p;
+      if (lane == (uint32_t)(nf & 63)) my = make_entry(key, L, meta);
       ++nf;
       pb += round16(L);
       pl += L;
@@ -1657,7 +1675,7 @@ __global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __
         if (k > 0) {
           flush();  // the buffered group goes out before the direct stores
           rec = rec && nf + k <= ecap;
-          if (rec && lane < k) entries[ebase + nf + lane] = WalkEntry{(uint32_t)q, k2, (uint32_t)L2, m2};
+          if (rec && lane < k) entries[ebase + nf + lane] = make_entry(k2, L2, m2);
           const uint64_t add_pb = wave_sum(lane < k ? round16(L2) : 0);
           const uint64_t add_pl = wave_sum(lane < k ? L2 : 0);
           nf += k;
@@ -1931,10 +1949,55 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
 template <bool NT>
 __device__ __forceinline__ WalkEntry ld_entry(const WalkEntry* p) {
   if constexpr (NT) {
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    return WalkEntry{v[0], v[1], v[2], v[3]};
+    const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+    return WalkEntry{(uint32_t)v, (uint32_t)(v >> 32)};
   } else {
     return *p;
+  }
+}
+
+// Segmented inclusive wave scan: a segment starts at every lane with head set
+// (and at lane 0).  Every lane must take part.
+__device__ __forceinline__ uint64_t wave_seg_scan(uint64_t v, bool head) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t vu = __shfl_up(v, d, 64);
+    const bool hu = __shfl_up((int)head, d, 64) != 0;
+    if (lane >= d && !head) {
+      v += vu;
+      head = hu;
+    }
+  }
+  return v;
+}
+
+// One round of entries (lane = frame): each frame's payload length L and the
+// segmented inclusive prefix `ip` of the frame sizes (hlen + L), so a frame
+// starts at (its row's position carry) + ip - (hlen + L).  Escaped lengths
+// (>= kLenEsc) are re-read from the header, lowest lane first: every frame
+// before it in its row is then resolved, so its position is exact.  `head`:
+// the lane starts a row in this round; pbase / coff: the position carry and
+// input offset of the lane's row (every lane must take part: shuffles).
+__device__ __forceinline__ void entry_round(const uint8_t* __restrict__ in, const WalkEntry& q, bool valid, bool head,
+                                            uint64_t pbase, uint64_t coff, uint64_t& L, uint64_t& ip) {
+  L = valid ? entry_len21(q) : 0;
+  bool esc = valid && L == kLenEsc;
+  uint64_t fsz = (valid && !esc) ? entry_hlen(q) + L : 0;
+  ip = wave_seg_scan(fsz, head);
+  for (;;) {
+    const uint64_t m = __ballot(esc);
+    if (m == 0) break;  // wave-uniform
+    if ((threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) {
+      uint64_t lo, hi;
+      load_window(in + coff + pbase + ip, lo, hi);  // (fsz == 0: ip is the frame's start)
+      DevHdr h;
+      parse_header(lo, hi, ~0ull, h);  // parsed by the walk: complete
+      L = h.length;
+      fsz = h.hlen + L;
+      esc = false;
+    }
+    ip = wave_seg_scan(fsz, head);
   }
 }
 
@@ -1966,30 +2029,36 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
   const bool unordered = (sum->flags & GEVWS_SUMMARY_UNORDERED) != 0;  // entry runs may collide: unused
   const int lane = threadIdx.x & 63;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kWalkBlock / 64);
-  auto record = [&](const WalkEntry& q, uint64_t f, uint64_t poff, uint64_t coff) {
+  // the record of entry q: payload length L, frame f, payload offset poff,
+  // header at input offset hpos
+  auto record = [&](const WalkEntry& q, uint64_t L, uint64_t f, uint64_t poff, uint64_t hpos) {
     DevHdr h;
-    h.b0 = q.meta & 0xff;
-    h.masked = (q.meta >> 8) & 1;
-    h.hlen = q.meta >> 16;
+    h.b0 = q.w & 0xff;
+    h.masked = (q.w >> 8) & 1;
+    h.hlen = entry_hlen(q);
     h.mask = q.mask;
-    h.length = q.len;
-    emit_record<NTR>(frames, tile_first, f, poff, coff + q.pos + h.hlen, h);
+    h.length = L;
+    emit_record<NTR>(frames, tile_first, f, poff, hpos + h.hlen, h);
   };
   // the per-connection rounds (64 entries per round, U rounds per load)
   auto one_conn = [&](uint64_t cnt, uint64_t first_frame, uint64_t payload_base, uint64_t coff, uint64_t ebase) {
     const WalkEntry* ce = entries + ebase;
-    uint64_t carry = payload_base;
+    uint64_t carry = payload_base, pcarry = 0;
     auto round = [&](const WalkEntry& q, uint64_t r0) {
       const uint64_t k = r0 + lane;
       const bool valid = k < cnt;
-      const uint64_t padded = valid ? round16(q.len) : 0;
+      uint64_t L, ip;
+      entry_round(in, q, valid, lane == 0, pcarry, coff, L, ip);
+      const uint64_t fsz = valid ? entry_hlen(q) + L : 0;
+      const uint64_t padded = valid ? round16(L) : 0;
       const uint64_t incl = wave_incl_scan(padded);
-      if (valid) record(q, first_frame + k, carry + incl - padded, coff);
+      if (valid) record(q, L, first_frame + k, carry + incl - padded, coff + pcarry + ip - fsz);
       carry += __shfl(incl, 63, 64);
+      pcarry += __shfl(ip, 63, 64);
     };
     if (U == 1 || cnt <= 64) {  // wave-uniform
       for (uint64_t k0 = 0; k0 < cnt; k0 += 64) {
-        WalkEntry q = {0, 0, 0, 0};
+        WalkEntry q = {0, 0};
         if (k0 + lane < cnt) q = ld_entry<NTR>(ce + k0 + lane);
         round(q, k0);
       }
@@ -2050,41 +2119,39 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
         jr[r] = lo;
         kr[r] = t - __shfl(tstart, (int)lo, 64);
         const uint64_t eb = __shfl(ebase, (int)lo, 64);  // (outside the t < T branch: see below)
-        q[r] = WalkEntry{0, 0, 0, 0};
+        q[r] = WalkEntry{0, 0};
         if (t < T) q[r] = ld_entry<NTR>(entries + eb + kr[r]);
       }
-      uint64_t carry = 0;  // lane j: its connection's padded bytes already placed
+      // lane j: its connection's padded bytes and stream bytes already placed
+      uint64_t carry = 0, pcarry = 0;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if ((uint64_t)r * 64 >= T) break;  // wave-uniform
         const uint64_t t = (uint64_t)r * 64 + lane;
         const bool valid = t < T;
         const uint32_t j = jr[r];
-        const uint64_t padded = valid ? round16(q[r].len) : 0;
-        // segmented inclusive scan: a segment starts at a connection's first
-        // frame and at lane 0
-        uint64_t v = padded;
-        bool head = kr[r] == 0 || lane == 0;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint64_t vu = __shfl_up(v, d, 64);
-          const bool hu = __shfl_up((int)head, d, 64) != 0;
-          if (lane >= d && !head) {
-            v += vu;
-            head = hu;
-          }
-        }
+        // a segment starts at a connection's first frame and at lane 0
+        const bool head = kr[r] == 0 || lane == 0;
         // every __shfl runs with the whole wave active: a ds_bpermute reads
         // nothing from a lane masked off by a branch (here: lane j of a
         // connection whose frames are all taken, in a round's short tail)
-        const uint64_t cj = __shfl(carry, (int)j, 64);
+        const uint64_t cj = __shfl(carry, (int)j, 64), pcj = __shfl(pcarry, (int)j, 64);
         const uint64_t fj = __shfl(ff, (int)j, 64), pj = __shfl(pbase, (int)j, 64), oj = __shfl(coff, (int)j, 64);
-        if (valid) record(q[r], fj + kr[r], pj + cj + v - padded, oj);
+        uint64_t L, ip;
+        entry_round(in, q[r], valid, head, pcj, oj, L, ip);
+        const uint64_t fsz = valid ? entry_hlen(q[r]) + L : 0;
+        const uint64_t padded = valid ? round16(L) : 0;
+        const uint64_t v = wave_seg_scan(padded, head);
+        if (valid) record(q[r], L, fj + kr[r], pj + cj + v - padded, oj + pcj + ip - fsz);
         // lane j adds its connection's bytes in this round (from the lane of its last frame here)
         const uint64_t r0 = (uint64_t)r * 64, r1 = r0 + 64;
         const uint64_t a = tstart > r0 ? tstart : r0, b = inc < r1 ? inc : r1;
-        const uint64_t got = __shfl(v, (int)((b > a ? b - 1 : r0) - r0), 64);
-        if (lane < G && b > a) carry += got;
+        const int src = (int)((b > a ? b - 1 : r0) - r0);
+        const uint64_t got = __shfl(v, src, 64), gotp = __shfl(ip, src, 64);
+        if (lane < G && b > a) {
+          carry += got;
+          pcarry += gotp;
+        }
       }
     }
     // phase 2: connections of more than kShort frames, one wave per
@@ -4787,12 +4854,12 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     const bool many = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
     const bool grp = wv == 4 || ((wv == 0 || wv == 1 || wv == 5 || wv == 8 || wv == 9 || wv >= 10) && many);
     if (wv >= 15 && wv <= 20) {
-      (wv == 15   ? k_walk_count<0, false, false, 0, false, 2, 2, 16>
-       : wv == 16 ? k_walk_count<8, false, false, 0, false, 2, 2, 16>
-       : wv == 17 ? k_walk_count<0, false, false, 0, false, 2, 2, 4>
-       : wv == 18 ? k_walk_count<0, false, false, 0, false, 2, 2, 8>
-       : wv == 19 ? k_walk_count<0, false, false, 0, false, 2, 2, 16, 1>
-                  : k_walk_count<0, false, false, 0, false, 2, 2, 16, 2>)
+      (wv == 15   ? k_walk_count<0, false, false, 0, false, 2, 2, 32>
+       : wv == 16 ? k_walk_count<8, false, false, 0, false, 2, 2, 32>
+       : wv == 17 ? k_walk_count<0, false, false, 0, false, 2, 2, 8>
+       : wv == 18 ? k_walk_count<0, false, false, 0, false, 2, 2, 16>
+       : wv == 19 ? k_walk_count<0, false, false, 0, false, 2, 2, 32, 1>
+                  : k_walk_count<0, false, false, 0, false, 2, 2, 32, 2>)
           <<<nblk, 2 * kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb,
                                              in_bytes, done, max_frames, payload_cap, d_summary, ~0ull, 1u, nullptr,
                                              nullptr, nullptr, nullptr, nullptr);
@@ -4854,7 +4921,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
       // LDS ring in whole 256-byte groups instead (C4 1.41 ms, its 2-way
       // share 0.94 -> 0.87, C1-shaped 0.042 -> 0.038;
       // profiles/r03_walk_writer_grp_ab.jsonl)
-      (plain ? k_walk_count<0, false, false, 0, false, 2, 2, 16> : k_walk_count<8, false, false, 0, false, 2, 2, 16>)
+      (plain ? k_walk_count<0, false, false, 0, false, 2, 2, 32> : k_walk_count<8, false, false, 0, false, 2, 2, 32>)
           <<<nblk, 2 * kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb,
                                              in_bytes, done, max_frames, payload_cap, d_summary, ~0ull, 1u, nullptr,
                                              nullptr, nullptr, nullptr, nullptr);

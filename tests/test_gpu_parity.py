@@ -720,6 +720,56 @@ def test_emit_variants(engine):
         engine.set_tuning(_abi.TUNE_EMIT_VARIANT, 0)
 
 
+def test_escaped_entry_lengths(engine):
+    """The walk's 8-byte entries hold payload lengths below 2^21 - 1; longer
+    frames are escaped and the record pass re-reads their header at the
+    position its prefix sum gives.  Frames at 2^21 - 2, 2^21 - 1, 2^21 and
+    3 MiB, alone, back to back (several escapes in one round of 64 entries),
+    first and last on their connection, among small frames, on short
+    connections (the grouped pass) and long ones (per connection), through
+    every record pass, the plain and writer walks, the split walk and the
+    budgeted walk's resumption -- bit-exact against the C oracle."""
+    from gev_amd import _abi
+    rng = np.random.default_rng(0xE5C)
+    esc = (1 << 21) - 1
+    bigs = [esc - 1, esc, esc + 1, 3 << 20]
+
+    def fr(L, form=None):
+        return wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), int(rng.choice([1, 2, 0])), True, 0,
+                               bool(rng.random() < 0.8), bytes(rng.integers(0, 256, 4, dtype=np.uint8)), form)
+
+    def small(n):
+        return b"".join(fr(int(rng.integers(0, 200))) for _ in range(n))
+
+    streams = [
+        fr(esc),                                        # alone
+        fr(esc - 1) + fr(esc) + fr(esc + 1),            # back to back
+        small(3) + fr(3 << 20) + small(2),              # short connection, escape in the middle
+        fr(esc + 1) + small(40) + fr(esc) + small(30),  # long connection (> 16 frames)
+        small(70) + fr(bigs[int(rng.integers(0, 4))]) + fr(esc) + small(5) + fr(esc, 64)[:-3],  # + cut tail
+        small(130) + fr(esc + 7) + small(1),            # escape in the third round of 64
+        fr(500, 64) + fr(esc + 2) + fr(esc + 3) + fr(esc + 4) + fr(9),
+    ]
+    streams += [small(int(rng.integers(0, 20))) + fr(bigs[i % 4]) + small(int(rng.integers(0, 90)))
+                for i in range(6)]
+    arena, conns = pack_streams(streams)
+    knobs = [(_abi.TUNE_EMIT_VARIANT, v) for v in (0, 1, 2, 3)]
+    knobs += [(_abi.TUNE_WALK_VARIANT, v) for v in (1, 3, 4, 15, 16, 17, 18)]
+    knobs += [(_abi.TUNE_SPLIT_LANES, k) for k in (2, 4, 16)]
+    knobs += [(_abi.TUNE_WALK_BUDGET, b) for b in (1, 3, 17)]
+    defaults = {_abi.TUNE_EMIT_VARIANT: 0, _abi.TUNE_WALK_VARIANT: 0, _abi.TUNE_SPLIT_LANES: 0,
+                _abi.TUNE_WALK_BUDGET: -1}
+    try:
+        assert_matches_oracle(engine, arena, conns, "default")
+        for knob, val in knobs:
+            engine.set_tuning(knob, val)
+            assert_matches_oracle(engine, arena, conns, f"knob {knob} = {val}")
+            engine.set_tuning(knob, defaults[knob])
+    finally:
+        for knob, val in defaults.items():
+            engine.set_tuning(knob, val)
+
+
 def test_walk_variant_knob_bounds(engine):
     from gev_amd import _abi
     with pytest.raises(ValueError):
