@@ -99,7 +99,8 @@ ZERO_COPY_MAX_DEFAULT = 256 * 1024  # GEVWS_ZERO_COPY_MAX_DEFAULT
 class ProtocolStats(ctypes.Structure):
     _fields_ = [("device_passes", ctypes.c_uint64), ("conns_staged", ctypes.c_uint64),
                 ("bytes_staged", ctypes.c_uint64), ("gated", ctypes.c_uint64),
-                ("zero_copy_passes", ctypes.c_uint64), ("handler_passes", ctypes.c_uint64)]
+                ("zero_copy_passes", ctypes.c_uint64), ("handler_passes", ctypes.c_uint64),
+                ("chained_handler_passes", ctypes.c_uint64)]
 
 
 class HostConn(ctypes.Structure):

@@ -2004,6 +2004,9 @@ __device__ __forceinline__ void entry_round(const uint8_t* __restrict__ in, cons
 constexpr int kEmitGroup = 16;
 constexpr uint64_t kEmitSplitPerCU = 32;  // record-pass workgroups per CU over k_walk_split's rows
 // NTR (measurement): the entry loads and record stores non-temporal.
+// (Measured and not kept: phase 2 software-pipelined, the next batch's entry
+// loads issued before this batch's rounds -- C4 0.448 -> 0.477 ms, 8-way share
+// 0.094 -> 0.108: the record pass is not bound by its entry loads' latency.)
 template <int U, int G = 0, bool NTR = false>
 __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restrict__ in,
                                                           const gevws_conn_in* __restrict__ conns, uint32_t n,
@@ -2176,11 +2179,15 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
         pbase = o.payload_base;
         coff = ci.off;
       }
-      for (uint64_t j = 0; j < GL; ++j) {  // wave-uniform
-        const uint64_t cnt = uniform64(__shfl(nf, (int)j, 64));
-        const uint64_t fj = uniform64(__shfl(ff, (int)j, 64)), pj = uniform64(__shfl(pbase, (int)j, 64));
-        const uint64_t oj = uniform64(__shfl(coff, (int)j, 64)), ej = uniform64(__shfl(ebase, (int)j, 64));
-        if (cnt) one_conn(cnt, fj, pj, oj, ej);
+      // the group's connections with long chains (a ballot: groups of only
+      // short or empty connections -- all of C1's -- cost one instruction;
+      // C1's record pass 0.030 -> 0.025 ms, profiles/r03_emit_pf_ab.jsonl)
+      for (uint64_t m = __ballot(lane < GL && nf > 0); m; m &= m - 1) {  // wave-uniform
+        const int j = __builtin_ctzll(m);
+        const uint64_t cnt = uniform64(__shfl(nf, j, 64));
+        const uint64_t fj = uniform64(__shfl(ff, j, 64)), pj = uniform64(__shfl(pbase, j, 64));
+        const uint64_t oj = uniform64(__shfl(coff, j, 64)), ej = uniform64(__shfl(ebase, j, 64));
+        one_conn(cnt, fj, pj, oj, ej);
       }
     }
   } else {
@@ -3746,8 +3753,13 @@ __device__ __forceinline__ void win_store(u32x4 v, u32x4* p) {
 // 10.70 -> 9.11 ms (profiles/r02_encode_pmc_split_c4*.json,
 // r02_encode_ab_g64_*.json); plain stores recovered part of it by merging
 // the pieces in L2 (10.24 ms) at 2 GB more reads.
+// EO (with HL, COMPACT): the interior chunks are stored only after the queue
+// barrier and the lane's first queued chunk has been assembled, so the
+// interior loads (issued before the barrier) and the first assembly's loads
+// are in flight together -- one exposed payload latency per window instead of
+// two.
 template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false, bool HL = false,
-          bool WNT = true, bool G64 = false, bool NTA = false, bool NTW = false>
+          bool WNT = true, bool G64 = false, bool NTA = false, bool NTW = false, bool EO = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
@@ -3897,6 +3909,38 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
           for (int u = 0; u < kWinTiles; ++u)
             if (queued & (1u << u))
               s_bnd[atomicAdd(&s_nb, 1u)] = ((uint32_t)(u * (int32_t)kTile + (int32_t)lane_off) >> 4) | (qlo[u] << 16);
+        }
+        if constexpr (EO) {
+          __syncthreads();  // the queue is complete
+          const uint32_t nb = s_nb;
+          const uint32_t i0 = fresh_tid();
+          u32x4 x0 = u32x4{0, 0, 0, 0};
+          uint32_t q0 = 0xffffffffu;
+          if (i0 < nb) {
+            q0 = s_bnd[i0];
+            if (!(G64 && q0 == 0xffffffffu)) {
+              const int32_t rel = (int32_t)((q0 & 0xffffu) << 4);
+              x0 = enc_assemble2<LH>(rel, wbase + (uint64_t)rel, total, q0 >> 16, (uint32_t)F, s_start, s_pend,
+                                     s_hlen, s_delta, s_h0, s_h1, payload, fr, f_lo);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < kWinTiles; ++u)
+            if (interior & (1u << u))
+              win_store<WNT>(v[u], reinterpret_cast<u32x4*>(out + wbase + u * kTile + fresh_tid() * 16));
+          if (q0 != 0xffffffffu)
+            win_store<WNT>(x0, reinterpret_cast<u32x4*>(out + wbase + (uint64_t)((q0 & 0xffffu) << 4)));
+          for (uint32_t i = i0 + kUnmaskBlock; i < nb; i += kUnmaskBlock) {
+            const uint32_t q = s_bnd[i];
+            if (G64 && q == 0xffffffffu) continue;
+            const int32_t rel = (int32_t)((q & 0xffffu) << 4);
+            const uint64_t a = wbase + (uint64_t)rel;
+            win_store<WNT>(enc_assemble2<LH>(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta,
+                                             s_h0, s_h1, payload, fr, f_lo),
+                           reinterpret_cast<u32x4*>(out + a));
+          }
+          t += wt;
+          continue;
         }
 #pragma unroll
         for (int u = 0; u < kWinTiles; ++u)
@@ -4307,7 +4351,8 @@ struct gevws_ctx {
                            // per CU); 4 = queued boundary chunks, LDS-light (round-1 default);
                            // 5 = 4 + loads before stores; 6 = 5 with plain window stores; 7 = 0 with
                            // plain window stores; 8 = 0 with plain (not non-temporal) streaming loads
-  int emit_variant = 0;    // 0 = grouped record pass (k_walk_emit G = 16), 1 = one wave per connection
+  int emit_variant = 0;    // 0 = grouped record pass (k_walk_emit G = 16), 1 = one wave per connection,
+                           // 2 = 0 non-temporal, 3 = 0 with 8 rounds per load
   uint64_t small_bytes = kSmallBytes;  // one-launch decode (k_decode_small) up to this many input bytes
   uint32_t span_conns_per_cu = 0;  // walk variant 0: one wave per connection up to this many per CU
   // the split walk's history: the last multi-kernel decode's frame / payload
@@ -4573,7 +4618,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->unmask_grid = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_ENCODE_VARIANT:
-      if (value < 0 || value > 9) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 10) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_EMIT_VARIANT:
@@ -5045,6 +5090,7 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
              : ctx->encode_variant == 7 ? k_encode<4, true, true, true, 7, true, true, false, true>
              : ctx->encode_variant == 8 ? k_encode<4, true, true, true, 7, true, true, true, true>
              : ctx->encode_variant == 9 ? k_encode<4, true, true, true, 7, true, true, true, true, true, true>
+             : ctx->encode_variant == 10 ? k_encode<4, true, true, true, 7, true, true, true, true, true, false, true>
                                         : k_encode<4, true, true, true, 7, true, true, true, true, true>;
   // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
   // workgroups per CU (the rest return at once), the window path gets 7

@@ -280,6 +280,7 @@ class Protocol {
     pend_.conns.assign(conns, conns + n);
     pend_.rings.assign(rings, rings + n);
     if (sg.zc) {
+      if (handler_ >= 0 && (r = ChainHandler(&sg)) < 0) return r;
       pend_.arena = sg.arena;
     } else {
       // frames + payload land in pinned memory with the summary: one
@@ -323,7 +324,7 @@ class Protocol {
           return fail();
       }
     }
-    if (handler_ >= 0) {
+    if (handler_ >= 0 && !ChainedDone(&sg)) {
       const int64_t h = RunHandler(&sg, arena);
       if (h < 0) return h;
     }
@@ -452,6 +453,57 @@ class Protocol {
     }
   };
 
+  // A zero-copy pass with the handler on: the handler step (dispatch +
+  // FrameToBytes, counts read on the device from the decode's summary) is
+  // enqueued right behind the decode, sized for the most the staged bytes can
+  // hold -- <= max_frames frames, payload <= the staged bytes, the close
+  // bodies' aux region after payload_cap in the pass's mapped arena -- so the
+  // pass has ONE synchronisation instead of two.  When the decode had to be
+  // re-run (capacity) or the step reports a capacity miss, RunHandler runs it
+  // again with the exact sizes.
+  static uint64_t ChainAuxSlots(const Staged& sg) { return std::min<uint64_t>(std::max<uint64_t>(sg.max_frames, 1), 4096); }
+  static uint64_t ChainArenaBytes(const Staged& sg) {
+    return ((sg.payload_cap + 15) & ~15ull) + 128 * ChainAuxSlots(sg) + 32;
+  }
+  int64_t ChainHandler(Staged* sg) {
+    const uint64_t n = std::max<uint64_t>(sg->max_frames, 1);
+    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+    const uint64_t aux_off = (sg->payload_cap + 15) & ~15ull;
+    const uint64_t rcap = sg->total + 141 * n + 16;
+    if (!grow_host(&h_rof_, &h_rof_cap_, 8 * n) || !grow_host(&h_roff_, &h_roff_cap_, 8 * n) ||
+        !grow_host(&h_hs_, &h_hs_cap_, 2 * sizeof(gevws_summary)) || !grow_dev(&d_rep_, &d_rep_cap_, 32 * n))
+      return fail();
+    sg->hd = Handled{};
+    sg->hd.rbuf = pool_->Acquire(rcap + GEVWS_OUT_PAD);
+    if (!sg->hd.rbuf || sg->arena_cap < ChainArenaBytes(*sg)) return fail();
+    const gevws_frame* dfr = (const gevws_frame*)device_of(h_out_);
+    const gevws_summary* dsum = (const gevws_summary*)device_of(h_res_);
+    uint8_t* dpay = (uint8_t*)device_of(sg->arena.get());
+    gevws_summary* dhs = (gevws_summary*)device_of(h_hs_);
+    int64_t* drof = (int64_t*)device_of(h_rof_);
+    uint64_t* droff = (uint64_t*)device_of(h_roff_);
+    uint8_t* drb = (uint8_t*)device_of(sg->hd.rbuf.get());
+    if (!dfr || !dsum || !dpay || !dhs || !drof || !droff || !drb) return fail();
+    if (gevws_dispatch_decoded_async(ctx_, st, dfr, n, dsum, handler_, dpay, aux_off, 128 * ChainAuxSlots(*sg),
+                                     (gevws_out_frame*)d_rep_, drof, dhs) != GEVWS_OK ||
+        gevws_encode_replies_async(ctx_, st, (const gevws_out_frame*)d_rep_, n, dhs, dpay, drb, rcap, droff,
+                                   dhs + 1) != GEVWS_OK)
+      return fail();
+    sg->hd.chained = true;
+    ++stats_.chained_handler_passes;
+    return 0;
+  }
+  // After Finish: did the chained step answer this pass?
+  bool ChainedDone(Staged* sg) {
+    if (!sg->hd.chained || sg->retried) return false;
+    memcpy(&sg->hd.disp, h_hs_, sizeof(gevws_summary));
+    memcpy(&sg->hd.enc, h_hs_ + sizeof(gevws_summary), sizeof(gevws_summary));
+    if (sg->hd.disp.status != GEVWS_OK || sg->hd.enc.status != GEVWS_OK) return false;
+    sg->hd.done = true;
+    ++stats_.handler_passes;
+    return true;
+  }
+
   // After the decode of sg finished (its frames in the pass's outputs: device
   // memory, or mapped host memory for a zero-copy pass): the handler step,
   // sized exactly from the decode's summary, then one synchronisation.  The
@@ -569,6 +621,7 @@ class Protocol {
   // the reply bytes in a pool buffer the delivered frames hold.
   struct Handled {
     bool done = false;
+    bool chained = false;  // enqueued behind the decode (ChainHandler)
     gevws_summary disp{}, enc{};
     std::shared_ptr<uint8_t> rbuf;
   };
@@ -636,9 +689,10 @@ class Protocol {
       const uint32_t m = (uint32_t)sg->cin.size();
       if (!grow_host(&h_out_, &h_out_cap_, std::max<uint64_t>(sg->max_frames, 1) * sizeof(gevws_frame)))
         return fail();
-      if (!sg->arena || sg->arena_cap < sg->payload_cap + 16) {
-        sg->arena = pool_->Acquire(sg->payload_cap + 16);
-        sg->arena_cap = sg->payload_cap + 16;
+      const uint64_t abytes = handler_ >= 0 ? ChainArenaBytes(*sg) : sg->payload_cap + 16;
+      if (!sg->arena || sg->arena_cap < abytes) {
+        sg->arena = pool_->Acquire(abytes);
+        sg->arena_cap = abytes;
       }
       uint8_t* din = (uint8_t*)device_of(h_in_);
       uint8_t* dres = (uint8_t*)device_of(h_res_);

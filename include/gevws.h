@@ -145,7 +145,8 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * round-1 default); 5 = 4 with the loads before the stores; 6 = 5 with plain
  * (not non-temporal) window stores; 7 = 0 with plain window stores; 8 = 0 with
  * plain streaming loads -- the default's are non-temporal; 9 = 0 with
- * non-temporal window loads as well),
+ * non-temporal window loads as well; 10 = 0 with a window's interior stores
+ * issued after its first queued chunk's assembly),
  * GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
  * uniform-stream speculation, 1 = plain chain walk, 2 = plain walk that
  * records no per-frame entries, so the emit pass re-walks every chain; 0 and
@@ -495,6 +496,8 @@ typedef struct gevws_protocol_stats {
     uint64_t gated;
     uint64_t zero_copy_passes;
     uint64_t handler_passes;  /* passes that ran the device handler step */
+    uint64_t chained_handler_passes; /* of those, enqueued behind a zero-copy
+                                      * decode (one synchronisation per pass) */
 } gevws_protocol_stats;
 void gevws_protocol_get_stats(const gevws_protocol *p, gevws_protocol_stats *out);
 

@@ -47,7 +47,7 @@ def test_encode_golden(engine, golden):
     assert np.array_equal(got, g["wire"])
 
 
-ENC_VARIANTS = list(range(10))
+ENC_VARIANTS = list(range(11))
 
 
 @pytest.mark.parametrize("variant", ENC_VARIANTS)
@@ -61,7 +61,8 @@ def test_encode_random_and_tiny_frames(engine, variant):
     LDS-light (round-1 default); 5: 4 + loads before stores; 6: 5 with plain
     window stores; 7: 0 with plain window stores; 8: 0 with plain streaming
     loads (the default's are non-temporal); 9: 0 with non-temporal window
-    loads."""
+    loads; 10: 0 with the interior stores after the first queued chunk's
+    assembly (both loads in flight together)."""
     from gev_amd import _abi
     engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, variant)
     try:

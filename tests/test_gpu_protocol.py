@@ -506,7 +506,50 @@ def test_device_handler_replies_match_oracle(engine, policy, zero_copy_max):
             assert rep == wrep and shut == wshut, (fr.header, fr.payload[:16], rep, wrep)
             n += 1
     assert n > 500
-    assert proto.stats()["handler_passes"] > 0
+    st = proto.stats()
+    assert st["handler_passes"] > 0
+    # zero-copy passes chain the handler behind the decode (one synchronisation)
+    assert (st["chained_handler_passes"] > 0) == (zero_copy_max > 0)
+
+
+def _handler_pass_matches_oracle(engine, proto, streams, policy):
+    conns = [gev_amd.Connection() for _ in streams]
+    rings = [gev_amd.RingBuffer(len(s) + 16) for s in streams]
+    for r, s in zip(rings, streams):
+        r.write(s)
+    proto.unpacket_batch(conns, rings)
+    n = 0
+    for c, r, s in zip(conns, rings, streams):
+        want = wo.decode_stream(s).frames
+        for fr in want:
+            h, data = proto.unpacket(c, r)
+            assert h is not None and h.opcode == fr.header.opcode and data == fr.payload
+            assert proto.reply(c) == wo.on_message(fr.header, fr.payload, policy)
+            n += 1
+        assert proto.unpacket(c, r)[0] is None
+    return n
+
+
+def test_chained_handler_falls_back_exactly(engine):
+    """The chained handler step is sized from the staged bytes; when that
+    guess is wrong the pass re-runs the step with the exact sizes: (1) a
+    zero-copy decode that misses its frame estimate (1 000 empty frames: the
+    decode itself re-runs, the chained step saw a failed decode), (2) more
+    close frames in one pass than the 4 096 aux slots the chain reserves.
+    Replies equal oracle/ws_oracle.on_message's either way."""
+    policy = wo.HANDLER_ECHO_TEXT
+    proto = gev_amd.Protocol(engine)
+    proto.set_zero_copy_max(1 << 30)
+    proto.set_handler(policy)
+    key = b"\x0a\x0b\x0c\x0d"
+    empties = b"".join(wo.encode_frame(b"", wo.OP_TEXT, True, 0, True, key) for _ in range(1000))
+    n = _handler_pass_matches_oracle(engine, proto, [empties, empties[:600]], policy)
+    assert n == 1100
+    body = (1000).to_bytes(2, "big") + b"r" * 121
+    closes = b"".join(wo.encode_frame(body, wo.OP_CLOSE, True, 0, True, key) for _ in range(4097))
+    assert _handler_pass_matches_oracle(engine, proto, [closes], policy) == 4097
+    st = proto.stats()
+    assert st["chained_handler_passes"] == 2 and st["handler_passes"] == 2
 
 
 def test_device_handler_off_by_default(engine):
