@@ -340,6 +340,32 @@ class Engine:
         wire, _ = self.encode(rep_host, out.payload, int(rep_host["payload_len"].sum()) + 14 * nr)
         return wire, reply_of[:n].cpu().numpy(), ds
 
+    def handle_decoded(self, out: "Batch", policy: int, max_frames: int, aux_slots: int, out_cap: int):
+        """gevws_handle_decoded_async: dispatch + encode of the replies chained
+        behind the decode with no host round trip (one launch when max_frames
+        <= 1 024).  Returns (wire device tensor, reply_of numpy, dispatch
+        summary, encode summary)."""
+        torch = _torch()
+        dev = torch.device("cuda", self.device)
+        aux_off = (out.payload.numel() - 16 - 128 * aux_slots) // 16 * 16
+        n = max(int(max_frames), 1)
+        replies = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        reply_of = torch.full((n,), -7, dtype=torch.int64, device=dev)
+        sums = torch.zeros(128, dtype=torch.uint8, device=dev)
+        wire = torch.zeros(out_cap + _abi.OUT_PAD, dtype=torch.uint8, device=dev)
+        off = torch.empty(n, dtype=torch.int64, device=dev)
+        st = lib.gevws_handle_decoded_async(self._ctx, None, out.frames.data_ptr(), int(max_frames),
+                                            out.summary.data_ptr(), int(policy), out.payload.data_ptr(), aux_off,
+                                            128 * aux_slots, replies.data_ptr(), reply_of.data_ptr(),
+                                            sums.data_ptr(), wire.data_ptr(), int(out_cap), off.data_ptr(),
+                                            sums.data_ptr() + 64)
+        if st != OK:
+            raise RuntimeError(f"gevws_handle_decoded_async: {status_string(st)}")
+        torch.cuda.synchronize(self.device)
+        ss = sums.cpu().numpy().view(SUMMARY_DTYPE)
+        nf = int(out.summary_host()["frames"])
+        return wire[: int(ss[1]["payload_bytes"])], reply_of[:nf].cpu().numpy(), ss[0], ss[1]
+
     def cipher_(self, buf, mask: bytes, offset: int = 0, nbytes: Optional[int] = None,
                 byte_offset: int = 0, stream=None) -> None:
         """ws.Cipher (cipher.go:14-53) in place on a device uint8 tensor region."""

@@ -188,6 +188,8 @@ SIGNATURES = {
     "gevws_encode_replies_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, P, P, ctypes.c_uint64, P, P]),
     "gevws_dispatch_decoded_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_int, P, ctypes.c_uint64,
                                                     ctypes.c_uint64, P, P, P]),
+    "gevws_handle_decoded_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_int, P, ctypes.c_uint64,
+                                                  ctypes.c_uint64, P, P, P, P, ctypes.c_uint64, P, P]),
     "gevws_dispatch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_int, P, ctypes.c_uint64,
                                             ctypes.c_uint64, P, P, P]),
     "gevws_cipher_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint64]),

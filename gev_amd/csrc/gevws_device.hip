@@ -3753,11 +3753,12 @@ __device__ __forceinline__ void win_store(u32x4 v, u32x4* p) {
 // 10.70 -> 9.11 ms (profiles/r02_encode_pmc_split_c4*.json,
 // r02_encode_ab_g64_*.json); plain stores recovered part of it by merging
 // the pieces in L2 (10.24 ms) at 2 GB more reads.
-// EO (with HL, COMPACT): the interior chunks are stored only after the queue
-// barrier and the lane's first queued chunk has been assembled, so the
-// interior loads (issued before the barrier) and the first assembly's loads
-// are in flight together -- one exposed payload latency per window instead of
-// two.
+// EO (with HL, COMPACT; the default since round 3): the interior chunks are
+// stored only after the queue barrier and the lane's first queued chunk has
+// been assembled, so the interior loads (issued before the barrier) and the
+// first assembly's loads are in flight together -- one exposed payload latency
+// per window instead of two.  C4 9.39 -> 9.17 ms, C2 / C5 equal
+// (profiles/r03_encode_eo_ab.jsonl; variant 10 keeps the stores before).
 template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false, bool HL = false,
           bool WNT = true, bool G64 = false, bool NTA = false, bool NTW = false, bool EO = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
@@ -4199,6 +4200,138 @@ __global__ __launch_bounds__(kWalkBlock) void k_disp_emit(const gevws_frame* __r
   }
 }
 
+
+// A live pass's handler step in ONE launch (gevws_handle_decoded_async on a
+// pass of at most kHandleSmallFrames decoded frames): k_disp_count /
+// k_disp_emit's dispatch and the encode's size / scan / FrameToBytes for the
+// replies, in one workgroup -- each step's counts by block scans, the replies'
+// wire image assembled 16 bytes per lane from an LDS table of every reply
+// (enc_assemble: headers rebuilt from the records, payloads by unaligned
+// loads).  Outputs and summaries are exactly the two-step chain's (seven
+// launches, ~5 us of GPU time each whatever their size).
+constexpr uint64_t kHandleSmallFrames = kEncWinFrames;
+__global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* __restrict__ fr, uint64_t max_frames,
+                                                            const gevws_summary* __restrict__ dec, int policy,
+                                                            uint8_t* __restrict__ payload, uint64_t aux_off,
+                                                            uint64_t aux_cap, gevws_out_frame* __restrict__ rep,
+                                                            int64_t* __restrict__ reply_of,
+                                                            gevws_summary* __restrict__ dsum, uint8_t* __restrict__ out,
+                                                            uint64_t out_cap, uint64_t* __restrict__ out_off,
+                                                            gevws_summary* __restrict__ esum) {
+  constexpr int WF = (int)kHandleSmallFrames;
+  __shared__ int32_t s_start[WF];
+  __shared__ int32_t s_pend[WF];
+  __shared__ uint8_t s_hlen[WF];
+  __shared__ uint64_t s_delta[WF];
+  __shared__ uint64_t s_h0[WF], s_h1[WF];
+  __shared__ uint32_t s_status;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t n = gated_count(max_frames, dec);
+  // 1. dispatch counts (k_disp_count + k_scan_blocks)
+  uint64_t rep_n = 0, aux_n = 0, shut_n = 0;
+  for (uint64_t f0 = 0; f0 < n; f0 += kWalkBlock) {  // workgroup-uniform
+    const uint64_t f = f0 + tid;
+    uint32_t op = 0;
+    const int k = f < n ? disp_kind(fr[f].hdr, policy, op) : 0;
+    const uint64_t v[3] = {(uint64_t)(k != 0), (uint64_t)(k == 2), (uint64_t)(k >= 2)};
+    uint64_t ex[3], tot[3];
+    block_excl_scan<kWalkBlock, 3>(v, ex, tot);
+    rep_n += tot[0];
+    aux_n += tot[1];
+    shut_n += tot[2];
+  }
+  const bool disp_ok = rep_n <= n && aux_n <= aux_cap / kAuxSlot;
+  if (tid == 0) {
+    gevws_summary sm;
+    memset(&sm, 0, sizeof(sm));
+    sm.frames = rep_n;
+    sm.payload_bytes = aux_n;
+    sm.errors = shut_n;
+    sm.status = disp_ok ? GEVWS_OK : GEVWS_ERR_CAPACITY;
+    *dsum = sm;
+  }
+  // 2. replies (k_disp_emit)
+  if (disp_ok) {
+    uint64_t c_rep = 0, c_aux = 0;
+    for (uint64_t f0 = 0; f0 < n; f0 += kWalkBlock) {
+      const uint64_t f = f0 + tid;
+      uint32_t op = 0;
+      int kind = 0;
+      gevws_frame in;
+      if (f < n) {
+        in = fr[f];
+        kind = disp_kind(in.hdr, policy, op);
+      }
+      const uint64_t v[2] = {(uint64_t)(kind != 0), (uint64_t)(kind == 2)};
+      uint64_t ex[2], tot[2];
+      block_excl_scan<kWalkBlock, 2>(v, ex, tot);
+      if (f < n) {
+        if (kind == 0) reply_of[f] = -1;
+        else disp_reply(in, kind, op, f, c_rep + ex[0], c_aux + ex[1], payload, aux_off, rep, reply_of,
+                        payload + aux_off);
+      }
+      c_rep += tot[0];
+      c_aux += tot[1];
+    }
+  }
+  __threadfence_block();  // the reply records before other lanes read them
+  __syncthreads();
+  // 3. encode sizes, wire offsets and the summary (k_enc_size + scan + k_enc_emit)
+  const uint64_t nr = disp_ok ? (rep_n < n ? rep_n : n) : 0;
+  uint64_t wire = 0, pl = 0;
+  for (uint64_t r0 = 0; r0 < nr; r0 += kWalkBlock) {
+    const uint64_t r = r0 + tid;
+    uint64_t w = 0, L = 0;
+    gevws_out_frame o;
+    if (r < nr) {
+      o = rep[r];
+      w = enc_hlen(o.hdr) + o.payload_len;
+      L = o.payload_len;
+    }
+    const uint64_t v[2] = {w, L};
+    uint64_t ex[2], tot[2];
+    block_excl_scan<kWalkBlock, 2>(v, ex, tot);
+    if (r < nr) {
+      const uint64_t oo = wire + ex[0];
+      out_off[r] = oo;
+      uint64_t lo, hi;
+      const uint32_t hl = enc_header(o.hdr, lo, hi);
+      s_start[r] = (int32_t)oo;
+      s_pend[r] = (int32_t)(oo + hl + o.payload_len);
+      s_hlen[r] = (uint8_t)hl;
+      s_delta[r] = o.payload_off - oo - hl;
+      s_h0[r] = lo;
+      s_h1[r] = hi;
+    }
+    wire += tot[0];
+    pl += tot[1];
+  }
+  if (tid == 0) {
+    gevws_summary sm;
+    memset(&sm, 0, sizeof(sm));
+    sm.frames = nr;
+    sm.payload_bytes = wire;
+    sm.payload_len = pl;
+    sm.status = wire > out_cap ? GEVWS_ERR_CAPACITY : GEVWS_OK;
+    s_status = (uint32_t)sm.status;
+    *esum = sm;
+  }
+  __syncthreads();
+  if (s_status != (uint32_t)GEVWS_OK || wire == 0) return;
+  // 4. the wire image, 16 bytes per lane (the last chunk's tail zeroed inside
+  // the GEVWS_OUT_PAD slack)
+  for (uint64_t a = (uint64_t)tid * 16; a < wire; a += (uint64_t)kWalkBlock * 16) {
+    const int32_t rel = (int32_t)a;
+    uint32_t lo = 0, hi = (uint32_t)nr - 1;  // the last reply starting at or before a
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+    }
+    const u32x4 x = enc_assemble<false>(rel, a, wire, lo, (uint32_t)nr, s_start, s_pend, s_hlen, s_delta, s_h0, s_h1,
+                                        payload, nullptr, 0);
+    __builtin_memcpy(out + a, &x, 16);
+  }
+}
 
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
 // p[i] ^= mask[(offset + i) & 3] for i in [0, n): 16-byte aligned chunks of the
@@ -5090,8 +5223,8 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
              : ctx->encode_variant == 7 ? k_encode<4, true, true, true, 7, true, true, false, true>
              : ctx->encode_variant == 8 ? k_encode<4, true, true, true, 7, true, true, true, true>
              : ctx->encode_variant == 9 ? k_encode<4, true, true, true, 7, true, true, true, true, true, true>
-             : ctx->encode_variant == 10 ? k_encode<4, true, true, true, 7, true, true, true, true, true, false, true>
-                                        : k_encode<4, true, true, true, 7, true, true, true, true, true>;
+             : ctx->encode_variant == 10 ? k_encode<4, true, true, true, 7, true, true, true, true, true>
+                                         : k_encode<4, true, true, true, 7, true, true, true, true, true, false, true>;
   // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
   // workgroups per CU (the rest return at once), the window path gets 7
   const uint32_t big = per_cu > 4 && grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
@@ -5155,6 +5288,33 @@ int gevws_dispatch_decoded_async(gevws_ctx* ctx, void* stream, const gevws_frame
   if (!d_decoded) return GEVWS_ERR_INVALID;
   return dispatch_impl(ctx, stream, d_frames, max_frames, d_decoded, policy, d_payload, aux_off, aux_cap, d_replies,
                        d_reply_of, d_summary);
+}
+
+int gevws_handle_decoded_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t max_frames,
+                               const gevws_summary* d_decoded, int policy, uint8_t* d_payload, uint64_t aux_off,
+                               uint64_t aux_cap, gevws_out_frame* d_replies, int64_t* d_reply_of,
+                               gevws_summary* d_disp_summary, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                               gevws_summary* d_enc_summary) {
+  if (!ctx || !d_decoded || !d_disp_summary || !d_enc_summary) return GEVWS_ERR_INVALID;
+  if (max_frames > kHandleSmallFrames || out_cap > 0x7fffffffull) {  // the two-step chain
+    int r = gevws_dispatch_decoded_async(ctx, stream, d_frames, max_frames, d_decoded, policy, d_payload, aux_off,
+                                         aux_cap, d_replies, d_reply_of, d_disp_summary);
+    if (r != GEVWS_OK) return r;
+    return gevws_encode_replies_async(ctx, stream, d_replies, max_frames, d_disp_summary, d_payload, d_out, out_cap,
+                                      d_out_off, d_enc_summary);
+  }
+  if (max_frames && (!d_frames || !d_payload || !d_replies || !d_reply_of || !d_out || !d_out_off))
+    return GEVWS_ERR_INVALID;
+  if (policy < GEVWS_HANDLER_NONE || policy > GEVWS_HANDLER_ECHO_TEXT) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  int r = order_after_last(ctx, st);
+  if (r != GEVWS_OK) return r;
+  k_handle_small<<<1, kWalkBlock, 0, st>>>(d_frames, max_frames, d_decoded, policy, d_payload, aux_off, aux_cap,
+                                           d_replies, d_reply_of, d_disp_summary, d_out, out_cap, d_out_off,
+                                           d_enc_summary);
+  GEVWS_HIP(hipGetLastError());
+  return mark_last(ctx, st);
 }
 
 int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t* d_src, uint64_t n,

@@ -484,10 +484,8 @@ class Protocol {
     uint64_t* droff = (uint64_t*)device_of(h_roff_);
     uint8_t* drb = (uint8_t*)device_of(sg->hd.rbuf.get());
     if (!dfr || !dsum || !dpay || !dhs || !drof || !droff || !drb) return fail();
-    if (gevws_dispatch_decoded_async(ctx_, st, dfr, n, dsum, handler_, dpay, aux_off, 128 * ChainAuxSlots(*sg),
-                                     (gevws_out_frame*)d_rep_, drof, dhs) != GEVWS_OK ||
-        gevws_encode_replies_async(ctx_, st, (const gevws_out_frame*)d_rep_, n, dhs, dpay, drb, rcap, droff,
-                                   dhs + 1) != GEVWS_OK)
+    if (gevws_handle_decoded_async(ctx_, st, dfr, n, dsum, handler_, dpay, aux_off, 128 * ChainAuxSlots(*sg),
+                                   (gevws_out_frame*)d_rep_, drof, dhs, drb, rcap, droff, dhs + 1) != GEVWS_OK)
       return fail();
     sg->hd.chained = true;
     ++stats_.chained_handler_passes;

@@ -137,7 +137,8 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * the encode kernel (0 = aligned non-temporal loads + register realign while streaming;
  * in frame windows all payload loads issued before the stores, and every
  * 64-byte group that holds a frame boundary queued whole and written by one
- * store instruction of the workgroup's assembly pass; frame headers rebuilt
+ * store instruction of the workgroup's assembly pass, a window's interior
+ * stores issued after its first queued chunk's assembly; frame headers rebuilt
  * from the records so 7 workgroups fit per CU; 1 = unaligned loads, boundary
  * chunks assembled by the lane that meets them; 2 = aligned loads, per-lane
  * assembly; 3 = boundary chunks queued alone, serialised headers kept in
@@ -146,7 +147,8 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * (not non-temporal) window stores; 7 = 0 with plain window stores; 8 = 0 with
  * plain streaming loads -- the default's are non-temporal; 9 = 0 with
  * non-temporal window loads as well; 10 = 0 with a window's interior stores
- * issued after its first queued chunk's assembly),
+ * issued before its queue pass instead of after its first queued chunk's
+ * assembly -- the default until round 3),
  * GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
  * uniform-stream speculation, 1 = plain chain walk, 2 = plain walk that
  * records no per-frame entries, so the emit pass re-walks every chain; 0 and
@@ -320,6 +322,16 @@ int gevws_dispatch_decoded_async(gevws_ctx *ctx, void *stream, const gevws_frame
 int gevws_encode_replies_async(gevws_ctx *ctx, void *stream, const gevws_out_frame *d_replies,
                                uint64_t max_replies, const gevws_summary *d_dispatched, const uint8_t *d_payload,
                                uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off, gevws_summary *d_summary);
+/* Both steps at once behind a decode: gevws_dispatch_decoded_async then
+ * gevws_encode_replies_async (same arguments, summaries and outputs).  A pass
+ * of at most 1 024 frames with out_cap < 2^31 -- a live event loop's -- runs
+ * them as ONE kernel launch (one workgroup); larger ones take the two steps'
+ * seven launches.  d_out needs GEVWS_OUT_PAD bytes of slack after out_cap. */
+int gevws_handle_decoded_async(gevws_ctx *ctx, void *stream, const gevws_frame *d_frames, uint64_t max_frames,
+                               const gevws_summary *d_decoded, int policy, uint8_t *d_payload, uint64_t aux_off,
+                               uint64_t aux_cap, gevws_out_frame *d_replies, int64_t *d_reply_of,
+                               gevws_summary *d_disp_summary, uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
+                               gevws_summary *d_enc_summary);
 
 /* Measurement helper, not on the reference path: n bytes (n % 16 == 0, d_dst
  * 16-byte aligned, d_src any alignment) copied with the unmask kernel's

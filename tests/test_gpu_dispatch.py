@@ -98,3 +98,40 @@ def test_close_reply_matrix(engine):
     want = b"".join(wo.on_message(fr.header, fr.payload, 0)[0] for fr in wo.decode_stream(s).frames)
     assert wire.cpu().numpy().tobytes() == want
     assert int(ds["errors"]) == len(frames)
+
+
+@pytest.mark.parametrize("policy,n_streams", [(gev_amd._abi.HANDLER_ECHO_TEXT, 12), (gev_amd._abi.HANDLER_NONE, 12),
+                                               (gev_amd._abi.HANDLER_ECHO_BINARY, 300)])
+def test_handle_decoded_one_launch_matches_two_steps(engine, policy, n_streams):
+    """gevws_handle_decoded_async (a live pass's handler step behind its
+    decode, no host round trip): with <= 1 024 frames it is ONE launch
+    (k_handle_small), else the dispatch + encode chain; either way the wire
+    bytes, reply_of and both summaries equal the oracle's replies and the
+    two-step path's, also with a frame bound above the decoded count."""
+    import torch
+    rng = np.random.default_rng(77 + policy + n_streams)
+    streams = [_client_stream(rng, int(rng.integers(1, 60))) for _ in range(n_streams)]
+    arena, conns = pack_streams(streams)
+    dev = torch.device("cuda", engine.device)
+    d_in = torch.zeros(len(arena) + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    d_in[: len(arena)] = torch.from_numpy(np.frombuffer(arena, np.uint8).copy()).to(dev)
+    want, shut, reps, nrep = b"", 0, [], 0
+    for s in streams:
+        for fr in wo.decode_stream(s).frames:
+            r, sd = wo.on_message(fr.header, fr.payload, policy)
+            shut += sd
+            reps.append(-1 if r is None else nrep)
+            if r is not None:
+                want += r
+                nrep += 1
+    nf = len(reps)
+    aux = max(nf, 1)
+    for bound in sorted({nf, nf + 37, nf + 1100}):  # (a bound below nf handles only its first frames)
+        out = engine.decode(d_in, len(arena), torch.from_numpy(conns.copy()).to(dev), conns.shape[0],
+                            aux_slots=aux)
+        wire, reply_of, ds, es = engine.handle_decoded(out, policy, bound, aux, len(want) + 64)
+        assert int(ds["status"]) == 0 and int(es["status"]) == 0, bound
+        assert int(ds["frames"]) == nrep and int(ds["errors"]) == shut, bound
+        assert int(es["frames"]) == nrep and int(es["payload_bytes"]) == len(want), bound
+        assert list(reply_of) == reps, bound
+        assert wire.cpu().numpy().tobytes() == want, bound

@@ -61,8 +61,9 @@ def test_encode_random_and_tiny_frames(engine, variant):
     LDS-light (round-1 default); 5: 4 + loads before stores; 6: 5 with plain
     window stores; 7: 0 with plain window stores; 8: 0 with plain streaming
     loads (the default's are non-temporal); 9: 0 with non-temporal window
-    loads; 10: 0 with the interior stores after the first queued chunk's
-    assembly (both loads in flight together)."""
+    loads; 10: 0 with the interior stores before the queue pass (the
+    default -- stores after the first queued chunk's assembly, both loads in
+    flight together -- until round 3)."""
     from gev_amd import _abi
     engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, variant)
     try:
