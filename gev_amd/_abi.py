@@ -53,6 +53,8 @@ TUNE_SPLIT_LANES = 8  # split header walk: lanes per connection (0 = auto, 1 = n
 TUNE_WALK_BUDGET = 10  # budgeted walk: frames per lane (0 = auto, -1 = never, > 0 = always)
 TUNE_RESUME_LANES = 11  # lanes per resumed connection (0 = default 8, 2/4/8/16)
 TUNE_BUDGET_FRAC = 12  # auto budget in 16ths of the previous mean chain
+TUNE_SPLIT_MIN_BYTES = 13  # split walk: bytes per segment at least (default 16 384)
+TUNE_SPLIT_LANES_PER_CU = 14  # split walk auto: lanes per CU at most (default 512)
 
 IN_PAD = 64
 SUMMARY_UNORDERED = 1  # summary.flags: connection table not in increasing input order

@@ -896,7 +896,9 @@ constexpr uint32_t kSyncWin = 256;                // bytes searched after a spli
 constexpr uint32_t kSyncRow = kSyncWin / 4 + 5;   // dwords per lane's LDS row (window + 16 B; odd stride)
 constexpr int kSyncDepth = 5;                     // consecutive plausible headers confirm a guess
 constexpr uint64_t kSplitMinBytes = 16384;        // a connection's segments are at least this long
-constexpr uint32_t kSplitMaxLanes = 16;
+constexpr uint32_t kSplitMaxLanes = 32;
+constexpr uint32_t kSplitAutoMaxLanes = 16;  // the auto choice's largest split
+constexpr uint32_t kResumeMaxLanes = 16;
 constexpr uint64_t kSplitLanesPerCU = 512;        // auto: split while the walk has fewer lanes per CU
 // auto: split only after a decode on this context whose connections averaged
 // this many frames of at most this many payload bytes (the long chains of
@@ -1063,7 +1065,8 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
                                                             uint64_t payload_cap, gevws_summary* __restrict__ sum,
                                                             gevws_conn_in* __restrict__ segs,
                                                             gevws_conn_out* __restrict__ sout,
-                                                            uint8_t* __restrict__ srec, int mode) {
+                                                            uint8_t* __restrict__ srec, int mode,
+                                                            uint64_t min_seg = kSplitMinBytes) {
   static_assert(KS >= 2 && KS <= (int)kSplitMaxLanes && (KS & (KS - 1)) == 0, "KS: a power of two");
   __shared__ uint32_t s_row[kCountBlock * kSyncRow];
   const uint32_t lane = threadIdx.x & 63, i = lane % KS;
@@ -1083,7 +1086,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
   bool found = active && i == 0;
   uint64_t b = 0;
   if (active && i > 0 && mode != 2) {  // mode 2 (measurement): no guesses
-    const uint64_t kc = ci.len / kSplitMinBytes < KS ? ci.len / kSplitMinBytes : KS;
+    const uint64_t kc = ci.len / min_seg < KS ? ci.len / min_seg : KS;
     if (i < kc) {
       // windows spread over the first half of the segment; guesses below
       // 3/4 of it, so they stay in increasing lane order
@@ -1247,7 +1250,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_resume(const uint8_t* __re
                                                              gevws_conn_in* __restrict__ segs,
                                                              gevws_conn_out* __restrict__ sout,
                                                              uint8_t* __restrict__ srec) {
-  static_assert(KS >= 2 && KS <= (int)kSplitMaxLanes && (KS & (KS - 1)) == 0, "KS: a power of two");
+  static_assert(KS >= 2 && KS <= (int)kResumeMaxLanes && (KS & (KS - 1)) == 0, "KS: a power of two");
   __shared__ uint32_t s_row[kCountBlock * kSyncRow];
   constexpr uint32_t G = kCountBlock / KS;  // connections per workgroup per round
   const uint32_t lane = threadIdx.x & 63, i = lane % KS;
@@ -3471,6 +3474,26 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
                                    sum->payload_bytes / kTile < kWideGridTiles);
 }
 
+// v5 alone at more workgroups per CU (measurement): U-tile streaming steps
+// and the register cap of WPE waves per SIMD -- a mixed-size batch's window
+// path wants more windows in flight per CU; auto5's 16-tile streaming steps
+// hold it to 4.
+template <int U, int WPE>
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_unmask_v5w(
+    const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
+  __shared__ int32_t s_lend[kWin4Frames];
+  __shared__ uint64_t s_delta[kWin4Frames];
+  __shared__ uint32_t s_key[kWin4Frames];
+  __shared__ __attribute__((aligned(16))) uint16_t s_own[2 * kWinChunks];
+  __shared__ uint32_t s_wtot[2 * (kUnmaskBlock / 64)];
+  __shared__ uint32_t s_tmap[kTmapN];
+  __shared__ uint64_t s_prof[1];
+  unmask_v5_body<U, true, 0>(in, frames, tile_first, sum, out, big_grid,
+                             WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap, s_prof},
+                             sum->payload_bytes / kTile < kWideGridTiles);
+}
+
 // ------------------------------------------------------------------ outbound encode (§8f row 1)
 // ws.WriteHeader (write.go:48-84) + ws.FrameToBytes (frame.go:274-278) for a
 // batch of frames: wire[f] = WriteHeader(hdr_f) || payload_f, frames back to
@@ -4507,6 +4530,8 @@ struct gevws_ctx {
   int64_t walk_budget = -1;
   uint32_t resume_lanes = 0;  // lanes per resumed connection (k_walk_resume): 0 = kResumeLanes
   uint32_t budget_frac16 = kBudgetFrac16;  // auto budget: this many 16ths of the previous mean chain
+  uint64_t split_min_bytes = kSplitMinBytes;        // split walk: bytes per segment at least
+  uint64_t split_lanes_per_cu = kSplitLanesPerCU;   // split walk auto: lanes per CU at most
   uint64_t last_budget = 0;  // budget of the last multi-kernel decode's walk (0 = not budgeted)
   int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
                            // 2 = plain walk without the entry table (emit re-walks); 0 and 1 store
@@ -4625,6 +4650,9 @@ const UnmaskVariant kUnmaskVariants[] = {
      "auto with v4 for mixed batches (the default until round 3: per-chunk binary searches in LDS, tile map read "
      "with scalar loads)", true},
     {k_unmask_auto5<1>, 16, "measurement: the default (v5) with its phases timed (gevws_unmask_profile)", true},
+    {k_unmask_v5w<8, 5>, 8, "v5 for every batch, 8-tile streaming steps, 5 waves per SIMD", true},
+    {k_unmask_v5w<8, 6>, 8, "v5 for every batch, 8-tile streaming steps, 6 waves per SIMD", true},
+    {k_unmask_v5w<16, 4>, 16, "v5 for every batch (the default's mixed-batch path alone)", true},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
@@ -4783,12 +4811,20 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->walk_budget = value;
       return GEVWS_OK;
     case GEVWS_TUNE_RESUME_LANES:
-      if (value < 0 || value == 1 || value > kSplitMaxLanes || (value & (value - 1))) return GEVWS_ERR_INVALID;
+      if (value < 0 || value == 1 || value > kResumeMaxLanes || (value & (value - 1))) return GEVWS_ERR_INVALID;
       ctx->resume_lanes = (uint32_t)value;
       return GEVWS_OK;
     case GEVWS_TUNE_BUDGET_FRAC:
       if (value < 1 || value > 64) return GEVWS_ERR_INVALID;
       ctx->budget_frac16 = (uint32_t)value;
+      return GEVWS_OK;
+    case GEVWS_TUNE_SPLIT_MIN_BYTES:
+      if (value < 1024 || value > (1ll << 30)) return GEVWS_ERR_INVALID;
+      ctx->split_min_bytes = (uint64_t)value;
+      return GEVWS_OK;
+    case GEVWS_TUNE_SPLIT_LANES_PER_CU:
+      if (value < 64 || value > 4096) return GEVWS_ERR_INVALID;
+      ctx->split_lanes_per_cu = (uint64_t)value;
       return GEVWS_OK;
     default:
       return GEVWS_ERR_INVALID;
@@ -4903,7 +4939,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
                ctx->stats_known &&
                ctx->prev_frames_per_conn >= kSplitMinFramesPerConn && ctx->prev_frame_bytes <= kSplitMaxFrameBytes) {
       if ((uint64_t)n_conns <= kSplitMaxConnsPerCU * ncu)
-        while (ks < kSplitMaxLanes && (uint64_t)n_conns * ks * 2 <= (uint64_t)kSplitLanesPerCU * ncu) ks *= 2;
+        while (ks < kSplitAutoMaxLanes && (uint64_t)n_conns * ks * 2 <= ctx->split_lanes_per_cu * ncu) ks *= 2;
     }
   }
   if ((uint64_t)n_conns * ks > 0xFFFFFFFFull) ks = 1;
@@ -5013,11 +5049,12 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   (grp ? k_walk_split<K, 8, true> : plain ? k_walk_split<K, 0, false> : k_walk_split<K, 8, false>)               \
       <<<nblk, kCountBlock, 0, st>>>(                                                                             \
       d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb_w, in_bytes, done, max_frames, payload_cap, \
-      d_summary, segs, sout, srec, ctx->split_mode)
+      d_summary, segs, sout, srec, ctx->split_mode, ctx->split_min_bytes)
     if (ks == 2) GEVWS_SPLIT(2);
     else if (ks == 4) GEVWS_SPLIT(4);
     else if (ks == 8) GEVWS_SPLIT(8);
-    else GEVWS_SPLIT(16);
+    else if (ks == 16) GEVWS_SPLIT(16);
+    else GEVWS_SPLIT(32);
 #undef GEVWS_SPLIT
   } else if (nblk && span) {
     if (wv == 7)

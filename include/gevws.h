@@ -171,7 +171,7 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * the segments between the guesses; a connection whose guesses do not all
  * line up is re-walked serially, so the output never depends on them): 0 =
  * auto (the batch's connections x lanes up to 256 per CU, streams of >= 32 KiB
- * mean), 1 = never, 2 / 4 / 8 / 16 = always. */
+ * mean), 1 = never, 2 / 4 / 8 / 16 / 32 = always. */
 #define GEVWS_TUNE_UNMASK_VARIANT 1
 #define GEVWS_TUNE_UNMASK_GRID 2
 #define GEVWS_TUNE_ENCODE_VARIANT 3
@@ -195,6 +195,12 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
 #define GEVWS_TUNE_WALK_BUDGET 10
 #define GEVWS_TUNE_RESUME_LANES 11  /* 0 = default (8), else 2 / 4 / 8 / 16 */
 #define GEVWS_TUNE_BUDGET_FRAC 12   /* auto budget in 16ths of the previous mean chain (default 18) */
+/* Split walk (GEVWS_TUNE_SPLIT_LANES): a connection is cut into segments of at
+ * least this many bytes (default 16 384; 1 024 .. 2^30) ... */
+#define GEVWS_TUNE_SPLIT_MIN_BYTES 13
+/* ... and the auto choice doubles the lanes per connection while the walk
+ * keeps at most this many lanes per CU (default 512; 64 .. 4 096). */
+#define GEVWS_TUNE_SPLIT_LANES_PER_CU 14
 int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
 /* Lanes per connection the last multi-kernel decode's header walk used (1 =
  * not split; GEVWS_TUNE_SPLIT_LANES), -1 for a null context.  The auto choice

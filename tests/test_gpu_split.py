@@ -102,16 +102,22 @@ def split_cases():
     return _cases()
 
 
-@pytest.mark.parametrize("lanes", [0, 2, 4, 8, 16])
-def test_split_walk_matches_oracle(engine, split_cases, lanes):
+@pytest.mark.parametrize("lanes,min_seg", [(0, 16384), (2, 16384), (4, 16384), (8, 16384), (16, 16384),
+                                           (32, 16384), (32, 4096), (16, 1024)])
+def test_split_walk_matches_oracle(engine, split_cases, lanes, min_seg):
+    """Every lane count (32: two connections per wave), and shorter minimum
+    segments (GEVWS_TUNE_SPLIT_MIN_BYTES: more guesses per connection, each
+    nearer the previous one)."""
     from gev_amd import _abi
     engine.set_tuning(_abi.TUNE_SMALL_BATCH, 0)
     engine.set_tuning(_abi.TUNE_SPLIT_LANES, lanes)
+    engine.set_tuning(_abi.TUNE_SPLIT_MIN_BYTES, min_seg)
     try:
         for name, (arena, conns) in split_cases.items():
-            assert_matches_oracle(engine, arena, conns, f"split lanes {lanes}: {name}")
+            assert_matches_oracle(engine, arena, conns, f"split lanes {lanes} min {min_seg}: {name}")
     finally:
         engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
+        engine.set_tuning(_abi.TUNE_SPLIT_MIN_BYTES, 16384)
         engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
 
 
@@ -139,10 +145,14 @@ def test_split_walk_streams_outside_the_arena(engine, split_cases):
 
 def test_split_lanes_knob_bounds(engine):
     from gev_amd import _abi
-    for bad in (-1, 3, 6, 32):
+    for bad in (-1, 3, 6, 64):
         with pytest.raises(ValueError):
             engine.set_tuning(_abi.TUNE_SPLIT_LANES, bad)
     engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
+    for knob, bad in ((_abi.TUNE_SPLIT_MIN_BYTES, 1023), (_abi.TUNE_SPLIT_LANES_PER_CU, 63),
+                      (_abi.TUNE_RESUME_LANES, 32)):
+        with pytest.raises(ValueError):
+            engine.set_tuning(knob, bad)
 
 
 def test_split_walk_auto_choice(engine, split_cases):

@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 DEFAULTS = {"WALK_BUDGET": -1, "RESUME_LANES": 0, "BUDGET_FRAC": 18, "SPLIT_LANES": 0, "WALK_VARIANT": 0,
+            "SPLIT_MIN_BYTES": 16384, "SPLIT_LANES_PER_CU": 512,
             "UNMASK_VARIANT": 0, "UNMASK_GRID": 0, "EMIT_VARIANT": 0, "SPLIT_MODE": 0}
 
 
