@@ -102,7 +102,7 @@ class ProtocolStats(ctypes.Structure):
     _fields_ = [("device_passes", ctypes.c_uint64), ("conns_staged", ctypes.c_uint64),
                 ("bytes_staged", ctypes.c_uint64), ("gated", ctypes.c_uint64),
                 ("zero_copy_passes", ctypes.c_uint64), ("handler_passes", ctypes.c_uint64),
-                ("chained_handler_passes", ctypes.c_uint64)]
+                ("chained_handler_passes", ctypes.c_uint64), ("signalled_passes", ctypes.c_uint64)]
 
 
 class HostConn(ctypes.Structure):
@@ -190,6 +190,8 @@ SIGNATURES = {
     "gevws_encode_replies_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, P, P, ctypes.c_uint64, P, P]),
     "gevws_dispatch_decoded_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_int, P, ctypes.c_uint64,
                                                     ctypes.c_uint64, P, P, P]),
+    "gevws_ctx_set_completion_flag": (ctypes.c_int, [P, P]),
+    "gevws_ctx_completion_seq": (ctypes.c_int64, [P]),
     "gevws_handle_decoded_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_int, P, ctypes.c_uint64,
                                                   ctypes.c_uint64, P, P, P, P, ctypes.c_uint64, P, P]),
     "gevws_dispatch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_int, P, ctypes.c_uint64,

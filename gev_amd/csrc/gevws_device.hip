@@ -2237,6 +2237,19 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
 // writing the records and unmasking payloads of up to kSmallLaneBytes itself
 // (all its chunk loads at once), and the workgroup unmasks the larger ones
 // together.  Output identical to the multi-kernel decode.
+// A live pass's last kernel announces its end in mapped host memory: every
+// thread's writes (records, payload, summaries) are fenced at system scope,
+// then one lane stores `seq` with a system-scope release (a vector store), so
+// a host that sees the flag sees the results -- it spins on host memory
+// instead of waiting in hipStreamSynchronize (gevws_ctx_set_completion_flag).
+// Callers reach it with the whole workgroup (it holds a barrier).
+__device__ __forceinline__ void signal_done(uint32_t* done, uint32_t seq) {
+  if (!done) return;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 constexpr uint32_t kSmallConns = 256;
 constexpr uint64_t kSmallBytes = 64 * 1024;
 constexpr uint32_t kSmallLaneBytes = 256;
@@ -2247,7 +2260,9 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
                                                               gevws_frame* __restrict__ frames, uint64_t max_frames,
                                                               uint8_t* __restrict__ payload, uint64_t payload_cap,
                                                               gevws_conn_out* __restrict__ cout,
-                                                              gevws_summary* __restrict__ sum) {
+                                                              gevws_summary* __restrict__ sum,
+                                                              uint32_t* __restrict__ done = nullptr,
+                                                              uint32_t seq = 0) {
   __shared__ uint64_t s_big[kSmallBig][3];  // {src_off, payload_off, length} of the larger payloads
   __shared__ uint32_t s_bkey[kSmallBig];
   __shared__ uint32_t s_nbig;
@@ -2301,7 +2316,10 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
     sm.status = ok ? GEVWS_OK : GEVWS_ERR_CAPACITY;
     *sum = sm;
   }
-  if (!ok) return;  // capacity error: nothing written (uniform)
+  if (!ok) {  // capacity error: nothing written (uniform)
+    signal_done(done, seq);
+    return;
+  }
   if (c < n) {
     gevws_conn_out o;
     o.first_frame = ex[0];
@@ -2361,6 +2379,7 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
       *reinterpret_cast<u32x4*>(payload + poff + 16 * j) = y;
     }
   }
+  signal_done(done, seq);
 }
 
 // ------------------------------------------------------------------ 4. unmask / compact
@@ -4240,7 +4259,9 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
                                                             int64_t* __restrict__ reply_of,
                                                             gevws_summary* __restrict__ dsum, uint8_t* __restrict__ out,
                                                             uint64_t out_cap, uint64_t* __restrict__ out_off,
-                                                            gevws_summary* __restrict__ esum) {
+                                                            gevws_summary* __restrict__ esum,
+                                                            uint32_t* __restrict__ done = nullptr,
+                                                            uint32_t seq = 0) {
   constexpr int WF = (int)kHandleSmallFrames;
   __shared__ int32_t s_start[WF];
   __shared__ int32_t s_pend[WF];
@@ -4340,7 +4361,10 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
     *esum = sm;
   }
   __syncthreads();
-  if (s_status != (uint32_t)GEVWS_OK || wire == 0) return;
+  if (s_status != (uint32_t)GEVWS_OK || wire == 0) {  // (workgroup-uniform)
+    signal_done(done, seq);
+    return;
+  }
   // 4. the wire image, 16 bytes per lane (the last chunk's tail zeroed inside
   // the GEVWS_OUT_PAD slack)
   for (uint64_t a = (uint64_t)tid * 16; a < wire; a += (uint64_t)kWalkBlock * 16) {
@@ -4354,6 +4378,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
                                         payload, nullptr, 0);
     __builtin_memcpy(out + a, &x, 16);
   }
+  signal_done(done, seq);
 }
 
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
@@ -4514,6 +4539,9 @@ struct gevws_ctx {
   // the split walk's history: the last multi-kernel decode's frame / payload
   // totals (written by k_walk_bases into mapped host memory) and its
   // connection count, read once that decode has finished
+  uint32_t* done_flag = nullptr;  // mapped host word the one-launch kernels signal (gevws_ctx_set_completion_flag)
+  uint32_t done_seq = 0;
+  int64_t last_signal = -1;  // the value the last call's last kernel stores there, -1: none
   uint64_t* h_stats = nullptr;
   uint64_t* d_stats = nullptr;
   bool stats_pending = false, stats_known = false;
@@ -4584,6 +4612,7 @@ int order_after_last(gevws_ctx* ctx, hipStream_t st) {
 }
 
 int mark_last(gevws_ctx* ctx, hipStream_t st) {
+  ctx->last_signal = -1;  // (the one-launch paths set it after this)
   GEVWS_HIP(hipEventRecord(ctx->last_done, st));
   ctx->last_stream = st;
   ctx->has_last = true;
@@ -4840,6 +4869,15 @@ const char* gevws_tuning_name(int key, int64_t value) {
 
 int gevws_ctx_last_split_lanes(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_ks : -1; }
 
+int gevws_ctx_set_completion_flag(gevws_ctx* ctx, uint32_t* d_flag) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  ctx->done_flag = d_flag;
+  ctx->last_signal = -1;
+  return GEVWS_OK;
+}
+
+int64_t gevws_ctx_completion_seq(const gevws_ctx* ctx) { return ctx ? ctx->last_signal : -1; }
+
 int64_t gevws_ctx_last_walk_budget(const gevws_ctx* ctx) { return ctx ? (int64_t)ctx->last_budget : -1; }
 
 int64_t gevws_ctx_last_resumed(gevws_ctx* ctx) {
@@ -4903,10 +4941,13 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
       ctx->unmask_variant == 0 && ctx->emit_variant == 0 && ctx->span_conns_per_cu == 0 && ctx->unmask_grid == 0) {
     int r = order_after_last(ctx, st);
     if (r != GEVWS_OK) return r;
+    const uint32_t seq = ctx->done_flag ? ++ctx->done_seq : 0u;
     k_decode_small<<<1, kSmallConns, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
-                                               payload_cap, d_conn_out, d_summary);
+                                               payload_cap, d_conn_out, d_summary, ctx->done_flag, seq);
     GEVWS_HIP(hipGetLastError());
-    return mark_last(ctx, st);
+    r = mark_last(ctx, st);
+    if (ctx->done_flag) ctx->last_signal = seq;
+    return r;
   }
   // connections per counting workgroup: 64, or fewer so a small batch covers every CU
   const uint32_t ncu = (uint32_t)ctx->num_cus;
@@ -5347,11 +5388,14 @@ int gevws_handle_decoded_async(gevws_ctx* ctx, void* stream, const gevws_frame* 
   hipStream_t st = pick_stream(ctx, stream);
   int r = order_after_last(ctx, st);
   if (r != GEVWS_OK) return r;
+  const uint32_t seq = ctx->done_flag ? ++ctx->done_seq : 0u;
   k_handle_small<<<1, kWalkBlock, 0, st>>>(d_frames, max_frames, d_decoded, policy, d_payload, aux_off, aux_cap,
                                            d_replies, d_reply_of, d_disp_summary, d_out, out_cap, d_out_off,
-                                           d_enc_summary);
+                                           d_enc_summary, ctx->done_flag, seq);
   GEVWS_HIP(hipGetLastError());
-  return mark_last(ctx, st);
+  r = mark_last(ctx, st);
+  if (ctx->done_flag) ctx->last_signal = seq;
+  return r;
 }
 
 int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t* d_src, uint64_t n,

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -629,6 +630,7 @@ class Protocol {
     uint64_t coff = 0, total = 0, res = 0, max_frames = 0, payload_cap = 0;
     bool retried = false;  // Finish re-ran the pass: copies enqueued before it are stale
     bool zc = false;       // zero-copy pass: kernels on the pinned buffers themselves
+    bool flagged = false;  // its one-launch kernels signal the protocol's flag word
     std::shared_ptr<uint8_t> arena;  // zero-copy: the payload arena the kernels write
     uint64_t arena_cap = 0;
     gevws_summary sum{};
@@ -665,6 +667,7 @@ class Protocol {
     hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
     sg->zc = allow_zc && total <= zc_max_;
     if (sg->zc) {
+      sg->flagged = EnsureFlag();  // (without it the pass synchronises the stream)
       // small pass: no copies -- the kernels read the staged bytes and write
       // records, payload and results into mapped host memory (a pass is then
       // its launches and one synchronisation, no H2D / D2H on the way)
@@ -715,11 +718,50 @@ class Protocol {
     return GEVWS_OK;
   }
 
+  // A zero-copy pass's launches end with a one-launch kernel that signals
+  // the protocol's mapped flag word (gevws_ctx_set_completion_flag): the host
+  // spins on it (~1 us after the kernel's last write) instead of sleeping in
+  // hipStreamSynchronize.  Passes with copies behind the kernels, or whose
+  // last launch does not signal, synchronise the stream.
+  // (set on the context for every zero-copy pass: another protocol on the
+  // same context may have pointed it elsewhere since)
+  bool EnsureFlag() {
+    if (!h_flag_) {
+      if (hipHostMalloc((void**)&h_flag_, 64, kHostFlags) != hipSuccess) {
+        h_flag_ = nullptr;
+        return false;
+      }
+      __atomic_store_n(h_flag_, 0u, __ATOMIC_RELEASE);
+    }
+    uint32_t* d = (uint32_t*)device_of(h_flag_);
+    if (!d || gevws_ctx_set_completion_flag(ctx_, d) != GEVWS_OK) {
+      (void)hipHostFree(h_flag_);
+      h_flag_ = nullptr;
+      return false;
+    }
+    return true;
+  }
+  int64_t Wait(const Staged* sg) {
+    const int64_t seq = (sg->zc && sg->flagged) ? gevws_ctx_completion_seq(ctx_) : -1;
+    if (seq >= 0) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (uint64_t i = 1;; ++i) {
+        if (__atomic_load_n(h_flag_, __ATOMIC_ACQUIRE) == (uint32_t)seq) {
+          ++stats_.signalled_passes;
+          return 0;
+        }
+        // a pass takes tens of us: past 50 ms, wait for the stream instead
+        if ((i & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+        __builtin_ia32_pause();
+      }
+    }
+    return hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_)) == hipSuccess ? 0 : fail();
+  }
+
   // Waits for the pass (and whatever the caller enqueued after it); on
   // GEVWS_ERR_CAPACITY runs it once more with the exact sizes.
   int64_t Finish(Staged* sg) {
-    hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
-    if (hipStreamSynchronize(st) != hipSuccess) return fail();
+    if (Wait(sg) < 0) return GEVWS_ERR_DEVICE;
     memcpy(&sg->sum, h_res_, sizeof(gevws_summary));
     if (sg->sum.status == GEVWS_ERR_CAPACITY) {
       sg->max_frames = std::max<uint64_t>(sg->sum.frames, 1);
@@ -727,7 +769,7 @@ class Protocol {
       sg->retried = true;
       int64_t r = Launch(sg);
       if (r < 0) return r;
-      if (hipStreamSynchronize(st) != hipSuccess) return fail();
+      if (Wait(sg) < 0) return GEVWS_ERR_DEVICE;
       memcpy(&sg->sum, h_res_, sizeof(gevws_summary));
     }
     return sg->sum.status == GEVWS_OK ? (int64_t)sg->sum.frames : (int64_t)sg->sum.status;
@@ -767,6 +809,11 @@ class Protocol {
   }
   void release() {
     if (ctx_) (void)hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_));
+    if (h_flag_) {
+      if (ctx_) (void)gevws_ctx_set_completion_flag(ctx_, nullptr);
+      (void)hipHostFree(h_flag_);
+      h_flag_ = nullptr;
+    }
     for (uint8_t* p : {h_in_, h_res_, h_out_, h_rof_, h_roff_, h_hs_})
       if (p) (void)hipHostFree(p);
     for (void* p : {d_in_, d_res_, d_frames_, d_payload_, d_rep_})
@@ -774,6 +821,7 @@ class Protocol {
   }
 
   gevws_ctx* ctx_;
+  uint32_t* h_flag_ = nullptr;  // completion word of the one-launch kernels (mapped pinned)
   struct Pending {  // the pass between BeginBatch and EndBatch
     bool active = false;
     std::vector<Connection*> conns;

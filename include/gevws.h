@@ -208,6 +208,17 @@ int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
  * has shown long chains of small frames (>= 256 frames per connection of <= 4
  * KiB each). */
 int gevws_ctx_last_split_lanes(const gevws_ctx *ctx);
+/* Completion signal of the one-launch kernels (a live pass's: the small-batch
+ * decode and gevws_handle_decoded_async's one-workgroup form).  With d_flag
+ * (the device address of a 32-bit word in mapped, coherent host memory) set,
+ * each such launch numbers itself and its kernel stores that number there
+ * after all its outputs are visible at system scope; a host then spins on
+ * host memory instead of hipStreamSynchronize.  NULL turns it off (the
+ * default).  gevws_ctx_completion_seq: the number the last call's last kernel
+ * stores, or -1 when that call ended with another kernel or copy (the caller
+ * synchronises the stream as usual). */
+int gevws_ctx_set_completion_flag(gevws_ctx *ctx, uint32_t *d_flag);
+int64_t gevws_ctx_completion_seq(const gevws_ctx *ctx);
 /* Frames per lane of the last multi-kernel decode's budgeted walk (0 = not
  * budgeted; -1 for a null context), and the connections it resumed (waits for
  * the context's last call; < 0 on error). */
@@ -516,6 +527,9 @@ typedef struct gevws_protocol_stats {
     uint64_t handler_passes;  /* passes that ran the device handler step */
     uint64_t chained_handler_passes; /* of those, enqueued behind a zero-copy
                                       * decode (one synchronisation per pass) */
+    uint64_t signalled_passes;       /* waits answered by the kernels' completion
+                                      * flag (gevws_ctx_set_completion_flag)
+                                      * instead of a stream synchronisation */
 } gevws_protocol_stats;
 void gevws_protocol_get_stats(const gevws_protocol *p, gevws_protocol_stats *out);
 

@@ -509,7 +509,9 @@ def test_device_handler_replies_match_oracle(engine, policy, zero_copy_max):
     st = proto.stats()
     assert st["handler_passes"] > 0
     # zero-copy passes chain the handler behind the decode (one synchronisation)
+    # and wait on the kernels' completion flag instead of the stream
     assert (st["chained_handler_passes"] > 0) == (zero_copy_max > 0)
+    assert (st["signalled_passes"] > 0) == (zero_copy_max > 0)
 
 
 def _handler_pass_matches_oracle(engine, proto, streams, policy):
@@ -550,6 +552,9 @@ def test_chained_handler_falls_back_exactly(engine):
     assert _handler_pass_matches_oracle(engine, proto, [closes], policy) == 4097
     st = proto.stats()
     assert st["chained_handler_passes"] == 2 and st["handler_passes"] == 2
+    # the first pass and its re-run decode signal (one-launch kernels); the
+    # 528 KB second pass takes the multi-kernel decode and synchronises
+    assert st["signalled_passes"] == 2
 
 
 def test_device_handler_off_by_default(engine):
