@@ -340,6 +340,21 @@ class Engine:
         wire, _ = self.encode(rep_host, out.payload, int(rep_host["payload_len"].sum()) + 14 * nr)
         return wire, reply_of[:n].cpu().numpy(), ds
 
+    def set_completion_flag(self, arena: Optional["PinnedArena"], offset: int = 0) -> None:
+        """gevws_ctx_set_completion_flag: the one-launch kernels store their
+        sequence number into the 32-bit word at arena.host[offset:offset+4]
+        (None: off)."""
+        addr = arena.at(offset).data_ptr() if arena is not None else None
+        st = lib.gevws_ctx_set_completion_flag(self._ctx, addr)
+        if st != OK:
+            raise RuntimeError(f"gevws_ctx_set_completion_flag: {status_string(st)}")
+
+    @property
+    def completion_seq(self) -> int:
+        """gevws_ctx_completion_seq: the number the last call's last kernel
+        stores into the completion word, -1 when it does not signal."""
+        return int(lib.gevws_ctx_completion_seq(self._ctx))
+
     def handle_decoded(self, out: "Batch", policy: int, max_frames: int, aux_slots: int, out_cap: int):
         """gevws_handle_decoded_async: dispatch + encode of the replies chained
         behind the decode with no host round trip (one launch when max_frames

@@ -770,6 +770,41 @@ def test_escaped_entry_lengths(engine):
             engine.set_tuning(knob, val)
 
 
+def test_completion_flag_signals_one_launch_passes(engine):
+    """gevws_ctx_set_completion_flag: a one-launch decode stores its
+    sequence number into the mapped word after its outputs (the host may read
+    them once it sees the number, no stream synchronisation); a multi-kernel
+    decode reports -1; every one-launch decode takes a new number."""
+    import time
+    import torch
+    arena = gev_amd.PinnedArena(4096)
+    rng = np.random.default_rng(4242)
+    small = pack_streams([random_stream(rng, 5, max_len=300) for _ in range(40)])
+    big = pack_streams([random_stream(rng, 40) for _ in range(60)])
+    try:
+        engine.set_completion_flag(arena, 64)
+        seen = []
+        for k in range(3):
+            out = gpu_decode(engine, *small)
+            seq = engine.completion_seq
+            assert seq > 0
+            t0 = time.time()
+            while int(arena.host[64:68].view(np.uint32)[0]) != seq:
+                assert time.time() - t0 < 5, "completion word never written"
+            want = ref.decode_batch(np.frombuffer(small[0], np.uint8).copy(), small[1][:, 0], small[1][:, 1])
+            assert out.frames_host().tobytes() == want["frames"].tobytes()
+            seen.append(seq)
+        assert seen == sorted(set(seen))
+        gpu_decode(engine, *big)
+        assert engine.completion_seq == -1  # > 64 KiB: the multi-kernel decode
+        torch.cuda.synchronize()
+    finally:
+        engine.set_completion_flag(None)
+        torch.cuda.synchronize()
+        arena.close()
+    assert engine.completion_seq == -1
+
+
 def test_walk_variant_knob_bounds(engine):
     from gev_amd import _abi
     with pytest.raises(ValueError):
