@@ -489,6 +489,7 @@ class Protocol {
                                    (gevws_out_frame*)d_rep_, drof, dhs, drb, rcap, droff, dhs + 1) != GEVWS_OK)
       return fail();
     sg->hd.chained = true;
+    sg->seq = gevws_ctx_completion_seq(ctx_);  // the handler step is the pass's last launch
     ++stats_.chained_handler_passes;
     return 0;
   }
@@ -631,6 +632,7 @@ class Protocol {
     bool retried = false;  // Finish re-ran the pass: copies enqueued before it are stale
     bool zc = false;       // zero-copy pass: kernels on the pinned buffers themselves
     bool flagged = false;  // its one-launch kernels signal the protocol's flag word
+    int64_t seq = -1;      // ... with this number (taken right after its launches)
     std::shared_ptr<uint8_t> arena;  // zero-copy: the payload arena the kernels write
     uint64_t arena_cap = 0;
     gevws_summary sum{};
@@ -700,9 +702,11 @@ class Protocol {
       void* dfr = sg->arena ? device_of(h_out_) : nullptr;
       void* dpay = sg->arena ? device_of(sg->arena.get()) : nullptr;
       if (!din || !dres || !dfr || !dpay) return fail();
-      return gevws_decode_batch_async(ctx_, st, din + sg->coff, sg->total, (gevws_conn_in*)din, m,
-                                      (gevws_frame*)dfr, sg->max_frames, (uint8_t*)dpay, sg->payload_cap,
-                                      (gevws_conn_out*)(dres + sizeof(gevws_summary)), (gevws_summary*)dres);
+      const int r = gevws_decode_batch_async(ctx_, st, din + sg->coff, sg->total, (gevws_conn_in*)din, m,
+                                             (gevws_frame*)dfr, sg->max_frames, (uint8_t*)dpay, sg->payload_cap,
+                                             (gevws_conn_out*)(dres + sizeof(gevws_summary)), (gevws_summary*)dres);
+      sg->seq = gevws_ctx_completion_seq(ctx_);
+      return r;
     }
     if (!grow_dev(&d_frames_, &d_frames_cap_, sg->max_frames * sizeof(gevws_frame)) ||
         !grow_dev(&d_payload_, &d_payload_cap_, sg->payload_cap + 16))
@@ -742,7 +746,7 @@ class Protocol {
     return true;
   }
   int64_t Wait(const Staged* sg) {
-    const int64_t seq = (sg->zc && sg->flagged) ? gevws_ctx_completion_seq(ctx_) : -1;
+    const int64_t seq = (sg->zc && sg->flagged) ? sg->seq : -1;
     if (seq >= 0) {
       const auto t0 = std::chrono::steady_clock::now();
       for (uint64_t i = 1;; ++i) {
