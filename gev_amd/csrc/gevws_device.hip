@@ -3801,15 +3801,25 @@ __device__ __forceinline__ void win_store(u32x4 v, u32x4* p) {
 // first assembly's loads are in flight together -- one exposed payload latency
 // per window instead of two.  C4 9.39 -> 9.17 ms, C2 / C5 equal
 // (profiles/r03_encode_eo_ab.jsonl; variant 10 keeps the stores before).
+// MAP (with HL, COMPACT, G64, EO): a chunk's frame comes from a chunk -> frame
+// map instead of a binary search over the window's frame starts (9 dependent
+// LDS reads per chunk on C4).  The fill marks, at the first chunk starting at
+// or after each frame's wire start, the last frame with that chunk; a wave
+// then max-scans its four 64-chunk segments, each seeded with the frame that
+// covers the segment's first chunk (as the unmask's v5, k_unmask_auto5).  The
+// window holds 896 frames (not 1 024) so the map fits 7 workgroups per CU.
 template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false, bool HL = false,
-          bool WNT = true, bool G64 = false, bool NTA = false, bool NTW = false, bool EO = false>
+          bool WNT = true, bool G64 = false, bool NTA = false, bool NTW = false, bool EO = false, bool MAP = false>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
                                                          const uint32_t* __restrict__ tile_first,
                                                          const gevws_summary* __restrict__ sum,
                                                          uint8_t* __restrict__ out, uint32_t big_grid) {
-  constexpr int WF = kEncWinFrames;  // frames per window held in LDS
+  static_assert(!MAP || (HL && COMPACT && G64 && EO), "the map replaces the default window path's search");
+  constexpr int WF = MAP ? 896 : kEncWinFrames;  // frames per window held in LDS
+  constexpr uint32_t kChunks = kWinTiles * kUnmaskBlock;  // 16-byte chunks per window
+  constexpr uint32_t kSegs = kChunks / 64;                // 64-chunk segments (one wave step each)
   __shared__ int32_t s_start[WF];  // wire start relative to the window, clamped >= -64
   __shared__ int32_t s_pend[WF];   // payload end relative to the window, clamped
   __shared__ uint8_t s_hlen[WF];
@@ -3818,7 +3828,14 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
   __shared__ uint64_t s_delta[WF];  // payload_off - out_off - hlen (mod 2^64)
   __shared__ uint64_t s_h0[LH ? 1 : WF];
   __shared__ uint64_t s_h1[LH ? 1 : WF];
+  __shared__ uint16_t s_own[MAP ? kChunks : 1];  // chunk -> last frame index + 1 whose start it is the first at/after
+  __shared__ uint32_t s_seed[MAP ? kSegs : 1];   // segment -> frame index + 1 covering its first chunk (0: none)
   if (sum->status != GEVWS_OK) return;
+  if constexpr (MAP) {  // the map and the seeds start empty; each reader clears what it read
+    for (uint32_t i = fresh_tid(); i < kChunks; i += kUnmaskBlock) s_own[i] = 0;
+    if (threadIdx.x < kSegs) s_seed[threadIdx.x] = 0;
+    __syncthreads();
+  }
   const uint64_t total = sum->payload_bytes;  // wire bytes
   const uint64_t nframes = sum->frames;
   const uint64_t ntiles = (total + kTile - 1) / kTile;
@@ -3896,6 +3913,17 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
           s_h0[i] = lo;
           s_h1[i] = hi;
         }
+        if constexpr (MAP) {
+          // key: the first chunk starting at or after the frame's wire start;
+          // the next frame starts at this one's end (the wire is contiguous)
+          const int64_t key = st <= 0 ? 0 : (st + 15) >> 4;
+          const int64_t nk = pe <= 0 ? 0 : (pe + 15) >> 4;
+          const bool last = i + 1 == F;
+          if (key < (int64_t)kChunks && (last || nk != key)) s_own[key] = (uint16_t)(i + 1);
+          // seed every segment whose first chunk this frame covers: key < 64 m <= nk
+          const int64_t m1 = last ? (int64_t)kSegs - 1 : (nk / 64 < (int64_t)kSegs - 1 ? nk / 64 : (int64_t)kSegs - 1);
+          for (int64_t m = key / 64 + 1; m <= m1; ++m) s_seed[m] = (uint32_t)(i + 1);
+        }
       }
       if (COMPACT && threadIdx.x == 0) s_nb = 0;
       __syncthreads();
@@ -3907,15 +3935,46 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
         u32x4 v[kWinTiles];
         uint32_t interior = 0, queued = 0;
         uint32_t qlo[kWinTiles];
+        uint32_t mlo[MAP ? kWinTiles : 1];
+        if constexpr (MAP) {
+          // chunk u * 256 + tid = segment 4 u + wave, lane: an inclusive max scan
+          // per segment, seeded; map entries and seeds cleared by their reader
+          const uint32_t tq = fresh_tid(), lane = tq & 63, wv = tq >> 6;
+#pragma unroll
+          for (int u = 0; u < kWinTiles; ++u) {
+            const uint32_t c = (uint32_t)u * kUnmaskBlock + tq;
+            mlo[u] = s_own[c];
+            s_own[c] = 0;
+          }
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1)
+#pragma unroll
+            for (int u = 0; u < kWinTiles; ++u) {
+              const uint32_t y = (uint32_t)__shfl_up((int)mlo[u], d, 64);
+              if (lane >= (uint32_t)d) mlo[u] = mlo[u] > y ? mlo[u] : y;
+            }
+#pragma unroll
+          for (int u = 0; u < kWinTiles; ++u) {
+            const uint32_t m = (uint32_t)u * (kUnmaskBlock / 64) + wv;
+            const uint32_t seed = s_seed[m];
+            mlo[u] = mlo[u] > seed ? mlo[u] : seed;
+            mlo[u] = mlo[u] ? mlo[u] - 1 : 0u;
+          }
+          if (lane < (uint32_t)kWinTiles) s_seed[lane * (kUnmaskBlock / 64) + wv] = 0;  // after the wave's reads
+        }
 #pragma unroll
         for (int u = 0; u < kWinTiles; ++u) {
           const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
           const uint64_t a = wbase + (uint64_t)rel;
           const bool valid = (uint64_t)u < wt && a < total;
           uint32_t lo = 0, hi = valid ? (uint32_t)F - 1 : 0u;
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+          if constexpr (MAP) {
+            lo = valid ? mlo[u] : 0u;
+          } else {
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi + 1) >> 1;
+              if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+            }
           }
           const bool in = valid && rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo];
           if constexpr (!G64) v[u] = ld16u_stream<NTW>(payload + (in ? a + s_delta[lo] : 0ull));  // (G64: below)
@@ -4808,7 +4867,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->unmask_grid = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_ENCODE_VARIANT:
-      if (value < 0 || value > 10) return GEVWS_ERR_INVALID;
+      if (value < 0 || value > 11) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_EMIT_VARIANT:
@@ -5302,6 +5361,7 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
              : ctx->encode_variant == 8 ? k_encode<4, true, true, true, 7, true, true, true, true>
              : ctx->encode_variant == 9 ? k_encode<4, true, true, true, 7, true, true, true, true, true, true>
              : ctx->encode_variant == 10 ? k_encode<4, true, true, true, 7, true, true, true, true, true>
+             : ctx->encode_variant == 11 ? k_encode<4, true, true, true, 7, true, true, true, true, true, false, true, true>
                                          : k_encode<4, true, true, true, 7, true, true, true, true, true, false, true>;
   // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
   // workgroups per CU (the rest return at once), the window path gets 7

@@ -47,7 +47,7 @@ def test_encode_golden(engine, golden):
     assert np.array_equal(got, g["wire"])
 
 
-ENC_VARIANTS = list(range(11))
+ENC_VARIANTS = list(range(12))
 
 
 @pytest.mark.parametrize("variant", ENC_VARIANTS)
@@ -63,7 +63,9 @@ def test_encode_random_and_tiny_frames(engine, variant):
     loads (the default's are non-temporal); 9: 0 with non-temporal window
     loads; 10: 0 with the interior stores before the queue pass (the
     default -- stores after the first queued chunk's assembly, both loads in
-    flight together -- until round 3)."""
+    flight together -- until round 3); 11: 0 with a chunk -> frame map
+    (marks + per-segment max scan) instead of a binary search per chunk, 896
+    frames per window."""
     from gev_amd import _abi
     engine.set_tuning(_abi.TUNE_ENCODE_VARIANT, variant)
     try:
