@@ -3809,7 +3809,8 @@ __device__ __forceinline__ void win_store(u32x4 v, u32x4* p) {
 // covers the segment's first chunk (as the unmask's v5, k_unmask_auto5).  The
 // window holds 896 frames (not 1 024) so the map fits 7 workgroups per CU.
 template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false, bool HL = false,
-          bool WNT = true, bool G64 = false, bool NTA = false, bool NTW = false, bool EO = false, bool MAP = false>
+          bool WNT = true, bool G64 = false, bool NTA = false, bool NTW = false, bool EO = false, bool MAP = false,
+          int WT = kWinTiles>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ out_off,
@@ -3818,12 +3819,12 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
                                                          uint8_t* __restrict__ out, uint32_t big_grid) {
   static_assert(!MAP || (HL && COMPACT && G64 && EO), "the map replaces the default window path's search");
   constexpr int WF = MAP ? 896 : kEncWinFrames;  // frames per window held in LDS
-  constexpr uint32_t kChunks = kWinTiles * kUnmaskBlock;  // 16-byte chunks per window
+  constexpr uint32_t kChunks = WT * kUnmaskBlock;  // 16-byte chunks per window
   constexpr uint32_t kSegs = kChunks / 64;                // 64-chunk segments (one wave step each)
   __shared__ int32_t s_start[WF];  // wire start relative to the window, clamped >= -64
   __shared__ int32_t s_pend[WF];   // payload end relative to the window, clamped
   __shared__ uint8_t s_hlen[WF];
-  __shared__ uint32_t s_bnd[COMPACT ? kWinTiles * kUnmaskBlock : 1];  // queued chunk: rel / 16 | frame << 16
+  __shared__ uint32_t s_bnd[COMPACT ? WT * kUnmaskBlock : 1];  // queued chunk: rel / 16 | frame << 16
   __shared__ uint32_t s_nb;
   __shared__ uint64_t s_delta[WF];  // payload_off - out_off - hlen (mod 2^64)
   __shared__ uint64_t s_h0[LH ? 1 : WF];
@@ -3891,7 +3892,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
       t += U;
       continue;
     }
-    const uint64_t wt = (tend - t) < (uint64_t)kWinTiles ? (tend - t) : (uint64_t)kWinTiles;
+    const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
     const uint64_t wbase = base;
     const uint64_t f_lo = tile_first[t];
     const uint64_t f_hi = (t + wt) < ntiles ? (uint64_t)tile_first[t + wt] : nframes - 1;
@@ -3932,16 +3933,16 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
         // loads (a boundary chunk from payload[0], always readable, result
         // unused): a load inside the interior/boundary branch made the
         // compiler wait for it at the branch's join
-        u32x4 v[kWinTiles];
+        u32x4 v[WT];
         uint32_t interior = 0, queued = 0;
-        uint32_t qlo[kWinTiles];
-        uint32_t mlo[MAP ? kWinTiles : 1];
+        uint32_t qlo[WT];
+        uint32_t mlo[MAP ? WT : 1];
         if constexpr (MAP) {
           // chunk u * 256 + tid = segment 4 u + wave, lane: an inclusive max scan
           // per segment, seeded; map entries and seeds cleared by their reader
           const uint32_t tq = fresh_tid(), lane = tq & 63, wv = tq >> 6;
 #pragma unroll
-          for (int u = 0; u < kWinTiles; ++u) {
+          for (int u = 0; u < WT; ++u) {
             const uint32_t c = (uint32_t)u * kUnmaskBlock + tq;
             mlo[u] = s_own[c];
             s_own[c] = 0;
@@ -3949,21 +3950,21 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
           for (int d = 1; d < 64; d <<= 1)
 #pragma unroll
-            for (int u = 0; u < kWinTiles; ++u) {
+            for (int u = 0; u < WT; ++u) {
               const uint32_t y = (uint32_t)__shfl_up((int)mlo[u], d, 64);
               if (lane >= (uint32_t)d) mlo[u] = mlo[u] > y ? mlo[u] : y;
             }
 #pragma unroll
-          for (int u = 0; u < kWinTiles; ++u) {
+          for (int u = 0; u < WT; ++u) {
             const uint32_t m = (uint32_t)u * (kUnmaskBlock / 64) + wv;
             const uint32_t seed = s_seed[m];
             mlo[u] = mlo[u] > seed ? mlo[u] : seed;
             mlo[u] = mlo[u] ? mlo[u] - 1 : 0u;
           }
-          if (lane < (uint32_t)kWinTiles) s_seed[lane * (kUnmaskBlock / 64) + wv] = 0;  // after the wave's reads
+          if (lane < (uint32_t)WT) s_seed[lane * (kUnmaskBlock / 64) + wv] = 0;  // after the wave's reads
         }
 #pragma unroll
-        for (int u = 0; u < kWinTiles; ++u) {
+        for (int u = 0; u < WT; ++u) {
           const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
           const uint64_t a = wbase + (uint64_t)rel;
           const bool valid = (uint64_t)u < wt && a < total;
@@ -3985,7 +3986,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
         if constexpr (G64) {
           const uint32_t lane = threadIdx.x & 63, g0 = lane & ~3u;
 #pragma unroll
-          for (int u = 0; u < kWinTiles; ++u) {
+          for (int u = 0; u < WT; ++u) {
             const uint64_t bal = __ballot((queued >> u) & 1u);  // whole wave active
             const bool defer = ((bal >> g0) & 0xFull) != 0;     // (group-uniform)
             uint32_t slot = 0;
@@ -4001,14 +4002,14 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
           // the loads, now that the chunks of queued groups are known (the
           // queue pass loads those itself)
 #pragma unroll
-          for (int u = 0; u < kWinTiles; ++u) {
+          for (int u = 0; u < WT; ++u) {
             const bool in = (interior >> u) & 1u;
             const uint64_t a = wbase + (uint64_t)(u * (int32_t)kTile + (int32_t)lane_off);
             v[u] = ld16u_stream<NTW>(payload + (in ? a + s_delta[qlo[u]] : 0ull));
           }
         } else {
 #pragma unroll
-          for (int u = 0; u < kWinTiles; ++u)
+          for (int u = 0; u < WT; ++u)
             if (queued & (1u << u))
               s_bnd[atomicAdd(&s_nb, 1u)] = ((uint32_t)(u * (int32_t)kTile + (int32_t)lane_off) >> 4) | (qlo[u] << 16);
         }
@@ -4027,7 +4028,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
             }
           }
 #pragma unroll
-          for (int u = 0; u < kWinTiles; ++u)
+          for (int u = 0; u < WT; ++u)
             if (interior & (1u << u))
               win_store<WNT>(v[u], reinterpret_cast<u32x4*>(out + wbase + u * kTile + fresh_tid() * 16));
           if (q0 != 0xffffffffu)
@@ -4045,12 +4046,12 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
           continue;
         }
 #pragma unroll
-        for (int u = 0; u < kWinTiles; ++u)
+        for (int u = 0; u < WT; ++u)
           if (interior & (1u << u))
             win_store<WNT>(v[u], reinterpret_cast<u32x4*>(out + wbase + u * kTile + fresh_tid() * 16));
       } else
 #pragma unroll
-      for (int u = 0; u < kWinTiles; ++u) {
+      for (int u = 0; u < WT; ++u) {
         const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
         const uint64_t a = wbase + (uint64_t)rel;
         if ((uint64_t)u >= wt || a >= total) continue;
