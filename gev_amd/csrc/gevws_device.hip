@@ -3619,20 +3619,53 @@ __global__ __launch_bounds__(kWalkBlock) void k_enc_emit(uint64_t n,
   if (sum->status != GEVWS_OK) return;
   n = gated_count(n, gate);
   const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;
-  uint64_t carry = blk[(uint64_t)blockIdx.x * kBlkFields + 1];
+  const uint64_t carry = blk[(uint64_t)blockIdx.x * kBlkFields + 1];
+  // every slab's wire sizes (k_enc_size left them in out_off) loaded at once,
+  // then ONE workgroup scan over all slabs: a wave scan per slab, and the 64
+  // (slab, wave) totals scanned by one wave in frame order -- two barriers per
+  // workgroup instead of two per slab
+  constexpr int NW = kWalkBlock / 64;
+  static_assert(kEncSlabs * NW == 64, "one lane per (slab, wave) total");
+  __shared__ uint64_t s_base[kEncSlabs * NW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t ws[kEncSlabs], inc[kEncSlabs];
+#pragma unroll
   for (int j = 0; j < kEncSlabs; ++j) {
     const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    ws[j] = f < n ? out_off[f] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kEncSlabs; ++j) {
+    inc[j] = wave_incl_scan(ws[j]);
+    if (lane == 63) s_base[j * NW + wv] = inc[j];
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const uint64_t x = s_base[lane];
+    s_base[lane] = wave_incl_scan(x) - x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kEncSlabs; ++j) {  // (fully unrolled: ws / inc stay in registers)
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
     if (f - threadIdx.x >= n) break;  // workgroup-uniform: slab past the batch
-    uint64_t v[1] = {0};
-    if (f < n) v[0] = out_off[f];  // the wire size k_enc_size left there
-    uint64_t ex[1], tot[1];
-    block_excl_scan<kWalkBlock, 1>(v, ex, tot);
-    if (f < n) {
-      const uint64_t o = carry + ex[0];
-      out_off[f] = o;
-      for (uint64_t t = (o + kTile - 1) / kTile; t * kTile < o + v[0]; ++t) tile_first[t] = (uint32_t)f;
+    // tile map: tiles whose first byte lies in the frame's wire bytes [o, o + v).
+    // A lane writes up to 4 entries itself; the rest of a big frame's range (a
+    // 1 MiB frame has 256) is written by its whole wave, 64 entries a store.
+    const uint64_t end = carry + s_base[j * NW + wv] + inc[j];
+    const uint64_t o = end - ws[j];
+    uint64_t t = (o + kTile - 1) / kTile;
+    const uint64_t te = f < n ? (end + kTile - 1) / kTile : t;
+    if (f < n) out_off[f] = o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k, ++t)
+      if (t < te) tile_first[t] = (uint32_t)f;
+    for (uint64_t rest = __ballot(t < te); rest; rest &= rest - 1) {  // (whole wave active here)
+      const int src = __builtin_ctzll(rest);
+      const uint64_t bt = __shfl((unsigned long long)t, src), be = __shfl((unsigned long long)te, src);
+      const uint32_t bf = (uint32_t)__shfl((unsigned long long)f, src);
+      for (uint64_t x = bt + (uint64_t)lane; x < be; x += 64) tile_first[x] = bf;
     }
-    carry += tot[0];
   }
 }
 
