@@ -3563,6 +3563,11 @@ __device__ __forceinline__ uint32_t enc_hlen(const gevws_header& h) {
 // 4 096 frames and the single-workgroup scan of partials stays short (C4:
 // 10.7 K partials instead of 171 K).
 constexpr int kEncSlabs = 16;
+// Tile-map entries a lane writes itself in k_enc_emit (unrolled, predicated);
+// a frame with more has the rest written by its whole wave.  16 as a plain
+// loop: C5 emit 79 -> 16 us but C4 138 -> 466 us
+// (profiles/r03_encode_emit_lane16_*), so 4.
+constexpr int kEncLaneTiles = 4;
 // The frame count of a chained pass (decode -> dispatch -> encode with no host
 // round trip): the producing step's summary gates the consumer -- its frames,
 // or none when it failed (a capacity error leaves stale records behind).
@@ -3650,15 +3655,16 @@ __global__ __launch_bounds__(kWalkBlock) void k_enc_emit(uint64_t n,
     const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
     if (f - threadIdx.x >= n) break;  // workgroup-uniform: slab past the batch
     // tile map: tiles whose first byte lies in the frame's wire bytes [o, o + v).
-    // A lane writes up to 4 entries itself; the rest of a big frame's range (a
-    // 1 MiB frame has 256) is written by its whole wave, 64 entries a store.
+    // A lane writes up to kEncLaneTiles entries itself; the rest of a big
+    // frame's range (a 1 MiB frame has 256) is written by its whole wave, 64
+    // entries a store.
     const uint64_t end = carry + s_base[j * NW + wv] + inc[j];
     const uint64_t o = end - ws[j];
     uint64_t t = (o + kTile - 1) / kTile;
     const uint64_t te = f < n ? (end + kTile - 1) / kTile : t;
     if (f < n) out_off[f] = o;
 #pragma unroll
-    for (int k = 0; k < 4; ++k, ++t)
+    for (int k = 0; k < kEncLaneTiles; ++k, ++t)
       if (t < te) tile_first[t] = (uint32_t)f;
     for (uint64_t rest = __ballot(t < te); rest; rest &= rest - 1) {  // (whole wave active here)
       const int src = __builtin_ctzll(rest);
