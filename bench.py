@@ -21,6 +21,12 @@ sample of the same workload.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`python bench.py --gpus N` (N > 1) without a launcher starts its N ranks itself
+(torch.distributed.run as a child process, before anything touches a GPU) and
+exits with their status; a rank whose WORLD_SIZE differs from --gpus, or an
+RCCL job with fewer GPUs than ranks, exits non-zero without a line.
+`--dry-run` runs only the launch / shard / count-reduce plumbing (gloo, no GPU).
+
 Measurement options (not the contract line's defaults): --inflight M (M
 batches in flight on M streams), --emulate-shard R/N (rank R's LPT share of an
 N-way strong split, on one GPU), --walk-variant / --unmask-variant /
@@ -162,6 +168,87 @@ def load_traffic(config_name: str):
         return None
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """`bench.py --gpus N` run without a launcher: start the N rank processes
+    itself -- torch.distributed.run as a CHILD process (never an exec), one rank
+    per GPU, rendezvous on 127.0.0.1 -- and return its exit status.  Rank 0's
+    JSON line reaches stdout through the inherited descriptor.  Nothing here
+    touches the GPU (device_count() does not initialise HIP on this image), so
+    the ranks are the only processes that open a device."""
+    import subprocess
+    if _backend() == "nccl":
+        ndev = _visible_devices()
+        if ndev < n:
+            log(f"error: --gpus {n} needs {n} GPUs for RCCL (one rank per device); {ndev} visible")
+            return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    log(f"launching {n} ranks: {' '.join(cmd[1:7])} ...")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def _backend() -> str:
+    return os.environ.get("GEV_DIST_BACKEND", "nccl")
+
+
+def _visible_devices() -> int:
+    import torch
+    return torch.cuda.device_count()
+
+
+def check_world(args, world: int, need_devices: bool) -> None:
+    """Refuse to print a line for a job shaped differently from what was asked:
+    WORLD_SIZE must be --gpus, and under RCCL every rank needs its own device."""
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report "
+                         f"n_gpus={world} for a {args.gpus}-GPU run")
+    if need_devices and _backend() == "nccl" and world > 1 and _visible_devices() < world:
+        raise SystemExit(f"bench: {world} ranks over RCCL need {world} GPUs (one per rank); "
+                         f"{_visible_devices()} visible")
+
+
+def dry_run(args) -> None:
+    """--dry-run: the N > 1 plumbing without a GPU (a CPU test of the launch):
+    rendezvous, this rank's share of the batch, the count all-reduce and the
+    max-over-ranks time, over gloo.  Counts come from the layouts, nothing is
+    decoded or timed, and `value` is null: not a measurement."""
+    import torch
+    from gev_amd import dist
+    world, rank, _ = dist.env()
+    check_world(args, world, need_devices=False)
+    if world > 1 and dist.backend() != "gloo":
+        raise SystemExit("bench --dry-run: GEV_DIST_BACKEND=gloo (no GPU is used)")
+    dist.init(dist.backend(), None)
+    scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
+    lay, glob = build_layout(args.config, rank, args.conns, world, scaling)
+    counts = torch.tensor([lay.n_frames, lay.payload_len, 0], dtype=torch.int64)
+    dist.reduce_counts(counts)
+    dist.barrier()
+    elapsed = dist.max_over_ranks(0.0, "cpu")
+    if rank == 0:
+        c = counts.tolist()
+        print(json.dumps({
+            "metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": 0,
+            "warmup": 0, "ms_per_step": None, "higher_is_better": True, "scaling": scaling,
+            "vs_baseline": None, "dtype": "u8", "data": "dry run: layouts only, nothing decoded",
+            "config": {"workload": lay.name, "connections_per_gpu": lay.n_conns,
+                       "global_connections": glob.n_conns if scaling == "strong" else glob.n_conns * world,
+                       "parallelism": f"connections sharded over {world} rank(s); {dist.backend()} all-reduce of counts"},
+            "decoded_per_step": {"frames": c[0], "payload_bytes": c[1], "errors": c[2], "ranks_summed": world},
+            "max_over_ranks_s": elapsed, "dry_run": True}), flush=True)
+    dist.finalize()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -193,7 +280,16 @@ def main():
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight: M contexts on M streams with M output arenas, step i on slot i %% M "
                          "(a server loop: one batch's header walk overlaps the previous batch's unmask)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="N > 1 plumbing only, no GPU (launch, shard, count all-reduce over gloo); value is null")
     args = ap.parse_args()
+
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.dry_run:
+        return dry_run(args)
 
     import numpy as np
     import torch
@@ -203,8 +299,7 @@ def main():
     from gev_amd.workloads import size_histogram
 
     world, rank, local = dist.env()
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    check_world(args, world, need_devices=True)
     gpu = local % max(torch.cuda.device_count(), 1)  # == local on a node with one rank per GPU
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)

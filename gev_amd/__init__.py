@@ -718,7 +718,12 @@ class Comm:
         n = len(self.devices)
         if len(engines) != n or len(batches) != n:
             raise ValueError("one engine and one batch per device of the communicator")
-        counts = [torch.zeros(3, dtype=torch.int64, device=torch.device("cuda", e.device)) for e in engines]
+        # written only by the contexts' streams (no fill on torch's stream); the
+        # blocks may have been freed by work still queued on torch's current
+        # stream, so that stream is drained first (this is the synchronous form)
+        counts = [torch.empty(3, dtype=torch.int64, device=torch.device("cuda", e.device)) for e in engines]
+        for e in engines:
+            torch.cuda.current_stream(torch.device("cuda", e.device)).synchronize()
         ctxs = (ctypes.c_void_p * n)(*[e._ctx for e in engines])
         sums = (ctypes.c_void_p * n)(*[b.summary.data_ptr() for b in batches])
         cnts = (ctypes.c_void_p * n)(*[c.data_ptr() for c in counts])

@@ -73,6 +73,9 @@ __global__ void k_counts_of(const gevws_summary* __restrict__ s, int64_t* __rest
 
 }  // namespace
 
+// gevws_device.hip (same library, not exported): waits on the context's last decode
+extern "C" int gevws_ctx_order_after_last(gevws_ctx* ctx, void* stream);
+
 struct gevws_comm {
   std::vector<int> devices;
   std::vector<ncclComm_t> comms;
@@ -130,6 +133,12 @@ int gevws_counts_allreduce_async(gevws_comm* c, gevws_ctx* const* ctxs, const ge
   for (int i = 0; i < n && st == GEVWS_OK; ++i) {
     (void)hipSetDevice(c->devices[i]);
     hipStream_t s = (hipStream_t)gevws_ctx_stream(ctxs[i]);
+    // the summary is written by the context's last decode, on whatever stream
+    // the caller gave it: order the read (and the reduce behind it) after that
+    if (gevws_ctx_order_after_last(ctxs[i], s) != GEVWS_OK) {
+      st = GEVWS_ERR_DEVICE;
+      break;
+    }
     k_counts_of<<<1, 64, 0, s>>>(d_summaries[i], d_counts[i]);
     if (hipGetLastError() != hipSuccess) st = GEVWS_ERR_DEVICE;
   }

@@ -4895,6 +4895,15 @@ int gevws_ctx_device(const gevws_ctx* ctx) { return ctx ? ctx->device : -1; }
 
 void* gevws_ctx_stream(const gevws_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
 
+// Not exported (no declaration in gevws.h, -fvisibility=hidden): lets the
+// multi-GPU count reduce (gevws_comm.cpp) order its work on `stream` after the
+// context's last decode, whichever stream that decode ran on.
+int gevws_ctx_order_after_last(gevws_ctx* ctx, void* stream) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  return order_after_last(ctx, reinterpret_cast<hipStream_t>(stream));
+}
+
 int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
   if (!ctx) return GEVWS_ERR_INVALID;
   switch (key) {

@@ -692,7 +692,6 @@ void gevws_protocol_set_upgrader(gevws_protocol *p, const gevws_upgrader *u);
 const uint8_t *gevws_protocol_packet(gevws_protocol *p, gevws_conn *c, const uint8_t *data,
                                      uint64_t n, uint64_t *out_len);
 
-#if defined(__GNUC__)
 /* ---------------------------------------------------------------- multi-GPU in one process
  * A gev server drives all its event loops from one process (server.go:80-91):
  * with NumLoops loops placed on the node's GPUs round-robin (loop l on device
@@ -709,7 +708,8 @@ int gevws_comm_size(const gevws_comm *comm);
 /* For every device i of the communicator: d_counts[i] (int64[3], device
  * memory on device i) = the sum over all devices of {frames, payload_len,
  * errors} of their decode summaries d_summaries[i], enqueued on ctxs[i]'s
- * stream after whatever it holds (one RCCL group, ncclAllReduce in place).
+ * stream after whatever it holds and after ctxs[i]'s last decode, whichever
+ * stream that ran on (one RCCL group, ncclAllReduce in place).
  * ctxs[i] must be on the communicator's device i.  The synchronous form
  * waits and also returns the totals in h_total. */
 int gevws_counts_allreduce_async(gevws_comm *comm, gevws_ctx *const *ctxs, const gevws_summary *const *d_summaries,
@@ -717,6 +717,7 @@ int gevws_counts_allreduce_async(gevws_comm *comm, gevws_ctx *const *ctxs, const
 int gevws_counts_allreduce(gevws_comm *comm, gevws_ctx *const *ctxs, const gevws_summary *const *d_summaries,
                            int64_t *const *d_counts, int64_t h_total[3]);
 
+#if defined(__GNUC__)
 #pragma GCC visibility pop
 #endif
 #ifdef __cplusplus

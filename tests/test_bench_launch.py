@@ -1,0 +1,63 @@
+"""bench.py's N > 1 launch on the CPU: `python bench.py --gpus N` with no
+external launcher starts its N ranks itself (torch.distributed.run as a child
+process) and reports an N-rank line, and a job shaped differently from --gpus
+exits non-zero instead of reporting n_gpus = 1.  The
+--dry-run mode runs the launch, rendezvous, shard and count all-reduce over
+gloo without touching a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, drop=("WORLD_SIZE", "RANK", "LOCAL_RANK")):
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT,
+                          capture_output=True, text=True, timeout=240, env=env)
+
+
+def _line(r):
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.stdout[-2000:], r.stderr[-2000:])
+    return json.loads(lines[0])
+
+
+def test_self_launch_two_ranks_weak():
+    r = _run(["--gpus", "2", "--dry-run", "--config", "c2"], {"GEV_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r)
+    assert d["n_gpus"] == 2 and d["dry_run"] is True and d["value"] is None
+    c = d["decoded_per_step"]
+    assert c["ranks_summed"] == 2 and c["frames"] == 2 * 262144 and c["payload_bytes"] == 2 * 262144 * 4096
+    assert d["config"]["global_connections"] == 2 * d["config"]["connections_per_gpu"]
+
+
+def test_self_launch_three_ranks_strong_split_covers_batch():
+    import bench
+    glob, _ = bench.build_layout("c5", 0, None)
+    r = _run(["--gpus", "3", "--dry-run", "--config", "c5", "--scaling", "strong"], {"GEV_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r)
+    assert d["n_gpus"] == 3 and d["decoded_per_step"]["ranks_summed"] == 3
+    assert d["decoded_per_step"]["frames"] == glob.n_frames
+    assert d["decoded_per_step"]["payload_bytes"] == glob.payload_len
+
+
+def test_rccl_without_enough_devices_exits_nonzero():
+    # this container has no GPU: --gpus 2 over RCCL must refuse before launching
+    r = _run(["--gpus", "2", "--dry-run", "--config", "c2"], {"GEV_DIST_BACKEND": "nccl"})
+    assert r.returncode != 0
+    assert "needs 2 GPUs" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_world_size_mismatch_exits_nonzero():
+    # launched as one rank while --gpus asks for two: no line, non-zero exit
+    r = _run(["--gpus", "2", "--dry-run", "--config", "c2"],
+             {"GEV_DIST_BACKEND": "gloo", "WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, drop=())
+    assert r.returncode != 0
+    assert "WORLD_SIZE=1" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -67,6 +67,33 @@ def test_bench_two_ranks_weak_c2():
     assert d["config"]["global_connections"] == 2 * d["config"]["connections_per_gpu"]
 
 
+def test_bench_self_launch_two_ranks_gloo():
+    """`bench.py --gpus 2` with no launcher starts its own two ranks (here both
+    on this GPU over gloo) and reports n_gpus 2, not a one-GPU line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["GEV_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "c2",
+                        "--steps", "2", "--warmup", "1", "--no-cpu", "--copy-reps", "0"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["decoded_per_step"]["ranks_summed"] == 2 and d["value"] > 0
+
+
+def test_bench_rccl_more_ranks_than_gpus_exits_nonzero():
+    import torch
+    n = torch.cuda.device_count() + 1
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GEV_DIST_BACKEND")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--config", "c2",
+                        "--steps", "1", "--warmup", "0", "--no-cpu", "--copy-reps", "0"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    assert f"needs {n} GPUs" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
 def test_bench_two_ranks_strong_c4():
     import bench
     glob, _ = bench.build_layout("c4", 0, None)

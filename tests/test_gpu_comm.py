@@ -32,6 +32,32 @@ def test_counts_allreduce_one_device(engine):
     assert tuple(int(x) for x in out.counts.cpu()) == tot
 
 
+def test_counts_allreduce_after_unsynchronised_decode(engine):
+    """decode_async on torch's stream, then the reduce at once, with no
+    synchronisation between them: the reduce must wait for the decode's summary
+    (ADVICE r3).  A 4 GiB-payload C3-shaped batch keeps the decode running
+    long after the host returns from the launch."""
+    import torch
+    from gev_amd import workloads as w
+    lay = w.config_c3(seed=11, n_conns=1024, n_frames=1 << 16)
+    dev = torch.device("cuda", engine.device)
+    arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    arena[lay.arena_bytes:] = 0
+    desc = torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev)
+    conns = torch.from_numpy(lay.conns.copy()).to(dev)
+    engine.synth(arena, desc, lay.n_frames, lay.seed)
+    out = engine.alloc_batch(lay.n_conns, lay.n_frames, lay.payload_padded)
+    comm = gev_amd.Comm([engine.device])
+    side = torch.cuda.Stream(dev)  # neither torch's current stream nor the context's own
+    for _ in range(3):
+        out.summary.zero_()
+        side.wait_stream(torch.cuda.current_stream(dev))
+        engine.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, lay.n_frames, lay.payload_padded,
+                            stream=side)
+        tot = comm.allreduce_counts([engine], [out])
+        assert tot == (lay.n_frames, lay.payload_len, 0)
+
+
 def test_comm_rejects_bad_arguments(engine):
     with pytest.raises(RuntimeError):
         gev_amd.Comm([gev_amd.device_count() + 3])
