@@ -280,6 +280,10 @@ def main():
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight: M contexts on M streams with M output arenas, step i on slot i %% M "
                          "(a server loop: one batch's header walk overlaps the previous batch's unmask)")
+    ap.add_argument("--front-cus", type=int, default=0,
+                    help="with --inflight >= 2: run each batch's walk / scan / record pass on a stream of this many "
+                         "CUs and its unmask on a stream of the others (CU masks), so batch k+1's walk overlaps "
+                         "batch k's unmask (0 = one stream per slot, no CU split)")
     ap.add_argument("--dry-run", action="store_true",
                     help="N > 1 plumbing only, no GPU (launch, shard, count all-reduce over gloo); value is null")
     args = ap.parse_args()
@@ -367,6 +371,19 @@ def main():
     sum64 = out.summary.view(torch.int64)
     outs = [out] + [e.alloc_batch(lay.n_conns, max_frames, cap) for e in engs[1:]]
     streams = [None] if M == 1 else [torch.cuda.Stream(dev) for _ in range(M)]
+    split = None
+    if args.front_cus:
+        if M < 2:
+            raise SystemExit("--front-cus needs --inflight >= 2")
+        ncu_dev = torch.cuda.get_device_properties(dev).multi_processor_count
+        fmask, bmask = gev_amd.cu_split_masks(ncu_dev, args.front_cus)
+        front, back = gev_amd.CuStream(gpu, fmask), gev_amd.CuStream(gpu, bmask)
+        for e in engs:
+            e.set_unmask_stream(back)
+        streams = [front] * M
+        split = {"front_cus": front.cus, "unmask_cus": back.cus}
+        log(f"split streams: walk / scan / record pass on {front.cus} CUs, unmask on {back.cus} CUs")
+        torch.cuda.synchronize()
     main_stream = torch.cuda.current_stream()
     n_step = [0]
 
@@ -377,7 +394,7 @@ def main():
                              stream=streams[k])
         if world > 1:  # decoded {frames, payload bytes, errors}, summed over GPUs (N = 1: read after the loop)
             if M > 1:
-                main_stream.wait_stream(streams[k])
+                engs[k].order_after_last(main_stream)
             torch.index_select(outs[k].summary.view(torch.int64), 0, sel, out=counts)
             dist.reduce_counts(counts)
 
@@ -477,6 +494,7 @@ def main():
                                    f"{' by greedy LPT over stream bytes' if scaling == 'strong' else ''}; "
                                    f"{'RCCL' if dist.backend() == 'nccl' else dist.backend()} all-reduce of counts"),
                    "batches_in_flight": M,
+                   **({"split_streams": split} if split else {}),
                    **({"emulated_shard": emulated} if emulated else {})},
         "frames_per_s": round(frames_step * args.steps / elapsed, 1),
         "decoded_per_step": {"frames": frames_step, "payload_bytes": payload_step, "errors": errors,

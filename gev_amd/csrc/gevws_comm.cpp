@@ -73,9 +73,6 @@ __global__ void k_counts_of(const gevws_summary* __restrict__ s, int64_t* __rest
 
 }  // namespace
 
-// gevws_device.hip (same library, not exported): waits on the context's last decode
-extern "C" int gevws_ctx_order_after_last(gevws_ctx* ctx, void* stream);
-
 struct gevws_comm {
   std::vector<int> devices;
   std::vector<ncclComm_t> comms;

@@ -4672,6 +4672,11 @@ struct gevws_ctx {
   bool has_last = false;
   int num_cus = 256;
   uint32_t* d_done = nullptr;  // the decode walk's finished-workgroup counter (zero between calls)
+  // split-stream decode (gevws_ctx_set_unmask_stream): the unmask on its own
+  // stream after the record pass (front_done), its grid for unmask_cus CUs
+  hipStream_t unmask_stream = nullptr;
+  int unmask_cus = 0;
+  hipEvent_t front_done = nullptr;
 };
 
 namespace {
@@ -4885,6 +4890,7 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (ctx->d_done) (void)hipFree(ctx->d_done);
   if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
+  if (ctx->front_done) (void)hipEventDestroy(ctx->front_done);
   for (auto& set : ctx->evs)
     for (auto& e : set.e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -4895,13 +4901,55 @@ int gevws_ctx_device(const gevws_ctx* ctx) { return ctx ? ctx->device : -1; }
 
 void* gevws_ctx_stream(const gevws_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
 
-// Not exported (no declaration in gevws.h, -fvisibility=hidden): lets the
-// multi-GPU count reduce (gevws_comm.cpp) order its work on `stream` after the
-// context's last decode, whichever stream that decode ran on.
+// (also used by the multi-GPU count reduce, gevws_comm.cpp)
 int gevws_ctx_order_after_last(gevws_ctx* ctx, void* stream) {
   if (!ctx) return GEVWS_ERR_INVALID;
   DeviceGuard g(ctx->device);
   return order_after_last(ctx, reinterpret_cast<hipStream_t>(stream));
+}
+
+int gevws_stream_cu_count(int device, void* stream) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) return 0;
+  if (!stream) return n;
+  std::vector<uint32_t> m((size_t)(n + 31) / 32, 0u);
+  if (hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(stream), (uint32_t)m.size(), m.data()) != hipSuccess)
+    return n;
+  int c = 0;
+  for (int i = 0; i < n; ++i) c += (m[(size_t)i / 32] >> (i % 32)) & 1u;
+  return c > 0 ? c : n;
+}
+
+int gevws_stream_create_cu_mask(int device, const uint32_t* cu_mask, uint32_t n_words, void** stream) {
+  if (!cu_mask || !n_words || !stream || device < 0 || device >= gevws_device_count()) return GEVWS_ERR_INVALID;
+  *stream = nullptr;
+  uint32_t any = 0;
+  for (uint32_t i = 0; i < n_words; ++i) any |= cu_mask[i];
+  if (!any) return GEVWS_ERR_INVALID;
+  DeviceGuard g(device);
+  hipStream_t s = nullptr;
+  GEVWS_HIP(hipExtStreamCreateWithCUMask(&s, n_words, cu_mask));
+  *stream = reinterpret_cast<void*>(s);
+  return GEVWS_OK;
+}
+
+int gevws_stream_destroy(void* stream) {
+  if (!stream) return GEVWS_OK;
+  return hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)) == hipSuccess ? GEVWS_OK : GEVWS_ERR_DEVICE;
+}
+
+int gevws_ctx_set_unmask_stream(gevws_ctx* ctx, void* unmask_stream) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  ctx->unmask_stream = reinterpret_cast<hipStream_t>(unmask_stream);
+  ctx->unmask_cus = unmask_stream ? gevws_stream_cu_count(ctx->device, unmask_stream) : 0;
+  if (ctx->unmask_cus <= 0 || ctx->unmask_cus > ctx->num_cus) ctx->unmask_cus = ctx->num_cus;
+  if (unmask_stream && !ctx->front_done &&
+      hipEventCreateWithFlags(&ctx->front_done, hipEventDisableTiming) != hipSuccess) {
+    ctx->unmask_stream = nullptr;
+    return GEVWS_ERR_DEVICE;
+  }
+  return GEVWS_OK;
 }
 
 int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
@@ -5343,12 +5391,20 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
                                                                           d_summary, d_frames, tile_first, entries,
                                                                           ne, gshift, e_rec, e_parent, e_ks);
   }
-  if (timed) GEVWS_HIP(hipEventRecord(ev[3], st));
-  r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);
+  // split streams: the unmask waits for the front (walk, scan, record pass)
+  // on its own stream; the next batch's front can then run beside it
+  hipStream_t ust = st;
+  if (ctx->unmask_stream && ctx->unmask_stream != st) {
+    ust = ctx->unmask_stream;
+    GEVWS_HIP(hipEventRecord(ctx->front_done, st));
+    GEVWS_HIP(hipStreamWaitEvent(ust, ctx->front_done, 0));
+  }
+  if (timed) GEVWS_HIP(hipEventRecord(ev[3], ust));  // (split: once the unmask stream may start it)
+  r = launch_unmask(ctx, ust, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);
   if (r != GEVWS_OK) return r;
-  if (timed) GEVWS_HIP(hipEventRecord(ev[4], st));
+  if (timed) GEVWS_HIP(hipEventRecord(ev[4], ust));
   GEVWS_HIP(hipGetLastError());
-  return mark_last(ctx, st);
+  return mark_last(ctx, ust);
 }
 
 int gevws_decode_batch(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64_t in_bytes,
@@ -5618,20 +5674,21 @@ static int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, c
                   uint8_t* d_payload) {
   const UnmaskVariant& v = kUnmaskVariants[ctx->unmask_variant];
   const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
-  const uint64_t norm = 4 * (uint64_t)ctx->num_cus;
+  // CUs the unmask's stream may use (all of the device's, or its CU mask's)
+  const uint32_t ucus = (uint32_t)(st == ctx->unmask_stream && ctx->unmask_cus > 0 ? ctx->unmask_cus : ctx->num_cus);
+  const uint64_t norm = 4 * (uint64_t)ucus;
   // the wide grid (kWideGridPerCU per CU) when the previous decode on this
   // context was a batch of mixed sizes (run frames < half) below
   // kWideGridTiles; the kernel still uses `norm` workgroups unless this
   // batch is one too
   const bool wide = v.wide && !ctx->unmask_grid && ctx->stats_known && ctx->prev_mixed &&
                     ntiles < kWideGridTiles && norm <= 0xffffu;
-  uint64_t grid = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : wide ? kWideGridPerCU * (uint64_t)ctx->num_cus : norm;
+  uint64_t grid = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : wide ? kWideGridPerCU * (uint64_t)ucus : norm;
   const uint64_t useful = (ntiles + v.unroll - 1) / v.unroll;
   if (grid > useful) grid = useful;
   if (grid < 1) grid = 1;
   ctx->last_unmask_grid = (uint32_t)grid;
   v.fn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary, d_payload,
-                                                ctx->unmask_grid ? 0u
-                                                                 : (uint32_t)ctx->num_cus | (wide ? (uint32_t)norm << 16 : 0u));
+                                                ctx->unmask_grid ? 0u : ucus | (wide ? (uint32_t)norm << 16 : 0u));
   return GEVWS_OK;
 }

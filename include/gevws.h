@@ -130,6 +130,28 @@ void gevws_ctx_destroy(gevws_ctx *ctx);
 int gevws_ctx_device(const gevws_ctx *ctx);
 /* The context's own non-blocking hipStream_t (one per event loop). */
 void *gevws_ctx_stream(const gevws_ctx *ctx);
+/* Makes `stream` wait for everything the context's last call enqueued,
+ * whichever stream(s) that ran on (e.g. a decode whose unmask ran on the
+ * context's unmask stream, below). */
+int gevws_ctx_order_after_last(gevws_ctx *ctx, void *stream);
+/* Split-stream decode (a server loop with two batches in flight): with an
+ * unmask stream set, gevws_decode_batch[_async] runs its header walk, scan and
+ * record pass on the caller's stream and the unmask on `unmask_stream`, after
+ * them (an event), with its grid sized for that stream's CUs.  The call's
+ * completion is then on the unmask stream (gevws_ctx_order_after_last orders
+ * other work after it).  Two contexts sharing one front and one unmask stream
+ * overlap batch k+1's walk with batch k's unmask; with CU-masked streams
+ * (gevws_stream_create_cu_mask) the two do not compete for the same CUs.
+ * NULL: the whole decode on the caller's stream (the default).  The one-launch
+ * small-batch decode ignores it. */
+int gevws_ctx_set_unmask_stream(gevws_ctx *ctx, void *unmask_stream);
+/* A non-blocking stream on `device` whose kernels run only on the CUs set in
+ * the n_words x 32-bit mask (hipExtStreamCreateWithCUMask; bit i = CU i). */
+int gevws_stream_create_cu_mask(int device, const uint32_t *cu_mask, uint32_t n_words, void **stream);
+int gevws_stream_destroy(void *stream);
+/* The number of CUs a stream may use (its CU mask's population; all of the
+ * device's for an unmasked stream or NULL). */
+int gevws_stream_cu_count(int device, void *stream);
 /* Tuning knobs for measurement (defaults are the tuned choice):
  * GEVWS_TUNE_UNMASK_VARIANT selects an unmask kernel variant (0 = default),
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto; when set it caps the

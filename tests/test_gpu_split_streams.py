@@ -1,0 +1,90 @@
+"""Split-stream decode (gevws_ctx_set_unmask_stream): the header walk, scan and
+record pass on one stream, the unmask on another, two batches in flight on
+CU-masked streams -- the server loop of connection.go:208-218 with batch k+1's
+walk beside batch k's unmask.  Results must be the oracle's, bit-exact, and
+every in-flight slot must verify."""
+import numpy as np
+import pytest
+import torch
+
+import gev_amd
+from oracle import ref
+from tests._helpers import host_result, pack_streams, random_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _masked_streams(dev_index, front_cus=32):
+    ncu = torch.cuda.get_device_properties(dev_index).multi_processor_count
+    fm, bm = gev_amd.cu_split_masks(ncu, front_cus)
+    return gev_amd.CuStream(dev_index, fm), gev_amd.CuStream(dev_index, bm), ncu
+
+
+def test_cu_masked_streams_report_their_cus(engine):
+    front, back, ncu = _masked_streams(engine.device)
+    assert front.cus == 32 and back.cus == ncu - 32
+    with pytest.raises(ValueError):
+        gev_amd.cu_split_masks(ncu, 12)
+
+
+def test_split_stream_decode_matches_oracle(engine):
+    front, back, _ = _masked_streams(engine.device)
+    dev = torch.device("cuda", engine.device)
+    rng = np.random.default_rng(77)
+    engine.set_unmask_stream(back)
+    try:
+        for it in range(4):
+            n = int(rng.integers(300, 900))  # above the one-launch small-batch path
+            arena, conns = pack_streams([random_stream(rng, int(rng.integers(0, 40))) for _ in range(n)])
+            a = np.frombuffer(arena, np.uint8).copy()
+            want = ref.decode_batch(a, conns[:, 0], conns[:, 1])
+            d_in = torch.zeros(a.size + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+            d_in[: a.size] = torch.from_numpy(a).to(dev)
+            d_conns = torch.from_numpy(conns.copy()).to(dev)
+            nf = max(int(want["frames"].shape[0]), 1)
+            cap = max(int(want["payload"].size), 16)
+            out = engine.alloc_batch(n, nf, cap)
+            torch.cuda.synchronize()
+            engine.decode_async(d_in, a.size, d_conns, n, out, nf, cap, stream=front)
+            engine.order_after_last(torch.cuda.current_stream(dev))
+            got = host_result(out)
+            assert int(got["summary"]["status"]) == 0
+            assert got["frames"][: want["frames"].shape[0]].tobytes() == want["frames"].tobytes(), it
+            assert np.array_equal(got["payload"][: want["payload"].size], want["payload"]), it
+            assert np.array_equal(got["conn_out"]["consumed"], want["conn_consumed"]), it
+    finally:
+        engine.set_unmask_stream(None)
+
+
+def test_two_batches_in_flight_on_masked_streams():
+    """Two contexts share the front and unmask streams; 6 steps alternate
+    between them with no host synchronisation; every slot's last batch is the
+    generator's plaintext on every byte."""
+    from gev_amd import workloads as w
+    front, back, _ = _masked_streams(0)
+    dev = torch.device("cuda", 0)
+    lay = w.config_c4(total_payload=256 << 20, n_conns=2048, seed=5)
+    arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    arena[lay.arena_bytes:] = 0
+    desc = torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev)
+    conns = torch.from_numpy(lay.conns.copy()).to(dev)
+    engs = [gev_amd.Engine(0) for _ in range(2)]
+    engs[0].synth(arena, desc, lay.n_frames, lay.seed)
+    torch.cuda.synchronize()
+    outs = [e.alloc_batch(lay.n_conns, lay.n_frames, lay.payload_padded) for e in engs]
+    for e in engs:
+        e.set_unmask_stream(back)
+    for i in range(6):
+        k = i % 2
+        engs[k].decode_async(arena, lay.arena_bytes, conns, lay.n_conns, outs[k], lay.n_frames,
+                             lay.payload_padded, stream=front)
+    torch.cuda.synchronize()
+    for k, e in enumerate(engs):
+        mism = torch.zeros(1, dtype=torch.int64, device=dev)
+        e.verify(desc, lay.n_frames, lay.seed, outs[k], mism)
+        torch.cuda.synchronize()
+        s = outs[k].summary_host()
+        assert int(mism.item()) == 0, k
+        assert int(s["frames"]) == lay.n_frames and int(s["payload_len"]) == lay.payload_len
+        e.set_unmask_stream(None)
+        e.close()
