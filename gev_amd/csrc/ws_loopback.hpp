@@ -47,6 +47,12 @@
 // (control frame sent, reply received) pair as hex for the oracle check
 // (tests/test_gpu_loopback.py against oracle/ws_oracle.on_message).
 //
+// --mode close mirrors TestWebSocketServer_CloseConnection
+// (wsserver_test.go:135-178): --conns clients dial and upgrade, --to-close of
+// them close (a close frame first with --close-frame 1, as x/net/websocket's
+// Conn.Close; a bare TCP close with 0), and the server's OnConnect - OnClose
+// count must be conns - to_close after the drain, then 0 once the rest close.
+//
 //   [--conns 1000] [--msg 128] [--seconds 5] [--loops 1] [--client-threads 4]
 //   [--port 0] [--device 0] [--mode echo|wsserver] [--ctrl 0] [--close-end 0]
 //   [--transcript FILE] [--seed 1] [--devices 1]
@@ -87,12 +93,18 @@ namespace wslb {
 inline std::atomic<bool> g_stop{false};
 inline std::atomic<uint64_t> g_batches{0}, g_batch_conns{0}, g_frames{0}, g_bad{0}, g_dev_ns{0};
 inline std::atomic<uint64_t> g_ctrl{0}, g_closed{0}, g_sent_async{0}, g_payload{0};
+// OnConnect / OnClose of every server loop (wsExample.ClientNum,
+// example/websocket/wsserver_test.go:22-45): +1 at accept, -1 when the loop
+// closes the connection (EOF or error on read, connection.go:288-303)
+inline std::atomic<int64_t> g_live{0};
 
-enum { kModeEcho = 0, kModeWsServer = 1 };
+enum { kModeEcho = 0, kModeWsServer = 1, kModeClose = 2 };
 struct Config {
   int mode = kModeEcho;
   double ctrl_prob = 0.0;  // wsserver: a control frame before a message with this probability
   bool close_end = false;  // wsserver: every client ends with a close frame
+  int to_close = 5;         // close mode: connections the client closes
+  bool close_frame = true;  // close mode: a close frame before the TCP close (x/net/websocket Conn.Close)
   std::string transcript;  // wsserver: (control frame sent, reply) pairs, hex
   unsigned seed = 1;
 };
@@ -160,7 +172,7 @@ struct ServerConn {
 template <class Decoder>
 void server_loop(int port, int device, std::atomic<int>* ready, int index) {
   Decoder dec(device);
-  const bool wss = g_cfg.mode == kModeWsServer;
+  const bool wss = g_cfg.mode != kModeEcho;
   if (wss) dec.set_handler(GEVWS_HANDLER_ECHO_TEXT);  // wsExample.OnMessage returns (MessageText, data)
   std::mt19937_64 route(g_cfg.seed * 1000003u + (unsigned)index);  // wsserver_test.go:47: rand.Int() % 2
   int ls = socket(AF_INET, SOCK_STREAM, 0);
@@ -254,7 +266,10 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
         break;
       }
     }
-    if (!s->out.empty() && !s->shut && !send_all(s->fd, s->out.data(), s->out.size())) g_bad.fetch_add(1);
+    // (close mode: the peer may already be gone when its close reply goes out;
+    // gev then just closes the connection, connection.go:305-328)
+    if (!s->out.empty() && !s->shut && !send_all(s->fd, s->out.data(), s->out.size()) && g_cfg.mode != kModeClose)
+      g_bad.fetch_add(1);
     if (shut && !s->shut) {  // c.ShutdownWrite() after the close reply (wrap.go:56)
       ::shutdown(s->fd, SHUT_WR);
       s->shut = true;
@@ -297,6 +312,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
           ServerConn sc{cfd, gevws_conn_new(), gevws_ring_new(4096), {}, {}, 0};  // DefaultBufferSize
           gevws_conn_set_upgraded(sc.c, 0);
           conns.emplace(cfd, std::move(sc));
+          g_live.fetch_add(1);  // OnConnect
           epoll_event ce{};
           ce.events = EPOLLIN;
           ce.data.fd = cfd;
@@ -316,6 +332,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
         gevws_conn_free(it->second.c);
         gevws_ring_free(it->second.r);
         conns.erase(it);
+        g_live.fetch_sub(1);  // OnClose
         continue;
       }
       gevws_ring_write(it->second.r, rbuf.data(), (uint64_t)k);
@@ -657,6 +674,76 @@ inline void ws_client_thread(int port, int nconn, double t_end, std::atomic<uint
   for (auto& p : tr) g_transcript.push_back(std::move(p));
 }
 
+// ------------------------------------------------------------------ wsserver_test.go:135-178 client
+// TestWebSocketServer_CloseConnection: n clients dial and upgrade (the server
+// counts OnConnect), then to_close of them close -- x/net/websocket's
+// Conn.Close writes a close frame and closes the socket (--close-frame 1), or a
+// bare TCP close (0) -- and after the drain (the reference sleeps 3 s) the
+// server's live count must be n - to_close.  Then the rest close and the count
+// must drain to 0.  Returns the counts seen.
+struct CloseResult {
+  int64_t after_connect = -1, after_close = -1, at_end = -1;
+  int upgraded = 0;
+  double drain_s = 0;
+};
+
+inline int64_t wait_live(int64_t want, double limit_s) {
+  const double t0 = now_s();
+  while (g_live.load() != want && now_s() - t0 < limit_s) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  return g_live.load();
+}
+
+inline CloseResult close_client(int port, int n, unsigned seed) {
+  CloseResult res;
+  std::mt19937_64 rng(seed);
+  const char req_fmt[] =
+      "GET / HTTP/1.1\r\nHost: 127.0.0.1:%d\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+      "Sec-WebSocket-Key: dGhlIHNhbXBsZSBub25jZQ==\r\nOrigin: ws://127.0.0.1\r\nSec-WebSocket-Version: 13\r\n\r\n";
+  char req[512];
+  const int rn = snprintf(req, sizeof(req), req_fmt, port);
+  std::vector<int> fds;
+  for (int i = 0; i < n; ++i) {  // websocket.Dial: connect, upgrade request, wait for the 101
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (fd < 0 || connect(fd, (sockaddr*)&a, sizeof(a))) {
+      perror("ws_loopback: connect");
+      _exit(2);
+    }
+    fds.push_back(fd);
+    send_all(fd, (const uint8_t*)req, (size_t)rn);
+    std::string got;
+    char b[1024];
+    const double t0 = now_s();
+    while (got.find("\r\n\r\n") == std::string::npos && now_s() - t0 < 5.0) {
+      const ssize_t k = ::recv(fd, b, sizeof(b), 0);
+      if (k <= 0) break;
+      got.append(b, (size_t)k);
+    }
+    if (got.compare(0, 12, "HTTP/1.1 101") == 0 && got.find("s3pPLMBiTxaQ9kYGzzhZRbK+xOo=") != std::string::npos)
+      ++res.upgraded;
+    else
+      g_bad.fetch_add(1);
+  }
+  res.after_connect = wait_live(n, 3.0);  // assert.Equal(t, n, ClientNum)
+  const double tc = now_s();
+  for (int i = 0; i < g_cfg.to_close && i < n; ++i) {
+    if (g_cfg.close_frame) {  // Conn.Close: WriteClose(1000), then rwc.Close
+      const uint8_t body[2] = {0x03, 0xE8};
+      auto f = masked_frame(rng, 0x88, body, 2);
+      if (!send_all(fds[i], f.data(), f.size())) g_bad.fetch_add(1);
+    }
+    close(fds[i]);
+  }
+  res.after_close = wait_live(n - g_cfg.to_close, 3.0);  // time.Sleep(3 s); assert n - toClose
+  res.drain_s = now_s() - tc;
+  for (int i = g_cfg.to_close; i < n; ++i) close(fds[i]);
+  res.at_end = wait_live(0, 3.0);
+  return res;
+}
+
 template <class Decoder>
 int loopback_main(int argc, char** argv) {
   int conns = 1000, loops = 1, cthreads = 4, port = 0, device = 0, ndev = 1;
@@ -673,14 +760,17 @@ int loopback_main(int argc, char** argv) {
     else if (k == "--port") port = atoi(v);
     else if (k == "--device") device = atoi(v);
     else if (k == "--devices") ndev = atoi(v) > 0 ? atoi(v) : 1;
-    else if (k == "--mode") g_cfg.mode = std::string(v) == "wsserver" ? kModeWsServer : kModeEcho;
+    else if (k == "--mode")
+      g_cfg.mode = std::string(v) == "wsserver" ? kModeWsServer : std::string(v) == "close" ? kModeClose : kModeEcho;
+    else if (k == "--to-close") g_cfg.to_close = atoi(v);
+    else if (k == "--close-frame") g_cfg.close_frame = atoi(v) != 0;
     else if (k == "--ctrl") g_cfg.ctrl_prob = atof(v);
     else if (k == "--close-end") g_cfg.close_end = atoi(v) != 0;
     else if (k == "--transcript") g_cfg.transcript = v;
     else if (k == "--seed") g_cfg.seed = (unsigned)atoi(v);
   }
   const bool wss = g_cfg.mode == kModeWsServer;
-  if (wss && !Decoder::kHandler && (g_cfg.ctrl_prob > 0 || g_cfg.close_end)) {
+  if (!Decoder::kHandler && (g_cfg.ctrl_prob > 0 || g_cfg.close_end || (g_cfg.mode == kModeClose && g_cfg.close_frame))) {
     fprintf(stderr, "ws_loopback: control frames need the device handler (%s has none)\n", Decoder::name());
     return 2;
   }
@@ -699,6 +789,20 @@ int loopback_main(int argc, char** argv) {
   std::vector<std::thread> servers;
   for (int l = 0; l < loops; ++l) servers.emplace_back(server_loop<Decoder>, port, device + l % ndev, &ready, l);
   while (ready.load() < loops) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  if (g_cfg.mode == kModeClose) {
+    const CloseResult r = close_client(port, conns, 77u * g_cfg.seed);
+    g_stop = true;
+    for (auto& t : servers) t.join();
+    printf("{\"mode\": \"close\", \"decoder\": \"%s\", \"connections\": %d, \"upgraded\": %d, \"loops\": %d, "
+           "\"to_close\": %d, \"close_frame\": %d, \"live_after_connect\": %lld, \"live_after_close\": %lld, "
+           "\"live_at_end\": %lld, \"drain_s\": %.3f, \"closes_answered\": %llu, \"errors\": %llu}\n",
+           Decoder::name(), conns, r.upgraded, loops, g_cfg.to_close, g_cfg.close_frame ? 1 : 0,
+           (long long)r.after_connect, (long long)r.after_close, (long long)r.at_end, r.drain_s,
+           (unsigned long long)g_closed.load(), (unsigned long long)g_bad.load());
+    const bool ok = g_bad.load() == 0 && r.upgraded == conns && r.after_connect == conns &&
+                    r.after_close == conns - g_cfg.to_close && r.at_end == 0;
+    return ok ? 0 : 1;
+  }
 
   std::atomic<uint64_t> total{0};
   std::atomic<int> upgraded{0};

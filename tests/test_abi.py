@@ -86,6 +86,26 @@ def test_ring_buffer_write_peek_retrieve_wrap():
     assert r.is_empty() and r.peek_all() == (b"", b"")
 
 
+def test_default_protocol_unpacket_ring_fixture():
+    """TestDefaultProtocol_UnPacket (protocol_test.go:13-31), the reference's one
+    ring-buffer fixture, literally: ringbuffer.New(4), Write("1234") -> 4,
+    Peek(2) + Retrieve(2), Write("ab") -> 2 (wraps into the freed front, no
+    growth), then DefaultProtocol.UnPacket (protocol.go:19-39: PeekAll, join the
+    two segments, RetrieveAll) returns "34ab" and Length() is 0."""
+    r = gev_amd.RingBuffer(4)
+    assert r.write(b"1234") == 4
+    assert r.capacity() == 4 and r.length() == 4
+    r.retrieve(2)  # (Peek(2) reads without consuming)
+    assert r.write(b"ab") == 2
+    assert r.capacity() == 4  # the write wrapped instead of growing
+    s, e = r.peek_all()
+    assert (s, e) == (b"34", b"ab")  # two segments: len(e) > 0 takes the userBuffer join
+    data = s + e
+    r.retrieve(len(s) + len(e))  # RetrieveAll
+    assert data == b"34ab"
+    assert r.length() == 0
+
+
 def test_ring_buffer_random_against_bytes_model():
     rng = np.random.default_rng(3)
     r = gev_amd.RingBuffer(16)

@@ -121,3 +121,31 @@ def test_wsserver_loops_placed_on_devices_round_robin():
     d = _run("gev_amd/ws_loopback", conns=64, seconds=1.0, loops=4, threads=2,
              extra=("--mode", "wsserver", "--devices", str(n)))
     assert d["devices"] == n and d["client_checked_echoes"] > 0
+
+
+# ---------------------------------------------------------------- wsserver_test.go:135-178
+def _run_close(binary, close_frame):
+    path = os.path.join(ROOT, binary)
+    assert os.path.exists(path), f"{binary} not built"
+    r = subprocess.run([path, "--mode", "close", "--conns", "10", "--to-close", "5", "--loops", "8",
+                        "--close-frame", str(close_frame)], capture_output=True, text=True, timeout=60)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.returncode, r.stdout[-1500:], r.stderr[-1500:])
+    d = json.loads(lines[0])
+    print(binary, json.dumps(d))
+    assert r.returncode == 0, d
+    return d
+
+
+@pytest.mark.parametrize("close_frame", [1, 0])
+def test_wsserver_close_connection_mirror(close_frame):
+    """TestWebSocketServer_CloseConnection (wsserver_test.go:135-178) on the
+    device-decode server: 8 loops, 10 clients dial and upgrade (OnConnect count
+    10), 5 close -- with a close frame first, as x/net/websocket's Conn.Close
+    (answered on the device: close reply + ShutdownWrite), or a bare TCP close
+    -- and after the drain the OnConnect - OnClose count is 5, then 0."""
+    d = _run_close("gev_amd/ws_loopback", close_frame)
+    assert d["decoder"] == "device"
+    assert (d["live_after_connect"], d["live_after_close"], d["live_at_end"]) == (10, 5, 0)
+    if close_frame:
+        assert d["closes_answered"] == 5
