@@ -72,6 +72,7 @@ class Batch:
     conn_out: "object"    # uint8 [n_conns, 32]     (gevws_conn_out)
     summary: "object"     # uint8 [64]              (gevws_summary)
     n_conns: int
+    aux_slots: int = 0    # close-reply slots reserved after the payload arena (alloc_batch)
 
     def summary_host(self) -> np.ndarray:
         return self.summary.cpu().numpy().view(SUMMARY_DTYPE)[0]
@@ -257,7 +258,7 @@ class Engine:
         return Batch(frames=torch.empty((max(max_frames, 1), 32), dtype=torch.uint8, device=dev),
                      payload=torch.empty(payload_cap + 16 + extra, dtype=torch.uint8, device=dev),
                      conn_out=torch.empty((max(n_conns, 1), 32), dtype=torch.uint8, device=dev),
-                     summary=torch.zeros(64, dtype=torch.uint8, device=dev), n_conns=n_conns)
+                     summary=torch.zeros(64, dtype=torch.uint8, device=dev), n_conns=n_conns, aux_slots=aux_slots)
 
     def decode_async(self, arena, in_bytes: int, conns, n_conns: int, out: Batch, max_frames: int,
                      payload_cap: int, stream=None) -> None:
@@ -377,6 +378,10 @@ class Engine:
         summary, encode summary)."""
         torch = _torch()
         dev = torch.device("cuda", self.device)
+        # the close bodies go into the slots alloc_batch reserved behind the
+        # payload arena, never over decoded payloads the replies still read
+        if not 0 <= aux_slots <= out.aux_slots:
+            raise ValueError(f"handle_decoded: aux_slots {aux_slots} outside the batch's {out.aux_slots} reserved slots")
         aux_off = (out.payload.numel() - 16 - 128 * aux_slots) // 16 * 16
         n = max(int(max_frames), 1)
         replies = torch.empty((n, 32), dtype=torch.uint8, device=dev)

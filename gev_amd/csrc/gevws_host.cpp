@@ -140,6 +140,7 @@ struct Delivered {
   std::shared_ptr<uint8_t> replies;
   uint64_t reply_off = 0, reply_len = 0;
   bool shutdown = false;
+  bool handled = false;  // the frame's pass ran the handler (its reply fields are the answer)
 };
 
 struct Connection {
@@ -225,7 +226,9 @@ class Protocol {
     c->reply_off = d.reply_off;
     c->reply_len = d.reply_len;
     c->shutdown = d.shutdown;
-    c->reply_valid = handler_ >= 0;
+    // (from the frame's own pass: a frame queued before set_handler() has no
+    // answer, one queued before the handler was turned off keeps its answer)
+    c->reply_valid = d.handled;
     *hdr = d.hdr;
     *out = c->current.get() + d.payload_off;
     *out_len = (uint64_t)d.hdr.length;
@@ -357,6 +360,7 @@ class Protocol {
         d.frame_bytes = f.src_off + (uint64_t)f.hdr.length - prev_end;
         d.payload_off = f.payload_off;
         d.arena = arena;
+        d.handled = handled;
         if (handled) {
           const int64_t r = rof[o.first_frame + k];
           if (r >= 0) {

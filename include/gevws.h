@@ -574,7 +574,8 @@ int gevws_protocol_set_handler(gevws_protocol *p, int policy);
  * c: *reply / *len = the reply frame's wire bytes (the `out` OnMessage returns;
  * len 0 = none), *shutdown_write = 1 for a close frame (c.ShutdownWrite() after
  * sending the reply, wrap.go:52-56).  Valid until the next UnPacket on c.
- * GEVWS_ERR_INVALID when no handler is set or no frame was returned yet. */
+ * GEVWS_ERR_INVALID when no frame was returned yet or the returned frame's
+ * pass did not run the handler (decoded while it was off). */
 int gevws_protocol_reply(const gevws_protocol *p, const gevws_conn *c, const uint8_t **reply, uint64_t *len,
                          int *shutdown_write);
 void gevws_protocol_set_zero_copy_max(gevws_protocol *p, uint64_t bytes);

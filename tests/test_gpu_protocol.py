@@ -567,3 +567,30 @@ def test_device_handler_off_by_default(engine):
         proto.reply(c)
     with pytest.raises(ValueError):
         proto.set_handler(7)
+
+
+def test_reply_follows_the_frames_own_pass(engine):
+    """gevws_protocol_reply answers from the pass that decoded the frame
+    (ADVICE r3): a ping queued while the handler was off has no answer even
+    after set_handler() (not an OK with no pong), and a frame decoded while the
+    handler was on keeps its pong after the handler is turned off."""
+    key = b"\x01\x02\x03\x04"
+    ping = wo.encode_frame(b"ping", wo.OP_PING, True, 0, True, key)
+    proto = gev_amd.Protocol(engine)
+    c, r = gev_amd.Connection(), gev_amd.RingBuffer(4096)
+    r.write(ping + ping)
+    proto.unpacket_batch([c], [r])  # both pings queued, no handler ran
+    proto.set_handler(wo.HANDLER_ECHO_TEXT)
+    h, data = proto.unpacket(c, r)
+    assert h is not None and data == b"ping"
+    with pytest.raises(RuntimeError):
+        proto.reply(c)
+    proto.unpacket(c, r)
+    # decoded with the handler on, handed out after it is turned off
+    r.write(ping)
+    proto.unpacket_batch([c], [r])
+    proto.set_handler(-1)
+    h, data = proto.unpacket(c, r)
+    assert h is not None and data == b"ping"
+    fr = wo.decode_stream(ping).frames[0]
+    assert proto.reply(c) == wo.on_message(fr.header, fr.payload, wo.HANDLER_ECHO_TEXT)
