@@ -30,7 +30,7 @@ RCCL job with fewer GPUs than ranks, exits non-zero without a line.
 Measurement options (not the contract line's defaults): --inflight M (M
 batches in flight on M streams), --emulate-shard R/N (rank R's LPT share of an
 N-way strong split, on one GPU), --walk-variant / --unmask-variant /
---emit-variant / --split-lanes (A/B), --split-mode (split-walk cost breakdown).
+--split-lanes (A/B), --front-cus (split-stream overlap with --inflight >= 2).
 The split header walk's auto choice (GEVWS_TUNE_SPLIT_LANES 0) looks at the
 previous finished decode on the context: the untimed verify decode walks
 unsplit, the warmup and timed steps split when that decode showed long chains
@@ -266,14 +266,8 @@ def main():
     ap.add_argument("--copy-reps", type=int, default=5, help="streaming-copy ceiling reps (0 = skip)")
     ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
     ap.add_argument("--unmask-variant", type=int, default=None, help="A/B: unmask kernel variant")
-    ap.add_argument("--emit-variant", type=int, default=None, help="A/B: record pass variant (GEVWS_TUNE_EMIT_VARIANT)")
     ap.add_argument("--split-lanes", type=int, default=None,
                     help="A/B: split header walk lanes per connection (GEVWS_TUNE_SPLIT_LANES; 0 = auto, 1 = off)")
-    ap.add_argument("--split-mode", type=int, default=0, help="measurement: GEVWS_TUNE_SPLIT_MODE")
-    ap.add_argument("--walk-budget", type=int, default=None,
-                    help="A/B: budgeted header walk, frames per lane (GEVWS_TUNE_WALK_BUDGET; 0 = auto, -1 = off)")
-    ap.add_argument("--resume-lanes", type=int, default=None, help="A/B: lanes per resumed connection")
-    ap.add_argument("--budget-frac", type=int, default=None, help="A/B: auto budget in 16ths of the mean chain")
     ap.add_argument("--emulate-shard", default=None, metavar="R/N",
                     help="projection, not the contract line: decode only rank R's LPT share of an N-way strong "
                          "split of the global batch, on this one GPU")
@@ -318,18 +312,8 @@ def main():
             e.set_tuning(_abi.TUNE_WALK_VARIANT, args.walk_variant)
         if args.unmask_variant is not None:
             e.set_tuning(_abi.TUNE_UNMASK_VARIANT, args.unmask_variant)
-        if args.emit_variant is not None:
-            e.set_tuning(_abi.TUNE_EMIT_VARIANT, args.emit_variant)
         if args.split_lanes is not None:
             e.set_tuning(_abi.TUNE_SPLIT_LANES, args.split_lanes)
-        if args.split_mode:
-            e.set_tuning(_abi.TUNE_SPLIT_MODE, args.split_mode)
-        if args.walk_budget is not None:
-            e.set_tuning(_abi.TUNE_WALK_BUDGET, args.walk_budget)
-        if args.resume_lanes is not None:
-            e.set_tuning(_abi.TUNE_RESUME_LANES, args.resume_lanes)
-        if args.budget_frac is not None:
-            e.set_tuning(_abi.TUNE_BUDGET_FRAC, args.budget_frac)
     t_setup = time.time()
     scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
     emulated = None
@@ -428,8 +412,7 @@ def main():
                 raise SystemExit(f"verification failed on in-flight slot {k}: mismatch={int(mism.item())}")
         del desc
 
-    walk_info = {"split_lanes": eng.last_split_lanes, "budget": eng.last_walk_budget,
-                 "resumed_connections": eng.last_resumed}
+    walk_info = {"split_lanes": eng.last_split_lanes}
     # achievable-bandwidth ceiling on this box, after the timed region: the
     # unmask kernel's streaming loop minus XOR / frame lookup (gevws_copy_async)
     # over the same byte count into the payload arena -- from the payload's

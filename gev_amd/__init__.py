@@ -209,19 +209,6 @@ class Engine:
         """Lanes per connection of the last multi-kernel decode's header walk (1 = not split)."""
         return int(lib.gevws_ctx_last_split_lanes(self._ctx))
 
-    @property
-    def last_walk_budget(self) -> int:
-        """Frames per lane of the last multi-kernel decode's budgeted walk (0 = not budgeted)."""
-        return int(lib.gevws_ctx_last_walk_budget(self._ctx))
-
-    @property
-    def last_resumed(self) -> int:
-        """Connections the last decode's budgeted walk resumed (waits for it)."""
-        r = int(lib.gevws_ctx_last_resumed(self._ctx))
-        if r < 0:
-            raise RuntimeError(f"last_resumed: {status_string(r)}")
-        return r
-
     @staticmethod
     def variant_name(i: int, key: int = _abi.TUNE_UNMASK_VARIANT) -> Optional[str]:
         n = lib.gevws_tuning_name(key, i)
@@ -420,18 +407,6 @@ class Engine:
         if st != OK:
             raise RuntimeError(status_string(st))
 
-    def gather_(self, src, nbytes: int, lanes: int, per_lane: int, dependent: bool, sink, seed: int = 1,
-                stream=None, load_kind: int = 0) -> None:
-        """gevws_gather_async: the header walk's random-line fetch ceiling (measurement only).
-        load_kind: 0 plain 16-byte loads, 1 / 2 two 8-byte system- / agent-scope loads, 3 one 4-byte
-        system-scope load."""
-        assert nbytes <= src.numel() and sink.numel() >= lanes and 0 <= load_kind < 4
-        st = lib.gevws_gather_async(self._ctx, _stream_handle(stream), src.data_ptr(), nbytes, lanes, per_lane,
-                                    (1 if dependent else 0) | (load_kind << 1), seed, sink.data_ptr())
-        if st != OK:
-            raise RuntimeError(status_string(st))
-
-    # -------------------------------------------------------------- synthetic batches
     def synth(self, arena, desc_dev, n_frames: int, seed: int, stream=None) -> None:
         st = lib.gevws_synth_async(self._ctx, _stream_handle(stream), arena.data_ptr(), desc_dev.data_ptr(),
                                    n_frames, seed)

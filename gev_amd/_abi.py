@@ -41,18 +41,13 @@ AUX_SLOT = 128
 HANDLER_NONE = 0
 HANDLER_ECHO_BINARY = 1
 HANDLER_ECHO_TEXT = 2
-TUNE_UNMASK_VARIANT = 1
+TUNE_UNMASK_VARIANT = 1  # 0 = auto (v3 / v5 per batch), 1 = v5 for every batch
 TUNE_UNMASK_GRID = 2
-TUNE_ENCODE_VARIANT = 3
-TUNE_WALK_VARIANT = 4
-TUNE_SPAN_CONNS_PER_CU = 5
-TUNE_EMIT_VARIANT = 6
+TUNE_ENCODE_VARIANT = 3  # 0 = the default encode (the only one at present)
+TUNE_WALK_VARIANT = 4  # 0 = default, 1 = plain chain walk, 2 = no entry table, 3 = writer wave always
 TUNE_SMALL_BATCH = 7  # one-launch decode up to this many input bytes (0 = never)
-TUNE_SPLIT_MODE = 9  # measurement: 1 = split guesses made then dropped, 2 = none made
-TUNE_SPLIT_LANES = 8  # split header walk: lanes per connection (0 = auto, 1 = never, 2/4/8/16)
-TUNE_WALK_BUDGET = 10  # budgeted walk: frames per lane (0 = auto, -1 = never, > 0 = always)
-TUNE_RESUME_LANES = 11  # lanes per resumed connection (0 = default 8, 2/4/8/16)
-TUNE_BUDGET_FRAC = 12  # auto budget in 16ths of the previous mean chain
+TUNE_SPLIT_LANES = 8  # split header walk: lanes per connection (0 = auto, 1 = never, 2/4/8/16/32)
+TUNE_RETIRED = (5, 6, 9, 10, 11, 12)  # round 1-3 measurement knobs, rejected
 TUNE_SPLIT_MIN_BYTES = 13  # split walk: bytes per segment at least (default 16 384)
 TUNE_SPLIT_LANES_PER_CU = 14  # split walk auto: lanes per CU at most (default 512)
 
@@ -183,9 +178,6 @@ SIGNATURES = {
     "gevws_ctx_set_tuning": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_last_split_lanes": (ctypes.c_int, [P]),
     "gevws_ctx_last_unmask_grid": (ctypes.c_int, [P]),
-    "gevws_ctx_last_walk_budget": (ctypes.c_int64, [P]),
-    "gevws_unmask_profile": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
-    "gevws_ctx_last_resumed": (ctypes.c_int64, [P]),
     "gevws_tuning_name": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32)]),
     "gevws_decode_batch_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_uint32, P,
@@ -228,8 +220,6 @@ SIGNATURES = {
     "gevws_protocol_unpacket_batch_end": (ctypes.c_int64, [P]),
     "gevws_protocol_packet": (U8P, [P, P, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "gevws_copy_async": (ctypes.c_int, [P, P, P, P, ctypes.c_uint64, ctypes.c_uint32]),
-    "gevws_gather_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
-                                          ctypes.c_uint64, P]),
     "gevws_pinned_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(P), ctypes.POINTER(P)]),
     "gevws_pinned_free": (ctypes.c_int, [P]),
     "gevws_upgrader_new": (P, []),

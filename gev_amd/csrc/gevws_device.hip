@@ -58,7 +58,6 @@ constexpr int kDecFields = 5;
 // for longer than the launch they save (C1-shaped batch: walk + scan 46 ->
 // 54 us fused; 256 blocks -- C2, C3, C5, an 8-way C4 share -- save 4-8 us)
 constexpr uint32_t kFusedScanMaxBlocks = 256;
-constexpr bool kFusedScan = true;  // see gevws_decode_batch_async
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ u32x4 ld16u(const uint8_t* p) {
@@ -297,8 +296,8 @@ __device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uin
 // base_c = S (off_c / SG + c), capacity S (len_c / SG + 1) with S = kSlotAlign
 // = 32, the granularity G the smallest power of two >= 64 B that keeps the
 // table within kEntryBudget; runs start on 256-byte boundaries, so the walk can
-// store its entries as whole groups (k_walk_count GRP: 32 bytes of four; the
-// LDS-ring writer: 256 bytes of 32).  The runs are
+// store its entries as whole groups (the LDS-ring writer: 256 bytes of 32).
+// The runs are
 // disjoint when the whole table is in increasing input order with no overlap
 // (for c < d: base_c + cap_c <= S ((off_c + len_c) / SG + 1 + c) <= base_d);
 // a neighbour check per connection cannot establish that (an
@@ -309,7 +308,7 @@ __device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uin
 // are written either way: base + cap <= n_entries holds for any table, so the
 // stores stay inside the table.  A connection whose frames outnumber its slots
 // (mean frame < G bytes) or whose stream is >= 4 GiB is re-walked too.
-constexpr uint64_t kGroupedWalkChainsPerCU = 128;  // k_walk_count GRP from n_conns >= this x CUs
+constexpr uint64_t kWriterChainsPerCU = 128;  // k_walk_count ST 2 (the writer wave) from n_conns >= this x CUs
 constexpr uint32_t kEntryGranMinShift = 6;        // 64-byte granularity when the table fits
 constexpr uint64_t kEntryBudget = 1ull << 29;     // entries (8 GiB of scratch) at most
 // slot runs start on 32-entry (256-byte) boundaries: the writer wave of the
@@ -392,36 +391,14 @@ __device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t ava
 // mixed-size traffic.  Interleaved A/B against D = 0
 // (profiles/r01_ab_walk2_*.json): the walk of fixed-size traffic takes 23-28 %
 // less time (C2, C3), mixed traffic 0-5 % more (C4, C5: a longer loop body on
-// a latency-bound chain).  GEVWS_TUNE_WALK_VARIANT 1 selects D = 0.
-// GRP: a lane keeps its last three entries in registers and stores each
-// 64-byte group of four at once.  One lane writes one entry per chain step,
-// ~1 us apart, so with many chains a group's line is evicted from L2 long
-// before single 16-byte stores would fill it: those reach HBM as partial
-// writes (C4: 1.78 GB of writes for 0.70 GB of entries,
-// profiles/r01_c4_pmc.csv).  The cost: on a step that stores a group the next
-// header load waits for three of its stores as well (the store count behind
-// the load depends on the path), which slows latency-bound walks of few
-// chains -- so the host enables GRP only for batches of many connections
-// (profiles/r01_ab_walk_grp_*.json).
-// NTH (measurement): header windows loaded non-temporally -- does the L2
-// then request less than a 128-byte line per header (the walk's reads are
-// 17x the header bytes, profiles/r02_pmc_split_before.json)?
-// PF: with each header load, also touch the PF 128-byte lines after it, so a
-// following small frame's header is an L2 hit (~200 cycles) instead of an HBM
-// miss (~900).  The touches are issued before the header load, so waiting for
-// the header (vmcnt counts loads in issue order) never waits longer for them;
-// they cost bandwidth, which a chain-bound walk of few connections has spare
-// (round 1 measured the same touch 30 % slower on all of C4, which is not).
+// a latency-bound chain), so the host runs D = 0 after a mixed batch.
 // The chain walk of one stream (k_walk_count's loop; also each segment of
 // k_walk_split): entries into [ebase, ebase + ecap) while rec, per-frame
 // counts into R (R.err / R.st carry in the caller's values).
-// The walk starts from the state in R (a fresh chain: walk_res_fresh; the
-// budgeted walk's resumption: the state it stopped in) and stops after
-// `budget` frames in all (R.more: the header at R.pos is not parsed yet).
 struct WalkRes {
   uint64_t pos, nf, pb, pl, same, lastf, firstf, err;
   int32_t st;
-  bool rec, more;
+  bool rec;
 };
 __device__ __forceinline__ WalkRes walk_res_fresh(uint64_t err = 0, int32_t st = GEVWS_OK) {
   WalkRes R;
@@ -429,23 +406,25 @@ __device__ __forceinline__ WalkRes walk_res_fresh(uint64_t err = 0, int32_t st =
   R.lastf = ~0ull;
   R.err = err;
   R.st = st;
-  R.rec = R.more = false;
+  R.rec = false;
   return R;
 }
 
-// ST: where entries go.  0 = global memory from the walking lane (GRP: in
-// 64-byte groups of four); 1 = nowhere (measurement); 2 = this lane's LDS ring
-// (WalkRing), drained to global memory by the workgroup's writer wave
-// (k_walk_count ST 2): the walker then issues no global stores at all, so
-// waiting for its header load (vmcnt counts loads and stores in order) never
-// waits for an entry store.
+// ST: where entries go.  0 = global memory, one 8-byte store per frame from the
+// walking lane (batches of few chains: latency-bound, the stores overlap the
+// next header load); 2 = this lane's LDS ring (WalkRing), drained to global
+// memory by the workgroup's writer wave (k_walk_count ST 2): the walker then
+// issues no global stores at all, so waiting for its header load (vmcnt counts
+// loads and stores in order) never waits for an entry store.  Batches of many
+// chains, whose walk is bound by line traffic: single entry stores scattered
+// among the random header reads cost far more than their bytes (C4: 1.60 ms
+// against 1.00 without entries, 1.26 through the writer;
+// profiles/r03_walk_writer_grp_ab.jsonl, r03_compact_entries_ab.jsonl).
 constexpr uint32_t kRingDone = 0x80000000u;   // head flag: the chain is finished
-// entries per lane's LDS ring for a writer group of WGS entries
-template <int WGS>
-constexpr uint32_t ring_size() { return WGS >= 8 ? 2u * WGS : 16u; }
+constexpr uint32_t kWriterGroup = 32;         // entries per writer store group (256 bytes)
+constexpr uint32_t kRing = 2 * kWriterGroup;  // entries per lane's LDS ring
 struct WalkRing {
-  WalkEntry* e;    // ring_size entries (LDS)
-  uint32_t mask;   // ring_size - 1
+  WalkEntry* e;    // kRing entries (LDS)
   uint32_t* head;  // entries published (whole groups of 4; | kRingDone with the count at the end)
   uint32_t* tail;  // entries the writer has taken
 };
@@ -456,18 +435,15 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int D, bool GRP, bool NTH = false, int PF = 0, int UNR = 2, int ST = 0>
+template <int D, int ST = 0>
 __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const uint64_t len, bool rec,
                                            const uint64_t ebase, const uint64_t ecap,
                                            WalkEntry* __restrict__ entries, WalkEntry* __restrict__ sink,
-                                           WalkRes& R, const uint64_t budget = ~0ull,
-                                           WalkRing ring = WalkRing{nullptr, 0, nullptr, nullptr}) {
-    constexpr bool NST = ST != 0;  // no global entry stores from this lane
-    // (GRP keeps the group's earlier entries in registers: a fresh chain only)
+                                           WalkRes& R, WalkRing ring = WalkRing{nullptr, nullptr, nullptr}) {
+    static_assert(ST == 0 || ST == 2, "entries from the lane or through the writer wave");
     uint64_t nf = R.nf, pb = R.pb, pl = R.pl, same = R.same, lastf = R.lastf, firstf = R.firstf, err = R.err;
     int32_t st = R.st;
     uint64_t pos = R.pos;
-    bool more = false;
     // software-pipelined: the next header's 16 bytes are requested before this
     // frame's entry is stored, so waiting for that load (vmcnt counts loads and
     // stores in issue order) never waits for the store's completion.  Reading
@@ -476,38 +452,21 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
     // outstanding (lanes not recording store to their own sink slot past the
     // table), so the compiler waits vmcnt(1), not vmcnt(0).
     uint64_t lo, hi;
-    load_window<NTH>(s + pos, lo, hi);
-    if constexpr (!NST) *sink = WalkEntry{0, 0};
+    load_window(s + pos, lo, hi);
+    if constexpr (ST == 0) *sink = WalkEntry{0, 0};
     uint64_t prev_fsz = 0;  // speculation (D > 0): size of the last frame and the run of equal sizes
     uint32_t run = 0;
-    WalkEntry g0 = {0, 0}, g1 = g0, g2 = g0;  // GRP: the last three entries, oldest first
-    auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
-      (void)p;  // positions are recomputed by the record pass
+    auto put_entry = [&](uint32_t key, uint64_t L, uint32_t meta) {
       rec = rec && nf < ecap;
       const WalkEntry e = make_entry(key, L, meta);
-      if constexpr (ST == 1) {  // measurement: no stores at all (the walk's pure chain cost)
-        rec = false;
-      } else if constexpr (ST == 2) {
+      if constexpr (ST == 2) {
         // room for this group in the ring? (the writer is normally far ahead:
         // it copies a group in a few hundred cycles, a step takes ~1 us)
         if ((nf & 3) == 0)
-          while ((uint32_t)nf + 4 - lds_ld(ring.tail) > ring.mask + 1) __builtin_amdgcn_s_sleep(1);
-        ring.e[nf & ring.mask] = e;
+          while ((uint32_t)nf + 4 - lds_ld(ring.tail) > kRing) __builtin_amdgcn_s_sleep(1);
+        ring.e[nf & (kRing - 1)] = e;
         __asm__ volatile("" ::: "memory");  // the entry before the head that publishes it (DS ops run in order)
         if ((nf & 3) == 3) lds_st(ring.head, (uint32_t)nf + 1);
-      } else if constexpr (GRP) {
-        if (rec && (nf & 3) == 3) {
-          WalkEntry* g = entries + ebase + (nf - 3);  // 64-byte aligned
-          g[0] = g0;
-          g[1] = g1;
-          g[2] = g2;
-          g[3] = e;
-        } else {
-          *sink = e;
-        }
-        g0 = g1;
-        g1 = g2;
-        g2 = e;
       } else {
         *(rec ? entries + ebase + nf : sink) = e;
       }
@@ -519,18 +478,9 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
       firstf = lastf == ~0ull ? f : firstf;
       lastf = f;
     };
-    uint32_t pfv[PF > 0 ? PF : 1] = {};
     // One chain step on the window (clo, chi) at pos; the next header's window
     // is loaded into (nlo, nhi).  false: the chain ends here.
     auto step = [&](const uint64_t clo, const uint64_t chi, uint64_t& nlo, uint64_t& nhi) -> bool {
-      if (nf >= budget) {  // the budgeted walk stops here; k_walk_resume goes on from pos
-        more = true;
-        return false;
-      }
-      if constexpr (PF > 0) {  // keep the touches' results alive (free: they landed before the header)
-#pragma unroll
-        for (int j = 0; j < PF; ++j) __asm__ volatile("" ::"v"(pfv[j]));
-      }
       // The chain is latency-bound (one load per frame, few lanes per SIMD):
       // only the next frame's position is computed before its header load is
       // issued -- at min(next, len), always inside the stream + GEVWS_IN_PAD
@@ -544,16 +494,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
       const uint64_t L = e64 ? L64 : (e16 ? L16 : (uint64_t)len7);
       const uint64_t fsz = hlen + L;
       const uint64_t next = pos + fsz;
-      if constexpr (PF > 0) {
-        const uint64_t nx = next <= len ? next : len;
-#pragma unroll
-        for (int j = 0; j < PF; ++j) {
-          const uint64_t q = nx + 128 * (j + 1);
-          pfv[j] = *reinterpret_cast<const uint32_t*>(s + (q <= len ? q : len));
-        }
-        __asm__ volatile("" ::: "memory");  // touches first, then the header load
-      }
-      load_window<NTH>(s + (next <= len ? next : len), nlo, nhi);  // (a wrapped next is <= len or clamped)
+      load_window(s + (next <= len ? next : len), nlo, nhi);  // (a wrapped next is <= len or clamped)
       const uint64_t avail = len - pos;
       const bool have_hdr = avail >= 6 && avail >= hlen;   // read.go:20-23, U1
       const bool msb = e64 && (L64 >> 63);                  // read.go:71-73
@@ -564,7 +505,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
       const uint32_t key = (e64 ? (uint32_t)(chi >> 16) : (e16 ? (uint32_t)(clo >> 32) : (uint32_t)(clo >> 16))) &
                            (0u - masked);
       const uint32_t meta = ((uint32_t)clo & 0xffu) | (masked << 8) | (hlen << 16);
-      put_entry(pos, key, L, meta);
+      put_entry(key, L, meta);
       pos = next;
       if constexpr (D > 0) {
         run = fsz == prev_fsz ? run + 1 : 1;
@@ -585,7 +526,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
               const uint64_t q = pos + (uint64_t)j * fsz;
               const bool in = q <= len;
               qn += in ? 1u : 0u;
-              load_window<NTH>(s + (in ? q : len), qlo[j], qhi[j]);
+              load_window(s + (in ? q : len), qlo[j], qhi[j]);
             }
             qlo[0] = nlo;
             qhi[0] = nhi;
@@ -600,7 +541,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
                   if (r == GEVWS_ERR_LEN_MSB) { st = GEVWS_ERR_LEN_MSB; err += 1; }
                   fail = stop = true;
                 } else {
-                  put_entry(pos, k2, L2, m2);
+                  put_entry(k2, L2, m2);
                   pos += h2 + L2;
                   if (h2 + L2 != fsz) {
                     stop = true;
@@ -611,48 +552,26 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
               }
             }
             if (fail) break;
-            load_window<NTH>(s + pos, nlo, nhi);  // the next batch's first window, or the chain's next header
+            load_window(s + pos, nlo, nhi);  // the next batch's first window, or the chain's next header
             if (stop || qn < (uint32_t)D || pos + fsz > len) break;
           }
           if (fail) return false;
-          if constexpr (!NST) *sink = WalkEntry{0, 0};  // same [load, store] in flight as the plain path
+          if constexpr (ST == 0) *sink = WalkEntry{0, 0};  // same [load, store] in flight as the plain path
         }
       }
       return true;
     };
-    if constexpr (UNR == 2) {
-      // two window buffers in turn: the window a step loads is the next
-      // step's current one in the same registers.  (With one buffer the
-      // compiler copies the loaded window into the loop-carried registers at
-      // the back edge -- a copy that waits for the load and, vmcnt being in
-      // order, for every entry store after it: each step then paid the load
-      // AND the stores' latency instead of overlapping them with the checks.)
-      uint64_t lo2 = 0, hi2 = 0;
-      for (;;) {
-        if (!step(lo, hi, lo2, hi2)) break;
-        if (!step(lo2, hi2, lo, hi)) break;
-      }
-    } else {
-      for (;;) {
-        uint64_t nlo, nhi;
-        if (!step(lo, hi, nlo, nhi)) break;
-        lo = nlo;
-        hi = nhi;
-      }
-    }
-    if (GRP && !NST && rec) {  // the last nf % 4 entries
-      const uint32_t r = (uint32_t)(nf & 3);
-      WalkEntry* g = entries + ebase + (nf - r);
-      if (r == 3) {
-        g[0] = g0;
-        g[1] = g1;
-        g[2] = g2;
-      } else if (r == 2) {
-        g[0] = g1;
-        g[1] = g2;
-      } else if (r == 1) {
-        g[0] = g2;
-      }
+    // two window buffers in turn: the window a step loads is the next step's
+    // current one in the same registers.  (With one buffer the compiler copies
+    // the loaded window into the loop-carried registers at the back edge -- a
+    // copy that waits for the load and, vmcnt being in order, for every entry
+    // store after it: each step then paid the load AND the stores' latency
+    // instead of overlapping them with the checks; C4 walk 1.61 -> 1.59 ms,
+    // profiles/r03_walk_unr_ab.jsonl.)
+    uint64_t lo2 = 0, hi2 = 0;
+    for (;;) {
+      if (!step(lo, hi, lo2, hi2)) break;
+      if (!step(lo2, hi2, lo, hi)) break;
     }
     R.pos = pos;
     R.nf = nf;
@@ -664,7 +583,6 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
     R.err = err;
     R.st = st;
     R.rec = rec;
-    R.more = more;
     if constexpr (ST == 2) {  // the rest of the entries, and the end of the chain
       __asm__ volatile("" ::: "memory");
       lds_st(ring.head, (uint32_t)nf | kRingDone);
@@ -672,18 +590,16 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
 }
 
 // The writer wave of k_walk_count ST 2: lane j copies walker lane j's ring to
-// its entry slots (ebase ~0: none) in groups of WGS entries (WGS x 8 bytes,
-// aligned: slot runs start on kSlotAlign entries) as they are published, the
-// last partial group when the chain is done; every slot below ecap only.
-// Whole groups: a 64-byte group is half an L2 line, and scattered half-line
-// writes among the walk's random line reads cost far more than their bytes
-// (C4: 0.7 GB of 64-byte entry groups made the walk 1.50 ms, 1.00 without).
-// NTW: the group stores non-temporal.
-template <int WGS, bool NTW = false>
+// its entry slots (ebase ~0: none) in groups of kWriterGroup entries (256
+// bytes, aligned: slot runs start on kSlotAlign entries) as they are
+// published, the last partial group when the chain is done; every slot below
+// ecap only.  Whole groups: a 64-byte group is half an L2 line, and scattered
+// half-line writes among the walk's random line reads cost far more than their
+// bytes (256-byte groups 1.262 ms on C4, 128-byte 1.284, 64-byte 1.345;
+// profiles/r03_compact_entries_ab.jsonl).
 __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries, WalkRing ring, uint64_t ebase,
                                                  uint64_t ecap) {
-  static_assert(WGS == 8 || WGS == 16 || WGS == 32, "group of 8, 16 or 32 entries");
-  static_assert(WGS <= (int)kSlotAlign, "groups aligned by the slot runs");
+  static_assert(kWriterGroup <= kSlotAlign, "groups aligned by the slot runs");
   uint32_t t = 0;
   bool fin = false;
   for (;;) {
@@ -691,28 +607,23 @@ __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries
       const uint32_t hv = lds_ld(ring.head);
       __asm__ volatile("" ::: "memory");  // the entries after the head that published them
       const uint32_t h = hv & ~kRingDone;
-      while (h - t >= (uint32_t)WGS) {
-        WalkEntry g[WGS];
+      while (h - t >= kWriterGroup) {
+        WalkEntry g[kWriterGroup];
 #pragma unroll
-        for (int k = 0; k < WGS; ++k) g[k] = ring.e[(t + k) & ring.mask];
-        if (ebase != ~0ull && t + WGS <= ecap) {
-          u32x4* d = reinterpret_cast<u32x4*>(entries + ebase + t);  // WGS x 8-byte aligned
+        for (uint32_t k = 0; k < kWriterGroup; ++k) g[k] = ring.e[(t + k) & (kRing - 1)];
+        if (ebase != ~0ull && t + kWriterGroup <= ecap) {
+          u32x4* d = reinterpret_cast<u32x4*>(entries + ebase + t);  // 256-byte aligned
 #pragma unroll
-          for (int k = 0; k < WGS / 2; ++k) {
-            const u32x4 v = {g[2 * k].mask, g[2 * k].w, g[2 * k + 1].mask, g[2 * k + 1].w};
-            if constexpr (NTW)
-              __builtin_nontemporal_store(v, d + k);
-            else
-              d[k] = v;
-          }
+          for (uint32_t k = 0; k < kWriterGroup / 2; ++k)
+            d[k] = u32x4{g[2 * k].mask, g[2 * k].w, g[2 * k + 1].mask, g[2 * k + 1].w};
         }
-        t += WGS;
+        t += kWriterGroup;
         __asm__ volatile("" ::: "memory");
         lds_st(ring.tail, t);
       }
       if (hv & kRingDone) {
         for (; t < h; ++t)
-          if (ebase != ~0ull && t < ecap) entries[ebase + t] = ring.e[t & ring.mask];
+          if (ebase != ~0ull && t < ecap) entries[ebase + t] = ring.e[t & (kRing - 1)];
         fin = true;
       }
     }
@@ -721,35 +632,14 @@ __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries
   }
 }
 
-// Budgeted walk (BUD, with k_walk_resume): a C4-sized batch (65 536 chains,
-// mean 668 frames, longest 1 204) walks for its LONGEST chain, and the last
-// few hundred steps run on a chip that is otherwise done.
-// With BUD every lane stops after `budget` frames (~ the mean chain, from the
-// context's history); the connections that finished write their results and
-// the record-pass rows of a split walk (row c*ks = the whole stream, rows
-// c*ks+1.. empty), the others append their state to a resume list that
-// k_walk_resume walks KS-wide from where they stopped.  Entries go to row
-// c*ks's slot run, so the resumption's row 0 continues them in place.  An
-// unfinished connection adds nothing to its block partial but the order flag;
-// k_walk_resume adds its totals.
-struct WalkResume {
-  uint32_t c, rec;
-  uint64_t pos, nf, pb, pl, same, lastf, firstf;
-};
-static_assert(sizeof(WalkResume) == 64, "one resume record per 64 bytes");
-
-template <int D, bool GRP, bool NTH = false, int PF = 0, bool BUD = false, int UNR = 2, int ST = 0, int WGS = 32,
-          int WM = 0>
+// 1. The counting walk: one lane per connection (wave 0), and with ST 2 a
+// second wave that writes the walkers' entries.
+template <int D, int ST>
 __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_walk_count(
     const uint8_t* __restrict__ in, const gevws_conn_in* __restrict__ conns, uint32_t n,
     gevws_conn_out* __restrict__ cout, uint64_t* __restrict__ blk, WalkEntry* __restrict__ entries, uint64_t n_entries,
     uint32_t gshift, uint32_t cpb, uint64_t in_bytes, uint32_t* __restrict__ done, uint64_t max_frames,
-    uint64_t payload_cap, gevws_summary* __restrict__ sum, uint64_t budget = ~0ull, uint32_t ks = 1,
-    gevws_conn_in* __restrict__ segs = nullptr, gevws_conn_out* __restrict__ sout = nullptr,
-    uint8_t* __restrict__ srec = nullptr, WalkResume* __restrict__ rlist = nullptr,
-    uint32_t* __restrict__ rcount = nullptr) {
-  // ST 2: wave 0 walks (lane = connection), wave 1 writes its entries
-  constexpr uint32_t kRing = ring_size<WGS>();
+    uint64_t payload_cap, gevws_summary* __restrict__ sum) {
   __shared__ WalkEntry s_ring[ST == 2 ? kCountBlock * kRing : 1];
   __shared__ uint32_t s_head[ST == 2 ? kCountBlock : 1], s_tail[ST == 2 ? kCountBlock : 1];
   __shared__ uint64_t s_ebase[ST == 2 ? kCountBlock : 1], s_ecap[ST == 2 ? kCountBlock : 1];
@@ -758,11 +648,8 @@ __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_wal
   const uint32_t c = blockIdx.x * cpb + lane;
   const bool active = walker && lane < cpb && c < n;
   uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0;
-  bool more = false;
-  WalkRes R = walk_res_fresh();
   gevws_conn_in ci = {0, 0};
   int32_t st = GEVWS_OK;
-  const uint64_t v0 = BUD ? (uint64_t)c * ks : c;  // entry slot run / sink of the connection's first row
   uint64_t ebase = 0, ecap = 0;
   bool rec0 = false;
   if (active) {
@@ -777,9 +664,9 @@ __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_wal
       st = GEVWS_ERR_INVALID;
       err += 1;
     }
-    rec0 = entry_slots_of(ci, (uint32_t)v0, n_entries, gshift, ebase, ecap);
+    rec0 = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
   }
-  const WalkRing ring = {s_ring + lane * kRing, kRing - 1, s_head + lane, s_tail + lane};
+  const WalkRing ring = {s_ring + lane * kRing, s_head + lane, s_tail + lane};
   if constexpr (ST == 2) {
     if (walker) {
       s_head[lane] = active ? 0u : kRingDone;
@@ -788,71 +675,23 @@ __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_wal
       s_ecap[lane] = ecap;
     }
     __syncthreads();
-    // WM (measurement): 1 = the writer drains the ring but stores nothing (the
-    // record pass re-walks); 2 = non-temporal group stores
-    if (!walker) walk_ring_writer<WGS, WM == 2>(entries, ring, WM == 1 ? ~0ull : s_ebase[lane], s_ecap[lane]);
+    if (!walker) walk_ring_writer(entries, ring, s_ebase[lane], s_ecap[lane]);
   }
   if (active) {
-    R = walk_res_fresh(err, st);
-    walk_chain<D, GRP, NTH, PF, UNR, ST>(in + ci.off, ci.len, rec0 && WM != 1, ebase, ecap, entries,
-                                         entries + n_entries + v0, R,
-                                         BUD ? budget : ~0ull, ring);
-    more = BUD && R.more;
-    if (!more) {
-      nf = R.nf;
-      pb = R.pb;
-      pl = R.pl;
-      err = R.err;
-      same = R.same;
-      gevws_conn_out o;
-      o.first_frame = R.rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
-      o.consumed = R.pos;
-      o.payload_base = pb;  // per-connection arena bytes; k_walk_emit turns it into a base
-      o.nframes = (uint32_t)nf;
-      o.status = R.st;
-      cout[c] = o;
-      if constexpr (BUD) {  // the record pass's rows: the whole stream, then empty rows
-        segs[v0] = ci;
-        gevws_conn_out so;
-        so.first_frame = 0;
-        so.consumed = R.pos;
-        so.payload_base = 0;
-        so.nframes = (uint32_t)nf;
-        so.status = R.st;
-        sout[v0] = so;
-        srec[v0] = R.rec ? 1 : 0;
-        so.consumed = 0;
-        so.nframes = 0;
-        so.status = GEVWS_OK;
-        for (uint32_t k = 1; k < ks; ++k) {
-          segs[v0 + k] = gevws_conn_in{ci.off + ci.len, 0};
-          sout[v0 + k] = so;
-          srec[v0 + k] = 0;
-        }
-      }
-    }
-  }
-  if constexpr (BUD) {
-    // append the unfinished connections to the resume list (one atomic per wave)
-    const uint64_t m = __ballot(more);
-    if (m) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(rcount, (uint32_t)__popcll(m));
-      base = (uint32_t)__shfl((int)base, 0, 64);
-      if (more) {
-        WalkResume w;
-        w.c = c;
-        w.rec = R.rec ? 1u : 0u;
-        w.pos = R.pos;
-        w.nf = R.nf;
-        w.pb = R.pb;
-        w.pl = R.pl;
-        w.same = R.same;
-        w.lastf = R.lastf;
-        w.firstf = R.firstf;
-        rlist[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = w;
-      }
-    }
+    WalkRes R = walk_res_fresh(err, st);
+    walk_chain<D, ST>(in + ci.off, ci.len, rec0, ebase, ecap, entries, entries + n_entries + c, R, ring);
+    nf = R.nf;
+    pb = R.pb;
+    pl = R.pl;
+    err = R.err;
+    same = R.same;
+    gevws_conn_out o;
+    o.first_frame = R.rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
+    o.consumed = R.pos;
+    o.payload_base = pb;  // per-connection arena bytes; k_walk_emit turns it into a base
+    o.nframes = (uint32_t)nf;
+    o.status = R.st;
+    cout[c] = o;
   }
   // block partial sums (one wave)
   const uint64_t vals[kDecFields] = {nf, pb, pl, err, same};
@@ -898,7 +737,6 @@ constexpr int kSyncDepth = 5;                     // consecutive plausible heade
 constexpr uint64_t kSplitMinBytes = 16384;        // a connection's segments are at least this long
 constexpr uint32_t kSplitMaxLanes = 32;
 constexpr uint32_t kSplitAutoMaxLanes = 16;  // the auto choice's largest split
-constexpr uint32_t kResumeMaxLanes = 16;
 constexpr uint64_t kSplitLanesPerCU = 512;        // auto: split while the walk has fewer lanes per CU
 // auto: split only after a decode on this context whose connections averaged
 // this many frames of at most this many payload bytes (the long chains of
@@ -1054,7 +892,7 @@ __device__ __forceinline__ bool sync_search(const uint8_t* __restrict__ s, uint6
   return false;
 }
 
-template <int KS, int D, bool GRP>
+template <int KS, int D>
 __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __restrict__ in,
                                                             const gevws_conn_in* __restrict__ conns, uint32_t n,
                                                             gevws_conn_out* __restrict__ cout,
@@ -1065,7 +903,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
                                                             uint64_t payload_cap, gevws_summary* __restrict__ sum,
                                                             gevws_conn_in* __restrict__ segs,
                                                             gevws_conn_out* __restrict__ sout,
-                                                            uint8_t* __restrict__ srec, int mode,
+                                                            uint8_t* __restrict__ srec,
                                                             uint64_t min_seg = kSplitMinBytes) {
   static_assert(KS >= 2 && KS <= (int)kSplitMaxLanes && (KS & (KS - 1)) == 0, "KS: a power of two");
   __shared__ uint32_t s_row[kCountBlock * kSyncRow];
@@ -1085,7 +923,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
   // after i/kc of the stream (kc: segments of >= kSplitMinBytes)
   bool found = active && i == 0;
   uint64_t b = 0;
-  if (active && i > 0 && mode != 2) {  // mode 2 (measurement): no guesses
+  if (active && i > 0) {
     const uint64_t kc = ci.len / min_seg < KS ? ci.len / min_seg : KS;
     if (i < kc) {
       // windows spread over the first half of the segment; guesses below
@@ -1096,7 +934,6 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
       found = sync_search(s, ci.len, t, step, t + seg * 3 / 4, m0, s_row + (threadIdx.x) * kSyncRow, b);
     }
   }
-  if (mode == 1 && i > 0) found = false;  // mode 1 (measurement): guesses made, then dropped
   // 2. a segment ends at the next lane's guess (or the stream's end);
   // lanes without a guess hold an empty segment there
   const uint64_t mine = found ? b : ~0ull;
@@ -1113,7 +950,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
   uint64_t ebase = 0, ecap = 0;
   const bool rec0 = active && entry_slots_of(sg, (uint32_t)v, n_entries, gshift, ebase, ecap);
   WalkRes R = walk_res_fresh();
-  if (active) walk_chain<D, GRP>(in + sg.off, sg.len, rec0, ebase, ecap, entries, entries + n_entries + v, R);
+  if (active) walk_chain<D>(in + sg.off, sg.len, rec0, ebase, ecap, entries, entries + n_entries + v, R);
   // 4. stitch the group's KS lanes (every lane takes part in the shuffles)
   const bool last = found && end == ci.len;
   const bool ok = !found || last || (R.st == GEVWS_OK && R.pos == slen);
@@ -1186,7 +1023,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
         // a guess missed: the whole chain, serially (no entries: the record
         // pass re-walks it as one segment)
         WalkRes S = walk_res_fresh();
-        walk_chain<0, false>(s, ci.len, false, 0, 0, entries, entries + n_entries + v, S);
+        walk_chain<0>(s, ci.len, false, 0, 0, entries, entries + n_entries + v, S);
         nf = S.nf;
         pb = S.pb;
         pl = S.pl;
@@ -1222,602 +1059,6 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
     }
   }
   if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
-}
-
-// ------------------------------------------------------------------ 1b. walk (count), resumed
-// The budgeted walk's unfinished connections (k_walk_count BUD), KS lanes
-// each, k_walk_split's way from where the chain stopped: lane 0 goes on from
-// the saved position in row 0 (its entries continue the ones already in that
-// row's slot run), lane i > 0 guesses a frame start near i/KS of the REST of
-// the stream and walks [its guess, the next guess) as row i; the rows are
-// accepted when every one but the last ends exactly on its end (induction
-// from lane 0's true position), else lane 0 walks the rest serially and the
-// record pass re-walks the connection as one row.  Persistent grid over the
-// list (its length is known only on the device).  Each connection's totals go
-// into its walk block's partials (atomics; the scan runs after this launch).
-constexpr uint32_t kResumeLanes = 8;       // default lanes per resumed connection
-constexpr uint64_t kResumeBlocksPerCU = 16;
-constexpr uint32_t kBudgetFrac16 = 18;     // default budget: 18/16 of the previous batch's mean chain
-template <int KS, int D>
-__global__ __launch_bounds__(kCountBlock) void k_walk_resume(const uint8_t* __restrict__ in,
-                                                             const gevws_conn_in* __restrict__ conns,
-                                                             gevws_conn_out* __restrict__ cout,
-                                                             uint64_t* __restrict__ blk,
-                                                             WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                             uint32_t gshift, uint32_t cpb,
-                                                             const WalkResume* __restrict__ rlist,
-                                                             const uint32_t* __restrict__ rcount,
-                                                             gevws_conn_in* __restrict__ segs,
-                                                             gevws_conn_out* __restrict__ sout,
-                                                             uint8_t* __restrict__ srec) {
-  static_assert(KS >= 2 && KS <= (int)kResumeMaxLanes && (KS & (KS - 1)) == 0, "KS: a power of two");
-  __shared__ uint32_t s_row[kCountBlock * kSyncRow];
-  constexpr uint32_t G = kCountBlock / KS;  // connections per workgroup per round
-  const uint32_t lane = threadIdx.x & 63, i = lane % KS;
-  const uint32_t cnt = uniform32(__hip_atomic_load(rcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  for (uint32_t base = blockIdx.x * G; base < cnt; base += gridDim.x * G) {  // wave-uniform
-    const uint32_t r = base + threadIdx.x / KS;
-    const bool active = r < cnt;
-    WalkResume w = {0, 0, 0, 0, 0, 0, 0, ~0ull, 0};
-    gevws_conn_in ci = {0, 0};
-    if (active) {
-      w = rlist[r];
-      ci = conns[w.c];
-    }
-    const uint8_t* s = in + ci.off;
-    const uint64_t v = (uint64_t)w.c * KS + i;
-    // 1. guesses in the rest of the stream [w.pos, len)
-    bool found = active && i == 0;
-    uint64_t b = 0;
-    if (active && i > 0) {
-      const uint64_t rem = ci.len - w.pos;
-      const uint64_t kc = rem / kSplitMinBytes < KS ? rem / kSplitMinBytes : KS;
-      if (i < kc) {
-        const uint64_t seg = rem / kc, t = w.pos + rem * i / kc;
-        const uint64_t step = seg / (2 * kSyncWindows) > kSyncWin ? seg / (2 * kSyncWindows) : kSyncWin;
-        const uint32_t m0 = (uint32_t)s[1] >> 7;  // the first frame's mask bit
-        found = sync_search(s, ci.len, t, step, t + seg * 3 / 4, m0, s_row + threadIdx.x * kSyncRow, b);
-      }
-    }
-    // 2. a row ends at the next lane's guess (or the stream's end)
-    const uint64_t mine = found ? b : ~0ull;
-    uint64_t end = ci.len;
-#pragma unroll
-    for (int j = KS - 1; j >= 1; --j) {
-      const uint64_t y = __shfl(mine, (int)((lane + j) & 63), 64);
-      if ((int)i + j < KS && y != ~0ull) end = y;
-    }
-    // row 0 is the stream's start to the first guess (walked from w.pos on)
-    const uint64_t rb = i == 0 ? 0 : (found ? b : end);
-    const gevws_conn_in sg = {ci.off + rb, found ? end - rb : 0};
-    uint64_t ebase = 0, ecap = 0;
-    bool rec0 = active && entry_slots_of(sg, (uint32_t)v, n_entries, gshift, ebase, ecap);
-    WalkRes R = walk_res_fresh();
-    if (i == 0) {
-      R.pos = w.pos;
-      R.nf = w.nf;
-      R.pb = w.pb;
-      R.pl = w.pl;
-      R.same = w.same;
-      R.lastf = w.lastf;
-      R.firstf = w.firstf;
-      // the entries already stored must fit row 0's (shorter) slot run
-      rec0 = rec0 && w.rec && w.nf <= ecap;
-    }
-    if (active) walk_chain<D, false>(in + sg.off, sg.len, rec0, ebase, ecap, entries, entries + n_entries + v, R);
-    // 3. stitch the group's KS lanes (every lane takes part in the shuffles)
-    const bool last = found && end == ci.len;
-    const bool ok = !found || last || (R.st == GEVWS_OK && R.pos == sg.len);
-    uint64_t prevlast = ~0ull;
-    bool got = false;
-#pragma unroll
-    for (int d = 1; d < KS; ++d) {
-      const uint64_t ynf = __shfl_up(R.nf, d, 64), ylast = __shfl_up(R.lastf, d, 64);
-      if (!got && (int)i >= d && ynf > 0) {
-        prevlast = ylast;
-        got = true;
-      }
-    }
-    // (row 0's own count already runs across the budget boundary)
-    const uint64_t same = R.same + ((i > 0 && R.nf > 0 && got && R.firstf == prevlast) ? 1 : 0);
-    uint64_t inf = R.nf, ipb = R.pb;
-#pragma unroll
-    for (int d = 1; d < KS; d <<= 1) {
-      const uint64_t a = __shfl_up(inf, d, 64), q = __shfl_up(ipb, d, 64);
-      if ((int)i >= d) {
-        inf += a;
-        ipb += q;
-      }
-    }
-    uint64_t t_nf = R.nf, t_pb = R.pb, t_pl = R.pl, t_same = same;
-    uint64_t t_cons = last ? rb + R.pos : 0;
-    int32_t t_st = last ? R.st : 0;
-    int t_ok = ok ? 1 : 0;
-#pragma unroll
-    for (int d = KS / 2; d >= 1; d >>= 1) {
-      t_nf += __shfl_xor(t_nf, d, 64);
-      t_pb += __shfl_xor(t_pb, d, 64);
-      t_pl += __shfl_xor(t_pl, d, 64);
-      t_same += __shfl_xor(t_same, d, 64);
-      t_cons += __shfl_xor(t_cons, d, 64);
-      t_st += __shfl_xor(t_st, d, 64);
-      t_ok &= __shfl_xor(t_ok, d, 64);
-    }
-    if (!active) continue;
-    const bool valid = t_ok != 0;
-    if (!valid && i == 0) {
-      // a guess missed: the rest of the chain serially from where the budget
-      // stopped it (no entries: the record pass re-walks the connection)
-      WalkRes S = walk_res_fresh();
-      S.pos = w.pos;
-      S.nf = w.nf;
-      S.pb = w.pb;
-      S.pl = w.pl;
-      S.same = w.same;
-      S.lastf = w.lastf;
-      S.firstf = w.firstf;
-      walk_chain<0, false>(s, ci.len, false, 0, 0, entries, entries + n_entries + v, S);
-      t_nf = S.nf;
-      t_pb = S.pb;
-      t_pl = S.pl;
-      t_same = S.same;
-      t_cons = S.pos;
-      t_st = S.st;
-    }
-    gevws_conn_out so;
-    if (valid) {
-      segs[v] = sg;
-      so.first_frame = inf - R.nf;  // relative to the connection's first frame
-      so.consumed = R.pos;
-      so.payload_base = ipb - R.pb;  // relative to the connection's payload base
-      so.nframes = (uint32_t)R.nf;
-      so.status = R.st;
-      srec[v] = R.rec ? 1 : 0;
-    } else {  // one row: the whole connection, re-walked by the record pass
-      segs[v] = i == 0 ? ci : gevws_conn_in{ci.off + ci.len, 0};
-      so.first_frame = 0;
-      so.consumed = 0;
-      so.payload_base = 0;
-      so.nframes = i == 0 ? (uint32_t)t_nf : 0u;
-      so.status = GEVWS_OK;
-      srec[v] = 0;
-    }
-    sout[v] = so;
-    if (i == 0) {
-      gevws_conn_out o;
-      o.first_frame = 0;
-      o.consumed = t_cons;
-      o.payload_base = t_pb;
-      o.nframes = (uint32_t)t_nf;
-      o.status = t_st;
-      cout[w.c] = o;
-      unsigned long long* bp = reinterpret_cast<unsigned long long*>(blk + (uint64_t)(w.c / cpb) * kDecFields);
-      atomicAdd(bp + 0, (unsigned long long)t_nf);
-      atomicAdd(bp + 1, (unsigned long long)t_pb);
-      atomicAdd(bp + 2, (unsigned long long)t_pl);
-      if (t_st < 0) atomicAdd(bp + 3, 1ull);
-      atomicAdd(bp + 4, (unsigned long long)t_same);
-    }
-  }
-}
-
-// ------------------------------------------------------------------ 1a'. walk (count), buffered
-// k_walk_count's chain costs one memory round trip per frame, and a wave
-// waits for its slowest lane at every step, so a C4-sized walk takes about
-// (longest chain) x (loaded latency) -- 1 132-1 204 frames x ~1.3 us.  Half of
-// C4's frames are under 128 bytes, so the next header is often within a few
-// hundred bytes of the current one.  Here each lane reads WB bytes of its
-// stream at once into its own LDS row and walks every frame whose 16-byte
-// header window lies inside that row (an inner loop of LDS reads and parses,
-// no memory wait); only then do the lanes that ran out of row reload, all in
-// the same round trip.  A wave's round trips per chain are the row reloads of
-// its worst lane instead of its frames.  Entries, per-connection results and
-// block partials are exactly k_walk_count's (D = 0).
-template <int WB, bool GRP>
-__global__ __launch_bounds__(kCountBlock) void k_walk_buf(const uint8_t* __restrict__ in,
-                                                          const gevws_conn_in* __restrict__ conns, uint32_t n,
-                                                          gevws_conn_out* __restrict__ cout,
-                                                          uint64_t* __restrict__ blk,
-                                                          WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                          uint32_t gshift, uint32_t cpb, uint64_t in_bytes,
-                                                          uint32_t* __restrict__ done, uint64_t max_frames,
-                                                          uint64_t payload_cap, gevws_summary* __restrict__ sum) {
-  constexpr int NC = WB / 16;
-  static_assert(WB % 16 == 0 && NC >= 2, "whole 16-byte chunks, at least two");
-  __shared__ u32x4 s_row[kCountBlock][NC + 1];  // chunk NC: read (shift 0, unused) by a window at the row's end
-  const uint32_t c = blockIdx.x * cpb + threadIdx.x;
-  uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0, lastf = ~0ull;
-  if (threadIdx.x < cpb && c < n) {
-    gevws_conn_in ci = conns[c];
-    if (out_of_order(conns, c, ci)) err = 1ull << 32;  // as k_walk_count
-    int32_t st = GEVWS_OK;
-    if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
-      ci.off = 0;
-      ci.len = 0;
-      st = GEVWS_ERR_INVALID;
-      err += 1;
-    }
-    const uint8_t* s = in + ci.off;
-    u32x4* row = s_row[threadIdx.x];
-    uint64_t pos = 0, wb = 0;  // row[k] = stream bytes [wb + 16k, wb + 16k + 16)
-    uint64_t ebase = 0, ecap = 0;
-    bool rec = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
-    WalkEntry* sink = entries + n_entries + c;
-    WalkEntry g0 = {0, 0}, g1 = g0, g2 = g0;
-    auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
-      (void)p;
-      rec = rec && nf < ecap;
-      const WalkEntry e = make_entry(key, L, meta);
-      if constexpr (GRP) {
-        if (rec && (nf & 3) == 3) {
-          WalkEntry* g = entries + ebase + (nf - 3);
-          g[0] = g0;
-          g[1] = g1;
-          g[2] = g2;
-          g[3] = e;
-        }
-        g0 = g1;
-        g1 = g2;
-        g2 = e;
-      } else if (rec) {
-        entries[ebase + nf] = e;
-      }
-      ++nf;
-      pb += round16(L);
-      pl += L;
-      const uint64_t f = (uint64_t)(meta >> 16) + L;
-      same += f == lastf;
-      lastf = f;
-    };
-    // the row at stream offset p & ~15: chunks starting past the stream end
-    // are loaded from its end instead (only bytes < len + 16 are ever parsed,
-    // and 16 bytes at any offset <= len stay inside GEVWS_IN_PAD)
-    auto reload = [&](uint64_t p) {
-      wb = p & ~15ull;
-      u32x4 v[NC];
-#pragma unroll
-      for (int k = 0; k < NC; ++k) {
-        const uint64_t a = wb + 16ull * k;
-        v[k] = ld16u(s + (a <= ci.len ? a : ci.len));
-      }
-#pragma unroll
-      for (int k = 0; k < NC; ++k) row[k] = v[k];
-    };
-    reload(0);
-    bool fin = false;
-    for (;;) {
-      while (pos + 16 <= wb + WB) {  // the frame's 16-byte window is in the row
-        const uint32_t o = (uint32_t)(pos - wb), k = o >> 4, r = o & 15u;
-        const u128 x = (u128_of(row[k]) >> (8 * r)) | (r ? u128_of(row[k + 1]) << (128 - 8 * r) : (u128)0);
-        const uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);
-        const uint32_t b1 = (uint32_t)(lo >> 8) & 0xffu;
-        const uint32_t masked = b1 >> 7, len7 = b1 & 0x7fu;
-        const bool e16 = len7 == 126, e64 = len7 == 127;
-        const uint32_t hlen = 2 + (e64 ? 8u : (e16 ? 2u : 0u)) + 4 * masked;
-        const uint64_t L64 = __builtin_bswap64((lo >> 16) | (hi << 48));
-        const uint64_t L16 = (((lo >> 16) & 0xff) << 8) | ((lo >> 24) & 0xff);
-        const uint64_t L = e64 ? L64 : (e16 ? L16 : (uint64_t)len7);
-        const uint64_t avail = ci.len - pos;
-        const bool have_hdr = avail >= 6 && avail >= hlen;  // read.go:20-23, U1
-        const bool msb = e64 && (L64 >> 63);                 // read.go:71-73
-        if (!have_hdr || msb || avail - hlen < L) {          // protocol.go:47 gate
-          if (have_hdr && msb) { st = GEVWS_ERR_LEN_MSB; err += 1; }
-          fin = true;
-          break;
-        }
-        const uint32_t key = (e64 ? (uint32_t)(hi >> 16) : (e16 ? (uint32_t)(lo >> 32) : (uint32_t)(lo >> 16))) &
-                             (0u - masked);
-        put_entry(pos, key, L, ((uint32_t)lo & 0xffu) | (masked << 8) | (hlen << 16));
-        pos += hlen + L;
-      }
-      if (fin) break;
-      reload(pos);
-    }
-    (void)sink;
-    if (GRP && rec) {  // the last nf % 4 entries
-      const uint32_t r = (uint32_t)(nf & 3);
-      WalkEntry* g = entries + ebase + (nf - r);
-      if (r == 3) {
-        g[0] = g0;
-        g[1] = g1;
-        g[2] = g2;
-      } else if (r == 2) {
-        g[0] = g1;
-        g[1] = g2;
-      } else if (r == 1) {
-        g[0] = g2;
-      }
-    }
-    gevws_conn_out o;
-    o.first_frame = rec ? 1 : 0;
-    o.consumed = pos;
-    o.payload_base = pb;
-    o.nframes = (uint32_t)nf;
-    o.status = st;
-    cout[c] = o;
-  }
-  const uint64_t vals[kDecFields] = {nf, pb, pl, err, same};
-#pragma unroll
-  for (int k = 0; k < kDecFields; ++k) {
-    const uint64_t sm = wave_sum(vals[k]);
-    if (threadIdx.x == 0) {
-      if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + k, sm);
-      else blk[(uint64_t)blockIdx.x * kDecFields + k] = sm;
-    }
-  }
-  if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
-}
-
-// ------------------------------------------------------------------ 1b. walk (count), one wave per connection
-// k_walk_count gives each connection one lane, one dependent header load per
-// frame: right for batches of many connections (C4's 65 536: the memory
-// system is kept busy by the chains' sheer number), but a batch of few
-// connections -- a GPU's LPT share of a strong split, C5 -- is bound by its
-// longest chain (C4: 1 204 frames, ~0.54 us per step on a lightly loaded
-// chip, profiles/r01_c4_strong_projection.jsonl).  Here a whole wave walks one
-// connection and shortens the chain's critical path two ways:
-//
-//  * ring mode: the wave streams the stream through a per-wave LDS ring of
-//    two K KiB halves (coalesced 16-byte loads, one chunk per lane per KiB);
-//    frames whose header lies in the ring are parsed out of LDS (a few LDS
-//    reads per frame instead of an HBM round trip), the next contiguous half
-//    is in flight while the wave walks the current one, and a frame that
-//    jumps past the ring (a big payload) reloads the ring at its end;
-//  * ballot mode: after three frames of equal size F, lane j loads the
-//    16-byte window at pos + j F and parses it; a ballot of "a complete frame
-//    of size F" gives the run's length -- up to 64 frames per memory latency,
-//    exactly the frames the serial chain would have found (each candidate is
-//    checked, the first non-matching one ends the batch and the walk goes on
-//    from the true position).
-//
-// Entries (the same WalkEntry slot runs as k_walk_count, so k_walk_emit is
-// shared) are gathered one per lane and stored 64 at a time (1 KiB coalesced).
-// Results are identical to k_walk_count's by construction: the chain is the
-// same serial chain, only where its header bytes come from differs.
-constexpr int kSpanWaves = 4;  // connections (waves) per workgroup
-
-template <int K>
-__global__ __launch_bounds__(kSpanWaves * 64) void k_walk_span(const uint8_t* __restrict__ in,
-                                                             const gevws_conn_in* __restrict__ conns, uint32_t n,
-                                                             gevws_conn_out* __restrict__ cout,
-                                                             uint64_t* __restrict__ blk,
-                                                             WalkEntry* __restrict__ entries, uint64_t n_entries,
-                                                             uint32_t gshift, uint64_t in_bytes,
-                                                             uint32_t* __restrict__ done, uint64_t max_frames,
-                                                             uint64_t payload_cap, gevws_summary* __restrict__ sum) {
-  constexpr uint64_t S = (uint64_t)K * 1024;  // bytes per ring half
-  constexpr uint32_t RW = (uint32_t)(2 * S / 8);  // ring words (u64) per wave
-  __shared__ uint64_t s_ring[kSpanWaves][RW];
-  __shared__ uint64_t s_part[kSpanWaves][kDecFields];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t c = blockIdx.x * kSpanWaves + wave;
-  uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0;  // wave-uniform
-  if (c < n) {
-    gevws_conn_in ci = conns[c];
-    ci.off = uniform64(ci.off);
-    ci.len = uniform64(ci.len);
-    if (out_of_order(conns, c, ci)) err = 1ull << 32;  // as k_walk_count (k_scan_blocks SPLIT)
-    int32_t st = GEVWS_OK;
-    if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
-      ci.off = 0;
-      ci.len = 0;
-      st = GEVWS_ERR_INVALID;
-      err += 1;
-    }
-    uint64_t ebase = 0, ecap = 0;
-    bool rec = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
-    uint64_t* ring = s_ring[wave];
-    const uint64_t sbeg = reinterpret_cast<uint64_t>(in) + ci.off;  // stream bytes [sbeg, send)
-    const uint64_t send = sbeg + ci.len;
-    // one K KiB half: chunk k * 64 + lane, loaded only where it holds stream bytes
-    auto issue = [&](uint64_t b, u32x4 (&v)[K]) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const uint64_t a = b + (uint64_t)(k * 64 + lane) * 16;
-        v[k] = a < send ? *reinterpret_cast<const u32x4*>(a) : u32x4{0, 0, 0, 0};
-      }
-    };
-    auto put = [&](uint64_t b, const u32x4 (&v)[K]) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const uint32_t w = (uint32_t)(((b >> 3) + 2ull * (k * 64 + lane)) % RW);  // even: b is 16-aligned
-        ring[w] = (uint64_t)v[k][0] | ((uint64_t)v[k][1] << 32);
-        ring[w + 1] = (uint64_t)v[k][2] | ((uint64_t)v[k][3] << 32);
-      }
-      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave reads other lanes' words next
-    };
-    // entries: entry i sits in lane i % 64 until its group of 64 is stored
-    WalkEntry my = {0, 0};
-    uint64_t flushed = 0;  // entries [0, flushed) are stored
-    auto flush = [&]() {
-      if (rec && nf > flushed) {
-        const uint64_t g = (nf - 1) & ~63ull;  // the group of the unstored entries
-        const uint64_t i = g + lane;
-        if (i >= flushed && i < nf) entries[ebase + i] = my;
-      }
-      flushed = nf;
-    };
-    auto put_entry = [&](uint64_t p, uint32_t key, uint64_t L, uint32_t meta) {
-      rec = rec && nf < ecap;
-      (void)p;
-      if (lane == (uint32_t)(nf & 63)) my = make_entry(key, L, meta);
-      ++nf;
-      pb += round16(L);
-      pl += L;
-      if ((nf & 63) == 0) flush();
-    };
-    uint64_t pos = 0, prev_fsz = 0;
-    uint32_t run = 0;
-    // ring state: [rb, rb + S) is written; [rb + S, rb + 2S) is in `nv` (in flight) until hi_ready
-    uint64_t rb = sbeg & ~15ull;
-    bool hi_ready = false;
-    u32x4 nv[K];
-    {
-      u32x4 v0[K];
-      issue(rb, v0);
-      issue(rb + S, nv);
-      put(rb, v0);
-    }
-    for (;;) {
-      const uint64_t x = sbeg + pos;
-      const uint64_t avail = ci.len - pos;
-      if (avail < 6) break;  // read.go:20-23
-      if (run >= 3) {
-        // ---- ballot mode: lane j checks the frame at pos + j F
-        const uint64_t F = prev_fsz;
-        const uint64_t q = pos + (uint64_t)lane * F;
-        const bool inside = q < ci.len;
-        uint64_t lo, hi;
-        load_window(reinterpret_cast<const uint8_t*>(sbeg + (inside ? q : ci.len)), lo, hi);
-        uint32_t m2 = 0, h2 = 0, k2 = 0;
-        uint64_t L2 = 0;
-        const int r = walk_parse(lo, hi, inside ? ci.len - q : 0, m2, h2, L2, k2);
-        const bool ok = inside && r == GEVWS_OK && h2 + L2 == F;
-        const uint64_t okm = __ballot(ok);
-        const uint32_t k = okm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);  // leading run of matches
-        if (k > 0) {
-          flush();  // the buffered group goes out before the direct stores
-          rec = rec && nf + k <= ecap;
-          if (rec && lane < k) entries[ebase + nf + lane] = make_entry(k2, L2, m2);
-          const uint64_t add_pb = wave_sum(lane < k ? round16(L2) : 0);
-          const uint64_t add_pl = wave_sum(lane < k ? L2 : 0);
-          nf += k;
-          pb += add_pb;
-          pl += add_pl;
-          same += k;  // each frame of the batch has the run's size F
-          flushed = nf;
-          pos += (uint64_t)k * F;
-        }
-        if (k < 64) run = 0;  // the frame at pos differs (or the stream ends there): ring mode
-        continue;
-      }
-      // ---- ring mode: bring the header window [x, x + 16) into the ring
-      if (x >= rb + S) {
-        if (x < rb + 2 * S) {  // into the upper half: slide by one half, prefetch the next
-          if (!hi_ready) put(rb + S, nv);
-          rb += S;
-          issue(rb + S, nv);
-        } else {  // past the ring: reload it at the header
-          rb = x & ~15ull;
-          u32x4 v0[K];
-          issue(rb, v0);
-          issue(rb + S, nv);
-          put(rb, v0);
-        }
-        hi_ready = false;
-      }
-      if (x + 16 > rb + S && !hi_ready) {  // the window reaches into the upper half
-        put(rb + S, nv);
-        hi_ready = true;
-      }
-      // the chain is serial and wave-uniform: read the words once into SGPRs
-      // so the parse runs on the scalar unit (as VALU work it is repeated by
-      // all 64 lanes and, with 32 waves per CU, bound by VALU issue)
-      const uint64_t qw = x >> 3;
-      const uint32_t sh = (uint32_t)(x & 7) * 8;
-      const uint64_t w0 = uniform64(ring[qw % RW]), w1 = uniform64(ring[(qw + 1) % RW]),
-                     w2 = uniform64(ring[(qw + 2) % RW]);
-      const uint64_t lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-      const uint64_t hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
-      uint32_t meta, hlen, key;
-      uint64_t L;
-      const int r = walk_parse(lo, hi, avail, meta, hlen, L, key);
-      if (r != GEVWS_OK) {
-        if (r == GEVWS_ERR_LEN_MSB) {
-          st = GEVWS_ERR_LEN_MSB;
-          err += 1;
-        }
-        break;
-      }
-      put_entry(pos, key, L, meta);
-      const uint64_t fsz = hlen + L;
-      same += fsz == prev_fsz;
-      run = fsz == prev_fsz ? run + 1 : 1;
-      prev_fsz = fsz;
-      pos += fsz;
-    }
-    flush();
-    if (lane == 0) {
-      gevws_conn_out o;
-      o.first_frame = rec ? 1 : 0;  // scratch flag for k_walk_emit: entries recorded
-      o.consumed = pos;
-      o.payload_base = pb;
-      o.nframes = (uint32_t)nf;
-      o.status = st;
-      cout[c] = o;
-    }
-  }
-  if (lane == 0) {
-    s_part[wave][0] = nf;
-    s_part[wave][1] = pb;
-    s_part[wave][2] = pl;
-    s_part[wave][3] = err;
-    s_part[wave][4] = same;
-  }
-  __syncthreads();
-  if (threadIdx.x < kDecFields) {
-    uint64_t sm = 0;
-#pragma unroll
-    for (int w = 0; w < kSpanWaves; ++w) sm += s_part[w][threadIdx.x];
-    if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + threadIdx.x, sm);
-    else blk[(uint64_t)blockIdx.x * kDecFields + threadIdx.x] = sm;
-  }
-  if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x < kDecFields);
-}
-
-// ------------------------------------------------------------------ 1b. gather ceiling (measurement)
-// The header walk's access pattern without its parsing: every lane fetches
-// `per_lane` 16-byte windows at random 128-byte lines of an n-byte buffer.
-// DEP: each address depends on the previous load's data (a chain, one load in
-// flight per lane, like the walk); else the lane issues 8 independent loads
-// at a time -- the random-line fetch rate of HBM, the walk's roofline.
-template <int LK>
-__device__ __forceinline__ uint64_t gather_load(const uint8_t* p) {
-  // LK 0: one plain 16-byte load; 1 / 2: two aligned 8-byte relaxed atomic
-  // loads at system / agent scope (gfx950: sc0 sc1 / sc1 -- miss L2 and
-  // fetch from memory); 3: one 4-byte system-scope load
-  if constexpr (LK == 0) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(p);
-    return (uint64_t)v[0] ^ v[2];
-  } else if constexpr (LK == 3) {
-    return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  } else {
-    constexpr int sc = LK == 1 ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
-    const uint64_t a = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, sc);
-    const uint64_t b = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p + 8), __ATOMIC_RELAXED, sc);
-    return a ^ b;
-  }
-}
-
-template <bool DEP, int LK = 0>
-__global__ __launch_bounds__(kCountBlock) void k_gather(const uint8_t* __restrict__ in, uint64_t lines,
-                                                        uint32_t per_lane, uint64_t seed, uint64_t* __restrict__ sink) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t x = seed ^ (g * 0x9E3779B97F4A7C15ull), acc = 0;
-  auto mix = [](uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-  };
-  if constexpr (DEP) {
-    for (uint32_t k = 0; k < per_lane; ++k) {
-      x = mix(x + acc);
-      const uint64_t v = gather_load<LK>(in + (x % lines) * 128 + ((x >> 60) & 7) * 16);
-      acc = v & 1u;  // the next address waits for this load's data
-    }
-  } else {
-    for (uint32_t k = 0; k < per_lane; k += 8) {
-      uint64_t v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint64_t z = mix(x + k + j);
-        v[j] = gather_load<LK>(in + (z % lines) * 128 + ((z >> 60) & 7) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc += v[j];
-    }
-  }
-  sink[g] = acc;
 }
 
 // ------------------------------------------------------------------ 2. scan of block partials
@@ -1878,13 +1119,11 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_co
                                                             const uint64_t* __restrict__ blk,
                                                             const gevws_summary* __restrict__ sum,
                                                             uint8_t* __restrict__ rec_flags, uint32_t cpb,
-                                                            uint64_t* __restrict__ stats = nullptr,
-                                                            const uint32_t* __restrict__ rcount = nullptr) {
-  if (stats && blockIdx.x == 0 && threadIdx.x == 0) {  // the split walk's history (see decode_split_lanes)
+                                                            uint64_t* __restrict__ stats = nullptr) {
+  if (stats && blockIdx.x == 0 && threadIdx.x == 0) {  // the context's history (split walk, D, wide grid)
     stats[0] = sum->frames;
     stats[1] = sum->payload_len;
     stats[2] = sum->run_frames;
-    stats[3] = rcount ? *rcount : 0;  // connections the budgeted walk resumed
   }
   if (sum->status != GEVWS_OK) return;  // capacity error: nothing written
   const uint32_t c = blockIdx.x * cpb + threadIdx.x;
@@ -1905,7 +1144,6 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_co
   cout[c] = o;
 }
 
-template <bool NT = false>
 __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, uint32_t* __restrict__ tile_first,
                                             uint64_t f, uint64_t poff, uint64_t src_off, const DevHdr& h) {
   // the 32-byte record as two 16-byte stores: {fin, rsv, opcode, masked,
@@ -1916,48 +1154,29 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
   u32x4* r = reinterpret_cast<u32x4*>(frames + f);
   const u32x4 r0 = u32x4{flags, h.mask, (uint32_t)h.length, (uint32_t)(h.length >> 32)};
   const u32x4 r1 = u32x4{(uint32_t)poff, (uint32_t)(poff >> 32), (uint32_t)src_off, (uint32_t)(src_off >> 32)};
-  if constexpr (NT) {
-    __builtin_nontemporal_store(r0, r);
-    __builtin_nontemporal_store(r1, r + 1);
-  } else {
-    r[0] = r0;
-    r[1] = r1;
-  }
+  r[0] = r0;  // (plain stores: the unmask reads the records from L2 right after;
+  r[1] = r1;  // non-temporal ones made C4's record pass 0.494 -> 0.551 ms, r02_emit_nt_ab.jsonl)
   const uint64_t padded = round16(h.length);
   // output tiles whose first byte lies in [poff, poff + padded)
   for (uint64_t t = (poff + kTile - 1) / kTile; t * kTile < poff + padded; ++t) tile_first[t] = (uint32_t)f;
 }
 
-// 3b. records + tile map, one wave per connection: 64 recorded entries at a
-// time (coalesced), wave prefix sum of their padded lengths -> payload
-// offsets, 64 contiguous 32-byte records per store.  Connections without
-// recorded entries are re-walked afterwards, one lane per connection.
-// U > 1: the entries of up to U rounds (64 each) are requested at once and
-// then turned into records round by round, so a connection of N frames costs
-// ceil(N / 64U) entry-load latencies instead of ceil(N / 64); rounds past the
-// connection's last frame are skipped (wave-uniform), their loads re-read the
-// last entry (one cached line).  Connections of <= 64 frames take one plain
-// round.
-//
-// G > 0 (grouped): a wave takes G consecutive connections at a time, their
-// metadata in one coalesced load (lane j = connection j).  When their
-// recorded frames number at most 64 R, the group's frames are enumerated
-// across connection boundaries -- lane l of round r takes the group's frame
-// r*64 + l, finds its connection by a binary search over the lanes' frame
-// prefix sums (__shfl), and the payload offsets come from a segmented wave
-// scan plus a per-connection carry kept in lane j -- so connections of a few
-// frames (C1: 16 frames of 136 B) fill whole waves instead of 16 lanes of
-// one, and all R rounds' entries are requested at once.  Longer groups take
-// the per-connection rounds above, connection by connection.
-template <bool NT>
-__device__ __forceinline__ WalkEntry ld_entry(const WalkEntry* p) {
-  if constexpr (NT) {
-    const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
-    return WalkEntry{(uint32_t)v, (uint32_t)(v >> 32)};
-  } else {
-    return *p;
-  }
-}
+// 3b. records + tile map from the walk's entries.  A wave takes G
+// consecutive connections at a time, their metadata in one coalesced load
+// (lane j = connection j).  Phase 1: when their recorded frames number at most
+// 64 R, the group's frames are enumerated across connection boundaries --
+// lane l of round r takes the group's frame r*64 + l, finds its connection by
+// a binary search over the lanes' frame prefix sums (__shfl), and the payload
+// offsets come from a segmented wave scan plus a per-connection carry kept in
+// lane j -- so connections of a few frames (C1: 16 frames of 136 B) fill whole
+// waves instead of 16 lanes of one, and all R rounds' entries are requested at
+// once (C4 0.53 -> 0.49 ms against one wave per connection,
+// profiles/r02_emit_ab.jsonl).  Phase 2: longer connections one wave each, 64
+// entries per round, U rounds' entries requested at once (a connection of N
+// frames costs ceil(N / 64U) entry-load latencies), wave prefix sum of the
+// padded lengths -> payload offsets, 64 contiguous 32-byte records per store.
+// Connections without recorded entries are re-walked afterwards, one lane per
+// connection.
 
 // Segmented inclusive wave scan: a segment starts at every lane with head set
 // (and at lane 0).  Every lane must take part.
@@ -2006,11 +1225,9 @@ __device__ __forceinline__ void entry_round(const uint8_t* __restrict__ in, cons
 
 constexpr int kEmitGroup = 16;
 constexpr uint64_t kEmitSplitPerCU = 32;  // record-pass workgroups per CU over k_walk_split's rows
-// NTR (measurement): the entry loads and record stores non-temporal.
 // (Measured and not kept: phase 2 software-pipelined, the next batch's entry
 // loads issued before this batch's rounds -- C4 0.448 -> 0.477 ms, 8-way share
 // 0.094 -> 0.108: the record pass is not bound by its entry loads' latency.)
-template <int U, int G = 0, bool NTR = false>
 __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restrict__ in,
                                                           const gevws_conn_in* __restrict__ conns, uint32_t n,
                                                           const gevws_conn_out* __restrict__ cout,
@@ -2021,6 +1238,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
                                                           uint32_t gshift, const uint8_t* __restrict__ rec_flags,
                                                           const gevws_conn_out* __restrict__ pout = nullptr,
                                                           uint32_t ks = 0) {
+  constexpr int U = 4, G = kEmitGroup;
   if (sum->status != GEVWS_OK) return;
   // k_walk_split's segments: frame / payload offsets relative to connection c / ks
   auto out_of = [&](uint64_t c) {
@@ -2044,7 +1262,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
     h.hlen = entry_hlen(q);
     h.mask = q.mask;
     h.length = L;
-    emit_record<NTR>(frames, tile_first, f, poff, hpos + h.hlen, h);
+    emit_record(frames, tile_first, f, poff, hpos + h.hlen, h);
   };
   // the per-connection rounds (64 entries per round, U rounds per load)
   auto one_conn = [&](uint64_t cnt, uint64_t first_frame, uint64_t payload_base, uint64_t coff, uint64_t ebase) {
@@ -2062,10 +1280,10 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
       carry += __shfl(incl, 63, 64);
       pcarry += __shfl(ip, 63, 64);
     };
-    if (U == 1 || cnt <= 64) {  // wave-uniform
+    if (cnt <= 64) {  // wave-uniform
       for (uint64_t k0 = 0; k0 < cnt; k0 += 64) {
         WalkEntry q = {0, 0};
-        if (k0 + lane < cnt) q = ld_entry<NTR>(ce + k0 + lane);
+        if (k0 + lane < cnt) q = ce[k0 + lane];
         round(q, k0);
       }
     } else {
@@ -2076,7 +1294,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
           // unconditional (clamped to the last entry): a branch around the
           // load would make the compiler wait for it inside the branch
           const uint64_t k = k0 + (uint64_t)u * 64 + lane;
-          q[u] = ld_entry<NTR>(ce + (k < cnt ? k : cnt - 1));
+          q[u] = ce[k < cnt ? k : cnt - 1];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -2086,7 +1304,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
       }
     }
   };
-  if constexpr (G > 0) {
+  {
     // phase 1: groups of G connections, their short connections (<= kShort
     // frames, so a group has at most 64 R) enumerated across boundaries
     constexpr int R = 4;
@@ -2126,7 +1344,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
         kr[r] = t - __shfl(tstart, (int)lo, 64);
         const uint64_t eb = __shfl(ebase, (int)lo, 64);  // (outside the t < T branch: see below)
         q[r] = WalkEntry{0, 0};
-        if (t < T) q[r] = ld_entry<NTR>(entries + eb + kr[r]);
+        if (t < T) q[r] = entries[eb + kr[r]];
       }
       // lane j: its connection's padded bytes and stream bytes already placed
       uint64_t carry = 0, pcarry = 0;
@@ -2193,18 +1411,6 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
         one_conn(cnt, fj, pj, oj, ej);
       }
     }
-  } else {
-  for (uint64_t c = (uint64_t)blockIdx.x * (kWalkBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
-    // everything the connection needs is requested at once (one latency)
-    const gevws_conn_out o = out_of(c);
-    const uint8_t recorded = rec_flags[c];
-    const gevws_conn_in ci = conns[c];
-    const uint64_t cnt = uniform64(o.nframes);  // one connection per wave
-    if (cnt == 0 || !recorded || unordered) continue;  // no frames / re-walked below
-    uint64_t ebase = 0, ecap = 0;
-    entry_slots_of(ci, (uint32_t)c, n_entries, gshift, ebase, ecap);
-    one_conn(cnt, o.first_frame, o.payload_base, ci.off, ebase);
-  }
   }
   // connections without recorded entries: one lane per connection re-walks
   const uint64_t nthreads = (uint64_t)gridDim.x * kWalkBlock;
@@ -2390,21 +1596,21 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
 // with 4 workgroups per CU and, for big frames, all but the first `big_grid`
 // return at once.  big_grid = 0 disables the adaptation (explicit grid).
 constexpr uint64_t kBigFrameBytes = 48 * 1024;
-// k_unmask_auto's wide grid (kWideGridPerCU workgroups per CU instead of 4),
+// k_unmask_auto5's wide grid (kWideGridPerCU workgroups per CU instead of 4),
 // launched when the context's previous decode was a batch of mixed frame
-// sizes (v4) below kWideGridTiles output tiles: there the contiguous runs of
-// 4 workgroups per CU finish unevenly (the window path's cost follows the
-// local frame density) and more, shorter runs balance -- C4's 8-way share
-// (590 K tiles) 1.15 -> 0.99 ms, its 4-way share (1.2 M) 2.15 -> 2.09; the
-// 2-way share (2.4 M), the full C4 (4.7 M tiles), C2, C3, C5 are best at 4
-// per CU (profiles/r02_grid_sweep.jsonl)
+// sizes below kWideGridTiles output tiles: there the contiguous runs of 4
+// workgroups per CU finish unevenly (the window path's cost follows the local
+// frame density) and more, shorter runs balance -- C4's 8-way share (590 K
+// tiles) 1.15 -> 0.99 ms, its 4-way share (1.2 M) 2.15 -> 2.09; the 2-way
+// share (2.4 M), the full C4 (4.7 M tiles), C2, C3, C5 are best at 4 per CU
+// (profiles/r02_grid_sweep.jsonl)
 constexpr uint32_t kWideGridPerCU = 32;
 constexpr uint64_t kWideGridTiles = 2ull << 20;
 
 // Workgroups that take a run of the output: big_grid (low 16 bits: one per CU)
 // for batches of big frames, else the whole grid -- or, when the host
-// launched a wide grid (k_unmask_auto; high 16 bits: the usual grid), the
-// usual grid unless the caller asks for the wide one.
+// launched a wide grid (high 16 bits: the usual grid), the usual grid unless
+// the caller asks for the wide one.
 __device__ __forceinline__ uint32_t active_groups(uint64_t total, uint64_t nframes, uint32_t big_grid,
                                                   bool wide = false) {
   const uint32_t ncu = big_grid & 0xffffu, norm = big_grid >> 16;
@@ -2436,105 +1642,78 @@ __device__ __forceinline__ u32x4 ld16u_stream(const uint8_t* p) {
   }
 }
 
-template <bool NT>
-__device__ __forceinline__ void st16_stream(uint8_t* p, u32x4 x) {
-  if constexpr (NT) {
-    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
-  } else {
-    *reinterpret_cast<u32x4*>(p) = x;
-  }
+__device__ __forceinline__ void st16_nt(uint8_t* p, u32x4 x) {
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
+}
+
+// One 16-byte chunk of a frame the per-lane fallback path takes (windows of
+// more than kWinFrames frames: runs of empty frames), found by a search in
+// the tile map's frame range.
+__device__ __forceinline__ void unmask_chunk_lookup(const uint8_t* __restrict__ in,
+                                                    const gevws_frame* __restrict__ frames,
+                                                    const uint32_t* __restrict__ tile_first, uint64_t t,
+                                                    uint64_t ntiles, uint64_t nframes, uint64_t p,
+                                                    uint8_t* __restrict__ out) {
+  const gevws_frame* fr = frames + find_frame(frames, tile_first, t, ntiles, nframes, p);
+  const uint64_t rel = p - fr->payload_off;
+  uint32_t k;
+  memcpy(&k, fr->hdr.mask, 4);
+  u32x4 x = ld16u(in + fr->src_off + rel) ^ (fr->hdr.masked ? k : 0u);
+  const int64_t r = fr->hdr.length - (int64_t)rel;
+  if (r < 16) x = keep_bytes(x, r);
+  st16_nt(out + p, x);
 }
 
 // Measurement helper (not on the reference path): the unmask kernel's
 // streaming loop with the frame lookup and the XOR taken out -- each workgroup
-// owns a contiguous run of 4 KiB tiles, U unaligned 16-byte loads per lane,
-// aligned non-temporal stores.  bench.py times it over the same bytes as the
-// achievable-bandwidth ceiling beside the 8 TB/s spec peak.
-// Loads of the copy ceiling: non-temporal like the unmask's streaming loads
-// (NTL), or plain (measurement).
+// owns a contiguous run of 4 KiB tiles, U 16-byte loads per lane, aligned
+// non-temporal stores.  bench.py times it over the same bytes as the
+// achievable-bandwidth ceiling beside the 8 TB/s spec peak.  NTL: loads
+// non-temporal like the unmask's streaming loads (else plain); WSPAN: the
+// unmask's streaming layout -- in steps of U tiles of which wave w copies the
+// contiguous U KiB at w * U KiB (16 aligned bytes per lane per KiB).
 template <bool NT>
 __device__ __forceinline__ u32x4 copy_ld(const uint8_t* p) {
   if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));  // unaligned nt load
   else return ld16u(p);
 }
 
-// WSPAN: the unmask's streaming layout -- a contiguous run of tiles per
-// workgroup, in steps of U tiles of which wave w copies the contiguous
-// U KiB at w * U KiB (16 aligned bytes per lane per KiB).
-template <int U, bool INTERLEAVE, bool NTL = true, bool WSPAN = false>
+template <int U, bool NTL, bool WSPAN>
 __global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __restrict__ src,
                                                               uint8_t* __restrict__ dst, uint64_t n) {
   const uint64_t ntiles = n / kTile;
   const uint32_t lane_off = threadIdx.x * 16;
-  if constexpr (WSPAN) {
-    const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
-    uint64_t t = (uint64_t)blockIdx.x * per;
-    const uint64_t tend = t + per < ntiles ? t + per : ntiles;
-    const uint64_t wrel = (uint64_t)(threadIdx.x >> 6) * U * 1024 + (threadIdx.x & 63) * 16;
-    for (; t + U <= tend; t += U) {
-      const uint64_t base = t * kTile + wrel;
-      u32x4 v[U];
+  const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  uint64_t t = (uint64_t)blockIdx.x * per;
+  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+  const uint64_t wrel = WSPAN ? (uint64_t)(threadIdx.x >> 6) * U * 1024 + (threadIdx.x & 63) * 16 : lane_off;
+  constexpr uint64_t kStride = WSPAN ? 1024 : kTile;  // between a lane's U chunks of a step
+  for (; t + U <= tend; t += U) {
+    const uint64_t base = t * kTile + wrel;
+    u32x4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = copy_ld<NTL>(src + base + u * 1024);
+    for (int u = 0; u < U; ++u) v[u] = copy_ld<NTL>(src + base + u * kStride);
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + base + u * 1024));
-    }
-    for (; t < tend; ++t) {
-      const uint64_t base = t * kTile + lane_off;
-      __builtin_nontemporal_store(copy_ld<NTL>(src + base), reinterpret_cast<u32x4*>(dst + base));
-    }
-  } else if constexpr (INTERLEAVE) {
-    // blocks of U consecutive tiles dealt round-robin over the workgroups
-    const uint64_t nblk = ntiles / U;
-    for (uint64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
-      const uint64_t base = b * U * kTile + lane_off;
-      u32x4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = copy_ld<NTL>(src + base + u * kTile);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + base + u * kTile));
-    }
-    for (uint64_t t = nblk * U + blockIdx.x; t < ntiles; t += gridDim.x) {
-      const uint64_t base = t * kTile + lane_off;
-      __builtin_nontemporal_store(copy_ld<NTL>(src + base), reinterpret_cast<u32x4*>(dst + base));
-    }
-  } else {
-    // a contiguous run of tiles per workgroup (the unmask kernel's mapping)
-    const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
-    uint64_t t = (uint64_t)blockIdx.x * per;
-    const uint64_t tend = t + per < ntiles ? t + per : ntiles;
-    for (; t + U <= tend; t += U) {
-      const uint64_t base = t * kTile + lane_off;
-      u32x4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = copy_ld<NTL>(src + base + u * kTile);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(dst + base + u * kTile));
-    }
-    for (; t < tend; ++t) {
-      const uint64_t base = t * kTile + lane_off;
-      __builtin_nontemporal_store(copy_ld<NTL>(src + base), reinterpret_cast<u32x4*>(dst + base));
-    }
+    for (int u = 0; u < U; ++u) st16_nt(dst + base + u * kStride, v[u]);
+  }
+  for (; t < tend; ++t) {
+    const uint64_t base = t * kTile + lane_off;
+    st16_nt(dst + base, copy_ld<NTL>(src + base));
   }
   // bytes past the last whole tile: 16 per lane, workgroup 0
   const uint64_t tail = ntiles * kTile;
   if (blockIdx.x == 0)
-    for (uint64_t p = tail + lane_off; p < n; p += kTile)
-      __builtin_nontemporal_store(copy_ld<NTL>(src + p), reinterpret_cast<u32x4*>(dst + p));
+    for (uint64_t p = tail + lane_off; p < n; p += kTile) st16_nt(dst + p, copy_ld<NTL>(src + p));
 }
 
-// v3 = v2's streaming fast path + a cooperative small-frame path.  When the
-// next U tiles are not inside the cached frame, the workgroup takes a window
-// of W tiles, loads the records of every frame overlapping it (tile map gives
-// the index range) into LDS with one coalesced pass, and each lane finds the
-// frame of each of its W chunks by binary search in LDS -- no dependent global
-// loads per chunk.  Windows with more than kWinFrames frames (runs of empty
-// frames) fall back to the per-lane global lookup.
-constexpr int kWinTiles = 4;
-constexpr int kWinFrames = 1024;
+// The unmask = ws.Cipher (cipher.go:14-53) of every frame's payload into its
+// 16-aligned slot of the payload arena (protocol.go:50-55: the zeroed make +
+// Read + Cipher; pad bytes zero).  Each workgroup owns a contiguous run of 4
+// KiB output tiles.  While one frame covers the next U tiles the loop streams
+// (stream_step); otherwise it takes a window of tiles whose frames' records it
+// loads into LDS, and each lane looks up the frame of each of its chunks.
+constexpr int kWinTiles = 4;      // v3 window (tiles)
+constexpr int kWinFrames = 1024;  // frames a window's LDS table holds (more: the per-lane fallback)
 
 // Value of `x` in lane+1, lane 63 gets lane 0's (DPP wave_rol:1).
 __device__ __forceinline__ u32x4 rot_next_lane(u32x4 x) {
@@ -2569,14 +1748,15 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t m) {
   return o;
 }
 
-
 // One streaming step: U whole tiles [base, base + U*kTile) of the output
 // arena inside one frame (payload offset f_po, source f_src, length f_len,
-// key f_key).  AL = 2: aligned loads, wave-contiguous spans, realigned in
-// registers (DPP lane rotate + v_alignbyte) when the source is misaligned;
-// AL = 0 / aligned source: plain (unaligned) loads.
-// NTA (measurement): the aligned streaming loads non-temporal.
-template <int U, bool NTL, bool NTS, int AL, bool NTA = false>
+// key f_key).  A misaligned source is read with aligned non-temporal loads
+// over wave-contiguous U KiB spans and realigned in registers (DPP lane rotate
+// + v_alignbyte): wave w covers U KiB-chunks [base + w*U KiB, +U KiB) of the
+// step, lane 63's successor chunk at step u is lane 0's chunk at u+1, so only
+// u = U-1 needs one extra load, by lane 63.  An aligned source: plain loads.
+// Stores: aligned, non-temporal.
+template <int U>
 __device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                             uint64_t base, uint64_t f_po, uint64_t f_src, int64_t f_len,
                                             uint32_t f_key) {
@@ -2586,21 +1766,14 @@ __device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint
   uint8_t* dst = out + base + lane_off;
   u32x4 v[U];
   const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(src) & 15);  // uniform: lanes 16 B apart
-  if (AL == 2 && mis != 0) {
-    // aligned loads, wave-contiguous mapping: wave w covers U KiB-chunks
-    // [base + w*U KiB, +U KiB) of the step; lane 63's successor chunk at
-    // step u is lane 0's chunk at u+1 (DPP rotate), so only u = U-1 needs
-    // one extra load, by lane 63
+  if (mis != 0) {
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t wrel = (uint64_t)wave * U * 1024 + lane * 16;  // this lane's offset in the step
     const uint8_t* a = in + f_src + (base - f_po) + wrel - mis;
     uint8_t* d = out + base + wrel;
     const bool last = lane == 63;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const u32x4* q = reinterpret_cast<const u32x4*>(a + u * 1024);
-      v[u] = NTA ? __builtin_nontemporal_load(q) : *q;
-    }
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + u * 1024));
     u32x4 e = u32x4{0, 0, 0, 0};
     if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
     u32x4 r = rot_next_lane(v[0]);
@@ -2611,84 +1784,23 @@ __device__ __forceinline__ void stream_step(const uint8_t* __restrict__ in, uint
       u32x4 x = funnel16(v[u], nx, mis) ^ f_key;
       const int64_t rem = f_len - (int64_t)(base - f_po + wrel + u * 1024);
       if (rem < 16) x = keep_bytes(x, rem);
-      st16_stream<NTS>(d + u * 1024, x);
+      st16_nt(d + u * 1024, x);
       r = rn;
     }
     return;
   }
 #pragma unroll
-  for (int u = 0; u < U; ++u) v[u] = ld16u_stream<NTL>(src + u * kTile);
+  for (int u = 0; u < U; ++u) v[u] = ld16u(src + u * kTile);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     u32x4 x = v[u] ^ f_key;
     const int64_t rem = f_len - (int64_t)(rel0 + u * kTile);
     if (rem < 16) x = keep_bytes(x, rem);
-    st16_stream<NTS>(dst + u * kTile, x);
+    st16_nt(dst + u * kTile, x);
   }
 }
 
-// A run of streaming steps inside one frame, software-pipelined: the loads of
-// step i+1 (U2 tiles, wave-contiguous U2 KiB per wave, aligned + register
-// realign as stream_step AL = 2) are issued before step i is realigned, XORed
-// and stored, so a wave always has a step's loads in flight -- with one
-// workgroup per CU for big frames a CU runs only 4 waves, and stream_step's
-// load-all / store-all leaves each wave's read queue empty while it stores.
-// Returns the tile after the run (it takes every whole step that fits in
-// [t, tend) and inside the frame's padded end f_end).
-template <int U2, bool NTS>
-__device__ __forceinline__ uint64_t stream_run(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t t,
-                                               uint64_t tend, uint64_t f_po, uint64_t f_src, int64_t f_len,
-                                               uint32_t f_key, uint64_t f_end) {
-  const uint64_t n1 = (tend - t) / U2, n2 = (f_end - t * kTile) / ((uint64_t)U2 * kTile);
-  const uint64_t n = n1 < n2 ? n1 : n2;
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t wrel = (uint64_t)wave * U2 * 1024 + lane * 16;
-  const uint8_t* src0 = in + f_src + (t * kTile - f_po);  // the run's first source byte (wave-uniform)
-  const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(src0) & 15);
-  const uint8_t* a0 = src0 - mis + wrel;
-  uint8_t* d0 = out + t * kTile + wrel;
-  const int64_t rem0 = f_len - (int64_t)(t * kTile - f_po + wrel);  // payload bytes from this lane's chunk, step 0
-  const bool last = lane == 63;
-  constexpr uint64_t kStep = (uint64_t)U2 * kTile;
-  auto load = [&](u32x4 (&v)[U2], u32x4& e, uint64_t i) {
-    const uint8_t* a = a0 + i * kStep;
-#pragma unroll
-    for (int u = 0; u < U2; ++u) v[u] = *reinterpret_cast<const u32x4*>(a + u * 1024);
-    e = u32x4{0, 0, 0, 0};
-    if (last && mis) e = *reinterpret_cast<const u32x4*>(a + (U2 - 1) * 1024 + 16);
-  };
-  auto emit = [&](const u32x4 (&v)[U2], const u32x4& e, uint64_t i) {
-    uint8_t* d = d0 + i * kStep;
-    const int64_t rem = rem0 - (int64_t)(i * kStep);
-    u32x4 r = rot_next_lane(v[0]);
-#pragma unroll
-    for (int u = 0; u < U2; ++u) {
-      u32x4 x = v[u];
-      if (mis) {
-        const u32x4 rn = u + 1 < U2 ? rot_next_lane(v[u + 1 < U2 ? u + 1 : u]) : e;
-        x = funnel16(v[u], last ? rn : r, mis);
-        r = rn;
-      }
-      x ^= f_key;
-      const int64_t rr = rem - (int64_t)u * 1024;
-      if (rr < 16) x = keep_bytes(x, rr);
-      st16_stream<NTS>(d + u * 1024, x);
-    }
-  };
-  u32x4 va[U2], vb[U2], ea, eb;
-  load(va, ea, 0);
-  uint64_t i = 0;
-  for (; i + 2 <= n; i += 2) {  // unrolled by two: va / vb alternate, no register copies
-    load(vb, eb, i + 1);
-    emit(va, ea, i);
-    if (i + 2 < n) load(va, ea, i + 2);
-    emit(vb, eb, i + 1);
-  }
-  if (i < n) emit(va, ea, i);
-  return t + n * U2;
-}
-
-// The LDS frame table of a window (kWinFrames entries each).
+// The LDS frame table of a v3 window (kWinFrames entries each).
 struct WinLds {
   uint32_t* start;   // frame start relative to the window (clamped at 0)
   int32_t* lend;     // payload end relative to the window (clamped)
@@ -2696,30 +1808,19 @@ struct WinLds {
   uint32_t* key;
 };
 
-// For each of a lane's WT window chunks at once: the largest frame j < F with
-// s_start[j] <= rel[u] (s_start is non-decreasing, s_start[0] <= every rel).
-// Binary lifting with a wave-uniform step count, the WT LDS reads of a step
-// issued together: the per-chunk bisection loops ran one after another, WT x
-// log2(F) dependent LDS round trips per window instead of log2(F).
-template <int WT, typename T>
-__device__ __forceinline__ void window_search(const T* s_start, uint32_t F, const T (&rel)[WT], uint32_t (&lo)[WT]) {
-#pragma unroll
-  for (int u = 0; u < WT; ++u) lo[u] = 0;
-  for (uint32_t step = F > 1 ? 1u << (31 - __builtin_clz(F - 1)) : 0u; step; step >>= 1) {
-    T st[WT];
-#pragma unroll
-    for (int u = 0; u < WT; ++u) st[u] = lo[u] + step < F ? s_start[lo[u] + step] : rel[u] + 1;
-#pragma unroll
-    for (int u = 0; u < WT; ++u) lo[u] += st[u] <= rel[u] ? step : 0u;
-  }
-}
-
-template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles, bool IS = false, bool NTA = false,
-          bool NTW = false>
+// v3: 16-tile streaming steps; a window is 4 tiles: the records of every frame
+// overlapping it (index range from the tile map) go into LDS with one
+// coalesced pass and each lane binary-searches LDS for the frame of each of
+// its 4 chunks, whose loads are unaligned non-temporal 16-byte loads.  The
+// scheme of batches of equal-size frames (C1, C2, C3, C5: -5 % on C1-shaped
+// and -2.4 % on C2 batches against v4's 8-tile windows, equal on C3;
+// profiles/r02_ab2.log).
+template <int U>
 __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
-                                               uint32_t big_grid, const WinLds& L, bool wide = false) {
+                                               uint32_t big_grid, const WinLds& L) {
+  constexpr int WT = kWinTiles;
   uint32_t* const s_start = L.start;
   int32_t* const s_lend = L.lend;
   uint64_t* const s_delta = L.delta;
@@ -2728,7 +1829,7 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
   const uint64_t total = sum->payload_bytes;
   const uint64_t nframes = sum->frames;
   const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint32_t groups = active_groups(total, nframes, big_grid, wide);
+  const uint32_t groups = active_groups(total, nframes, big_grid);
   if (blockIdx.x >= groups) return;
   const uint64_t per = (ntiles + groups - 1) / groups;
   uint64_t t = (uint64_t)blockIdx.x * per;
@@ -2749,7 +1850,7 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
       f_key = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
     }
     if (t + U <= tend && base + U * kTile <= f_end) {
-      stream_step<U, NTL, NTS, AL, NTA>(in, out, base, f_po, f_src, f_len, f_key);
+      stream_step<U>(in, out, base, f_po, f_src, f_len, f_key);
       t += U;
       continue;
     }
@@ -2765,11 +1866,11 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
       for (uint64_t i = threadIdx.x; i < F; i += kUnmaskBlock) {
         const uint64_t* rec = reinterpret_cast<const uint64_t*>(frames + f_lo + i);
         const uint64_t w0 = rec[0];
-        const uint64_t L = rec[1];
+        const uint64_t Ln = rec[1];
         const uint64_t po = rec[2];
         const uint64_t so = rec[3];
         s_start[i] = po > wbase ? (uint32_t)(po - wbase) : 0u;
-        const uint64_t lend = po + L;  // end of payload bytes
+        const uint64_t lend = po + Ln;  // end of payload bytes
         s_lend[i] = lend <= wbase ? 0 : (lend - wbase > 0x7fffffffull ? 0x7fffffff : (int32_t)(lend - wbase));
         s_delta[i] = so - po;
         s_key[i] = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
@@ -2778,12 +1879,6 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
       u32x4 v[WT];
       uint32_t key[WT];
       int32_t rem[WT];
-      uint32_t relv[WT], lov[WT];
-      if constexpr (IS) {
-#pragma unroll
-        for (int u = 0; u < WT; ++u) relv[u] = (uint32_t)(u * kTile) + lane_off;
-        window_search<WT>(s_start, (uint32_t)F, relv, lov);
-      }
 #pragma unroll
       for (int u = 0; u < WT; ++u) {
         const uint32_t rel = (uint32_t)(u * kTile) + lane_off;
@@ -2793,17 +1888,13 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
         v[u] = u32x4{0, 0, 0, 0};
         if ((uint64_t)u < wt && p < total) {
           uint32_t lo = 0, hi = (uint32_t)F - 1;
-          if constexpr (IS) {
-            lo = lov[u];
-          } else {
-            while (lo < hi) {
-              const uint32_t mid = (lo + hi + 1) >> 1;
-              if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
-            }
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
           }
           rem[u] = s_lend[lo] - (int32_t)rel;
           key[u] = s_key[lo];
-          v[u] = ld16u_stream<NTL || NTW>(in + (p + s_delta[lo]));
+          v[u] = ld16u_stream<true>(in + (p + s_delta[lo]));
         }
       }
 #pragma unroll
@@ -2811,55 +1902,49 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
         if (rem[u] > 0) {
           u32x4 x = v[u] ^ key[u];
           if (rem[u] < 16) x = keep_bytes(x, rem[u]);
-          st16_stream<NTS>(out + wbase + (uint32_t)(u * kTile) + lane_off, x);
+          st16_nt(out + wbase + (uint32_t)(u * kTile) + lane_off, x);
         }
       }
       t = wend_t;
       continue;
     }
     // ---- too many frames in the window (runs of empty frames): per-lane lookup, one tile
-    {
-      const uint64_t p = base + lane_off;
-      if (p < total) {
-        const gevws_frame* fr = frames + find_frame(frames, tile_first, t, ntiles, nframes, p);
-        const uint64_t rel = p - fr->payload_off;
-        uint32_t k;
-        memcpy(&k, fr->hdr.mask, 4);
-        u32x4 x = ld16u_stream<NTL>(in + fr->src_off + rel) ^ (fr->hdr.masked ? k : 0u);
-        const int64_t r = fr->hdr.length - (int64_t)rel;
-        if (r < 16) x = keep_bytes(x, r);
-        st16_stream<NTS>(out + p, x);
-      }
-      t += 1;
-    }
+    const uint64_t p = base + lane_off;
+    if (p < total) unmask_chunk_lookup(in, frames, tile_first, t, ntiles, nframes, p, out);
+    t += 1;
   }
 }
 
-template <int U, bool NTL, bool NTS, int AL = 0, int WT = kWinTiles>
-__global__ __launch_bounds__(kUnmaskBlock) void k_unmask_v3(const uint8_t* __restrict__ in,
-                                                            const gevws_frame* __restrict__ frames,
-                                                            const uint32_t* __restrict__ tile_first,
-                                                            const gevws_summary* __restrict__ sum,
-                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
-  __shared__ uint32_t s_start[kWinFrames];   // frame start relative to the window (clamped at 0)
-  __shared__ int32_t s_lend[kWinFrames];     // payload end relative to the window (clamped)
-  __shared__ uint64_t s_delta[kWinFrames];   // src_off - payload_off (mod 2^64)
-  __shared__ uint32_t s_key[kWinFrames];
-  unmask_v3_body<U, NTL, NTS, AL, WT>(in, frames, tile_first, sum, out, big_grid, WinLds{s_start, s_lend, s_delta, s_key});
-}
-
-// v4 = v3 with the window path software-pipelined.  In v3 every window is one
-// chain of dependent global loads: the tile map and the cached-frame record
-// (scalar) that decide streaming vs window, the window's records, the LDS
-// search, the payload loads.  v4 decides the NEXT step while the current
-// window's payload loads are in flight: it loads the next window's tile-map
-// entries -- first frame a, last frame b and the frame at tile +U, which equals
-// a iff one frame covers the next U tiles (the next step streams) -- and, for a
-// window, its first 256 records into registers (one per lane), which
-// the next iteration writes to LDS without waiting on a fresh load.  WT tiles
-// per window.
-
-constexpr int kWin4Frames = 1024;
+// v5: the window path for batches of mixed sizes (C4), software-pipelined and
+// with its two latency chains out of the critical path.  8-tile windows; the
+// NEXT step is decided while the current window's payload loads are in flight
+// (its tile-map entries -- first frame a, last frame b and the frame at tile
+// +U, which equals a iff one frame covers the next U tiles -- and, for a
+// window, its first 256 records into registers, one per lane).  Profiled
+// (round 3, cycle counters; profiles/r03_unmask_profile*.jsonl) an 8-tile
+// window of round 2's v4 spent a quarter of its ~37 K cycles in the per-chunk
+// searches and a third in the next-step decision.  v5:
+//  * chunk -> frame by a map instead of a search: every non-empty frame marks
+//    its first 16-byte chunk in the window (payloads are 16-aligned and
+//    contiguous, so each chunk belongs to exactly one frame: the last one
+//    starting at or before it), and a workgroup prefix-max over the 2 048
+//    chunk slots turns the marks into the owner of every chunk; a lane then
+//    reads its 8 owners and their attributes in two LDS round trips, all
+//    chunks at once.  The map is double-buffered: window k clears the buffer
+//    window k+1 fills.
+//  * the tile map through an LDS cache of kTmapN entries (refilled by the
+//    whole workgroup every ~60 windows): a decision is LDS reads, not global.
+// C4 7.75 -> 7.40 ms against v4 (profiles/r03_unmask_v5*_ab.jsonl).
+// amdgpu_waves_per_eu(4): four workgroups per CU (128 VGPRs); 5 or 6 measured
+// slower (r03_unmask_occ_ab.jsonl).  Every lane id is re-derived where it is
+// used (fresh_tid): held across the loop, the fill's per-lane LDS / record
+// addresses were spilled, and each spill reload -- a scratch load queued
+// behind the window's global loads, vmcnt being in order -- serialised them
+// (C4: 2 GB of the 22.9 GB read per launch in round 1).
+constexpr int kWin5Frames = 1024;
+constexpr uint32_t kWinChunks = 8 * (uint32_t)kTile / 16;  // 2 048 chunks in an 8-tile window
+constexpr uint32_t kQuarter = kWinChunks / (kUnmaskBlock / 64);  // chunks per wave
+constexpr uint32_t kTmapN = 512;
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 struct WinRec {
@@ -2872,355 +1957,22 @@ __device__ __forceinline__ WinRec load_rec(const gevws_frame* __restrict__ frame
   return WinRec{r[0], r[1]};
 }
 
-// amdgpu_waves_per_eu(4): four workgroups per CU (128 VGPRs; a few loop-
-// invariant lane values spill to scratch).  Three per CU (140 VGPRs, no
-// spills) measured 25-40 % slower on C2/C4/C5.
-// WC (wave-contiguous window mapping): in the window path wave w takes the
-// contiguous WT KiB [w*WT KiB, (w+1)*WT KiB) of the window, 1 KiB per step,
-// instead of 1 KiB of every tile.  The chunk loads are unaligned (the source
-// shifts by the header lengths), so each wave instruction touches 9 lines for
-// 8 lines of data; with tile-strided spans the 9th line is the first line of
-// ANOTHER wave's span, which runs skewed and finds it evicted -- the C4 window
-// path read 10 % more than its bytes (profiles/r02_pmc_split_before.json:
-// 22.87 GB of 128-byte requests for 20.84 GB).  Wave-contiguous, the shared
-// line belongs to the same wave's next instruction, issued right behind it.
-// FT (measurement switch): false re-creates the round-1 kernel whose fill
-// addresses were spilled (threadIdx.x used directly).
-// SP: streaming steps as software-pipelined runs (stream_run, U / 2 tiles per step).
-// PROF (measurement): thread 0 of every workgroup stamps the phases of its
-// loop with s_memtime and adds the cycle counts into g_uprof (gevws_unmask_profile):
-//   0 kernel, 1 streaming steps, 2 window first barrier, 3 fill, 4 second
-//   barrier, 5 search + payload load issue, 6 next-step decision + record
-//   prefetch, 7 wait for the payload + XOR + stores, 8 windows, 9 windows of
-//   more than 256 frames, 10 frames over all windows, 11 streaming steps,
-//   12 workgroups, 13 fallback (per-lane lookup) tiles; PROF 2 waits for the
-//   window's payload loads right after issuing them (phase 14: the loads'
-//   own latency, then decision and stores run on landed data).
-__device__ unsigned long long g_uprof[16];
-__device__ __forceinline__ uint64_t stamp() {
-  __asm__ volatile("" ::: "memory");
-  const uint64_t t = __builtin_amdgcn_s_memtime();
-  __asm__ volatile("" ::: "memory");
-  return t;
-}
-
-template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false, bool IS = false,
-          bool NTA = false, bool NTW = false, int PROF = 0>
-__device__ __forceinline__ void unmask_v4_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
-                                               const uint32_t* __restrict__ tile_first,
-                                               const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
-                                               uint32_t big_grid, const WinLds& L, bool wide = false) {
-  uint64_t pr[16] = {};
-  uint64_t tk0 = 0, tp = 0;
-  if constexpr (PROF) tk0 = stamp();
-  auto lap = [&](int k) {  // time since the previous stamp into phase k
-    if constexpr (PROF) {
-      const uint64_t t = stamp();
-      pr[k] += t - tp;
-      tp = t;
-    }
-  };
-  auto prof_flush = [&]() {
-    if constexpr (PROF) {
-      pr[0] = stamp() - tk0;
-      pr[12] = 1;
-      if (fresh_tid() == 0)
-        for (int k = 0; k < 16; ++k)
-          if (pr[k]) __hip_atomic_fetch_add(&g_uprof[k], (unsigned long long)pr[k], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-  uint32_t* const s_start = L.start;
-  int32_t* const s_lend = L.lend;
-  uint64_t* const s_delta = L.delta;
-  uint32_t* const s_key = L.key;
-  if (sum->status != GEVWS_OK) return;
-  const uint64_t total = sum->payload_bytes;
-  const uint64_t nframes = sum->frames;
-  const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint32_t groups = active_groups(total, nframes, big_grid, wide);
-  if (blockIdx.x >= groups) return;
-  const uint64_t per = (ntiles + groups - 1) / groups;
-  uint64_t t = (uint64_t)blockIdx.x * per;
-  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
-  const uint32_t lane_off = threadIdx.x * 16;
-  if constexpr (PROF) tp = stamp();
-  uint64_t f_po = 0, f_end = 0, f_src = 0;  // the cached (streaming) frame
-  int64_t f_len = 0;
-  uint32_t f_key = 0;
-  // decision for tile pf_t, made during the previous window
-  uint64_t pf_t = ~0ull, pf_a = 0, pf_b = 0;
-  bool pf_stream = false;
-  WinRec r0 = {};  // record pf_a + tid when !pf_stream
-  auto cache_frame = [&](uint64_t f) {  // wave-uniform: SGPRs
-    const uint64_t* rec = reinterpret_cast<const uint64_t*>(frames + f);
-    const uint64_t w0 = uniform64(rec[0]);
-    f_len = (int64_t)uniform64(rec[1]);
-    f_po = uniform64(rec[2]);
-    f_src = uniform64(rec[3]);
-    f_end = f_po + round16((uint64_t)f_len);
-    f_key = ((w0 >> 24) & 0xff) ? (uint32_t)(w0 >> 32) : 0u;
-  };
-  // step decision for tile x: a = first frame; stream iff one frame covers
-  // [x, x+U) -- the tile map puts frame a at tile x+U-1 too, and its record
-  // (then cached for the streaming step) ends at or past tile x+U; otherwise
-  // b = last frame of the window [x, x+WT)
-  auto decide = [&](uint64_t x, uint64_t& a, uint64_t& b, bool& stream) {
-    a = uniform32(tile_first[x]);
-    stream = false;
-    if (x + U <= tend && uniform32(tile_first[x + U - 1]) == a) {
-      cache_frame(a);
-      stream = x * kTile >= f_po && (x + U) * kTile <= f_end;
-    }
-    const uint64_t wt = (tend - x) < (uint64_t)WT ? (tend - x) : (uint64_t)WT;
-    b = x + wt < ntiles ? (uint64_t)uniform32(tile_first[x + wt]) : nframes - 1;
-  };
-  while (t < tend) {
-    const uint64_t base = t * kTile;
-    if (t + U <= tend && base >= f_po && base + U * kTile <= f_end) {  // still inside the cached frame
-      if constexpr (SP) t = stream_run<U / 2, NTS>(in, out, t, tend, f_po, f_src, f_len, f_key, f_end);
-      else {
-        stream_step<U, false, NTS, 2, NTA>(in, out, base, f_po, f_src, f_len, f_key);
-        t += U;
-      }
-      pf_t = ~0ull;  // (never t here; redefining r0 keeps it dead across the step)
-      r0 = WinRec{};
-      lap(1);
-      if constexpr (PROF) ++pr[11];
-      continue;
-    }
-    uint64_t a, b;
-    bool stream, have = false;
-    if (pf_t == t) {
-      a = pf_a;
-      b = pf_b;
-      stream = pf_stream;
-      have = !pf_stream;
-    } else {
-      decide(t, a, b, stream);
-    }
-    if (stream) {  // decide() cached frame a, which covers [t, t+U)
-      if constexpr (SP) t = stream_run<U / 2, NTS>(in, out, t, tend, f_po, f_src, f_len, f_key, f_end);
-      else {
-        stream_step<U, false, NTS, 2, NTA>(in, out, base, f_po, f_src, f_len, f_key);
-        t += U;
-      }
-      pf_t = ~0ull;
-      r0 = WinRec{};
-      lap(1);
-      if constexpr (PROF) ++pr[11];
-      continue;
-    }
-    // ---- window path
-    const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
-    const uint64_t wend_t = t + wt;
-    const uint64_t wbase = base;
-    const uint64_t F = b - a + 1;
-    if (F > (uint64_t)kWin4Frames) {
-      // too many frames in the window (runs of empty frames): per-lane lookup, one tile
-      const uint64_t p = base + lane_off;
-      if (p < total) {
-        const gevws_frame* fr = frames + find_frame(frames, tile_first, t, ntiles, nframes, p);
-        const uint64_t rel = p - fr->payload_off;
-        uint32_t k;
-        memcpy(&k, fr->hdr.mask, 4);
-        u32x4 x = ld16u(in + fr->src_off + rel) ^ (fr->hdr.masked ? k : 0u);
-        const int64_t r = fr->hdr.length - (int64_t)rel;
-        if (r < 16) x = keep_bytes(x, r);
-        st16_stream<NTS>(out + p, x);
-      }
-      t += 1;
-      lap(7);
-      if constexpr (PROF) ++pr[13];
-      continue;
-    }
-    lap(6);
-    __syncthreads();  // previous window's readers are done with the LDS table
-    lap(2);
-    auto fill = [&](uint64_t i, const WinRec& q) {
-      const uint64_t L = q.lo[1], po = q.hi[0], so = q.hi[1];
-      s_start[i] = po > wbase ? (uint32_t)(po - wbase) : 0u;
-      const uint64_t lend = po + L;  // end of payload bytes
-      s_lend[i] = lend <= wbase ? 0 : (lend - wbase > 0x7fffffffull ? 0x7fffffff : (int32_t)(lend - wbase));
-      s_delta[i] = so - po;
-      s_key[i] = ((q.lo[0] >> 24) & 0xff) ? (uint32_t)(q.lo[0] >> 32) : 0u;
-    };
-    // threadIdx.x re-read here (fresh_tid): otherwise the compiler keeps the
-    // fill's per-lane LDS / record addresses live across the whole loop and
-    // spills them; their reloads are scratch loads that queue behind the
-    // window's global loads (vmcnt is in order) and miss in L2 under the
-    // stream (C4: 2 GB of the 22.9 GB read per launch)
-    const uint32_t tid = FT ? fresh_tid() : threadIdx.x;
-    if (tid < F) fill(tid, have ? r0 : load_rec(frames, a + tid));
-    for (uint64_t i = tid + kUnmaskBlock; i < F; i += kUnmaskBlock) fill(i, load_rec(frames, a + i));
-    lap(3);
-    __syncthreads();
-    lap(4);
-    u32x4 v[WT];
-    uint32_t key[WT];
-    int32_t rem[WT];
-    uint32_t relv[WT], lov[WT];
-    if constexpr (IS) {
-#pragma unroll
-      for (int u = 0; u < WT; ++u)
-        relv[u] = WC ? (threadIdx.x >> 6) * (uint32_t)(WT * 1024) + (uint32_t)u * 1024 + (threadIdx.x & 63) * 16
-                     : (uint32_t)(u * kTile) + lane_off;
-      window_search<WT>(s_start, (uint32_t)F, relv, lov);
-    }
-#pragma unroll
-    for (int u = 0; u < WT; ++u) {
-      const uint32_t rel = WC ? (threadIdx.x >> 6) * (uint32_t)(WT * 1024) + (uint32_t)u * 1024 + (threadIdx.x & 63) * 16
-                              : (uint32_t)(u * kTile) + lane_off;
-      const uint64_t p = wbase + rel;
-      rem[u] = 0;
-      key[u] = 0;
-      v[u] = u32x4{0, 0, 0, 0};
-      if ((WC ? (uint64_t)rel < wt * kTile : (uint64_t)u < wt) && p < total) {
-        uint32_t lo = 0, hi = (uint32_t)F - 1;
-        if constexpr (IS) {
-          lo = lov[u];
-        } else {
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
-          }
-        }
-        rem[u] = s_lend[lo] - (int32_t)rel;
-        key[u] = s_key[lo];
-        v[u] = ld16u_stream<NTW>(in + (p + s_delta[lo]));
-      }
-    }
-    // decide the next step (and fetch the next window's records) while this
-    // window's payload loads are in flight
-    lap(5);
-    if constexpr (PROF == 2) {
-      __builtin_amdgcn_s_waitcnt(0);  // (measurement) every load of this wave landed
-      lap(14);
-    }
-    __asm__ volatile("" ::: "memory");
-    pf_t = ~0ull;
-    if (wend_t < tend) {
-      decide(wend_t, pf_a, pf_b, pf_stream);
-      pf_t = wend_t;
-      if (!pf_stream) {
-        const uint64_t nF = pf_b - pf_a + 1;
-        const uint32_t tid = FT ? fresh_tid() : threadIdx.x;  // (a spilled frames + tid * 32 would wait vmcnt(0) on its reload)
-        if (tid < nF) r0 = load_rec(frames, pf_a + tid);
-      }
-    }
-    lap(6);
-#pragma unroll
-    for (int u = 0; u < WT; ++u) {
-      if (rem[u] > 0) {
-        u32x4 x = v[u] ^ key[u];
-        if (rem[u] < 16) x = keep_bytes(x, rem[u]);
-        const uint32_t rel = WC ? (threadIdx.x >> 6) * (uint32_t)(WT * 1024) + (uint32_t)u * 1024 + (threadIdx.x & 63) * 16
-                                : (uint32_t)(u * kTile) + lane_off;
-        st16_stream<NTS>(out + wbase + rel, x);
-      }
-    }
-    t = wend_t;
-    lap(7);
-    if constexpr (PROF) {
-      ++pr[8];
-      pr[9] += F > 256 ? 1 : 0;
-      pr[10] += F;
-    }
-  }
-  prof_flush();
-}
-
-template <int U, int WT, bool NTS, bool WC = false, bool FT = true, bool SP = false>
-__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_v4(const uint8_t* __restrict__ in,
-                                                            const gevws_frame* __restrict__ frames,
-                                                            const uint32_t* __restrict__ tile_first,
-                                                            const gevws_summary* __restrict__ sum,
-                                                            uint8_t* __restrict__ out, uint32_t big_grid) {
-  __shared__ uint32_t s_start[kWin4Frames];
-  __shared__ int32_t s_lend[kWin4Frames];
-  __shared__ uint64_t s_delta[kWin4Frames];
-  __shared__ uint32_t s_key[kWin4Frames];
-  unmask_v4_body<U, WT, NTS, WC, FT, SP>(in, frames, tile_first, sum, out, big_grid,
-                                         WinLds{s_start, s_lend, s_delta, s_key});
-}
-
-// The default unmask: the batch's own statistics pick the window scheme --
-// batches of equal-size frames (at least half of the frames the size of the
-// one before them on the connection: C1, C2, C3) take v3's 4-tile windows,
-// mixed ones (C4, C5) v4's pipelined 8-tile windows (interleaved A/B:
-// v3-4 -5 % on C1-shaped and -2.4 % on C2 batches, v4-8 -3 % on C4 and -2 % on
-// C5, equal on C3; profiles/r02_ab2.log).  One kernel, one LDS table, the
-// choice is a uniform branch on the summary the walk wrote.
-template <bool IS, bool NTA = false, bool NTW = false, int PROF = 0>
-__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto(
-    const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
-    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
-  __shared__ uint32_t s_start[kWin4Frames];
-  __shared__ int32_t s_lend[kWin4Frames];
-  __shared__ uint64_t s_delta[kWin4Frames];
-  __shared__ uint32_t s_key[kWin4Frames];
-  static_assert(kWinFrames == kWin4Frames, "one LDS table for both bodies");
-  const WinLds L{s_start, s_lend, s_delta, s_key};
-  if (2 * sum->run_frames >= sum->frames)  // frames the size of their predecessor on the connection
-    unmask_v3_body<16, false, true, 2, kWinTiles, IS, NTA, NTW>(in, frames, tile_first, sum, out, big_grid, L);
-  else  // mixed sizes: the whole (wide) grid for a batch of fewer than kWideGridTiles tiles
-    unmask_v4_body<16, 8, true, false, true, false, IS, NTA, NTW, PROF>(in, frames, tile_first, sum, out, big_grid,
-                                                                         L, sum->payload_bytes / kTile < kWideGridTiles);
-}
-
-// v5 = v4 with the two latency chains of a window taken out of the critical
-// path (profiled with the PROF variant: per 8-tile window ~37 K cycles, a
-// quarter in the per-chunk searches -- eight binary searches one after the
-// other, each ~7 dependent LDS reads, before the chunk's payload load can
-// issue -- and a third in the next-step decision -- a chain of scalar loads of
-// the tile map and a record; profiles/r03_unmask_profile*.jsonl):
-//  * chunk -> frame by a map instead of a search: every non-empty frame marks
-//    its first 16-byte chunk in the window (payloads are 16-aligned and
-//    contiguous, so each chunk belongs to exactly one frame: the last one
-//    starting at or before it), and a workgroup prefix-max over the 2 048
-//    chunk slots turns the marks into the owner of every chunk; a lane then
-//    reads its 8 owners and their attributes in two LDS round trips, all
-//    chunks at once.  The map is double-buffered: window k clears the buffer
-//    window k+1 fills.
-//  * the tile map through an LDS cache of kTmapN entries (refilled by the
-//    whole workgroup every ~60 windows): a decision is LDS reads, not global.
-constexpr uint32_t kWinChunks = 8 * (uint32_t)kTile / 16;  // 2 048 chunks in an 8-tile window
-constexpr uint32_t kQuarter = kWinChunks / (kUnmaskBlock / 64);  // chunks per wave
-constexpr uint32_t kTmapN = 512;
-
 struct WinLds5 {
-  int32_t* lend;    // [kWin4Frames] payload end relative to the window (clamped)
-  uint64_t* delta;  // [kWin4Frames] src_off - payload_off
-  uint32_t* key;    // [kWin4Frames]
+  int32_t* lend;    // [kWin5Frames] payload end relative to the window (clamped)
+  uint64_t* delta;  // [kWin5Frames] src_off - payload_off
+  uint32_t* key;    // [kWin5Frames]
   uint16_t* own;    // [2][kWinChunks] window chunk -> frame index + 1 (marks, then their prefix max)
   uint32_t* wtot;   // [2][kUnmaskBlock / 64] per map: frame index + 1 covering each wave quarter's first chunk
   uint32_t* tmap;   // [kTmapN] tile_first[tm0 ...]
-  uint64_t* prof;   // [16] PROF counters
 };
 
-template <int U, bool NTS, int PROF = 0>
+template <int U>
 __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
                                                uint32_t big_grid, const WinLds5& L, bool wide = false) {
   constexpr int WT = 8;
   static_assert(WT * kTile / 16 == kWinChunks && kWinChunks == 8 * kUnmaskBlock, "8 chunks per thread");
-  // (PROF: the counters live in LDS, updated by thread 0 -- registers for
-  // them made the kernel spill, and the spill reloads distorted the phases)
-  uint64_t tk0 = 0, tp = 0;
-  if constexpr (PROF) tk0 = stamp();
-  auto pr_add = [&](int k, uint64_t v) {
-    if constexpr (PROF) {
-      if (fresh_tid() == 0) L.prof[k] += v;
-    }
-  };
-  auto lap = [&](int k) {
-    if constexpr (PROF) {
-      const uint64_t t = stamp();
-      pr_add(k, t - tp);
-      tp = t;
-    }
-  };
   if (sum->status != GEVWS_OK) return;
   const uint64_t total = sum->payload_bytes;
   const uint64_t nframes = sum->frames;
@@ -3232,22 +1984,20 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
   const uint64_t tend = t + per < ntiles ? t + per : ntiles;
   {  // both chunk maps (and their wave seeds) start empty
     const uint32_t tid = fresh_tid();
-    if (PROF && tid < 16) L.prof[tid] = 0;
     reinterpret_cast<u32x4*>(L.own)[tid] = u32x4{0, 0, 0, 0};
     reinterpret_cast<u32x4*>(L.own + kWinChunks)[tid] = u32x4{0, 0, 0, 0};
     if (tid < 2 * (kUnmaskBlock / 64)) L.wtot[tid] = 0;
   }
   __syncthreads();
-  if constexpr (PROF) tp = stamp();
   uint64_t f_po = 0, f_end = 0, f_src = 0;  // the cached (streaming) frame
   int64_t f_len = 0;
   uint32_t f_key = 0;
-  uint64_t pf_t = ~0ull, pf_a = 0, pf_b = 0;
+  uint64_t pf_t = ~0ull, pf_a = 0, pf_b = 0;  // decision for tile pf_t, made during the previous window
   bool pf_stream = false;
-  WinRec r0 = {};
+  WinRec r0 = {};  // record pf_a + tid when !pf_stream
   uint32_t buf = 0;          // chunk map of this window
   uint64_t tm0 = ~0ull;      // first tile of the cached tile map
-  auto cache_frame = [&](uint64_t f) {
+  auto cache_frame = [&](uint64_t f) {  // wave-uniform: SGPRs
     const uint64_t* rec = reinterpret_cast<const uint64_t*>(frames + f);
     const uint64_t w0 = uniform64(rec[0]);
     f_len = (int64_t)uniform64(rec[1]);
@@ -3270,6 +2020,10 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
     }
     return uniform32(L.tmap[x - tm0]);
   };
+  // step decision for tile x: a = first frame; stream iff one frame covers
+  // [x, x+U) -- the tile map puts frame a at tile x+U-1 too, and its record
+  // (then cached for the streaming step) ends at or past tile x+U; otherwise
+  // b = last frame of the window [x, x+WT)
   auto decide = [&](uint64_t x, uint64_t& a, uint64_t& b, bool& stream) {
     a = tmap_at(x);
     stream = false;
@@ -3282,13 +2036,11 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
   };
   while (t < tend) {
     const uint64_t base = t * kTile;
-    if (t + U <= tend && base >= f_po && base + U * kTile <= f_end) {
-      stream_step<U, false, NTS, 2, true>(in, out, base, f_po, f_src, f_len, f_key);
+    if (t + U <= tend && base >= f_po && base + U * kTile <= f_end) {  // still inside the cached frame
+      stream_step<U>(in, out, base, f_po, f_src, f_len, f_key);
       t += U;
       pf_t = ~0ull;
-      r0 = WinRec{};
-      lap(1);
-      pr_add(11, 1);
+      r0 = WinRec{};  // (redefined: dead across the step)
       continue;
     }
     uint64_t a, b;
@@ -3301,43 +2053,28 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
     } else {
       decide(t, a, b, stream);
     }
-    if (stream) {
-      stream_step<U, false, NTS, 2, true>(in, out, base, f_po, f_src, f_len, f_key);
+    if (stream) {  // decide() cached frame a, which covers [t, t+U)
+      stream_step<U>(in, out, base, f_po, f_src, f_len, f_key);
       t += U;
       pf_t = ~0ull;
       r0 = WinRec{};
-      lap(1);
-      pr_add(11, 1);
       continue;
     }
     const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
     const uint64_t wend_t = t + wt;
     const uint64_t wbase = base;
     const uint64_t F = b - a + 1;
-    if (F > (uint64_t)kWin4Frames) {  // runs of empty frames: per-lane lookup, one tile
+    if (F > (uint64_t)kWin5Frames) {  // runs of empty frames: per-lane lookup, one tile
       const uint64_t p = base + fresh_tid() * 16;
-      if (p < total) {
-        const gevws_frame* fr = frames + find_frame(frames, tile_first, t, ntiles, nframes, p);
-        const uint64_t rel = p - fr->payload_off;
-        uint32_t k;
-        memcpy(&k, fr->hdr.mask, 4);
-        u32x4 x = ld16u(in + fr->src_off + rel) ^ (fr->hdr.masked ? k : 0u);
-        const int64_t r = fr->hdr.length - (int64_t)rel;
-        if (r < 16) x = keep_bytes(x, r);
-        st16_stream<NTS>(out + p, x);
-      }
+      if (p < total) unmask_chunk_lookup(in, frames, tile_first, t, ntiles, nframes, p, out);
       t += 1;
       pf_t = ~0ull;
       r0 = WinRec{};
-      lap(7);
-      pr_add(13, 1);
       continue;
     }
     uint16_t* const own = L.own + buf * kWinChunks;
     uint32_t* const carry = L.wtot + buf * (kUnmaskBlock / 64);
-    lap(6);
     __syncthreads();  // previous window's readers are done with the frame table
-    lap(2);
     auto fill = [&](uint64_t i, const WinRec& q) {
       const uint64_t Ln = q.lo[1], po = q.hi[0], so = q.hi[1];
       const uint64_t lend = po + Ln;
@@ -3358,9 +2095,7 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
     const uint32_t tid = fresh_tid();
     if (tid < F) fill(tid, have ? r0 : load_rec(frames, a + tid));
     for (uint64_t i = tid + kUnmaskBlock; i < F; i += kUnmaskBlock) fill(i, load_rec(frames, a + i));
-    lap(3);
     __syncthreads();
-    lap(4);
     // prefix max over the chunk marks, per wave over its own quarter of the
     // window (wave w: chunks [512 w, 512 (w + 1)), lane l the 8 from 512 w + 8 l),
     // seeded with the frame covering the quarter's first chunk; the wave then
@@ -3398,7 +2133,6 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
       reinterpret_cast<u32x4*>(L.own + (buf ^ 1) * kWinChunks)[j] = u32x4{0, 0, 0, 0};
       if (lane == 0) L.wtot[(buf ^ 1) * (kUnmaskBlock / 64) + w] = 0;
     }
-    lap(5);
     u32x4 v[WT];
     uint32_t key[WT];
     int32_t rem[WT];
@@ -3411,9 +2145,6 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
       const uint32_t o = own[c];
       lov[u] = o ? o - 1 : 0;
     }
-    // (the lane's chunk offsets re-derived from a fresh threadIdx.x: kept live
-    // across the loop they spill, and each reload -- a scratch load queued
-    // behind the payload loads, vmcnt being in order -- serialises them)
     const uint32_t tl = fresh_tid();
     const uint32_t loff = (tl >> 6) * kQuarter * 16 + (tl & 63) * 16;
 #pragma unroll
@@ -3430,7 +2161,8 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
         v[u] = ld16u_stream<true>(in + (p + L.delta[lo]));
       }
     }
-    lap(5);
+    // decide the next step (and fetch the next window's records) while this
+    // window's payload loads are in flight
     __asm__ volatile("" ::: "memory");
     pf_t = ~0ull;
     if (wend_t < tend) {
@@ -3442,7 +2174,6 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
         if (tid2 < nF) r0 = load_rec(frames, pf_a + tid2);
       }
     }
-    lap(6);
     const uint32_t ts = fresh_tid();
     const uint32_t soff = (ts >> 6) * kQuarter * 16 + (ts & 63) * 16;
 #pragma unroll
@@ -3450,67 +2181,53 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
       if (rem[u] > 0) {
         u32x4 x = v[u] ^ key[u];
         if (rem[u] < 16) x = keep_bytes(x, rem[u]);
-        st16_stream<NTS>(out + wbase + (uint32_t)u * 1024 + soff, x);
+        st16_nt(out + wbase + (uint32_t)u * 1024 + soff, x);
       }
     }
     buf ^= 1;
     t = wend_t;
-    lap(7);
-    pr_add(8, 1);
-    pr_add(9, F > 256 ? 1 : 0);
-    pr_add(10, F);
-  }
-  if constexpr (PROF) {
-    pr_add(0, stamp() - tk0);
-    pr_add(12, 1);
-    if (fresh_tid() == 0)
-      for (int k = 0; k < 16; ++k)
-        if (L.prof[k]) __hip_atomic_fetch_add(&g_uprof[k], (unsigned long long)L.prof[k], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// The default unmask with v5 for mixed batches (v3's 4-tile windows for
-// batches of equal-size frames, as k_unmask_auto).
-template <int PROF = 0>
+// The default unmask: the batch's own statistics pick the window scheme --
+// batches of equal-size frames (at least half of the frames the size of the
+// one before them on the connection: C1, C2, C3, C5) take v3's 4-tile windows,
+// mixed ones (C4) v5's pipelined 8-tile windows, with the whole (wide) grid
+// for a batch of fewer than kWideGridTiles tiles.  One kernel, one LDS
+// budget, the choice is a uniform branch on the summary the walk wrote.
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto5(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
     const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
-  __shared__ uint32_t s_start[kWin4Frames];
-  __shared__ int32_t s_lend[kWin4Frames];
-  __shared__ uint64_t s_delta[kWin4Frames];
-  __shared__ uint32_t s_key[kWin4Frames];
+  static_assert(kWinFrames == kWin5Frames, "one frame table for both bodies");
+  __shared__ uint32_t s_start[kWinFrames];
+  __shared__ int32_t s_lend[kWinFrames];
+  __shared__ uint64_t s_delta[kWinFrames];
+  __shared__ uint32_t s_key[kWinFrames];
   __shared__ __attribute__((aligned(16))) uint16_t s_own[2 * kWinChunks];
   __shared__ uint32_t s_wtot[2 * (kUnmaskBlock / 64)];
   __shared__ uint32_t s_tmap[kTmapN];
-  __shared__ uint64_t s_prof[PROF ? 16 : 1];
   if (2 * sum->run_frames >= sum->frames)
-    unmask_v3_body<16, false, true, 2, kWinTiles, false, true, true>(in, frames, tile_first, sum, out, big_grid,
-                                                                     WinLds{s_start, s_lend, s_delta, s_key});
+    unmask_v3_body<16>(in, frames, tile_first, sum, out, big_grid, WinLds{s_start, s_lend, s_delta, s_key});
   else
-    unmask_v5_body<16, true, PROF>(in, frames, tile_first, sum, out, big_grid,
-                                   WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap, s_prof},
-                                   sum->payload_bytes / kTile < kWideGridTiles);
+    unmask_v5_body<16>(in, frames, tile_first, sum, out, big_grid,
+                       WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap},
+                       sum->payload_bytes / kTile < kWideGridTiles);
 }
 
-// v5 alone at more workgroups per CU (measurement): U-tile streaming steps
-// and the register cap of WPE waves per SIMD -- a mixed-size batch's window
-// path wants more windows in flight per CU; auto5's 16-tile streaming steps
-// hold it to 4.
-template <int U, int WPE>
-__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_unmask_v5w(
+// v5 for every batch (GEVWS_TUNE_UNMASK_VARIANT 1): the mixed-size path on any
+// batch, so the parity tests run it over equal-size frames too.
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_v5(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
     const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
-  __shared__ int32_t s_lend[kWin4Frames];
-  __shared__ uint64_t s_delta[kWin4Frames];
-  __shared__ uint32_t s_key[kWin4Frames];
+  __shared__ int32_t s_lend[kWin5Frames];
+  __shared__ uint64_t s_delta[kWin5Frames];
+  __shared__ uint32_t s_key[kWin5Frames];
   __shared__ __attribute__((aligned(16))) uint16_t s_own[2 * kWinChunks];
   __shared__ uint32_t s_wtot[2 * (kUnmaskBlock / 64)];
   __shared__ uint32_t s_tmap[kTmapN];
-  __shared__ uint64_t s_prof[1];
-  unmask_v5_body<U, true, 0>(in, frames, tile_first, sum, out, big_grid,
-                             WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap, s_prof},
-                             sum->payload_bytes / kTile < kWideGridTiles);
+  unmask_v5_body<16>(in, frames, tile_first, sum, out, big_grid,
+                     WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap},
+                     sum->payload_bytes / kTile < kWideGridTiles);
 }
 
 // ------------------------------------------------------------------ outbound encode (§8f row 1)
@@ -3696,25 +2413,35 @@ __device__ __forceinline__ u128 byte_mask(int k0, int k1) {
   return hi & ~lo;
 }
 
+// The LDS frame table of an encode window.  LH: the serialised headers are
+// not kept in LDS (h0 / h1 unused) but rebuilt from the frame's record (an L2
+// hit: the window just loaded it), which frees 16 KiB of LDS per workgroup for
+// occupancy -- k_encode; the one-workgroup k_handle_small keeps them in LDS.
+struct EncWin {
+  const int32_t* start;  // wire start relative to the window, clamped >= -64
+  const int32_t* pend;   // payload end relative to the window, clamped
+  const uint8_t* hlen;
+  const uint64_t* delta;  // payload_off - out_off - hlen (mod 2^64)
+  const uint64_t* h0;     // !LH: serialised header bytes 0-7 / 8-15
+  const uint64_t* h1;
+};
+
 // Assemble the 16 output bytes at window-relative position `rel` (absolute `a`)
-// from the frames overlapping it (at most 8: every frame is >= 2 wire bytes):
-// header bytes from the frame's serialised header, payload bytes from ONE
-// unaligned 16-byte load per frame (all loads independent).
-// LH: the serialised headers are not kept in LDS but rebuilt from the frame's
-// record (an L2 hit: the window just loaded it), which frees 16 KiB of LDS per
-// workgroup for occupancy.
+// from the frames overlapping it (at most 8: every frame is >= 2 wire bytes),
+// starting at frame lo: header bytes from the frame's serialised header,
+// payload bytes from ONE unaligned 16-byte load per frame.  The first two
+// frames' loads are issued together (most boundary chunks hold the end of one
+// payload and the header + start of the next: C2 -2.6 %, C5 -1.6 % against one
+// at a time, profiles/r01_encode_ab_asm2_*.json); further frames (frames of a
+// few bytes) continue one by one.
 template <bool LH>
-__device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
-                                              const int32_t* s_start, const int32_t* s_pend, const uint8_t* s_hlen,
-                                              const uint64_t* s_delta, const uint64_t* s_h0, const uint64_t* s_h1,
-                                              const uint8_t* __restrict__ payload,
-                                              const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
-  u128 acc = 0;
-  const int kmax = (a + 16 <= total) ? 16 : (int)(total - a);
-  for (uint32_t j = lo; j < F && s_start[j] < rel + kmax; ++j) {
-    const int32_t hs = s_start[j];
-    const int32_t ps = hs + (int32_t)s_hlen[j];
-    const int32_t pe = s_pend[j];
+__device__ __forceinline__ void enc_assemble_from(u128& acc, int32_t rel, uint64_t a, int kmax, uint32_t j, uint32_t F,
+                                                  const EncWin& W, const uint8_t* __restrict__ payload,
+                                                  const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
+  for (; j < F && W.start[j] < rel + kmax; ++j) {
+    const int32_t hs = W.start[j];
+    const int32_t ps = hs + (int32_t)W.hlen[j];
+    const int32_t pe = W.pend[j];
     // header bytes [max(hs, rel), min(ps, rel + kmax))
     const int32_t h0 = hs > rel ? hs : rel;
     const int32_t h1 = ps < rel + kmax ? ps : rel + kmax;
@@ -3725,34 +2452,25 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
         enc_header(fr[f_lo + j].hdr, hl, hh);
         H = (u128)hl | ((u128)hh << 64);
       } else {
-        H = (u128)s_h0[j] | ((u128)s_h1[j] << 64);
+        H = (u128)W.h0[j] | ((u128)W.h1[j] << 64);
       }
-      const u128 part = (H >> (8 * (h0 - hs))) << (8 * (h0 - rel));
-      acc |= part & byte_mask(h0 - rel, h1 - rel);
+      acc |= ((H >> (8 * (h0 - hs))) << (8 * (h0 - rel))) & byte_mask(h0 - rel, h1 - rel);
     }
     // payload bytes [max(ps, rel), min(pe, rel + kmax))
     const int32_t p0 = ps > rel ? ps : rel;
     const int32_t p1 = pe < rel + kmax ? pe : rel + kmax;
     if (p0 < p1) {
       const int k0 = p0 - rel;
-      const u128 v = u128_of(ld16u(payload + (a + (uint64_t)k0 + s_delta[j])));
+      const u128 v = u128_of(ld16u(payload + (a + (uint64_t)k0 + W.delta[j])));
       acc |= (v << (8 * k0)) & byte_mask(k0, p1 - rel);
     }
   }
-  return u32x4_of(acc);
 }
 
-// enc_assemble with the first two overlapping frames' loads issued together
-// (most boundary chunks hold the end of one payload and the header + start of
-// the next); further frames (frames of a few bytes) continue in the loop.
-// The default encode's assembly: C2 -2.6 %, C5 -1.6 %, C3 / C4 -0.3..-0.5 %
-// (profiles/r01_encode_ab_asm2_*.json).
 template <bool LH>
-__device__ __forceinline__ u32x4 enc_assemble2(int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
-                                               const int32_t* s_start, const int32_t* s_pend, const uint8_t* s_hlen,
-                                               const uint64_t* s_delta, const uint64_t* s_h0, const uint64_t* s_h1,
-                                               const uint8_t* __restrict__ payload,
-                                               const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
+__device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
+                                              const EncWin& W, const uint8_t* __restrict__ payload,
+                                              const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
   const int kmax = (a + 16 <= total) ? 16 : (int)(total - a);
   int32_t hs[2], h0[2], h1[2], p0[2], p1[2];
   u32x4 pv[2];
@@ -3760,21 +2478,21 @@ __device__ __forceinline__ u32x4 enc_assemble2(int32_t rel, uint64_t a, uint64_t
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const uint32_t j = lo + k;
-    const bool in = j < F && s_start[j < F ? j : lo] < rel + kmax;
+    const bool in = j < F && W.start[j < F ? j : lo] < rel + kmax;
     const uint32_t jj = in ? j : lo;
-    hs[k] = s_start[jj];
-    const int32_t ps = hs[k] + (int32_t)s_hlen[jj];
-    const int32_t pe = s_pend[jj];
+    hs[k] = W.start[jj];
+    const int32_t ps = hs[k] + (int32_t)W.hlen[jj];
+    const int32_t pe = W.pend[jj];
     h0[k] = hs[k] > rel ? hs[k] : rel;
     h1[k] = in ? (ps < rel + kmax ? ps : rel + kmax) : h0[k];
     p0[k] = ps > rel ? ps : rel;
     p1[k] = in ? (pe < rel + kmax ? pe : rel + kmax) : p0[k];
     pv[k] = u32x4{0, 0, 0, 0};
     hv[k] = u64x2{0, 0};
-    if (p0[k] < p1[k]) pv[k] = ld16u(payload + (a + (uint64_t)(p0[k] - rel) + s_delta[jj]));
+    if (p0[k] < p1[k]) pv[k] = ld16u(payload + (a + (uint64_t)(p0[k] - rel) + W.delta[jj]));
     if (h0[k] < h1[k]) {
       if constexpr (LH) hv[k] = *reinterpret_cast<const u64x2*>(fr + f_lo + jj);  // the header half of the record
-      else hv[k] = u64x2{s_h0[jj], s_h1[jj]};
+      else hv[k] = u64x2{W.h0[jj], W.h1[jj]};
     }
   }
   u128 acc = 0;
@@ -3798,84 +2516,54 @@ __device__ __forceinline__ u32x4 enc_assemble2(int32_t rel, uint64_t a, uint64_t
       acc |= (u128_of(pv[k]) << (8 * k0)) & byte_mask(k0, p1[k] - rel);
     }
   }
-  if (lo + 2 < F && s_start[lo + 2] < rel + kmax) {  // more frames in these 16 bytes
-    const u32x4 rest =
-        enc_assemble<LH>(rel, a, total, lo + 2, F, s_start, s_pend, s_hlen, s_delta, s_h0, s_h1, payload, fr, f_lo);
-    acc |= u128_of(rest);
-  }
+  if (lo + 2 < F && W.start[lo + 2] < rel + kmax)  // more frames in these 16 bytes
+    enc_assemble_from<LH>(acc, rel, a, kmax, lo + 2, F, W, payload, fr, f_lo);
   return u32x4_of(acc);
 }
 
-// A 16-byte store of the encode's window path, non-temporal or plain.
-template <bool NT>
-__device__ __forceinline__ void win_store(u32x4 v, u32x4* p) {
-  if constexpr (NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-
-// COMPACT: a window's chunks that straddle a frame boundary (header bytes or
-// two frames' pieces) are queued in LDS and assembled afterwards by the whole
-// workgroup, one chunk per lane, instead of by the one or two lanes of each
-// wave that meet them while the other lanes of the wave wait.
-// WPE: waves per SIMD the register allocation must allow (amdgpu_waves_per_eu);
-// the window path is latency-bound, so the default LDS-light kernel is held to
-// 72 VGPRs for 7 workgroups per CU (C2 -4 %, C4 -2 % against 6 per CU; 8 per CU
-// at 64 VGPRs was slower on C5, profiles/r01_encode_ab_occ_*.json).
-// HL: the window's payload loads are all issued before its stores (as the
-// decode's window path does); without it each chunk's store waited for its
-// own load.  Alone it changed nothing measurable (C4 11.46 vs 11.47 ms).
-// WNT: the window path's stores are non-temporal (false: plain stores).
-// G64 (with HL): a 64-byte group of chunks holding a frame boundary is
-// written whole by the queue pass -- its interior chunks are queued with it,
-// four consecutive queue slots, so one store instruction writes the group's
-// 64 bytes.  Without it every frame boundary left its line to HBM as two
-// partial writes (the interior chunks, then the queued boundary chunk): C4
-// 46 M 32-byte write requests per launch, 0 with it, and the whole C4 encode
-// 10.70 -> 9.11 ms (profiles/r02_encode_pmc_split_c4*.json,
-// r02_encode_ab_g64_*.json); plain stores recovered part of it by merging
-// the pieces in L2 (10.24 ms) at 2 GB more reads.
-// EO (with HL, COMPACT; the default since round 3): the interior chunks are
-// stored only after the queue barrier and the lane's first queued chunk has
-// been assembled, so the interior loads (issued before the barrier) and the
-// first assembly's loads are in flight together -- one exposed payload latency
-// per window instead of two.  C4 9.39 -> 9.17 ms, C2 / C5 equal
-// (profiles/r03_encode_eo_ab.jsonl; variant 10 keeps the stores before).
-// MAP (with HL, COMPACT, G64, EO): a chunk's frame comes from a chunk -> frame
-// map instead of a binary search over the window's frame starts (9 dependent
-// LDS reads per chunk on C4).  The fill marks, at the first chunk starting at
-// or after each frame's wire start, the last frame with that chunk; a wave
-// then max-scans its four 64-chunk segments, each seeded with the frame that
-// covers the segment's first chunk (as the unmask's v5, k_unmask_auto5).  The
-// window holds 896 frames (not 1 024) so the map fits 7 workgroups per CU.
-template <int U, bool AL, bool COMPACT, bool LH = false, int WPE = 1, bool A2 = false, bool HL = false,
-          bool WNT = true, bool G64 = false, bool NTA = false, bool NTW = false, bool EO = false, bool MAP = false,
-          int WT = kWinTiles>
-__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode(const gevws_out_frame* __restrict__ fr,
-                                                         const uint8_t* __restrict__ payload,
-                                                         const uint64_t* __restrict__ out_off,
-                                                         const uint32_t* __restrict__ tile_first,
-                                                         const gevws_summary* __restrict__ sum,
-                                                         uint8_t* __restrict__ out, uint32_t big_grid) {
-  static_assert(!MAP || (HL && COMPACT && G64 && EO), "the map replaces the default window path's search");
-  constexpr int WF = MAP ? 896 : kEncWinFrames;  // frames per window held in LDS
-  constexpr uint32_t kChunks = WT * kUnmaskBlock;  // 16-byte chunks per window
-  constexpr uint32_t kSegs = kChunks / 64;                // 64-chunk segments (one wave step each)
-  __shared__ int32_t s_start[WF];  // wire start relative to the window, clamped >= -64
-  __shared__ int32_t s_pend[WF];   // payload end relative to the window, clamped
+// The encode's byte stream (k_enc_size / k_enc_emit placed every frame's wire
+// bytes and the output-tile -> frame map).  Each workgroup owns a contiguous
+// run of output tiles.
+//  * Inside one payload for the next U tiles: stream (a misaligned source as
+//    the unmask's streaming path: wave-contiguous U KiB spans, aligned
+//    non-temporal loads, DPP rotate + v_alignbyte; an aligned one with plain
+//    loads), aligned non-temporal stores.
+//  * Otherwise a window of kWinTiles tiles: its frames' wire starts, payload
+//    ends, header lengths and payload offsets in LDS; each lane finds the
+//    frame of each of its chunks by binary search; a chunk inside one payload
+//    is loaded (unaligned) and stored; a chunk that straddles a frame boundary
+//    (header bytes or two frames' pieces) is queued in LDS and assembled
+//    afterwards by the whole workgroup, one chunk per lane, instead of by the
+//    one or two lanes of each wave that meet them while the other lanes wait.
+//    A 64-byte group of chunks holding a boundary is queued whole (its
+//    interior chunks with it, four consecutive slots), so one store writes the
+//    group's 64 bytes: otherwise every frame boundary left its line to HBM as
+//    two partial writes (C4: 46 M 32-byte write requests per launch, 0 with
+//    it; the whole C4 encode 10.70 -> 9.11 ms, profiles/r02_encode_ab_g64_*.json).
+//    All the window's payload loads are issued before its stores, and the
+//    interior chunks are stored only after the queue barrier and the lane's
+//    first queued chunk has been assembled, so the interior loads and the first
+//    assembly's loads are in flight together (C4 9.39 -> 9.17 ms,
+//    profiles/r03_encode_eo_ab.jsonl).
+// The window path is latency-bound: the kernel is held to 72 VGPRs for 7
+// workgroups per CU (amdgpu_waves_per_eu(7): C2 -4 %, C4 -2 % against 6 per
+// CU; 8 per CU at 64 VGPRs was slower on C5, profiles/r01_encode_ab_occ_*.json).
+// Measured and not kept: 8-tile windows (C4 9.71 -> 12.23 ms), a chunk ->
+// frame map instead of the search (C4 9.35 -> 9.57 ms), non-temporal window
+// loads (C4 +8.8 %) -- DESIGN.md §5.
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(7))) void k_encode(
+    const gevws_out_frame* __restrict__ fr, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ out_off,
+    const uint32_t* __restrict__ tile_first, const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
+    uint32_t big_grid) {
+  constexpr int U = 4, WT = kWinTiles, WF = kEncWinFrames;
+  __shared__ int32_t s_start[WF];
+  __shared__ int32_t s_pend[WF];
   __shared__ uint8_t s_hlen[WF];
-  __shared__ uint32_t s_bnd[COMPACT ? WT * kUnmaskBlock : 1];  // queued chunk: rel / 16 | frame << 16
+  __shared__ uint32_t s_bnd[WT * kUnmaskBlock];  // queued chunk: rel / 16 | frame << 16 (~0: a group's filler)
   __shared__ uint32_t s_nb;
-  __shared__ uint64_t s_delta[WF];  // payload_off - out_off - hlen (mod 2^64)
-  __shared__ uint64_t s_h0[LH ? 1 : WF];
-  __shared__ uint64_t s_h1[LH ? 1 : WF];
-  __shared__ uint16_t s_own[MAP ? kChunks : 1];  // chunk -> last frame index + 1 whose start it is the first at/after
-  __shared__ uint32_t s_seed[MAP ? kSegs : 1];   // segment -> frame index + 1 covering its first chunk (0: none)
+  __shared__ uint64_t s_delta[WF];
+  const EncWin W{s_start, s_pend, s_hlen, s_delta, nullptr, nullptr};
   if (sum->status != GEVWS_OK) return;
-  if constexpr (MAP) {  // the map and the seeds start empty; each reader clears what it read
-    for (uint32_t i = fresh_tid(); i < kChunks; i += kUnmaskBlock) s_own[i] = 0;
-    if (threadIdx.x < kSegs) s_seed[threadIdx.x] = 0;
-    __syncthreads();
-  }
   const uint64_t total = sum->payload_bytes;  // wire bytes
   const uint64_t nframes = sum->frames;
   const uint64_t ntiles = (total + kTile - 1) / kTile;
@@ -3899,26 +2587,21 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
       u32x4 v[U];
       const uint8_t* s0 = payload + (base + c_delta);
       const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(s0) & 15);  // wave-uniform
-      if (AL && mis != 0) {
-        // as k_unmask_v3's streaming path: wave-contiguous U KiB spans, aligned
-        // loads, neighbour chunk by DPP rotate, lane 63's last successor loaded
+      if (mis != 0) {
         const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         const uint64_t wrel = (uint64_t)wave * U * 1024 + lane * 16;
         const uint8_t* a = s0 + wrel - mis;
         uint8_t* d = out + base + wrel;
         const bool last = lane == 63;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const u32x4* q = reinterpret_cast<const u32x4*>(a + u * 1024);
-          v[u] = NTA ? __builtin_nontemporal_load(q) : *q;
-        }
+        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + u * 1024));
         u32x4 e = u32x4{0, 0, 0, 0};
         if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
         u32x4 r = rot_next_lane(v[0]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const u32x4 rn = u + 1 < U ? rot_next_lane(v[u + 1 < U ? u + 1 : u]) : e;
-          __builtin_nontemporal_store(funnel16(v[u], last ? rn : r, mis), reinterpret_cast<u32x4*>(d + u * 1024));
+          st16_nt(d + u * 1024, funnel16(v[u], last ? rn : r, mis));
           r = rn;
         }
         t += U;
@@ -3927,7 +2610,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = ld16u(payload + (base + u * kTile + lane_off + c_delta));
 #pragma unroll
-      for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(out + base + u * kTile + lane_off));
+      for (int u = 0; u < U; ++u) st16_nt(out + base + u * kTile + lane_off, v[u]);
       t += U;
       continue;
     }
@@ -3938,10 +2621,9 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
     const uint64_t F = f_hi - f_lo + 1;
     if (F <= (uint64_t)WF) {
       __syncthreads();
-      for (uint64_t i = fresh_tid(); i < F; i += kUnmaskBlock) {  // (fresh_tid: see k_unmask_v4's fill)
+      for (uint64_t i = fresh_tid(); i < F; i += kUnmaskBlock) {
         const gevws_out_frame o = fr[f_lo + i];
-        uint64_t lo, hi;
-        const uint32_t hl = enc_header(o.hdr, lo, hi);
+        const uint32_t hl = enc_hlen(o.hdr);
         const uint64_t oo = out_off[f_lo + i];
         const int64_t st = (int64_t)(oo - wbase);
         s_start[i] = st < -64 ? -64 : (int32_t)st;
@@ -3949,181 +2631,76 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(WP
         s_pend[i] = pe > 0x7fffffffll ? 0x7fffffff : (int32_t)pe;
         s_hlen[i] = hl;
         s_delta[i] = o.payload_off - oo - hl;
-        if constexpr (!LH) {
-          s_h0[i] = lo;
-          s_h1[i] = hi;
-        }
-        if constexpr (MAP) {
-          // key: the first chunk starting at or after the frame's wire start;
-          // the next frame starts at this one's end (the wire is contiguous)
-          const int64_t key = st <= 0 ? 0 : (st + 15) >> 4;
-          const int64_t nk = pe <= 0 ? 0 : (pe + 15) >> 4;
-          const bool last = i + 1 == F;
-          if (key < (int64_t)kChunks && (last || nk != key)) s_own[key] = (uint16_t)(i + 1);
-          // seed every segment whose first chunk this frame covers: key < 64 m <= nk
-          const int64_t m1 = last ? (int64_t)kSegs - 1 : (nk / 64 < (int64_t)kSegs - 1 ? nk / 64 : (int64_t)kSegs - 1);
-          for (int64_t m = key / 64 + 1; m <= m1; ++m) s_seed[m] = (uint32_t)(i + 1);
-        }
       }
-      if (COMPACT && threadIdx.x == 0) s_nb = 0;
+      if (threadIdx.x == 0) s_nb = 0;
       __syncthreads();
-      if constexpr (HL && COMPACT) {
-        // loads first, the queue entries after them.  Every valid chunk
-        // loads (a boundary chunk from payload[0], always readable, result
-        // unused): a load inside the interior/boundary branch made the
-        // compiler wait for it at the branch's join
-        u32x4 v[WT];
-        uint32_t interior = 0, queued = 0;
-        uint32_t qlo[WT];
-        uint32_t mlo[MAP ? WT : 1];
-        if constexpr (MAP) {
-          // chunk u * 256 + tid = segment 4 u + wave, lane: an inclusive max scan
-          // per segment, seeded; map entries and seeds cleared by their reader
-          const uint32_t tq = fresh_tid(), lane = tq & 63, wv = tq >> 6;
-#pragma unroll
-          for (int u = 0; u < WT; ++u) {
-            const uint32_t c = (uint32_t)u * kUnmaskBlock + tq;
-            mlo[u] = s_own[c];
-            s_own[c] = 0;
-          }
-#pragma unroll
-          for (int d = 1; d < 64; d <<= 1)
-#pragma unroll
-            for (int u = 0; u < WT; ++u) {
-              const uint32_t y = (uint32_t)__shfl_up((int)mlo[u], d, 64);
-              if (lane >= (uint32_t)d) mlo[u] = mlo[u] > y ? mlo[u] : y;
-            }
-#pragma unroll
-          for (int u = 0; u < WT; ++u) {
-            const uint32_t m = (uint32_t)u * (kUnmaskBlock / 64) + wv;
-            const uint32_t seed = s_seed[m];
-            mlo[u] = mlo[u] > seed ? mlo[u] : seed;
-            mlo[u] = mlo[u] ? mlo[u] - 1 : 0u;
-          }
-          if (lane < (uint32_t)WT) s_seed[lane * (kUnmaskBlock / 64) + wv] = 0;  // after the wave's reads
-        }
-#pragma unroll
-        for (int u = 0; u < WT; ++u) {
-          const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
-          const uint64_t a = wbase + (uint64_t)rel;
-          const bool valid = (uint64_t)u < wt && a < total;
-          uint32_t lo = 0, hi = valid ? (uint32_t)F - 1 : 0u;
-          if constexpr (MAP) {
-            lo = valid ? mlo[u] : 0u;
-          } else {
-            while (lo < hi) {
-              const uint32_t mid = (lo + hi + 1) >> 1;
-              if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
-            }
-          }
-          const bool in = valid && rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo];
-          if constexpr (!G64) v[u] = ld16u_stream<NTW>(payload + (in ? a + s_delta[lo] : 0ull));  // (G64: below)
-          qlo[u] = lo;
-          interior |= (in ? 1u : 0u) << u;
-          queued |= (valid && !in ? 1u : 0u) << u;
-        }
-        if constexpr (G64) {
-          const uint32_t lane = threadIdx.x & 63, g0 = lane & ~3u;
-#pragma unroll
-          for (int u = 0; u < WT; ++u) {
-            const uint64_t bal = __ballot((queued >> u) & 1u);  // whole wave active
-            const bool defer = ((bal >> g0) & 0xFull) != 0;     // (group-uniform)
-            uint32_t slot = 0;
-            if (defer && (lane & 3u) == 0) slot = atomicAdd(&s_nb, 4u);
-            slot = __shfl(slot, (int)g0);
-            if (defer) {
-              const bool valid = (interior | queued) & (1u << u);
-              s_bnd[slot + (lane & 3u)] =
-                  valid ? ((uint32_t)(u * (int32_t)kTile + (int32_t)lane_off) >> 4) | (qlo[u] << 16) : 0xffffffffu;
-              interior &= ~(1u << u);
-            }
-          }
-          // the loads, now that the chunks of queued groups are known (the
-          // queue pass loads those itself)
-#pragma unroll
-          for (int u = 0; u < WT; ++u) {
-            const bool in = (interior >> u) & 1u;
-            const uint64_t a = wbase + (uint64_t)(u * (int32_t)kTile + (int32_t)lane_off);
-            v[u] = ld16u_stream<NTW>(payload + (in ? a + s_delta[qlo[u]] : 0ull));
-          }
-        } else {
-#pragma unroll
-          for (int u = 0; u < WT; ++u)
-            if (queued & (1u << u))
-              s_bnd[atomicAdd(&s_nb, 1u)] = ((uint32_t)(u * (int32_t)kTile + (int32_t)lane_off) >> 4) | (qlo[u] << 16);
-        }
-        if constexpr (EO) {
-          __syncthreads();  // the queue is complete
-          const uint32_t nb = s_nb;
-          const uint32_t i0 = fresh_tid();
-          u32x4 x0 = u32x4{0, 0, 0, 0};
-          uint32_t q0 = 0xffffffffu;
-          if (i0 < nb) {
-            q0 = s_bnd[i0];
-            if (!(G64 && q0 == 0xffffffffu)) {
-              const int32_t rel = (int32_t)((q0 & 0xffffu) << 4);
-              x0 = enc_assemble2<LH>(rel, wbase + (uint64_t)rel, total, q0 >> 16, (uint32_t)F, s_start, s_pend,
-                                     s_hlen, s_delta, s_h0, s_h1, payload, fr, f_lo);
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < WT; ++u)
-            if (interior & (1u << u))
-              win_store<WNT>(v[u], reinterpret_cast<u32x4*>(out + wbase + u * kTile + fresh_tid() * 16));
-          if (q0 != 0xffffffffu)
-            win_store<WNT>(x0, reinterpret_cast<u32x4*>(out + wbase + (uint64_t)((q0 & 0xffffu) << 4)));
-          for (uint32_t i = i0 + kUnmaskBlock; i < nb; i += kUnmaskBlock) {
-            const uint32_t q = s_bnd[i];
-            if (G64 && q == 0xffffffffu) continue;
-            const int32_t rel = (int32_t)((q & 0xffffu) << 4);
-            const uint64_t a = wbase + (uint64_t)rel;
-            win_store<WNT>(enc_assemble2<LH>(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta,
-                                             s_h0, s_h1, payload, fr, f_lo),
-                           reinterpret_cast<u32x4*>(out + a));
-          }
-          t += wt;
-          continue;
-        }
-#pragma unroll
-        for (int u = 0; u < WT; ++u)
-          if (interior & (1u << u))
-            win_store<WNT>(v[u], reinterpret_cast<u32x4*>(out + wbase + u * kTile + fresh_tid() * 16));
-      } else
+      // every chunk's frame and kind first (interior of one payload, or a
+      // boundary to queue); a load inside the interior/boundary branch made
+      // the compiler wait for it at the branch's join
+      u32x4 v[WT];
+      uint32_t interior = 0, queued = 0;
+      uint32_t qlo[WT];
 #pragma unroll
       for (int u = 0; u < WT; ++u) {
         const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
         const uint64_t a = wbase + (uint64_t)rel;
-        if ((uint64_t)u >= wt || a >= total) continue;
-        uint32_t lo = 0, hi = (uint32_t)F - 1;
+        const bool valid = (uint64_t)u < wt && a < total;
+        uint32_t lo = 0, hi = valid ? (uint32_t)F - 1 : 0u;
         while (lo < hi) {
           const uint32_t mid = (lo + hi + 1) >> 1;
           if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
         }
-        if (rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo]) {  // interior of one payload
-          win_store<WNT>(ld16u_stream<NTW>(payload + (a + s_delta[lo])), reinterpret_cast<u32x4*>(out + a));
-        } else if constexpr (COMPACT) {
-          s_bnd[atomicAdd(&s_nb, 1u)] = ((uint32_t)rel >> 4) | (lo << 16);
-        } else {
-          const u32x4 x = enc_assemble<LH>(rel, a, total, lo, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
-                                           s_h1, payload, fr, f_lo);
-          win_store<WNT>(x, reinterpret_cast<u32x4*>(out + a));
+        const bool in = valid && rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo];
+        qlo[u] = lo;
+        interior |= (in ? 1u : 0u) << u;
+        queued |= (valid && !in ? 1u : 0u) << u;
+      }
+      // 64-byte groups holding a queued chunk go to the queue whole
+      const uint32_t lane = threadIdx.x & 63, g0 = lane & ~3u;
+#pragma unroll
+      for (int u = 0; u < WT; ++u) {
+        const uint64_t bal = __ballot((queued >> u) & 1u);  // whole wave active
+        const bool defer = ((bal >> g0) & 0xFull) != 0;     // (group-uniform)
+        uint32_t slot = 0;
+        if (defer && (lane & 3u) == 0) slot = atomicAdd(&s_nb, 4u);
+        slot = __shfl(slot, (int)g0);
+        if (defer) {
+          const bool valid = (interior | queued) & (1u << u);
+          s_bnd[slot + (lane & 3u)] =
+              valid ? ((uint32_t)(u * (int32_t)kTile + (int32_t)lane_off) >> 4) | (qlo[u] << 16) : 0xffffffffu;
+          interior &= ~(1u << u);
         }
       }
-      if constexpr (COMPACT) {
-        __syncthreads();
-        const uint32_t nb = s_nb;
-        for (uint32_t i = fresh_tid(); i < nb; i += kUnmaskBlock) {
-          const uint32_t q = s_bnd[i];
-          if (G64 && q == 0xffffffffu) continue;  // a group's slot past the batch's end
-          const int32_t rel = (int32_t)((q & 0xffffu) << 4);
-          const uint64_t a = wbase + (uint64_t)rel;
-          const u32x4 x =
-              A2 ? enc_assemble2<LH>(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
-                                     s_h1, payload, fr, f_lo)
-                 : enc_assemble<LH>(rel, a, total, q >> 16, (uint32_t)F, s_start, s_pend, s_hlen, s_delta, s_h0,
-                                    s_h1, payload, fr, f_lo);
-          win_store<WNT>(x, reinterpret_cast<u32x4*>(out + a));
+      // the interior loads (the queue pass loads its chunks itself; every lane
+      // loads, a non-interior chunk from payload[0], always readable, unused)
+#pragma unroll
+      for (int u = 0; u < WT; ++u) {
+        const bool in = (interior >> u) & 1u;
+        const uint64_t a = wbase + (uint64_t)(u * (int32_t)kTile + (int32_t)lane_off);
+        v[u] = ld16u(payload + (in ? a + s_delta[qlo[u]] : 0ull));
+      }
+      __syncthreads();  // the queue is complete
+      const uint32_t nb = s_nb;
+      const uint32_t i0 = fresh_tid();
+      u32x4 x0 = u32x4{0, 0, 0, 0};
+      uint32_t q0 = 0xffffffffu;
+      if (i0 < nb) {
+        q0 = s_bnd[i0];
+        if (q0 != 0xffffffffu) {
+          const int32_t rel = (int32_t)((q0 & 0xffffu) << 4);
+          x0 = enc_assemble<true>(rel, wbase + (uint64_t)rel, total, q0 >> 16, (uint32_t)F, W, payload, fr, f_lo);
         }
+      }
+#pragma unroll
+      for (int u = 0; u < WT; ++u)
+        if (interior & (1u << u)) st16_nt(out + wbase + u * kTile + fresh_tid() * 16, v[u]);
+      if (q0 != 0xffffffffu) st16_nt(out + wbase + (uint64_t)((q0 & 0xffffu) << 4), x0);
+      for (uint32_t i = i0 + kUnmaskBlock; i < nb; i += kUnmaskBlock) {
+        const uint32_t q = s_bnd[i];
+        if (q == 0xffffffffu) continue;  // a group's slot past the batch's end
+        const int32_t rel = (int32_t)((q & 0xffffu) << 4);
+        const uint64_t a = wbase + (uint64_t)rel;
+        st16_nt(out + a, enc_assemble<true>(rel, a, total, q >> 16, (uint32_t)F, W, payload, fr, f_lo));
       }
       t += wt;
       continue;
@@ -4473,7 +3050,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
       const uint32_t mid = (lo + hi + 1) >> 1;
       if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
     }
-    const u32x4 x = enc_assemble<false>(rel, a, wire, lo, (uint32_t)nr, s_start, s_pend, s_hlen, s_delta, s_h0, s_h1,
+    const u32x4 x = enc_assemble<false>(rel, a, wire, lo, (uint32_t)nr, EncWin{s_start, s_pend, s_hlen, s_delta, s_h0, s_h1},
                                         payload, nullptr, 0);
     __builtin_memcpy(out + a, &x, 16);
   }
@@ -4622,25 +3199,17 @@ struct gevws_ctx {
   std::vector<EventSet> evs;  // one set per timed call since the last gevws_ctx_timing
   size_t evs_used = 0;
   gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
-  int unmask_variant = 0;
-  int unmask_grid = 0;  // 0 = auto
-  int encode_variant = 0;  // 0 = aligned-load streaming + window loads before stores + boundary
-                           // 64-byte groups queued whole, headers rebuilt from the records (7
-                           // workgroups per CU); 1 = unaligned loads, per-lane assembly; 2 = aligned
-                           // loads, per-lane assembly; 3 = queued boundary chunks, headers in LDS (4
-                           // per CU); 4 = queued boundary chunks, LDS-light (round-1 default);
-                           // 5 = 4 + loads before stores; 6 = 5 with plain window stores; 7 = 0 with
-                           // plain window stores; 8 = 0 with plain (not non-temporal) streaming loads
-  int emit_variant = 0;    // 0 = grouped record pass (k_walk_emit G = 16), 1 = one wave per connection,
-                           // 2 = 0 non-temporal, 3 = 0 with 8 rounds per load
+  int unmask_variant = 0;  // GEVWS_TUNE_UNMASK_VARIANT (kUnmaskVariants)
+  int unmask_grid = 0;     // 0 = auto
+  int encode_variant = 0;  // GEVWS_TUNE_ENCODE_VARIANT (kNumEncodeVariants)
   uint64_t small_bytes = kSmallBytes;  // one-launch decode (k_decode_small) up to this many input bytes
-  uint32_t span_conns_per_cu = 0;  // walk variant 0: one wave per connection up to this many per CU
-  // the split walk's history: the last multi-kernel decode's frame / payload
-  // totals (written by k_walk_bases into mapped host memory) and its
-  // connection count, read once that decode has finished
   uint32_t* done_flag = nullptr;  // mapped host word the one-launch kernels signal (gevws_ctx_set_completion_flag)
   uint32_t done_seq = 0;
   int64_t last_signal = -1;  // the value the last call's last kernel stores there, -1: none
+  // the context's history: the last multi-kernel decode's frame / payload /
+  // equal-size-run totals (written by k_walk_bases into mapped host memory)
+  // and its connection count, read once that decode has finished; it picks
+  // the split walk, the walk's speculation and the unmask's wide grid
   uint64_t* h_stats = nullptr;
   uint64_t* d_stats = nullptr;
   bool stats_pending = false, stats_known = false;
@@ -4648,22 +3217,12 @@ struct gevws_ctx {
   bool prev_mixed = false;
   uint32_t last_unmask_grid = 0;  // workgroups of the last decode's unmask launch
   uint32_t last_ks = 1;    // lanes per connection of the last multi-kernel decode's walk
-  int split_mode = 0;       // measurement: 1 = guesses made then dropped, 2 = no guesses, 3 = the
-                            // default walk keeps its speculation (D = 8) whatever the history
-  uint32_t split_lanes = 0;  // walk variant 0: lanes per connection (k_walk_split); 0 = auto, 1 = off
-  // frames per lane of the budgeted walk: 0 = auto, -1 = never (the default:
-  // measured slower than the plain walk on C4 and its shares,
-  // profiles/r03_budget_ab.jsonl), > 0 = always
-  int64_t walk_budget = -1;
-  uint32_t resume_lanes = 0;  // lanes per resumed connection (k_walk_resume): 0 = kResumeLanes
-  uint32_t budget_frac16 = kBudgetFrac16;  // auto budget: this many 16ths of the previous mean chain
+  uint32_t split_lanes = 0;  // lanes per connection (k_walk_split); 0 = auto, 1 = off
   uint64_t split_min_bytes = kSplitMinBytes;        // split walk: bytes per segment at least
   uint64_t split_lanes_per_cu = kSplitLanesPerCU;   // split walk auto: lanes per CU at most
-  uint64_t last_budget = 0;  // budget of the last multi-kernel decode's walk (0 = not budgeted)
-  int walk_variant = 0;    // 0 = with uniform-stream speculation (8 windows), 1 = plain chain walk,
-                           // 2 = plain walk without the entry table (emit re-walks); 0 and 1 store
-                           // entries in 64-byte groups for batches of many connections; 3 / 4 =
-                           // speculation with single / grouped entry stores regardless of the batch
+  int walk_variant = 0;    // 0 = speculation (D = 8) unless the history is mixed, 1 = plain chain walk
+                           // (D = 0), 2 = no entry table (the record pass re-walks every chain), 3 =
+                           // the writer wave whatever the batch size
   // Scratch is per context: calls on a different stream than the previous one
   // first wait for it (one in-flight batch per context; use one context per
   // stream for concurrency).
@@ -4745,77 +3304,30 @@ struct UnmaskVariant {
   const char* name;
   bool wide = false;  // may launch the wide grid (k_unmask_auto)
 };
-// Variant 0 is the default; the others are kept for A/B measurement
-// (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
+// Variant 0 is the default (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
+// The measurement variants of rounds 1-3 (v3 / v4 window shapes, interleaved
+// searches, phase-profiled builds, other occupancies) are gone from the
+// library; their measurements stay in profiles/ and DESIGN.md §5.
 const UnmaskVariant kUnmaskVariants[] = {
-    {k_unmask_auto5<0>, 16,
-     "auto: v3 4-tile windows for batches of equal-size frames, v5 (v4's pipelined 8-tile windows with a chunk -> "
-     "frame map instead of per-chunk searches and the tile map cached in LDS) otherwise; non-temporal streaming "
-     "and window loads; a wide grid for a smaller batch of mixed sizes after one on this context", true},
-    {k_unmask_v4<16, 8, true>, 16,
-     "v4 U16 streaming (aligned loads, DPP rotate) + pipelined 8-tile LDS window (next step's tile map and "
-     "records fetched during the current window's payload loads)"},
-    {k_unmask_v3<16, false, true, 2>, 16,
-     "v3 U16 + 4-tile LDS window; streaming path: aligned loads, wave-contiguous 16 KiB spans, DPP rotate"},
-    {k_unmask_v3<16, false, true, 2, 8>, 16, "v3 with an 8-tile window (no pipelining)"},
-    {k_unmask_v3<16, false, true>, 16, "v3 U16 + 4-tile LDS window, unaligned streaming loads"},
-    {k_unmask_v4<16, 8, true, true>, 16,
-     "v4 with a wave-contiguous window mapping (each wave 8 contiguous KiB of the 32 KiB window)"},
-    {k_unmask_v4<16, 4, true, true>, 16, "v4 with a 4-tile wave-contiguous window"},
-    {k_unmask_v4<16, 8, true, false, false>, 16, "v4 as in round 1 (fill addresses spilled to scratch)"},
-    {k_unmask_v4<16, 4, true>, 16, "v4 with a 4-tile pipelined window"},
-    {k_unmask_v4<16, 8, true, false, true, true>, 16,
-     "v4 with software-pipelined streaming runs (8-tile steps, next step's loads before this step's stores)"},
-    {k_unmask_v4<8, 8, true, false, true, true>, 8,
-     "v4, pipelined streaming runs of 4-tile steps (streams from 8 tiles inside a frame)"},
-    {k_unmask_auto<true>, 16,
-     "auto with the window chunks' frame searches interleaved (binary lifting, one LDS round trip per step for "
-     "all chunks of a lane)"},
-    {k_unmask_auto<false>, 16, "auto with plain (temporal) streaming loads (the default until round 2's end)"},
-    {k_unmask_auto<false, true>, 16, "auto with non-temporal streaming loads, plain window loads"},
-    {k_unmask_auto<false, true, true, 1>, 16,
-     "measurement: the default with v4's phases timed per workgroup (gevws_unmask_profile)", true},
-    {k_unmask_auto<true, true, true, 1>, 16,
-     "measurement: 14 with the window searches interleaved (binary lifting, as 11)", true},
-    {k_unmask_auto<false, true, true, 2>, 16,
-     "measurement: 14 waiting for each window's payload loads right after issuing them (their latency)", true},
-    {k_unmask_auto<false, true, true>, 16,
-     "auto with v4 for mixed batches (the default until round 3: per-chunk binary searches in LDS, tile map read "
-     "with scalar loads)", true},
-    {k_unmask_auto5<1>, 16, "measurement: the default (v5) with its phases timed (gevws_unmask_profile)", true},
-    {k_unmask_v5w<8, 5>, 8, "v5 for every batch, 8-tile streaming steps, 5 waves per SIMD", true},
-    {k_unmask_v5w<8, 6>, 8, "v5 for every batch, 8-tile streaming steps, 6 waves per SIMD", true},
-    {k_unmask_v5w<16, 4>, 16, "v5 for every batch (the default's mixed-batch path alone)", true},
+    {k_unmask_auto5, 16,
+     "auto: v3 4-tile windows for batches of equal-size frames, v5 (pipelined 8-tile windows with a chunk -> frame "
+     "map and the tile map cached in LDS) otherwise; non-temporal streaming and window loads; a wide grid for a "
+     "smaller batch of mixed sizes after one on this context", true},
+    {k_unmask_v5, 16, "v5 for every batch (the default's mixed-batch path alone)", true},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
 // GEVWS_TUNE_WALK_VARIANT values (0 = the default choice per batch).
 const char* const kWalkVariants[] = {
-    "default: one wave per connection (k_walk_span, K = 1) up to GEVWS_TUNE_SPAN_CONNS_PER_CU connections per CU, "
-    "else one lane per connection with uniform-stream speculation (k_walk_count D = 8; from 128 connections per CU "
-    "the entries go through an LDS ring to a writer wave, 256-byte groups)",
+    "default: one lane per connection with uniform-stream speculation (D = 8; plain D = 0 after a batch of mixed "
+    "sizes on this context); from 128 connections per CU the entries go through an LDS ring to a writer wave "
+    "(256-byte groups); the split walk for few long chains of small frames",
     "one lane per connection, plain chain walk (D = 0)",
-    "one lane per connection, no entry table (the record pass re-walks every chain)",
-    "one lane per connection, speculation, single entry stores",
-    "one lane per connection, speculation, grouped entry stores",
-    "one lane per connection, speculation, non-temporal header loads",
-    "one wave per connection: LDS ring of 2 x 1 KiB + ballot over equal-size runs",
-    "one wave per connection: LDS ring of 2 x 2 KiB + ballot over equal-size runs",
-    "one lane per connection, plain chain walk, each header load also touches the next 128-byte line",
-    "one lane per connection, plain chain walk, each header load also touches the next two 128-byte lines",
-    "one lane per connection, 128-byte LDS row per lane: every header inside it walked before the next load",
-    "one lane per connection, 256-byte LDS row per lane: every header inside it walked before the next load",
-    "as 0 (speculating lane walk) with one window buffer (the round-2 loop: the back edge copies the loaded window)",
-    "as 1 (plain lane walk) with one window buffer (the round-2 loop)",
-    "measurement: plain lane walk storing nothing (no entries, no sink; the record pass re-walks every chain)",
-    "plain lane walk, entries through an LDS ring per lane drained to HBM by a writer wave in 256-byte groups",
-    "as 15 with uniform-stream speculation",
-    "as 15 with 64-byte groups",
-    "as 15 with 128-byte groups",
-    "measurement: as 15 with the writer storing nothing (the record pass re-walks every chain)",
-    "as 15 with non-temporal group stores",
+    "no entry table (the record pass re-walks every chain)",
+    "entries through the writer wave whatever the batch size (the default's path for >= 128 connections per CU)",
 };
 constexpr int kNumWalkVariants = sizeof(kWalkVariants) / sizeof(kWalkVariants[0]);
+constexpr int kNumEncodeVariants = 1;  // GEVWS_TUNE_ENCODE_VARIANT: 0 = k_encode
 
 }  // namespace
 
@@ -4964,44 +3476,20 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->unmask_grid = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_ENCODE_VARIANT:
-      if (value < 0 || value > 11) return GEVWS_ERR_INVALID;
+      if (value < 0 || value >= kNumEncodeVariants) return GEVWS_ERR_INVALID;
       ctx->encode_variant = (int)value;
-      return GEVWS_OK;
-    case GEVWS_TUNE_EMIT_VARIANT:
-      if (value < 0 || value > 3) return GEVWS_ERR_INVALID;
-      ctx->emit_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_SMALL_BATCH:
       if (value < 0 || (uint64_t)value > kSmallBytes) return GEVWS_ERR_INVALID;
       ctx->small_bytes = (uint64_t)value;
       return GEVWS_OK;
-    case GEVWS_TUNE_SPAN_CONNS_PER_CU:
-      if (value < 0 || value > (1 << 20)) return GEVWS_ERR_INVALID;
-      ctx->span_conns_per_cu = (uint32_t)value;
-      return GEVWS_OK;
     case GEVWS_TUNE_SPLIT_LANES:
       if (value < 0 || value > kSplitMaxLanes || (value > 1 && (value & (value - 1)))) return GEVWS_ERR_INVALID;
       ctx->split_lanes = (uint32_t)value;
       return GEVWS_OK;
-    case GEVWS_TUNE_SPLIT_MODE:
-      if (value < 0 || value > 3) return GEVWS_ERR_INVALID;
-      ctx->split_mode = (int)value;
-      return GEVWS_OK;
     case GEVWS_TUNE_WALK_VARIANT:
       if (value < 0 || value >= kNumWalkVariants) return GEVWS_ERR_INVALID;
       ctx->walk_variant = (int)value;
-      return GEVWS_OK;
-    case GEVWS_TUNE_WALK_BUDGET:
-      if (value < -1 || value > 0xFFFFFFFFll) return GEVWS_ERR_INVALID;
-      ctx->walk_budget = value;
-      return GEVWS_OK;
-    case GEVWS_TUNE_RESUME_LANES:
-      if (value < 0 || value == 1 || value > kResumeMaxLanes || (value & (value - 1))) return GEVWS_ERR_INVALID;
-      ctx->resume_lanes = (uint32_t)value;
-      return GEVWS_OK;
-    case GEVWS_TUNE_BUDGET_FRAC:
-      if (value < 1 || value > 64) return GEVWS_ERR_INVALID;
-      ctx->budget_frac16 = (uint32_t)value;
       return GEVWS_OK;
     case GEVWS_TUNE_SPLIT_MIN_BYTES:
       if (value < 1024 || value > (1ll << 30)) return GEVWS_ERR_INVALID;
@@ -5034,28 +3522,7 @@ int gevws_ctx_set_completion_flag(gevws_ctx* ctx, uint32_t* d_flag) {
 
 int64_t gevws_ctx_completion_seq(const gevws_ctx* ctx) { return ctx ? ctx->last_signal : -1; }
 
-int64_t gevws_ctx_last_walk_budget(const gevws_ctx* ctx) { return ctx ? (int64_t)ctx->last_budget : -1; }
-
-int64_t gevws_ctx_last_resumed(gevws_ctx* ctx) {
-  if (!ctx) return -1;
-  DeviceGuard g(ctx->device);
-  if (ctx->has_last && hipEventSynchronize(ctx->last_done) != hipSuccess) return GEVWS_ERR_DEVICE;
-  return (int64_t)ctx->h_stats[3];
-}
-
 int gevws_ctx_last_unmask_grid(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_unmask_grid : -1; }
-
-int gevws_unmask_profile(gevws_ctx* ctx, uint64_t out[16], int reset) {
-  if (!ctx || !out) return GEVWS_ERR_INVALID;
-  DeviceGuard g(ctx->device);
-  GEVWS_HIP(hipDeviceSynchronize());
-  GEVWS_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_uprof), 16 * sizeof(uint64_t)));
-  if (reset) {
-    const uint64_t z[16] = {};
-    GEVWS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_uprof), z, sizeof(z)));
-  }
-  return GEVWS_OK;
-}
 
 int gevws_ctx_set_timing(gevws_ctx* ctx, int enable) {
   if (!ctx) return GEVWS_ERR_INVALID;
@@ -5094,7 +3561,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   // a small batch with the default kernels: the whole decode in one launch
   // (per-phase timing and the variant knobs keep the multi-kernel path)
   if (n_conns <= kSmallConns && in_bytes <= ctx->small_bytes && !ctx->timing && ctx->walk_variant == 0 &&
-      ctx->unmask_variant == 0 && ctx->emit_variant == 0 && ctx->span_conns_per_cu == 0 && ctx->unmask_grid == 0) {
+      ctx->unmask_variant == 0 && ctx->unmask_grid == 0) {
     int r = order_after_last(ctx, st);
     if (r != GEVWS_OK) return r;
     const uint32_t seq = ctx->done_flag ? ++ctx->done_seq : 0u;
@@ -5105,35 +3572,28 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     if (ctx->done_flag) ctx->last_signal = seq;
     return r;
   }
-  // connections per counting workgroup: 64, or fewer so a small batch covers every CU
   const uint32_t ncu = (uint32_t)ctx->num_cus;
-  // header walk: one wave per connection (k_walk_span) when the batch has few
-  // connections for the chip -- its chains, not the memory system, bound the
-  // walk -- else one lane per connection (k_walk_count)
-  const int wv = ctx->walk_variant;
-  const bool span = wv == 6 || wv == 7 ||
-                    (wv == 0 && (uint64_t)n_conns <= (uint64_t)ctx->span_conns_per_cu * ncu);
-  const uint32_t cpb = span ? (uint32_t)kSpanWaves
-                            : n_conns >= (uint32_t)kCountBlock * ncu
-                                  ? (uint32_t)kCountBlock
-                                  : (n_conns + ncu - 1) / ncu > 0 ? (n_conns + ncu - 1) / ncu : 1;
-  // split walk (k_walk_split): ks lanes per connection when the batch has too
-  // few connections to keep kSplitLanesPerCU lanes per CU walking, and they
-  // are long enough to split
-  uint32_t ks = 1;
+  // connections per counting workgroup: 64, or fewer so a small batch covers every CU
+  const uint32_t cpb = n_conns >= (uint32_t)kCountBlock * ncu ? (uint32_t)kCountBlock
+                                                             : (n_conns + ncu - 1) / ncu > 0 ? (n_conns + ncu - 1) / ncu : 1;
+  // the context's history, once its last multi-kernel decode has finished
   if (ctx->stats_pending && hipEventQuery(ctx->last_done) == hipSuccess) {
     ctx->stats_pending = false;
     ctx->stats_known = true;
     const uint64_t fr = ctx->h_stats[0], pl = ctx->h_stats[1];
     ctx->prev_frames_per_conn = ctx->stats_conns ? fr / ctx->stats_conns : 0;
     ctx->prev_frame_bytes = fr ? pl / fr : 0;
-    ctx->prev_mixed = 2 * ctx->h_stats[2] < fr;  // k_unmask_auto's v4 choice
+    ctx->prev_mixed = 2 * ctx->h_stats[2] < fr;  // k_unmask_auto5's v5 choice
   }
-  if (!span && wv == 0 && n_conns) {
+  // split walk (k_walk_split): ks lanes per connection when the batch has too
+  // few connections to keep kSplitLanesPerCU lanes per CU walking, and they
+  // are long chains of small frames (the previous decode's)
+  const int wv = ctx->walk_variant;
+  uint32_t ks = 1;
+  if (wv == 0 && n_conns) {
     if (ctx->split_lanes >= 2) {
       ks = ctx->split_lanes;
-    } else if (ctx->split_lanes == 0 && ctx->walk_budget <= 0 && in_bytes / n_conns >= 2 * kSplitMinBytes &&
-               ctx->stats_known &&
+    } else if (ctx->split_lanes == 0 && in_bytes / n_conns >= 2 * kSplitMinBytes && ctx->stats_known &&
                ctx->prev_frames_per_conn >= kSplitMinFramesPerConn && ctx->prev_frame_bytes <= kSplitMaxFrameBytes) {
       if ((uint64_t)n_conns <= kSplitMaxConnsPerCU * ncu)
         while (ks < kSplitAutoMaxLanes && (uint64_t)n_conns * ks * 2 <= ctx->split_lanes_per_cu * ncu) ks *= 2;
@@ -5141,31 +3601,9 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   }
   if ((uint64_t)n_conns * ks > 0xFFFFFFFFull) ks = 1;
   ctx->last_ks = ks;
-  // budgeted walk (k_walk_count BUD + k_walk_resume): a batch of many long
-  // chains of small frames -- too many connections for the split walk --
-  // walks each chain for ~ the previous batch's mean chain length, then the
-  // unfinished ones rks lanes wide from where they stopped
-  uint64_t budget = 0;
-  uint32_t rks = 1;
-  if (!span && wv == 0 && n_conns && ks == 1 && ctx->walk_budget >= 0) {
-    if (ctx->walk_budget > 0) {
-      budget = (uint64_t)ctx->walk_budget;
-    } else if (ctx->stats_known && ctx->prev_frames_per_conn >= kSplitMinFramesPerConn &&
-               ctx->prev_frame_bytes <= kSplitMaxFrameBytes && in_bytes / n_conns >= 2 * kSplitMinBytes) {
-      budget = ctx->prev_frames_per_conn * ctx->budget_frac16 / 16;
-      if (budget < 1) budget = 1;
-    }
-    if (budget) rks = ctx->resume_lanes ? ctx->resume_lanes : kResumeLanes;
-    if ((uint64_t)n_conns * rks > 0xFFFFFFFFull) {
-      budget = 0;
-      rks = 1;
-    }
-  }
-  ctx->last_budget = budget;
-  const uint32_t rows = ks > 1 ? ks : rks;  // record-pass rows per connection
   const uint32_t cpb_w = ks > 1 ? (kCountBlock / ks < cpb ? kCountBlock / ks : cpb) : cpb;
   const uint32_t nblk = (n_conns + cpb_w - 1) / cpb_w;
-  const uint64_t n_v = (uint64_t)n_conns * rows;  // rows of the record pass's connection table
+  const uint64_t n_v = (uint64_t)n_conns * ks;  // rows of the record pass's connection table
   const uint64_t ntiles_cap = (payload_cap + kTile - 1) / kTile + 1;
   const size_t blk_bytes = ((size_t)nblk * kDecFields * sizeof(uint64_t) + 255) & ~size_t(255);
   const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
@@ -5173,14 +3611,11 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   while ((in_bytes >> gshift) > kEntryBudget) ++gshift;
   const uint64_t n_entries = kSlotAlign * ((in_bytes >> (gshift + kSlotShift)) + n_v + 1);
   const size_t flag_bytes = ((size_t)n_conns + 255) & ~size_t(255);
-  const size_t seg_bytes = rows > 1 ? ((n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out) + 1) + 1023) & ~size_t(255)) : 0;
-  // the budgeted walk's resume list + its length
-  const size_t res_bytes = budget ? (size_t)n_conns * sizeof(WalkResume) + 256 : 0;
+  const size_t seg_bytes = ks > 1 ? ((n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out) + 1) + 1023) & ~size_t(255)) : 0;
   // + one sink slot per walk lane after the table (k_walk_count / k_walk_split)
   int r = order_after_last(ctx, st);
   if (r != GEVWS_OK) return r;
-  r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + seg_bytes + res_bytes +
-                              (n_entries + n_v) * sizeof(WalkEntry));
+  r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + seg_bytes + (n_entries + n_v) * sizeof(WalkEntry));
   if (r != GEVWS_OK) return r;
   char* sp = reinterpret_cast<char*>(ctx->scratch);
   uint64_t* blk = reinterpret_cast<uint64_t*>(sp);
@@ -5190,9 +3625,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   gevws_conn_in* segs = reinterpret_cast<gevws_conn_in*>(segp);
   gevws_conn_out* sout = reinterpret_cast<gevws_conn_out*>(segp + n_v * sizeof(gevws_conn_in));
   uint8_t* srec = reinterpret_cast<uint8_t*>(segp + n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out)));
-  WalkResume* rlist = reinterpret_cast<WalkResume*>(segp + seg_bytes);
-  uint32_t* rcount = reinterpret_cast<uint32_t*>(segp + seg_bytes + res_bytes - 256);
-  WalkEntry* entries = reinterpret_cast<WalkEntry*>(segp + seg_bytes + res_bytes);
+  WalkEntry* entries = reinterpret_cast<WalkEntry*>(segp + seg_bytes);
   const bool timed = ctx->timing;
   hipEvent_t* ev = nullptr;
   if (timed) {
@@ -5204,192 +3637,63 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
     ev = ctx->evs[ctx->evs_used++].e;
     GEVWS_HIP(hipEventRecord(ev[0], st));
   }
-  // walk variant 2 (measurement): no entry table -- the counting walk stores
-  // nothing per frame and the emit pass re-walks every chain
-  const uint64_t ne = ctx->walk_variant == 2 ? 0 : n_entries;
+  // walk variant 2: no entry table -- the counting walk stores nothing per
+  // frame and the record pass re-walks every chain
+  const uint64_t ne = wv == 2 ? 0 : n_entries;
   // The walk's last workgroup scans the partials itself (walk_block_done) and
   // saves the k_scan_blocks launch (with release / acquire fences instead of
   // coherent partials it was slower: C1-shaped walk 0.034 -> 0.074 ms,
   // profiles/r02_steps_fused.jsonl).
-  // (the budgeted walk's partials are complete only after k_walk_resume)
-  const bool fused = kFusedScan && nblk > 0 && nblk <= kFusedScanMaxBlocks && !budget;
+  const bool fused = nblk > 0 && nblk <= kFusedScanMaxBlocks;
   uint32_t* done = fused ? ctx->d_done : nullptr;
-  // the default walk's uniform-stream speculation (D = 8) pays on long runs of
-  // equal frames (C2, C3: -23..-28 %) and costs 2-7 % elsewhere (C1, C4,
+  // the walk's uniform-stream speculation (D = 8) pays on long runs of equal
+  // frames (C2, C3: -23..-28 %) and costs 2-7 % elsewhere (C1, C4,
   // profiles/r02_walk_store_count_ab.jsonl); after a decode on this context
   // whose frames were mostly NOT the size of their predecessor the plain
   // chain walk (D = 0) runs instead
-  const bool plain = wv == 0 && ctx->split_mode != 3 && ctx->stats_known && ctx->prev_mixed;
-  if (nblk && budget) {
-    const bool grp = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
-    GEVWS_HIP(hipMemsetAsync(rcount, 0, sizeof(uint32_t), st));
-    auto kc = grp ? (plain ? k_walk_count<0, true, false, 0, true> : k_walk_count<8, true, false, 0, true>)
-                  : (plain ? k_walk_count<0, false, false, 0, true> : k_walk_count<8, false, false, 0, true>);
-    kc<<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes,
-                                     nullptr, max_frames, payload_cap, d_summary, budget, rks, segs, sout, srec, rlist,
-                                     rcount);
-    uint64_t rgrid = ((uint64_t)n_conns * rks + kCountBlock - 1) / kCountBlock;
-    if (rgrid > kResumeBlocksPerCU * ncu) rgrid = kResumeBlocksPerCU * ncu;
-#define GEVWS_RESUME(K)                                                                                  \
-  (plain ? k_walk_resume<K, 0> : k_walk_resume<K, 8>)<<<(uint32_t)rgrid, kCountBlock, 0, st>>>(        \
-      d_in, d_conns, d_conn_out, blk, entries, ne, gshift, cpb, rlist, rcount, segs, sout, srec)
-    if (rks == 2) GEVWS_RESUME(2);
-    else if (rks == 4) GEVWS_RESUME(4);
-    else if (rks == 8) GEVWS_RESUME(8);
-    else GEVWS_RESUME(16);
-#undef GEVWS_RESUME
-  } else if (nblk && ks > 1) {
-    // (entry groups by the real connection count: the segments of one
-    // connection are one chain's worth of line traffic)
-    const bool grp = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
+  const bool plain = wv == 1 || (wv != 1 && ctx->stats_known && ctx->prev_mixed);
+  if (nblk && ks > 1) {
 #define GEVWS_SPLIT(K)                                                                                            \
-  (grp ? k_walk_split<K, 8, true> : plain ? k_walk_split<K, 0, false> : k_walk_split<K, 8, false>)               \
-      <<<nblk, kCountBlock, 0, st>>>(                                                                             \
+  (plain ? k_walk_split<K, 0> : k_walk_split<K, 8>)<<<nblk, kCountBlock, 0, st>>>(                                \
       d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb_w, in_bytes, done, max_frames, payload_cap, \
-      d_summary, segs, sout, srec, ctx->split_mode, ctx->split_min_bytes)
+      d_summary, segs, sout, srec, ctx->split_min_bytes)
     if (ks == 2) GEVWS_SPLIT(2);
     else if (ks == 4) GEVWS_SPLIT(4);
     else if (ks == 8) GEVWS_SPLIT(8);
     else if (ks == 16) GEVWS_SPLIT(16);
     else GEVWS_SPLIT(32);
 #undef GEVWS_SPLIT
-  } else if (nblk && span) {
-    if (wv == 7)
-      k_walk_span<2><<<nblk, kSpanWaves * 64, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
-                                                       in_bytes, done, max_frames, payload_cap, d_summary);
-    else
-      k_walk_span<1><<<nblk, kSpanWaves * 64, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift,
-                                                       in_bytes, done, max_frames, payload_cap, d_summary);
+  } else if (nblk && (wv == 3 || (uint64_t)n_conns >= kWriterChainsPerCU * (uint64_t)ncu)) {
+    // many chains: the walk is bound by its line traffic -- entries through
+    // each lane's LDS ring to the workgroup's writer wave (k_walk_count ST 2)
+    (plain ? k_walk_count<0, 2> : k_walk_count<8, 2>)<<<nblk, 2 * kCountBlock, 0, st>>>(
+        d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes, done, max_frames, payload_cap,
+        d_summary);
   } else if (nblk) {
-    // grouped entry stores pay off when the walk is bound by its line traffic
-    // (many concurrent chains), not by chain latency (few)
-    const bool many = (uint64_t)n_conns >= kGroupedWalkChainsPerCU * (uint64_t)ncu;
-    const bool grp = wv == 4 || ((wv == 0 || wv == 1 || wv == 5 || wv == 8 || wv == 9 || wv >= 10) && many);
-    if (wv >= 15 && wv <= 20) {
-      (wv == 15   ? k_walk_count<0, false, false, 0, false, 2, 2, 32>
-       : wv == 16 ? k_walk_count<8, false, false, 0, false, 2, 2, 32>
-       : wv == 17 ? k_walk_count<0, false, false, 0, false, 2, 2, 8>
-       : wv == 18 ? k_walk_count<0, false, false, 0, false, 2, 2, 16>
-       : wv == 19 ? k_walk_count<0, false, false, 0, false, 2, 2, 32, 1>
-                  : k_walk_count<0, false, false, 0, false, 2, 2, 32, 2>)
-          <<<nblk, 2 * kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb,
-                                             in_bytes, done, max_frames, payload_cap, d_summary, ~0ull, 1u, nullptr,
-                                             nullptr, nullptr, nullptr, nullptr);
-    } else if (wv == 14) {
-      k_walk_count<0, false, false, 0, false, 2, 1><<<nblk, kCountBlock, 0, st>>>(
-          d_in, d_conns, n_conns, d_conn_out, blk, entries, 0, gshift, cpb, in_bytes, done, max_frames, payload_cap,
-          d_summary);
-    } else if (wv == 12 || wv == 13) {
-      auto k1 = wv == 12 ? (grp ? k_walk_count<8, true, false, 0, false, 1> : k_walk_count<8, false, false, 0, false, 1>)
-                         : (grp ? k_walk_count<0, true, false, 0, false, 1> : k_walk_count<0, false, false, 0, false, 1>);
-      k1<<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes,
-                                       done, max_frames, payload_cap, d_summary, ~0ull, 1u, nullptr, nullptr, nullptr,
-                                       nullptr, nullptr);
-    } else if (wv == 10 || wv == 11) {
-      auto kb = wv == 10 ? (grp ? k_walk_buf<128, true> : k_walk_buf<128, false>)
-                         : (grp ? k_walk_buf<256, true> : k_walk_buf<256, false>);
-      kb<<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes,
-                                       done, max_frames, payload_cap, d_summary);
-    } else if (wv == 8 || wv == 9) {
-      if (grp && wv == 8)
-        k_walk_count<0, true, false, 1><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
-                                                                     entries, ne, gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-      else if (wv == 8)
-        k_walk_count<0, false, false, 1><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
-                                                                      entries, ne, gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-      else if (grp)
-        k_walk_count<0, true, false, 2><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
-                                                                     entries, ne, gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-      else
-        k_walk_count<0, false, false, 2><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk,
-                                                                      entries, ne, gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-    } else if (wv == 5) {
-      if (grp)
-        k_walk_count<8, true, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries,
-                                                                  ne, gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-      else
-        k_walk_count<8, false, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries,
-                                                                   ne, gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-    } else if (wv == 1) {
-      if (grp)
-        k_walk_count<0, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                            gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-      else
-        k_walk_count<0, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                             gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-    } else if (wv == 0 && grp) {
-      // many chains: the walk is bound by its line traffic, and entry stores
-      // from the walking lanes -- half-line groups scattered among the random
-      // header reads -- cost far more than their bytes (C4: 1.60 ms against
-      // 1.00 without entries); a writer wave per workgroup drains each lane's
-      // LDS ring in whole 256-byte groups instead (C4 1.41 ms, its 2-way
-      // share 0.94 -> 0.87, C1-shaped 0.042 -> 0.038;
-      // profiles/r03_walk_writer_grp_ab.jsonl)
-      (plain ? k_walk_count<0, false, false, 0, false, 2, 2, 32> : k_walk_count<8, false, false, 0, false, 2, 2, 32>)
-          <<<nblk, 2 * kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb,
-                                             in_bytes, done, max_frames, payload_cap, d_summary, ~0ull, 1u, nullptr,
-                                             nullptr, nullptr, nullptr, nullptr);
-    } else if (grp && plain) {
-      k_walk_count<0, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                          gshift, cpb, in_bytes, done, max_frames, payload_cap,
-                                                          d_summary);
-    } else if (plain) {
-      k_walk_count<0, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                           gshift, cpb, in_bytes, done, max_frames, payload_cap,
-                                                           d_summary);
-    } else if (grp) {
-      k_walk_count<8, true><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                          gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-    } else {
-      k_walk_count<8, false><<<nblk, kCountBlock, 0, st>>>(d_in, d_conns, n_conns, d_conn_out, blk, entries, ne,
-                                                           gshift, cpb, in_bytes, done, max_frames,
-                                                            payload_cap, d_summary);
-    }
+    (plain ? k_walk_count<0, 0> : k_walk_count<8, 0>)<<<nblk, kCountBlock, 0, st>>>(
+        d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes, done, max_frames, payload_cap,
+        d_summary);
   }
   if (timed) GEVWS_HIP(hipEventRecord(ev[1], st));
   if (!fused) k_scan_blocks<true, kDecFields><<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
   if (timed) GEVWS_HIP(hipEventRecord(ev[2], st));
   if (nblk) {
-    k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb_w, ctx->d_stats,
-                                               budget ? rcount : nullptr);
+    k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb_w, ctx->d_stats);
     ctx->stats_pending = true;
     ctx->stats_conns = n_conns;
     // the record pass walks the segments when the walk was split
-    const gevws_conn_in* e_conns = rows > 1 ? segs : d_conns;
-    const gevws_conn_out* e_out = rows > 1 ? sout : d_conn_out;
-    const uint8_t* e_rec = rows > 1 ? srec : rec_flags;
-    const gevws_conn_out* e_parent = rows > 1 ? d_conn_out : nullptr;
-    const uint32_t e_ks = rows > 1 ? rows : 0;
+    const gevws_conn_in* e_conns = ks > 1 ? segs : d_conns;
+    const gevws_conn_out* e_out = ks > 1 ? sout : d_conn_out;
+    const uint8_t* e_rec = ks > 1 ? srec : rec_flags;
+    const gevws_conn_out* e_parent = ks > 1 ? d_conn_out : nullptr;
     uint64_t egrid = (n_v + kWalkBlock / 64 - 1) / (kWalkBlock / 64);
     // (split rows: each row is a chain of ~100 frames whose entries cost a
     // load round trip, so more waves share them out)
-    const uint64_t ecap = (ks > 1 ? kEmitSplitPerCU : 8) * (uint64_t)ctx->num_cus;
+    const uint64_t ecap = (ks > 1 ? kEmitSplitPerCU : 8) * (uint64_t)ncu;
     if (egrid > ecap) egrid = ecap;
-    if (ctx->emit_variant == 1)
-      k_walk_emit<4><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out, d_summary,
-                                                              d_frames, tile_first, entries, ne, gshift, e_rec,
-                                                              e_parent, e_ks);
-    else if (ctx->emit_variant == 2)
-      k_walk_emit<4, kEmitGroup, true><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(
-          d_in, e_conns, (uint32_t)n_v, e_out, d_summary, d_frames, tile_first, entries, ne, gshift, e_rec, e_parent,
-          e_ks);
-    else if (ctx->emit_variant == 3)
-      k_walk_emit<8, kEmitGroup><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out,
-                                                                          d_summary, d_frames, tile_first, entries,
-                                                                          ne, gshift, e_rec, e_parent, e_ks);
-    else
-      k_walk_emit<4, kEmitGroup><<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out,
-                                                                          d_summary, d_frames, tile_first, entries,
-                                                                          ne, gshift, e_rec, e_parent, e_ks);
+    k_walk_emit<<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out, d_summary, d_frames,
+                                                          tile_first, entries, ne, gshift, e_rec, e_parent,
+                                                          ks > 1 ? ks : 0);
   }
   // split streams: the unmask waits for the front (walk, scan, record pass)
   // on its own stream; the next batch's front can then run beside it
@@ -5445,7 +3749,7 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_out_off, gate);
   k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
   if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(n, blk, d_summary, d_out_off, tile_first, gate);
-  const uint64_t per_cu = (ctx->encode_variant == 0 || ctx->encode_variant >= 4) ? 7 : 4;  // LDS-light: 7 per CU
+  const uint64_t per_cu = 7;  // the window path's occupancy (k_encode)
   uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
   // (GEVWS_TUNE_UNMASK_GRID, when set, caps the encode's grid too: measurement)
   const uint64_t gcap = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : per_cu * (uint64_t)ctx->num_cus;
@@ -5453,26 +3757,13 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   if (grid < 1) grid = 1;
   // every frame boundary takes the window path, which needs several
   // workgroups per CU to hide its latency (C3: 22.6 ms at 4/CU vs 36 ms at
-  // 1/CU); the LDS-light default runs 7 per CU (C2 -18 %, C4 -4 % against
-  // 4, profiles/r01_encode_ab_lds_*.json, r01_encode_ab_occ_*.json) and 4 for
-  // batches of big frames
-  auto enc = ctx->encode_variant == 1   ? k_encode<4, false, false>
-             : ctx->encode_variant == 2 ? k_encode<4, true, false>
-             : ctx->encode_variant == 3 ? k_encode<4, true, true>
-             : ctx->encode_variant == 4 ? k_encode<4, true, true, true, 7, true>  // round-1 default
-             : ctx->encode_variant == 5 ? k_encode<4, true, true, true, 7, true, true>
-             : ctx->encode_variant == 6 ? k_encode<4, true, true, true, 7, true, true, false>
-             : ctx->encode_variant == 7 ? k_encode<4, true, true, true, 7, true, true, false, true>
-             : ctx->encode_variant == 8 ? k_encode<4, true, true, true, 7, true, true, true, true>
-             : ctx->encode_variant == 9 ? k_encode<4, true, true, true, 7, true, true, true, true, true, true>
-             : ctx->encode_variant == 10 ? k_encode<4, true, true, true, 7, true, true, true, true, true>
-             : ctx->encode_variant == 11 ? k_encode<4, true, true, true, 7, true, true, true, true, true, false, true, true>
-                                         : k_encode<4, true, true, true, 7, true, true, true, true, true, false, true>;
-  // LDS-light variant: batches of big frames (mean >= kBigFrameBytes) keep 4
-  // workgroups per CU (the rest return at once), the window path gets 7
-  const uint32_t big = per_cu > 4 && grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
-  enc<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
-                                                       big);
+  // 1/CU); it runs 7 per CU (C2 -18 %, C4 -4 % against 4,
+  // profiles/r01_encode_ab_lds_*.json, r01_encode_ab_occ_*.json), and
+  // batches of big frames (mean >= kBigFrameBytes) keep 4 per CU (the rest
+  // return at once)
+  const uint32_t big = grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
+  k_encode<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
+                                                     big);
   GEVWS_HIP(hipGetLastError());
   return mark_last(ctx, st);
 }
@@ -5570,34 +3861,14 @@ int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t
   if (n == 0) return GEVWS_OK;
   DeviceGuard g(ctx->device);
   hipStream_t st = pick_stream(ctx, stream);
-  // high bit: interleaved block mapping; next bit: plain loads; next: the
-  // unmask's wave-contiguous spans (measurement variants)
-  const bool inter = grid & 0x80000000u, plain = grid & 0x40000000u, wspan = grid & 0x20000000u;
+  // bit 30: plain loads (else non-temporal); bit 29: the unmask's
+  // wave-contiguous spans (else tile-strided lanes)
+  const bool plain = grid & 0x40000000u, wspan = grid & 0x20000000u;
   grid &= 0x1fffffffu;
   if (grid == 0) grid = (uint32_t)ctx->num_cus;
-  if (wspan)
-    (plain ? k_copy_stream<16, false, false, true> : k_copy_stream<16, false, true, true>)<<<grid, kUnmaskBlock, 0,
-                                                                                            st>>>(d_src, d_dst, n);
-  else if (inter)
-    (plain ? k_copy_stream<16, true, false> : k_copy_stream<16, true>)<<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst, n);
-  else
-    (plain ? k_copy_stream<16, false, false> : k_copy_stream<16, false>)<<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst,
-                                                                                                        n);
-  GEVWS_HIP(hipGetLastError());
-  return GEVWS_OK;
-}
-
-int gevws_gather_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64_t in_bytes, uint32_t lanes,
-                       uint32_t per_lane, int dependent, uint64_t seed, uint64_t* d_sink) {
-  if (!ctx || !d_in || !d_sink || in_bytes < 128 || lanes == 0 || (lanes % kCountBlock) || (per_lane % 8))
-    return GEVWS_ERR_INVALID;
-  DeviceGuard g(ctx->device);
-  hipStream_t st = pick_stream(ctx, stream);
-  // dependent: bit 0 = chain; bits 1-2 = load kind (gather_load)
-  using K = void (*)(const uint8_t*, uint64_t, uint32_t, uint64_t, uint64_t*);
-  static const K ks[8] = {k_gather<false, 0>, k_gather<true, 0>, k_gather<false, 1>, k_gather<true, 1>,
-                          k_gather<false, 2>, k_gather<true, 2>, k_gather<false, 3>, k_gather<true, 3>};
-  ks[dependent & 7]<<<lanes / kCountBlock, kCountBlock, 0, st>>>(d_in, in_bytes / 128, per_lane, seed, d_sink);
+  auto k = wspan ? (plain ? k_copy_stream<16, false, true> : k_copy_stream<16, true, true>)
+                 : (plain ? k_copy_stream<16, false, false> : k_copy_stream<16, true, false>);
+  k<<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst, n);
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;
 }

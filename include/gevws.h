@@ -152,71 +152,33 @@ int gevws_stream_destroy(void *stream);
 /* The number of CUs a stream may use (its CU mask's population; all of the
  * device's for an unmasked stream or NULL). */
 int gevws_stream_cu_count(int device, void *stream);
-/* Tuning knobs for measurement (defaults are the tuned choice):
- * GEVWS_TUNE_UNMASK_VARIANT selects an unmask kernel variant (0 = default),
+/* Tuning knobs for measurement and parity tests (defaults are the tuned
+ * choice): GEVWS_TUNE_UNMASK_VARIANT the unmask kernel (0 = default: v3 4-tile
+ * windows for batches of equal-size frames, v5 pipelined 8-tile windows with
+ * a chunk -> frame map for mixed sizes; 1 = v5 for every batch),
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto; when set it caps the
- * encode's grid too), GEVWS_TUNE_ENCODE_VARIANT
- * the encode kernel (0 = aligned non-temporal loads + register realign while streaming;
- * in frame windows all payload loads issued before the stores, and every
- * 64-byte group that holds a frame boundary queued whole and written by one
- * store instruction of the workgroup's assembly pass, a window's interior
- * stores issued after its first queued chunk's assembly; frame headers rebuilt
- * from the records so 7 workgroups fit per CU; 1 = unaligned loads, boundary
- * chunks assembled by the lane that meets them; 2 = aligned loads, per-lane
- * assembly; 3 = boundary chunks queued alone, serialised headers kept in
- * LDS, 4 workgroups per CU; 4 = boundary chunks queued alone, LDS-light (the
- * round-1 default); 5 = 4 with the loads before the stores; 6 = 5 with plain
- * (not non-temporal) window stores; 7 = 0 with plain window stores; 8 = 0 with
- * plain streaming loads -- the default's are non-temporal; 9 = 0 with
- * non-temporal window loads as well; 10 = 0 with a window's interior stores
- * issued before its queue pass instead of after its first queued chunk's
- * assembly -- the default until round 3),
- * GEVWS_TUNE_WALK_VARIANT the header walk (0 = with
- * uniform-stream speculation, 1 = plain chain walk, 2 = plain walk that
- * records no per-frame entries, so the emit pass re-walks every chain; 0 and
- * 1 store the per-frame entries in 64-byte groups when the batch has >= 128
- * connections per CU; 3 / 4 = speculation with single / grouped entry stores
- * whatever the batch; gevws_tuning_name lists them all, 0 being the per-batch
- * default), GEVWS_TUNE_SPAN_CONNS_PER_CU the batch size (connections per CU)
- * up to which the default walk takes one wave per connection (0 = never, the
- * default: k_walk_span is issue-bound), GEVWS_TUNE_EMIT_VARIANT
- * the record pass (0 = groups of 16 connections with few frames enumerated
- * across connection boundaries, 1 = one wave per connection, 2 = 0 with
- * non-temporal entry loads and record stores, 3 = 0 with 8 rounds of 64
- * entries per load instead of 4),
- * GEVWS_TUNE_SMALL_BATCH the input size in bytes (default and maximum 65 536;
- * 0 = never) up to which a batch of at most 256 connections is decoded by ONE
- * kernel launch -- walk, scan, records and unmask in a single workgroup --
- * when every other knob is at its default and per-phase timing is off,
- * GEVWS_TUNE_SPLIT_LANES the lanes per connection of the default walk's split
- * form (k_walk_split: lanes guess frame starts inside the stream and walk
- * the segments between the guesses; a connection whose guesses do not all
- * line up is re-walked serially, so the output never depends on them): 0 =
- * auto (the batch's connections x lanes up to 256 per CU, streams of >= 32 KiB
- * mean), 1 = never, 2 / 4 / 8 / 16 / 32 = always. */
+ * encode's grid too), GEVWS_TUNE_ENCODE_VARIANT the encode kernel (0 = the
+ * default; the only one at present), GEVWS_TUNE_WALK_VARIANT the header walk (0 = the
+ * default choice per batch; 1 = plain chain walk without the uniform-stream
+ * speculation; 2 = no per-frame entries, the record pass re-walks every
+ * chain; 3 = the entries through the writer wave whatever the batch size),
+ * GEVWS_TUNE_SMALL_BATCH the input size in bytes (default and maximum
+ * 65 536; 0 = never) up to which a batch of at most 256 connections is
+ * decoded by ONE kernel launch -- walk, scan, records and unmask in a single
+ * workgroup -- when every other knob is at its default and per-phase timing
+ * is off, GEVWS_TUNE_SPLIT_LANES the lanes per connection of the default
+ * walk's split form (k_walk_split: lanes guess frame starts inside the stream
+ * and walk the segments between the guesses; a connection whose guesses do
+ * not all line up is re-walked serially, so the output never depends on
+ * them): 0 = auto (the batch's connections x lanes up to 256 per CU, streams
+ * of >= 32 KiB mean), 1 = never, 2 / 4 / 8 / 16 / 32 = always.  Keys 5, 6,
+ * 9-12 (round 1-3 measurement variants) are retired and rejected. */
 #define GEVWS_TUNE_UNMASK_VARIANT 1
 #define GEVWS_TUNE_UNMASK_GRID 2
 #define GEVWS_TUNE_ENCODE_VARIANT 3
 #define GEVWS_TUNE_WALK_VARIANT 4
-#define GEVWS_TUNE_SPAN_CONNS_PER_CU 5
-#define GEVWS_TUNE_EMIT_VARIANT 6
 #define GEVWS_TUNE_SMALL_BATCH 7
 #define GEVWS_TUNE_SPLIT_LANES 8
-#define GEVWS_TUNE_SPLIT_MODE 9  /* measurement: 1 = split guesses made then dropped, 2 = none made, \
-                                    3 = keep the walk's speculation after a mixed-size batch */
-/* Budgeted header walk (a batch of many long chains of small frames): every
- * lane walks its connection for at most this many frames, then the
- * connections not finished are walked on from where they stopped with
- * GEVWS_TUNE_RESUME_LANES lanes each (k_walk_split's guesses, checked by the
- * chain itself, over the rest of the stream).  0 = auto (after a decode on
- * this context whose connections averaged >= 256 frames of <= 4 KiB, when the
- * split walk is not chosen: GEVWS_TUNE_BUDGET_FRAC 16ths of that mean), -1 =
- * never (the default: measured slower than the plain walk),
- * > 0 = this budget for every multi-kernel decode (instead of the split walk's
- * auto choice; GEVWS_TUNE_SPLIT_LANES >= 2 still splits). */
-#define GEVWS_TUNE_WALK_BUDGET 10
-#define GEVWS_TUNE_RESUME_LANES 11  /* 0 = default (8), else 2 / 4 / 8 / 16 */
-#define GEVWS_TUNE_BUDGET_FRAC 12   /* auto budget in 16ths of the previous mean chain (default 18) */
 /* Split walk (GEVWS_TUNE_SPLIT_LANES): a connection is cut into segments of at
  * least this many bytes (default 16 384; 1 024 .. 2^30) ... */
 #define GEVWS_TUNE_SPLIT_MIN_BYTES 13
@@ -241,25 +203,11 @@ int gevws_ctx_last_split_lanes(const gevws_ctx *ctx);
  * synchronises the stream as usual). */
 int gevws_ctx_set_completion_flag(gevws_ctx *ctx, uint32_t *d_flag);
 int64_t gevws_ctx_completion_seq(const gevws_ctx *ctx);
-/* Frames per lane of the last multi-kernel decode's budgeted walk (0 = not
- * budgeted; -1 for a null context), and the connections it resumed (waits for
- * the context's last call; < 0 on error). */
-int64_t gevws_ctx_last_walk_budget(const gevws_ctx *ctx);
-int64_t gevws_ctx_last_resumed(gevws_ctx *ctx);
 /* Workgroups of the last multi-kernel decode's unmask launch (-1 for a null
  * context): 4 per CU, or 32 per CU after a decode on this context of a batch
  * of mixed frame sizes below 8 GiB of output (the kernel then uses the wide
  * grid if this batch is one too). */
 int gevws_ctx_last_unmask_grid(const gevws_ctx *ctx);
-/* Measurement: the phase cycle counts the profiled unmask variants
- * (GEVWS_TUNE_UNMASK_VARIANT 14 -- v4 -- and 18 -- v5, the default) accumulated on ctx's device since the last
- * reset -- 0 kernel, 1 streaming steps, 2 window first barrier, 3 window fill,
- * 4 second barrier, 5 search + payload load issue, 6 next-step decision, 7
- * payload wait + XOR + stores, 8 windows, 9 windows of > 256 frames, 10 frames
- * over the windows, 11 streaming steps, 12 workgroups, 13 per-lane fallback
- * tiles (cycles summed over workgroups, thread 0's view) -- then zeroes them
- * when reset != 0.  Waits for the device. */
-int gevws_unmask_profile(gevws_ctx *ctx, uint64_t out[16], int reset);
 /* Human-readable name of a variant (GEVWS_TUNE_UNMASK_VARIANT or
  * GEVWS_TUNE_WALK_VARIANT), or NULL past the last one. */
 const char *gevws_tuning_name(int key, int64_t value);
@@ -376,24 +324,12 @@ int gevws_handle_decoded_async(gevws_ctx *ctx, void *stream, const gevws_frame *
  * 16-byte aligned, d_src any alignment) copied with the unmask kernel's
  * streaming access pattern minus the XOR and frame lookup -- the achievable
  * HBM rate bench.py reports beside the spec peak.  grid 0 = one workgroup per
- * CU (the unmask kernel's grid for large frames); grid | 0x80000000 deals
- * 64 KiB blocks round-robin over the workgroups instead of contiguous runs;
- * grid | 0x40000000 uses plain loads instead of the non-temporal ones the
+ * CU (the unmask kernel's grid for large frames), each a contiguous run of
+ * tiles; grid | 0x40000000 uses plain loads instead of the non-temporal ones the
  * unmask kernel's streaming path uses; grid | 0x20000000 copies in the
  * unmask's wave layout (each wave a contiguous 16 KiB span per step). */
 int gevws_copy_async(gevws_ctx *ctx, void *stream, uint8_t *d_dst, const uint8_t *d_src, uint64_t n,
                      uint32_t grid);
-
-/* Measurement helper, not on the reference path: the header walk's access
- * pattern without its parsing -- `lanes` lanes (a multiple of 64), each
- * fetching `per_lane` (a multiple of 8) 16-byte windows at random 128-byte
- * lines of d_in[0, in_bytes); `dependent` != 0 makes each address depend on
- * the previous load's data (one load in flight per lane, as in the walk),
- * else 8 independent loads are in flight per lane.  One u64 per lane is
- * written to d_sink.  bench / tools use it as the walk's random-line fetch
- * ceiling. */
-int gevws_gather_async(gevws_ctx *ctx, void *stream, const uint8_t *d_in, uint64_t in_bytes, uint32_t lanes,
-                       uint32_t per_lane, int dependent, uint64_t seed, uint64_t *d_sink);
 
 /* Host-ingress helper, not on the reference path: `bytes` of page-locked host
  * memory mapped into the device address space (hipHostMallocMapped).

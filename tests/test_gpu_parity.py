@@ -668,28 +668,22 @@ def test_walk_variants_uniform_runs(engine):
     arena, conns = pack_streams([random_stream(rng, int(rng.integers(1, 40))) for _ in range(90)])
     cases.append((arena, conns[rng.permutation(conns.shape[0])]))
     walks = engine.variants(_abi.TUNE_WALK_VARIANT)
-    assert len(walks) >= 8
+    assert walks == [0, 1, 2, 3]
     try:
         for v in walks:
             engine.set_tuning(_abi.TUNE_WALK_VARIANT, v)
             for k, (arena, conns) in enumerate(cases):
                 assert_matches_oracle(engine, arena, conns, f"walk variant {v} case {k}")
-        # the default's choice of walk by batch size, both sides of the threshold
-        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 0)
-        for per_cu in (0, 1 << 20):
-            engine.set_tuning(_abi.TUNE_SPAN_CONNS_PER_CU, per_cu)  # never / always
-            for k, (arena, conns) in enumerate(cases):
-                assert_matches_oracle(engine, arena, conns, f"span threshold {per_cu} case {k}")
     finally:
         engine.set_tuning(_abi.TUNE_WALK_VARIANT, 0)
-        engine.set_tuning(_abi.TUNE_SPAN_CONNS_PER_CU, 0)
 
 
-def test_emit_variants(engine):
-    """Every record pass (grouped: frames of up to 16 short connections
-    enumerated across connection boundaries; per connection; grouped with
-    non-temporal entry loads / record stores) bit-exact on batches of short,
-    long, empty, unrecorded and mixed connections."""
+def test_record_pass_groups(engine):
+    """The record pass (frames of up to 16 short connections enumerated across
+    connection boundaries, long connections one wave each, unrecorded ones
+    re-walked) bit-exact on batches of short, long, empty, unrecorded and mixed
+    connections, from entries stored by the walking lanes and by the writer
+    wave, and with no entries at all."""
     from gev_amd import _abi
     rng = np.random.default_rng(9191)
     cases = []
@@ -712,12 +706,12 @@ def test_emit_variants(engine):
         cases.append(pack_streams([b"".join(wo.encode_frame(bytes(20), 2, True, 0, True, b"\1\2\3\4")
                                             for _ in range(nfr)) for _ in range(40)]))
     try:
-        for v in (0, 1, 2, 3):
-            engine.set_tuning(_abi.TUNE_EMIT_VARIANT, v)
+        for v in (0, 3, 2):
+            engine.set_tuning(_abi.TUNE_WALK_VARIANT, v)
             for k, (arena, conns) in enumerate(cases):
-                assert_matches_oracle(engine, arena, conns, f"emit variant {v} case {k}")
+                assert_matches_oracle(engine, arena, conns, f"walk variant {v} case {k}")
     finally:
-        engine.set_tuning(_abi.TUNE_EMIT_VARIANT, 0)
+        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 0)
 
 
 def test_escaped_entry_lengths(engine):
@@ -727,8 +721,8 @@ def test_escaped_entry_lengths(engine):
     3 MiB, alone, back to back (several escapes in one round of 64 entries),
     first and last on their connection, among small frames, on short
     connections (the grouped pass) and long ones (per connection), through
-    every record pass, the plain and writer walks, the split walk and the
-    budgeted walk's resumption -- bit-exact against the C oracle."""
+    the plain and writer walks and the split walk -- bit-exact against the C
+    oracle."""
     from gev_amd import _abi
     rng = np.random.default_rng(0xE5C)
     esc = (1 << 21) - 1
@@ -753,12 +747,9 @@ def test_escaped_entry_lengths(engine):
     streams += [small(int(rng.integers(0, 20))) + fr(bigs[i % 4]) + small(int(rng.integers(0, 90)))
                 for i in range(6)]
     arena, conns = pack_streams(streams)
-    knobs = [(_abi.TUNE_EMIT_VARIANT, v) for v in (0, 1, 2, 3)]
-    knobs += [(_abi.TUNE_WALK_VARIANT, v) for v in (1, 3, 4, 15, 16, 17, 18)]
+    knobs = [(_abi.TUNE_WALK_VARIANT, v) for v in (1, 2, 3)]
     knobs += [(_abi.TUNE_SPLIT_LANES, k) for k in (2, 4, 16)]
-    knobs += [(_abi.TUNE_WALK_BUDGET, b) for b in (1, 3, 17)]
-    defaults = {_abi.TUNE_EMIT_VARIANT: 0, _abi.TUNE_WALK_VARIANT: 0, _abi.TUNE_SPLIT_LANES: 0,
-                _abi.TUNE_WALK_BUDGET: -1}
+    defaults = {_abi.TUNE_WALK_VARIANT: 0, _abi.TUNE_SPLIT_LANES: 0}
     try:
         assert_matches_oracle(engine, arena, conns, "default")
         for knob, val in knobs:
@@ -811,3 +802,8 @@ def test_walk_variant_knob_bounds(engine):
         engine.set_tuning(_abi.TUNE_WALK_VARIANT, len(engine.variants(_abi.TUNE_WALK_VARIANT)))
     with pytest.raises(ValueError):
         engine.set_tuning(_abi.TUNE_WALK_VARIANT, -1)
+    with pytest.raises(ValueError):
+        engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, len(engine.variants(_abi.TUNE_UNMASK_VARIANT)))
+    for key in _abi.TUNE_RETIRED:  # round 1-3 measurement knobs are gone
+        with pytest.raises(ValueError):
+            engine.set_tuning(key, 0)

@@ -149,8 +149,7 @@ def test_split_lanes_knob_bounds(engine):
         with pytest.raises(ValueError):
             engine.set_tuning(_abi.TUNE_SPLIT_LANES, bad)
     engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
-    for knob, bad in ((_abi.TUNE_SPLIT_MIN_BYTES, 1023), (_abi.TUNE_SPLIT_LANES_PER_CU, 63),
-                      (_abi.TUNE_RESUME_LANES, 32)):
+    for knob, bad in ((_abi.TUNE_SPLIT_MIN_BYTES, 1023), (_abi.TUNE_SPLIT_LANES_PER_CU, 63)):
         with pytest.raises(ValueError):
             engine.set_tuning(knob, bad)
 
@@ -193,7 +192,7 @@ def test_wide_unmask_grid_after_mixed_batch(engine):
     import torch
     from gev_amd import workloads as w
     from tests.test_gpu_parity import _synth_decode_verify
-    mixed = w.config_c4(total_payload=512 << 20, n_conns=1024, seed=5)       # 131 K output tiles, v4
+    mixed = w.config_c4(total_payload=512 << 20, n_conns=1024, seed=5)       # 131 K output tiles, v5
     uniform = w.uniform(1024, 128, 4096, seed=6)                             # 512 MiB of 4 KiB frames, v3
     ncu = torch.cuda.get_device_properties(engine.device).multi_processor_count
     _synth_decode_verify(engine, uniform, check_slice_conns=4)
@@ -205,100 +204,3 @@ def test_wide_unmask_grid_after_mixed_batch(engine):
     assert engine.last_unmask_grid > 4 * ncu
     _synth_decode_verify(engine, uniform, check_slice_conns=4)
     assert engine.last_unmask_grid <= 4 * ncu
-
-
-# ---------------------------------------------------------------- budgeted walk
-# k_walk_count BUD + k_walk_resume (GEVWS_TUNE_WALK_BUDGET / _RESUME_LANES):
-# every lane stops after `budget` frames and the unfinished connections are
-# walked on from the saved position, KS lanes each with guesses over the rest
-# of the stream.  Forced small budgets (1, 3, 17) put nearly every connection
-# through the resume path, at every point of its chain: the same cases, the
-# same bar -- the oracle's records, bytes, per-connection results and summary.
-@pytest.mark.parametrize("budget,lanes", [(1, 2), (1, 16), (3, 8), (17, 4), (17, 16), (200, 8), (5000, 8)])
-def test_budgeted_walk_matches_oracle(engine, split_cases, budget, lanes):
-    from gev_amd import _abi
-    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 0)
-    engine.set_tuning(_abi.TUNE_WALK_BUDGET, budget)
-    engine.set_tuning(_abi.TUNE_RESUME_LANES, lanes)
-    try:
-        for name, (arena, conns) in split_cases.items():
-            assert_matches_oracle(engine, arena, conns, f"budget {budget} lanes {lanes}: {name}")
-            assert engine.last_walk_budget == budget
-            nf = ref.decode_batch(np.frombuffer(arena, np.uint8).copy(), conns[:, 0], conns[:, 1])["conn_nframes"]
-            # a connection is resumed when the budget stopped it (>= budget frames seen)
-            assert engine.last_resumed >= int((nf > budget).sum()), name
-    finally:
-        engine.set_tuning(_abi.TUNE_WALK_BUDGET, -1)
-        engine.set_tuning(_abi.TUNE_RESUME_LANES, 0)
-        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
-
-
-def test_budgeted_walk_streams_outside_the_arena_and_random(engine):
-    """Out-of-arena rows and random mixed streams (every header form, RSV,
-    reserved opcodes, partial tails) through the budgeted walk."""
-    import gev_amd
-    from gev_amd import _abi
-    from tests._helpers import random_stream
-    rng = np.random.default_rng(0xB0D6)
-    arena, conns = pack_streams([random_stream(rng, int(rng.integers(0, 120))) for _ in range(300)])
-    n = len(arena)
-    bad = np.array([[n - 4, 10], [n + 100, 70_000]], np.int64)
-    table = np.concatenate([conns[:3], bad[:1], conns[3:50], bad[1:], conns[50:]])
-    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 0)
-    try:
-        for budget, lanes in ((1, 4), (7, 16), (30, 2)):
-            engine.set_tuning(_abi.TUNE_WALK_BUDGET, budget)
-            engine.set_tuning(_abi.TUNE_RESUME_LANES, lanes)
-            assert_matches_oracle(engine, arena, conns, f"random, budget {budget}")
-            got = host_result(gpu_decode(engine, arena, table))
-            st = got["conn_out"]["status"]
-            assert list(st[[3, 51]]) == [gev_amd.ERR_INVALID] * 2
-            want = ref.decode_batch(np.frombuffer(arena, np.uint8).copy(), conns[:, 0], conns[:, 1])
-            assert got["frames"].tobytes() == want["frames"].tobytes()
-            assert np.array_equal(got["payload"], want["payload"])
-    finally:
-        engine.set_tuning(_abi.TUNE_WALK_BUDGET, -1)
-        engine.set_tuning(_abi.TUNE_RESUME_LANES, 0)
-        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
-
-
-def test_budget_knob_bounds(engine):
-    from gev_amd import _abi
-    for key, bad in ((_abi.TUNE_WALK_BUDGET, -2), (_abi.TUNE_RESUME_LANES, 1), (_abi.TUNE_RESUME_LANES, 3),
-                     (_abi.TUNE_RESUME_LANES, 32), (_abi.TUNE_BUDGET_FRAC, 0)):
-        with pytest.raises(ValueError):
-            engine.set_tuning(key, bad)
-    engine.set_tuning(_abi.TUNE_WALK_BUDGET, -1)
-    engine.set_tuning(_abi.TUNE_RESUME_LANES, 0)
-
-
-def test_budgeted_walk_auto_choice(engine):
-    """Auto: a batch of more connections than the split walk takes (> 32 per
-    CU) whose previous decode on the context showed long chains of small
-    frames is walked with a budget of 18/16 of that mean chain; its unfinished
-    connections are resumed -- exact by the generator property on every byte
-    and the oracle on the leading connections; never budgeted after big
-    frames or on a context's first batch."""
-    import torch
-    from gev_amd import _abi
-    from gev_amd import workloads as w
-    from tests.test_gpu_parity import _synth_decode_verify
-    ncu = torch.cuda.get_device_properties(engine.device).multi_processor_count
-    engine.set_tuning(_abi.TUNE_WALK_BUDGET, 0)  # auto (the default is off)
-    n = 33 * ncu
-    mixed = w.config_c4(total_payload=n * 160_000, n_conns=n, alpha=1.1, lo=64, hi=4096, seed=11)
-    big = w.uniform(n, 8, 64 << 10, seed=12)
-    _synth_decode_verify(engine, big, check_slice_conns=2)
-    _synth_decode_verify(engine, mixed, check_slice_conns=4)
-    assert engine.last_walk_budget == 0
-    _synth_decode_verify(engine, mixed, check_slice_conns=4)
-    mean = mixed.n_frames // n
-    assert engine.last_walk_budget == mean * 18 // 16, (engine.last_walk_budget, mean)
-    assert engine.last_resumed > 0
-    _synth_decode_verify(engine, big, check_slice_conns=2)
-    engine.set_tuning(_abi.TUNE_WALK_BUDGET, -1)
-    try:
-        _synth_decode_verify(engine, mixed, check_slice_conns=2)
-        assert engine.last_walk_budget == 0
-    finally:
-        engine.set_tuning(_abi.TUNE_WALK_BUDGET, -1)

@@ -5,14 +5,14 @@ the order every round).  Every configuration is verified bit-exact on every
 workload first (decode(mask(P)) == P on every byte, frame / payload counts).
 
     python tools/ab_decode.py --workloads c4,c4@0/2,c4@0/4,c4@0/8 \
-        --configs 'off:WALK_BUDGET=-1;auto:WALK_BUDGET=0;b16:BUDGET_FRAC=16' --rounds 4 --reps 3
+        --configs 'auto:SPLIT_LANES=0;off:SPLIT_LANES=1;v5:UNMASK_VARIANT=1' --rounds 4 --reps 3
 
 A workload is a bench.py config name, optionally `@R/N` for rank R's LPT share
 of an N-way strong split.  A configuration is `name:KEY=VAL,KEY=VAL` with KEY
 a gev_amd._abi TUNE_* suffix; keys a configuration does not name are at their
 defaults.  Prints one JSON object: per workload x configuration the median
-per-phase HIP-event times (walk, scan, emit, unmask, step) and the walk's
-budget / resumed connections.
+per-phase HIP-event times (walk, scan, emit, unmask, step), the walk's split
+lanes and the unmask grid.
 """
 from __future__ import annotations
 
@@ -25,9 +25,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULTS = {"WALK_BUDGET": -1, "RESUME_LANES": 0, "BUDGET_FRAC": 18, "SPLIT_LANES": 0, "WALK_VARIANT": 0,
-            "SPLIT_MIN_BYTES": 16384, "SPLIT_LANES_PER_CU": 512,
-            "UNMASK_VARIANT": 0, "UNMASK_GRID": 0, "EMIT_VARIANT": 0, "SPLIT_MODE": 0}
+DEFAULTS = {"SPLIT_LANES": 0, "WALK_VARIANT": 0, "SPLIT_MIN_BYTES": 16384, "SPLIT_LANES_PER_CU": 512,
+            "UNMASK_VARIANT": 0, "UNMASK_GRID": 0}
 
 
 def parse_configs(spec: str):
@@ -122,8 +121,7 @@ def main():
                 eng.set_timing(False)
                 ms, calls = eng.timing()
                 res[cname].append([x / calls for x in ms])
-                info[cname] = {"split_lanes": eng.last_split_lanes, "budget": eng.last_walk_budget,
-                               "resumed": eng.last_resumed, "unmask_grid": eng.last_unmask_grid}
+                info[cname] = {"split_lanes": eng.last_split_lanes, "unmask_grid": eng.last_unmask_grid}
             print(f"[ab] {wspec}: round {r} done", file=sys.stderr, flush=True)
         wrep = {"workload": wspec, "name": lay.name, "n_conns": lay.n_conns, "n_frames": lay.n_frames,
                 "configs": []}
