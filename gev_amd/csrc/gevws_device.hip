@@ -323,7 +323,7 @@ constexpr uint64_t kSlotAlign = 1ull << kSlotShift;
 // pass, where the prefix sum gives its position (rare: frames of 2 MiB and
 // more, whose unmask dwarfs one header load).  Round 2's 16-byte entry
 // (position, key, length, meta) cost the walk 0.71 GB of C4's writes and the
-// record pass as many reads (profiles/r03_pmc_split.json).
+// record pass as many reads (profiles/r03/r03_pmc_split.json).
 constexpr uint32_t kLenEsc = (1u << 21) - 1;
 struct WalkEntry {
   uint32_t mask;
@@ -389,7 +389,7 @@ __device__ __forceinline__ int walk_parse(uint64_t lo, uint64_t hi, uint64_t ava
 // position, so the result never depends on the guess.  Requiring three equal
 // frames keeps the batch path (and the wave divergence it costs) out of
 // mixed-size traffic.  Interleaved A/B against D = 0
-// (profiles/r01_ab_walk2_*.json): the walk of fixed-size traffic takes 23-28 %
+// (profiles/r01/r01_ab_walk2_*.json): the walk of fixed-size traffic takes 23-28 %
 // less time (C2, C3), mixed traffic 0-5 % more (C4, C5: a longer loop body on
 // a latency-bound chain), so the host runs D = 0 after a mixed batch.
 // The chain walk of one stream (k_walk_count's loop; also each segment of
@@ -419,7 +419,7 @@ __device__ __forceinline__ WalkRes walk_res_fresh(uint64_t err = 0, int32_t st =
 // chains, whose walk is bound by line traffic: single entry stores scattered
 // among the random header reads cost far more than their bytes (C4: 1.60 ms
 // against 1.00 without entries, 1.26 through the writer;
-// profiles/r03_walk_writer_grp_ab.jsonl, r03_compact_entries_ab.jsonl).
+// profiles/r03/r03_walk_writer_grp_ab.jsonl, r03_compact_entries_ab.jsonl).
 constexpr uint32_t kRingDone = 0x80000000u;   // head flag: the chain is finished
 constexpr uint32_t kWriterGroup = 32;         // entries per writer store group (256 bytes)
 constexpr uint32_t kRing = 2 * kWriterGroup;  // entries per lane's LDS ring
@@ -567,7 +567,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
     // copy that waits for the load and, vmcnt being in order, for every entry
     // store after it: each step then paid the load AND the stores' latency
     // instead of overlapping them with the checks; C4 walk 1.61 -> 1.59 ms,
-    // profiles/r03_walk_unr_ab.jsonl.)
+    // profiles/r03/r03_walk_unr_ab.jsonl.)
     uint64_t lo2 = 0, hi2 = 0;
     for (;;) {
       if (!step(lo, hi, lo2, hi2)) break;
@@ -596,7 +596,7 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
 // ecap only.  Whole groups: a 64-byte group is half an L2 line, and scattered
 // half-line writes among the walk's random line reads cost far more than their
 // bytes (256-byte groups 1.262 ms on C4, 128-byte 1.284, 64-byte 1.345;
-// profiles/r03_compact_entries_ab.jsonl).
+// profiles/r03/r03_compact_entries_ab.jsonl).
 __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries, WalkRing ring, uint64_t ebase,
                                                  uint64_t ecap) {
   static_assert(kWriterGroup <= kSlotAlign, "groups aligned by the slot runs");
@@ -1149,7 +1149,7 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
   // the 32-byte record as two 16-byte stores: {fin, rsv, opcode, masked,
   // mask[4], length} and {payload_off, src_off} (gevws_frame's layout)
   // (C4's emit 0.64 -> 0.55 ms against the field-by-field struct store, which
-  // compiled to three stores of 8 + 16 + 8 bytes; profiles/r01_ab_emit_store_*.json)
+  // compiled to three stores of 8 + 16 + 8 bytes; profiles/r01/r01_ab_emit_store_*.json)
   const uint32_t flags = (h.b0 >> 7) | (((h.b0 & 0x70) >> 4) << 8) | ((h.b0 & 0x0f) << 16) | ((h.masked & 1) << 24);
   u32x4* r = reinterpret_cast<u32x4*>(frames + f);
   const u32x4 r0 = u32x4{flags, h.mask, (uint32_t)h.length, (uint32_t)(h.length >> 32)};
@@ -1171,7 +1171,7 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
 // lane j -- so connections of a few frames (C1: 16 frames of 136 B) fill whole
 // waves instead of 16 lanes of one, and all R rounds' entries are requested at
 // once (C4 0.53 -> 0.49 ms against one wave per connection,
-// profiles/r02_emit_ab.jsonl).  Phase 2: longer connections one wave each, 64
+// profiles/r02/r02_emit_ab.jsonl).  Phase 2: longer connections one wave each, 64
 // entries per round, U rounds' entries requested at once (a connection of N
 // frames costs ceil(N / 64U) entry-load latencies), wave prefix sum of the
 // padded lengths -> payload offsets, 64 contiguous 32-byte records per store.
@@ -1383,7 +1383,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
     // load) when the batch has more connections than the grid has waves
     // (half the grid's waves busy: C4's 65 536 connections 0.43 ms in groups of
     // 16 vs 0.53 ms in groups of 8 over every wave -- fewer record streams
-    // interleave in DRAM; profiles/r02_emit_ab.jsonl)
+    // interleave in DRAM; profiles/r02/r02_emit_ab.jsonl)
     const uint64_t per = (2 * (uint64_t)n + nwaves - 1) / nwaves;
     const uint64_t GL = per < 1 ? 1 : (per > 16 ? 16 : per);
     const uint64_t nl = ((uint64_t)n + GL - 1) / GL;
@@ -1402,7 +1402,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
       }
       // the group's connections with long chains (a ballot: groups of only
       // short or empty connections -- all of C1's -- cost one instruction;
-      // C1's record pass 0.030 -> 0.025 ms, profiles/r03_emit_pf_ab.jsonl)
+      // C1's record pass 0.030 -> 0.025 ms, profiles/r03/r03_emit_pf_ab.jsonl)
       for (uint64_t m = __ballot(lane < GL && nf > 0); m; m &= m - 1) {  // wave-uniform
         const int j = __builtin_ctzll(m);
         const uint64_t cnt = uniform64(__shfl(nf, j, 64));
@@ -1435,7 +1435,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
 // ------------------------------------------------------------------ 3c. small batches, one launch
 // A live server's pass is small (C1: ~100 connections x 136 B per loop
 // iteration) and pays per launch, not per byte: four kernels cost ~5 us each
-// of GPU time whatever their size (profiles/r02_loopback_*), plus their host
+// of GPU time whatever their size (profiles/r02/r02_loopback_*), plus their host
 // launch costs.  Batches of at most kSmallConns connections and
 // GEVWS_TUNE_SMALL_BATCH bytes (default kSmallBytes) run the whole decode in
 // ONE workgroup: each lane walks its connection (k_walk_count's rules), a
@@ -1591,7 +1591,7 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
 // ------------------------------------------------------------------ 4. unmask / compact
 // Streams of big frames run fastest with one workgroup per CU (fewer
 // concurrent streams: better DRAM row locality); small frames need more
-// workgroups to hide the window path's latency (profiles/r01_grid_*.json).  The
+// workgroups to hide the window path's latency (profiles/r01/r01_grid_*.json).  The
 // batch's mean frame size is only known on the device, so kernels are launched
 // with 4 workgroups per CU and, for big frames, all but the first `big_grid`
 // return at once.  big_grid = 0 disables the adaptation (explicit grid).
@@ -1603,7 +1603,7 @@ constexpr uint64_t kBigFrameBytes = 48 * 1024;
 // frame density) and more, shorter runs balance -- C4's 8-way share (590 K
 // tiles) 1.15 -> 0.99 ms, its 4-way share (1.2 M) 2.15 -> 2.09; the 2-way
 // share (2.4 M), the full C4 (4.7 M tiles), C2, C3, C5 are best at 4 per CU
-// (profiles/r02_grid_sweep.jsonl)
+// (profiles/r02/r02_grid_sweep.jsonl)
 constexpr uint32_t kWideGridPerCU = 32;
 constexpr uint64_t kWideGridTiles = 2ull << 20;
 
@@ -1814,7 +1814,7 @@ struct WinLds {
 // its 4 chunks, whose loads are unaligned non-temporal 16-byte loads.  The
 // scheme of batches of equal-size frames (C1, C2, C3, C5: -5 % on C1-shaped
 // and -2.4 % on C2 batches against v4's 8-tile windows, equal on C3;
-// profiles/r02_ab2.log).
+// profiles/r02/r02_ab2.log).
 template <int U>
 __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
@@ -1921,7 +1921,7 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
 // (its tile-map entries -- first frame a, last frame b and the frame at tile
 // +U, which equals a iff one frame covers the next U tiles -- and, for a
 // window, its first 256 records into registers, one per lane).  Profiled
-// (round 3, cycle counters; profiles/r03_unmask_profile*.jsonl) an 8-tile
+// (round 3, cycle counters; profiles/r03/r03_unmask_profile*.jsonl) an 8-tile
 // window of round 2's v4 spent a quarter of its ~37 K cycles in the per-chunk
 // searches and a third in the next-step decision.  v5:
 //  * chunk -> frame by a map instead of a search: every non-empty frame marks
@@ -1934,7 +1934,7 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
 //    window k+1 fills.
 //  * the tile map through an LDS cache of kTmapN entries (refilled by the
 //    whole workgroup every ~60 windows): a decision is LDS reads, not global.
-// C4 7.75 -> 7.40 ms against v4 (profiles/r03_unmask_v5*_ab.jsonl).
+// C4 7.75 -> 7.40 ms against v4 (profiles/r03/r03_unmask_v5*_ab.jsonl).
 // amdgpu_waves_per_eu(4): four workgroups per CU (128 VGPRs); 5 or 6 measured
 // slower (r03_unmask_occ_ab.jsonl).  Every lane id is re-derived where it is
 // used (fresh_tid): held across the loop, the fill's per-lane LDS / record
@@ -2283,7 +2283,7 @@ constexpr int kEncSlabs = 16;
 // Tile-map entries a lane writes itself in k_enc_emit (unrolled, predicated);
 // a frame with more has the rest written by its whole wave.  16 as a plain
 // loop: C5 emit 79 -> 16 us but C4 138 -> 466 us
-// (profiles/r03_encode_emit_lane16_*), so 4.
+// (profiles/r03/r03_encode_emit_lane16_*), so 4.
 constexpr int kEncLaneTiles = 4;
 // The frame count of a chained pass (decode -> dispatch -> encode with no host
 // round trip): the producing step's summary gates the consumer -- its frames,
@@ -2432,7 +2432,7 @@ struct EncWin {
 // payload bytes from ONE unaligned 16-byte load per frame.  The first two
 // frames' loads are issued together (most boundary chunks hold the end of one
 // payload and the header + start of the next: C2 -2.6 %, C5 -1.6 % against one
-// at a time, profiles/r01_encode_ab_asm2_*.json); further frames (frames of a
+// at a time, profiles/r01/r01_encode_ab_asm2_*.json); further frames (frames of a
 // few bytes) continue one by one.
 template <bool LH>
 __device__ __forceinline__ void enc_assemble_from(u128& acc, int32_t rel, uint64_t a, int kmax, uint32_t j, uint32_t F,
@@ -2539,15 +2539,15 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
 //    interior chunks with it, four consecutive slots), so one store writes the
 //    group's 64 bytes: otherwise every frame boundary left its line to HBM as
 //    two partial writes (C4: 46 M 32-byte write requests per launch, 0 with
-//    it; the whole C4 encode 10.70 -> 9.11 ms, profiles/r02_encode_ab_g64_*.json).
+//    it; the whole C4 encode 10.70 -> 9.11 ms, profiles/r02/r02_encode_ab_g64_*.json).
 //    All the window's payload loads are issued before its stores, and the
 //    interior chunks are stored only after the queue barrier and the lane's
 //    first queued chunk has been assembled, so the interior loads and the first
 //    assembly's loads are in flight together (C4 9.39 -> 9.17 ms,
-//    profiles/r03_encode_eo_ab.jsonl).
+//    profiles/r03/r03_encode_eo_ab.jsonl).
 // The window path is latency-bound: the kernel is held to 72 VGPRs for 7
 // workgroups per CU (amdgpu_waves_per_eu(7): C2 -4 %, C4 -2 % against 6 per
-// CU; 8 per CU at 64 VGPRs was slower on C5, profiles/r01_encode_ab_occ_*.json).
+// CU; 8 per CU at 64 VGPRs was slower on C5, profiles/r01/r01_encode_ab_occ_*.json).
 // Measured and not kept: 8-tile windows (C4 9.71 -> 12.23 ms), a chunk ->
 // frame map instead of the search (C4 9.35 -> 9.57 ms), non-temporal window
 // loads (C4 +8.8 %) -- DESIGN.md §5.
@@ -3643,12 +3643,12 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   // The walk's last workgroup scans the partials itself (walk_block_done) and
   // saves the k_scan_blocks launch (with release / acquire fences instead of
   // coherent partials it was slower: C1-shaped walk 0.034 -> 0.074 ms,
-  // profiles/r02_steps_fused.jsonl).
+  // profiles/r02/r02_steps_fused.jsonl).
   const bool fused = nblk > 0 && nblk <= kFusedScanMaxBlocks;
   uint32_t* done = fused ? ctx->d_done : nullptr;
   // the walk's uniform-stream speculation (D = 8) pays on long runs of equal
   // frames (C2, C3: -23..-28 %) and costs 2-7 % elsewhere (C1, C4,
-  // profiles/r02_walk_store_count_ab.jsonl); after a decode on this context
+  // profiles/r02/r02_walk_store_count_ab.jsonl); after a decode on this context
   // whose frames were mostly NOT the size of their predecessor the plain
   // chain walk (D = 0) runs instead
   const bool plain = wv == 1 || (wv != 1 && ctx->stats_known && ctx->prev_mixed);
@@ -3758,7 +3758,7 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   // every frame boundary takes the window path, which needs several
   // workgroups per CU to hide its latency (C3: 22.6 ms at 4/CU vs 36 ms at
   // 1/CU); it runs 7 per CU (C2 -18 %, C4 -4 % against 4,
-  // profiles/r01_encode_ab_lds_*.json, r01_encode_ab_occ_*.json), and
+  // profiles/r01/r01_encode_ab_lds_*.json, r01_encode_ab_occ_*.json), and
   // batches of big frames (mean >= kBigFrameBytes) keep 4 per CU (the rest
   // return at once)
   const uint32_t big = grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;

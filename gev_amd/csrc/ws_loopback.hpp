@@ -203,7 +203,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
   // device pass of iteration k runs while iteration k+1 waits on epoll and
   // reads its sockets, and its frames are echoed after those reads.  Measured
   // slower than the serial loop (pass, then echo) with closed-loop clients
-  // (profiles/r02_loopback_pipeline_ab.jsonl): a connection only sends again
+  // (profiles/r02/r02_loopback_pipeline_ab.jsonl): a connection only sends again
   // once echoed, so the overlap splits the connections into two alternating
   // passes of half the size, twice the fixed cost per pass -- default off.
   const char* pe = getenv("GEVWS_LB_PIPELINE");

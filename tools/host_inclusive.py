@@ -17,6 +17,10 @@ live server's zero-copy pass.
 
     python tools/host_inclusive.py [--gib 8] [--chunk-mib 64] [--streams 2] [--reps 3] [--sweep 64:2,128:3]
                                    [--direct-out] [--zero-copy-in]
+
+The report carries the pinned copy rates one way at a time and both ways at
+once (two streams): the last is the bound of the overlapped pipeline
+(`frac_of_bidirectional`).
 """
 from __future__ import annotations
 
@@ -142,9 +146,12 @@ def main():
         return {"chunk_mib": chunk_mib, "streams": S, "chunks": n_chunks, "seconds": round(t, 4),
                 "payload_GiBps": round(lay.payload_len / t / 2**30, 2), "frames_per_s": round(lay.n_frames / t, 1)}
 
-    # raw pinned copy rates of the same byte counts
-    n_tmp = min(2 << 30, lay.arena_bytes)
+    # raw pinned copy rates of the same byte counts: one direction at a time,
+    # and both at once on two streams -- the bound of an overlapped pipeline,
+    # whose every payload byte crosses PCIe once each way
+    n_tmp = min(2 << 30, lay.arena_bytes, h_pay.numel())
     d_tmp = torch.empty(n_tmp, dtype=torch.uint8, device=dev)
+    d_tmp2 = torch.empty(n_tmp, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(3):
@@ -156,7 +163,17 @@ def main():
         h_pay[:n_tmp].copy_(d_tmp, non_blocking=True)
     torch.cuda.synchronize()
     d2h = 3 * n_tmp / (time.perf_counter() - t0)
-    del d_tmp
+    s_up, s_down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        with torch.cuda.stream(s_up):
+            d_tmp.copy_(h_in[:n_tmp], non_blocking=True)
+        with torch.cuda.stream(s_down):
+            h_pay[:n_tmp].copy_(d_tmp2, non_blocking=True)
+    torch.cuda.synchronize()
+    bidir = 3 * n_tmp / (time.perf_counter() - t0)  # bytes each way per second, both at once
+    del d_tmp, d_tmp2
     configs = [(args.chunk_mib, args.streams)]
     if args.sweep:
         configs = [tuple(int(x) for x in item.split(":")) for item in args.sweep.split(",")]
@@ -168,7 +185,10 @@ def main():
     res = {"mode": mode,
            "workload": lay.name, "payload_bytes": lay.payload_len, "input_bytes": lay.arena_bytes,
            "payload_GiBps": best["payload_GiBps"], "frames_per_s": best["frames_per_s"], "best": best,
-           "runs": runs, "pinned_h2d_GBps": round(h2d / 1e9, 2), "pinned_d2h_GBps": round(d2h / 1e9, 2)}
+           "runs": runs, "pinned_h2d_GBps": round(h2d / 1e9, 2), "pinned_d2h_GBps": round(d2h / 1e9, 2),
+           "pinned_bidirectional_GBps_each_way": round(bidir / 1e9, 2),
+           # the pipeline moves about one input byte in and one payload byte out per payload byte
+           "frac_of_bidirectional": round(best["payload_GiBps"] * 2**30 / bidir, 3)}
     print(json.dumps(res))
 
 

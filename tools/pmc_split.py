@@ -14,7 +14,7 @@ requests of each size directly gives the read bytes for any access pattern:
 (all `_sum` over the TCC instances).  Prints / writes a JSON table: per kernel
 the mean per dispatch of every counter and the derived bytes.
 
-    python tools/pmc_split.py --prefix split --configs c4 c3 c5 [--out profiles/r02_pmc_split.json]
+    python tools/pmc_split.py --prefix split --configs c4 c3 c5 [--out profiles/r02/r02_pmc_split.json]
 """
 from __future__ import annotations
 
