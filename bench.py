@@ -264,6 +264,9 @@ def main():
                     help="threads of the all-cores CPU baseline (0 = every CPU this process may use)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--copy-reps", type=int, default=5, help="streaming-copy ceiling reps (0 = skip)")
+    ap.add_argument("--copy-interleave", type=int, default=0,
+                    help="R rounds of [decode, size-matched aligned copy] after the timed region: the unmask "
+                         "against the copy rate in the same clock state (0 = skip)")
     ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
     ap.add_argument("--unmask-variant", type=int, default=None, help="A/B: unmask kernel variant")
     ap.add_argument("--split-lanes", type=int, default=None,
@@ -441,6 +444,36 @@ def main():
             torch.cuda.synchronize()
             copy_by_load[name] = round(2 * n_copy / (e0.elapsed_time(e1) / args.copy_reps / 1e3) / 1e9, 1)
         copy_gbps = max(copy_by_load.values())
+    # --copy-interleave R: R rounds of [one decode (its unmask timed by HIP
+    # events), one aligned copy of the same byte count (plain and
+    # non-temporal loads, the faster)] back to back, so the ceiling is taken in
+    # the same clock / thermal state as the unmask it is compared with
+    interleaved = None
+    if args.copy_interleave > 0:
+        n_copy = lay.payload_padded // 16 * 16
+        ums, cms = [], []
+        for _ in range(args.copy_interleave):
+            engs[0].set_timing(True)
+            engs[0].decode_async(arena, lay.arena_bytes, conns, lay.n_conns, outs[0], max_frames, cap,
+                                 stream=streams[0])
+            engs[0].set_timing(False)
+            best = None
+            for flag in (0, 0x40000000):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                eng.copy_(out.payload, arena, n_copy, src_offset=0, grid=flag)
+                e1.record()
+                torch.cuda.synchronize()
+                t = e0.elapsed_time(e1)
+                best = t if best is None else min(best, t)
+            ph, cl = engs[0].timing()
+            ums.append(ph[3] / max(cl, 1))
+            cms.append(best)
+        um, cm = sorted(ums)[len(ums) // 2], sorted(cms)[len(cms) // 2]
+        ua = lay.algorithmic_bytes() / (um / 1e3) / 1e9
+        cg = 2 * n_copy / (cm / 1e3) / 1e9
+        interleaved = {"rounds": args.copy_interleave, "unmask_ms": round(um, 4), "copy_ms": round(cm, 4),
+                       "unmask_GBps": round(ua, 1), "copy_GBps": round(cg, 1), "frac_of_copy": round(ua / cg, 4)}
     if world == 1:
         torch.index_select(sum64, 0, sel, out=counts)
     c = counts.cpu().numpy()
@@ -493,7 +526,8 @@ def main():
                      "pipeline_frac": round(pipeline_gbps / HBM_PEAK_GBPS, 4),
                      "copy_ceiling": None if copy_gbps is None else round(copy_gbps, 1),
                      "copy_ceiling_by_load": copy_by_load or None,
-                     "frac_of_copy_ceiling": None if copy_gbps is None else round(achieved / copy_gbps, 4)},
+                     "frac_of_copy_ceiling": None if copy_gbps is None else round(achieved / copy_gbps, 4),
+                     **({"copy_interleaved": interleaved} if interleaved else {})},
         "verified_bit_exact": True,
         "frame_size_histogram": (size_histogram(glob) if args.config in ("c4", "c5") else None),
         "cpu_baseline": None,

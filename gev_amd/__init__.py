@@ -687,18 +687,23 @@ class Upgrader:
 def cu_split_masks(num_cus: int, front_cus: int, xcds: int = 8) -> Tuple[List[int], List[int]]:
     """CU masks (32-bit words) for a front stream of `front_cus` CUs and a back
     stream of the rest, the front's CUs spread evenly over the XCDs.  Bit i is
-    CU i; whether the runtime numbers CUs XCD by XCD (XCD = i / per_xcd) or
+    CU i; whether the runtime numbers CUs XCD by XCD (XCD = i // per_xcd) or
     round-robin (XCD = i % xcds), each XCD gets front_cus / xcds of the front's
-    CUs and keeps the rest for the back: CU 32 b + b + 8 m (m < front_cus /
-    xcds) sits on XCD b either way."""
+    CUs and keeps the rest for the back: front CU m of XCD b is bit
+    per_xcd * b + (b + m // 4 + xcds * (m % 4)) % per_xcd, which lies in XCD
+    b's block and is congruent to b + m // 4 (mod xcds), so the m of each block
+    also cover every residue equally."""
     per = num_cus // xcds
-    if num_cus % xcds or per % xcds or front_cus % xcds or not 0 < front_cus < num_cus or front_cus // xcds > per // xcds:
-        raise ValueError(f"cu_split_masks({num_cus}, {front_cus}): front CUs must be a multiple of {xcds}, "
-                         f"at most {num_cus // xcds}")
+    k = front_cus // xcds
+    if num_cus % xcds or per % xcds or front_cus % (4 * xcds if k >= 4 else xcds) or not 0 < front_cus < num_cus \
+            or (k > 4 and k % 4) or k > per - 4:
+        raise ValueError(f"cu_split_masks({num_cus}, {front_cus}): front CUs must be {xcds} x (1..4 or a "
+                         f"multiple of 4 up to {per - 4})")
     front = set()
     for b in range(xcds):
-        for m in range(front_cus // xcds):
-            front.add(per * b + (b + xcds * m) % per)
+        for m in range(k):
+            front.add(per * b + (b + m // 4 + xcds * (m % 4)) % per)
+    assert len(front) == front_cus
     words = (num_cus + 31) // 32
     fw, bw = [0] * words, [0] * words
     for i in range(num_cus):
