@@ -1,0 +1,977 @@
+// gevws_encode.hip -- the two next rows of SURVEY.md §8f on the device:
+// outbound encode, ws.WriteHeader (write.go:48-84) + ws.FrameToBytes
+// (frame.go:274-278) for a batch of reply frames written back to back as
+// handlerProtocol's send buffer (connection.go:213); and control-frame
+// dispatch, HandlerWrap.OnMessage (wrap.go:38-90) + util.HandleClose /
+// HandlePing / HandlePong / CheckCloseFrameData (util.go:27-85).
+#include "gevws_internal.hpp"
+
+namespace {
+
+// ------------------------------------------------------------------ outbound encode (§8f row 1)
+// ws.WriteHeader (write.go:48-84) + ws.FrameToBytes (frame.go:274-278) for a
+// batch of frames: wire[f] = WriteHeader(hdr_f) || payload_f, frames back to
+// back (as handlerProtocol appends Packet output to its tmpBuffer,
+// connection.go:213).  Go's byte arithmetic is kept: Rsv << 4 truncated to a
+// byte, OpCode OR-ed as a whole byte, byte(Length) for any Length <= 125.
+
+__device__ __forceinline__ uint32_t enc_header(const gevws_header& h, uint64_t& lo, uint64_t& hi) {
+  const uint32_t b0 = ((h.fin ? 0x80u : 0u) | ((uint32_t)h.rsv << 4) | h.opcode) & 0xffu;
+  const int64_t L = h.length;
+  uint32_t b1, n;
+  lo = 0;
+  hi = 0;
+  if (L <= 125) {
+    b1 = (uint32_t)L & 0xffu;
+    n = 2;
+  } else if (L <= 0xFFFF) {
+    b1 = 126;
+    lo = ((uint64_t)((L >> 8) & 0xff) << 16) | ((uint64_t)(L & 0xff) << 24);
+    n = 4;
+  } else {
+    b1 = 127;
+    const uint64_t be = __builtin_bswap64((uint64_t)L);  // bytes 2..9, big-endian
+    lo = be << 16;
+    hi = be >> 48;
+    n = 10;
+  }
+  if (h.masked) {
+    b1 |= 0x80;
+    uint32_t k;
+    memcpy(&k, h.mask, 4);
+    if (n == 2) lo |= (uint64_t)k << 16;
+    else if (n == 4) lo |= (uint64_t)k << 32;
+    else hi |= (uint64_t)k << 16;
+    n += 4;
+  }
+  lo |= (uint64_t)b0 | ((uint64_t)b1 << 8);
+  return n;
+}
+
+__device__ __forceinline__ uint32_t enc_hlen(const gevws_header& h) {
+  const int64_t L = h.length;
+  return (L <= 125 ? 2u : (L <= 0xFFFF ? 4u : 10u)) + (h.masked ? 4u : 0u);
+}
+
+// A workgroup sizes kEncSlabs consecutive slabs of kWalkBlock frames (one
+// frame per lane per slab, coalesced), so the batch has one block partial per
+// 4 096 frames and the single-workgroup scan of partials stays short (C4:
+// 10.7 K partials instead of 171 K).
+constexpr int kEncSlabs = 16;
+// Tile-map entries a lane writes itself in k_enc_emit (unrolled, predicated);
+// a frame with more has the rest written by its whole wave.  16 as a plain
+// loop: C5 emit 79 -> 16 us but C4 138 -> 466 us
+// (profiles/r03/r03_encode_emit_lane16_*), so 4.
+constexpr int kEncLaneTiles = 4;
+// The frame count of a chained pass (decode -> dispatch -> encode with no host
+// round trip): the producing step's summary gates the consumer -- its frames,
+// or none when it failed (a capacity error leaves stale records behind).
+__device__ __forceinline__ uint64_t gated_count(uint64_t n, const gevws_summary* __restrict__ gate) {
+  if (!gate) return n;
+  const gevws_summary g = *gate;
+  return g.status != GEVWS_OK ? 0 : (g.frames < n ? g.frames : n);
+}
+
+// Also writes each frame's wire size (h + L) into out_off[f], which k_enc_emit
+// turns into the offset in place: the emit pass reads 8 bytes per frame
+// instead of the 32-byte record again (C4: 0.35 instead of 1.4 GB).
+__global__ __launch_bounds__(kWalkBlock) void k_enc_size(const gevws_out_frame* __restrict__ fr, uint64_t n,
+                                                         uint64_t* __restrict__ blk, uint64_t* __restrict__ out_off,
+                                                         const gevws_summary* __restrict__ gate = nullptr) {
+  n = gated_count(n, gate);
+  const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;
+  uint64_t one = 0, wire = 0, pl = 0;
+#pragma unroll 4
+  for (int j = 0; j < kEncSlabs; ++j) {
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    if (f < n) {
+      const gevws_out_frame o = fr[f];
+      const uint64_t w = enc_hlen(o.hdr) + o.payload_len;
+      one += 1;
+      pl += o.payload_len;
+      wire += w;
+      out_off[f] = w;
+    }
+  }
+  __shared__ uint64_t s_part[3][kWalkBlock / 64];
+  const uint64_t vals[3] = {one, wire, pl};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint64_t sm = wave_sum(vals[k]);
+    if (lane == 0) s_part[k][w] = sm;
+  }
+  __syncthreads();
+  if (threadIdx.x < kBlkFields) {
+    uint64_t sm = 0;
+    if (threadIdx.x < 3)
+      for (int j = 0; j < kWalkBlock / 64; ++j) sm += s_part[threadIdx.x][j];
+    blk[(uint64_t)blockIdx.x * kBlkFields + threadIdx.x] = sm;
+  }
+}
+
+__global__ __launch_bounds__(kWalkBlock) void k_enc_emit(uint64_t n,
+                                                         const uint64_t* __restrict__ blk,
+                                                         const gevws_summary* __restrict__ sum,
+                                                         uint64_t* __restrict__ out_off,
+                                                         uint32_t* __restrict__ tile_first,
+                                                         const gevws_summary* __restrict__ gate = nullptr) {
+  if (sum->status != GEVWS_OK) return;
+  n = gated_count(n, gate);
+  const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;
+  const uint64_t carry = blk[(uint64_t)blockIdx.x * kBlkFields + 1];
+  // every slab's wire sizes (k_enc_size left them in out_off) loaded at once,
+  // then ONE workgroup scan over all slabs: a wave scan per slab, and the 64
+  // (slab, wave) totals scanned by one wave in frame order -- two barriers per
+  // workgroup instead of two per slab
+  constexpr int NW = kWalkBlock / 64;
+  static_assert(kEncSlabs * NW == 64, "one lane per (slab, wave) total");
+  __shared__ uint64_t s_base[kEncSlabs * NW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t ws[kEncSlabs], inc[kEncSlabs];
+#pragma unroll
+  for (int j = 0; j < kEncSlabs; ++j) {
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    ws[j] = f < n ? out_off[f] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kEncSlabs; ++j) {
+    inc[j] = wave_incl_scan(ws[j]);
+    if (lane == 63) s_base[j * NW + wv] = inc[j];
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const uint64_t x = s_base[lane];
+    s_base[lane] = wave_incl_scan(x) - x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kEncSlabs; ++j) {  // (fully unrolled: ws / inc stay in registers)
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    if (f - threadIdx.x >= n) break;  // workgroup-uniform: slab past the batch
+    // tile map: tiles whose first byte lies in the frame's wire bytes [o, o + v).
+    // A lane writes up to kEncLaneTiles entries itself; the rest of a big
+    // frame's range (a 1 MiB frame has 256) is written by its whole wave, 64
+    // entries a store.
+    const uint64_t end = carry + s_base[j * NW + wv] + inc[j];
+    const uint64_t o = end - ws[j];
+    uint64_t t = (o + kTile - 1) / kTile;
+    const uint64_t te = f < n ? (end + kTile - 1) / kTile : t;
+    if (f < n) out_off[f] = o;
+#pragma unroll
+    for (int k = 0; k < kEncLaneTiles; ++k, ++t)
+      if (t < te) tile_first[t] = (uint32_t)f;
+    for (uint64_t rest = __ballot(t < te); rest; rest &= rest - 1) {  // (whole wave active here)
+      const int src = __builtin_ctzll(rest);
+      const uint64_t bt = __shfl((unsigned long long)t, src), be = __shfl((unsigned long long)te, src);
+      const uint32_t bf = (uint32_t)__shfl((unsigned long long)f, src);
+      for (uint64_t x = bt + (uint64_t)lane; x < be; x += 64) tile_first[x] = bf;
+    }
+  }
+}
+
+// One output byte at absolute position `a` of frame f (global-memory form, used
+// by the fallback path).
+__device__ __forceinline__ uint8_t enc_byte_global(const gevws_out_frame* __restrict__ fr,
+                                                   const uint64_t* __restrict__ out_off,
+                                                   const uint8_t* __restrict__ payload, uint64_t f, uint64_t a) {
+  const gevws_out_frame o = fr[f];
+  uint64_t lo, hi;
+  const uint32_t hl = enc_header(o.hdr, lo, hi);
+  const uint64_t r = a - out_off[f];
+  if (r < hl) return (uint8_t)(r < 8 ? (lo >> (8 * r)) : (hi >> (8 * (r - 8))));
+  return payload[o.payload_off + (r - hl)];
+}
+
+constexpr int kEncWinFrames = 1024;
+// bytes [k0, k1) of a 16-byte lane (0 <= k0 < k1 <= 16)
+__device__ __forceinline__ u128 byte_mask(int k0, int k1) {
+  const u128 hi = (k1 >= 16) ? ~(u128)0 : (((u128)1 << (8 * k1)) - 1);
+  const u128 lo = ((u128)1 << (8 * k0)) - 1;
+  return hi & ~lo;
+}
+
+// The LDS frame table of an encode window.  LH: the serialised headers are
+// not kept in LDS (h0 / h1 unused) but rebuilt from the frame's record (an L2
+// hit: the window just loaded it), which frees 16 KiB of LDS per workgroup for
+// occupancy -- k_encode; the one-workgroup k_handle_small keeps them in LDS.
+struct EncWin {
+  const int32_t* start;  // wire start relative to the window, clamped >= -64
+  const int32_t* pend;   // payload end relative to the window, clamped
+  const uint8_t* hlen;
+  const uint64_t* delta;  // payload_off - out_off - hlen (mod 2^64)
+  const uint64_t* h0;     // !LH: serialised header bytes 0-7 / 8-15
+  const uint64_t* h1;
+};
+
+// Assemble the 16 output bytes at window-relative position `rel` (absolute `a`)
+// from the frames overlapping it (at most 8: every frame is >= 2 wire bytes),
+// starting at frame lo: header bytes from the frame's serialised header,
+// payload bytes from ONE unaligned 16-byte load per frame.  The first two
+// frames' loads are issued together (most boundary chunks hold the end of one
+// payload and the header + start of the next: C2 -2.6 %, C5 -1.6 % against one
+// at a time, profiles/r01/r01_encode_ab_asm2_*.json); further frames (frames of a
+// few bytes) continue one by one.
+template <bool LH>
+__device__ __forceinline__ void enc_assemble_from(u128& acc, int32_t rel, uint64_t a, int kmax, uint32_t j, uint32_t F,
+                                                  const EncWin& W, const uint8_t* __restrict__ payload,
+                                                  const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
+  for (; j < F && W.start[j] < rel + kmax; ++j) {
+    const int32_t hs = W.start[j];
+    const int32_t ps = hs + (int32_t)W.hlen[j];
+    const int32_t pe = W.pend[j];
+    // header bytes [max(hs, rel), min(ps, rel + kmax))
+    const int32_t h0 = hs > rel ? hs : rel;
+    const int32_t h1 = ps < rel + kmax ? ps : rel + kmax;
+    if (h0 < h1) {
+      u128 H;
+      if constexpr (LH) {
+        uint64_t hl, hh;
+        enc_header(fr[f_lo + j].hdr, hl, hh);
+        H = (u128)hl | ((u128)hh << 64);
+      } else {
+        H = (u128)W.h0[j] | ((u128)W.h1[j] << 64);
+      }
+      acc |= ((H >> (8 * (h0 - hs))) << (8 * (h0 - rel))) & byte_mask(h0 - rel, h1 - rel);
+    }
+    // payload bytes [max(ps, rel), min(pe, rel + kmax))
+    const int32_t p0 = ps > rel ? ps : rel;
+    const int32_t p1 = pe < rel + kmax ? pe : rel + kmax;
+    if (p0 < p1) {
+      const int k0 = p0 - rel;
+      const u128 v = u128_of(ld16u(payload + (a + (uint64_t)k0 + W.delta[j])));
+      acc |= (v << (8 * k0)) & byte_mask(k0, p1 - rel);
+    }
+  }
+}
+
+template <bool LH>
+__device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
+                                              const EncWin& W, const uint8_t* __restrict__ payload,
+                                              const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
+  const int kmax = (a + 16 <= total) ? 16 : (int)(total - a);
+  int32_t hs[2], h0[2], h1[2], p0[2], p1[2];
+  u32x4 pv[2];
+  u64x2 hv[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t j = lo + k;
+    const bool in = j < F && W.start[j < F ? j : lo] < rel + kmax;
+    const uint32_t jj = in ? j : lo;
+    hs[k] = W.start[jj];
+    const int32_t ps = hs[k] + (int32_t)W.hlen[jj];
+    const int32_t pe = W.pend[jj];
+    h0[k] = hs[k] > rel ? hs[k] : rel;
+    h1[k] = in ? (ps < rel + kmax ? ps : rel + kmax) : h0[k];
+    p0[k] = ps > rel ? ps : rel;
+    p1[k] = in ? (pe < rel + kmax ? pe : rel + kmax) : p0[k];
+    pv[k] = u32x4{0, 0, 0, 0};
+    hv[k] = u64x2{0, 0};
+    if (p0[k] < p1[k]) pv[k] = ld16u(payload + (a + (uint64_t)(p0[k] - rel) + W.delta[jj]));
+    if (h0[k] < h1[k]) {
+      if constexpr (LH) hv[k] = *reinterpret_cast<const u64x2*>(fr + f_lo + jj);  // the header half of the record
+      else hv[k] = u64x2{W.h0[jj], W.h1[jj]};
+    }
+  }
+  u128 acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (h0[k] < h1[k]) {
+      u128 H;
+      if constexpr (LH) {
+        gevws_header hd;
+        memcpy(&hd, &hv[k], 16);
+        uint64_t hl, hh;
+        enc_header(hd, hl, hh);
+        H = (u128)hl | ((u128)hh << 64);
+      } else {
+        H = (u128)hv[k][0] | ((u128)hv[k][1] << 64);
+      }
+      acc |= ((H >> (8 * (h0[k] - hs[k]))) << (8 * (h0[k] - rel))) & byte_mask(h0[k] - rel, h1[k] - rel);
+    }
+    if (p0[k] < p1[k]) {
+      const int k0 = p0[k] - rel;
+      acc |= (u128_of(pv[k]) << (8 * k0)) & byte_mask(k0, p1[k] - rel);
+    }
+  }
+  if (lo + 2 < F && W.start[lo + 2] < rel + kmax)  // more frames in these 16 bytes
+    enc_assemble_from<LH>(acc, rel, a, kmax, lo + 2, F, W, payload, fr, f_lo);
+  return u32x4_of(acc);
+}
+
+// The encode's byte stream (k_enc_size / k_enc_emit placed every frame's wire
+// bytes and the output-tile -> frame map).  Each workgroup owns a contiguous
+// run of output tiles.
+//  * Inside one payload for the next U tiles: stream (a misaligned source as
+//    the unmask's streaming path: wave-contiguous U KiB spans, aligned
+//    non-temporal loads, DPP rotate + v_alignbyte; an aligned one with plain
+//    loads), aligned non-temporal stores.
+//  * Otherwise a window of kWinTiles tiles: its frames' wire starts, payload
+//    ends, header lengths and payload offsets in LDS; each lane finds the
+//    frame of each of its chunks by binary search; a chunk inside one payload
+//    is loaded (unaligned) and stored; a chunk that straddles a frame boundary
+//    (header bytes or two frames' pieces) is queued in LDS and assembled
+//    afterwards by the whole workgroup, one chunk per lane, instead of by the
+//    one or two lanes of each wave that meet them while the other lanes wait.
+//    A 64-byte group of chunks holding a boundary is queued whole (its
+//    interior chunks with it, four consecutive slots), so one store writes the
+//    group's 64 bytes: otherwise every frame boundary left its line to HBM as
+//    two partial writes (C4: 46 M 32-byte write requests per launch, 0 with
+//    it; the whole C4 encode 10.70 -> 9.11 ms, profiles/r02/r02_encode_ab_g64_*.json).
+//    All the window's payload loads are issued before its stores, and the
+//    interior chunks are stored only after the queue barrier and the lane's
+//    first queued chunk has been assembled, so the interior loads and the first
+//    assembly's loads are in flight together (C4 9.39 -> 9.17 ms,
+//    profiles/r03/r03_encode_eo_ab.jsonl).
+// The window path is latency-bound: the kernel is held to 72 VGPRs for 7
+// workgroups per CU (amdgpu_waves_per_eu(7): C2 -4 %, C4 -2 % against 6 per
+// CU; 8 per CU at 64 VGPRs was slower on C5, profiles/r01/r01_encode_ab_occ_*.json).
+// Measured and not kept: 8-tile windows (C4 9.71 -> 12.23 ms), a chunk ->
+// frame map instead of the search (C4 9.35 -> 9.57 ms), non-temporal window
+// loads (C4 +8.8 %) -- DESIGN.md §5.
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(7))) void k_encode(
+    const gevws_out_frame* __restrict__ fr, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ out_off,
+    const uint32_t* __restrict__ tile_first, const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
+    uint32_t big_grid) {
+  constexpr int U = 4, WT = kWinTiles, WF = kEncWinFrames;
+  __shared__ int32_t s_start[WF];
+  __shared__ int32_t s_pend[WF];
+  __shared__ uint8_t s_hlen[WF];
+  __shared__ uint32_t s_bnd[WT * kUnmaskBlock];  // queued chunk: rel / 16 | frame << 16 (~0: a group's filler)
+  __shared__ uint32_t s_nb;
+  __shared__ uint64_t s_delta[WF];
+  const EncWin W{s_start, s_pend, s_hlen, s_delta, nullptr, nullptr};
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t total = sum->payload_bytes;  // wire bytes
+  const uint64_t nframes = sum->frames;
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint32_t groups = active_groups(total, nframes, big_grid);
+  if (blockIdx.x >= groups) return;
+  const uint64_t per = (ntiles + groups - 1) / groups;
+  uint64_t t = (uint64_t)blockIdx.x * per;
+  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+  uint64_t c_ps = 0, c_pe = 0, c_delta = 0;  // cached frame: payload [c_ps, c_pe) in wire coordinates
+  while (t < tend) {
+    const uint32_t lane_off = fresh_tid() * 16;  // recomputed per step: held, it was spilled
+    const uint64_t base = t * kTile;
+    if (base >= c_pe) {  // workgroup-uniform refresh (scalar loads)
+      const uint64_t f = tile_first[t];
+      const gevws_out_frame o = fr[f];
+      c_ps = out_off[f] + enc_hlen(o.hdr);
+      c_pe = c_ps + o.payload_len;
+      c_delta = o.payload_off - c_ps;
+    }
+    if (t + U <= tend && base >= c_ps && base + U * kTile <= c_pe) {  // inside one payload: stream
+      u32x4 v[U];
+      const uint8_t* s0 = payload + (base + c_delta);
+      const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(s0) & 15);  // wave-uniform
+      if (mis != 0) {
+        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const uint64_t wrel = (uint64_t)wave * U * 1024 + lane * 16;
+        const uint8_t* a = s0 + wrel - mis;
+        uint8_t* d = out + base + wrel;
+        const bool last = lane == 63;
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + u * 1024));
+        u32x4 e = u32x4{0, 0, 0, 0};
+        if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
+        u32x4 r = rot_next_lane(v[0]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const u32x4 rn = u + 1 < U ? rot_next_lane(v[u + 1 < U ? u + 1 : u]) : e;
+          st16_nt(d + u * 1024, funnel16(v[u], last ? rn : r, mis));
+          r = rn;
+        }
+        t += U;
+        continue;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld16u(payload + (base + u * kTile + lane_off + c_delta));
+#pragma unroll
+      for (int u = 0; u < U; ++u) st16_nt(out + base + u * kTile + lane_off, v[u]);
+      t += U;
+      continue;
+    }
+    const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
+    const uint64_t wbase = base;
+    const uint64_t f_lo = tile_first[t];
+    const uint64_t f_hi = (t + wt) < ntiles ? (uint64_t)tile_first[t + wt] : nframes - 1;
+    const uint64_t F = f_hi - f_lo + 1;
+    if (F <= (uint64_t)WF) {
+      __syncthreads();
+      for (uint64_t i = fresh_tid(); i < F; i += kUnmaskBlock) {
+        const gevws_out_frame o = fr[f_lo + i];
+        const uint32_t hl = enc_hlen(o.hdr);
+        const uint64_t oo = out_off[f_lo + i];
+        const int64_t st = (int64_t)(oo - wbase);
+        s_start[i] = st < -64 ? -64 : (int32_t)st;
+        const int64_t pe = st + hl + (int64_t)o.payload_len;
+        s_pend[i] = pe > 0x7fffffffll ? 0x7fffffff : (int32_t)pe;
+        s_hlen[i] = hl;
+        s_delta[i] = o.payload_off - oo - hl;
+      }
+      if (threadIdx.x == 0) s_nb = 0;
+      __syncthreads();
+      // every chunk's frame and kind first (interior of one payload, or a
+      // boundary to queue); a load inside the interior/boundary branch made
+      // the compiler wait for it at the branch's join
+      u32x4 v[WT];
+      uint32_t interior = 0, queued = 0;
+      uint32_t qlo[WT];
+#pragma unroll
+      for (int u = 0; u < WT; ++u) {
+        const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
+        const uint64_t a = wbase + (uint64_t)rel;
+        const bool valid = (uint64_t)u < wt && a < total;
+        uint32_t lo = 0, hi = valid ? (uint32_t)F - 1 : 0u;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+        }
+        const bool in = valid && rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo];
+        qlo[u] = lo;
+        interior |= (in ? 1u : 0u) << u;
+        queued |= (valid && !in ? 1u : 0u) << u;
+      }
+      // 64-byte groups holding a queued chunk go to the queue whole
+      const uint32_t lane = threadIdx.x & 63, g0 = lane & ~3u;
+#pragma unroll
+      for (int u = 0; u < WT; ++u) {
+        const uint64_t bal = __ballot((queued >> u) & 1u);  // whole wave active
+        const bool defer = ((bal >> g0) & 0xFull) != 0;     // (group-uniform)
+        uint32_t slot = 0;
+        if (defer && (lane & 3u) == 0) slot = atomicAdd(&s_nb, 4u);
+        slot = __shfl(slot, (int)g0);
+        if (defer) {
+          const bool valid = (interior | queued) & (1u << u);
+          s_bnd[slot + (lane & 3u)] =
+              valid ? ((uint32_t)(u * (int32_t)kTile + (int32_t)lane_off) >> 4) | (qlo[u] << 16) : 0xffffffffu;
+          interior &= ~(1u << u);
+        }
+      }
+      // the interior loads (the queue pass loads its chunks itself; every lane
+      // loads, a non-interior chunk from payload[0], always readable, unused)
+#pragma unroll
+      for (int u = 0; u < WT; ++u) {
+        const bool in = (interior >> u) & 1u;
+        const uint64_t a = wbase + (uint64_t)(u * (int32_t)kTile + (int32_t)lane_off);
+        v[u] = ld16u(payload + (in ? a + s_delta[qlo[u]] : 0ull));
+      }
+      __syncthreads();  // the queue is complete
+      const uint32_t nb = s_nb;
+      const uint32_t i0 = fresh_tid();
+      u32x4 x0 = u32x4{0, 0, 0, 0};
+      uint32_t q0 = 0xffffffffu;
+      if (i0 < nb) {
+        q0 = s_bnd[i0];
+        if (q0 != 0xffffffffu) {
+          const int32_t rel = (int32_t)((q0 & 0xffffu) << 4);
+          x0 = enc_assemble<true>(rel, wbase + (uint64_t)rel, total, q0 >> 16, (uint32_t)F, W, payload, fr, f_lo);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < WT; ++u)
+        if (interior & (1u << u)) st16_nt(out + wbase + u * kTile + fresh_tid() * 16, v[u]);
+      if (q0 != 0xffffffffu) st16_nt(out + wbase + (uint64_t)((q0 & 0xffffu) << 4), x0);
+      for (uint32_t i = i0 + kUnmaskBlock; i < nb; i += kUnmaskBlock) {
+        const uint32_t q = s_bnd[i];
+        if (q == 0xffffffffu) continue;  // a group's slot past the batch's end
+        const int32_t rel = (int32_t)((q & 0xffffu) << 4);
+        const uint64_t a = wbase + (uint64_t)rel;
+        st16_nt(out + a, enc_assemble<true>(rel, a, total, q >> 16, (uint32_t)F, W, payload, fr, f_lo));
+      }
+      t += wt;
+      continue;
+    }
+    // more than kEncWinFrames frames in the window (frames of a few bytes):
+    // one tile, per-lane global lookup and byte assembly
+    {
+      const uint64_t a = t * kTile + lane_off;
+      if (a < total) {
+        uint64_t lo = tile_first[t];
+        uint64_t hi = (t + 1 < ntiles) ? (uint64_t)tile_first[t + 1] : nframes - 1;
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi + 1) >> 1;
+          if (out_off[mid] <= a) lo = mid; else hi = mid - 1;
+        }
+        uint32_t w[4] = {0, 0, 0, 0};
+        uint64_t j = lo;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          while (j + 1 < nframes && out_off[j + 1] <= a + k) ++j;
+          const uint32_t byte = (a + k < total) ? enc_byte_global(fr, out_off, payload, j, a + k) : 0u;
+          w[k >> 2] |= byte << (8 * (k & 3));
+        }
+        *reinterpret_cast<u32x4*>(out + a) = u32x4{w[0], w[1], w[2], w[3]};
+      }
+      t += 1;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ control-frame dispatch (§8f row 2)
+// HandlerWrap.OnMessage (plugins/websocket/wrap.go:38-90) for decoded frames:
+// close -> util.HandleClose (util.go:27-46) + ShutdownWrite; ping -> pong with
+// the same payload (util.go:49-51); pong -> ping (util.go:54-56, kept as the
+// reference has it); other control opcodes -> nothing; data frames -> the echo
+// policy standing in for the user's WSHandler (empty replies send nothing,
+// wrap.go:72).  Replies are gevws_out_frame records for gevws_encode_batch.
+
+constexpr uint32_t kAuxSlot = 128;  // one close body (<= 125 bytes) per slot
+
+__device__ __constant__ char kErrNotInUse[] = "status code is not in use";
+__device__ __constant__ char kErrAppLevel[] = "status code is only application level";
+__device__ __constant__ char kErrNoMeaning[] = "status code has no meaning yet";
+__device__ __constant__ char kErrUnknown[] = "status code is not defined in spec";
+__device__ __constant__ char kErrUtf8[] = "invalid utf8 sequence in close reason";
+
+// unicode/utf8.ValidString: strict UTF-8.
+__device__ bool utf8_valid(const uint8_t* p, uint64_t n) {
+  uint64_t i = 0;
+  while (i < n) {
+    const uint32_t c = p[i];
+    if (c < 0x80) { ++i; continue; }
+    uint32_t need, lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) need = 1;
+    else if (c == 0xE0) { need = 2; lo = 0xA0; }
+    else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) need = 2;
+    else if (c == 0xED) { need = 2; hi = 0x9F; }
+    else if (c == 0xF0) { need = 3; lo = 0x90; }
+    else if (c >= 0xF1 && c <= 0xF3) need = 3;
+    else if (c == 0xF4) { need = 3; hi = 0x8F; }
+    else return false;
+    if (i + need >= n) return false;  // truncated sequence
+    const uint32_t c1 = p[i + 1];
+    if (c1 < lo || c1 > hi) return false;
+    for (uint32_t k = 2; k <= need; ++k)
+      if ((p[i + k] & 0xC0) != 0x80) return false;
+    i += need + 1;
+  }
+  return true;
+}
+
+// 0: no reply, 1: reply with the frame's own payload, 2: close reply (aux body), 3: bare close header
+__device__ __forceinline__ int disp_kind(const gevws_header& h, int policy, uint32_t& op_out) {
+  const uint32_t op = h.opcode;
+  if (op & 8) {
+    if (op == 0x8) return h.length == 0 ? 3 : 2;
+    if (op == 0x9) { op_out = 0xA; return 1; }
+    if (op == 0xA) { op_out = 0x9; return 1; }
+    return 0;
+  }
+  if (policy == GEVWS_HANDLER_NONE || h.length <= 0) return 0;
+  op_out = policy == GEVWS_HANDLER_ECHO_BINARY ? 0x2u : 0x1u;
+  return 1;
+}
+
+__global__ __launch_bounds__(kWalkBlock) void k_disp_count(const gevws_frame* __restrict__ fr, uint64_t n, int policy,
+                                                           uint64_t* __restrict__ blk,
+                                                           const gevws_summary* __restrict__ gate = nullptr) {
+  n = gated_count(n, gate);
+  const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;  // as k_enc_size
+  uint64_t rep = 0, aux = 0, shut = 0;
+#pragma unroll 4
+  for (int j = 0; j < kEncSlabs; ++j) {
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    if (f < n) {
+      uint32_t op;
+      const int k = disp_kind(fr[f].hdr, policy, op);
+      rep += k != 0;
+      aux += k == 2;
+      shut += k >= 2;
+    }
+  }
+  __shared__ uint64_t s_part[3][kWalkBlock / 64];
+  const uint64_t vals[3] = {rep, aux, shut};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint64_t sm = wave_sum(vals[k]);
+    if (lane == 0) s_part[k][w] = sm;
+  }
+  __syncthreads();
+  if (threadIdx.x < kBlkFields) {
+    uint64_t sm = 0;
+    const int fld = threadIdx.x == 3 ? 2 : (threadIdx.x == 2 ? -1 : threadIdx.x);
+    if (fld >= 0)
+      for (int j = 0; j < kWalkBlock / 64; ++j) sm += s_part[fld][j];
+    blk[(uint64_t)blockIdx.x * kBlkFields + threadIdx.x] = sm;  // [replies, aux slots, 0, shutdowns]
+  }
+}
+
+__device__ void put_close_body(uint8_t* dst, uint32_t code, const uint8_t* reason, uint64_t rlen, uint32_t& n) {
+  // ws.NewCloseFrameBody (frame.go:251-259): BE16 code + reason cropped to 123 bytes
+  const uint64_t crop = rlen < 123 ? rlen : 123;
+  dst[0] = (uint8_t)(code >> 8);
+  dst[1] = (uint8_t)code;
+  for (uint64_t i = 0; i < crop; ++i) dst[2 + i] = reason[i];
+  n = (uint32_t)(2 + crop);
+}
+
+__device__ void put_close_error(uint8_t* dst, const char* msg, uint32_t& n) {
+  uint64_t len = 0;
+  while (msg[len]) ++len;
+  put_close_body(dst, 1002, reinterpret_cast<const uint8_t*>(msg), len, n);  // StatusProtocolError
+}
+
+// One reply record (and for a close its aux-slot body) for decoded frame f.
+__device__ __forceinline__ void disp_reply(const gevws_frame& in, int kind, uint32_t op, uint64_t f, uint64_t r,
+                                        uint64_t slot, const uint8_t* __restrict__ payload, uint64_t aux_off,
+                                        gevws_out_frame* __restrict__ rep, int64_t* __restrict__ reply_of,
+                                        uint8_t* __restrict__ aux_base) {
+  reply_of[f] = (int64_t)r;
+  gevws_out_frame o;
+  memset(&o, 0, sizeof(o));
+  o.hdr.fin = 1;
+  if (kind == 1) {
+    o.hdr.opcode = (uint8_t)op;
+    o.hdr.length = in.hdr.length;
+    o.payload_off = in.payload_off;
+    o.payload_len = (uint64_t)in.hdr.length;
+  } else if (kind == 3) {
+    o.hdr.opcode = 0x8;  // WriteHeader(&Header{Fin: true, OpCode: OpClose}), util.go:28-33
+  } else {
+    uint8_t* body = aux_base + slot * kAuxSlot;
+    const uint8_t* p = payload + in.payload_off;
+    const uint64_t L = (uint64_t)in.hdr.length;
+    uint32_t code = 0;
+    const uint8_t* reason = p;
+    uint64_t rlen = 0;
+    if (L >= 2) {  // ParseCloseFrameData, read.go:89-102
+      code = ((uint32_t)p[0] << 8) | p[1];
+      reason = p + 2;
+      rlen = L - 2;
+    }
+    uint32_t nb;
+    const bool defined = code == 1000 || code == 1001 || code == 1002 || code == 1003 || code == 1007 ||
+                         code == 1008 || code == 1009 || code == 1010 || code == 1011 || code == 1005 ||
+                         code == 1006 || code == 1015;
+    if (code <= 999) put_close_error(body, kErrNotInUse, nb);
+    else if (code == 1005 || code == 1006 || code == 1015) put_close_error(body, kErrAppLevel, nb);
+    else if (code == 1004) put_close_error(body, kErrNoMeaning, nb);
+    else if (code >= 1000 && code <= 2999 && !defined) put_close_error(body, kErrUnknown, nb);
+    else if (!utf8_valid(reason, rlen)) put_close_error(body, kErrUtf8, nb);
+    else put_close_body(body, code, reason, rlen, nb);
+    o.hdr.opcode = 0x8;
+    o.hdr.length = nb;
+    o.payload_off = aux_off + slot * kAuxSlot;
+    o.payload_len = nb;
+  }
+  rep[r] = o;
+}
+
+__global__ __launch_bounds__(kWalkBlock) void k_disp_emit(const gevws_frame* __restrict__ fr, uint64_t n, int policy,
+                                                          const uint8_t* __restrict__ payload, uint64_t aux_off,
+                                                          const uint64_t* __restrict__ blk,
+                                                          const gevws_summary* __restrict__ sum,
+                                                          gevws_out_frame* __restrict__ rep,
+                                                          int64_t* __restrict__ reply_of,
+                                                          uint8_t* __restrict__ aux_base,
+                                                          const gevws_summary* __restrict__ gate = nullptr) {
+  if (sum->status != GEVWS_OK) return;
+  n = gated_count(n, gate);
+  const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;  // as k_enc_emit
+  uint64_t c_rep = blk[(uint64_t)blockIdx.x * kBlkFields + 0], c_aux = blk[(uint64_t)blockIdx.x * kBlkFields + 1];
+  for (int j = 0; j < kEncSlabs; ++j) {
+    const uint64_t f = f0 + (uint64_t)j * kWalkBlock;
+    if (f - threadIdx.x >= n) break;  // workgroup-uniform: slab past the batch
+    uint32_t op = 0;
+    int kind = 0;
+    gevws_frame in;
+    if (f < n) {
+      in = fr[f];
+      kind = disp_kind(in.hdr, policy, op);
+    }
+    uint64_t v[2] = {(uint64_t)(kind != 0), (uint64_t)(kind == 2)};
+    uint64_t ex[2], tot[2];
+    block_excl_scan<kWalkBlock, 2>(v, ex, tot);
+    if (f < n) {
+      if (kind == 0)
+        reply_of[f] = -1;
+      else
+        disp_reply(in, kind, op, f, c_rep + ex[0], c_aux + ex[1], payload, aux_off, rep, reply_of, aux_base);
+    }
+    c_rep += tot[0];
+    c_aux += tot[1];
+  }
+}
+
+
+// A live pass's handler step in ONE launch (gevws_handle_decoded_async on a
+// pass of at most kHandleSmallFrames decoded frames): k_disp_count /
+// k_disp_emit's dispatch and the encode's size / scan / FrameToBytes for the
+// replies, in one workgroup -- each step's counts by block scans, the replies'
+// wire image assembled 16 bytes per lane from an LDS table of every reply
+// (enc_assemble: headers rebuilt from the records, payloads by unaligned
+// loads).  Outputs and summaries are exactly the two-step chain's (seven
+// launches, ~5 us of GPU time each whatever their size).
+constexpr uint64_t kHandleSmallFrames = kEncWinFrames;
+__global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* __restrict__ fr, uint64_t max_frames,
+                                                            const gevws_summary* __restrict__ dec, int policy,
+                                                            uint8_t* __restrict__ payload, uint64_t aux_off,
+                                                            uint64_t aux_cap, gevws_out_frame* __restrict__ rep,
+                                                            int64_t* __restrict__ reply_of,
+                                                            gevws_summary* __restrict__ dsum, uint8_t* __restrict__ out,
+                                                            uint64_t out_cap, uint64_t* __restrict__ out_off,
+                                                            gevws_summary* __restrict__ esum,
+                                                            uint32_t* __restrict__ done = nullptr,
+                                                            uint32_t seq = 0) {
+  constexpr int WF = (int)kHandleSmallFrames;
+  __shared__ int32_t s_start[WF];
+  __shared__ int32_t s_pend[WF];
+  __shared__ uint8_t s_hlen[WF];
+  __shared__ uint64_t s_delta[WF];
+  __shared__ uint64_t s_h0[WF], s_h1[WF];
+  __shared__ uint32_t s_status;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t n = gated_count(max_frames, dec);
+  // 1. dispatch counts (k_disp_count + k_scan_blocks)
+  uint64_t rep_n = 0, aux_n = 0, shut_n = 0;
+  for (uint64_t f0 = 0; f0 < n; f0 += kWalkBlock) {  // workgroup-uniform
+    const uint64_t f = f0 + tid;
+    uint32_t op = 0;
+    const int k = f < n ? disp_kind(fr[f].hdr, policy, op) : 0;
+    const uint64_t v[3] = {(uint64_t)(k != 0), (uint64_t)(k == 2), (uint64_t)(k >= 2)};
+    uint64_t ex[3], tot[3];
+    block_excl_scan<kWalkBlock, 3>(v, ex, tot);
+    rep_n += tot[0];
+    aux_n += tot[1];
+    shut_n += tot[2];
+  }
+  const bool disp_ok = rep_n <= n && aux_n <= aux_cap / kAuxSlot;
+  if (tid == 0) {
+    gevws_summary sm;
+    memset(&sm, 0, sizeof(sm));
+    sm.frames = rep_n;
+    sm.payload_bytes = aux_n;
+    sm.errors = shut_n;
+    sm.status = disp_ok ? GEVWS_OK : GEVWS_ERR_CAPACITY;
+    *dsum = sm;
+  }
+  // 2. replies (k_disp_emit)
+  if (disp_ok) {
+    uint64_t c_rep = 0, c_aux = 0;
+    for (uint64_t f0 = 0; f0 < n; f0 += kWalkBlock) {
+      const uint64_t f = f0 + tid;
+      uint32_t op = 0;
+      int kind = 0;
+      gevws_frame in;
+      if (f < n) {
+        in = fr[f];
+        kind = disp_kind(in.hdr, policy, op);
+      }
+      const uint64_t v[2] = {(uint64_t)(kind != 0), (uint64_t)(kind == 2)};
+      uint64_t ex[2], tot[2];
+      block_excl_scan<kWalkBlock, 2>(v, ex, tot);
+      if (f < n) {
+        if (kind == 0) reply_of[f] = -1;
+        else disp_reply(in, kind, op, f, c_rep + ex[0], c_aux + ex[1], payload, aux_off, rep, reply_of,
+                        payload + aux_off);
+      }
+      c_rep += tot[0];
+      c_aux += tot[1];
+    }
+  }
+  __threadfence_block();  // the reply records before other lanes read them
+  __syncthreads();
+  // 3. encode sizes, wire offsets and the summary (k_enc_size + scan + k_enc_emit)
+  const uint64_t nr = disp_ok ? (rep_n < n ? rep_n : n) : 0;
+  uint64_t wire = 0, pl = 0;
+  for (uint64_t r0 = 0; r0 < nr; r0 += kWalkBlock) {
+    const uint64_t r = r0 + tid;
+    uint64_t w = 0, L = 0;
+    gevws_out_frame o;
+    if (r < nr) {
+      o = rep[r];
+      w = enc_hlen(o.hdr) + o.payload_len;
+      L = o.payload_len;
+    }
+    const uint64_t v[2] = {w, L};
+    uint64_t ex[2], tot[2];
+    block_excl_scan<kWalkBlock, 2>(v, ex, tot);
+    if (r < nr) {
+      const uint64_t oo = wire + ex[0];
+      out_off[r] = oo;
+      uint64_t lo, hi;
+      const uint32_t hl = enc_header(o.hdr, lo, hi);
+      s_start[r] = (int32_t)oo;
+      s_pend[r] = (int32_t)(oo + hl + o.payload_len);
+      s_hlen[r] = (uint8_t)hl;
+      s_delta[r] = o.payload_off - oo - hl;
+      s_h0[r] = lo;
+      s_h1[r] = hi;
+    }
+    wire += tot[0];
+    pl += tot[1];
+  }
+  if (tid == 0) {
+    gevws_summary sm;
+    memset(&sm, 0, sizeof(sm));
+    sm.frames = nr;
+    sm.payload_bytes = wire;
+    sm.payload_len = pl;
+    sm.status = wire > out_cap ? GEVWS_ERR_CAPACITY : GEVWS_OK;
+    s_status = (uint32_t)sm.status;
+    *esum = sm;
+  }
+  __syncthreads();
+  if (s_status != (uint32_t)GEVWS_OK || wire == 0) {  // (workgroup-uniform)
+    signal_done(done, seq);
+    return;
+  }
+  // 4. the wire image, 16 bytes per lane (the last chunk's tail zeroed inside
+  // the GEVWS_OUT_PAD slack)
+  for (uint64_t a = (uint64_t)tid * 16; a < wire; a += (uint64_t)kWalkBlock * 16) {
+    const int32_t rel = (int32_t)a;
+    uint32_t lo = 0, hi = (uint32_t)nr - 1;  // the last reply starting at or before a
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+    }
+    const u32x4 x = enc_assemble<false>(rel, a, wire, lo, (uint32_t)nr, EncWin{s_start, s_pend, s_hlen, s_delta, s_h0, s_h1},
+                                        payload, nullptr, 0);
+    __builtin_memcpy(out + a, &x, 16);
+  }
+  signal_done(done, seq);
+}
+
+constexpr int kNumEncodeVariants = 1;  // GEVWS_TUNE_ENCODE_VARIANT: 0 = k_encode
+
+}  // namespace
+
+namespace gevws_impl {
+
+int encode_variant_count() { return kNumEncodeVariants; }
+
+}  // namespace gevws_impl
+
+using namespace gevws_impl;
+
+extern "C" {
+
+static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_frames, uint64_t n,
+                       const gevws_summary* gate, const uint8_t* d_payload, uint8_t* d_out, uint64_t out_cap,
+                       uint64_t* d_out_off, gevws_summary* d_summary) {
+  if (!ctx || !d_summary || (n && (!d_frames || !d_out || !d_out_off))) return GEVWS_ERR_INVALID;
+  if (n > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  const uint64_t nblk64 = (n + (uint64_t)kWalkBlock * kEncSlabs - 1) / ((uint64_t)kWalkBlock * kEncSlabs);
+  const uint32_t nblk = (uint32_t)nblk64;
+  const uint64_t ntiles_cap = (out_cap + kTile - 1) / kTile + 1;
+  const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
+  int r = order_after_last(ctx, st);
+  if (r != GEVWS_OK) return r;
+  r = ensure_scratch(ctx, blk_bytes + ntiles_cap * sizeof(uint32_t));
+  if (r != GEVWS_OK) return r;
+  uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
+  uint32_t* tile_first = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes);
+  if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_out_off, gate);
+  k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
+  if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(n, blk, d_summary, d_out_off, tile_first, gate);
+  const uint64_t per_cu = 7;  // the window path's occupancy (k_encode)
+  uint64_t grid = (out_cap / kTile + kWinTiles - 1) / kWinTiles;
+  // (GEVWS_TUNE_UNMASK_GRID, when set, caps the encode's grid too: measurement)
+  const uint64_t gcap = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : per_cu * (uint64_t)ctx->num_cus;
+  if (grid > gcap) grid = gcap;
+  if (grid < 1) grid = 1;
+  // every frame boundary takes the window path, which needs several
+  // workgroups per CU to hide its latency (C3: 22.6 ms at 4/CU vs 36 ms at
+  // 1/CU); it runs 7 per CU (C2 -18 %, C4 -4 % against 4,
+  // profiles/r01/r01_encode_ab_lds_*.json, r01_encode_ab_occ_*.json), and
+  // batches of big frames (mean >= kBigFrameBytes) keep 4 per CU (the rest
+  // return at once)
+  const uint32_t big = grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
+  k_encode<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out,
+                                                     big);
+  GEVWS_HIP(hipGetLastError());
+  return mark_last(ctx, st);
+}
+
+int gevws_encode_batch_async(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_frames, uint64_t n,
+                             const uint8_t* d_payload, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                             gevws_summary* d_summary) {
+  return encode_impl(ctx, stream, d_frames, n, nullptr, d_payload, d_out, out_cap, d_out_off, d_summary);
+}
+
+int gevws_encode_replies_async(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_replies,
+                               uint64_t max_replies, const gevws_summary* d_dispatched, const uint8_t* d_payload,
+                               uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off, gevws_summary* d_summary) {
+  if (!d_dispatched) return GEVWS_ERR_INVALID;
+  return encode_impl(ctx, stream, d_replies, max_replies, d_dispatched, d_payload, d_out, out_cap, d_out_off,
+                     d_summary);
+}
+
+static int dispatch_impl(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t n,
+                         const gevws_summary* gate, int policy, uint8_t* d_payload, uint64_t aux_off,
+                         uint64_t aux_cap, gevws_out_frame* d_replies, int64_t* d_reply_of,
+                         gevws_summary* d_summary) {
+  if (!ctx || !d_summary || (n && (!d_frames || !d_payload || !d_replies || !d_reply_of))) return GEVWS_ERR_INVALID;
+  if (policy < GEVWS_HANDLER_NONE || policy > GEVWS_HANDLER_ECHO_TEXT) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  const uint64_t nblk64 = (n + (uint64_t)kWalkBlock * kEncSlabs - 1) / ((uint64_t)kWalkBlock * kEncSlabs);
+  if (nblk64 > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
+  const uint32_t nblk = (uint32_t)nblk64;
+  const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
+  int r = order_after_last(ctx, st);
+  if (r != GEVWS_OK) return r;
+  r = ensure_scratch(ctx, blk_bytes);
+  if (r != GEVWS_OK) return r;
+  uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
+  if (nblk) k_disp_count<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, blk, gate);
+  k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, aux_cap / kAuxSlot, d_summary);
+  if (nblk)
+    k_disp_emit<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, policy, d_payload, aux_off, blk, d_summary, d_replies,
+                                              d_reply_of, d_payload + aux_off, gate);
+  GEVWS_HIP(hipGetLastError());
+  return mark_last(ctx, st);
+}
+
+int gevws_dispatch_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t n, int policy,
+                         uint8_t* d_payload, uint64_t aux_off, uint64_t aux_cap, gevws_out_frame* d_replies,
+                         int64_t* d_reply_of, gevws_summary* d_summary) {
+  return dispatch_impl(ctx, stream, d_frames, n, nullptr, policy, d_payload, aux_off, aux_cap, d_replies,
+                       d_reply_of, d_summary);
+}
+
+int gevws_dispatch_decoded_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t max_frames,
+                                 const gevws_summary* d_decoded, int policy, uint8_t* d_payload, uint64_t aux_off,
+                                 uint64_t aux_cap, gevws_out_frame* d_replies, int64_t* d_reply_of,
+                                 gevws_summary* d_summary) {
+  if (!d_decoded) return GEVWS_ERR_INVALID;
+  return dispatch_impl(ctx, stream, d_frames, max_frames, d_decoded, policy, d_payload, aux_off, aux_cap, d_replies,
+                       d_reply_of, d_summary);
+}
+
+int gevws_handle_decoded_async(gevws_ctx* ctx, void* stream, const gevws_frame* d_frames, uint64_t max_frames,
+                               const gevws_summary* d_decoded, int policy, uint8_t* d_payload, uint64_t aux_off,
+                               uint64_t aux_cap, gevws_out_frame* d_replies, int64_t* d_reply_of,
+                               gevws_summary* d_disp_summary, uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off,
+                               gevws_summary* d_enc_summary) {
+  if (!ctx || !d_decoded || !d_disp_summary || !d_enc_summary) return GEVWS_ERR_INVALID;
+  if (max_frames > kHandleSmallFrames || out_cap > 0x7fffffffull) {  // the two-step chain
+    int r = gevws_dispatch_decoded_async(ctx, stream, d_frames, max_frames, d_decoded, policy, d_payload, aux_off,
+                                         aux_cap, d_replies, d_reply_of, d_disp_summary);
+    if (r != GEVWS_OK) return r;
+    return gevws_encode_replies_async(ctx, stream, d_replies, max_frames, d_disp_summary, d_payload, d_out, out_cap,
+                                      d_out_off, d_enc_summary);
+  }
+  if (max_frames && (!d_frames || !d_payload || !d_replies || !d_reply_of || !d_out || !d_out_off))
+    return GEVWS_ERR_INVALID;
+  if (policy < GEVWS_HANDLER_NONE || policy > GEVWS_HANDLER_ECHO_TEXT) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  hipStream_t st = pick_stream(ctx, stream);
+  int r = order_after_last(ctx, st);
+  if (r != GEVWS_OK) return r;
+  const uint32_t seq = ctx->done_flag ? ++ctx->done_seq : 0u;
+  k_handle_small<<<1, kWalkBlock, 0, st>>>(d_frames, max_frames, d_decoded, policy, d_payload, aux_off, aux_cap,
+                                           d_replies, d_reply_of, d_disp_summary, d_out, out_cap, d_out_off,
+                                           d_enc_summary, ctx->done_flag, seq);
+  GEVWS_HIP(hipGetLastError());
+  r = mark_last(ctx, st);
+  if (ctx->done_flag) ctx->last_signal = seq;
+  return r;
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+// gevws_internal.hpp -- the host side shared by the files of libgevws.so: the
+// context behind gevws_ctx (include/gevws.h), stream / scratch helpers, and
+// the launchers one file provides to another.  Nothing here is exported
+// (-fvisibility=hidden; the C ABI is declared in gevws.h only).
+#pragma once
+
+#include <vector>
+
+#include "gevws_kernels.hpp"
+
+struct gevws_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  bool timing = false;
+  struct EventSet {
+    hipEvent_t e[5];
+  };
+  std::vector<EventSet> evs;  // one set per timed call since the last gevws_ctx_timing
+  size_t evs_used = 0;
+  gevws_summary* d_sum = nullptr;  // summary slot of the synchronous entry point
+  int unmask_variant = 0;  // GEVWS_TUNE_UNMASK_VARIANT (kUnmaskVariants)
+  int unmask_grid = 0;     // 0 = auto
+  int encode_variant = 0;  // GEVWS_TUNE_ENCODE_VARIANT (kNumEncodeVariants)
+  uint64_t small_bytes = kSmallBytes;  // one-launch decode (k_decode_small) up to this many input bytes
+  uint32_t* done_flag = nullptr;  // mapped host word the one-launch kernels signal (gevws_ctx_set_completion_flag)
+  uint32_t done_seq = 0;
+  int64_t last_signal = -1;  // the value the last call's last kernel stores there, -1: none
+  // the context's history: the last multi-kernel decode's frame / payload /
+  // equal-size-run totals (written by k_walk_bases into mapped host memory)
+  // and its connection count, read once that decode has finished; it picks
+  // the split walk, the walk's speculation and the unmask's wide grid
+  uint64_t* h_stats = nullptr;
+  uint64_t* d_stats = nullptr;
+  bool stats_pending = false, stats_known = false;
+  uint64_t stats_conns = 0, prev_frames_per_conn = 0, prev_frame_bytes = 0;
+  bool prev_mixed = false;
+  uint32_t last_unmask_grid = 0;  // workgroups of the last decode's unmask launch
+  uint32_t last_ks = 1;    // lanes per connection of the last multi-kernel decode's walk
+  uint32_t split_lanes = 0;  // lanes per connection (k_walk_split); 0 = auto, 1 = off
+  uint64_t split_min_bytes = kSplitMinBytes;        // split walk: bytes per segment at least
+  uint64_t split_lanes_per_cu = kSplitLanesPerCU;   // split walk auto: lanes per CU at most
+  int walk_variant = 0;    // 0 = speculation (D = 8) unless the history is mixed, 1 = plain chain walk
+                           // (D = 0), 2 = no entry table (the record pass re-walks every chain), 3 =
+                           // the writer wave whatever the batch size
+  // Scratch is per context: calls on a different stream than the previous one
+  // first wait for it (one in-flight batch per context; use one context per
+  // stream for concurrency).
+  hipEvent_t last_done = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool has_last = false;
+  int num_cus = 256;
+  uint32_t* d_done = nullptr;  // the decode walk's finished-workgroup counter (zero between calls)
+  // split-stream decode (gevws_ctx_set_unmask_stream): the unmask on its own
+  // stream after the record pass (front_done), its grid for unmask_cus CUs
+  hipStream_t unmask_stream = nullptr;
+  int unmask_cus = 0;
+  hipEvent_t front_done = nullptr;
+};
+
+namespace gevws_impl {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+#define GEVWS_HIP(call)                                                                \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      fprintf(stderr, "[gevws] %s failed: %s\n", #call, hipGetErrorString(e_));          \
+      return GEVWS_ERR_DEVICE;                                                          \
+    }                                                                                   \
+  } while (0)
+
+// NULL = the HIP default (null) stream, as in every HIP/CUDA API; callers
+// that want the context's own stream pass gevws_ctx_stream(ctx).
+inline hipStream_t pick_stream(gevws_ctx* ctx, void* stream) {
+  (void)ctx;
+  return reinterpret_cast<hipStream_t>(stream);
+}
+
+// Orders this call after the context's previous one when the stream changes.
+inline int order_after_last(gevws_ctx* ctx, hipStream_t st) {
+  if (ctx->has_last && ctx->last_stream != st) GEVWS_HIP(hipStreamWaitEvent(st, ctx->last_done, 0));
+  return GEVWS_OK;
+}
+
+inline int mark_last(gevws_ctx* ctx, hipStream_t st) {
+  ctx->last_signal = -1;  // (the one-launch paths set it after this)
+  GEVWS_HIP(hipEventRecord(ctx->last_done, st));
+  ctx->last_stream = st;
+  ctx->has_last = true;
+  return GEVWS_OK;
+}
+
+inline int ensure_scratch(gevws_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->scratch_bytes) return GEVWS_OK;
+  if (ctx->scratch) {
+    GEVWS_HIP(hipDeviceSynchronize());
+    GEVWS_HIP(hipFree(ctx->scratch));
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+  }
+  size_t want = bytes + bytes / 4 + 4096;
+  GEVWS_HIP(hipMalloc(&ctx->scratch, want));
+  ctx->scratch_bytes = want;
+  return GEVWS_OK;
+}
+
+// ---- gevws_walk.hip: the decode up to the unmask
+// the one-launch decode of a small batch (k_decode_small)
+int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
+                 const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
+                 uint8_t* d_payload, uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary);
+// header walk, scan, bases and record pass into the context's scratch; the
+// output-tile -> frame map for the unmask in *tile_first.  ev: the timing
+// events 0..2 (walk start, walk end, scan end) or null.
+int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
+                 const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
+                 uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary, hipEvent_t* ev,
+                 uint32_t** tile_first);
+int walk_variant_count();
+const char* walk_variant_name(int i);
+
+// ---- gevws_unmask.hip
+int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const uint8_t* d_in,
+                  const gevws_frame* d_frames, const uint32_t* tile_first, const gevws_summary* d_summary,
+                  uint8_t* d_payload);
+int unmask_variant_count();
+const char* unmask_variant_name(int i);
+
+// ---- gevws_encode.hip
+int encode_variant_count();
+
+}  // namespace gevws_impl
