@@ -457,6 +457,7 @@ def main():
             engs[0].decode_async(arena, lay.arena_bytes, conns, lay.n_conns, outs[0], max_frames, cap,
                                  stream=streams[0])
             engs[0].set_timing(False)
+            engs[0].order_after_last(torch.cuda.current_stream())  # (split streams: the unmask ran elsewhere)
             best = None
             for flag in (0, 0x40000000):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
