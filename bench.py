@@ -281,6 +281,8 @@ def main():
                     help="with --inflight >= 2: run each batch's walk / scan / record pass on a stream of this many "
                          "CUs and its unmask on a stream of the others (CU masks), so batch k+1's walk overlaps "
                          "batch k's unmask (0 = one stream per slot, no CU split)")
+    ap.add_argument("--input-mem", choices=["default", "fine", "uncached"], default="default",
+                    help="measurement: the input arena's memory kind (gevws_device_alloc)")
     ap.add_argument("--dry-run", action="store_true",
                     help="N > 1 plumbing only, no GPU (launch, shard, count all-reduce over gloo); value is null")
     args = ap.parse_args()
@@ -332,8 +334,12 @@ def main():
         raise SystemExit(f"rank {rank}: no connections in this rank's share ({glob.n_conns} in the batch)")
     log(f"rank {rank}: {lay.name}: {lay.n_frames} frames, {lay.n_conns} connections, "
         f"{lay.arena_bytes / 2**30:.2f} GiB in, {lay.payload_padded / 2**30:.2f} GiB out")
-    arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
-    arena[lay.arena_bytes:] = 0
+    if args.input_mem == "default":
+        arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+        arena[lay.arena_bytes:] = 0
+    else:  # measurement: the input arena in fine-grained / uncached device memory (zeroed)
+        arena = gev_amd.DeviceArena(gpu, lay.arena_bytes + gev_amd.IN_PAD,
+                                    gev_amd.MEM_FINE if args.input_mem == "fine" else gev_amd.MEM_UNCACHED)
     desc = torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev)
     conns = torch.from_numpy(lay.conns.copy()).to(dev)
     eng.synth(arena, desc, lay.n_frames, lay.seed)
@@ -511,6 +517,7 @@ def main():
                                    f"{' by greedy LPT over stream bytes' if scaling == 'strong' else ''}; "
                                    f"{'RCCL' if dist.backend() == 'nccl' else dist.backend()} all-reduce of counts"),
                    "batches_in_flight": M,
+                   **({"input_mem": args.input_mem} if args.input_mem != "default" else {}),
                    **({"split_streams": split} if split else {}),
                    **({"emulated_shard": emulated} if emulated else {})},
         "frames_per_s": round(frames_step * args.steps / elapsed, 1),

@@ -24,7 +24,8 @@ import numpy as np
 
 from . import _abi
 from ._abi import (ERR_CAPACITY, ERR_DEVICE, ERR_HANDSHAKE, ERR_INVALID, ERR_LEN_MSB, ERR_NOT_UPGRADED,
-                   HANDSHAKE, IN_PAD, NEED_MORE, OK, PAYLOAD_ALIGN, SUMMARY_UNORDERED, TILE, Header)
+                   HANDSHAKE, IN_PAD, MEM_DEFAULT, MEM_FINE, MEM_UNCACHED, NEED_MORE, OK, PAYLOAD_ALIGN,
+                   SUMMARY_UNORDERED, TILE, Header)
 
 lib = _abi.load()
 
@@ -682,6 +683,36 @@ class Upgrader:
         data = ctypes.string_at(out, n.value) if n.value else b""
         err = None if st == OK else HandshakeError(info.error, info.reason, info.http_code)
         return data, info, err
+
+
+class DeviceArena:
+    """gevws_device_alloc: zeroed device memory of a chosen kind (default,
+    fine-grained or uncached); `data_ptr()` / `at(off)` for the launch
+    wrappers (measurement helper: where the input arena lives)."""
+
+    def __init__(self, device: int, nbytes: int, kind: int = 0):
+        p = ctypes.c_void_p()
+        st = lib.gevws_device_alloc(device, nbytes, kind, ctypes.byref(p))
+        if st != OK:
+            raise RuntimeError(f"gevws_device_alloc({nbytes}, kind {kind}): {status_string(st)}")
+        self.device, self.nbytes, self.kind, self._p = device, nbytes, kind, p.value
+
+    def data_ptr(self) -> int:
+        return self._p
+
+    def at(self, offset: int = 0) -> _DevAddr:
+        if not 0 <= offset <= self.nbytes:
+            raise ValueError(f"DeviceArena.at({offset}): outside {self.nbytes} bytes")
+        return _DevAddr(self._p + offset)
+
+    def close(self) -> None:
+        if getattr(self, "_p", None):
+            lib.gevws_device_free(self.device, self._p)
+            self._p = None
+
+    def __del__(self, _free=lib.gevws_device_free):
+        if getattr(self, "_p", None):
+            _free(self.device, self._p)
 
 
 def cu_split_masks(num_cus: int, front_cus: int, xcds: int = 8) -> Tuple[List[int], List[int]]:

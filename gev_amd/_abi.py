@@ -52,6 +52,7 @@ TUNE_SPLIT_MIN_BYTES = 13  # split walk: bytes per segment at least (default 16 
 TUNE_SPLIT_LANES_PER_CU = 14  # split walk auto: lanes per CU at most (default 512)
 
 IN_PAD = 64
+MEM_DEFAULT, MEM_FINE, MEM_UNCACHED = 0, 1, 2  # gevws_device_alloc kinds
 SUMMARY_UNORDERED = 1  # summary.flags: connection table not in increasing input order
 PAYLOAD_ALIGN = 16
 TILE = 4096
@@ -222,6 +223,8 @@ SIGNATURES = {
     "gevws_copy_async": (ctypes.c_int, [P, P, P, P, ctypes.c_uint64, ctypes.c_uint32]),
     "gevws_pinned_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(P), ctypes.POINTER(P)]),
     "gevws_pinned_free": (ctypes.c_int, [P]),
+    "gevws_device_alloc": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(P)]),
+    "gevws_device_free": (ctypes.c_int, [ctypes.c_int, P]),
     "gevws_upgrader_new": (P, []),
     "gevws_upgrader_free": (None, [P]),
     "gevws_upgrader_set_header": (None, [P, P, ctypes.c_uint64]),

@@ -406,6 +406,32 @@ int gevws_pinned_alloc(uint64_t bytes, void** host_ptr, void** dev_ptr) {
   return GEVWS_OK;
 }
 
+int gevws_device_alloc(int device, uint64_t bytes, int kind, void** ptr) {
+  if (!ptr || bytes == 0 || device < 0 || device >= gevws_device_count()) return GEVWS_ERR_INVALID;
+  if (kind < GEVWS_MEM_DEFAULT || kind > GEVWS_MEM_UNCACHED) return GEVWS_ERR_INVALID;
+  *ptr = nullptr;
+  DeviceGuard g(device);
+  void* p = nullptr;
+  if (kind == GEVWS_MEM_DEFAULT) {
+    GEVWS_HIP(hipMalloc(&p, bytes));
+  } else {
+    GEVWS_HIP(hipExtMallocWithFlags(&p, bytes, kind == GEVWS_MEM_FINE ? hipDeviceMallocFinegrained
+                                                                     : hipDeviceMallocUncached));
+  }
+  if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    return GEVWS_ERR_DEVICE;
+  }
+  *ptr = p;
+  return GEVWS_OK;
+}
+
+int gevws_device_free(int device, void* ptr) {
+  if (!ptr) return GEVWS_OK;
+  DeviceGuard g(device);
+  return hipFree(ptr) == hipSuccess ? GEVWS_OK : GEVWS_ERR_DEVICE;
+}
+
 int gevws_pinned_free(void* host_ptr) {
   if (!host_ptr) return GEVWS_OK;
   return hipHostFree(host_ptr) == hipSuccess ? GEVWS_OK : GEVWS_ERR_DEVICE;

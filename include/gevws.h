@@ -340,6 +340,18 @@ int gevws_copy_async(gevws_ctx *ctx, void *stream, uint8_t *d_dst, const uint8_t
 int gevws_pinned_alloc(uint64_t bytes, void **host_ptr, void **dev_ptr);
 int gevws_pinned_free(void *host_ptr);
 
+/* Measurement helper, not on the reference path: `bytes` of device memory on
+ * `device`, zeroed, of one of three kinds -- GEVWS_MEM_DEFAULT (hipMalloc:
+ * coarse-grained, cached in L2), GEVWS_MEM_FINE (fine-grained) or
+ * GEVWS_MEM_UNCACHED (hipDeviceMallocUncached: accesses bypass L2, so a
+ * 16-byte header read need not fetch a whole 128-byte line).  An input arena
+ * placed in it is decoded like any other.  Free with gevws_device_free. */
+#define GEVWS_MEM_DEFAULT 0
+#define GEVWS_MEM_FINE 1
+#define GEVWS_MEM_UNCACHED 2
+int gevws_device_alloc(int device, uint64_t bytes, int kind, void **ptr);
+int gevws_device_free(int device, void *ptr);
+
 /* ws.Cipher(payload, mask, offset), plugins/websocket/ws/cipher.go:14-53, on a
  * device buffer in place: p[i] ^= mask[(offset+i) % 4]. */
 int gevws_cipher_async(gevws_ctx *ctx, void *stream, uint8_t *d_p, uint64_t n,

@@ -88,3 +88,33 @@ def test_two_batches_in_flight_on_masked_streams():
         assert int(s["frames"]) == lay.n_frames and int(s["payload_len"]) == lay.payload_len
         e.set_unmask_stream(None)
         e.close()
+
+
+@pytest.mark.parametrize("kind", ["fine", "uncached"])
+def test_decode_from_fine_and_uncached_input(kind):
+    """The input arena in fine-grained or uncached device memory
+    (gevws_device_alloc, the bench's --input-mem): the same records and
+    payload bytes as from default memory, and every byte the generator's."""
+    from gev_amd import workloads as w
+    dev = torch.device("cuda", 0)
+    eng = gev_amd.Engine(0)
+    lay = w.config_c4(total_payload=64 << 20, n_conns=512, seed=9)
+    desc = torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev)
+    conns = torch.from_numpy(lay.conns.copy()).to(dev)
+    base = torch.zeros(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    arena = gev_amd.DeviceArena(0, lay.arena_bytes + gev_amd.IN_PAD,
+                                gev_amd.MEM_FINE if kind == "fine" else gev_amd.MEM_UNCACHED)
+    outs = []
+    for a in (base, arena):
+        eng.synth(a, desc, lay.n_frames, lay.seed)
+        out = eng.alloc_batch(lay.n_conns, lay.n_frames, lay.payload_padded)
+        eng.decode_async(a, lay.arena_bytes, conns, lay.n_conns, out, lay.n_frames, lay.payload_padded)
+        mism = torch.zeros(1, dtype=torch.int64, device=dev)
+        eng.verify(desc, lay.n_frames, lay.seed, out, mism)
+        torch.cuda.synchronize()
+        assert int(mism.item()) == 0
+        outs.append(out)
+    assert torch.equal(outs[0].frames, outs[1].frames)
+    assert torch.equal(outs[0].payload[:lay.payload_padded], outs[1].payload[:lay.payload_padded])
+    arena.close()
+    eng.close()
