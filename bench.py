@@ -456,7 +456,7 @@ def main():
     # the same clock / thermal state as the unmask it is compared with
     interleaved = None
     if args.copy_interleave > 0:
-        n_copy = lay.payload_padded // 16 * 16
+        n_copy = min(lay.payload_padded, lay.arena_bytes) // 16 * 16
         ums, cms = [], []
         for _ in range(args.copy_interleave):
             engs[0].set_timing(True)
