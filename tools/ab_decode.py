@@ -51,6 +51,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None, help="also append the report as one JSON line to this file")
+    ap.add_argument("--unverified", default="",
+                    help="comma-separated configuration names that are timed but not verified (measurement-only "
+                         "upper bounds whose bytes are wrong by construction); reported with verified: false")
     args = ap.parse_args()
 
     import numpy as np
@@ -95,7 +98,10 @@ def main():
             eng.decode_async(arena, lay.arena_bytes, conns, lay.n_conns, out, lay.n_frames, lay.payload_padded)
 
         mism = torch.zeros(1, dtype=torch.int64, device=dev)
+        unverified = set(filter(None, args.unverified.split(",")))
         for cname, d in cfgs:
+            if cname in unverified:
+                continue
             apply(d)
             for _ in range(2):  # the second decode sees the first one's history (auto choices)
                 out.payload.zero_()
@@ -106,7 +112,7 @@ def main():
             torch.cuda.synchronize()
             s = out.summary_host()
             assert int(mism.item()) == 0 and int(s["frames"]) == lay.n_frames, (wspec, cname, int(mism.item()))
-        print(f"[ab] {wspec}: every configuration bit-exact", file=sys.stderr, flush=True)
+        print(f"[ab] {wspec}: every verified configuration bit-exact", file=sys.stderr, flush=True)
         res = {c: [] for c, _ in cfgs}
         info = {}
         for r in range(args.rounds):
@@ -132,7 +138,8 @@ def main():
             wrep["configs"].append({"config": cname, "tuning": d, "walk_ms": round(med[0], 4),
                                     "scan_ms": round(med[1], 4), "emit_ms": round(med[2], 4),
                                     "unmask_ms": round(med[3], 4), "step_ms": round(step, 4),
-                                    "walk_ms_all": [round(row[0], 4) for row in rows], **info[cname]})
+                                    "walk_ms_all": [round(row[0], 4) for row in rows], "verified": cname not in unverified,
+                                    **info[cname]})
             print(f"[ab] {wspec} {cname}: walk {med[0]:.4f} emit {med[2]:.4f} unmask {med[3]:.4f} "
                   f"step {step:.4f} {info[cname]}", file=sys.stderr, flush=True)
         report["workloads"].append(wrep)
