@@ -53,7 +53,13 @@ __device__ __forceinline__ u32x4 copy_ld(const uint8_t* p) {
   else return ld16u(p);
 }
 
-template <int U, bool NTL, bool WSPAN>
+template <bool PS>
+__device__ __forceinline__ void copy_st(uint8_t* p, u32x4 x) {
+  if constexpr (PS) *reinterpret_cast<u32x4*>(p) = x;  // (p may be misaligned: gfx950 unaligned access mode)
+  else st16_nt(p, x);
+}
+
+template <int U, bool NTL, bool WSPAN, bool PS = false>
 __global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __restrict__ src,
                                                               uint8_t* __restrict__ dst, uint64_t n) {
   const uint64_t ntiles = n / kTile;
@@ -69,16 +75,16 @@ __global__ __launch_bounds__(kUnmaskBlock) void k_copy_stream(const uint8_t* __r
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = copy_ld<NTL>(src + base + u * kStride);
 #pragma unroll
-    for (int u = 0; u < U; ++u) st16_nt(dst + base + u * kStride, v[u]);
+    for (int u = 0; u < U; ++u) copy_st<PS>(dst + base + u * kStride, v[u]);
   }
   for (; t < tend; ++t) {
     const uint64_t base = t * kTile + lane_off;
-    st16_nt(dst + base, copy_ld<NTL>(src + base));
+    copy_st<PS>(dst + base, copy_ld<NTL>(src + base));
   }
   // bytes past the last whole tile: 16 per lane, workgroup 0
   const uint64_t tail = ntiles * kTile;
   if (blockIdx.x == 0)
-    for (uint64_t p = tail + lane_off; p < n; p += kTile) st16_nt(dst + p, copy_ld<NTL>(src + p));
+    for (uint64_t p = tail + lane_off; p < n; p += kTile) copy_st<PS>(dst + p, copy_ld<NTL>(src + p));
 }
 
 // The unmask = ws.Cipher (cipher.go:14-53) of every frame's payload into its
@@ -659,17 +665,21 @@ extern "C" {
 int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t* d_src, uint64_t n,
                      uint32_t grid) {
   if (!ctx || (n && (!d_dst || !d_src))) return GEVWS_ERR_INVALID;
-  if ((n & 15) || (reinterpret_cast<uint64_t>(d_dst) & 15)) return GEVWS_ERR_INVALID;
+  // bit 30: plain loads (else non-temporal); bit 29: the unmask's
+  // wave-contiguous spans (else tile-strided lanes); bit 28: plain stores to
+  // a destination of any alignment (else non-temporal, 16-aligned)
+  // bit 27: non-temporal stores to a destination of any alignment
+  const bool plain = grid & 0x40000000u, wspan = grid & 0x20000000u, pstore = grid & 0x10000000u,
+             anyal = pstore || (grid & 0x08000000u);
+  if ((n & 15) || (!anyal && (reinterpret_cast<uint64_t>(d_dst) & 15))) return GEVWS_ERR_INVALID;
   if (n == 0) return GEVWS_OK;
   DeviceGuard g(ctx->device);
   hipStream_t st = pick_stream(ctx, stream);
-  // bit 30: plain loads (else non-temporal); bit 29: the unmask's
-  // wave-contiguous spans (else tile-strided lanes)
-  const bool plain = grid & 0x40000000u, wspan = grid & 0x20000000u;
-  grid &= 0x1fffffffu;
+  grid &= 0x07ffffffu;
   if (grid == 0) grid = (uint32_t)ctx->num_cus;
-  auto k = wspan ? (plain ? k_copy_stream<16, false, true> : k_copy_stream<16, true, true>)
-                 : (plain ? k_copy_stream<16, false, false> : k_copy_stream<16, true, false>);
+  auto k = pstore ? (plain ? k_copy_stream<16, false, false, true> : k_copy_stream<16, true, false, true>)
+           : wspan ? (plain ? k_copy_stream<16, false, true> : k_copy_stream<16, true, true>)
+                   : (plain ? k_copy_stream<16, false, false> : k_copy_stream<16, true, false>);
   k<<<grid, kUnmaskBlock, 0, st>>>(d_src, d_dst, n);
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;

@@ -327,7 +327,11 @@ int gevws_handle_decoded_async(gevws_ctx *ctx, void *stream, const gevws_frame *
  * CU (the unmask kernel's grid for large frames), each a contiguous run of
  * tiles; grid | 0x40000000 uses plain loads instead of the non-temporal ones the
  * unmask kernel's streaming path uses; grid | 0x20000000 copies in the
- * unmask's wave layout (each wave a contiguous 16 KiB span per step). */
+ * unmask's wave layout (each wave a contiguous 16 KiB span per step);
+ * grid | 0x10000000 stores with plain 16-byte stores and then accepts a
+ * d_dst of any alignment (the access pattern of an encode that scatters
+ * aligned payload chunks to their wire positions); grid | 0x08000000 the
+ * same with non-temporal stores. */
 int gevws_copy_async(gevws_ctx *ctx, void *stream, uint8_t *d_dst, const uint8_t *d_src, uint64_t n,
                      uint32_t grid);
 

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="0", help="encode variants to A/B, e.g. 0,1 (interleaved rounds)")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--unverified", default="", help="variants timed without the equal-bytes check "
+                                                      "(measurement-only upper bounds)")
     ap.add_argument("--grids", default="0", help="encode grid caps to A/B (GEVWS_TUNE_UNMASK_GRID; 0 = the default)")
     args = ap.parse_args()
     import numpy as np
@@ -68,7 +70,10 @@ def main():
     if len(variants) > 1:
         # every variant's whole wire equals the first one's
         ref_wire = wire.clone()
+        unverified = {int(x) for x in filter(None, args.unverified.split(","))}
         for v in variants[1:]:
+            if v in unverified:
+                continue
             eng.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, v)
             eng.encode_async(d_rep, lay.n_frames, out.payload, wire, wire_total, off, summ)
             torch.cuda.synchronize()
