@@ -382,6 +382,8 @@ int gevws_decode_batch(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64
   int r = gevws_decode_batch_async(ctx, stream, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames,
                                    d_payload, payload_cap, d_conn_out, d_sum);
   if (r == GEVWS_OK) {
+    r = order_after_last(ctx, st);  // a split-stream decode ends on the unmask stream
+    if (r != GEVWS_OK) return r;
     GEVWS_HIP(hipMemcpyAsync(h_summary, d_sum, sizeof(gevws_summary), hipMemcpyDeviceToHost, st));
     GEVWS_HIP(hipStreamSynchronize(st));
     r = h_summary->status;

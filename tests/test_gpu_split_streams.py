@@ -3,6 +3,8 @@ record pass on one stream, the unmask on another, two batches in flight on
 CU-masked streams -- the server loop of connection.go:208-218 with batch k+1's
 walk beside batch k's unmask.  Results must be the oracle's, bit-exact, and
 every in-flight slot must verify."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -118,3 +120,73 @@ def test_decode_from_fine_and_uncached_input(kind):
     assert torch.equal(outs[0].payload[:lay.payload_padded], outs[1].payload[:lay.payload_padded])
     arena.close()
     eng.close()
+
+
+def test_sync_decode_waits_for_the_unmask_stream(engine):
+    """gevws_decode_batch (the synchronous form) with an unmask stream set
+    returns only after the unmask: checked on a third stream with no device
+    synchronisation in between, every payload byte is the generator's."""
+    from gev_amd import workloads as w
+    front, back, _ = _masked_streams(engine.device)
+    dev = torch.device("cuda", engine.device)
+    lay = w.config_c4(total_payload=256 << 20, n_conns=2048, seed=11)
+    arena = torch.zeros(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    desc = torch.from_numpy(lay.desc.view(np.uint8).copy()).to(dev)
+    conns = torch.from_numpy(lay.conns.copy()).to(dev)
+    engine.synth(arena, desc, lay.n_frames, lay.seed)
+    out = engine.alloc_batch(lay.n_conns, lay.n_frames, lay.payload_padded)
+    mism = torch.zeros(1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    from gev_amd import _abi
+    h_sum = _abi.Summary()
+    engine.set_unmask_stream(back)
+    try:
+        st = gev_amd.lib.gevws_decode_batch(engine._ctx, front.cuda_stream, arena.data_ptr(), lay.arena_bytes,
+                                            conns.data_ptr(), lay.n_conns, out.frames.data_ptr(), lay.n_frames,
+                                            out.payload.data_ptr(), lay.payload_padded, out.conn_out.data_ptr(),
+                                            ctypes.byref(h_sum))
+        assert st == gev_amd.OK
+        assert int(h_sum.frames) == lay.n_frames
+        s = torch.cuda.Stream(dev)
+        engine.verify(desc, lay.n_frames, lay.seed, out, mism, stream=s)
+        s.synchronize()
+        assert int(mism.item()) == 0
+    finally:
+        engine.set_unmask_stream(None)
+
+
+@pytest.mark.parametrize("zero_copy_max", [0, 1 << 30])
+def test_protocol_pass_on_a_context_with_an_unmask_stream(engine, zero_copy_max):
+    """The host protocol's multi-kernel pass (more than 256 connections) on a
+    context whose decode ends on an unmask stream: its stream waits for the
+    unmask, so the delivered payloads are the oracle's."""
+    from oracle import ws_oracle as wo
+    front, back, _ = _masked_streams(engine.device)
+    rng = np.random.default_rng(31)
+    streams = []
+    for _ in range(300):
+        s = b""
+        for _ in range(int(rng.integers(1, 6))):
+            L = int(rng.integers(0, 3000))
+            s += wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), 2, True, 0, True,
+                                 bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+        streams.append(s)
+    engine.set_unmask_stream(back)
+    try:
+        proto = gev_amd.Protocol(engine)
+        proto.set_zero_copy_max(zero_copy_max)
+        conns = [gev_amd.Connection() for _ in streams]
+        rings = []
+        for s in streams:
+            r = gev_amd.RingBuffer(64)
+            r.write(s)
+            rings.append(r)
+        n = proto.unpacket_batch(conns, rings)
+        assert n == sum(len(wo.decode_stream(s).frames) for s in streams)
+        for c, r, s in zip(conns, rings, streams):
+            for fr in wo.decode_stream(s).frames:
+                h, data = proto.unpacket(c, r)
+                assert h is not None and h.length == fr.header.length
+                assert data == fr.payload
+    finally:
+        engine.set_unmask_stream(None)
