@@ -192,6 +192,7 @@ class Engine:
         st = lib.gevws_ctx_set_unmask_stream(self._ctx, None if stream is None else getattr(stream, "cuda_stream", stream))
         if st != OK:
             raise RuntimeError(f"gevws_ctx_set_unmask_stream: {status_string(st)}")
+        self._unmask_stream = stream  # kept alive while the context may launch on it
 
     def order_after_last(self, stream=None) -> None:
         """Make `stream` (default: torch's current stream) wait for this

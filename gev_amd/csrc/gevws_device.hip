@@ -174,6 +174,9 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (!ctx) return;
   DeviceGuard g(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  // the last call may have ended on another stream (a caller's, the unmask
+  // stream): its kernels still read the scratch freed below
+  if (ctx->has_last && ctx->last_done) (void)hipEventSynchronize(ctx->last_done);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->d_sum) (void)hipFree(ctx->d_sum);
   if (ctx->d_done) (void)hipFree(ctx->d_done);
