@@ -14,6 +14,18 @@ from tests._helpers import gpu_decode, host_result, pack_streams, random_stream
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=[0, 1], ids=["k_encode", "k_encode5"])
+def enc_variant(request, engine):
+    """Every encode kernel (GEVWS_TUNE_ENCODE_VARIANT): 0 = 4-tile windows at 7
+    workgroups per CU, 1 = 8-tile pipelined windows with a chunk map at 4."""
+    try:
+        engine.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, request.param)
+    except RuntimeError:
+        pytest.skip("no such encode variant")
+    yield request.param
+    engine.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, 0)
+
+
 def _dev(engine):
     import torch
     return torch.device("cuda", engine.device)
@@ -39,7 +51,7 @@ def _encode_check(engine, fr: np.ndarray, payload: np.ndarray, tag=""):
     return got
 
 
-def test_encode_golden(engine, golden):
+def test_encode_golden(engine, golden, enc_variant):
     g = golden["encode"]
     offs = np.concatenate([[0], np.cumsum(g["payload_len"])[:-1]]).astype(np.uint64)
     fr = _records(g["hdr"], offs, g["payload_len"])
@@ -47,7 +59,7 @@ def test_encode_golden(engine, golden):
     assert np.array_equal(got, g["wire"])
 
 
-def test_encode_random_and_tiny_frames(engine):
+def test_encode_random_and_tiny_frames(engine, enc_variant):
     """Random batches: payloads out of frame order, every header form, RSV /
     opcode bytes outside the spec, lengths that disagree with the payload
     (Go's byte arithmetic), 1 to 5 000 frames, up to 200 KB each: aligned-load
@@ -85,7 +97,7 @@ def _uniform_frames(wire_len: int, n: int, rng):
     return _records(hd, offs, np.full(n, L)), payload
 
 
-def test_encode_window_queue_at_capacity(engine):
+def test_encode_window_queue_at_capacity(engine, enc_variant):
     """Windows whose boundary queues are as full as they get: 1 024 frames
     of 16 wire bytes in one 4-tile window (every chunk holds a header, so the
     workgroup queue takes all 1 024 chunks -- as single chunks or as 256
@@ -97,7 +109,10 @@ def test_encode_window_queue_at_capacity(engine):
     capacity and for groups cut by the batch's end (sentinel slots)."""
     rng = np.random.default_rng(1234)
     for wl, n in [(16, 1024), (16, 1025), (32, 512), (32, 513), (17, 963), (24, 682), (33, 1000),
-                  (16, 1024 * 3), (32, 512 * 5)]:
+                  (16, 1024 * 3), (32, 512 * 5),
+                  # k_encode5's 8-tile windows: 1 024 frames of 32 B fill its table, 33 / 40 / 64 B
+                  # put a boundary in every 64-byte group (its whole 2 048-chunk queue), 16 B overflow
+                  (32, 1024), (32, 1025), (33, 2000), (40, 1700), (64, 1100), (16, 2048 * 2)]:
         fr, pay = _uniform_frames(wl, n, rng)
         _encode_check(engine, fr, pay, f"{wl}B x {n}")
     lens = np.concatenate([rng.integers(0, 4, 200), [20000], rng.integers(0, 14, 700), [9000],
@@ -116,7 +131,7 @@ def test_encode_empty_batch(engine):
     assert wire.numel() == 0 and off.size == 0
 
 
-def test_echo_round_trip_on_device(engine):
+def test_echo_round_trip_on_device(engine, enc_variant):
     """Client frames (masked) -> device decode -> server replies
     NewBinaryFrame(payload) whose payloads are the decoded arena slots -> device
     encode -> device decode of the reply stream: the same payload bytes."""
@@ -149,7 +164,7 @@ def test_echo_round_trip_on_device(engine):
     assert np.array_equal(back["payload"], got["payload"])  # same 16-byte-aligned arena layout
 
 
-def test_echo_round_trip_c2_full_size(engine):
+def test_echo_round_trip_c2_full_size(engine, enc_variant):
     """Full C2 batch (262 144 x 4 KiB): decode, encode the binary replies,
     decode the reply stream, compare the payload arenas on the device."""
     import torch
