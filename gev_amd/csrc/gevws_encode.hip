@@ -1179,7 +1179,13 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
   signal_done(done, seq);
 }
 
-constexpr int kNumEncodeVariants = 2;  // GEVWS_TUNE_ENCODE_VARIANT: 0 = k_encode, 1 = k_encode5
+// GEVWS_TUNE_ENCODE_VARIANT: 0 = auto (k_encode5 when the caller's capacity
+// per frame is at least kEnc5MinMeanBytes, else k_encode), 1 = k_encode5,
+// 2 = k_encode.  Interleaved (profiles/r04/r04_encode5_ab.jsonl,
+// r04_encode5_c1_ab.jsonl): k_encode5 C2 -5 %, C3 -2..-4 %, C5 -1 %, C4 equal,
+// C1-shaped 128-byte frames +10 %.
+constexpr int kNumEncodeVariants = 3;
+constexpr uint64_t kEnc5MinMeanBytes = 1024;
 
 }  // namespace
 
@@ -1213,7 +1219,8 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_out_off, gate);
   k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
   if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(n, blk, d_summary, d_out_off, tile_first, gate);
-  const bool v5 = ctx->encode_variant == 1;
+  const bool v5 = ctx->encode_variant == 1 ||
+                  (ctx->encode_variant == 0 && n && out_cap / n >= kEnc5MinMeanBytes);
   const uint64_t per_cu = v5 ? 4 : 7;  // the window path's occupancy (k_encode5 / k_encode)
   uint64_t grid = (out_cap / kTile + (v5 ? 8 : kWinTiles) - 1) / (v5 ? 8 : kWinTiles);
   // (GEVWS_TUNE_UNMASK_GRID, when set, caps the encode's grid too: measurement)

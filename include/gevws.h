@@ -158,7 +158,9 @@ int gevws_stream_cu_count(int device, void *stream);
  * a chunk -> frame map for mixed sizes; 1 = v5 for every batch),
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto; when set it caps the
  * encode's grid too), GEVWS_TUNE_ENCODE_VARIANT the encode kernel (0 = the
- * default; the only one at present), GEVWS_TUNE_WALK_VARIANT the header walk (0 = the
+ * default: 8-tile pipelined windows with a chunk map when out_cap / n >= 1 024
+ * bytes, else 4-tile windows at seven workgroups per CU; 1 = always the
+ * former, 2 = always the latter), GEVWS_TUNE_WALK_VARIANT the header walk (0 = the
  * default choice per batch; 1 = plain chain walk without the uniform-stream
  * speculation; 2 = no per-frame entries, the record pass re-walks every
  * chain; 3 = the entries through the writer wave whatever the batch size),

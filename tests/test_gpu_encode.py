@@ -14,10 +14,11 @@ from tests._helpers import gpu_decode, host_result, pack_streams, random_stream
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 1], ids=["k_encode", "k_encode5"])
+@pytest.fixture(params=[0, 1, 2], ids=["auto", "k_encode5", "k_encode"])
 def enc_variant(request, engine):
-    """Every encode kernel (GEVWS_TUNE_ENCODE_VARIANT): 0 = 4-tile windows at 7
-    workgroups per CU, 1 = 8-tile pipelined windows with a chunk map at 4."""
+    """Every encode kernel (GEVWS_TUNE_ENCODE_VARIANT): 0 = the per-batch
+    choice, 1 = 8-tile pipelined windows with a chunk map at 4 workgroups per
+    CU, 2 = 4-tile windows at 7."""
     try:
         engine.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, request.param)
     except RuntimeError:
