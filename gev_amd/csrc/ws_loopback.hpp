@@ -73,6 +73,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <memory>
 #include <chrono>
 #include <deque>
 #include <mutex>
@@ -159,6 +160,7 @@ struct ServerConn {
   int poisoned = 0;
   std::vector<uint8_t> queued;  // wsserver: c.Send(PackData(...)) output, sent after the loop iteration
   bool shut = false;            // wsserver: ShutdownWrite done (a close was answered)
+  int half = 0;                 // split passes: which of the loop's two decoders owns it
 };
 
 // Decoder concept:
@@ -174,6 +176,20 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
   Decoder dec(device);
   const bool wss = g_cfg.mode != kModeEcho;
   if (wss) dec.set_handler(GEVWS_HANDLER_ECHO_TEXT);  // wsExample.OnMessage returns (MessageText, data)
+  // GEVWS_LB_SPLIT=K (a pipelined decoder): an iteration with at least K
+  // readable upgraded connections makes TWO device passes, each on its own
+  // decoder (connections alternate between them at accept): the first half's
+  // pass runs while the second half's sockets are read, the second half's
+  // while the first half's echoes are written -- every echo still goes out
+  // in the iteration that read its frame.
+  const char* se = getenv("GEVWS_LB_SPLIT");
+  const uint32_t split_min = Decoder::kPipelined && se ? (uint32_t)strtoul(se, nullptr, 10) : 0;
+  std::unique_ptr<Decoder> dec2;
+  if (split_min) {
+    dec2.reset(new Decoder(device));
+    if (wss) dec2->set_handler(GEVWS_HANDLER_ECHO_TEXT);
+  }
+  uint32_t accepted = 0;
   std::mt19937_64 route(g_cfg.seed * 1000003u + (unsigned)index);  // wsserver_test.go:47: rand.Int() % 2
   int ls = socket(AF_INET, SOCK_STREAM, 0);
   int one = 1;
@@ -211,7 +227,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
   bool pending = false;
   // handlerProtocol for one connection: UnPacket until (nil, nil), echo
   std::vector<ServerConn*> queued_conns;
-  auto handle = [&](ServerConn* s, double& t_dec) {
+  auto handle_with = [&](Decoder& dec, ServerConn* s, double& t_dec) {
     s->out.clear();
     bool shut = false;
     for (;;) {
@@ -284,6 +300,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
     }
     queued_conns.clear();
   };
+  auto handle = [&](ServerConn* s, double& t_dec) { handle_with(dec, s, t_dec); };
   // the pass in flight, ended and its frames handed out (also before a
   // connection it holds is closed: the protocol writes to its rings' owners)
   auto finish = [&](double& t_dec) {
@@ -299,17 +316,48 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
     for (ServerConn* s : inflight) handle(s, t_dec);
   };
   double t_close = 0;
+  std::vector<int> deferred;                  // split: the second half's readable fds
+  std::vector<ServerConn*> readable2, upgraded2;
   while (!g_stop.load(std::memory_order_relaxed)) {
     const int n = epoll_wait(ep, evs.data(), (int)evs.size(), pending ? 0 : 5);
     readable.clear();
+    deferred.clear();
+    // one read(2) per readable connection (handleRead), its bytes into the ring
+    auto read_conn = [&](int fd, std::vector<ServerConn*>& into) {
+      auto it = conns.find(fd);
+      if (it == conns.end()) return;
+      const ssize_t k = ::read(fd, rbuf.data(), rbuf.size());
+      if (k <= 0) {
+        if (k < 0 && (errno == EAGAIN || errno == EINTR)) return;
+        finish(t_close);
+        flush_queued();
+        epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
+        close(fd);
+        gevws_conn_free(it->second.c);
+        gevws_ring_free(it->second.r);
+        conns.erase(it);
+        g_live.fetch_sub(1);  // OnClose
+        return;
+      }
+      gevws_ring_write(it->second.r, rbuf.data(), (uint64_t)k);
+      into.push_back(&it->second);
+    };
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
+      if (fd != ls && split_min) {
+        auto it = conns.find(fd);
+        if (it != conns.end() && it->second.half == 1) {  // read after the first half's pass is launched
+          deferred.push_back(fd);
+          continue;
+        }
+      }
       if (fd == ls) {
         for (;;) {
           int cfd = accept4(ls, nullptr, nullptr, SOCK_NONBLOCK);
           if (cfd < 0) break;
           setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
           ServerConn sc{cfd, gevws_conn_new(), gevws_ring_new(4096), {}, {}, 0};  // DefaultBufferSize
+          sc.half = split_min ? (int)(accepted++ & 1u) : 0;
           gevws_conn_set_upgraded(sc.c, 0);
           conns.emplace(cfd, std::move(sc));
           g_live.fetch_add(1);  // OnConnect
@@ -320,23 +368,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
         }
         continue;
       }
-      auto it = conns.find(fd);
-      if (it == conns.end()) continue;
-      const ssize_t k = ::read(fd, rbuf.data(), rbuf.size());  // one read per event (handleRead)
-      if (k <= 0) {
-        if (k < 0 && (errno == EAGAIN || errno == EINTR)) continue;
-        finish(t_close);
-        flush_queued();
-        epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
-        close(fd);
-        gevws_conn_free(it->second.c);
-        gevws_ring_free(it->second.r);
-        conns.erase(it);
-        g_live.fetch_sub(1);  // OnClose
-        continue;
-      }
-      gevws_ring_write(it->second.r, rbuf.data(), (uint64_t)k);
-      readable.push_back(&it->second);
+      read_conn(fd, readable);
     }
     // decode time of the iteration: the pass plus the UnPacket calls (the
     // device decoder's UnPacket only pops queued frames; the CPU decoder's
@@ -344,6 +376,48 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
     double t_dec = t_close;
     t_close = 0;
     finish(t_dec);  // the pass begun last iteration: its frames go out now
+    if (split_min && readable.size() + deferred.size() >= split_min) {
+      // two passes: the first half's runs while the second half is read, the
+      // second half's while the first half's echoes are written
+      auto begin_half = [&](Decoder& d, std::vector<ServerConn*>& rd, std::vector<ServerConn*>& up) -> bool {
+        up.clear();
+        for (ServerConn* s : rd)
+          if (gevws_conn_upgraded(s->c)) up.push_back(s);
+        if (up.empty()) return false;
+        const double td = now_s();
+        const int64_t f = d.begin(up.data(), (uint32_t)up.size());
+        t_dec += now_s() - td;
+        if (f < 0) {
+          fprintf(stderr, "ws_loopback: decoder pass %s\n", gevws_status_string((int)f));
+          exit(3);
+        }
+        g_batches.fetch_add(1, std::memory_order_relaxed);
+        g_batch_conns.fetch_add(up.size(), std::memory_order_relaxed);
+        return true;
+      };
+      auto end_half = [&](Decoder& d, bool began, std::vector<ServerConn*>& rd) {
+        if (began) {
+          const double td = now_s();
+          const int64_t f = d.end();
+          t_dec += now_s() - td;
+          if (f < 0) {
+            fprintf(stderr, "ws_loopback: decoder pass %s\n", gevws_status_string((int)f));
+            exit(3);
+          }
+        }
+        for (ServerConn* s : rd) handle_with(d, s, t_dec);  // (handshakes too)
+      };
+      const bool b1 = begin_half(dec, readable, upgraded);
+      readable2.clear();
+      for (int fd : deferred) read_conn(fd, readable2);
+      const bool b2 = begin_half(*dec2, readable2, upgraded2);
+      end_half(dec, b1, readable);
+      end_half(*dec2, b2, readable2);
+      flush_queued();
+      g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
+      continue;
+    }
+    for (int fd : deferred) read_conn(fd, readable);  // (split on, a small iteration: one pass)
     if (readable.empty()) {
       flush_queued();
       g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
@@ -376,6 +450,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
     g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
   }
   if (pending) (void)dec.end();
+  dec2.reset();
   for (auto& kv : conns) {
     close(kv.first);
     gevws_conn_free(kv.second.c);

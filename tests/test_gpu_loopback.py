@@ -62,6 +62,31 @@ def test_c1_loopback_pipelined_loop(msg):
          env={"GEVWS_LB_PIPELINE": "1"})
 
 
+@pytest.mark.parametrize("msg", [128, 65536])
+def test_c1_loopback_split_passes(msg):
+    """GEVWS_LB_SPLIT=2: an iteration makes two device passes on two decoders
+    (connections alternate between them), the first half's in flight while
+    the second half's sockets are read; every echo checked byte for byte,
+    including 64 KiB frames carried across reads."""
+    _run("gev_amd/ws_loopback", conns=100 if msg == 128 else 16, seconds=1.5, msg=msg,
+         env={"GEVWS_LB_SPLIT": "2"})
+
+
+def test_wsserver_mirror_split_passes_with_control_frames(tmp_path):
+    """The wsserver mirror with split passes: control replies and closes still
+    answered by each half's device handler (the oracle's replies)."""
+    from oracle import ws_oracle as wo
+    tr = tmp_path / "transcript.txt"
+    d = _run("gev_amd/ws_loopback", conns=100, seconds=1.5, loops=2, threads=4,
+             env={"GEVWS_LB_SPLIT": "2"},
+             extra=("--mode", "wsserver", "--ctrl", "0.3", "--close-end", "1", "--transcript", str(tr)))
+    assert d["closes_answered"] == 100
+    for sent_hex, reply_hex in (ln.split() for ln in tr.read_text().splitlines() if ln.strip()):
+        fr = wo.decode_stream(bytes.fromhex(sent_hex)).frames
+        want, _ = wo.on_message(fr[0].header, fr[0].payload, wo.HANDLER_ECHO_TEXT)
+        assert bytes.fromhex(reply_hex) == want
+
+
 # ---------------------------------------------------------------- wsserver_test.go on the live server
 def test_wsserver_test_mirror_8_loops_100_clients():
     """example/websocket/wsserver_test.go:73-133, the reference's own hot-path
