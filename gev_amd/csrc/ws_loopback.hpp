@@ -72,6 +72,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <memory>
 #include <chrono>
@@ -176,19 +177,24 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
   Decoder dec(device);
   const bool wss = g_cfg.mode != kModeEcho;
   if (wss) dec.set_handler(GEVWS_HANDLER_ECHO_TEXT);  // wsExample.OnMessage returns (MessageText, data)
-  // GEVWS_LB_SPLIT=K (a pipelined decoder): an iteration with at least K
-  // readable upgraded connections makes TWO device passes, each on its own
-  // decoder (connections alternate between them at accept): the first half's
-  // pass runs while the second half's sockets are read, the second half's
-  // while the first half's echoes are written -- every echo still goes out
-  // in the iteration that read its frame.
+  // GEVWS_LB_SPLIT=K (a pipelined decoder; default 64, 0 = off): an
+  // iteration with at least K readable connections makes W = GEVWS_LB_WAYS
+  // (default 2, at most 8) device passes, each on its own decoder
+  // (connections are dealt to them at accept): group g's pass runs while
+  // groups g+1.. are read and groups ..g-1 are echoed -- every echo still goes
+  // out in the iteration that read its frame.  100 connections on one loop:
+  // 461-463 k -> 482-493 k echoes/s with two groups, 3 or 4 no better
+  // (profiles/r04/r04_loopback_split_ways.jsonl).
   const char* se = getenv("GEVWS_LB_SPLIT");
-  const uint32_t split_min = Decoder::kPipelined && se ? (uint32_t)strtoul(se, nullptr, 10) : 0;
-  std::unique_ptr<Decoder> dec2;
-  if (split_min) {
-    dec2.reset(new Decoder(device));
-    if (wss) dec2->set_handler(GEVWS_HANDLER_ECHO_TEXT);
+  const uint32_t split_min = Decoder::kPipelined ? (se ? (uint32_t)strtoul(se, nullptr, 10) : 64u) : 0u;
+  const char* we = getenv("GEVWS_LB_WAYS");
+  const uint32_t ways = split_min ? std::min(8u, std::max(2u, we ? (uint32_t)strtoul(we, nullptr, 10) : 2u)) : 1u;
+  std::vector<std::unique_ptr<Decoder>> decs;  // groups 1 .. ways-1 (group 0: dec)
+  for (uint32_t g = 1; g < ways; ++g) {
+    decs.emplace_back(new Decoder(device));
+    if (wss) decs.back()->set_handler(GEVWS_HANDLER_ECHO_TEXT);
   }
+  auto dec_of = [&](uint32_t g) -> Decoder& { return g == 0 ? dec : *decs[g - 1]; };
   uint32_t accepted = 0;
   std::mt19937_64 route(g_cfg.seed * 1000003u + (unsigned)index);  // wsserver_test.go:47: rand.Int() % 2
   int ls = socket(AF_INET, SOCK_STREAM, 0);
@@ -316,12 +322,12 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
     for (ServerConn* s : inflight) handle(s, t_dec);
   };
   double t_close = 0;
-  std::vector<int> deferred;                  // split: the second half's readable fds
-  std::vector<ServerConn*> readable2, upgraded2;
+  std::vector<std::vector<int>> deferred(ways);     // split: groups 1.. readable fds
+  std::vector<std::vector<ServerConn*>> rd(ways), up(ways);
   while (!g_stop.load(std::memory_order_relaxed)) {
     const int n = epoll_wait(ep, evs.data(), (int)evs.size(), pending ? 0 : 5);
     readable.clear();
-    deferred.clear();
+    for (auto& d : deferred) d.clear();
     // one read(2) per readable connection (handleRead), its bytes into the ring
     auto read_conn = [&](int fd, std::vector<ServerConn*>& into) {
       auto it = conns.find(fd);
@@ -346,8 +352,8 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
       const int fd = evs[i].data.fd;
       if (fd != ls && split_min) {
         auto it = conns.find(fd);
-        if (it != conns.end() && it->second.half == 1) {  // read after the first half's pass is launched
-          deferred.push_back(fd);
+        if (it != conns.end() && it->second.half != 0) {  // read after the earlier groups' passes are launched
+          deferred[it->second.half].push_back(fd);
           continue;
         }
       }
@@ -357,7 +363,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
           if (cfd < 0) break;
           setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
           ServerConn sc{cfd, gevws_conn_new(), gevws_ring_new(4096), {}, {}, 0};  // DefaultBufferSize
-          sc.half = split_min ? (int)(accepted++ & 1u) : 0;
+          sc.half = split_min ? (int)(accepted++ % ways) : 0;
           gevws_conn_set_upgraded(sc.c, 0);
           conns.emplace(cfd, std::move(sc));
           g_live.fetch_add(1);  // OnConnect
@@ -376,26 +382,28 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
     double t_dec = t_close;
     t_close = 0;
     finish(t_dec);  // the pass begun last iteration: its frames go out now
-    if (split_min && readable.size() + deferred.size() >= split_min) {
-      // two passes: the first half's runs while the second half is read, the
-      // second half's while the first half's echoes are written
-      auto begin_half = [&](Decoder& d, std::vector<ServerConn*>& rd, std::vector<ServerConn*>& up) -> bool {
-        up.clear();
-        for (ServerConn* s : rd)
-          if (gevws_conn_upgraded(s->c)) up.push_back(s);
-        if (up.empty()) return false;
+    size_t nready = readable.size();
+    for (auto& d : deferred) nready += d.size();
+    if (split_min && !pipeline && nready >= split_min) {  // (not with GEVWS_LB_PIPELINE)
+      // W passes: group g's begins once its sockets are read, ends once the
+      // groups after it are read and the groups before it echoed
+      auto begin_group = [&](Decoder& d, std::vector<ServerConn*>& rg, std::vector<ServerConn*>& ug) -> bool {
+        ug.clear();
+        for (ServerConn* s : rg)
+          if (gevws_conn_upgraded(s->c)) ug.push_back(s);
+        if (ug.empty()) return false;
         const double td = now_s();
-        const int64_t f = d.begin(up.data(), (uint32_t)up.size());
+        const int64_t f = d.begin(ug.data(), (uint32_t)ug.size());
         t_dec += now_s() - td;
         if (f < 0) {
           fprintf(stderr, "ws_loopback: decoder pass %s\n", gevws_status_string((int)f));
           exit(3);
         }
         g_batches.fetch_add(1, std::memory_order_relaxed);
-        g_batch_conns.fetch_add(up.size(), std::memory_order_relaxed);
+        g_batch_conns.fetch_add(ug.size(), std::memory_order_relaxed);
         return true;
       };
-      auto end_half = [&](Decoder& d, bool began, std::vector<ServerConn*>& rd) {
+      auto end_group = [&](Decoder& d, bool began, std::vector<ServerConn*>& rg) {
         if (began) {
           const double td = now_s();
           const int64_t f = d.end();
@@ -405,19 +413,25 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
             exit(3);
           }
         }
-        for (ServerConn* s : rd) handle_with(d, s, t_dec);  // (handshakes too)
+        for (ServerConn* s : rg) handle_with(d, s, t_dec);  // (handshakes too)
       };
-      const bool b1 = begin_half(dec, readable, upgraded);
-      readable2.clear();
-      for (int fd : deferred) read_conn(fd, readable2);
-      const bool b2 = begin_half(*dec2, readable2, upgraded2);
-      end_half(dec, b1, readable);
-      end_half(*dec2, b2, readable2);
+      bool began[8] = {};
+      rd[0].swap(readable);
+      for (uint32_t g = 0; g < ways; ++g) {
+        if (g) {
+          rd[g].clear();
+          for (int fd : deferred[g]) read_conn(fd, rd[g]);
+        }
+        began[g] = begin_group(dec_of(g), rd[g], up[g]);
+      }
+      for (uint32_t g = 0; g < ways; ++g) end_group(dec_of(g), began[g], rd[g]);
+      rd[0].swap(readable);
       flush_queued();
       g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
       continue;
     }
-    for (int fd : deferred) read_conn(fd, readable);  // (split on, a small iteration: one pass)
+    for (uint32_t g = 1; g < ways; ++g)
+      for (int fd : deferred[g]) read_conn(fd, readable);  // (split on, a small iteration: one pass)
     if (readable.empty()) {
       flush_queued();
       g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
@@ -450,7 +464,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
     g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
   }
   if (pending) (void)dec.end();
-  dec2.reset();
+  decs.clear();
   for (auto& kv : conns) {
     close(kv.first);
     gevws_conn_free(kv.second.c);

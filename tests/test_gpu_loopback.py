@@ -62,14 +62,14 @@ def test_c1_loopback_pipelined_loop(msg):
          env={"GEVWS_LB_PIPELINE": "1"})
 
 
-@pytest.mark.parametrize("msg", [128, 65536])
-def test_c1_loopback_split_passes(msg):
-    """GEVWS_LB_SPLIT=2: an iteration makes two device passes on two decoders
-    (connections alternate between them), the first half's in flight while
-    the second half's sockets are read; every echo checked byte for byte,
+@pytest.mark.parametrize("msg,ways", [(128, 2), (128, 4), (65536, 3)])
+def test_c1_loopback_split_passes(msg, ways):
+    """GEVWS_LB_SPLIT=2: an iteration makes W device passes on W decoders
+    (connections dealt to them at accept), group g's in flight while the
+    later groups' sockets are read; every echo checked byte for byte,
     including 64 KiB frames carried across reads."""
     _run("gev_amd/ws_loopback", conns=100 if msg == 128 else 16, seconds=1.5, msg=msg,
-         env={"GEVWS_LB_SPLIT": "2"})
+         env={"GEVWS_LB_SPLIT": "2", "GEVWS_LB_WAYS": str(ways)})
 
 
 def test_wsserver_mirror_split_passes_with_control_frames(tmp_path):
