@@ -125,6 +125,50 @@ def test_encode_window_queue_at_capacity(engine, enc_variant):
     _encode_check(engine, _records(hd, offs, lens), payload, "tiny runs")
 
 
+def _arena_batch(rng, lens, p0=0, hdr_len=None):
+    """Replies whose payloads sit in a decode's payload-arena layout: slots of
+    round16(L) bytes back to back from a 16-aligned p0 (an echo server's case)."""
+    lens = np.asarray(lens, dtype=np.int64)
+    slots = (lens + 15) // 16 * 16
+    offs = p0 + np.concatenate([[0], np.cumsum(slots)[:-1]]).astype(np.uint64)
+    payload = rng.integers(0, 256, int(p0 + slots.sum()) + 16, dtype=np.uint8)
+    hd = []
+    for i, L in enumerate(lens):
+        hl = int(L) if hdr_len is None else hdr_len(i, int(L))
+        h = wo.Header(bool(rng.random() < .8), 0, int(rng.choice([1, 2, 9, 10])), bool(rng.random() < .3),
+                      bytes(rng.integers(0, 256, 4, dtype=np.uint8)), hl)
+        hd.append(np.frombuffer(h.pack(), np.uint8))
+    return _records(np.array(hd), offs, lens), payload
+
+
+def test_encode_decode_arena_layouts(engine, enc_variant):
+    """Payload slots back to back as a decode leaves them (an echo server's
+    replies) -- every header form, empty frames first / last / in runs longer
+    than a window's table, 1-15 byte tails, frames spanning many streaming
+    steps, a batch of only empty frames, and a p0 past the arena start; plus
+    one slot out of place."""
+    rng = np.random.default_rng(77)
+    cases = [
+        [0, 5, 0, 130, 1, 15, 16, 17, 0],
+        list(rng.integers(0, 300, 3000)),
+        list(rng.integers(64, 4096, 2000)),
+        [0] * 1500 + [100] + [0] * 1300 + [3],
+        [0, 0, 0],
+        [70000, 1, 300000, 0, 65536, 65535, 131072 + 7],
+        list(np.clip((64 * (1 - rng.random(20000)) ** (-1 / 1.1)).astype(np.int64), 64, 1 << 20)),
+    ]
+    for k, lens in enumerate(cases):
+        fr, pay = _arena_batch(rng, lens, p0=16 * int(rng.integers(0, 5)))
+        _encode_check(engine, fr, pay, f"arena case {k}")
+    # one slot moved: not the arena layout
+    fr, pay = _arena_batch(rng, list(rng.integers(0, 500, 200)))
+    fr["payload_off"][57] += 16
+    _encode_check(engine, fr, pay, "arena layout broken")
+    # header lengths that disagree with the payload (Go's byte arithmetic)
+    fr, pay = _arena_batch(rng, list(rng.integers(0, 500, 300)), hdr_len=lambda i, L: (L * 7 + i) % 70000)
+    _encode_check(engine, fr, pay, "arena, odd header lengths")
+
+
 def test_encode_empty_batch(engine):
     import torch
     fr = np.zeros(0, gev_amd.OUT_FRAME_DTYPE)
