@@ -115,7 +115,9 @@ __global__ __launch_bounds__(kWalkBlock) void k_enc_emit(uint64_t n,
                                                          const gevws_summary* __restrict__ sum,
                                                          uint64_t* __restrict__ out_off,
                                                          uint32_t* __restrict__ tile_first,
-                                                         const gevws_summary* __restrict__ gate = nullptr) {
+                                                         const gevws_summary* __restrict__ gate = nullptr,
+                                                         uint32_t* __restrict__ work = nullptr) {
+  if (work && blockIdx.x == 0 && threadIdx.x == 0) *work = 0;  // k_encode6's run counter
   if (sum->status != GEVWS_OK) return;
   n = gated_count(n, gate);
   const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;
@@ -853,6 +855,328 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   }
 }
 
+// The encode with one wave per step (k_encode6): every wave walks its own run
+// of tiles, ST = U / 4 tiles a step, with no workgroup barrier.  A step inside
+// one payload is streamed as in k_encode; otherwise the step's frames go into
+// the wave's LDS table, each frame that is the last to start in its chunk marks
+// that chunk in a one-byte-per-chunk map, and one per-wave prefix max turns the
+// marks into every chunk's frame (no search).  A chunk inside one payload is
+// loaded and stored; 64-byte groups holding any other chunk are queued in the
+// wave's LDS (slots from a ballot, no atomics) and assembled after the
+// interior loads are in flight, one chunk per lane.
+// LDS written by some lanes of a wave and read by others: the hardware keeps a
+// wave's LDS operations in order, the fence keeps the compiler from moving them.
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// How waves share the tiles (`mode`, -1 = chosen on the device):
+//  0  one contiguous run per wave -- batches of big frames (mean >= kBigFrameBytes,
+//     the streaming path: long runs keep DRAM pages open);
+//  1  each wave takes every nwaves-th run of K tiles (K <= kEnc6Run, at least
+//     8 runs a wave): a run's cost follows the local frame density, and runs
+//     spread over the whole batch even it out;
+//  2  runs of K = kEnc6Run tiles from a work counter (one lane's vector atomic
+//     per run; k_enc_emit zeroes it) -- batches of at least kEnc6DynRuns runs
+//     a wave, where the atomics are few against the work they balance.
+constexpr uint64_t kEnc6Run = 64;
+constexpr uint64_t kEnc6DynRuns = 8;
+template <int U>
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(U == 4 ? 8 : 4))) void k_encode6(
+    const gevws_out_frame* __restrict__ fr, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ out_off,
+    const uint32_t* __restrict__ tile_first, const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
+    uint32_t big_grid, uint32_t* __restrict__ work, int mode) {
+  static_assert(U == 4 || U == 8, "one or two tiles a step");
+  constexpr int NW = kUnmaskBlock / 64, ST = U / 4, TF = 16 * U, MW = U / 4;
+  // frame i of the step: wire start (step-relative, >= -64) * 16 | header
+  // length, payload end (step-relative, clamped), payload_off - wire start -
+  // header length (lo / hi)
+  __shared__ u32x4 s_ta[NW][TF];
+  __shared__ u64x2 s_tb[NW][TF];            // header bytes 0-7, bytes 8-13
+  __shared__ uint32_t s_map[NW][64 * MW];  // chunk -> frame, one byte per chunk (lane l: chunks U l ..)
+  __shared__ uint16_t s_q[NW][64 * U];     // queued chunks (0xffff: a group's slot past the run)
+  if (sum->status != GEVWS_OK) return;
+  const uint64_t total = sum->payload_bytes;  // wire bytes
+  const uint64_t nframes = sum->frames;
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  if (ntiles == 0) return;
+  const uint32_t groups = active_groups(total, nframes, big_grid);
+  if (blockIdx.x >= groups) return;
+  const uint32_t w = uniform32(threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)groups * NW;
+  const uint64_t per = (ntiles + nwaves - 1) / nwaves;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + w;
+  if (mode < 0)
+    mode = total / nframes >= kBigFrameBytes ? 0 : (ntiles >= kEnc6DynRuns * kEnc6Run * nwaves ? 2 : 1);
+  uint64_t t = mode ? 0 : gw * per;
+  uint64_t tend = mode ? 0 : (t + per < ntiles ? t + per : ntiles);
+  // modes 1 / 2: run length K (a multiple of the step) and the wave's next run
+  uint64_t K = ntiles / (nwaves * 8);
+  K = K > kEnc6Run ? kEnc6Run : K;
+  K = K < (uint64_t)ST ? (uint64_t)ST : K - K % ST;
+  uint64_t run = gw;
+  uint8_t* const mb = reinterpret_cast<uint8_t*>(s_map[w]);
+  uint64_t c_f = ~0ull, c_ps = 0, c_pe = 0, c_delta = 0;  // cached frame: payload [c_ps, c_pe) in wire coordinates
+  for (;;) {
+    if (t >= tend) {
+      if (mode == 0) break;
+      if (mode == 2) {
+        uint32_t g = 0;
+        if ((fresh_tid() & 63) == 0) g = atomicAdd(work, 1u);
+        run = uniform32((uint32_t)__shfl((int)g, 0, 64));
+      }
+      t = run * K;
+      if (t >= ntiles) break;
+      tend = t + K < ntiles ? t + K : ntiles;
+      run += nwaves;
+      continue;
+    }
+    const uint64_t B = t * kTile;
+    const uint64_t nt = tend - t < (uint64_t)ST ? tend - t : (uint64_t)ST;  // tiles this step
+    const uint64_t send = B + nt * kTile;
+    const uint64_t lim = send < total ? send : total;  // the step writes [B, lim)
+    uint64_t fa = c_f, fb = c_f;
+    if (!(B >= c_ps && send <= c_pe)) {
+      // the step's first and last frames; a step with one frame may lie in its payload
+      fa = uniform32(tile_first[t]);
+      fb = t + nt < ntiles ? (uint64_t)uniform32(tile_first[t + nt]) : nframes - 1;
+      if (fa == fb && fa != c_f) {
+        c_f = fa;
+        const uint64_t* rec = reinterpret_cast<const uint64_t*>(fr + fa);
+        const uint64_t w0 = uniform64(rec[0]), len = uniform64(rec[1]);
+        const uint64_t po = uniform64(rec[2]), pl = uniform64(rec[3]);
+        gevws_header h;
+        memcpy(&h, &w0, 8);
+        h.length = (int64_t)len;
+        c_ps = uniform64(out_off[fa]) + enc_hlen(h);
+        c_pe = c_ps + pl;
+        c_delta = po - c_ps;
+      }
+    }
+    if (B >= c_ps && send <= c_pe) {  // inside one payload: stream the step
+      const uint8_t* s0 = payload + (B + c_delta);
+      const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(s0) & 15);  // wave-uniform
+      const uint32_t lane = fresh_tid() & 63;
+      const int nu = (int)nt * 4;
+      u32x4 v[U];
+      if (mis != 0) {
+        const uint8_t* a = s0 + lane * 16 - mis;
+        uint8_t* d = out + B + lane * 16;
+        const bool last = lane == 63;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (u < nu) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + u * 1024));
+        u32x4 e = u32x4{0, 0, 0, 0};
+        if (last) e = *reinterpret_cast<const u32x4*>(a + (nu - 1) * 1024 + 16);
+        u32x4 r = rot_next_lane(v[0]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u < nu) {
+            const u32x4 rn = u + 1 < nu ? rot_next_lane(v[u + 1 < U ? u + 1 : u]) : e;
+            st16_nt(d + u * 1024, funnel16(v[u], last ? rn : r, mis));
+            r = rn;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (u < nu) v[u] = ld16u(s0 + u * 1024 + lane * 16);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (u < nu) st16_nt(out + B + u * 1024 + lane * 16, v[u]);
+      }
+      t += nt;
+      continue;
+    }
+    const uint64_t n = fb - fa + 1;
+    if (n > (uint64_t)TF) {
+      // frames of a few bytes: per-lane global lookup and byte assembly (as k_encode)
+      const uint32_t lane = fresh_tid() & 63;
+#pragma unroll 1
+      for (int u = 0; u < U; ++u) {
+        const uint64_t p = B + (uint64_t)u * 1024 + lane * 16;
+        if (p < lim) {
+          uint64_t lo = fa, hi = fb;
+          while (lo < hi) {
+            const uint64_t mid = (lo + hi + 1) >> 1;
+            if (out_off[mid] <= p) lo = mid; else hi = mid - 1;
+          }
+          uint32_t wd[4] = {0, 0, 0, 0};
+          uint64_t j = lo;
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            while (j + 1 < nframes && out_off[j + 1] <= p + k) ++j;
+            const uint32_t byte = (p + k < total) ? enc_byte_global(fr, out_off, payload, j, p + k) : 0u;
+            wd[k >> 2] |= byte << (8 * (k & 3));
+          }
+          *reinterpret_cast<u32x4*>(out + p) = u32x4{wd[0], wd[1], wd[2], wd[3]};
+        }
+      }
+      t += nt;
+      continue;
+    }
+    // the step's frame table and chunk marks
+    {
+      const uint32_t lane = fresh_tid() & 63;
+#pragma unroll
+      for (int k = 0; k < MW; ++k) s_map[w][lane * MW + k] = 0;
+      wave_lds_order();
+#pragma unroll
+      for (int k = 0; k < TF / 64; ++k) {
+        const uint32_t i = lane + 64 * k;
+        if (i < n) {
+          const uint64_t f = fa + i;
+          const u64x2* r = reinterpret_cast<const u64x2*>(fr + f);
+          const u64x2 h2 = r[0], p2 = r[1];
+          const uint64_t oo = out_off[f];
+          gevws_header h;
+          memcpy(&h, &h2, 16);
+          uint64_t hlo, hhi;
+          const uint32_t hl = enc_header(h, hlo, hhi);
+          const int64_t st = (int64_t)(oo - B);
+          const int64_t end = st + hl + (int64_t)p2[1];  // the next frame's start
+          const int32_t stc = st < -64 ? -64 : (int32_t)st;
+          const uint64_t d = p2[0] - oo - hl;
+          s_ta[w][i] = u32x4{(uint32_t)(stc * 16) | hl, end > 0x7fffffffll ? 0x7fffffffu : (uint32_t)end,
+                             (uint32_t)d, (uint32_t)(d >> 32)};
+          s_tb[w][i] = u64x2{hlo, hhi};
+          // the last frame to start in its chunk marks it (the batch's last frame always)
+          if (st >= 0 && st < (int64_t)(U * 1024)) {
+            const int64_t sc = st >> 4;
+            if (end >= (sc + 1) * 16 || f == nframes - 1) mb[sc] = (uint8_t)i;
+          }
+        }
+      }
+      wave_lds_order();
+      // prefix max over the chunks (lane l holds chunks U l .. U l + U - 1)
+      uint32_t b[U];
+#pragma unroll
+      for (int k = 0; k < MW; ++k) {
+        const uint32_t m = s_map[w][lane * MW + k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[4 * k + j] = (m >> (8 * j)) & 0xffu;
+      }
+#pragma unroll
+      for (int j = 1; j < U; ++j) b[j] = b[j] > b[j - 1] ? b[j] : b[j - 1];
+      uint32_t inc = b[U - 1];
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, dd, 64);
+        if (lane >= (uint32_t)dd) inc = inc > y ? inc : y;
+      }
+      uint32_t exc = (uint32_t)__shfl_up((int)inc, 1, 64);
+      if (lane == 0) exc = 0;
+#pragma unroll
+      for (int k = 0; k < MW; ++k) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m |= (b[4 * k + j] > exc ? b[4 * k + j] : exc) << (8 * j);
+        s_map[w][lane * MW + k] = m;
+      }
+      wave_lds_order();
+    }
+    // classify the lane's chunks (chunk u * 64 + lane, byte u * 1 KiB + 16 lane),
+    // queue the 64-byte groups holding a chunk that is not inside one payload
+    // (whole, in order), and load the rest
+    uint32_t interior = 0, nb = 0;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t lane = fresh_tid() & 63;
+      const uint32_t c = (uint32_t)u * 64 + lane;
+      const int32_t x = (int32_t)(c * 16);
+      const bool valid = B + (uint64_t)x < lim;
+      const u32x4 ta = s_ta[w][mb[c]];
+      const int32_t ps = ((int32_t)ta[0] >> 4) + (int32_t)(ta[0] & 15u);
+      const bool in = valid && ps <= x && x + 16 <= (int32_t)ta[1];
+      const uint64_t bal = __ballot(valid && !in);
+      const bool defer = ((bal >> (lane & ~3u)) & 0xFull) != 0;  // (group-uniform)
+      const uint64_t dbal = __ballot(defer);
+      if (defer) {
+        const uint32_t slot =
+            nb + __builtin_amdgcn_mbcnt_hi((uint32_t)(dbal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dbal, 0u));
+        s_q[w][slot] = valid ? (uint16_t)c : (uint16_t)0xffffu;
+      }
+      nb += (uint32_t)__builtin_popcountll(dbal);
+      const bool ld = in && !defer;
+      interior |= (ld ? 1u : 0u) << u;
+      // every lane loads; a chunk not stored here from payload[0]
+      v[u] = ld16u(payload + (ld ? B + (uint64_t)x + ((uint64_t)ta[2] | ((uint64_t)ta[3] << 32)) : 0ull));
+    }
+    wave_lds_order();
+    // a queued chunk: header and payload bytes of the frames overlapping it.
+    // Payload bytes come from the 16 bytes at the chunk's position in the
+    // frame's payload coordinates (no shift), unless those would start before
+    // the buffer.
+    auto paddr = [&](const u32x4& ta, int32_t x, int32_t kend) -> uint64_t {
+      const int32_t hs = (int32_t)ta[0] >> 4, ps = hs + (int32_t)(ta[0] & 15u), pe = (int32_t)ta[1];
+      const int32_t p0 = ps > x ? ps : x, p1 = pe < kend ? pe : kend;
+      if (hs >= kend || p0 >= p1) return 0;  // (payload[0], always readable, unused)
+      const uint64_t d = (uint64_t)ta[2] | ((uint64_t)ta[3] << 32);
+      const uint64_t off = B + (uint64_t)x + d;
+      return (int64_t)off >= 0 ? off : B + (uint64_t)p0 + d;
+    };
+    auto piece = [&](u128& acc, uint32_t j, const u32x4& ta, const u32x4& pv4, int32_t x, int32_t kend) {
+      const int32_t hs = (int32_t)ta[0] >> 4;
+      if (hs >= kend) return;
+      const int32_t ps = hs + (int32_t)(ta[0] & 15u), pe = (int32_t)ta[1];
+      const int32_t h0 = hs > x ? hs : x, h1 = ps < kend ? ps : kend;
+      if (h0 < h1) {
+        const u64x2 tb = s_tb[w][j];
+        const u128 H = (u128)tb[0] | ((u128)tb[1] << 64);
+        acc |= ((H >> (8 * (h0 - hs))) << (8 * (h0 - x))) & byte_mask(h0 - x, h1 - x);
+      }
+      const int32_t p0 = ps > x ? ps : x, p1 = pe < kend ? pe : kend;
+      if (p0 < p1) {
+        const uint64_t d = (uint64_t)ta[2] | ((uint64_t)ta[3] << 32);
+        const bool at_x = (int64_t)(B + (uint64_t)x + d) >= 0;
+        const u128 pv = u128_of(pv4);
+        acc |= (at_x ? pv : (pv << (8 * (p0 - x)))) & byte_mask(p0 - x, p1 - x);
+      }
+    };
+    auto assemble = [&](uint32_t c) -> u32x4 {
+      const int32_t x = (int32_t)(c * 16);
+      const uint64_t a = B + (uint64_t)x;
+      const int32_t kend = x + ((a + 16 <= total) ? 16 : (int32_t)(total - a));
+      // the frame holding the byte before the chunk (the step's first frame
+      // for chunk 0) and the next one: both payload loads issued together
+      const uint32_t j0 = c ? (uint32_t)mb[c - 1] : 0u;
+      const uint32_t j1 = j0 + 1 < (uint32_t)n ? j0 + 1 : j0;
+      const u32x4 t0 = s_ta[w][j0], t1 = s_ta[w][j1];
+      const uint64_t a0 = paddr(t0, x, kend);
+      const uint64_t a1 = j1 != j0 ? paddr(t1, x, kend) : 0ull;
+      const u32x4 v0 = ld16u(payload + a0), v1 = ld16u(payload + a1);
+      u128 acc = 0;
+      piece(acc, j0, t0, v0, x, kend);
+      if (j1 != j0) piece(acc, j1, t1, v1, x, kend);
+      for (uint32_t j = j0 + 2; j < (uint32_t)n; ++j) {  // frames of a few bytes
+        const u32x4 ta = s_ta[w][j];
+        if (((int32_t)ta[0] >> 4) >= kend) break;
+        piece(acc, j, ta, ld16u(payload + paddr(ta, x, kend)), x, kend);
+      }
+      return u32x4_of(acc);
+    };
+    const uint32_t i0 = fresh_tid() & 63;
+    u32x4 x0 = u32x4{0, 0, 0, 0};
+    uint32_t q0 = 0xffffu;
+    if (i0 < nb) {
+      q0 = s_q[w][i0];
+      if (q0 != 0xffffu) x0 = assemble(q0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (interior & (1u << u)) st16_nt(out + B + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16, v[u]);
+    if (q0 != 0xffffu) st16_nt(out + B + (uint64_t)q0 * 16, x0);
+    for (uint32_t i = i0 + 64; i < nb; i += 64) {
+      const uint32_t q = s_q[w][i];
+      if (q != 0xffffu) st16_nt(out + B + (uint64_t)q * 16, assemble(q));
+    }
+    wave_lds_order();  // this step's readers are done with the table, the map and the queue
+    t += nt;
+  }
+}
+
 // ------------------------------------------------------------------ control-frame dispatch (§8f row 2)
 // HandlerWrap.OnMessage (plugins/websocket/wrap.go:38-90) for decoded frames:
 // close -> util.HandleClose (util.go:27-46) + ShutdownWrite; ping -> pong with
@@ -1179,13 +1503,13 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
   signal_done(done, seq);
 }
 
-// GEVWS_TUNE_ENCODE_VARIANT: 0 = auto (k_encode5 when the caller's capacity
-// per frame is at least kEnc5MinMeanBytes, else k_encode), 1 = k_encode5,
-// 2 = k_encode.  Interleaved (profiles/r04/r04_encode5_ab.jsonl,
-// r04_encode5_c1_ab.jsonl): k_encode5 C2 -5 %, C3 -2..-4 %, C5 -1 %, C4 equal,
-// C1-shaped 128-byte frames +10 %.
-constexpr int kNumEncodeVariants = 3;
-constexpr uint64_t kEnc5MinMeanBytes = 1024;
+// GEVWS_TUNE_ENCODE_VARIANT: 0 = k_encode6 (two tiles a wave step when the
+// caller's capacity per frame exceeds kEnc6MinMeanBytes, else one; the run
+// mode chosen on the device), 1 = k_encode5, 2 = k_encode, 3 / 4 = k_encode6
+// with one / two tiles a step, 5 / 6 / 7 = two tiles a step in run mode 0 /
+// 1 / 2 (measurement).  DESIGN.md §5, profiles/r04/r04_encode6_ab.jsonl.
+constexpr int kNumEncodeVariants = 8;
+constexpr uint64_t kEnc6MinMeanBytes = 256;
 
 }  // namespace
 
@@ -1212,17 +1536,24 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   const size_t blk_bytes = ((size_t)nblk * kBlkFields * sizeof(uint64_t) + 255) & ~size_t(255);
   int r = order_after_last(ctx, st);
   if (r != GEVWS_OK) return r;
-  r = ensure_scratch(ctx, blk_bytes + ntiles_cap * sizeof(uint32_t));
+  const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
+  r = ensure_scratch(ctx, blk_bytes + tile_bytes + 256);
   if (r != GEVWS_OK) return r;
   uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
   uint32_t* tile_first = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes);
+  uint32_t* work = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes + tile_bytes);
   if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_out_off, gate);
   k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
-  if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(n, blk, d_summary, d_out_off, tile_first, gate);
-  const bool v5 = ctx->encode_variant == 1 ||
-                  (ctx->encode_variant == 0 && n && out_cap / n >= kEnc5MinMeanBytes);
-  const uint64_t per_cu = v5 ? 4 : 7;  // the window path's occupancy (k_encode5 / k_encode)
-  uint64_t grid = (out_cap / kTile + (v5 ? 8 : kWinTiles) - 1) / (v5 ? 8 : kWinTiles);
+  if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(n, blk, d_summary, d_out_off, tile_first, gate, work);
+  const bool v6 = ctx->encode_variant == 0 || ctx->encode_variant >= 3;
+  const bool v5 = ctx->encode_variant == 1;
+  // the window path's occupancy (k_encode6 / k_encode5 / k_encode) and tiles per workgroup step
+  // k_encode6's step: two tiles a wave for frames of more than kEnc6MinMeanBytes (by capacity)
+  const bool u8 = ctx->encode_variant == 4 || ctx->encode_variant >= 5 ||
+                  (ctx->encode_variant == 0 && n && out_cap / n > kEnc6MinMeanBytes);
+  const uint64_t per_cu = v6 ? (u8 ? 4 : 8) : v5 ? 4 : 7;
+  const uint64_t wtiles = v6 ? (u8 ? 8 : 4) : v5 ? 8 : kWinTiles;
+  uint64_t grid = (out_cap / kTile + wtiles - 1) / wtiles;
   // (GEVWS_TUNE_UNMASK_GRID, when set, caps the encode's grid too: measurement)
   const uint64_t gcap = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : per_cu * (uint64_t)ctx->num_cus;
   if (grid > gcap) grid = gcap;
@@ -1234,8 +1565,14 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   // batches of big frames (mean >= kBigFrameBytes) keep 4 per CU (the rest
   // return at once)
   const uint32_t big = grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
-  auto kfn = v5 ? k_encode5 : k_encode;
-  kfn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out, big);
+  if (v6) {
+    const int mode = ctx->encode_variant >= 5 ? ctx->encode_variant - 5 : -1;
+    (u8 ? k_encode6<8> : k_encode6<4>)<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(
+        d_frames, d_payload, d_out_off, tile_first, d_summary, d_out, big, work, mode);
+  } else {
+    auto kfn = v5 ? k_encode5 : k_encode;
+    kfn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out, big);
+  }
   GEVWS_HIP(hipGetLastError());
   return mark_last(ctx, st);
 }

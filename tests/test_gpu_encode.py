@@ -14,11 +14,13 @@ from tests._helpers import gpu_decode, host_result, pack_streams, random_stream
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["auto", "k_encode5", "k_encode"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7], ids=["auto", "k_encode5", "k_encode", "k_encode6_4", "k_encode6_8", "k_encode6_8_contiguous", "k_encode6_8_cyclic", "k_encode6_8_counter"])
 def enc_variant(request, engine):
-    """Every encode kernel (GEVWS_TUNE_ENCODE_VARIANT): 0 = the per-batch
-    choice, 1 = 8-tile pipelined windows with a chunk map at 4 workgroups per
-    CU, 2 = 4-tile windows at 7."""
+    """Every encode kernel (GEVWS_TUNE_ENCODE_VARIANT): 0 = the default
+    (k_encode6, its step and run mode chosen per batch), 1 = k_encode5 (8-tile
+    windows at 4 workgroups per CU), 2 = k_encode (4-tile windows at 7), 3 / 4
+    = k_encode6 with one / two tiles a wave step, 5 / 6 / 7 = two tiles a step
+    with contiguous / cyclic / counter runs."""
     try:
         engine.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, request.param)
     except RuntimeError:
