@@ -301,569 +301,32 @@ __device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t 
   return u32x4_of(acc);
 }
 
-// The encode's byte stream (k_enc_size / k_enc_emit placed every frame's wire
-// bytes and the output-tile -> frame map).  Each workgroup owns a contiguous
-// run of output tiles.
-//  * Inside one payload for the next U tiles: stream (a misaligned source as
-//    the unmask's streaming path: wave-contiguous U KiB spans, aligned
+// The encode's byte stream, one wave per step (k_encode6; k_enc_size /
+// k_enc_emit placed every frame's wire bytes and the output-tile -> frame
+// map).  Every wave walks its own runs of tiles, ST = U / 4 tiles a step, with
+// no workgroup barrier.
+//  * A step inside one payload is streamed (a misaligned source as the
+//    unmask's streaming path: wave-contiguous 1 KiB spans, aligned
 //    non-temporal loads, DPP rotate + v_alignbyte; an aligned one with plain
 //    loads), aligned non-temporal stores.
-//  * Otherwise a window of kWinTiles tiles: its frames' wire starts, payload
-//    ends, header lengths and payload offsets in LDS; each lane finds the
-//    frame of each of its chunks by binary search; a chunk inside one payload
-//    is loaded (unaligned) and stored; a chunk that straddles a frame boundary
-//    (header bytes or two frames' pieces) is queued in LDS and assembled
-//    afterwards by the whole workgroup, one chunk per lane, instead of by the
-//    one or two lanes of each wave that meet them while the other lanes wait.
-//    A 64-byte group of chunks holding a boundary is queued whole (its
-//    interior chunks with it, four consecutive slots), so one store writes the
-//    group's 64 bytes: otherwise every frame boundary left its line to HBM as
-//    two partial writes (C4: 46 M 32-byte write requests per launch, 0 with
-//    it; the whole C4 encode 10.70 -> 9.11 ms, profiles/r02/r02_encode_ab_g64_*.json).
-//    All the window's payload loads are issued before its stores, and the
-//    interior chunks are stored only after the queue barrier and the lane's
-//    first queued chunk has been assembled, so the interior loads and the first
-//    assembly's loads are in flight together (C4 9.39 -> 9.17 ms,
-//    profiles/r03/r03_encode_eo_ab.jsonl).
-// The window path is latency-bound: the kernel is held to 72 VGPRs for 7
-// workgroups per CU (amdgpu_waves_per_eu(7): C2 -4 %, C4 -2 % against 6 per
-// CU; 8 per CU at 64 VGPRs was slower on C5, profiles/r01/r01_encode_ab_occ_*.json).
-// Measured and not kept: 8-tile windows (C4 9.71 -> 12.23 ms), a chunk ->
-// frame map instead of the search (C4 9.35 -> 9.57 ms), non-temporal window
-// loads (C4 +8.8 %) -- DESIGN.md §5.
-__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(7))) void k_encode(
-    const gevws_out_frame* __restrict__ fr, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ out_off,
-    const uint32_t* __restrict__ tile_first, const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
-    uint32_t big_grid) {
-  constexpr int U = 4, WT = kWinTiles, WF = kEncWinFrames;
-  __shared__ int32_t s_start[WF];
-  __shared__ int32_t s_pend[WF];
-  __shared__ uint8_t s_hlen[WF];
-  __shared__ uint32_t s_bnd[WT * kUnmaskBlock];  // queued chunk: rel / 16 | frame << 16 (~0: a group's filler)
-  __shared__ uint32_t s_nb;
-  __shared__ uint64_t s_delta[WF];
-  const EncWin W{s_start, s_pend, s_hlen, s_delta, nullptr, nullptr};
-  if (sum->status != GEVWS_OK) return;
-  const uint64_t total = sum->payload_bytes;  // wire bytes
-  const uint64_t nframes = sum->frames;
-  const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint32_t groups = active_groups(total, nframes, big_grid);
-  if (blockIdx.x >= groups) return;
-  const uint64_t per = (ntiles + groups - 1) / groups;
-  uint64_t t = (uint64_t)blockIdx.x * per;
-  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
-  uint64_t c_ps = 0, c_pe = 0, c_delta = 0;  // cached frame: payload [c_ps, c_pe) in wire coordinates
-  while (t < tend) {
-    const uint32_t lane_off = fresh_tid() * 16;  // recomputed per step: held, it was spilled
-    const uint64_t base = t * kTile;
-    if (base >= c_pe) {  // workgroup-uniform refresh (scalar loads)
-      const uint64_t f = tile_first[t];
-      const gevws_out_frame o = fr[f];
-      c_ps = out_off[f] + enc_hlen(o.hdr);
-      c_pe = c_ps + o.payload_len;
-      c_delta = o.payload_off - c_ps;
-    }
-    if (t + U <= tend && base >= c_ps && base + U * kTile <= c_pe) {  // inside one payload: stream
-      u32x4 v[U];
-      const uint8_t* s0 = payload + (base + c_delta);
-      const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(s0) & 15);  // wave-uniform
-      if (mis != 0) {
-        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        const uint64_t wrel = (uint64_t)wave * U * 1024 + lane * 16;
-        const uint8_t* a = s0 + wrel - mis;
-        uint8_t* d = out + base + wrel;
-        const bool last = lane == 63;
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + u * 1024));
-        u32x4 e = u32x4{0, 0, 0, 0};
-        if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
-        u32x4 r = rot_next_lane(v[0]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const u32x4 rn = u + 1 < U ? rot_next_lane(v[u + 1 < U ? u + 1 : u]) : e;
-          st16_nt(d + u * 1024, funnel16(v[u], last ? rn : r, mis));
-          r = rn;
-        }
-        t += U;
-        continue;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16u(payload + (base + u * kTile + lane_off + c_delta));
-#pragma unroll
-      for (int u = 0; u < U; ++u) st16_nt(out + base + u * kTile + lane_off, v[u]);
-      t += U;
-      continue;
-    }
-    const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
-    const uint64_t wbase = base;
-    const uint64_t f_lo = tile_first[t];
-    const uint64_t f_hi = (t + wt) < ntiles ? (uint64_t)tile_first[t + wt] : nframes - 1;
-    const uint64_t F = f_hi - f_lo + 1;
-    if (F <= (uint64_t)WF) {
-      __syncthreads();
-      for (uint64_t i = fresh_tid(); i < F; i += kUnmaskBlock) {
-        const gevws_out_frame o = fr[f_lo + i];
-        const uint32_t hl = enc_hlen(o.hdr);
-        const uint64_t oo = out_off[f_lo + i];
-        const int64_t st = (int64_t)(oo - wbase);
-        s_start[i] = st < -64 ? -64 : (int32_t)st;
-        const int64_t pe = st + hl + (int64_t)o.payload_len;
-        s_pend[i] = pe > 0x7fffffffll ? 0x7fffffff : (int32_t)pe;
-        s_hlen[i] = hl;
-        s_delta[i] = o.payload_off - oo - hl;
-      }
-      if (threadIdx.x == 0) s_nb = 0;
-      __syncthreads();
-      // every chunk's frame and kind first (interior of one payload, or a
-      // boundary to queue); a load inside the interior/boundary branch made
-      // the compiler wait for it at the branch's join
-      u32x4 v[WT];
-      uint32_t interior = 0, queued = 0;
-      uint32_t qlo[WT];
-#pragma unroll
-      for (int u = 0; u < WT; ++u) {
-        const int32_t rel = u * (int32_t)kTile + (int32_t)lane_off;
-        const uint64_t a = wbase + (uint64_t)rel;
-        const bool valid = (uint64_t)u < wt && a < total;
-        uint32_t lo = 0, hi = valid ? (uint32_t)F - 1 : 0u;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi + 1) >> 1;
-          if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
-        }
-        const bool in = valid && rel >= s_start[lo] + (int32_t)s_hlen[lo] && rel + 16 <= s_pend[lo];
-        qlo[u] = lo;
-        interior |= (in ? 1u : 0u) << u;
-        queued |= (valid && !in ? 1u : 0u) << u;
-      }
-      // 64-byte groups holding a queued chunk go to the queue whole
-      const uint32_t lane = threadIdx.x & 63, g0 = lane & ~3u;
-#pragma unroll
-      for (int u = 0; u < WT; ++u) {
-        const uint64_t bal = __ballot((queued >> u) & 1u);  // whole wave active
-        const bool defer = ((bal >> g0) & 0xFull) != 0;     // (group-uniform)
-        uint32_t slot = 0;
-        if (defer && (lane & 3u) == 0) slot = atomicAdd(&s_nb, 4u);
-        slot = __shfl(slot, (int)g0);
-        if (defer) {
-          const bool valid = (interior | queued) & (1u << u);
-          s_bnd[slot + (lane & 3u)] =
-              valid ? ((uint32_t)(u * (int32_t)kTile + (int32_t)lane_off) >> 4) | (qlo[u] << 16) : 0xffffffffu;
-          interior &= ~(1u << u);
-        }
-      }
-      // the interior loads (the queue pass loads its chunks itself; every lane
-      // loads, a non-interior chunk from payload[0], always readable, unused)
-#pragma unroll
-      for (int u = 0; u < WT; ++u) {
-        const bool in = (interior >> u) & 1u;
-        const uint64_t a = wbase + (uint64_t)(u * (int32_t)kTile + (int32_t)lane_off);
-        v[u] = ld16u(payload + (in ? a + s_delta[qlo[u]] : 0ull));
-      }
-      __syncthreads();  // the queue is complete
-      const uint32_t nb = s_nb;
-      const uint32_t i0 = fresh_tid();
-      u32x4 x0 = u32x4{0, 0, 0, 0};
-      uint32_t q0 = 0xffffffffu;
-      if (i0 < nb) {
-        q0 = s_bnd[i0];
-        if (q0 != 0xffffffffu) {
-          const int32_t rel = (int32_t)((q0 & 0xffffu) << 4);
-          x0 = enc_assemble<true>(rel, wbase + (uint64_t)rel, total, q0 >> 16, (uint32_t)F, W, payload, fr, f_lo);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < WT; ++u)
-        if (interior & (1u << u)) st16_nt(out + wbase + u * kTile + fresh_tid() * 16, v[u]);
-      if (q0 != 0xffffffffu) st16_nt(out + wbase + (uint64_t)((q0 & 0xffffu) << 4), x0);
-      for (uint32_t i = i0 + kUnmaskBlock; i < nb; i += kUnmaskBlock) {
-        const uint32_t q = s_bnd[i];
-        if (q == 0xffffffffu) continue;  // a group's slot past the batch's end
-        const int32_t rel = (int32_t)((q & 0xffffu) << 4);
-        const uint64_t a = wbase + (uint64_t)rel;
-        st16_nt(out + a, enc_assemble<true>(rel, a, total, q >> 16, (uint32_t)F, W, payload, fr, f_lo));
-      }
-      t += wt;
-      continue;
-    }
-    // more than kEncWinFrames frames in the window (frames of a few bytes):
-    // one tile, per-lane global lookup and byte assembly
-    {
-      const uint64_t a = t * kTile + lane_off;
-      if (a < total) {
-        uint64_t lo = tile_first[t];
-        uint64_t hi = (t + 1 < ntiles) ? (uint64_t)tile_first[t + 1] : nframes - 1;
-        while (lo < hi) {
-          const uint64_t mid = (lo + hi + 1) >> 1;
-          if (out_off[mid] <= a) lo = mid; else hi = mid - 1;
-        }
-        uint32_t w[4] = {0, 0, 0, 0};
-        uint64_t j = lo;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          while (j + 1 < nframes && out_off[j + 1] <= a + k) ++j;
-          const uint32_t byte = (a + k < total) ? enc_byte_global(fr, out_off, payload, j, a + k) : 0u;
-          w[k >> 2] |= byte << (8 * (k & 3));
-        }
-        *reinterpret_cast<u32x4*>(out + a) = u32x4{w[0], w[1], w[2], w[3]};
-      }
-      t += 1;
-    }
-  }
-}
-
-// The encode with the unmask v5's window machinery (k_encode5): 8-tile (32
-// KiB) windows at four workgroups per CU (128 VGPRs), each chunk's frame from
-// a chunk map instead of a binary search, and the next step decided -- its
-// first records loaded into registers -- while the window's payload loads are
-// in flight.  Boundary chunks go through the same 64-byte-group queue and
-// workgroup assembly as k_encode.
-//  * chunk map: wire frames are contiguous, so the frame holding a chunk's
-//    last byte is the last one starting in that chunk or before it.  Each
-//    frame that is the last to start in its chunk marks that chunk (its end,
-//    the next frame's start, lies in a later chunk: one writer per slot), the
-//    frame holding the byte before each wave quarter seeds that quarter, and a
-//    per-wave prefix max turns the marks into every chunk's frame.
-//  * a chunk is interior when that frame's payload covers all 16 bytes; the
-//    assembly of a queued chunk starts at the frame holding its first byte
-//    (the map's frame, or the one before it when that starts inside the chunk).
-constexpr int kEnc5Frames = 1024;
-constexpr uint32_t kEnc5Chunks = 8 * (uint32_t)kTile / 16;             // 2 048 chunks in a window
-constexpr uint32_t kEnc5Quarter = kEnc5Chunks / (kUnmaskBlock / 64);   // chunks per wave
-constexpr uint32_t kEnc5TmapN = 512;
-
-struct EncRec5 {
-  u64x2 h;      // header half of the record (fin, rsv, opcode, masked, mask[4], length)
-  u64x2 p;      // payload_off, payload_len
-  uint64_t oo;  // wire offset
-};
-
-__device__ __forceinline__ EncRec5 load_enc_rec(const gevws_out_frame* __restrict__ fr,
-                                                const uint64_t* __restrict__ out_off, uint64_t f) {
-  const u64x2* r = reinterpret_cast<const u64x2*>(fr + f);
-  return EncRec5{r[0], r[1], out_off[f]};
-}
-
-__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_encode5(
-    const gevws_out_frame* __restrict__ fr, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ out_off,
-    const uint32_t* __restrict__ tile_first, const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
-    uint32_t big_grid) {
-  constexpr int U = 4, WT = 8, WF = kEnc5Frames, NW = kUnmaskBlock / 64;
-  static_assert(WT * kTile / 16 == kEnc5Chunks && kEnc5Chunks == 8 * kUnmaskBlock, "8 chunks per thread");
-  __shared__ int32_t s_start[WF];
-  __shared__ int32_t s_pend[WF];
-  __shared__ uint8_t s_hlen[WF];
-  __shared__ uint64_t s_delta[WF];
-  __shared__ __attribute__((aligned(16))) uint16_t s_own[2 * kEnc5Chunks];
-  __shared__ uint32_t s_seed[2 * NW];
-  __shared__ uint32_t s_bnd[kEnc5Chunks];  // queued chunk: chunk | frame << 16 (~0: a group's filler)
-  __shared__ uint32_t s_nb;
-  __shared__ uint32_t s_tmap[kEnc5TmapN];
-  const EncWin W{s_start, s_pend, s_hlen, s_delta, nullptr, nullptr};
-  if (sum->status != GEVWS_OK) return;
-  const uint64_t total = sum->payload_bytes;  // wire bytes
-  const uint64_t nframes = sum->frames;
-  const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint32_t groups = active_groups(total, nframes, big_grid);
-  if (blockIdx.x >= groups) return;
-  const uint64_t per = (ntiles + groups - 1) / groups;
-  uint64_t t = (uint64_t)blockIdx.x * per;
-  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
-  {  // both chunk maps and their seeds start empty
-    const uint32_t tid = fresh_tid();
-    reinterpret_cast<u32x4*>(s_own)[tid] = u32x4{0, 0, 0, 0};
-    reinterpret_cast<u32x4*>(s_own + kEnc5Chunks)[tid] = u32x4{0, 0, 0, 0};
-    if (tid < 2 * NW) s_seed[tid] = 0;
-  }
-  __syncthreads();
-  uint64_t c_ps = 0, c_pe = 0, c_delta = 0;  // cached frame: payload [c_ps, c_pe) in wire coordinates
-  uint64_t pf_t = ~0ull, pf_a = 0, pf_b = 0;  // decision for tile pf_t, made during the previous window
-  bool pf_stream = false;
-  EncRec5 r0 = {};  // record pf_a + tid when !pf_stream
-  uint32_t buf = 0;
-  uint64_t tm0 = ~0ull;
-  auto cache_frame = [&](uint64_t f) {  // wave-uniform
-    const uint64_t* rec = reinterpret_cast<const uint64_t*>(fr + f);
-    const uint64_t w0 = uniform64(rec[0]), len = uniform64(rec[1]);
-    const uint64_t po = uniform64(rec[2]), pl = uniform64(rec[3]);
-    gevws_header h;
-    memcpy(&h, &w0, 8);
-    h.length = (int64_t)len;
-    c_ps = uniform64(out_off[f]) + enc_hlen(h);
-    c_pe = c_ps + pl;
-    c_delta = po - c_ps;
-  };
-  auto tmap_at = [&](uint64_t x) -> uint64_t {
-    if (tm0 == ~0ull || x < tm0 || x + 16 >= tm0 + kEnc5TmapN) {
-      __syncthreads();
-      tm0 = x;
-      for (uint32_t i = fresh_tid(); i < kEnc5TmapN; i += kUnmaskBlock) {
-        const uint64_t y = x + i;
-        s_tmap[i] = y < ntiles ? tile_first[y] : 0u;
-      }
-      __syncthreads();
-    }
-    return uniform32(s_tmap[x - tm0]);
-  };
-  auto decide = [&](uint64_t x, uint64_t& a, uint64_t& b, bool& stream) {
-    a = tmap_at(x);
-    stream = false;
-    if (x + U <= tend && tmap_at(x + U - 1) == a) {
-      cache_frame(a);
-      stream = x * kTile >= c_ps && (x + U) * kTile <= c_pe;
-    }
-    const uint64_t wt = (tend - x) < (uint64_t)WT ? (tend - x) : (uint64_t)WT;
-    b = x + wt < ntiles ? tmap_at(x + wt) : nframes - 1;
-  };
-  // the streaming step of k_encode: U tiles inside one payload
-  auto stream_tiles = [&](uint64_t base) {
-    u32x4 v[U];
-    const uint8_t* s0 = payload + (base + c_delta);
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(s0) & 15);  // wave-uniform
-    if (mis != 0) {
-      const uint32_t tid = fresh_tid(), wave = tid >> 6, lane = tid & 63;
-      const uint64_t wrel = (uint64_t)wave * U * 1024 + lane * 16;
-      const uint8_t* a = s0 + wrel - mis;
-      uint8_t* d = out + base + wrel;
-      const bool last = lane == 63;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + u * 1024));
-      u32x4 e = u32x4{0, 0, 0, 0};
-      if (last) e = *reinterpret_cast<const u32x4*>(a + (U - 1) * 1024 + 16);
-      u32x4 r = rot_next_lane(v[0]);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const u32x4 rn = u + 1 < U ? rot_next_lane(v[u + 1 < U ? u + 1 : u]) : e;
-        st16_nt(d + u * 1024, funnel16(v[u], last ? rn : r, mis));
-        r = rn;
-      }
-      return;
-    }
-    const uint32_t lane_off = fresh_tid() * 16;
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld16u(payload + (base + u * kTile + lane_off + c_delta));
-#pragma unroll
-    for (int u = 0; u < U; ++u) st16_nt(out + base + u * kTile + lane_off, v[u]);
-  };
-  while (t < tend) {
-    const uint64_t base = t * kTile;
-    if (t + U <= tend && base >= c_ps && base + U * kTile <= c_pe) {  // still inside the cached payload
-      stream_tiles(base);
-      t += U;
-      pf_t = ~0ull;
-      r0 = EncRec5{};
-      continue;
-    }
-    uint64_t a, b;
-    bool stream, have = false;
-    if (pf_t == t) {
-      a = pf_a;
-      b = pf_b;
-      stream = pf_stream;
-      have = !pf_stream;
-    } else {
-      decide(t, a, b, stream);
-    }
-    if (stream) {
-      stream_tiles(base);
-      t += U;
-      pf_t = ~0ull;
-      r0 = EncRec5{};
-      continue;
-    }
-    const uint64_t wt = (tend - t) < (uint64_t)WT ? (tend - t) : (uint64_t)WT;
-    const uint64_t wend_t = t + wt;
-    const uint64_t wbase = base;
-    const uint64_t F = b - a + 1;
-    if (F > (uint64_t)WF) {
-      // more than kEnc5Frames frames in the window (frames of a few bytes):
-      // one tile, per-lane global lookup and byte assembly (as k_encode)
-      const uint64_t p = t * kTile + fresh_tid() * 16;
-      if (p < total) {
-        uint64_t lo = tile_first[t];
-        uint64_t hi = (t + 1 < ntiles) ? (uint64_t)tile_first[t + 1] : nframes - 1;
-        while (lo < hi) {
-          const uint64_t mid = (lo + hi + 1) >> 1;
-          if (out_off[mid] <= p) lo = mid; else hi = mid - 1;
-        }
-        uint32_t w[4] = {0, 0, 0, 0};
-        uint64_t j = lo;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          while (j + 1 < nframes && out_off[j + 1] <= p + k) ++j;
-          const uint32_t byte = (p + k < total) ? enc_byte_global(fr, out_off, payload, j, p + k) : 0u;
-          w[k >> 2] |= byte << (8 * (k & 3));
-        }
-        *reinterpret_cast<u32x4*>(out + p) = u32x4{w[0], w[1], w[2], w[3]};
-      }
-      t += 1;
-      pf_t = ~0ull;
-      r0 = EncRec5{};
-      continue;
-    }
-    uint16_t* const own = s_own + buf * kEnc5Chunks;
-    uint32_t* const seed = s_seed + buf * NW;
-    __syncthreads();  // the previous window's readers are done with the tables and the queue
-    auto fill = [&](uint64_t i, const EncRec5& q) {
-      gevws_header h;
-      memcpy(&h, &q.h, 16);
-      const uint32_t hl = enc_hlen(h);
-      const int64_t st = (int64_t)(q.oo - wbase);
-      const int64_t end = st + hl + (int64_t)q.p[1];  // the next frame's start
-      s_start[i] = st < -64 ? -64 : (int32_t)st;
-      s_pend[i] = end > 0x7fffffffll ? 0x7fffffff : (int32_t)end;
-      s_hlen[i] = (uint8_t)hl;
-      s_delta[i] = q.p[0] - q.oo - hl;
-      // the last frame to start in its chunk marks it (the batch's last frame always)
-      if (st >= 0 && st < (int64_t)(WT * kTile)) {
-        const int64_t sc = st >> 4;
-        if (end >= (sc + 1) * 16 || a + i == nframes - 1) own[sc] = (uint16_t)(i + 1);
-      }
-      // the frame holding the byte before wave w's quarter seeds w's scan
-#pragma unroll
-      for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
-        const int64_t x = (int64_t)w * kEnc5Quarter * 16 - 1;
-        if (st <= x && x < end) seed[w] = (uint32_t)(i + 1);
-      }
-    };
-    const uint32_t tid = fresh_tid();
-    if (tid < F) fill(tid, have ? r0 : load_enc_rec(fr, out_off, a + tid));
-    for (uint64_t i = tid + kUnmaskBlock; i < F; i += kUnmaskBlock) fill(i, load_enc_rec(fr, out_off, a + i));
-    if (tid == 0) s_nb = 0;
-    __syncthreads();
-    {  // per-wave prefix max over the quarter's marks, seeded (as the unmask v5)
-      const uint32_t j = fresh_tid(), lane = j & 63, w = j >> 6;
-      u32x4 m = reinterpret_cast<const u32x4*>(own)[j];
-      uint32_t run[8];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        run[2 * k] = m[k] & 0xffffu;
-        run[2 * k + 1] = m[k] >> 16;
-      }
-#pragma unroll
-      for (int k = 1; k < 8; ++k) run[k] = run[k] > run[k - 1] ? run[k] : run[k - 1];
-      uint32_t inc = run[7];
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
-        if (lane >= (uint32_t)d) inc = inc > y ? inc : y;
-      }
-      uint32_t exc = (uint32_t)__shfl_up((int)inc, 1, 64);
-      const uint32_t sd = seed[w];
-      if (lane == 0) exc = 0;
-      exc = exc > sd ? exc : sd;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t lo16 = run[2 * k] > exc ? run[2 * k] : exc;
-        const uint32_t hi16 = run[2 * k + 1] > exc ? run[2 * k + 1] : exc;
-        m[k] = lo16 | (hi16 << 16);
-      }
-      reinterpret_cast<u32x4*>(own)[j] = m;
-      // (a zero made here: a loop-invariant zero vector was hoisted out of
-      // the loop and spilled, its reload waiting for every load in flight)
-      uint32_t z;
-      __asm__ volatile("v_mov_b32 %0, 0" : "=v"(z));
-      reinterpret_cast<u32x4*>(s_own + (buf ^ 1) * kEnc5Chunks)[j] = u32x4{z, z, z, z};
-      if (lane == 0) s_seed[(buf ^ 1) * NW + w] = 0;
-    }
-    // classify the lane's 8 chunks (wave w, step u: chunks 512 w + 64 u + lane);
-    // a chunk's frame is re-read from the map where it is needed (held across
-    // the queue pass, 8 more VGPRs spilled)
-    auto chunk_of = [&](int u) -> uint32_t {
-      const uint32_t tq = fresh_tid();
-      return (tq >> 6) * kEnc5Quarter + (uint32_t)u * 64 + (tq & 63);
-    };
-    auto frame_of = [&](uint32_t c) -> uint32_t {
-      const uint32_t o = own[c];
-      return o ? o - 1 : 0;
-    };
-    u32x4 v[WT];
-    uint32_t interior = 0, queued = 0;
-#pragma unroll
-    for (int u = 0; u < WT; ++u) {
-      const uint32_t c = chunk_of(u);
-      const int32_t rel = (int32_t)(c * 16);
-      const bool valid = (uint64_t)rel < wt * kTile && wbase + (uint64_t)rel < total;
-      const uint32_t lo = frame_of(c);
-      const bool in = valid && s_start[lo] + (int32_t)s_hlen[lo] <= rel && rel + 16 <= s_pend[lo];
-      interior |= (in ? 1u : 0u) << u;
-      queued |= (valid && !in ? 1u : 0u) << u;
-    }
-    // 64-byte groups holding a queued chunk go to the queue whole
-    {
-      const uint32_t lane = fresh_tid() & 63, g0 = lane & ~3u;
-#pragma unroll
-      for (int u = 0; u < WT; ++u) {
-        const uint64_t bal = __ballot((queued >> u) & 1u);  // whole wave active
-        const bool defer = ((bal >> g0) & 0xFull) != 0;     // (group-uniform)
-        uint32_t slot = 0;
-        if (defer && (lane & 3u) == 0) slot = atomicAdd(&s_nb, 4u);
-        slot = __shfl(slot, (int)g0);
-        if (defer) {
-          const uint32_t c = chunk_of(u);
-          const bool valid = (interior | queued) & (1u << u);
-          s_bnd[slot + (lane & 3u)] = valid ? c | (frame_of(c) << 16) : 0xffffffffu;
-          interior &= ~(1u << u);
-        }
-      }
-    }
-    // the interior loads (every lane loads; a non-interior chunk from payload[0])
-#pragma unroll
-    for (int u = 0; u < WT; ++u) {
-      const uint32_t c = chunk_of(u);
-      const bool in = (interior >> u) & 1u;
-      v[u] = ld16u(payload + (in ? wbase + (uint64_t)c * 16 + s_delta[frame_of(c)] : 0ull));
-    }
-    // decide the next step (and fetch the next window's records) while the
-    // payload loads are in flight
-    __asm__ volatile("" ::: "memory");
-    pf_t = ~0ull;
-    if (wend_t < tend) {
-      decide(wend_t, pf_a, pf_b, pf_stream);
-      pf_t = wend_t;
-      if (!pf_stream) {
-        const uint64_t nF = pf_b - pf_a + 1;
-        const uint32_t tid2 = fresh_tid();
-        if (tid2 < nF) r0 = load_enc_rec(fr, out_off, pf_a + tid2);
-      }
-    }
-    __syncthreads();  // the queue is complete
-    const uint32_t nb = s_nb;
-    auto assemble = [&](uint32_t q) -> u32x4 {
-      const int32_t rel = (int32_t)((q & 0xffffu) << 4);
-      uint32_t j0 = q >> 16;  // the frame holding the chunk's last byte ...
-      while (j0 > 0 && s_start[j0] > rel) --j0;  // ... back to the one holding its first
-      return enc_assemble<true>(rel, wbase + (uint64_t)rel, total, j0, (uint32_t)F, W, payload, fr, a);
-    };
-    const uint32_t i0 = fresh_tid();
-    u32x4 x0 = u32x4{0, 0, 0, 0};
-    uint32_t q0 = 0xffffffffu;
-    if (i0 < nb) {
-      q0 = s_bnd[i0];
-      if (q0 != 0xffffffffu) x0 = assemble(q0);
-    }
-#pragma unroll
-    for (int u = 0; u < WT; ++u)
-      if (interior & (1u << u)) st16_nt(out + wbase + (uint64_t)chunk_of(u) * 16, v[u]);
-    if (q0 != 0xffffffffu) st16_nt(out + wbase + (uint64_t)((q0 & 0xffffu) << 4), x0);
-    for (uint32_t i = i0 + kUnmaskBlock; i < nb; i += kUnmaskBlock) {
-      const uint32_t q = s_bnd[i];
-      if (q == 0xffffffffu) continue;  // a group's slot past the batch's end
-      st16_nt(out + wbase + (uint64_t)((q & 0xffffu) << 4), assemble(q));
-    }
-    buf ^= 1;
-    t = wend_t;
-  }
-}
-
-// The encode with one wave per step (k_encode6): every wave walks its own run
-// of tiles, ST = U / 4 tiles a step, with no workgroup barrier.  A step inside
-// one payload is streamed as in k_encode; otherwise the step's frames go into
-// the wave's LDS table, each frame that is the last to start in its chunk marks
-// that chunk in a one-byte-per-chunk map, and one per-wave prefix max turns the
-// marks into every chunk's frame (no search).  A chunk inside one payload is
-// loaded and stored; 64-byte groups holding any other chunk are queued in the
-// wave's LDS (slots from a ballot, no atomics) and assembled after the
-// interior loads are in flight, one chunk per lane.
+//  * Otherwise the step's frames (at most 16 U, one or two per lane) go into
+//    the wave's LDS table, each frame that is the last to start in its chunk
+//    marks that chunk in a one-byte-per-chunk map (its end, the next frame's
+//    start, lies in a later chunk: one writer per slot), and one per-wave
+//    prefix max turns the marks into every chunk's frame -- no search.  A
+//    chunk inside one payload is loaded (unaligned) and stored.  A 64-byte
+//    group holding any other chunk is queued whole in the wave's LDS (slots
+//    from a ballot, no atomics) and assembled after the interior loads are in
+//    flight, one chunk per lane: the frame holding the byte before the chunk
+//    and the next one, both payload loads issued together.  Queuing the whole
+//    group makes one store write its 64 bytes: otherwise every frame boundary
+//    left its line to HBM as two partial writes (C4: 46 M 32-byte write
+//    requests per launch; the encode 10.70 -> 9.11 ms, profiles/r02/r02_encode_ab_g64_*.json;
+//    queuing only the boundary chunks with plain stores for the shared lines
+//    measured slower again, profiles/r04/r04_encode6_dev.jsonl).
+// It replaced round 3's workgroup-window kernels k_encode (4-tile windows, a
+// binary search per chunk) and k_encode5 (8-tile windows with a chunk map):
+// C4 -9 %, C2 -7 %, C1-shaped -19 %, C5 -7 %, C3 equal (profiles/r04/r04_encode6_ab.jsonl).
 // LDS written by some lanes of a wave and read by others: the hardware keeps a
 // wave's LDS operations in order, the fence keeps the compiler from moving them.
 __device__ __forceinline__ void wave_lds_order() {
@@ -1503,12 +966,12 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
   signal_done(done, seq);
 }
 
-// GEVWS_TUNE_ENCODE_VARIANT: 0 = k_encode6 (two tiles a wave step when the
-// caller's capacity per frame exceeds kEnc6MinMeanBytes, else one; the run
-// mode chosen on the device), 1 = k_encode5, 2 = k_encode, 3 / 4 = k_encode6
-// with one / two tiles a step, 5 / 6 / 7 = two tiles a step in run mode 0 /
-// 1 / 2 (measurement).  DESIGN.md §5, profiles/r04/r04_encode6_ab.jsonl.
-constexpr int kNumEncodeVariants = 8;
+// GEVWS_TUNE_ENCODE_VARIANT: 0 = two tiles a wave step when the caller's
+// capacity per frame exceeds kEnc6MinMeanBytes, else one (C1-shaped 128-byte
+// frames 0.097 vs 0.104 ms, C4 8.83 vs 8.97, C2 0.431 vs 0.454), the run mode
+// chosen on the device; 1 / 2 = one / two tiles a step; 3 / 4 / 5 = two tiles
+// a step in run mode 0 / 1 / 2 (measurement).
+constexpr int kNumEncodeVariants = 6;
 constexpr uint64_t kEnc6MinMeanBytes = 256;
 
 }  // namespace
@@ -1545,34 +1008,24 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   if (nblk) k_enc_size<<<nblk, kWalkBlock, 0, st>>>(d_frames, n, blk, d_out_off, gate);
   k_scan_blocks<false><<<1, kScanBlock, 0, st>>>(blk, nblk, n, out_cap, d_summary);
   if (nblk) k_enc_emit<<<nblk, kWalkBlock, 0, st>>>(n, blk, d_summary, d_out_off, tile_first, gate, work);
-  const bool v6 = ctx->encode_variant == 0 || ctx->encode_variant >= 3;
-  const bool v5 = ctx->encode_variant == 1;
-  // the window path's occupancy (k_encode6 / k_encode5 / k_encode) and tiles per workgroup step
-  // k_encode6's step: two tiles a wave for frames of more than kEnc6MinMeanBytes (by capacity)
-  const bool u8 = ctx->encode_variant == 4 || ctx->encode_variant >= 5 ||
-                  (ctx->encode_variant == 0 && n && out_cap / n > kEnc6MinMeanBytes);
-  const uint64_t per_cu = v6 ? (u8 ? 4 : 8) : v5 ? 4 : 7;
-  const uint64_t wtiles = v6 ? (u8 ? 8 : 4) : v5 ? 8 : kWinTiles;
+  // k_encode6's step: two tiles a wave for frames of more than
+  // kEnc6MinMeanBytes (by the caller's capacity), at 4 workgroups per CU (121
+  // VGPRs), else one tile at 8 (64 VGPRs)
+  const int v = ctx->encode_variant;
+  const bool u8 = v == 2 || v >= 3 || (v == 0 && n && out_cap / n > kEnc6MinMeanBytes);
+  const uint64_t per_cu = u8 ? 4 : 8;
+  const uint64_t wtiles = u8 ? 8 : 4;  // tiles per workgroup step
   uint64_t grid = (out_cap / kTile + wtiles - 1) / wtiles;
   // (GEVWS_TUNE_UNMASK_GRID, when set, caps the encode's grid too: measurement)
   const uint64_t gcap = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : per_cu * (uint64_t)ctx->num_cus;
   if (grid > gcap) grid = gcap;
   if (grid < 1) grid = 1;
-  // every frame boundary takes the window path, which needs several
-  // workgroups per CU to hide its latency (C3: 22.6 ms at 4/CU vs 36 ms at
-  // 1/CU); it runs 7 per CU (C2 -18 %, C4 -4 % against 4,
-  // profiles/r01/r01_encode_ab_lds_*.json, r01_encode_ab_occ_*.json), and
-  // batches of big frames (mean >= kBigFrameBytes) keep 4 per CU (the rest
-  // return at once)
+  // batches of big frames (mean >= kBigFrameBytes) keep 4 workgroups per CU
+  // (the rest return at once)
   const uint32_t big = grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
-  if (v6) {
-    const int mode = ctx->encode_variant >= 5 ? ctx->encode_variant - 5 : -1;
-    (u8 ? k_encode6<8> : k_encode6<4>)<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(
-        d_frames, d_payload, d_out_off, tile_first, d_summary, d_out, big, work, mode);
-  } else {
-    auto kfn = v5 ? k_encode5 : k_encode;
-    kfn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_frames, d_payload, d_out_off, tile_first, d_summary, d_out, big);
-  }
+  const int mode = v >= 3 ? v - 3 : -1;
+  (u8 ? k_encode6<8> : k_encode6<4>)<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(
+      d_frames, d_payload, d_out_off, tile_first, d_summary, d_out, big, work, mode);
   GEVWS_HIP(hipGetLastError());
   return mark_last(ctx, st);
 }

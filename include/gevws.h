@@ -157,10 +157,11 @@ int gevws_stream_cu_count(int device, void *stream);
  * windows for batches of equal-size frames, v5 pipelined 8-tile windows with
  * a chunk -> frame map for mixed sizes; 1 = v5 for every batch),
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto; when set it caps the
- * encode's grid too), GEVWS_TUNE_ENCODE_VARIANT the encode kernel (0 = the
- * default: 8-tile pipelined windows with a chunk map when out_cap / n >= 1 024
- * bytes, else 4-tile windows at seven workgroups per CU; 1 = always the
- * former, 2 = always the latter), GEVWS_TUNE_WALK_VARIANT the header walk (0 = the
+ * encode's grid too), GEVWS_TUNE_ENCODE_VARIANT the encode's step (0 = the
+ * default: two 4 KiB tiles a wave step when out_cap / n > 256 bytes, else
+ * one, and the waves' runs of tiles chosen on the device; 1 / 2 = always one /
+ * two tiles; 3 / 4 / 5 = two tiles with contiguous / cyclic / counter runs),
+ * GEVWS_TUNE_WALK_VARIANT the header walk (0 = the
  * default choice per batch; 1 = plain chain walk without the uniform-stream
  * speculation; 2 = no per-frame entries, the record pass re-walks every
  * chain; 3 = the entries through the writer wave whatever the batch size),

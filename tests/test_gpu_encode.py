@@ -14,13 +14,13 @@ from tests._helpers import gpu_decode, host_result, pack_streams, random_stream
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7], ids=["auto", "k_encode5", "k_encode", "k_encode6_4", "k_encode6_8", "k_encode6_8_contiguous", "k_encode6_8_cyclic", "k_encode6_8_counter"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5],
+                ids=["auto", "one_tile", "two_tiles", "two_tiles_contiguous", "two_tiles_cyclic", "two_tiles_counter"])
 def enc_variant(request, engine):
-    """Every encode kernel (GEVWS_TUNE_ENCODE_VARIANT): 0 = the default
-    (k_encode6, its step and run mode chosen per batch), 1 = k_encode5 (8-tile
-    windows at 4 workgroups per CU), 2 = k_encode (4-tile windows at 7), 3 / 4
-    = k_encode6 with one / two tiles a wave step, 5 / 6 / 7 = two tiles a step
-    with contiguous / cyclic / counter runs."""
+    """Every form of the encode kernel k_encode6 (GEVWS_TUNE_ENCODE_VARIANT):
+    0 = the default (its step and run mode chosen per batch), 1 / 2 = one /
+    two tiles a wave step, 3 / 4 / 5 = two tiles a step with contiguous /
+    cyclic / counter runs."""
     try:
         engine.set_tuning(gev_amd._abi.TUNE_ENCODE_VARIANT, request.param)
     except RuntimeError:
@@ -113,9 +113,11 @@ def test_encode_window_queue_at_capacity(engine, enc_variant):
     rng = np.random.default_rng(1234)
     for wl, n in [(16, 1024), (16, 1025), (32, 512), (32, 513), (17, 963), (24, 682), (33, 1000),
                   (16, 1024 * 3), (32, 512 * 5),
-                  # k_encode5's 8-tile windows: 1 024 frames of 32 B fill its table, 33 / 40 / 64 B
-                  # put a boundary in every 64-byte group (its whole 2 048-chunk queue), 16 B overflow
-                  (32, 1024), (32, 1025), (33, 2000), (40, 1700), (64, 1100), (16, 2048 * 2)]:
+                  # 33 / 40 / 64 B put a boundary in every 64-byte group (a step's whole queue)
+                  (32, 1024), (32, 1025), (33, 2000), (40, 1700), (64, 1100), (16, 2048 * 2),
+                  # k_encode6's step tables (64 frames a tile, 128 a two-tile step): 64-66 B
+                  # frames put 63-65 frames in a tile, 70 B about 118 in a step
+                  (64, 2000), (65, 2000), (66, 2000), (70, 3000)]:
         fr, pay = _uniform_frames(wl, n, rng)
         _encode_check(engine, fr, pay, f"{wl}B x {n}")
     lens = np.concatenate([rng.integers(0, 4, 200), [20000], rng.integers(0, 14, 700), [9000],
