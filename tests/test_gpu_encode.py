@@ -71,6 +71,46 @@ def test_encode_random_and_tiny_frames(engine, enc_variant):
     _encode_random(engine)
 
 
+def test_encode_capacity_error_leaves_wire_sizes(engine, enc_variant):
+    """A wire total past out_cap: GEVWS_ERR_CAPACITY, the summary still holds
+    the totals, and d_out_off[f] holds frame f's wire size h + L (the contract
+    of include/gevws.h) -- 20 000 frames over several offset-pass
+    workgroups.  The exact capacity then encodes."""
+    import torch
+    rng = np.random.default_rng(77)
+    n = 20000
+    lens = rng.integers(0, 400, n)
+    lens[rng.integers(0, n, 20)] = rng.integers(126, 70000, 20)  # 4- and 10-byte headers too
+    payload = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    hd = np.array([np.frombuffer(wo.Header(True, 0, 2, bool(i % 3 == 0), b"\1\2\3\4", int(L)).pack(), np.uint8)
+                   for i, L in enumerate(lens)])
+    fr = _records(hd, offs, lens)
+    want, woff = ref.encode_batch(fr, payload)
+    total = int(want.size)
+    sizes = np.diff(np.append(woff, np.uint64(total)))
+    dev = _dev(engine)
+    d_fr = torch.from_numpy(fr.view(np.uint8).reshape(-1, 32).copy()).to(dev)
+    d_pay = torch.from_numpy(np.concatenate([payload, np.zeros(16, np.uint8)])).to(dev)
+    wire = torch.zeros(total + gev_amd._abi.OUT_PAD, dtype=torch.uint8, device=dev)
+    off = torch.zeros(n, dtype=torch.int64, device=dev)
+    summ = torch.zeros(64, dtype=torch.uint8, device=dev)
+    for cap in (total - 1, total // 2, 0):
+        engine.encode_async(d_fr, n, d_pay, wire, cap, off, summ)
+        torch.cuda.synchronize(dev)
+        s = summ.cpu().numpy().view(gev_amd.SUMMARY_DTYPE)[0]
+        assert int(s["status"]) == gev_amd.ERR_CAPACITY, cap
+        assert int(s["frames"]) == n and int(s["payload_bytes"]) == total, cap
+        assert int(s["payload_len"]) == int(lens.sum()), cap
+        assert np.array_equal(off.cpu().numpy().astype(np.uint64), sizes), cap
+    engine.encode_async(d_fr, n, d_pay, wire, total, off, summ)
+    torch.cuda.synchronize(dev)
+    s = summ.cpu().numpy().view(gev_amd.SUMMARY_DTYPE)[0]
+    assert int(s["status"]) == 0 and int(s["payload_bytes"]) == total
+    assert np.array_equal(off.cpu().numpy().astype(np.uint64), woff)
+    assert np.array_equal(wire[:total].cpu().numpy(), want)
+
+
 def _encode_random(engine):
     rng = np.random.default_rng(41)
     for trial, (n, maxlen) in enumerate([(1, 0), (5, 10), (300, 3000), (3000, 0), (5000, 20), (200, 70000),
