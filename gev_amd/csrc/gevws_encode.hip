@@ -63,6 +63,8 @@ constexpr int kEncSlabs = 16;
 // loop: C5 emit 79 -> 16 us but C4 138 -> 466 us
 // (profiles/r03/r03_encode_emit_lane16_*), so 4.
 constexpr int kEncLaneTiles = 4;
+// k_encode6's run mode 2: one run counter per XCD, 64 bytes apart (zeroed by k_enc_emit)
+constexpr uint32_t kEnc6Counters = 8;
 // The frame count of a chained pass (decode -> dispatch -> encode with no host
 // round trip): the producing step's summary gates the consumer -- its frames,
 // or none when it failed (a capacity error leaves stale records behind).
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_enc_emit(uint64_t n,
                                                          uint32_t* __restrict__ tile_first,
                                                          const gevws_summary* __restrict__ gate = nullptr,
                                                          uint32_t* __restrict__ work = nullptr) {
-  if (work && blockIdx.x == 0 && threadIdx.x == 0) *work = 0;  // k_encode6's run counter
+  if (work && blockIdx.x == 0 && threadIdx.x < kEnc6Counters) work[threadIdx.x * 16] = 0;  // k_encode6's run counters
   if (sum->status != GEVWS_OK) return;
   n = gated_count(n, gate);
   const uint64_t f0 = (uint64_t)blockIdx.x * kWalkBlock * kEncSlabs + threadIdx.x;
@@ -339,12 +341,16 @@ __device__ __forceinline__ void wave_lds_order() {
 //     the streaming path: long runs keep DRAM pages open);
 //  1  each wave takes every nwaves-th run of K tiles (K <= kEnc6Run, at least
 //     8 runs a wave): a run's cost follows the local frame density, and runs
-//     spread over the whole batch even it out;
-//  2  runs of K = kEnc6Run tiles from a work counter (one lane's vector atomic
-//     per run; k_enc_emit zeroes it) -- batches of at least kEnc6DynRuns runs
-//     a wave, where the atomics are few against the work they balance.
+//     spread over the whole batch even it out -- small batches (fewer than
+//     kEnc6CounterMinTiles tiles a wave);
+//  2  runs of kEnc6CounterRun tiles from a work counter, one counter per XCD
+//     over its eighth of the tiles (one lane's vector atomic per run; k_enc_emit
+//     zeroes them) -- every other batch.  One counter for the whole grid
+//     saturated at runs of 4 tiles (C4 14.3 ms); eight keep C4 at 8.2 ms
+//     against 9.0 with runs of 64 (profiles/r04/r04_encode6_counter_ab.jsonl).
 constexpr uint64_t kEnc6Run = 64;
-constexpr uint64_t kEnc6DynRuns = 8;
+constexpr uint64_t kEnc6CounterRun = 4;
+constexpr uint64_t kEnc6CounterMinTiles = 16;  // per wave, for mode 2
 template <int U>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(U == 4 ? 8 : 4))) void k_encode6(
     const gevws_out_frame* __restrict__ fr, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ out_off,
@@ -371,13 +377,21 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(U 
   const uint64_t per = (ntiles + nwaves - 1) / nwaves;
   const uint64_t gw = (uint64_t)blockIdx.x * NW + w;
   if (mode < 0)
-    mode = total / nframes >= kBigFrameBytes ? 0 : (ntiles >= kEnc6DynRuns * kEnc6Run * nwaves ? 2 : 1);
+    mode = total / nframes >= kBigFrameBytes ? 0 : (ntiles >= kEnc6CounterMinTiles * nwaves ? 2 : 1);
   uint64_t t = mode ? 0 : gw * per;
   uint64_t tend = mode ? 0 : (t + per < ntiles ? t + per : ntiles);
   // modes 1 / 2: run length K (a multiple of the step) and the wave's next run
   uint64_t K = ntiles / (nwaves * 8);
   K = K > kEnc6Run ? kEnc6Run : K;
   K = K < (uint64_t)ST ? (uint64_t)ST : K - K % ST;
+  if (mode == 2 && groups < kEnc6Counters) mode = 1;  // (every counter needs its workgroups)
+  if (mode == 2) K = kEnc6CounterRun;
+  // mode 2: the workgroups of each XCD (blockIdx.x mod 8, the dispatch's
+  // round robin) share one counter over their eighth of the tiles
+  const uint32_t xc = blockIdx.x % kEnc6Counters;
+  const uint64_t segn = ((ntiles + kEnc6Counters - 1) / kEnc6Counters + K - 1) / K * K;
+  const uint64_t seg0 = xc * segn < ntiles ? xc * segn : ntiles;
+  const uint64_t seg1 = seg0 + segn < ntiles ? seg0 + segn : ntiles;
   uint64_t run = gw;
   uint8_t* const mb = reinterpret_cast<uint8_t*>(s_map[w]);
   uint64_t c_f = ~0ull, c_ps = 0, c_pe = 0, c_delta = 0;  // cached frame: payload [c_ps, c_pe) in wire coordinates
@@ -386,8 +400,11 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(U 
       if (mode == 0) break;
       if (mode == 2) {
         uint32_t g = 0;
-        if ((fresh_tid() & 63) == 0) g = atomicAdd(work, 1u);
-        run = uniform32((uint32_t)__shfl((int)g, 0, 64));
+        if ((fresh_tid() & 63) == 0) g = atomicAdd(work + xc * 16, 1u);
+        t = seg0 + (uint64_t)uniform32((uint32_t)__shfl((int)g, 0, 64)) * K;
+        if (t >= seg1) break;
+        tend = t + K < seg1 ? t + K : seg1;
+        continue;
       }
       t = run * K;
       if (t >= ntiles) break;
@@ -971,7 +988,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
 // frames 0.097 vs 0.104 ms, C4 8.83 vs 8.97, C2 0.431 vs 0.454), the run mode
 // chosen on the device; 1 / 2 = one / two tiles a step; 3 / 4 / 5 = two tiles
 // a step in run mode 0 / 1 / 2 (measurement).
-constexpr int kNumEncodeVariants = 6;
+constexpr int kNumEncodeVariants = 7;
 constexpr uint64_t kEnc6MinMeanBytes = 256;
 
 }  // namespace
@@ -1000,7 +1017,7 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   int r = order_after_last(ctx, st);
   if (r != GEVWS_OK) return r;
   const size_t tile_bytes = (ntiles_cap * sizeof(uint32_t) + 255) & ~size_t(255);
-  r = ensure_scratch(ctx, blk_bytes + tile_bytes + 256);
+  r = ensure_scratch(ctx, blk_bytes + tile_bytes + kEnc6Counters * 64);
   if (r != GEVWS_OK) return r;
   uint64_t* blk = reinterpret_cast<uint64_t*>(ctx->scratch);
   uint32_t* tile_first = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ctx->scratch) + blk_bytes);
@@ -1012,7 +1029,7 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   // kEnc6MinMeanBytes (by the caller's capacity), at 4 workgroups per CU (121
   // VGPRs), else one tile at 8 (64 VGPRs)
   const int v = ctx->encode_variant;
-  const bool u8 = v == 2 || v >= 3 || (v == 0 && n && out_cap / n > kEnc6MinMeanBytes);
+  const bool u8 = v == 2 || (v >= 3 && v < 6) || (v == 0 && n && out_cap / n > kEnc6MinMeanBytes);
   const uint64_t per_cu = u8 ? 4 : 8;
   const uint64_t wtiles = u8 ? 8 : 4;  // tiles per workgroup step
   uint64_t grid = (out_cap / kTile + wtiles - 1) / wtiles;
@@ -1023,7 +1040,7 @@ static int encode_impl(gevws_ctx* ctx, void* stream, const gevws_out_frame* d_fr
   // batches of big frames (mean >= kBigFrameBytes) keep 4 workgroups per CU
   // (the rest return at once)
   const uint32_t big = grid > 4ull * ctx->num_cus ? 4u * (uint32_t)ctx->num_cus : 0u;
-  const int mode = v >= 3 ? v - 3 : -1;
+  const int mode = v == 6 ? 1 : v >= 3 ? v - 3 : -1;  // 6: MEASUREMENT
   (u8 ? k_encode6<8> : k_encode6<4>)<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(
       d_frames, d_payload, d_out_off, tile_first, d_summary, d_out, big, work, mode);
   GEVWS_HIP(hipGetLastError());
