@@ -37,6 +37,7 @@ struct gevws_ctx {
   uint64_t stats_conns = 0, prev_frames_per_conn = 0, prev_frame_bytes = 0;
   bool prev_mixed = false;
   uint32_t last_unmask_grid = 0;  // workgroups of the last decode's unmask launch
+  uint32_t* unmask_runs = nullptr;  // the unmask v5 path's per-XCD run counters (decode scratch)
   uint32_t last_ks = 1;    // lanes per connection of the last multi-kernel decode's walk
   uint32_t split_lanes = 0;  // lanes per connection (k_walk_split); 0 = auto, 1 = off
   uint64_t split_min_bytes = kSplitMinBytes;        // split walk: bytes per segment at least

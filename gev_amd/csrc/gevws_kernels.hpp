@@ -290,6 +290,15 @@ constexpr uint64_t kBigFrameBytes = 48 * 1024;
 // (profiles/r02/r02_grid_sweep.jsonl)
 constexpr uint32_t kWideGridPerCU = 32;
 constexpr uint64_t kWideGridTiles = 2ull << 20;
+// The unmask v5 path's runs: the workgroups of each XCD (blockIdx.x mod 8, the
+// dispatch's round robin) take runs of kUnmaskRun tiles of their eighth of the
+// output from one counter (k_walk_bases zeroes them) instead of one contiguous
+// run each -- a run's cost follows the local frame density, and short runs
+// even it out (C4 7.44 -> 6.90 ms, its 2-way share 4.28 -> 3.72, 4-way 2.05
+// -> 1.86; runs of 32 / 64 tiles in between; profiles/r04/r04_unmask_counter_ab.jsonl).
+// One counter per XCD: one for the whole grid saturates (k_encode6 measured it).
+constexpr uint32_t kUnmaskRunCounters = 8;
+constexpr uint64_t kUnmaskRun = 16;
 
 // Workgroups that take a run of the output: big_grid (low 16 bits: one per CU)
 // for batches of big frames, else the whole grid -- or, when the host

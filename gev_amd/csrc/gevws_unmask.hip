@@ -309,14 +309,15 @@ struct WinLds5 {
   uint32_t* key;    // [kWin5Frames]
   uint16_t* own;    // [2][kWinChunks] window chunk -> frame index + 1 (marks, then their prefix max)
   uint32_t* wtot;   // [2][kUnmaskBlock / 64] per map: frame index + 1 covering each wave quarter's first chunk
-  uint32_t* tmap;   // [kTmapN] tile_first[tm0 ...]
+  uint32_t* tmap;   // [kTmapN + 1] tile_first[tm0 ...], then the run index of a grab
 };
 
 template <int U>
 __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
-                                               uint32_t big_grid, const WinLds5& L, bool wide = false) {
+                                               uint32_t big_grid, const WinLds5& L, bool wide = false,
+                                               uint32_t* __restrict__ runs = nullptr) {
   constexpr int WT = 8;
   static_assert(WT * kTile / 16 == kWinChunks && kWinChunks == 8 * kUnmaskBlock, "8 chunks per thread");
   if (sum->status != GEVWS_OK) return;
@@ -326,8 +327,15 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
   const uint32_t groups = active_groups(total, nframes, big_grid, wide);
   if (blockIdx.x >= groups) return;
   const uint64_t per = (ntiles + groups - 1) / groups;
-  uint64_t t = (uint64_t)blockIdx.x * per;
-  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+  // counter runs (kUnmaskRun tiles of this XCD's eighth) when every counter
+  // has workgroups, else one contiguous run per workgroup
+  const bool dyn = runs != nullptr && groups >= kUnmaskRunCounters;
+  uint64_t t = dyn ? 0 : (uint64_t)blockIdx.x * per;
+  uint64_t tend = dyn ? 0 : (t + per < ntiles ? t + per : ntiles);
+  const uint32_t xc = blockIdx.x % kUnmaskRunCounters;
+  const uint64_t segn = ((ntiles + kUnmaskRunCounters - 1) / kUnmaskRunCounters + kUnmaskRun - 1) / kUnmaskRun * kUnmaskRun;
+  const uint64_t seg0 = xc * segn < ntiles ? xc * segn : ntiles;
+  const uint64_t seg1 = seg0 + segn < ntiles ? seg0 + segn : ntiles;
   {  // both chunk maps (and their wave seeds) start empty
     const uint32_t tid = fresh_tid();
     reinterpret_cast<u32x4*>(L.own)[tid] = u32x4{0, 0, 0, 0};
@@ -380,6 +388,17 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
     const uint64_t wt = (tend - x) < (uint64_t)WT ? (tend - x) : (uint64_t)WT;
     b = x + wt < ntiles ? tmap_at(x + wt) : nframes - 1;
   };
+  for (;;) {
+  if (dyn) {  // the next run: thread 0's vector atomic, through LDS
+    __syncthreads();
+    if (threadIdx.x == 0) L.tmap[kTmapN] = atomicAdd(runs + xc * 16, 1u);
+    __syncthreads();
+    t = seg0 + (uint64_t)L.tmap[kTmapN] * kUnmaskRun;
+    if (t >= seg1) break;
+    tend = t + kUnmaskRun < seg1 ? t + kUnmaskRun : seg1;
+    pf_t = ~0ull;
+    r0 = WinRec{};
+  }
   while (t < tend) {
     const uint64_t base = t * kTile;
     if (t + U <= tend && base >= f_po && base + U * kTile <= f_end) {  // still inside the cached frame
@@ -533,6 +552,8 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
     buf ^= 1;
     t = wend_t;
   }
+  if (!dyn) break;
+  }
 }
 
 // The default unmask: the batch's own statistics pick the window scheme --
@@ -543,7 +564,7 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
 // budget, the choice is a uniform branch on the summary the walk wrote.
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto5(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
-    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs) {
   static_assert(kWinFrames == kWin5Frames, "one frame table for both bodies");
   __shared__ uint32_t s_start[kWinFrames];
   __shared__ int32_t s_lend[kWinFrames];
@@ -551,29 +572,29 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   __shared__ uint32_t s_key[kWinFrames];
   __shared__ __attribute__((aligned(16))) uint16_t s_own[2 * kWinChunks];
   __shared__ uint32_t s_wtot[2 * (kUnmaskBlock / 64)];
-  __shared__ uint32_t s_tmap[kTmapN];
+  __shared__ uint32_t s_tmap[kTmapN + 1];
   if (2 * sum->run_frames >= sum->frames)
     unmask_v3_body<16>(in, frames, tile_first, sum, out, big_grid, WinLds{s_start, s_lend, s_delta, s_key});
   else
     unmask_v5_body<16>(in, frames, tile_first, sum, out, big_grid,
                        WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap},
-                       sum->payload_bytes / kTile < kWideGridTiles);
+                       sum->payload_bytes / kTile < kWideGridTiles, runs);
 }
 
 // v5 for every batch (GEVWS_TUNE_UNMASK_VARIANT 1): the mixed-size path on any
 // batch, so the parity tests run it over equal-size frames too.
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_v5(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
-    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid) {
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs) {
   __shared__ int32_t s_lend[kWin5Frames];
   __shared__ uint64_t s_delta[kWin5Frames];
   __shared__ uint32_t s_key[kWin5Frames];
   __shared__ __attribute__((aligned(16))) uint16_t s_own[2 * kWinChunks];
   __shared__ uint32_t s_wtot[2 * (kUnmaskBlock / 64)];
-  __shared__ uint32_t s_tmap[kTmapN];
+  __shared__ uint32_t s_tmap[kTmapN + 1];
   unmask_v5_body<16>(in, frames, tile_first, sum, out, big_grid,
                      WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap},
-                     sum->payload_bytes / kTile < kWideGridTiles);
+                     sum->payload_bytes / kTile < kWideGridTiles, runs);
 }
 
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
@@ -605,12 +626,13 @@ __global__ __launch_bounds__(256) void k_cipher(uint8_t* __restrict__ p, uint64_
 }
 
 using UnmaskFn = void (*)(const uint8_t*, const gevws_frame*, const uint32_t*, const gevws_summary*, uint8_t*,
-                         uint32_t);
+                         uint32_t, uint32_t*);
 struct UnmaskVariant {
   UnmaskFn fn;
   int unroll;
   const char* name;
   bool wide = false;  // may launch the wide grid (k_unmask_auto)
+  bool runs = true;   // the v5 path's counter runs (else one contiguous run per workgroup)
 };
 // Variant 0 is the default (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 // The measurement variants of rounds 1-3 (v3 / v4 window shapes, interleaved
@@ -622,6 +644,8 @@ const UnmaskVariant kUnmaskVariants[] = {
      "map and the tile map cached in LDS) otherwise; non-temporal streaming and window loads; a wide grid for a "
      "smaller batch of mixed sizes after one on this context", true},
     {k_unmask_v5, 16, "v5 for every batch (the default's mixed-batch path alone)", true},
+    {k_unmask_auto5, 16, "the default with one contiguous run per workgroup on the v5 path (rounds 1-3; measurement)",
+     true, false},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
@@ -652,7 +676,8 @@ int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const ui
   if (grid < 1) grid = 1;
   ctx->last_unmask_grid = (uint32_t)grid;
   v.fn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary, d_payload,
-                                                ctx->unmask_grid ? 0u : ucus | (wide ? (uint32_t)norm << 16 : 0u));
+                                                ctx->unmask_grid ? 0u : ucus | (wide ? (uint32_t)norm << 16 : 0u),
+                                                v.runs ? ctx->unmask_runs : nullptr);
   return GEVWS_OK;
 }
 

@@ -877,7 +877,11 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_co
                                                             const uint64_t* __restrict__ blk,
                                                             const gevws_summary* __restrict__ sum,
                                                             uint8_t* __restrict__ rec_flags, uint32_t cpb,
-                                                            uint64_t* __restrict__ stats = nullptr) {
+                                                            uint64_t* __restrict__ stats = nullptr,
+                                                            uint32_t* __restrict__ runs = nullptr) {
+  // the unmask's per-XCD run counters start at zero (before the capacity check:
+  // the unmask reads them whatever the status)
+  if (runs && blockIdx.x == 0 && threadIdx.x < kUnmaskRunCounters) runs[threadIdx.x * 16] = 0;
   if (stats && blockIdx.x == 0 && threadIdx.x == 0) {  // the context's history (split walk, D, wide grid)
     stats[0] = sum->frames;
     stats[1] = sum->payload_len;
@@ -1410,13 +1414,16 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   // + one sink slot per walk lane after the table (k_walk_count / k_walk_split)
   int r = order_after_last(ctx, st);
   if (r != GEVWS_OK) return r;
-  r = ensure_scratch(ctx, blk_bytes + tile_bytes + flag_bytes + seg_bytes + (n_entries + n_v) * sizeof(WalkEntry));
+  const size_t run_bytes = kUnmaskRunCounters * 64;  // the unmask's run counters, 64 bytes apart
+  r = ensure_scratch(ctx, blk_bytes + tile_bytes + run_bytes + flag_bytes + seg_bytes +
+                              (n_entries + n_v) * sizeof(WalkEntry));
   if (r != GEVWS_OK) return r;
   char* sp = reinterpret_cast<char*>(ctx->scratch);
   uint64_t* blk = reinterpret_cast<uint64_t*>(sp);
   uint32_t* tile_first = reinterpret_cast<uint32_t*>(sp + blk_bytes);
-  uint8_t* rec_flags = reinterpret_cast<uint8_t*>(sp + blk_bytes + tile_bytes);
-  char* segp = sp + blk_bytes + tile_bytes + flag_bytes;
+  ctx->unmask_runs = reinterpret_cast<uint32_t*>(sp + blk_bytes + tile_bytes);
+  uint8_t* rec_flags = reinterpret_cast<uint8_t*>(sp + blk_bytes + tile_bytes + run_bytes);
+  char* segp = sp + blk_bytes + tile_bytes + run_bytes + flag_bytes;
   gevws_conn_in* segs = reinterpret_cast<gevws_conn_in*>(segp);
   gevws_conn_out* sout = reinterpret_cast<gevws_conn_out*>(segp + n_v * sizeof(gevws_conn_in));
   uint8_t* srec = reinterpret_cast<uint8_t*>(segp + n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out)));
@@ -1464,7 +1471,8 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   if (!fused) k_scan_blocks<true, kDecFields><<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
   if (ev) GEVWS_HIP(hipEventRecord(ev[2], st));
   if (nblk) {
-    k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb_w, ctx->d_stats);
+    k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb_w, ctx->d_stats,
+                                               ctx->unmask_runs);
     ctx->stats_pending = true;
     ctx->stats_conns = n_conns;
     // the record pass walks the segments when the walk was split
