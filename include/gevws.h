@@ -155,7 +155,9 @@ int gevws_stream_cu_count(int device, void *stream);
 /* Tuning knobs for measurement and parity tests (defaults are the tuned
  * choice): GEVWS_TUNE_UNMASK_VARIANT the unmask kernel (0 = default: v3 4-tile
  * windows for batches of equal-size frames, v5 pipelined 8-tile windows with
- * a chunk -> frame map for mixed sizes; 1 = v5 for every batch),
+ * a chunk -> frame map for mixed sizes, its workgroups taking runs of 16
+ * tiles from a per-XCD counter; 1 = v5 for every batch; 2 = the default with
+ * one contiguous run per workgroup on the v5 path),
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto; when set it caps the
  * encode's grid too), GEVWS_TUNE_ENCODE_VARIANT the encode's step (0 = the
  * default: two 4 KiB tiles a wave step when out_cap / n > 256 bytes, else
