@@ -299,6 +299,7 @@ constexpr uint64_t kWideGridTiles = 2ull << 20;
 // One counter per XCD: one for the whole grid saturates (k_encode6 measured it).
 constexpr uint32_t kUnmaskRunCounters = 8;
 constexpr uint64_t kUnmaskRun = 16;
+constexpr uint64_t kUnmaskRunMinTiles = 64;  // the v3 path's counter runs: tiles a workgroup at least
 
 // Workgroups that take a run of the output: big_grid (low 16 bits: one per CU)
 // for batches of big frames, else the whole grid -- or, when the host

@@ -166,7 +166,8 @@ template <int U>
 __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames,
                                                const uint32_t* __restrict__ tile_first,
                                                const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out,
-                                               uint32_t big_grid, const WinLds& L) {
+                                               uint32_t big_grid, const WinLds& L, uint32_t* __restrict__ runs = nullptr,
+                                               uint32_t* __restrict__ s_run = nullptr) {
   constexpr int WT = kWinTiles;
   uint32_t* const s_start = L.start;
   int32_t* const s_lend = L.lend;
@@ -179,12 +180,31 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
   const uint32_t groups = active_groups(total, nframes, big_grid);
   if (blockIdx.x >= groups) return;
   const uint64_t per = (ntiles + groups - 1) / groups;
-  uint64_t t = (uint64_t)blockIdx.x * per;
-  const uint64_t tend = t + per < ntiles ? t + per : ntiles;
+  // counter runs as the v5 path's, for batches of frames below kBigFrameBytes
+  // with at least kUnmaskRunMinTiles tiles a workgroup: C2 -4 %, C5 equal;
+  // big frames want long runs (C3 +15 %) and small batches few (C1-shaped +13
+  // %, profiles/r04/r04_unmask_counter_ab.jsonl)
+  const bool dyn = runs != nullptr && groups >= kUnmaskRunCounters && nframes && total / nframes < kBigFrameBytes &&
+                   ntiles >= kUnmaskRunMinTiles * groups;
+  uint64_t t = dyn ? 0 : (uint64_t)blockIdx.x * per;
+  uint64_t tend = dyn ? 0 : (t + per < ntiles ? t + per : ntiles);
+  const uint32_t xc = blockIdx.x % kUnmaskRunCounters;
+  const uint64_t segn = ((ntiles + kUnmaskRunCounters - 1) / kUnmaskRunCounters + kUnmaskRun - 1) / kUnmaskRun * kUnmaskRun;
+  const uint64_t seg0 = xc * segn < ntiles ? xc * segn : ntiles;
+  const uint64_t seg1 = seg0 + segn < ntiles ? seg0 + segn : ntiles;
   const uint32_t lane_off = threadIdx.x * 16;
   uint64_t f_po = 0, f_end = 0, f_src = 0;
   int64_t f_len = 0;
   uint32_t f_key = 0;
+  for (;;) {
+  if (dyn) {
+    __syncthreads();
+    if (threadIdx.x == 0) *s_run = atomicAdd(runs + xc * 16, 1u);
+    __syncthreads();
+    t = seg0 + (uint64_t)*s_run * kUnmaskRun;
+    if (t >= seg1) break;
+    tend = t + kUnmaskRun < seg1 ? t + kUnmaskRun : seg1;
+  }
   while (t < tend) {
     const uint64_t base = t * kTile;
     if (base >= f_end) {  // workgroup-uniform: refresh the cached frame (scalar loads)
@@ -259,6 +279,8 @@ __device__ __forceinline__ void unmask_v3_body(const uint8_t* __restrict__ in, c
     const uint64_t p = base + lane_off;
     if (p < total) unmask_chunk_lookup(in, frames, tile_first, t, ntiles, nframes, p, out);
     t += 1;
+  }
+  if (!dyn) break;
   }
 }
 
@@ -574,7 +596,8 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   __shared__ uint32_t s_wtot[2 * (kUnmaskBlock / 64)];
   __shared__ uint32_t s_tmap[kTmapN + 1];
   if (2 * sum->run_frames >= sum->frames)
-    unmask_v3_body<16>(in, frames, tile_first, sum, out, big_grid, WinLds{s_start, s_lend, s_delta, s_key});
+    unmask_v3_body<16>(in, frames, tile_first, sum, out, big_grid, WinLds{s_start, s_lend, s_delta, s_key}, runs,
+                       s_tmap + kTmapN);
   else
     unmask_v5_body<16>(in, frames, tile_first, sum, out, big_grid,
                        WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap},
