@@ -30,7 +30,7 @@ RCCL job with fewer GPUs than ranks, exits non-zero without a line.
 Measurement options (not the contract line's defaults): --inflight M (M
 batches in flight on M streams), --emulate-shard R/N (rank R's LPT share of an
 N-way strong split, on one GPU), --walk-variant / --unmask-variant /
---split-lanes (A/B), --front-cus (split-stream overlap with --inflight >= 2).
+--split-lanes (A/B).
 The split header walk's auto choice (GEVWS_TUNE_SPLIT_LANES 0) looks at the
 previous finished decode on the context: the untimed verify decode walks
 unsplit, the warmup and timed steps split when that decode showed long chains
@@ -177,19 +177,60 @@ def _free_port() -> int:
     return port
 
 
+def _env_device_list(name: str):
+    """Entries of a *_VISIBLE_DEVICES variable (None when unset)."""
+    v = os.environ.get(name)
+    if v is None:
+        return None
+    return [x for x in v.split(",") if x.strip()]
+
+
+def count_gpus_without_hip(kfd_root: str | None = None):
+    """GPUs this job may use, counted WITHOUT any HIP call (the self-launching
+    parent must not hold a HIP runtime while its ranks run): the KFD topology
+    nodes with a non-zero gpu_id (CPU nodes have 0), narrowed by
+    ROCR_VISIBLE_DEVICES and then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.
+    None when the topology is not readable -- the caller then skips its check
+    and leaves the refusal to each rank's check_world.  (GEV_KFD_TOPOLOGY
+    points the CPU tests at a fake topology.)"""
+    if kfd_root is None:
+        kfd_root = os.environ.get("GEV_KFD_TOPOLOGY", "/sys/class/kfd/kfd/topology/nodes")
+    try:
+        nodes = os.listdir(kfd_root)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(kfd_root, node, "gpu_id")) as f:
+                n += int(f.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        lst = _env_device_list(var)
+        if lst is not None:
+            n = min(n, len(lst))
+    return n
+
+
 def launch_ranks(n: int, argv: list) -> int:
     """`bench.py --gpus N` run without a launcher: start the N rank processes
     itself -- torch.distributed.run as a CHILD process (never an exec), one rank
     per GPU, rendezvous on 127.0.0.1 -- and return its exit status.  Rank 0's
     JSON line reaches stdout through the inherited descriptor.  Nothing here
-    touches the GPU (device_count() does not initialise HIP on this image), so
-    the ranks are the only processes that open a device."""
+    touches the GPU: the device count comes from the KFD topology in sysfs
+    (count_gpus_without_hip), never from torch.cuda (whose device_count()
+    falls back to a HIP call when amdsmi fails), so the ranks are the only
+    processes that open a device.  Without a readable topology the check is
+    left to the ranks (check_world)."""
     import subprocess
     if _backend() == "nccl":
-        ndev = _visible_devices()
-        if ndev < n:
+        ndev = count_gpus_without_hip()
+        if ndev is not None and ndev < n:
             log(f"error: --gpus {n} needs {n} GPUs for RCCL (one rank per device); {ndev} visible")
             return 3
+        if ndev is None:
+            log("device count unavailable without HIP (no KFD topology); each rank checks its own")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
     log(f"launching {n} ranks: {' '.join(cmd[1:7])} ...")
@@ -202,18 +243,21 @@ def _backend() -> str:
 
 
 def _visible_devices() -> int:
+    """Inside a rank only (a rank opens its GPU anyway): torch's count."""
     import torch
     return torch.cuda.device_count()
 
 
 def check_world(args, world: int, need_devices: bool) -> None:
     """Refuse to print a line for a job shaped differently from what was asked:
-    WORLD_SIZE must be --gpus, and under RCCL every rank needs its own device."""
+    WORLD_SIZE must be --gpus, and under RCCL every rank needs its own device
+    (checked in the rank, also for --dry-run: a dry run over RCCL is refused
+    the same way)."""
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report "
                          f"n_gpus={world} for a {args.gpus}-GPU run")
     if need_devices and _backend() == "nccl" and world > 1 and _visible_devices() < world:
-        raise SystemExit(f"bench: {world} ranks over RCCL need {world} GPUs (one per rank); "
+        raise SystemExit(f"bench: {world} ranks over RCCL needs {world} GPUs (one per rank); "
                          f"{_visible_devices()} visible")
 
 
@@ -225,7 +269,7 @@ def dry_run(args) -> None:
     import torch
     from gev_amd import dist
     world, rank, _ = dist.env()
-    check_world(args, world, need_devices=False)
+    check_world(args, world, need_devices=True)
     if world > 1 and dist.backend() != "gloo":
         raise SystemExit("bench --dry-run: GEV_DIST_BACKEND=gloo (no GPU is used)")
     dist.init(dist.backend(), None)
@@ -277,10 +321,6 @@ def main():
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight: M contexts on M streams with M output arenas, step i on slot i %% M "
                          "(a server loop: one batch's header walk overlaps the previous batch's unmask)")
-    ap.add_argument("--front-cus", type=int, default=0,
-                    help="with --inflight >= 2: run each batch's walk / scan / record pass on a stream of this many "
-                         "CUs and its unmask on a stream of the others (CU masks), so batch k+1's walk overlaps "
-                         "batch k's unmask (0 = one stream per slot, no CU split)")
     ap.add_argument("--input-mem", choices=["default", "fine", "uncached"], default="default",
                     help="measurement: the input arena's memory kind (gevws_device_alloc)")
     ap.add_argument("--dry-run", action="store_true",
@@ -364,19 +404,6 @@ def main():
     sum64 = out.summary.view(torch.int64)
     outs = [out] + [e.alloc_batch(lay.n_conns, max_frames, cap) for e in engs[1:]]
     streams = [None] if M == 1 else [torch.cuda.Stream(dev) for _ in range(M)]
-    split = None
-    if args.front_cus:
-        if M < 2:
-            raise SystemExit("--front-cus needs --inflight >= 2")
-        ncu_dev = torch.cuda.get_device_properties(dev).multi_processor_count
-        fmask, bmask = gev_amd.cu_split_masks(ncu_dev, args.front_cus)
-        front, back = gev_amd.CuStream(gpu, fmask), gev_amd.CuStream(gpu, bmask)
-        for e in engs:
-            e.set_unmask_stream(back)
-        streams = [front] * M
-        split = {"front_cus": front.cus, "unmask_cus": back.cus}
-        log(f"split streams: walk / scan / record pass on {front.cus} CUs, unmask on {back.cus} CUs")
-        torch.cuda.synchronize()
     main_stream = torch.cuda.current_stream()
     n_step = [0]
 
@@ -463,7 +490,7 @@ def main():
             engs[0].decode_async(arena, lay.arena_bytes, conns, lay.n_conns, outs[0], max_frames, cap,
                                  stream=streams[0])
             engs[0].set_timing(False)
-            engs[0].order_after_last(torch.cuda.current_stream())  # (split streams: the unmask ran elsewhere)
+            engs[0].order_after_last(torch.cuda.current_stream())
             best = None
             for flag in (0, 0x40000000):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -518,7 +545,6 @@ def main():
                                    f"{'RCCL' if dist.backend() == 'nccl' else dist.backend()} all-reduce of counts"),
                    "batches_in_flight": M,
                    **({"input_mem": args.input_mem} if args.input_mem != "default" else {}),
-                   **({"split_streams": split} if split else {}),
                    **({"emulated_shard": emulated} if emulated else {})},
         "frames_per_s": round(frames_step * args.steps / elapsed, 1),
         "decoded_per_step": {"frames": frames_step, "payload_bytes": payload_step, "errors": errors,

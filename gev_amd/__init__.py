@@ -185,18 +185,10 @@ class Engine:
         if st != OK:
             raise ValueError(f"set_tuning({key}, {value}): {status_string(st)}")
 
-    # -------------------------------------------------------------- split streams
-    def set_unmask_stream(self, stream) -> None:
-        """gevws_ctx_set_unmask_stream: the decode's unmask on `stream` (a
-        CuStream, torch stream or raw handle; None = the decode's own stream)."""
-        st = lib.gevws_ctx_set_unmask_stream(self._ctx, None if stream is None else getattr(stream, "cuda_stream", stream))
-        if st != OK:
-            raise RuntimeError(f"gevws_ctx_set_unmask_stream: {status_string(st)}")
-        self._unmask_stream = stream  # kept alive while the context may launch on it
-
+    # -------------------------------------------------------------- stream ordering
     def order_after_last(self, stream=None) -> None:
         """Make `stream` (default: torch's current stream) wait for this
-        context's last call, whichever streams it ran on."""
+        context's last call, whichever stream it ran on."""
         st = lib.gevws_ctx_order_after_last(self._ctx, _stream_handle(stream))
         if st != OK:
             raise RuntimeError(f"gevws_ctx_order_after_last: {status_string(st)}")
@@ -714,59 +706,6 @@ class DeviceArena:
     def __del__(self, _free=lib.gevws_device_free):
         if getattr(self, "_p", None):
             _free(self.device, self._p)
-
-
-def cu_split_masks(num_cus: int, front_cus: int, xcds: int = 8) -> Tuple[List[int], List[int]]:
-    """CU masks (32-bit words) for a front stream of `front_cus` CUs and a back
-    stream of the rest, the front's CUs spread evenly over the XCDs.  Bit i is
-    CU i; whether the runtime numbers CUs XCD by XCD (XCD = i // per_xcd) or
-    round-robin (XCD = i % xcds), each XCD gets front_cus / xcds of the front's
-    CUs and keeps the rest for the back: front CU m of XCD b is bit
-    per_xcd * b + (b + m // 4 + xcds * (m % 4)) % per_xcd, which lies in XCD
-    b's block and is congruent to b + m // 4 (mod xcds), so the m of each block
-    also cover every residue equally."""
-    per = num_cus // xcds
-    k = front_cus // xcds
-    if num_cus % xcds or per % xcds or front_cus % (4 * xcds if k >= 4 else xcds) or not 0 < front_cus < num_cus \
-            or (k > 4 and k % 4) or k > per - 4:
-        raise ValueError(f"cu_split_masks({num_cus}, {front_cus}): front CUs must be {xcds} x (1..4 or a "
-                         f"multiple of 4 up to {per - 4})")
-    front = set()
-    for b in range(xcds):
-        for m in range(k):
-            front.add(per * b + (b + m // 4 + xcds * (m % 4)) % per)
-    assert len(front) == front_cus
-    words = (num_cus + 31) // 32
-    fw, bw = [0] * words, [0] * words
-    for i in range(num_cus):
-        (fw if i in front else bw)[i // 32] |= 1 << (i % 32)
-    return fw, bw
-
-
-class CuStream:
-    """gevws_stream_create_cu_mask: a non-blocking stream whose kernels run on
-    the CUs of `mask` only (32-bit words, bit i = CU i)."""
-
-    def __init__(self, device: int, mask: Sequence[int]):
-        arr = (ctypes.c_uint32 * len(mask))(*mask)
-        h = ctypes.c_void_p()
-        st = lib.gevws_stream_create_cu_mask(device, arr, len(mask), ctypes.byref(h))
-        if st != OK:
-            raise RuntimeError(f"gevws_stream_create_cu_mask: {status_string(st)}")
-        self.device, self.cuda_stream = device, h.value
-        self.cus = int(lib.gevws_stream_cu_count(device, h.value))
-
-    def torch_stream(self):
-        return _torch().cuda.ExternalStream(self.cuda_stream, device=_torch().device("cuda", self.device))
-
-    def close(self) -> None:
-        if getattr(self, "cuda_stream", None):
-            lib.gevws_stream_destroy(self.cuda_stream)
-            self.cuda_stream = None
-
-    def __del__(self, _free=lib.gevws_stream_destroy):
-        if getattr(self, "cuda_stream", None):
-            _free(self.cuda_stream)
 
 
 class Comm:

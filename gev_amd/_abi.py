@@ -170,11 +170,6 @@ SIGNATURES = {
     "gevws_ctx_device": (ctypes.c_int, [P]),
     "gevws_ctx_stream": (P, [P]),
     "gevws_ctx_order_after_last": (ctypes.c_int, [P, P]),
-    "gevws_ctx_set_unmask_stream": (ctypes.c_int, [P, P]),
-    "gevws_stream_create_cu_mask": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32,
-                                                   ctypes.POINTER(P)]),
-    "gevws_stream_destroy": (ctypes.c_int, [P]),
-    "gevws_stream_cu_count": (ctypes.c_int, [ctypes.c_int, P]),
     "gevws_ctx_set_timing": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_ctx_set_tuning": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_last_split_lanes": (ctypes.c_int, [P]),

@@ -174,15 +174,14 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (!ctx) return;
   DeviceGuard g(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  // the last call may have ended on another stream (a caller's, the unmask
-  // stream): its kernels still read the scratch freed below
+  // the last call may have run on another stream (a caller's): its kernels
+  // still read the scratch freed below
   if (ctx->has_last && ctx->last_done) (void)hipEventSynchronize(ctx->last_done);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->d_sum) (void)hipFree(ctx->d_sum);
   if (ctx->d_done) (void)hipFree(ctx->d_done);
   if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
-  if (ctx->front_done) (void)hipEventDestroy(ctx->front_done);
   for (auto& set : ctx->evs)
     for (auto& e : set.e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -198,50 +197,6 @@ int gevws_ctx_order_after_last(gevws_ctx* ctx, void* stream) {
   if (!ctx) return GEVWS_ERR_INVALID;
   DeviceGuard g(ctx->device);
   return order_after_last(ctx, reinterpret_cast<hipStream_t>(stream));
-}
-
-int gevws_stream_cu_count(int device, void* stream) {
-  int n = 0;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) return 0;
-  if (!stream) return n;
-  std::vector<uint32_t> m((size_t)(n + 31) / 32, 0u);
-  if (hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(stream), (uint32_t)m.size(), m.data()) != hipSuccess)
-    return n;
-  int c = 0;
-  for (int i = 0; i < n; ++i) c += (m[(size_t)i / 32] >> (i % 32)) & 1u;
-  return c > 0 ? c : n;
-}
-
-int gevws_stream_create_cu_mask(int device, const uint32_t* cu_mask, uint32_t n_words, void** stream) {
-  if (!cu_mask || !n_words || !stream || device < 0 || device >= gevws_device_count()) return GEVWS_ERR_INVALID;
-  *stream = nullptr;
-  uint32_t any = 0;
-  for (uint32_t i = 0; i < n_words; ++i) any |= cu_mask[i];
-  if (!any) return GEVWS_ERR_INVALID;
-  DeviceGuard g(device);
-  hipStream_t s = nullptr;
-  GEVWS_HIP(hipExtStreamCreateWithCUMask(&s, n_words, cu_mask));
-  *stream = reinterpret_cast<void*>(s);
-  return GEVWS_OK;
-}
-
-int gevws_stream_destroy(void* stream) {
-  if (!stream) return GEVWS_OK;
-  return hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)) == hipSuccess ? GEVWS_OK : GEVWS_ERR_DEVICE;
-}
-
-int gevws_ctx_set_unmask_stream(gevws_ctx* ctx, void* unmask_stream) {
-  if (!ctx) return GEVWS_ERR_INVALID;
-  DeviceGuard g(ctx->device);
-  ctx->unmask_stream = reinterpret_cast<hipStream_t>(unmask_stream);
-  ctx->unmask_cus = unmask_stream ? gevws_stream_cu_count(ctx->device, unmask_stream) : 0;
-  if (ctx->unmask_cus <= 0 || ctx->unmask_cus > ctx->num_cus) ctx->unmask_cus = ctx->num_cus;
-  if (unmask_stream && !ctx->front_done &&
-      hipEventCreateWithFlags(&ctx->front_done, hipEventDisableTiming) != hipSuccess) {
-    ctx->unmask_stream = nullptr;
-    return GEVWS_ERR_DEVICE;
-  }
-  return GEVWS_OK;
 }
 
 int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
@@ -358,20 +313,12 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   int r = decode_front(ctx, st, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, payload_cap, d_conn_out,
                        d_summary, ev, &tile_first);
   if (r != GEVWS_OK) return r;
-  // split streams: the unmask waits for the front (walk, scan, record pass)
-  // on its own stream; the next batch's front can then run beside it
-  hipStream_t ust = st;
-  if (ctx->unmask_stream && ctx->unmask_stream != st) {
-    ust = ctx->unmask_stream;
-    GEVWS_HIP(hipEventRecord(ctx->front_done, st));
-    GEVWS_HIP(hipStreamWaitEvent(ust, ctx->front_done, 0));
-  }
-  if (ev) GEVWS_HIP(hipEventRecord(ev[3], ust));  // (split: once the unmask stream may start it)
-  r = launch_unmask(ctx, ust, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);
+  if (ev) GEVWS_HIP(hipEventRecord(ev[3], st));
+  r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);
   if (r != GEVWS_OK) return r;
-  if (ev) GEVWS_HIP(hipEventRecord(ev[4], ust));
+  if (ev) GEVWS_HIP(hipEventRecord(ev[4], st));
   GEVWS_HIP(hipGetLastError());
-  return mark_last(ctx, ust);
+  return mark_last(ctx, st);
 }
 
 int gevws_decode_batch(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64_t in_bytes,
@@ -385,8 +332,6 @@ int gevws_decode_batch(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64
   int r = gevws_decode_batch_async(ctx, stream, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames,
                                    d_payload, payload_cap, d_conn_out, d_sum);
   if (r == GEVWS_OK) {
-    r = order_after_last(ctx, st);  // a split-stream decode ends on the unmask stream
-    if (r != GEVWS_OK) return r;
     GEVWS_HIP(hipMemcpyAsync(h_summary, d_sum, sizeof(gevws_summary), hipMemcpyDeviceToHost, st));
     GEVWS_HIP(hipStreamSynchronize(st));
     r = h_summary->status;

@@ -709,9 +709,6 @@ class Protocol {
       const int r = gevws_decode_batch_async(ctx_, st, din + sg->coff, sg->total, (gevws_conn_in*)din, m,
                                              (gevws_frame*)dfr, sg->max_frames, (uint8_t*)dpay, sg->payload_cap,
                                              (gevws_conn_out*)(dres + sizeof(gevws_summary)), (gevws_summary*)dres);
-      // (a context with an unmask stream ends the decode there: the pass's
-      // stream waits for it, so the stream synchronisation covers the payload)
-      if (r == GEVWS_OK && gevws_ctx_order_after_last(ctx_, st) != GEVWS_OK) return fail();
       sg->seq = gevws_ctx_completion_seq(ctx_);
       return r;
     }
@@ -725,7 +722,6 @@ class Protocol {
                                      (gevws_frame*)d_frames_, sg->max_frames, (uint8_t*)d_payload_, sg->payload_cap,
                                      d_cout, d_sum);
     if (r != GEVWS_OK) return r;
-    if (gevws_ctx_order_after_last(ctx_, st) != GEVWS_OK) return fail();  // (split-stream decode, as above)
     if (hipMemcpyAsync(h_res_, d_res_, sg->res, hipMemcpyDeviceToHost, st) != hipSuccess) return fail();
     return GEVWS_OK;
   }

@@ -53,11 +53,6 @@ struct gevws_ctx {
   bool has_last = false;
   int num_cus = 256;
   uint32_t* d_done = nullptr;  // the decode walk's finished-workgroup counter (zero between calls)
-  // split-stream decode (gevws_ctx_set_unmask_stream): the unmask on its own
-  // stream after the record pass (front_done), its grid for unmask_cus CUs
-  hipStream_t unmask_stream = nullptr;
-  int unmask_cus = 0;
-  hipEvent_t front_done = nullptr;
 };
 
 namespace gevws_impl {

@@ -684,8 +684,7 @@ int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const ui
                   uint8_t* d_payload) {
   const UnmaskVariant& v = kUnmaskVariants[ctx->unmask_variant];
   const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
-  // CUs the unmask's stream may use (all of the device's, or its CU mask's)
-  const uint32_t ucus = (uint32_t)(st == ctx->unmask_stream && ctx->unmask_cus > 0 ? ctx->unmask_cus : ctx->num_cus);
+  const uint32_t ucus = (uint32_t)ctx->num_cus;
   const uint64_t norm = 4 * (uint64_t)ucus;
   // the wide grid (kWideGridPerCU per CU) when the previous decode on this
   // context was a batch of mixed sizes (run frames < half) below
@@ -713,6 +712,7 @@ extern "C" {
 int gevws_copy_async(gevws_ctx* ctx, void* stream, uint8_t* d_dst, const uint8_t* d_src, uint64_t n,
                      uint32_t grid) {
   if (!ctx || (n && (!d_dst || !d_src))) return GEVWS_ERR_INVALID;
+  if (grid & 0x80000000u) return GEVWS_ERR_INVALID;  // no such flag (ABI 2: unknown bits are rejected)
   // bit 30: plain loads (else non-temporal); bit 29: the unmask's
   // wave-contiguous spans (else tile-strided lanes); bit 28: plain stores to
   // a destination of any alignment (else non-temporal, 16-aligned)

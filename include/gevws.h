@@ -24,7 +24,13 @@ extern "C" {
 #pragma GCC visibility push(default)
 #endif
 
-#define GEVWS_ABI_VERSION 1
+/* 2 (round 5): the split-stream calls gevws_ctx_set_unmask_stream,
+ * gevws_stream_create_cu_mask, gevws_stream_destroy and gevws_stream_cu_count
+ * are gone, gevws_copy_async rejects unknown flag bits, and the round-1..3
+ * measurement exports (gevws_gather_async, gevws_unmask_profile,
+ * gevws_ctx_last_walk_budget, gevws_ctx_last_resumed; tuning keys 5, 6, 9-12)
+ * removed in round 4 are counted here too. */
+#define GEVWS_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- status codes */
 enum {
@@ -130,28 +136,14 @@ void gevws_ctx_destroy(gevws_ctx *ctx);
 int gevws_ctx_device(const gevws_ctx *ctx);
 /* The context's own non-blocking hipStream_t (one per event loop). */
 void *gevws_ctx_stream(const gevws_ctx *ctx);
-/* Makes `stream` wait for everything the context's last call enqueued,
- * whichever stream(s) that ran on (e.g. a decode whose unmask ran on the
- * context's unmask stream, below). */
+/* Makes `stream` wait for everything the context's last call enqueued (on
+ * whichever stream that call was given).  The calls that use the context's
+ * scratch (decode, encode, dispatch) order themselves after its previous such
+ * call when the stream changes; the helpers that do not (gevws_copy_async,
+ * gevws_cipher_async, gevws_synth_async, gevws_synth_verify_async) follow
+ * plain HIP stream semantics, so a caller that points one at a decode's
+ * outputs from another stream orders it first, with this or an event. */
 int gevws_ctx_order_after_last(gevws_ctx *ctx, void *stream);
-/* Split-stream decode (a server loop with two batches in flight): with an
- * unmask stream set, gevws_decode_batch[_async] runs its header walk, scan and
- * record pass on the caller's stream and the unmask on `unmask_stream`, after
- * them (an event), with its grid sized for that stream's CUs.  The call's
- * completion is then on the unmask stream (gevws_ctx_order_after_last orders
- * other work after it).  Two contexts sharing one front and one unmask stream
- * overlap batch k+1's walk with batch k's unmask; with CU-masked streams
- * (gevws_stream_create_cu_mask) the two do not compete for the same CUs.
- * NULL: the whole decode on the caller's stream (the default).  The one-launch
- * small-batch decode ignores it. */
-int gevws_ctx_set_unmask_stream(gevws_ctx *ctx, void *unmask_stream);
-/* A non-blocking stream on `device` whose kernels run only on the CUs set in
- * the n_words x 32-bit mask (hipExtStreamCreateWithCUMask; bit i = CU i). */
-int gevws_stream_create_cu_mask(int device, const uint32_t *cu_mask, uint32_t n_words, void **stream);
-int gevws_stream_destroy(void *stream);
-/* The number of CUs a stream may use (its CU mask's population; all of the
- * device's for an unmasked stream or NULL). */
-int gevws_stream_cu_count(int device, void *stream);
 /* Tuning knobs for measurement and parity tests (defaults are the tuned
  * choice): GEVWS_TUNE_UNMASK_VARIANT the unmask kernel (0 = default: v3 4-tile
  * windows for batches of equal-size frames, v5 pipelined 8-tile windows with

@@ -4,8 +4,8 @@
 # under its own time limit, and the first failure ends the run (no GPU work
 # after a fault, abort or timeout).
 #
-#   bash scripts/gpu.sh 'test tests/test_gpu_split_streams.py' \
-#                       'bench c4s32 --config c4 --inflight 2 --front-cus 32' \
+#   bash scripts/gpu.sh 'test tests/test_gpu_parity.py' \
+#                       'bench c4i2 --config c4 --inflight 2' \
 #                       'prof c4 --config c4 --steps 5' \
 #                       'pmc c4_rd TCC_EA0_RDREQ_32B,TCC_EA0_RDREQ_64B -- --config c4 --steps 3' \
 #                       'py tools/host_inclusive.py --out gpurun_out/x.json'

@@ -61,3 +61,74 @@ def test_world_size_mismatch_exits_nonzero():
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def _fake_kfd(tmp_path, gpu_ids):
+    root = tmp_path / "nodes"
+    for i, g in enumerate(gpu_ids):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "gpu_id").write_text(f"{g}\n")
+    return str(root)
+
+
+def test_device_count_reads_kfd_topology_and_visibility(tmp_path, monkeypatch):
+    import bench
+    root = _fake_kfd(tmp_path, [0, 4417, 52213, 12001, 61400])  # node 0 = the CPU
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    assert bench.count_gpus_without_hip(root) == 4
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2")
+    assert bench.count_gpus_without_hip(root) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert bench.count_gpus_without_hip(root) == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.count_gpus_without_hip(root) == 0
+    assert bench.count_gpus_without_hip(str(tmp_path / "absent")) is None
+
+
+# The self-launching parent with every torch device-count path booby-trapped:
+# torch.cuda.device_count() (amdsmi) and torch._C._cuda_getDeviceCount() (its
+# HIP fallback) raise, so any HIP-touching count in the parent ends the run.
+_TRAP = r"""
+import runpy, sys, torch
+def _boom(*a, **k):
+    raise RuntimeError("parent touched the GPU device count")
+torch.cuda.device_count = _boom
+torch._C._cuda_getDeviceCount = _boom
+sys.argv = [sys.argv[1]] + sys.argv[2:]
+runpy.run_path(sys.argv[0], run_name="__main__")
+"""
+
+
+def _run_trapped(args, env_extra):
+    drop = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+    env = {k: v for k, v in os.environ.items() if k not in drop}  # (this container sets HIP_VISIBLE_DEVICES=)
+    env.update(env_extra)
+    return subprocess.run([sys.executable, "-c", _TRAP, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT,
+                          capture_output=True, text=True, timeout=240, env=env)
+
+
+def test_parent_launches_without_hip_device_count():
+    r = _run_trapped(["--gpus", "2", "--dry-run", "--config", "c2"], {"GEV_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "parent touched" not in r.stderr
+    assert _line(r)["n_gpus"] == 2
+
+
+def test_parent_rccl_check_uses_kfd_topology(tmp_path):
+    # two GPUs in the (fake) topology: the parent's check passes without HIP and
+    # launches; this container's ranks then find no device and refuse themselves
+    root = _fake_kfd(tmp_path, [0, 11, 12])
+    r = _run_trapped(["--gpus", "2", "--dry-run", "--config", "c2"],
+                     {"GEV_DIST_BACKEND": "nccl", "GEV_KFD_TOPOLOGY": root})
+    assert "parent touched" not in r.stderr
+    assert "launching 2 ranks" in r.stderr
+    assert r.returncode != 0 and "needs 2 GPUs" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    # one GPU in the topology: the parent refuses before launching anything
+    root1 = _fake_kfd(tmp_path / "one", [0, 11])
+    r = _run_trapped(["--gpus", "2", "--dry-run", "--config", "c2"],
+                     {"GEV_DIST_BACKEND": "nccl", "GEV_KFD_TOPOLOGY": root1})
+    assert "parent touched" not in r.stderr
+    assert r.returncode == 3 and "needs 2 GPUs" in r.stderr and "launching" not in r.stderr

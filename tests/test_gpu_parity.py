@@ -807,3 +807,24 @@ def test_walk_variant_knob_bounds(engine):
     for key in _abi.TUNE_RETIRED:  # round 1-3 measurement knobs are gone
         with pytest.raises(ValueError):
             engine.set_tuning(key, 0)
+
+
+@pytest.mark.gpu
+def test_copy_helper_copies_and_rejects_unknown_flags(engine):
+    """gevws_copy_async (the bench's copy ceiling): every load / layout flag
+    copies the bytes exactly, from an aligned and a misaligned source; an
+    unknown flag bit is GEVWS_ERR_INVALID, not silently masked (ABI 2,
+    ADVICE r4)."""
+    import torch
+    dev = torch.device("cuda", engine.device)
+    n = 3 * 4096 * 16 + 4096 + 48  # whole tiles per workgroup, a partial step and a tail
+    src = torch.randint(0, 256, (n + 64,), dtype=torch.uint8, device=dev)
+    for flags in (0, 0x40000000, 0x20000000, 0x20000000 | 0x40000000, 0x10000000, 0x08000000):
+        for so in (0, 7):
+            dst = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+            engine.copy_(dst, src, n, src_offset=so, grid=flags | 3)
+            torch.cuda.synchronize()
+            assert torch.equal(dst[:n], src[so:so + n]), (hex(flags), so)
+            assert int(dst[n:].sum()) == 0
+    with pytest.raises(RuntimeError):
+        engine.copy_(dst, src, n, grid=0x80000000)
