@@ -395,8 +395,6 @@ def main():
     mismatch = int(mism.item())
     if mismatch or int(s["frames"]) != lay.n_frames or int(s["payload_len"]) != lay.payload_len:
         raise SystemExit(f"verification failed: mismatch={mismatch} frames={int(s['frames'])}")
-    if M == 1:
-        del desc
     log(f"rank {rank}: setup+verify {time.time() - t_setup:.1f}s, bit-exact")
 
     counts = torch.zeros(3, dtype=torch.int64, device=dev)
@@ -439,14 +437,17 @@ def main():
         phases = [a + b for a, b in zip(phases, ph)]
         calls += cl
     elapsed = dist.max_over_ranks(t1 - t0, dev)
-    if M > 1:  # every slot's last batch checked too (outside the timed region)
-        for k in range(1, M):
-            mism.zero_()
-            engs[k].verify(desc, lay.n_frames, lay.seed, outs[k], mism)
-            torch.cuda.synchronize()
-            if int(mism.item()):
-                raise SystemExit(f"verification failed on in-flight slot {k}: mismatch={int(mism.item())}")
-        del desc
+    # the timed steps' own output checked too (outside the timed region): every
+    # slot's last batch, decode(mask(P)) == P on every byte
+    for k in range(M):
+        mism.zero_()
+        engs[k].verify(desc, lay.n_frames, lay.seed, outs[k], mism)
+        torch.cuda.synchronize()
+        sk = outs[k].summary_host()
+        if int(mism.item()) or int(sk["status"]) != 0 or int(sk["frames"]) != lay.n_frames:
+            raise SystemExit(f"verification of the timed output failed (slot {k}): mismatch={int(mism.item())} "
+                             f"status={int(sk['status'])}")
+    del desc
 
     walk_info = {"split_lanes": eng.last_split_lanes}
     # achievable-bandwidth ceiling on this box, after the timed region: the

@@ -578,15 +578,404 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
   }
 }
 
-// The default unmask: the batch's own statistics pick the window scheme --
-// batches of equal-size frames (at least half of the frames the size of the
-// one before them on the connection: C1, C2, C3, C5) take v3's 4-tile windows,
-// mixed ones (C4) v5's pipelined 8-tile windows, with the whole (wide) grid
-// for a batch of fewer than kWideGridTiles tiles.  One kernel, one LDS
-// budget, the choice is a uniform branch on the summary the walk wrote.
+// ------------------------------------------------------------------ fused record + unmask (mixed batches)
+// The record pass (k_walk_emit) and the unmask (v5) of a batch of mixed frame
+// sizes in ONE kernel, driven by the walk's 8-byte entries instead of the
+// 32-byte records and the tile map: the v5 path read back every record the
+// record pass had just written (C4: 1.40 GB of a 47.95 GB step) and the
+// record pass ran as its own launch (0.48 ms).  Every wave works alone (no
+// workgroup barrier), on whole rows (connections, or k_walk_split's segments):
+//  * rows come in units of A.unit_rows from per-XCD counters (blockIdx mod 8,
+//    the dispatch's round robin), then from the other XCDs' counters;
+//  * a row's frames go in rounds of 256 (4 entries a lane): the entries'
+//    segmented wave scans give each header's position and payload offset
+//    (entry_round, as k_walk_emit), the lane writes its frame's 32-byte record
+//    (= the (ctx, out) of protocol.go:57-58) and its LDS table slot (source -
+//    destination delta, payload end, key);
+//  * the round's payloads are contiguous in the arena: the wave unmasks them
+//    in steps of 8 KiB (8 chunks a lane, 64-lane coalesced 1 KiB spans) --
+//    a step inside one frame streams; otherwise every frame starting in the
+//    step marks its first chunk in the wave's LDS map and one wave prefix max
+//    gives every chunk its frame (ws.Cipher, cipher.go:14-53, phase 0 per
+//    frame, protocol.go:54; pad bytes zero as Go's make);
+//  * frames of at least A.big_bytes padded bytes are not unmasked inline: the
+//    lane queues them as pieces of kPieceBytes (source, destination, length,
+//    key, stamp) and every wave, once no rows are left, takes pieces until
+//    all rows are done and the queue is empty -- so the tail of the row phase
+//    is filled with pieces, and no wave holds a 1 MiB frame alone at the end.
+// Rows without entries (an unordered connection table, a stream >= 4 GiB,
+// more frames than entry slots) are walked header by header by lane 0,
+// 256 frames a round, into the same LDS entries (slow, rare).
+// Queue entries and counters cross XCDs (whose L2s are not coherent): they are
+// written and read as agent-scope atomics (L2-bypassing), a piece's stamp
+// written after its other words are complete (s_waitcnt), a wave's rows
+// counted done after every piece it queued is complete.
+constexpr uint32_t kFusedRound = 256;                 // frames per round (4 entries a lane)
+constexpr uint32_t kFusedStep = 8;                    // chunks per lane per unmask step
+constexpr uint32_t kFusedStepChunks = 64 * kFusedStep;
+constexpr uint64_t kFusedStepBytes = 16ull * kFusedStepChunks;
+constexpr uint64_t kPieceBytes = 64 * 1024;           // a deferred frame's piece
+constexpr uint32_t kFusedMaxSpins = 1u << 24;         // a wave waiting for a piece gives up after this many sleeps
+
+struct FusedTab {
+  uint64_t delta;  // src_off - payload_off (mod 2^64)
+  uint64_t end;    // payload_off + length; payload_off for a deferred frame (no inline chunk)
+};
+struct FusedLds {
+  FusedTab* tab;   // [kFusedRound] per wave (the round's frames; lane 0's re-walk entries before that)
+  uint32_t* key;   // [kFusedRound]
+  uint16_t* own;   // [kFusedStepChunks] chunk -> slot + 1
+};
+
+__device__ __forceinline__ uint64_t agent_ld64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void agent_st64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t agent_ld32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lds_fence() { __asm__ volatile("" ::: "memory"); }
+
+// Bytes [dst, dst + len) of the arena from in[src ...] ^ key (len > 0; the
+// last chunk's bytes past len zeroed), by the whole wave: 16 chunks a lane in
+// flight per batch.
+__device__ __forceinline__ void fused_piece(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t src,
+                                            uint64_t dst, uint64_t len, uint32_t key) {
+  constexpr int U = 16;
+  const uint64_t nch = (len + 15) >> 4;
+  for (uint64_t c0 = 0; c0 < nch; c0 += 64 * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t c = c0 + (uint64_t)u * 64 + (fresh_tid() & 63);
+      v[u] = u32x4{0, 0, 0, 0};
+      if (c < nch) v[u] = ld16u_stream<true>(in + src + 16 * c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t c = c0 + (uint64_t)u * 64 + (fresh_tid() & 63);
+      if (c < nch) {
+        u32x4 x = v[u] ^ key;
+        const int64_t rem = (int64_t)len - (int64_t)(16 * c);
+        if (rem < 16) x = keep_bytes(x, rem);
+        st16_nt(out + dst + 16 * c, x);
+      }
+    }
+  }
+}
+
+// The round's payload range [R0, R1): slots s = u * 64 + lane hold frames with
+// payload offset po[u] and padded length pd[u] (0: no payload / no frame).
+__device__ __forceinline__ void fused_unmask_range(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                   const FusedLds& L, const uint64_t (&po)[4], const uint64_t (&pd)[4],
+                                                   uint64_t R0, uint64_t R1, uint64_t big_bytes) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t p = R0;
+  while (p < R1) {  // wave-uniform
+    // the frame covering p: the last slot with a payload starting at or before it
+    int s = -1;
+#pragma unroll
+    for (int u = 3; u >= 0; --u) {
+      const uint64_t m = __ballot(pd[u] > 0 && po[u] <= p);
+      if (s < 0 && m) s = u * 64 + 63 - __builtin_clzll(m);
+    }
+    if (s < 0) return;  // (cannot happen: the round's first payload starts at R0)
+    uint64_t spo = 0, spd = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (u == (s >> 6)) {
+        spo = uniform64(__shfl(po[u], s & 63, 64));
+        spd = uniform64(__shfl(pd[u], s & 63, 64));
+      }
+    if (spd >= big_bytes) {  // a deferred frame: its pieces are queued
+      p = spo + spd;
+      continue;
+    }
+    if (spo + spd >= p + kFusedStepBytes) {  // the whole step inside frame s: stream it
+      const FusedTab te = L.tab[s];
+      const uint32_t key = L.key[s];
+      u32x4 v[kFusedStep];
+#pragma unroll
+      for (int u = 0; u < (int)kFusedStep; ++u)
+        v[u] = ld16u_stream<true>(in + (p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16 + te.delta));
+#pragma unroll
+      for (int u = 0; u < (int)kFusedStep; ++u) {
+        const uint64_t q = p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16;
+        u32x4 x = v[u] ^ key;
+        const int64_t rem = (int64_t)(te.end - q);
+        if (rem < 16) x = keep_bytes(x, rem);
+        st16_nt(out + q, x);
+      }
+      p += kFusedStepBytes;
+      continue;
+    }
+    // chunk -> slot map of the step: marks of the frames starting inside it,
+    // then a wave prefix max seeded with slot s
+    reinterpret_cast<u32x4*>(L.own)[lane] = u32x4{0, 0, 0, 0};
+    lds_fence();
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (pd[u] > 0 && po[u] > p && po[u] < p + kFusedStepBytes)
+        L.own[(po[u] - p) >> 4] = (uint16_t)(u * 64 + lane + 1);
+    lds_fence();
+    {
+      u32x4 m = reinterpret_cast<const u32x4*>(L.own)[lane];
+      uint32_t run[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        run[2 * k] = m[k] & 0xffffu;
+        run[2 * k + 1] = m[k] >> 16;
+      }
+#pragma unroll
+      for (int k = 1; k < 8; ++k) run[k] = run[k] > run[k - 1] ? run[k] : run[k - 1];
+      uint32_t inc = run[7];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= (uint32_t)d) inc = inc > y ? inc : y;
+      }
+      uint32_t exc = (uint32_t)__shfl_up((int)inc, 1, 64);
+      if (lane == 0) exc = 0;
+      const uint32_t seed = (uint32_t)s + 1;
+      exc = exc > seed ? exc : seed;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t lo16 = run[2 * k] > exc ? run[2 * k] : exc;
+        const uint32_t hi16 = run[2 * k + 1] > exc ? run[2 * k + 1] : exc;
+        m[k] = lo16 | (hi16 << 16);
+      }
+      reinterpret_cast<u32x4*>(L.own)[lane] = m;
+    }
+    lds_fence();
+    u32x4 v[kFusedStep];
+    uint32_t key[kFusedStep];
+    int32_t rem[kFusedStep];
+#pragma unroll
+    for (int u = 0; u < (int)kFusedStep; ++u) {
+      const uint32_t c = (uint32_t)u * 64 + (fresh_tid() & 63);
+      const uint64_t q = p + 16ull * c;
+      rem[u] = 0;
+      key[u] = 0;
+      v[u] = u32x4{0, 0, 0, 0};
+      if (q < R1) {
+        const uint32_t sl = (uint32_t)L.own[c] - 1u;
+        const FusedTab te = L.tab[sl];
+        const int64_t r = (int64_t)(te.end - q);
+        rem[u] = r <= 0 ? 0 : (r > 16 ? 16 : (int32_t)r);
+        key[u] = L.key[sl];
+        if (r > 0) v[u] = ld16u_stream<true>(in + (q + te.delta));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < (int)kFusedStep; ++u) {
+      if (rem[u] > 0) {
+        u32x4 x = v[u] ^ key[u];
+        if (rem[u] < 16) x = keep_bytes(x, rem[u]);
+        st16_nt(out + p + 16ull * ((uint32_t)u * 64 + (fresh_tid() & 63)), x);
+      }
+    }
+    lds_fence();  // (the next step's map clear after this step's reads)
+    p += kFusedStepBytes;
+  }
+}
+
+// One row: records + inline unmask of its frames below A.big_bytes, pieces of
+// the others queued.
+__device__ __forceinline__ void fused_row(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                          const FusedArgs& A, const FusedLds& L, uint64_t c, bool unordered) {
+  const uint32_t lane = threadIdx.x & 63;
+  gevws_conn_out o = A.rout[c];
+  if (A.ks) {
+    const gevws_conn_out pr = A.pout[c / A.ks];
+    o.first_frame += pr.first_frame;
+    o.payload_base += pr.payload_base;
+  }
+  const uint64_t cnt = uniform64(o.nframes);
+  if (cnt == 0) return;
+  const gevws_conn_in ci = A.rows[c];
+  const uint64_t coff = uniform64(ci.off), clen = uniform64(ci.len);
+  uint64_t ebase = 0, ecap = 0;
+  const bool rec = A.rec_flags[c] && !unordered &&
+                   entry_slots_of(gevws_conn_in{coff, clen}, (uint32_t)c, A.n_entries, A.gshift, ebase, ecap);
+  const uint64_t f0 = uniform64(o.first_frame);
+  uint64_t carry = uniform64(o.payload_base), pcarry = 0;
+  for (uint64_t k0 = 0; k0 < cnt; k0 += kFusedRound) {
+    WalkEntry q[4];
+    if (rec) {
+      const WalkEntry* ce = reinterpret_cast<const WalkEntry*>(A.entries) + ebase;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t k = k0 + (uint64_t)u * 64 + lane;
+        q[u] = ce[k < cnt ? k : cnt - 1];
+      }
+    } else {  // no entries: lane 0 walks this round's headers into LDS
+      WalkEntry* buf = reinterpret_cast<WalkEntry*>(L.tab);
+      const uint64_t m = cnt - k0 < kFusedRound ? cnt - k0 : kFusedRound;
+      lds_fence();
+      if (lane == 0) {
+        uint64_t pos = pcarry;
+        for (uint64_t i = 0; i < m; ++i) {
+          uint64_t lo, hi;
+          load_window(in + coff + pos, lo, hi);
+          DevHdr h;
+          parse_header(lo, hi, clen - pos, h);  // succeeded in the counting walk
+          buf[i] = make_entry(h.mask, h.length, h.b0 | (h.masked << 8) | (h.hlen << 16));
+          pos += h.hlen + h.length;
+        }
+      }
+      lds_fence();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t k = (uint64_t)u * 64 + lane;
+        q[u] = buf[k < m ? k : m - 1];
+      }
+      lds_fence();
+    }
+    const uint64_t R0 = carry;
+    uint64_t po[4], pd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      po[u] = 0;
+      pd[u] = 0;
+      if (k0 + (uint64_t)u * 64 >= cnt) continue;  // wave-uniform
+      const uint64_t k = k0 + (uint64_t)u * 64 + lane;
+      const bool valid = k < cnt;
+      uint64_t Ln, ip;
+      entry_round(in, q[u], valid, lane == 0, pcarry, coff, Ln, ip);
+      const uint32_t hlen = entry_hlen(q[u]);
+      const uint64_t fsz = valid ? hlen + Ln : 0;
+      const uint64_t padded = valid ? round16(Ln) : 0;
+      const uint64_t incl = wave_incl_scan(padded);
+      const uint64_t poff = carry + incl - padded;
+      const uint64_t src = coff + pcarry + ip - fsz + hlen;
+      const uint32_t key = q[u].mask;  // 0 for an unmasked frame (the walk zeroes it)
+      const bool big = valid && padded >= A.big_bytes;
+      if (valid) {
+        const uint32_t b0 = q[u].w & 0xffu, masked = (q[u].w >> 8) & 1u;
+        const uint32_t flags = (b0 >> 7) | (((b0 & 0x70u) >> 4) << 8) | ((b0 & 0x0fu) << 16) | (masked << 24);
+        u32x4* r = reinterpret_cast<u32x4*>(A.frames + f0 + k);
+        r[0] = u32x4{flags, key, (uint32_t)Ln, (uint32_t)(Ln >> 32)};
+        r[1] = u32x4{(uint32_t)poff, (uint32_t)(poff >> 32), (uint32_t)src, (uint32_t)(src >> 32)};
+      }
+      const uint32_t s = (uint32_t)u * 64 + lane;
+      L.tab[s] = FusedTab{src - poff, big ? poff : poff + Ln};
+      L.key[s] = key;
+      po[u] = poff;
+      pd[u] = padded;
+      if (__ballot(big)) {  // queue the deferred frames' pieces
+        const uint64_t np = big ? (padded + kPieceBytes - 1) / kPieceBytes : 0;
+        const uint64_t ni = wave_incl_scan(np);
+        const uint64_t tot = uniform64(__shfl(ni, 63, 64));
+        uint32_t base = 0;
+        if (lane == 0)
+          base = __hip_atomic_fetch_add(A.ctr + kCtrPieces * 16, (uint32_t)tot, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+        base = uniform32(__shfl((int)base, 0, 64));
+        for (uint64_t j = 0; j < np; ++j) {
+          const uint64_t idx = base + ni - np + j;
+          if (idx >= A.piece_cap) break;  // (sized for the worst case: never)
+          uint64_t* e = A.pieces + 4 * idx;
+          const uint64_t off = j * kPieceBytes;
+          const uint64_t len = Ln - off < kPieceBytes ? Ln - off : kPieceBytes;
+          agent_st64(e + 0, src + off);
+          agent_st64(e + 1, poff + off);
+          agent_st64(e + 2, (len << 32) | key);
+          __builtin_amdgcn_s_waitcnt(0);  // the words above are complete before the stamp
+          agent_st64(e + 3, A.gen);
+        }
+      }
+      carry += uniform64(__shfl(incl, 63, 64));
+      pcarry += uniform64(__shfl(ip, 63, 64));
+    }
+    lds_fence();
+    fused_unmask_range(in, out, L, po, pd, R0, carry, A.big_bytes);
+  }
+}
+
+__device__ void fused_body(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                           const gevws_summary* __restrict__ sum, const FusedArgs& A, const FusedLds& L) {
+  if (sum->status != GEVWS_OK) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const bool unordered = (sum->flags & GEVWS_SUMMARY_UNORDERED) != 0;
+  const uint64_t n = A.n_rows;
+  const uint64_t segn = (n + kUnmaskRunCounters - 1) / kUnmaskRunCounters;
+  const uint32_t xc = blockIdx.x % kUnmaskRunCounters;
+  // 1. rows: this XCD's counter, then the others'
+  for (uint32_t x = 0; x < kUnmaskRunCounters;) {
+    const uint32_t sx = (xc + x) % kUnmaskRunCounters;
+    const uint64_t s0 = (uint64_t)sx * segn < n ? (uint64_t)sx * segn : n;
+    const uint64_t s1 = s0 + segn < n ? s0 + segn : n;
+    uint32_t u = 0;
+    if (lane == 0) u = __hip_atomic_fetch_add(A.ctr + sx * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    u = uniform32(__shfl((int)u, 0, 64));
+    const uint64_t r0 = s0 + (uint64_t)u * A.unit_rows;
+    if (r0 >= s1) {
+      ++x;
+      continue;
+    }
+    const uint64_t r1 = r0 + A.unit_rows < s1 ? r0 + A.unit_rows : s1;
+    for (uint64_t c = r0; c < r1; ++c) fused_row(in, out, A, L, c, unordered);
+    __builtin_amdgcn_s_waitcnt(0);  // every piece this wave queued is complete
+    if (lane == 0)
+      __hip_atomic_fetch_add(A.ctr + kCtrRowsDone * 16, (uint32_t)(r1 - r0), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // 2. pieces, until every row is done and every queued piece taken
+  uint32_t spins = 0;
+  for (;;) {
+    uint32_t pc = agent_ld32(A.ctr + kCtrPieces * 16);
+    uint32_t cur = agent_ld32(A.ctr + kCtrCursor * 16);
+    if (cur >= pc) {
+      if (agent_ld32(A.ctr + kCtrRowsDone * 16) >= n) {
+        // every row is done, so the piece count is final
+        pc = agent_ld32(A.ctr + kCtrPieces * 16);
+        cur = agent_ld32(A.ctr + kCtrCursor * 16);
+        if (cur >= pc) break;
+      } else {
+        if (++spins > kFusedMaxSpins) break;
+        __builtin_amdgcn_s_sleep(8);
+        continue;
+      }
+    }
+    uint32_t got = 0;
+    if (lane == 0)
+      got = __hip_atomic_compare_exchange_strong(A.ctr + kCtrCursor * 16, &cur, cur + 1, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+    if (!uniform32(__shfl((int)got, 0, 64))) continue;  // another wave took it
+    const uint64_t idx = uniform32(__shfl((int)cur, 0, 64));
+    if (idx >= A.piece_cap) continue;
+    const uint64_t* e = A.pieces + 4 * idx;
+    uint32_t wait = 0;
+    while (uniform64(agent_ld64(e + 3)) != A.gen) {  // queued, not yet stamped
+      if (++wait > kFusedMaxSpins) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (wait > kFusedMaxSpins) {
+      spins = kFusedMaxSpins + 1;
+      break;
+    }
+    const uint64_t src = uniform64(agent_ld64(e + 0)), dst = uniform64(agent_ld64(e + 1));
+    const uint64_t w2 = uniform64(agent_ld64(e + 2));
+    fused_piece(in, out, src, dst, w2 >> 32, (uint32_t)w2);
+    spins = 0;
+  }
+  if (spins > kFusedMaxSpins && lane == 0)  // gave up waiting: the output is incomplete, say so
+    __hip_atomic_store(&A.sum->status, (int32_t)GEVWS_ERR_DEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The round-4 default unmask (GEVWS_TUNE_UNMASK_VARIANT 2 since round 5): the
+// batch's own statistics pick the window scheme -- batches of equal-size
+// frames (at least half of the frames the size of the one before them on the
+// connection: C1, C2, C3, C5) take v3's 4-tile windows, mixed ones (C4) v5's
+// pipelined 8-tile windows, with the whole (wide) grid for a batch of fewer
+// than kWideGridTiles tiles.  One kernel, one LDS budget, the choice is a
+// uniform branch on the summary the walk wrote.
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto5(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
-    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs) {
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs,
+    FusedArgs) {
   static_assert(kWinFrames == kWin5Frames, "one frame table for both bodies");
   __shared__ uint32_t s_start[kWinFrames];
   __shared__ int32_t s_lend[kWinFrames];
@@ -608,7 +997,8 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
 // batch, so the parity tests run it over equal-size frames too.
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_v5(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
-    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs) {
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs,
+    FusedArgs) {
   __shared__ int32_t s_lend[kWin5Frames];
   __shared__ uint64_t s_delta[kWin5Frames];
   __shared__ uint32_t s_key[kWin5Frames];
@@ -618,6 +1008,36 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   unmask_v5_body<16>(in, frames, tile_first, sum, out, big_grid,
                      WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap},
                      sum->payload_bytes / kTile < kWideGridTiles, runs);
+}
+
+// The default since round 5: batches of equal-size frames take v3 (records and
+// tile map from k_walk_emit), mixed ones the fused record + unmask path (the
+// record pass skipped them, k_walk_emit's gate); ALL = the fused path for
+// every batch (GEVWS_TUNE_UNMASK_VARIANT 3; the record pass skips every batch).
+constexpr uint32_t kFusedLdsPerWave = kFusedRound * (sizeof(FusedTab) + 4) + kFusedStepChunks * 2;
+constexpr uint32_t kV3LdsBytes = kWinFrames * (4 + 4 + 8 + 4);
+constexpr uint32_t kFusedLdsBytes = (kUnmaskBlock / 64) * kFusedLdsPerWave > kV3LdsBytes
+                                        ? (kUnmaskBlock / 64) * kFusedLdsPerWave : kV3LdsBytes;
+template <bool ALL>
+__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_fused(
+    const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs,
+    FusedArgs A) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_raw[kFusedLdsBytes];
+  __shared__ uint32_t s_run;
+  if (!ALL && 2 * sum->run_frames >= sum->frames) {
+    uint32_t* s_start = reinterpret_cast<uint32_t*>(s_raw);
+    int32_t* s_lend = reinterpret_cast<int32_t*>(s_raw + 4 * kWinFrames);
+    uint64_t* s_delta = reinterpret_cast<uint64_t*>(s_raw + 8 * kWinFrames);
+    uint32_t* s_key = reinterpret_cast<uint32_t*>(s_raw + 16 * kWinFrames);
+    unmask_v3_body<16>(in, frames, tile_first, sum, out, big_grid, WinLds{s_start, s_lend, s_delta, s_key}, runs,
+                       &s_run);
+    return;
+  }
+  uint8_t* w = s_raw + (threadIdx.x >> 6) * kFusedLdsPerWave;
+  const FusedLds L{reinterpret_cast<FusedTab*>(w), reinterpret_cast<uint32_t*>(w + kFusedRound * sizeof(FusedTab)),
+                   reinterpret_cast<uint16_t*>(w + kFusedRound * (sizeof(FusedTab) + 4))};
+  fused_body(in, out, sum, A, L);
 }
 
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
@@ -649,26 +1069,29 @@ __global__ __launch_bounds__(256) void k_cipher(uint8_t* __restrict__ p, uint64_
 }
 
 using UnmaskFn = void (*)(const uint8_t*, const gevws_frame*, const uint32_t*, const gevws_summary*, uint8_t*,
-                         uint32_t, uint32_t*);
+                         uint32_t, uint32_t*, FusedArgs);
 struct UnmaskVariant {
   UnmaskFn fn;
   int unroll;
   const char* name;
-  bool wide = false;  // may launch the wide grid (k_unmask_auto)
-  bool runs = true;   // the v5 path's counter runs (else one contiguous run per workgroup)
+  bool wide = false;   // may launch the wide grid
+  bool runs = true;    // counter runs (v3 / v5) / the fused path's counters
+  int emit_gate = 0;   // k_walk_emit: 0 = every batch, 1 = not for mixed batches, 2 = never (the fused path writes the records)
 };
 // Variant 0 is the default (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 // The measurement variants of rounds 1-3 (v3 / v4 window shapes, interleaved
 // searches, phase-profiled builds, other occupancies) are gone from the
 // library; their measurements stay in profiles/ and DESIGN.md §5.
 const UnmaskVariant kUnmaskVariants[] = {
+    {k_unmask_fused<false>, 16,
+     "auto: v3 4-tile windows for batches of equal-size frames; for mixed sizes the fused record + unmask path "
+     "(records and payloads straight from the walk's entries, one wave per row, big frames in queued pieces)",
+     true, true, 1},
+    {k_unmask_v5, 16, "v5 for every batch (the round-4 mixed-batch path alone)", true, true, 0},
     {k_unmask_auto5, 16,
-     "auto: v3 4-tile windows for batches of equal-size frames, v5 (pipelined 8-tile windows with a chunk -> frame "
-     "map and the tile map cached in LDS) otherwise; non-temporal streaming and window loads; a wide grid for a "
-     "smaller batch of mixed sizes after one on this context", true},
-    {k_unmask_v5, 16, "v5 for every batch (the default's mixed-batch path alone)", true},
-    {k_unmask_auto5, 16, "the default with one contiguous run per workgroup on the v5 path (rounds 1-3; measurement)",
-     true, false},
+     "round 4's default: v3 for equal-size batches, v5 (pipelined 8-tile windows with a chunk -> frame map, records "
+     "read back) for mixed ones", true, true, 0},
+    {k_unmask_fused<true>, 16, "the fused record + unmask path for every batch", true, true, 2},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
@@ -679,17 +1102,19 @@ namespace gevws_impl {
 int unmask_variant_count() { return kNumUnmaskVariants; }
 const char* unmask_variant_name(int i) { return i >= 0 && i < kNumUnmaskVariants ? kUnmaskVariants[i].name : nullptr; }
 
+int unmask_emit_gate(const gevws_ctx* ctx) { return kUnmaskVariants[ctx->unmask_variant].emit_gate; }
+
 int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const uint8_t* d_in,
                   const gevws_frame* d_frames, const uint32_t* tile_first, const gevws_summary* d_summary,
-                  uint8_t* d_payload) {
+                  uint8_t* d_payload, const FusedArgs& fa) {
   const UnmaskVariant& v = kUnmaskVariants[ctx->unmask_variant];
   const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
   const uint32_t ucus = (uint32_t)ctx->num_cus;
   const uint64_t norm = 4 * (uint64_t)ucus;
   // the wide grid (kWideGridPerCU per CU) when the previous decode on this
   // context was a batch of mixed sizes (run frames < half) below
-  // kWideGridTiles; the kernel still uses `norm` workgroups unless this
-  // batch is one too
+  // kWideGridTiles; the v3 / v5 bodies still use `norm` workgroups unless
+  // this batch is one too (the fused path's waves take rows as they come)
   const bool wide = v.wide && !ctx->unmask_grid && ctx->stats_known && ctx->prev_mixed &&
                     ntiles < kWideGridTiles && norm <= 0xffffu;
   uint64_t grid = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : wide ? kWideGridPerCU * (uint64_t)ucus : norm;
@@ -699,7 +1124,7 @@ int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const ui
   ctx->last_unmask_grid = (uint32_t)grid;
   v.fn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary, d_payload,
                                                 ctx->unmask_grid ? 0u : ucus | (wide ? (uint32_t)norm << 16 : 0u),
-                                                v.runs ? ctx->unmask_runs : nullptr);
+                                                v.runs ? ctx->unmask_runs : nullptr, fa);
   return GEVWS_OK;
 }
 
