@@ -857,6 +857,14 @@ class Protocol:
         lib.gevws_protocol_get_stats(self._p, ctypes.byref(s))
         return {k: int(getattr(s, k)) for k, _ in _abi.ProtocolStats._fields_}
 
+    def timeline(self) -> dict:
+        """Where the batched passes' time went (gevws_protocol_get_timeline):
+        host ns per phase summed over the passes, and the one-launch kernels'
+        GPU ns for passes answered by the completion flag."""
+        t = _abi.ProtocolTimeline()
+        lib.gevws_protocol_get_timeline(self._p, ctypes.byref(t))
+        return {k: int(getattr(t, k)) for k, _ in _abi.ProtocolTimeline._fields_}
+
     def decode_host(self, segments: Sequence[Tuple[bytes, bytes]]):
         """gevws_decode_host_batch: [(first, end)] host segments per connection ->
         (frames, payload arena, conn_out, summary) as numpy arrays (the FFI form)."""

@@ -102,6 +102,11 @@ class ProtocolStats(ctypes.Structure):
                 ("chained_handler_passes", ctypes.c_uint64), ("signalled_passes", ctypes.c_uint64)]
 
 
+class ProtocolTimeline(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("passes", "signalled", "ns_select", "ns_stage", "ns_launch", "ns_wait",
+                                             "ns_deliver", "ns_gpu_decode", "ns_gpu_handler", "ns_gpu_gap")]
+
+
 class HostConn(ctypes.Structure):
     _fields_ = [("seg0", ctypes.c_void_p), ("n0", ctypes.c_uint64), ("seg1", ctypes.c_void_p),
                 ("n1", ctypes.c_uint64)]
@@ -171,6 +176,7 @@ SIGNATURES = {
     "gevws_ctx_device": (ctypes.c_int, [P]),
     "gevws_ctx_stream": (P, [P]),
     "gevws_ctx_order_after_last": (ctypes.c_int, [P, P]),
+    "gevws_ctx_set_timeline_ticks": (ctypes.c_int, [P, P]),
     "gevws_ctx_set_timing": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_ctx_set_tuning": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_last_split_lanes": (ctypes.c_int, [P]),
@@ -238,6 +244,7 @@ SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_uint32)]),
     "gevws_cipher": (None, [P, ctypes.c_uint64, P, ctypes.c_uint64]),
     "gevws_protocol_get_stats": (None, [P, ctypes.POINTER(ProtocolStats)]),
+    "gevws_protocol_get_timeline": (None, [P, ctypes.POINTER(ProtocolTimeline)]),
     "gevws_protocol_set_zero_copy_max": (None, [P, ctypes.c_uint64]),
     "gevws_protocol_set_handler": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_comm_create": (P, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),

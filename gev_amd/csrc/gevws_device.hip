@@ -261,6 +261,12 @@ int gevws_ctx_set_completion_flag(gevws_ctx* ctx, uint32_t* d_flag) {
 
 int64_t gevws_ctx_completion_seq(const gevws_ctx* ctx) { return ctx ? ctx->last_signal : -1; }
 
+int gevws_ctx_set_timeline_ticks(gevws_ctx* ctx, uint64_t* d_ticks) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  ctx->ticks = d_ticks;
+  return GEVWS_OK;
+}
+
 int gevws_ctx_last_unmask_grid(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_unmask_grid : -1; }
 
 int gevws_ctx_set_timing(gevws_ctx* ctx, int enable) {

@@ -863,8 +863,9 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
                                                             uint64_t out_cap, uint64_t* __restrict__ out_off,
                                                             gevws_summary* __restrict__ esum,
                                                             uint32_t* __restrict__ done = nullptr,
-                                                            uint32_t seq = 0) {
+                                                            uint32_t seq = 0, uint64_t* __restrict__ ticks = nullptr) {
   constexpr int WF = (int)kHandleSmallFrames;
+  const uint64_t t0 = done ? gpu_ticks() : 0;
   __shared__ int32_t s_start[WF];
   __shared__ int32_t s_pend[WF];
   __shared__ uint8_t s_hlen[WF];
@@ -964,7 +965,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
   }
   __syncthreads();
   if (s_status != (uint32_t)GEVWS_OK || wire == 0) {  // (workgroup-uniform)
-    signal_done(done, seq);
+    signal_done(done, seq, ticks, t0, 1);
     return;
   }
   // 4. the wire image, 16 bytes per lane (the last chunk's tail zeroed inside
@@ -980,7 +981,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
                                         payload, nullptr, 0);
     __builtin_memcpy(out + a, &x, 16);
   }
-  signal_done(done, seq);
+  signal_done(done, seq, ticks, t0, 1);
 }
 
 // GEVWS_TUNE_ENCODE_VARIANT: 0 = two tiles a wave step when the caller's
@@ -1126,7 +1127,7 @@ int gevws_handle_decoded_async(gevws_ctx* ctx, void* stream, const gevws_frame* 
   const uint32_t seq = ctx->done_flag ? ++ctx->done_seq : 0u;
   k_handle_small<<<1, kWalkBlock, 0, st>>>(d_frames, max_frames, d_decoded, policy, d_payload, aux_off, aux_cap,
                                            d_replies, d_reply_of, d_disp_summary, d_out, out_cap, d_out_off,
-                                           d_enc_summary, ctx->done_flag, seq);
+                                           d_enc_summary, ctx->done_flag, seq, ctx->done_flag ? ctx->ticks : nullptr);
   GEVWS_HIP(hipGetLastError());
   r = mark_last(ctx, st);
   if (ctx->done_flag) ctx->last_signal = seq;

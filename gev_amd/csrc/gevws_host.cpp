@@ -255,6 +255,7 @@ class Protocol {
   // but are not read; UnPacket ends a pass in flight first.
   int64_t BeginBatch(Connection* const* conns, RingBuffer* const* rings, uint32_t n) {
     if (pend_.active) return GEVWS_ERR_INVALID;
+    const auto tb0 = std::chrono::steady_clock::now();
     // Skipped: connections that still hold undelivered frames (their ring
     // prefix is decoded already), poisoned ones, ones whose first undecoded
     // frame is not complete yet (the carried gate), and repeats of a
@@ -279,6 +280,9 @@ class Protocol {
     DeviceScope scope(gevws_ctx_device(ctx_));
     pend_.sg = Staged{};
     Staged& sg = pend_.sg;
+    const auto tb1 = std::chrono::steady_clock::now();
+    tl_.ns_select += ns_since(tb0, tb1);
+    stage_end_ = tb1;
     int64_t r = StageDecode(segs.data(), m, &sg, true);
     if (r < 0) return r;
     pend_.conns.assign(conns, conns + n);
@@ -301,6 +305,9 @@ class Protocol {
         return fail();
     }
     pend_.active = true;
+    const auto tb2 = std::chrono::steady_clock::now();
+    tl_.ns_stage += ns_since(tb1, stage_end_);
+    tl_.ns_launch += ns_since(stage_end_, tb2);
     return (int64_t)m;
   }
 
@@ -310,8 +317,26 @@ class Protocol {
     DeviceScope scope(gevws_ctx_device(ctx_));
     Staged& sg = pend_.sg;
     std::shared_ptr<uint8_t> arena = std::move(pend_.arena);
+    const auto te0 = std::chrono::steady_clock::now();
     int64_t r = Finish(&sg);
     if (r < 0) return r;
+    const auto te1 = std::chrono::steady_clock::now();
+    ++tl_.passes;
+    tl_.ns_wait += ns_since(te0, te1);
+    if (last_signalled_ && h_ticks_ && !sg.retried) {
+      const uint64_t d0 = __atomic_load_n(h_ticks_ + 0, __ATOMIC_ACQUIRE), d1 = h_ticks_[1];
+      const uint64_t k0 = h_ticks_[2], k1 = h_ticks_[3];
+      ++tl_.signalled;
+      if (d1 > d0 && d0) tl_.ns_gpu_decode += (uint64_t)((double)(d1 - d0) * ns_per_tick_);
+      if (k1 > k0 && k0) tl_.ns_gpu_handler += (uint64_t)((double)(k1 - k0) * ns_per_tick_);
+      if (k0 > d1 && d1 && k0) tl_.ns_gpu_gap += (uint64_t)((double)(k0 - d1) * ns_per_tick_);
+      memset(h_ticks_, 0, 32);
+    }
+    struct DeliverTimer {  // the rest of EndBatch: queueing the frames on their connections
+      gevws_protocol_timeline& tl;
+      std::chrono::steady_clock::time_point t;
+      ~DeliverTimer() { tl.ns_deliver += ns_since(t, std::chrono::steady_clock::now()); }
+    } deliver_timer{tl_, te1};
     if (sg.zc) {
       arena = sg.arena;
     } else {
@@ -428,6 +453,7 @@ class Protocol {
   }
 
   void GetStats(gevws_protocol_stats* out) const { *out = stats_; }
+  void GetTimeline(gevws_protocol_timeline* out) const { *out = tl_; }
   int SetHandler(int policy) {
     if (policy < -1 || policy > GEVWS_HANDLER_ECHO_TEXT) return GEVWS_ERR_INVALID;
     handler_ = policy;
@@ -687,6 +713,7 @@ class Protocol {
     ++stats_.device_passes;
     stats_.conns_staged += m;
     stats_.bytes_staged += stage;
+    stage_end_ = std::chrono::steady_clock::now();
     return Launch(sg);
   }
 
@@ -747,15 +774,27 @@ class Protocol {
       h_flag_ = nullptr;
       return false;
     }
+    if (!h_ticks_ && hipHostMalloc((void**)&h_ticks_, 64, kHostFlags) == hipSuccess) {
+      int khz = 0;
+      if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, gevws_ctx_device(ctx_)) == hipSuccess &&
+          khz > 0)
+        ns_per_tick_ = 1e6 / khz;
+    }
+    if (h_ticks_) {
+      memset(h_ticks_, 0, 32);  // a kernel of this pass that stamps sets its end tick
+      (void)gevws_ctx_set_timeline_ticks(ctx_, (uint64_t*)device_of(h_ticks_));
+    }
     return true;
   }
   int64_t Wait(const Staged* sg) {
+    last_signalled_ = false;
     const int64_t seq = (sg->zc && sg->flagged) ? sg->seq : -1;
     if (seq >= 0) {
       const auto t0 = std::chrono::steady_clock::now();
       for (uint64_t i = 1;; ++i) {
         if (__atomic_load_n(h_flag_, __ATOMIC_ACQUIRE) == (uint32_t)seq) {
           ++stats_.signalled_passes;
+          last_signalled_ = true;
           return 0;
         }
         // a pass takes tens of us: past 50 ms, wait for the stream instead
@@ -822,6 +861,11 @@ class Protocol {
       (void)hipHostFree(h_flag_);
       h_flag_ = nullptr;
     }
+    if (h_ticks_) {
+      if (ctx_) (void)gevws_ctx_set_timeline_ticks(ctx_, nullptr);
+      (void)hipHostFree(h_ticks_);
+      h_ticks_ = nullptr;
+    }
     for (uint8_t* p : {h_in_, h_res_, h_out_, h_rof_, h_roff_, h_hs_})
       if (p) (void)hipHostFree(p);
     for (void* p : {d_in_, d_res_, d_frames_, d_payload_, d_rep_})
@@ -854,6 +898,16 @@ class Protocol {
   void* d_rep_ = nullptr;  // reply records (gevws_out_frame)
   uint64_t d_rep_cap_ = 0;
   gevws_protocol_stats stats_{};
+  // per-pass timeline (gevws_protocol_get_timeline): host phases and, via the
+  // one-launch kernels' tick stamps in h_ticks_ (mapped pinned u64[4]), GPU time
+  gevws_protocol_timeline tl_{};
+  uint64_t* h_ticks_ = nullptr;
+  double ns_per_tick_ = 10.0;  // 100 MHz unless the device says otherwise
+  std::chrono::steady_clock::time_point stage_end_;
+  bool last_signalled_ = false;
+  static uint64_t ns_since(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+  }
 };
 
 }  // namespace gevws
@@ -922,6 +976,10 @@ int64_t gevws_protocol_unpacket_batch_begin(gevws_protocol* p, gevws_conn* const
 int64_t gevws_protocol_unpacket_batch_end(gevws_protocol* p) {
   if (!p) return GEVWS_ERR_INVALID;
   return p->EndBatch();
+}
+
+void gevws_protocol_get_timeline(const gevws_protocol* p, gevws_protocol_timeline* out) {
+  if (p && out) p->GetTimeline(out);
 }
 
 void gevws_protocol_get_stats(const gevws_protocol* p, gevws_protocol_stats* out) {

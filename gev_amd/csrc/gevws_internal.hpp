@@ -26,6 +26,7 @@ struct gevws_ctx {
   uint64_t small_bytes = kSmallBytes;  // one-launch decode (k_decode_small) up to this many input bytes
   uint32_t* done_flag = nullptr;  // mapped host word the one-launch kernels signal (gevws_ctx_set_completion_flag)
   uint32_t done_seq = 0;
+  uint64_t* ticks = nullptr;  // mapped host u64[4]: the one-launch kernels' start / end ticks (gevws_ctx_set_timeline_ticks)
   int64_t last_signal = -1;  // the value the last call's last kernel stores there, -1: none
   // the context's history: the last multi-kernel decode's frame / payload /
   // equal-size-run totals (written by k_walk_bases into mapped host memory)

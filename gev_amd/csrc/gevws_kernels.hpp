@@ -259,9 +259,20 @@ constexpr uint64_t kSmallBytes = 64 * 1024;
 // then one lane stores `seq` with a system-scope release (a vector store), so
 // a host that sees the flag sees the results -- it spins on host memory
 // instead of waiting in hipStreamSynchronize (gevws_ctx_set_completion_flag).
-// Callers reach it with the whole workgroup (it holds a barrier).
-__device__ __forceinline__ void signal_done(uint32_t* done, uint32_t seq) {
+// Before the flag, with `ticks` set (gevws_ctx_set_timeline_ticks), thread 0
+// also stores the kernel's start tick t0 and its end tick (s_memrealtime, the
+// GPU's constant-rate wall clock) at ticks[2 slot], ticks[2 slot + 1] (slot 0:
+// the decode, 1: the handler step): the host's per-pass timeline
+// (gevws_protocol_get_timeline).  Callers reach it with the whole workgroup
+// (it holds a barrier).
+__device__ __forceinline__ uint64_t gpu_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void signal_done(uint32_t* done, uint32_t seq, uint64_t* ticks = nullptr, uint64_t t0 = 0,
+                                            int slot = 0) {
   if (!done) return;
+  if (ticks && threadIdx.x == 0) {
+    ticks[2 * slot] = t0;
+    ticks[2 * slot + 1] = gpu_ticks();
+  }
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1132,10 +1132,11 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
                                                               gevws_conn_out* __restrict__ cout,
                                                               gevws_summary* __restrict__ sum,
                                                               uint32_t* __restrict__ done = nullptr,
-                                                              uint32_t seq = 0) {
+                                                              uint32_t seq = 0, uint64_t* __restrict__ ticks = nullptr) {
   __shared__ uint64_t s_big[kSmallBig][3];  // {src_off, payload_off, length} of the larger payloads
   __shared__ uint32_t s_bkey[kSmallBig];
   __shared__ uint32_t s_nbig;
+  const uint64_t t0 = done ? gpu_ticks() : 0;
   const uint32_t c = threadIdx.x;
   if (c == 0) s_nbig = 0;
   gevws_conn_in ci{0, 0};
@@ -1187,7 +1188,7 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
     *sum = sm;
   }
   if (!ok) {  // capacity error: nothing written (uniform)
-    signal_done(done, seq);
+    signal_done(done, seq, ticks, t0, 0);
     return;
   }
   if (c < n) {
@@ -1249,7 +1250,7 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
       *reinterpret_cast<u32x4*>(payload + poff + 16 * j) = y;
     }
   }
-  signal_done(done, seq);
+  signal_done(done, seq, ticks, t0, 0);
 }
 
 // GEVWS_TUNE_WALK_VARIANT values (0 = the default choice per batch).
@@ -1277,7 +1278,8 @@ int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   if (r != GEVWS_OK) return r;
   const uint32_t seq = ctx->done_flag ? ++ctx->done_seq : 0u;
   k_decode_small<<<1, kSmallConns, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
-                                             payload_cap, d_conn_out, d_summary, ctx->done_flag, seq);
+                                             payload_cap, d_conn_out, d_summary, ctx->done_flag, seq,
+                                             ctx->done_flag ? ctx->ticks : nullptr);
   GEVWS_HIP(hipGetLastError());
   r = mark_last(ctx, st);
   if (ctx->done_flag) ctx->last_signal = seq;

@@ -66,6 +66,8 @@ struct DeviceDecoder {
   int reply(wslb::ServerConn* s, const uint8_t** out, uint64_t* len, int* shutdown_write) {
     return gevws_protocol_reply(p, s->c, out, len, shutdown_write);
   }
+  static constexpr bool kTimeline = true;
+  void timeline(gevws_protocol_timeline* t) const { gevws_protocol_get_timeline(p, t); }
   static const char* name() { return "device"; }
   static const char* path() { return "batched device decode (gevws_protocol_unpacket_batch) -> UnPacket"; }
 };

@@ -84,6 +84,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <string>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -94,6 +95,22 @@ namespace wslb {
 
 inline std::atomic<bool> g_stop{false};
 inline std::atomic<uint64_t> g_batches{0}, g_batch_conns{0}, g_frames{0}, g_bad{0}, g_dev_ns{0};
+// every loop's decoders' pass timelines (Decoder::kTimeline), summed at loop exit
+inline std::mutex g_tl_mu;
+inline gevws_protocol_timeline g_tl{};
+inline void add_timeline(const gevws_protocol_timeline& t) {
+  std::lock_guard<std::mutex> g(g_tl_mu);
+  g_tl.passes += t.passes;
+  g_tl.signalled += t.signalled;
+  g_tl.ns_select += t.ns_select;
+  g_tl.ns_stage += t.ns_stage;
+  g_tl.ns_launch += t.ns_launch;
+  g_tl.ns_wait += t.ns_wait;
+  g_tl.ns_deliver += t.ns_deliver;
+  g_tl.ns_gpu_decode += t.ns_gpu_decode;
+  g_tl.ns_gpu_handler += t.ns_gpu_handler;
+  g_tl.ns_gpu_gap += t.ns_gpu_gap;
+}
 inline std::atomic<uint64_t> g_ctrl{0}, g_closed{0}, g_sent_async{0}, g_payload{0};
 // OnConnect / OnClose of every server loop (wsExample.ClientNum,
 // example/websocket/wsserver_test.go:22-45): +1 at accept, -1 when the loop
@@ -464,6 +481,15 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
     g_dev_ns.fetch_add((uint64_t)(t_dec * 1e9), std::memory_order_relaxed);
   }
   if (pending) (void)dec.end();
+  if constexpr (Decoder::kTimeline) {
+    gevws_protocol_timeline t;
+    dec.timeline(&t);
+    add_timeline(t);
+    for (auto& d : decs) {
+      d->timeline(&t);
+      add_timeline(t);
+    }
+  }
   decs.clear();
   for (auto& kv : conns) {
     close(kv.first);
@@ -833,6 +859,24 @@ inline CloseResult close_client(int port, int n, unsigned seed) {
   return res;
 }
 
+// The batched passes' timeline per pass in microseconds (whole run, warm-up
+// included): host select / stage / launch / wait / deliver, and for passes
+// answered by the completion flag the kernels' own GPU time.
+inline std::string timeline_json() {
+  const gevws_protocol_timeline& t = g_tl;
+  if (t.passes == 0) return "null";
+  const double p = (double)t.passes, s = t.signalled ? (double)t.signalled : 1.0;
+  char b[512];
+  snprintf(b, sizeof(b),
+           "{\"passes\": %llu, \"select\": %.2f, \"stage\": %.2f, \"launch\": %.2f, \"wait\": %.2f, "
+           "\"deliver\": %.2f, \"signalled_share\": %.3f, \"gpu_decode\": %.2f, \"gpu_handler\": %.2f, "
+           "\"gpu_gap\": %.2f}",
+           (unsigned long long)t.passes, t.ns_select / p / 1e3, t.ns_stage / p / 1e3, t.ns_launch / p / 1e3,
+           t.ns_wait / p / 1e3, t.ns_deliver / p / 1e3, t.signalled / p, t.ns_gpu_decode / s / 1e3,
+           t.ns_gpu_handler / s / 1e3, t.ns_gpu_gap / s / 1e3);
+  return b;
+}
+
 template <class Decoder>
 int loopback_main(int argc, char** argv) {
   int conns = 1000, loops = 1, cthreads = 4, port = 0, device = 0, ndev = 1;
@@ -941,14 +985,14 @@ int loopback_main(int argc, char** argv) {
          "\"mean_conns_per_pass\": %.1f, \"decode_us_per_pass\": %.1f, \"decode_share_of_loop_time\": %.3f, "
          "\"client_checked_echoes\": %llu, \"mode\": \"%s\", \"control_frames\": %llu, "
          "\"async_sends\": %llu, \"closes_answered\": %llu, \"transcript_pairs\": %zu, \"devices\": %d, "
-         "\"errors\": %llu}\n",
+         "\"pass_timeline_us\": %s, \"errors\": %llu}\n",
          Decoder::path(), Decoder::name(), conns, upgraded.load(), wss ? (size_t)0 : msg, loops, cthreads, dt, mps,
          (double)(p1 - p0) / dt / 1048576.0, (double)(b1 - b0) / dt,
          b1 > b0 ? (double)(c1 - c0) / (double)(b1 - b0) : 0.0,
          b1 > b0 ? (double)(d1 - d0) / 1e3 / (double)(b1 - b0) : 0.0, (double)(d1 - d0) / 1e9 / (dt * loops),
          (unsigned long long)total.load(), wss ? "wsserver" : "echo", (unsigned long long)g_ctrl.load(),
          (unsigned long long)g_sent_async.load(), (unsigned long long)g_closed.load(), g_transcript.size(), ndev,
-         (unsigned long long)g_bad.load());
+         timeline_json().c_str(), (unsigned long long)g_bad.load());
   return g_bad.load() == 0 && upgraded.load() == conns ? 0 : 1;
 }
 

@@ -206,6 +206,12 @@ int gevws_ctx_last_split_lanes(const gevws_ctx *ctx);
  * stores, or -1 when that call ended with another kernel or copy (the caller
  * synchronises the stream as usual). */
 int gevws_ctx_set_completion_flag(gevws_ctx *ctx, uint32_t *d_flag);
+/* With a completion flag set: d_ticks (device address of 4 u64 in mapped,
+ * coherent host memory, or NULL = off) receives, before the flag, each
+ * one-launch kernel's start and end tick of the GPU's constant-rate wall
+ * clock (s_memrealtime; hipDeviceAttributeWallClockRate kHz): [0] / [1] the
+ * small-batch decode, [2] / [3] the one-workgroup handler step. */
+int gevws_ctx_set_timeline_ticks(gevws_ctx *ctx, uint64_t *d_ticks);
 int64_t gevws_ctx_completion_seq(const gevws_ctx *ctx);
 /* Workgroups of the last multi-kernel decode's unmask launch (-1 for a null
  * context): 4 per CU, or 32 per CU after a decode on this context of a batch
@@ -510,6 +516,28 @@ typedef struct gevws_protocol_stats {
                                       * instead of a stream synchronisation */
 } gevws_protocol_stats;
 void gevws_protocol_get_stats(const gevws_protocol *p, gevws_protocol_stats *out);
+
+/* Where a batched pass's time goes (measurement, not on the reference path):
+ * host nanoseconds summed over the batched passes so far -- selecting the
+ * ready connections (the host gate, protocol.go:47), staging their bytes into
+ * pinned memory, enqueuing the launches (and copies), waiting for the
+ * completion flag or the stream, and queueing the frames on their
+ * connections -- and, for passes answered by the completion flag, the
+ * one-launch kernels' own GPU time from their tick stamps.  ns_wait minus the
+ * GPU time is the launch and completion latency. */
+typedef struct gevws_protocol_timeline {
+    uint64_t passes;
+    uint64_t signalled;        /* passes whose wait was the completion flag (GPU times below) */
+    uint64_t ns_select;
+    uint64_t ns_stage;
+    uint64_t ns_launch;
+    uint64_t ns_wait;
+    uint64_t ns_deliver;
+    uint64_t ns_gpu_decode;    /* signalled passes: k_decode_small's start -> end */
+    uint64_t ns_gpu_handler;   /* signalled passes with the handler step: k_handle_small's */
+    uint64_t ns_gpu_gap;       /* signalled passes with the handler: decode end -> handler start */
+} gevws_protocol_timeline;
+void gevws_protocol_get_timeline(const gevws_protocol *p, gevws_protocol_timeline *out);
 
 /* Batched passes over at most `bytes` of buffered input (default
  * GEVWS_ZERO_COPY_MAX_DEFAULT; 0 = never) run zero-copy: the kernels read the

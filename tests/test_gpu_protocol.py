@@ -594,3 +594,34 @@ def test_reply_follows_the_frames_own_pass(engine):
     assert h is not None and data == b"ping"
     fr = wo.decode_stream(ping).frames[0]
     assert proto.reply(c) == wo.on_message(fr.header, fr.payload, wo.HANDLER_ECHO_TEXT)
+
+
+def test_pass_timeline_small_zero_copy_pass(engine):
+    """gevws_protocol_get_timeline: a small zero-copy pass
+    (one launch, answered by the completion flag) reports its host phases and
+    the kernel's own GPU time from its tick stamps; the frames are still the
+    oracle's."""
+    rng = np.random.default_rng(5)
+    proto = gev_amd.Protocol(engine)
+    conns = [gev_amd.Connection() for _ in range(100)]
+    rings, streams = [], []
+    for c in conns:
+        s = b"".join(wo.encode_frame(bytes(rng.integers(0, 256, 128, dtype=np.uint8)), 1, True, 0, True,
+                                     bytes(rng.integers(0, 256, 4, dtype=np.uint8))) for _ in range(2))
+        r = gev_amd.RingBuffer(4096)
+        r.write(s)
+        rings.append(r)
+        streams.append(s)
+    for k in range(3):
+        assert proto.unpacket_batch(conns, rings) == 200
+        for c, r, s in zip(conns, rings, streams):
+            for fr in wo.decode_stream(s).frames:
+                h, data = proto.unpacket(c, r)
+                assert data == fr.payload
+            r.write(s)
+    t = proto.timeline()
+    assert t["passes"] == 3 and t["signalled"] == 3, t
+    for k in ("ns_select", "ns_stage", "ns_launch", "ns_wait", "ns_deliver", "ns_gpu_decode"):
+        assert t[k] > 0, (k, t)
+    assert t["ns_gpu_decode"] < t["ns_wait"] < 3 * 10**9, t  # the kernel ran inside the wait
+    assert t["ns_gpu_handler"] == 0 and t["ns_gpu_gap"] == 0

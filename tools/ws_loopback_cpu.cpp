@@ -34,6 +34,8 @@ struct CpuDecoder {
   ~CpuDecoder() { gevws_upgrader_free(u); }
   int64_t pass(wslb::ServerConn* const*, uint32_t) { return 0; }  // per-frame decode happens in unpacket
   static constexpr bool kPipelined = false;  // nothing to overlap: the decode runs in unpacket
+  static constexpr bool kTimeline = false;    // no device passes
+  void timeline(gevws_protocol_timeline*) const {}
   int64_t begin(wslb::ServerConn* const*, uint32_t) { return 0; }
   int64_t end() { return 0; }
   // no device handler: the wsserver mode's text echo is framed on the host
