@@ -154,18 +154,22 @@ def cpu_baseline(name: str, seconds: float, threads: int, vectorized: bool = Fal
 
 def load_traffic(config_name: str):
     """HBM bytes per unmask launch from a committed rocprofv3 --pmc pass (see
-    profiles/README.md), or None.  The passes are taken at N = 1,
-    so the figure applies to a rank's launch only when that rank runs the same
-    batch (N = 1, or weak scaling)."""
+    profiles/README.md) and where they come from (file and
+    commit), or (None, None).  The passes are taken at N = 1, so the figure
+    applies to a rank's launch only when that rank runs the same batch (N = 1,
+    or weak scaling)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     try:
         d = json.load(open(p))
         e = d.get(config_name)
-        return None if e is None else int(e["hbm_bytes_per_launch"])
+        if e is None:
+            return None, None
+        return int(e["hbm_bytes_per_launch"]), {"file": e.get("source"), "commit": e.get("commit"),
+                                                "kernel": e.get("kernel")}
     except Exception:
-        return None
+        return None, None
 
 
 def _free_port() -> int:
@@ -524,6 +528,10 @@ def main():
     if rank != 0:
         dist.finalize()
         return
+    # (the committed counts describe the default kernels on the full batch)
+    traffic, traffic_src = (load_traffic(args.config)
+                            if (scaling == "weak" or world == 1) and not emulated and not args.unmask_variant
+                            and not args.walk_variant else (None, None))
     result = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -555,7 +563,7 @@ def main():
         "phases_ms": {"walk_count": round(mean_ms[0], 4), "scan": round(mean_ms[1], 4),
                       "walk_emit": round(mean_ms[2], 4), "unmask": round(unmask_ms, 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": (load_traffic(args.config) if (scaling == "weak" or world == 1) and not emulated else None),
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "k_unmask", "algorithmic_bytes_per_launch": alg_bytes,
                      "pipeline_achieved": round(pipeline_gbps, 1),
                      "pipeline_frac": round(pipeline_gbps / HBM_PEAK_GBPS, 4),

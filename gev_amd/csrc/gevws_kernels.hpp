@@ -311,10 +311,10 @@ constexpr uint64_t kWideGridTiles = 2ull << 20;
 constexpr uint32_t kUnmaskRunCounters = 8;
 // The decode scratch's work counters, 64 bytes apart, zeroed by k_walk_bases
 // for every decode: slots 0-7 the per-XCD runs above (or the fused record +
-// unmask path's per-XCD row counters), 8 rows finished, 9 pieces queued, 10
-// pieces taken (the fused path, gevws_unmask.hip).
-constexpr uint32_t kWorkCounters = 16;
-constexpr uint32_t kCtrRowsDone = 8, kCtrPieces = 9, kCtrCursor = 10;
+// unmask path's per-XCD row counters), 8 rows finished, 9 pieces queued,
+// 16-23 the per-XCD piece cursors (the fused path, gevws_unmask.hip).
+constexpr uint32_t kWorkCounters = 24;
+constexpr uint32_t kCtrRowsDone = 8, kCtrPieces = 9, kCtrCursor = 16;
 constexpr uint64_t kUnmaskRun = 16;
 constexpr uint64_t kUnmaskRunMinTiles = 64;  // the v3 path's counter runs: tiles a workgroup at least
 

@@ -615,7 +615,7 @@ constexpr uint32_t kFusedStep = 8;                    // chunks per lane per unm
 constexpr uint32_t kFusedStepChunks = 64 * kFusedStep;
 constexpr uint64_t kFusedStepBytes = 16ull * kFusedStepChunks;
 constexpr uint64_t kPieceBytes = 64 * 1024;           // a deferred frame's piece
-constexpr uint32_t kFusedMaxSpins = 1u << 24;         // a wave waiting for a piece gives up after this many sleeps
+constexpr uint32_t kFusedMaxSpins = 1u << 21;         // a wave waiting for a piece gives up after this many sleeps (~3 s)
 
 struct FusedTab {
   uint64_t delta;  // src_off - payload_off (mod 2^64)
@@ -922,44 +922,48 @@ __device__ void fused_body(const uint8_t* __restrict__ in, uint8_t* __restrict__
       __hip_atomic_fetch_add(A.ctr + kCtrRowsDone * 16, (uint32_t)(r1 - r0), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
   }
-  // 2. pieces, until every row is done and every queued piece taken
+  // 2. pieces: the waves of XCD x take queue indices x, x + 8, ... in turn
+  // (one fetch-add each on that XCD's cursor; a compare-and-swap on one
+  // shared cursor serialised thousands of waves per claim: C4 1 982 ms); a
+  // claimed index is processed once queued, or dropped once every row is
+  // done and the queue ended below it
   uint32_t spins = 0;
+  bool have = false;
+  uint64_t idx = 0;
   for (;;) {
-    uint32_t pc = agent_ld32(A.ctr + kCtrPieces * 16);
-    uint32_t cur = agent_ld32(A.ctr + kCtrCursor * 16);
-    if (cur >= pc) {
-      if (agent_ld32(A.ctr + kCtrRowsDone * 16) >= n) {
-        // every row is done, so the piece count is final
-        pc = agent_ld32(A.ctr + kCtrPieces * 16);
-        cur = agent_ld32(A.ctr + kCtrCursor * 16);
-        if (cur >= pc) break;
-      } else {
-        if (++spins > kFusedMaxSpins) break;
-        __builtin_amdgcn_s_sleep(8);
-        continue;
+    if (!have) {
+      uint32_t k = 0;
+      if (lane == 0)
+        k = __hip_atomic_fetch_add(A.ctr + (kCtrCursor + xc) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      idx = (uint64_t)uniform32((uint32_t)__shfl((int)k, 0, 64)) * kUnmaskRunCounters + xc;
+      have = true;
+    }
+    if (idx >= A.piece_cap) break;  // (beyond any queue this decode can have)
+    if (idx < uniform32(agent_ld32(A.ctr + kCtrPieces * 16))) {
+      const uint64_t* e = A.pieces + 4 * idx;
+      uint32_t wait = 0;
+      while (uniform64(agent_ld64(e + 3)) != A.gen) {  // queued, not yet stamped
+        if (++wait > kFusedMaxSpins) break;
+        __builtin_amdgcn_s_sleep(2);
       }
+      if (wait > kFusedMaxSpins) {
+        spins = kFusedMaxSpins + 1;
+        break;
+      }
+      const uint64_t src = uniform64(agent_ld64(e + 0)), dst = uniform64(agent_ld64(e + 1));
+      const uint64_t w2 = uniform64(agent_ld64(e + 2));
+      fused_piece(in, out, src, dst, w2 >> 32, (uint32_t)w2);
+      have = false;
+      spins = 0;
+      continue;
     }
-    uint32_t got = 0;
-    if (lane == 0)
-      got = __hip_atomic_compare_exchange_strong(A.ctr + kCtrCursor * 16, &cur, cur + 1, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
-    if (!uniform32(__shfl((int)got, 0, 64))) continue;  // another wave took it
-    const uint64_t idx = uniform32(__shfl((int)cur, 0, 64));
-    if (idx >= A.piece_cap) continue;
-    const uint64_t* e = A.pieces + 4 * idx;
-    uint32_t wait = 0;
-    while (uniform64(agent_ld64(e + 3)) != A.gen) {  // queued, not yet stamped
-      if (++wait > kFusedMaxSpins) break;
-      __builtin_amdgcn_s_sleep(2);
+    if (uniform32(agent_ld32(A.ctr + kCtrRowsDone * 16)) >= n) {
+      // every row is done, so the piece count is final
+      if (idx >= uniform32(agent_ld32(A.ctr + kCtrPieces * 16))) break;
+      continue;
     }
-    if (wait > kFusedMaxSpins) {
-      spins = kFusedMaxSpins + 1;
-      break;
-    }
-    const uint64_t src = uniform64(agent_ld64(e + 0)), dst = uniform64(agent_ld64(e + 1));
-    const uint64_t w2 = uniform64(agent_ld64(e + 2));
-    fused_piece(in, out, src, dst, w2 >> 32, (uint32_t)w2);
-    spins = 0;
+    if (++spins > kFusedMaxSpins) break;
+    __builtin_amdgcn_s_sleep(64);
   }
   if (spins > kFusedMaxSpins && lane == 0)  // gave up waiting: the output is incomplete, say so
     __hip_atomic_store(&A.sum->status, (int32_t)GEVWS_ERR_DEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

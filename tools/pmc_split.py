@@ -79,8 +79,14 @@ def main():
                     help="also record the unmask kernel's bytes per launch in profiles/pmc_traffic.json "
                          "(bench.py's roofline.traffic)")
     ap.add_argument("--source", default=None, help="profile file named as the source in pmc_traffic.json")
+    ap.add_argument("--commit", default=None,
+                    help="the commit the counted kernels were built from (default: this checkout's HEAD)")
     args = ap.parse_args()
     res = {cfg: table(args.src, args.prefix, cfg) for cfg in args.configs}
+    if args.traffic and args.commit is None:
+        import subprocess
+        args.commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                     text=True).stdout.strip() or None
     if args.traffic:
         tj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         tab = json.load(open(tj)) if os.path.exists(tj) else {}
@@ -93,7 +99,8 @@ def main():
                         "read_bytes": int(d["read_bytes"]), "write_bytes": int(d["write_bytes"]),
                         "method": "TCC_EA0_RDREQ_{32B,64B,128B} x size + TCC_EA0_WRREQ(_64B) x size, per launch "
                                   "(exact for any access width; FETCH_SIZE tallies 128-B reads at 64 B on gfx950)",
-                        "source": args.source or f"gpurun_out/{args.prefix}_{cfg}_rd,_wr"}
+                        "source": args.source or f"gpurun_out/{args.prefix}_{cfg}_rd,_wr",
+                        "commit": args.commit}
         json.dump(tab, open(tj, "w"), indent=1)
     for cfg, t in res.items():
         print(f"== {cfg}")
