@@ -611,20 +611,21 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
 // written after its other words are complete (s_waitcnt), a wave's rows
 // counted done after every piece it queued is complete.
 constexpr uint32_t kFusedRound = 256;                 // frames per round (4 entries a lane)
-constexpr uint32_t kFusedStep = 8;                    // chunks per lane per unmask step
-constexpr uint32_t kFusedStepChunks = 64 * kFusedStep;
-constexpr uint64_t kFusedStepBytes = 16ull * kFusedStepChunks;
+constexpr uint32_t kFusedStepMax = 16;                // chunks per lane per unmask step, at most
+constexpr uint32_t kFusedStepChunks = 64 * kFusedStepMax;
 constexpr uint64_t kPieceBytes = 64 * 1024;           // a deferred frame's piece
 constexpr uint32_t kFusedMaxSpins = 1u << 21;         // a wave waiting for a piece gives up after this many sleeps (~3 s)
 
-struct FusedTab {
+struct FusedTab {  // one slot of a round (32 bytes)
   uint64_t delta;  // src_off - payload_off (mod 2^64)
   uint64_t end;    // payload_off + length; payload_off for a deferred frame (no inline chunk)
+  uint64_t start;  // payload_off
+  uint32_t key;
+  uint32_t pd;     // padded length, saturated at 2^32 - 16 (such a frame is deferred whatever it is); 0: none
 };
 struct FusedLds {
   FusedTab* tab;   // [kFusedRound] per wave (the round's frames; lane 0's re-walk entries before that)
-  uint32_t* key;   // [kFusedRound]
-  uint16_t* own;   // [kFusedStepChunks] chunk -> slot + 1
+  uint16_t* own;   // [64 S] chunk -> slot + 1
 };
 
 __device__ __forceinline__ uint64_t agent_ld64(const uint64_t* p) {
@@ -666,14 +667,30 @@ __device__ __forceinline__ void fused_piece(const uint8_t* __restrict__ in, uint
   }
 }
 
-// The round's payload range [R0, R1): slots s = u * 64 + lane hold frames with
-// payload offset po[u] and padded length pd[u] (0: no payload / no frame).
+// The round's payload range [R0, R1): slot s = u * 64 + lane of the wave's
+// LDS table holds a frame's payload offset (start) and padded length (pd; 0:
+// no payload / no frame); a lane reads its four slots' at every step (held in
+// registers across the round they pushed the S = 16 loads into scratch).
+// S chunks per lane per step (S KiB per wave): at S = 16 the loaded vectors
+// take 64 VGPRs, so a chunk keeps only its slot (a byte of 4 packed words)
+// across the loads and re-reads its key and payload end from LDS to store.
+template <int S>
 __device__ __forceinline__ void fused_unmask_range(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                   const FusedLds& L, const uint64_t (&po)[4], const uint64_t (&pd)[4],
-                                                   uint64_t R0, uint64_t R1, uint64_t big_bytes) {
+                                                   const FusedLds& L, uint64_t R0, uint64_t R1, uint64_t big_bytes) {
+  static_assert(S == 8 || S == 16, "8 or 16 chunks a lane");
+  constexpr uint64_t SB = 1024ull * S;  // bytes per step
+  constexpr int MQ = S / 8;             // u32x4 words of the map per lane
   const uint32_t lane = threadIdx.x & 63;
   uint64_t p = R0;
   while (p < R1) {  // wave-uniform
+    uint64_t po[4];
+    uint32_t pd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(&L.tab[u * 64 + lane].start);  // start, key, pd
+      po[u] = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+      pd[u] = w[3];
+    }
     // the frame covering p: the last slot with a payload starting at or before it
     int s = -1;
 #pragma unroll
@@ -687,50 +704,59 @@ __device__ __forceinline__ void fused_unmask_range(const uint8_t* __restrict__ i
     for (int u = 0; u < 4; ++u)
       if (u == (s >> 6)) {
         spo = uniform64(__shfl(po[u], s & 63, 64));
-        spd = uniform64(__shfl(pd[u], s & 63, 64));
+        spd = uniform32((uint32_t)__shfl((int)pd[u], s & 63, 64));
       }
-    if (spd >= big_bytes) {  // a deferred frame: its pieces are queued
-      p = spo + spd;
+    if (spd >= big_bytes) {  // a deferred frame (pieces queued): on to the next payload after p
+      uint64_t nxt = R1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t m = __ballot(pd[u] > 0 && po[u] > p);
+        if (nxt == R1 && m) nxt = uniform64(__shfl(po[u], __builtin_ctzll(m), 64));
+      }
+      p = nxt;
       continue;
     }
-    if (spo + spd >= p + kFusedStepBytes) {  // the whole step inside frame s: stream it
+    if (spo + spd >= p + SB) {  // the whole step inside frame s: stream it
       const FusedTab te = L.tab[s];
-      const uint32_t key = L.key[s];
-      u32x4 v[kFusedStep];
+      const uint32_t key = te.key;
+      u32x4 v[S];
 #pragma unroll
-      for (int u = 0; u < (int)kFusedStep; ++u)
+      for (int u = 0; u < S; ++u)
         v[u] = ld16u_stream<true>(in + (p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16 + te.delta));
 #pragma unroll
-      for (int u = 0; u < (int)kFusedStep; ++u) {
+      for (int u = 0; u < S; ++u) {
         const uint64_t q = p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16;
         u32x4 x = v[u] ^ key;
         const int64_t rem = (int64_t)(te.end - q);
         if (rem < 16) x = keep_bytes(x, rem);
         st16_nt(out + q, x);
       }
-      p += kFusedStepBytes;
+      p += SB;
       continue;
     }
     // chunk -> slot map of the step: marks of the frames starting inside it,
     // then a wave prefix max seeded with slot s
-    reinterpret_cast<u32x4*>(L.own)[lane] = u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < MQ; ++k) reinterpret_cast<u32x4*>(L.own)[lane * MQ + k] = u32x4{0, 0, 0, 0};
     lds_fence();
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (pd[u] > 0 && po[u] > p && po[u] < p + kFusedStepBytes)
-        L.own[(po[u] - p) >> 4] = (uint16_t)(u * 64 + lane + 1);
+      if (pd[u] > 0 && po[u] > p && po[u] < p + SB) L.own[(po[u] - p) >> 4] = (uint16_t)(u * 64 + lane + 1);
     lds_fence();
     {
-      u32x4 m = reinterpret_cast<const u32x4*>(L.own)[lane];
-      uint32_t run[8];
+      uint32_t run[8 * MQ];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        run[2 * k] = m[k] & 0xffffu;
-        run[2 * k + 1] = m[k] >> 16;
+      for (int k = 0; k < MQ; ++k) {
+        const u32x4 m = reinterpret_cast<const u32x4*>(L.own)[lane * MQ + k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          run[8 * k + 2 * j] = m[j] & 0xffffu;
+          run[8 * k + 2 * j + 1] = m[j] >> 16;
+        }
       }
 #pragma unroll
-      for (int k = 1; k < 8; ++k) run[k] = run[k] > run[k - 1] ? run[k] : run[k - 1];
-      uint32_t inc = run[7];
+      for (int k = 1; k < 8 * MQ; ++k) run[k] = run[k] > run[k - 1] ? run[k] : run[k - 1];
+      uint32_t inc = run[8 * MQ - 1];
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
@@ -741,48 +767,57 @@ __device__ __forceinline__ void fused_unmask_range(const uint8_t* __restrict__ i
       const uint32_t seed = (uint32_t)s + 1;
       exc = exc > seed ? exc : seed;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t lo16 = run[2 * k] > exc ? run[2 * k] : exc;
-        const uint32_t hi16 = run[2 * k + 1] > exc ? run[2 * k + 1] : exc;
-        m[k] = lo16 | (hi16 << 16);
+      for (int k = 0; k < MQ; ++k) {
+        u32x4 m;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t lo16 = run[8 * k + 2 * j] > exc ? run[8 * k + 2 * j] : exc;
+          const uint32_t hi16 = run[8 * k + 2 * j + 1] > exc ? run[8 * k + 2 * j + 1] : exc;
+          m[j] = lo16 | (hi16 << 16);
+        }
+        reinterpret_cast<u32x4*>(L.own)[lane * MQ + k] = m;
       }
-      reinterpret_cast<u32x4*>(L.own)[lane] = m;
     }
     lds_fence();
-    u32x4 v[kFusedStep];
-    uint32_t key[kFusedStep];
-    int32_t rem[kFusedStep];
+    u32x4 v[S];
+    uint32_t sl4[S / 4];  // each chunk's slot, a byte each
+    uint32_t live = 0;    // chunks with payload bytes
 #pragma unroll
-    for (int u = 0; u < (int)kFusedStep; ++u) {
+    for (int k = 0; k < S / 4; ++k) sl4[k] = 0;
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
       const uint32_t c = (uint32_t)u * 64 + (fresh_tid() & 63);
       const uint64_t q = p + 16ull * c;
-      rem[u] = 0;
-      key[u] = 0;
       v[u] = u32x4{0, 0, 0, 0};
       if (q < R1) {
         const uint32_t sl = (uint32_t)L.own[c] - 1u;
-        const FusedTab te = L.tab[sl];
-        const int64_t r = (int64_t)(te.end - q);
-        rem[u] = r <= 0 ? 0 : (r > 16 ? 16 : (int32_t)r);
-        key[u] = L.key[sl];
-        if (r > 0) v[u] = ld16u_stream<true>(in + (q + te.delta));
+        const u64x2 te = *reinterpret_cast<const u64x2*>(&L.tab[sl]);  // delta, end
+        sl4[u >> 2] |= sl << (8 * (u & 3));
+        if ((int64_t)(te[1] - q) > 0) {
+          live |= 1u << u;
+          v[u] = ld16u_stream<true>(in + (q + te[0]));
+        }
       }
     }
 #pragma unroll
-    for (int u = 0; u < (int)kFusedStep; ++u) {
-      if (rem[u] > 0) {
-        u32x4 x = v[u] ^ key[u];
-        if (rem[u] < 16) x = keep_bytes(x, rem[u]);
-        st16_nt(out + p + 16ull * ((uint32_t)u * 64 + (fresh_tid() & 63)), x);
+    for (int u = 0; u < S; ++u) {
+      if (live & (1u << u)) {
+        const uint32_t sl = (sl4[u >> 2] >> (8 * (u & 3))) & 0xffu;
+        const uint64_t q = p + 16ull * ((uint32_t)u * 64 + (fresh_tid() & 63));
+        const int64_t rem = (int64_t)(L.tab[sl].end - q);
+        u32x4 x = v[u] ^ L.tab[sl].key;
+        if (rem < 16) x = keep_bytes(x, rem);
+        st16_nt(out + q, x);
       }
     }
     lds_fence();  // (the next step's map clear after this step's reads)
-    p += kFusedStepBytes;
+    p += SB;
   }
 }
 
 // One row: records + inline unmask of its frames below A.big_bytes, pieces of
 // the others queued.
+template <int S>
 __device__ __forceinline__ void fused_row(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                           const FusedArgs& A, const FusedLds& L, uint64_t c, bool unordered) {
   const uint32_t lane = threadIdx.x & 63;
@@ -834,12 +869,12 @@ __device__ __forceinline__ void fused_row(const uint8_t* __restrict__ in, uint8_
       lds_fence();
     }
     const uint64_t R0 = carry;
-    uint64_t po[4], pd[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      po[u] = 0;
-      pd[u] = 0;
-      if (k0 + (uint64_t)u * 64 >= cnt) continue;  // wave-uniform
+      if (k0 + (uint64_t)u * 64 >= cnt) {  // wave-uniform: no frames in these slots
+        L.tab[u * 64 + lane].pd = 0;
+        continue;
+      }
       const uint64_t k = k0 + (uint64_t)u * 64 + lane;
       const bool valid = k < cnt;
       uint64_t Ln, ip;
@@ -851,7 +886,8 @@ __device__ __forceinline__ void fused_row(const uint8_t* __restrict__ in, uint8_
       const uint64_t poff = carry + incl - padded;
       const uint64_t src = coff + pcarry + ip - fsz + hlen;
       const uint32_t key = q[u].mask;  // 0 for an unmasked frame (the walk zeroes it)
-      const bool big = valid && padded >= A.big_bytes;
+      const uint32_t pds = padded < 0xfffffff0ull ? (uint32_t)padded : 0xfffffff0u;
+      const bool big = valid && pds >= A.big_bytes;
       if (valid) {
         const uint32_t b0 = q[u].w & 0xffu, masked = (q[u].w >> 8) & 1u;
         const uint32_t flags = (b0 >> 7) | (((b0 & 0x70u) >> 4) << 8) | ((b0 & 0x0fu) << 16) | (masked << 24);
@@ -860,10 +896,7 @@ __device__ __forceinline__ void fused_row(const uint8_t* __restrict__ in, uint8_
         r[1] = u32x4{(uint32_t)poff, (uint32_t)(poff >> 32), (uint32_t)src, (uint32_t)(src >> 32)};
       }
       const uint32_t s = (uint32_t)u * 64 + lane;
-      L.tab[s] = FusedTab{src - poff, big ? poff : poff + Ln};
-      L.key[s] = key;
-      po[u] = poff;
-      pd[u] = padded;
+      L.tab[s] = FusedTab{src - poff, big ? poff : poff + Ln, poff, key, pds};
       if (__ballot(big)) {  // queue the deferred frames' pieces
         const uint64_t np = big ? (padded + kPieceBytes - 1) / kPieceBytes : 0;
         const uint64_t ni = wave_incl_scan(np);
@@ -890,10 +923,11 @@ __device__ __forceinline__ void fused_row(const uint8_t* __restrict__ in, uint8_
       pcarry += uniform64(__shfl(ip, 63, 64));
     }
     lds_fence();
-    fused_unmask_range(in, out, L, po, pd, R0, carry, A.big_bytes);
+    fused_unmask_range<S>(in, out, L, R0, carry, A.big_bytes);
   }
 }
 
+template <int S>
 __device__ void fused_body(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                            const gevws_summary* __restrict__ sum, const FusedArgs& A, const FusedLds& L) {
   if (sum->status != GEVWS_OK) return;
@@ -916,7 +950,7 @@ __device__ void fused_body(const uint8_t* __restrict__ in, uint8_t* __restrict__
       continue;
     }
     const uint64_t r1 = r0 + A.unit_rows < s1 ? r0 + A.unit_rows : s1;
-    for (uint64_t c = r0; c < r1; ++c) fused_row(in, out, A, L, c, unordered);
+    for (uint64_t c = r0; c < r1; ++c) fused_row<S>(in, out, A, L, c, unordered);
     __builtin_amdgcn_s_waitcnt(0);  // every piece this wave queued is complete
     if (lane == 0)
       __hip_atomic_fetch_add(A.ctr + kCtrRowsDone * 16, (uint32_t)(r1 - r0), __ATOMIC_RELAXED,
@@ -1018,30 +1052,30 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
 // tile map from k_walk_emit), mixed ones the fused record + unmask path (the
 // record pass skipped them, k_walk_emit's gate); ALL = the fused path for
 // every batch (GEVWS_TUNE_UNMASK_VARIANT 3; the record pass skips every batch).
-constexpr uint32_t kFusedLdsPerWave = kFusedRound * (sizeof(FusedTab) + 4) + kFusedStepChunks * 2;
-constexpr uint32_t kV3LdsBytes = kWinFrames * (4 + 4 + 8 + 4);
+constexpr uint32_t kFusedLdsPerWave = kFusedRound * sizeof(FusedTab) + kFusedStepChunks * 2;
+constexpr uint32_t kV3LdsBytes = kWinFrames * (4 + 4 + 8 + 4) + 16;
 constexpr uint32_t kFusedLdsBytes = (kUnmaskBlock / 64) * kFusedLdsPerWave > kV3LdsBytes
                                         ? (kUnmaskBlock / 64) * kFusedLdsPerWave : kV3LdsBytes;
-template <bool ALL>
+static_assert(4 * kFusedLdsBytes <= 160 * 1024, "four workgroups a CU");
+template <bool ALL, int S = 16>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_fused(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
     const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs,
     FusedArgs A) {
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[kFusedLdsBytes];
-  __shared__ uint32_t s_run;
   if (!ALL && 2 * sum->run_frames >= sum->frames) {
     uint32_t* s_start = reinterpret_cast<uint32_t*>(s_raw);
     int32_t* s_lend = reinterpret_cast<int32_t*>(s_raw + 4 * kWinFrames);
     uint64_t* s_delta = reinterpret_cast<uint64_t*>(s_raw + 8 * kWinFrames);
     uint32_t* s_key = reinterpret_cast<uint32_t*>(s_raw + 16 * kWinFrames);
+    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_raw + 20 * kWinFrames);
     unmask_v3_body<16>(in, frames, tile_first, sum, out, big_grid, WinLds{s_start, s_lend, s_delta, s_key}, runs,
-                       &s_run);
+                       s_run);
     return;
   }
   uint8_t* w = s_raw + (threadIdx.x >> 6) * kFusedLdsPerWave;
-  const FusedLds L{reinterpret_cast<FusedTab*>(w), reinterpret_cast<uint32_t*>(w + kFusedRound * sizeof(FusedTab)),
-                   reinterpret_cast<uint16_t*>(w + kFusedRound * (sizeof(FusedTab) + 4))};
-  fused_body(in, out, sum, A, L);
+  const FusedLds L{reinterpret_cast<FusedTab*>(w), reinterpret_cast<uint16_t*>(w + kFusedRound * sizeof(FusedTab))};
+  fused_body<S>(in, out, sum, A, L);
 }
 
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
@@ -1096,6 +1130,7 @@ const UnmaskVariant kUnmaskVariants[] = {
      "round 4's default: v3 for equal-size batches, v5 (pipelined 8-tile windows with a chunk -> frame map, records "
      "read back) for mixed ones", true, true, 0},
     {k_unmask_fused<true>, 16, "the fused record + unmask path for every batch", true, true, 2},
+    {k_unmask_fused<false, 8>, 16, "the default with 8 KiB fused steps (measurement)", true, true, 1},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
