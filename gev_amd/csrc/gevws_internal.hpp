@@ -44,6 +44,7 @@ struct gevws_ctx {
   // the next decode_gen; the queue sits at the start of the scratch and is
   // zeroed whenever the scratch is new or the queue grows
   uint64_t fused_big_bytes = 32 * 1024;
+  bool fused_ok = false;  // this decode's rows suit the fused path (decode_front; unmask variant 0)
   uint64_t decode_gen = 0;
   void* pieces_zeroed_at = nullptr;
   size_t pieces_zeroed_bytes = 0;

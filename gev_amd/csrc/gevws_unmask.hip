@@ -611,8 +611,8 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
 // written after its other words are complete (s_waitcnt), a wave's rows
 // counted done after every piece it queued is complete.
 constexpr uint32_t kFusedRound = 256;                 // frames per round (4 entries a lane)
-constexpr uint32_t kFusedStepMax = 16;                // chunks per lane per unmask step, at most
-constexpr uint32_t kFusedStepChunks = 64 * kFusedStepMax;
+constexpr uint32_t kFusedStep = 8;                    // chunks per lane per unmask step
+constexpr uint32_t kFusedStepChunks = 2 * 64 * kFusedStep;  // the wave's chunk map, double-buffered
 constexpr uint64_t kPieceBytes = 64 * 1024;           // a deferred frame's piece
 constexpr uint32_t kFusedMaxSpins = 1u << 21;         // a wave waiting for a piece gives up after this many sleeps (~3 s)
 
@@ -625,7 +625,7 @@ struct FusedTab {  // one slot of a round (32 bytes)
 };
 struct FusedLds {
   FusedTab* tab;   // [kFusedRound] per wave (the round's frames; lane 0's re-walk entries before that)
-  uint16_t* own;   // [64 S] chunk -> slot + 1
+  uint16_t* own;   // [2][64 S] chunk -> slot + 1 (two halves: this step's, the next one's)
 };
 
 __device__ __forceinline__ uint64_t agent_ld64(const uint64_t* p) {
@@ -669,94 +669,84 @@ __device__ __forceinline__ void fused_piece(const uint8_t* __restrict__ in, uint
 
 // The round's payload range [R0, R1): slot s = u * 64 + lane of the wave's
 // LDS table holds a frame's payload offset (start) and padded length (pd; 0:
-// no payload / no frame); a lane reads its four slots' at every step (held in
-// registers across the round they pushed the S = 16 loads into scratch).
-// S chunks per lane per step (S KiB per wave): at S = 16 the loaded vectors
-// take 64 VGPRs, so a chunk keeps only its slot (a byte of 4 packed words)
-// across the loads and re-reads its key and payload end from LDS to store.
+// no payload / no frame).  Steps of S KiB (S chunks a lane, 64-lane
+// coalesced 1 KiB spans), software-pipelined: the NEXT step is decided --
+// skip a deferred frame, stream inside one frame, or a chunk -> slot map
+// built in the other half of the wave's double-buffered map -- while this
+// step's loads are in flight (without the overlap the map's chain of LDS round
+// trips sat between every step's loads: C4 7.69 ms).  A chunk keeps only its
+// slot (a byte of packed words) across the loads and re-reads its key and
+// payload end from LDS to store.
+struct FusedStep {
+  uint64_t p;       // step start (payload arena offset)
+  int kind;         // 0 done, 2 stream inside slot s, 3 mapped
+  uint32_t s;       // the slot covering p
+};
+
 template <int S>
 __device__ __forceinline__ void fused_unmask_range(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                    const FusedLds& L, uint64_t R0, uint64_t R1, uint64_t big_bytes) {
-  static_assert(S == 8 || S == 16, "8 or 16 chunks a lane");
+  static_assert(S == 8, "8 chunks a lane (the map's two halves: 2 x 512 slots)");
   constexpr uint64_t SB = 1024ull * S;  // bytes per step
-  constexpr int MQ = S / 8;             // u32x4 words of the map per lane
+  constexpr uint32_t NC = 64 * S;       // chunks per step
   const uint32_t lane = threadIdx.x & 63;
-  uint64_t p = R0;
-  while (p < R1) {  // wave-uniform
-    uint64_t po[4];
-    uint32_t pd[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const u32x4 w = *reinterpret_cast<const u32x4*>(&L.tab[u * 64 + lane].start);  // start, key, pd
-      po[u] = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-      pd[u] = w[3];
-    }
-    // the frame covering p: the last slot with a payload starting at or before it
-    int s = -1;
-#pragma unroll
-    for (int u = 3; u >= 0; --u) {
-      const uint64_t m = __ballot(pd[u] > 0 && po[u] <= p);
-      if (s < 0 && m) s = u * 64 + 63 - __builtin_clzll(m);
-    }
-    if (s < 0) return;  // (cannot happen: the round's first payload starts at R0)
-    uint64_t spo = 0, spd = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (u == (s >> 6)) {
-        spo = uniform64(__shfl(po[u], s & 63, 64));
-        spd = uniform32((uint32_t)__shfl((int)pd[u], s & 63, 64));
-      }
-    if (spd >= big_bytes) {  // a deferred frame (pieces queued): on to the next payload after p
-      uint64_t nxt = R1;
+  // The step at p (skipping deferred frames) and, for a mapped step, its map in half b.
+  auto plan = [&](uint64_t p, uint32_t b) -> FusedStep {
+    for (;;) {  // wave-uniform
+      if (p >= R1) return FusedStep{p, 0, 0};
+      uint64_t po[4];
+      uint32_t pd[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const uint64_t m = __ballot(pd[u] > 0 && po[u] > p);
-        if (nxt == R1 && m) nxt = uniform64(__shfl(po[u], __builtin_ctzll(m), 64));
+        const u32x4 w = *reinterpret_cast<const u32x4*>(&L.tab[u * 64 + lane].start);  // start, key, pd
+        po[u] = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        pd[u] = w[3];
       }
-      p = nxt;
-      continue;
-    }
-    if (spo + spd >= p + SB) {  // the whole step inside frame s: stream it
-      const FusedTab te = L.tab[s];
-      const uint32_t key = te.key;
-      u32x4 v[S];
+      // the frame covering p: the last slot with a payload starting at or before it
+      int s = -1;
 #pragma unroll
-      for (int u = 0; u < S; ++u)
-        v[u] = ld16u_stream<true>(in + (p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16 + te.delta));
-#pragma unroll
-      for (int u = 0; u < S; ++u) {
-        const uint64_t q = p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16;
-        u32x4 x = v[u] ^ key;
-        const int64_t rem = (int64_t)(te.end - q);
-        if (rem < 16) x = keep_bytes(x, rem);
-        st16_nt(out + q, x);
+      for (int u = 3; u >= 0; --u) {
+        const uint64_t m = __ballot(pd[u] > 0 && po[u] <= p);
+        if (s < 0 && m) s = u * 64 + 63 - __builtin_clzll(m);
       }
-      p += SB;
-      continue;
-    }
-    // chunk -> slot map of the step: marks of the frames starting inside it,
-    // then a wave prefix max seeded with slot s
+      if (s < 0) return FusedStep{R1, 0, 0};  // (cannot happen: the round's first payload starts at R0)
+      uint64_t spo = 0, spd = 0;
 #pragma unroll
-    for (int k = 0; k < MQ; ++k) reinterpret_cast<u32x4*>(L.own)[lane * MQ + k] = u32x4{0, 0, 0, 0};
-    lds_fence();
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (pd[u] > 0 && po[u] > p && po[u] < p + SB) L.own[(po[u] - p) >> 4] = (uint16_t)(u * 64 + lane + 1);
-    lds_fence();
-    {
-      uint32_t run[8 * MQ];
-#pragma unroll
-      for (int k = 0; k < MQ; ++k) {
-        const u32x4 m = reinterpret_cast<const u32x4*>(L.own)[lane * MQ + k];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          run[8 * k + 2 * j] = m[j] & 0xffffu;
-          run[8 * k + 2 * j + 1] = m[j] >> 16;
+      for (int u = 0; u < 4; ++u)
+        if (u == (s >> 6)) {
+          spo = uniform64(__shfl(po[u], s & 63, 64));
+          spd = uniform32((uint32_t)__shfl((int)pd[u], s & 63, 64));
         }
+      if (spd >= big_bytes) {  // a deferred frame (pieces queued): on to the next payload after p
+        uint64_t nxt = R1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint64_t m = __ballot(pd[u] > 0 && po[u] > p);
+          if (nxt == R1 && m) nxt = uniform64(__shfl(po[u], __builtin_ctzll(m), 64));
+        }
+        p = nxt;
+        continue;
+      }
+      if (spo + spd >= p + SB) return FusedStep{p, 2, (uint32_t)s};  // the whole step inside frame s
+      // chunk -> slot map: marks of the frames starting inside the step, then
+      // a wave prefix max seeded with slot s
+      uint16_t* own = L.own + b * NC;
+      reinterpret_cast<u32x4*>(own)[lane] = u32x4{0, 0, 0, 0};
+      lds_fence();
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (pd[u] > 0 && po[u] > p && po[u] < p + SB) own[(po[u] - p) >> 4] = (uint16_t)(u * 64 + lane + 1);
+      lds_fence();
+      u32x4 m = reinterpret_cast<const u32x4*>(own)[lane];
+      uint32_t run[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        run[2 * j] = m[j] & 0xffffu;
+        run[2 * j + 1] = m[j] >> 16;
       }
 #pragma unroll
-      for (int k = 1; k < 8 * MQ; ++k) run[k] = run[k] > run[k - 1] ? run[k] : run[k - 1];
-      uint32_t inc = run[8 * MQ - 1];
+      for (int k = 1; k < 8; ++k) run[k] = run[k] > run[k - 1] ? run[k] : run[k - 1];
+      uint32_t inc = run[7];
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
@@ -767,52 +757,81 @@ __device__ __forceinline__ void fused_unmask_range(const uint8_t* __restrict__ i
       const uint32_t seed = (uint32_t)s + 1;
       exc = exc > seed ? exc : seed;
 #pragma unroll
-      for (int k = 0; k < MQ; ++k) {
-        u32x4 m;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t lo16 = run[8 * k + 2 * j] > exc ? run[8 * k + 2 * j] : exc;
-          const uint32_t hi16 = run[8 * k + 2 * j + 1] > exc ? run[8 * k + 2 * j + 1] : exc;
-          m[j] = lo16 | (hi16 << 16);
-        }
-        reinterpret_cast<u32x4*>(L.own)[lane * MQ + k] = m;
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo16 = run[2 * j] > exc ? run[2 * j] : exc;
+        const uint32_t hi16 = run[2 * j + 1] > exc ? run[2 * j + 1] : exc;
+        m[j] = lo16 | (hi16 << 16);
       }
+      reinterpret_cast<u32x4*>(own)[lane] = m;
+      lds_fence();
+      return FusedStep{p, 3, (uint32_t)s};
     }
-    lds_fence();
+  };
+  uint32_t b = 0;
+  FusedStep cur = plan(R0, b);
+  while (cur.kind != 0) {  // wave-uniform
     u32x4 v[S];
-    uint32_t sl4[S / 4];  // each chunk's slot, a byte each
+    uint32_t sl4[S / 4];  // each chunk's slot, a byte each (mapped steps)
     uint32_t live = 0;    // chunks with payload bytes
+    uint64_t sdelta = 0, send = 0;
+    uint32_t skey = 0;
+    if (cur.kind == 2) {
+      const FusedTab& te = L.tab[cur.s];
+      sdelta = uniform64(te.delta);
+      send = uniform64(te.end);
+      skey = uniform32(te.key);
 #pragma unroll
-    for (int k = 0; k < S / 4; ++k) sl4[k] = 0;
+      for (int u = 0; u < S; ++u)
+        v[u] = ld16u_stream<true>(in + (cur.p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16 + sdelta));
+    } else {
+      const uint16_t* own = L.own + b * NC;
 #pragma unroll
-    for (int u = 0; u < S; ++u) {
-      const uint32_t c = (uint32_t)u * 64 + (fresh_tid() & 63);
-      const uint64_t q = p + 16ull * c;
-      v[u] = u32x4{0, 0, 0, 0};
-      if (q < R1) {
-        const uint32_t sl = (uint32_t)L.own[c] - 1u;
-        const u64x2 te = *reinterpret_cast<const u64x2*>(&L.tab[sl]);  // delta, end
-        sl4[u >> 2] |= sl << (8 * (u & 3));
-        if ((int64_t)(te[1] - q) > 0) {
-          live |= 1u << u;
-          v[u] = ld16u_stream<true>(in + (q + te[0]));
+      for (int k = 0; k < S / 4; ++k) sl4[k] = 0;
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        const uint32_t c = (uint32_t)u * 64 + (fresh_tid() & 63);
+        const uint64_t q = cur.p + 16ull * c;
+        v[u] = u32x4{0, 0, 0, 0};
+        if (q < R1) {
+          const uint32_t sl = (uint32_t)own[c] - 1u;
+          const u64x2 te = *reinterpret_cast<const u64x2*>(&L.tab[sl]);  // delta, end
+          sl4[u >> 2] |= sl << (8 * (u & 3));
+          if ((int64_t)(te[1] - q) > 0) {
+            live |= 1u << u;
+            v[u] = ld16u_stream<true>(in + (q + te[0]));
+          }
         }
       }
     }
+    // the next step, while this one's loads are in flight
+    __asm__ volatile("" ::: "memory");
+    const FusedStep nxt = plan(cur.p + SB, b ^ 1);
+    if (cur.kind == 2) {
 #pragma unroll
-    for (int u = 0; u < S; ++u) {
-      if (live & (1u << u)) {
-        const uint32_t sl = (sl4[u >> 2] >> (8 * (u & 3))) & 0xffu;
-        const uint64_t q = p + 16ull * ((uint32_t)u * 64 + (fresh_tid() & 63));
-        const int64_t rem = (int64_t)(L.tab[sl].end - q);
-        u32x4 x = v[u] ^ L.tab[sl].key;
+      for (int u = 0; u < S; ++u) {
+        const uint64_t q = cur.p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16;
+        u32x4 x = v[u] ^ skey;
+        const int64_t rem = (int64_t)(send - q);
         if (rem < 16) x = keep_bytes(x, rem);
         st16_nt(out + q, x);
       }
+    } else {
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        if (live & (1u << u)) {
+          const uint32_t sl = (sl4[u >> 2] >> (8 * (u & 3))) & 0xffu;
+          const uint64_t q = cur.p + 16ull * ((uint32_t)u * 64 + (fresh_tid() & 63));
+          const int64_t rem = (int64_t)(L.tab[sl].end - q);
+          u32x4 x = v[u] ^ L.tab[sl].key;
+          if (rem < 16) x = keep_bytes(x, rem);
+          st16_nt(out + q, x);
+        }
+      }
     }
-    lds_fence();  // (the next step's map clear after this step's reads)
-    p += SB;
+    cur = nxt;
+    b ^= 1;
   }
+  lds_fence();  // (the next round's table writes after this round's reads)
 }
 
 // One row: records + inline unmask of its frames below A.big_bytes, pieces of
@@ -1057,7 +1076,7 @@ constexpr uint32_t kV3LdsBytes = kWinFrames * (4 + 4 + 8 + 4) + 16;
 constexpr uint32_t kFusedLdsBytes = (kUnmaskBlock / 64) * kFusedLdsPerWave > kV3LdsBytes
                                         ? (kUnmaskBlock / 64) * kFusedLdsPerWave : kV3LdsBytes;
 static_assert(4 * kFusedLdsBytes <= 160 * 1024, "four workgroups a CU");
-template <bool ALL, int S = 16>
+template <bool ALL, int S = kFusedStep>
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_fused(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
     const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs,
@@ -1123,14 +1142,14 @@ struct UnmaskVariant {
 const UnmaskVariant kUnmaskVariants[] = {
     {k_unmask_fused<false>, 16,
      "auto: v3 4-tile windows for batches of equal-size frames; for mixed sizes the fused record + unmask path "
-     "(records and payloads straight from the walk's entries, one wave per row, big frames in queued pieces)",
+     "(records and payloads straight from the walk's entries, one wave per row, big frames in queued pieces) when "
+     "the batch has >= 16 rows a wave of 64 KiB - 1 MiB, else round 4's record pass + v5",
      true, true, 1},
     {k_unmask_v5, 16, "v5 for every batch (the round-4 mixed-batch path alone)", true, true, 0},
     {k_unmask_auto5, 16,
      "round 4's default: v3 for equal-size batches, v5 (pipelined 8-tile windows with a chunk -> frame map, records "
      "read back) for mixed ones", true, true, 0},
     {k_unmask_fused<true>, 16, "the fused record + unmask path for every batch", true, true, 2},
-    {k_unmask_fused<false, 8>, 16, "the default with 8 KiB fused steps (measurement)", true, true, 1},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
@@ -1141,12 +1160,18 @@ namespace gevws_impl {
 int unmask_variant_count() { return kNumUnmaskVariants; }
 const char* unmask_variant_name(int i) { return i >= 0 && i < kNumUnmaskVariants ? kUnmaskVariants[i].name : nullptr; }
 
-int unmask_emit_gate(const gevws_ctx* ctx) { return kUnmaskVariants[ctx->unmask_variant].emit_gate; }
+// Variant 0 takes the fused path only for batches decode_front found suited
+// (ctx->fused_ok); the others run round 4's record pass + v3 / v5 (variant 2).
+static const UnmaskVariant& unmask_variant_of(const gevws_ctx* ctx) {
+  return (ctx->unmask_variant == 0 && !ctx->fused_ok) ? kUnmaskVariants[2] : kUnmaskVariants[ctx->unmask_variant];
+}
+
+int unmask_emit_gate(const gevws_ctx* ctx) { return unmask_variant_of(ctx).emit_gate; }
 
 int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const uint8_t* d_in,
                   const gevws_frame* d_frames, const uint32_t* tile_first, const gevws_summary* d_summary,
                   uint8_t* d_payload, const FusedArgs& fa) {
-  const UnmaskVariant& v = kUnmaskVariants[ctx->unmask_variant];
+  const UnmaskVariant& v = unmask_variant_of(ctx);
   const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
   const uint32_t ucus = (uint32_t)ctx->num_cus;
   const uint64_t norm = 4 * (uint64_t)ucus;

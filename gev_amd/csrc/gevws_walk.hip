@@ -900,6 +900,10 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
 // connection.
 
 constexpr int kEmitGroup = 16;
+// decode_front's rule for the fused record + unmask path (unmask variant 0)
+constexpr uint64_t kFusedMinRowsPerCU = 256;         // 16 rows a wave at 16 waves a CU
+constexpr uint64_t kFusedMinRowBytes = 64 * 1024;
+constexpr uint64_t kFusedMaxRowBytes = 1024 * 1024;
 constexpr uint64_t kEmitSplitPerCU = 32;  // record-pass workgroups per CU over k_walk_split's rows
 // (Measured and not kept: phase 2 software-pipelined, the next batch's entry
 // loads issued before this batch's rounds -- C4 0.448 -> 0.477 ms, 8-way share
@@ -1370,6 +1374,17 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   fa->n_entries = wv == 2 ? 0 : n_entries;
   fa->n_rows = (uint32_t)n_v;
   fa->gshift = gshift;
+  // the fused record + unmask path pays where every wave gets many rows of
+  // moderate size: a wave writes a row's records and unmasks its payloads
+  // alone, so a few big rows (C5: 256 rows of 4 MiB) or few rows per wave
+  // (C4's 2-way share, 8 a wave) leave waves idle at the end, and tiny rows
+  // (the 8-way share's split segments, 18 KB) pay the per-row latencies
+  // (profiles/r05/r05_fused_ab.jsonl); those batches keep the record pass + v5
+  {
+    const uint64_t per_row = n_v ? in_bytes / n_v : 0;
+    ctx->fused_ok = n_v >= kFusedMinRowsPerCU * (uint64_t)ncu && per_row >= kFusedMinRowBytes &&
+                    per_row <= kFusedMaxRowBytes;
+  }
   {  // rows per grab: ~16 grabs a wave (4 waves a workgroup, 4 workgroups a CU), at most 64 rows
     const uint64_t per = n_v / (16ull * 16 * ncu);
     fa->unit_rows = (uint32_t)(per < 1 ? 1 : (per > 64 ? 64 : per));
