@@ -317,8 +317,6 @@ def main():
                          "against the copy rate in the same clock state (0 = skip)")
     ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
     ap.add_argument("--unmask-variant", type=int, default=None, help="A/B: unmask kernel variant")
-    ap.add_argument("--fused-big-bytes", type=int, default=None,
-                    help="A/B: the fused record + unmask path's deferred-frame threshold (GEVWS_TUNE_FUSED_BIG_BYTES)")
     ap.add_argument("--split-lanes", type=int, default=None,
                     help="A/B: split header walk lanes per connection (GEVWS_TUNE_SPLIT_LANES; 0 = auto, 1 = off)")
     ap.add_argument("--emulate-shard", default=None, metavar="R/N",
@@ -365,8 +363,6 @@ def main():
             e.set_tuning(_abi.TUNE_UNMASK_VARIANT, args.unmask_variant)
         if args.split_lanes is not None:
             e.set_tuning(_abi.TUNE_SPLIT_LANES, args.split_lanes)
-        if args.fused_big_bytes is not None:
-            e.set_tuning(_abi.TUNE_FUSED_BIG_BYTES, args.fused_big_bytes)
     t_setup = time.time()
     scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
     emulated = None
@@ -535,7 +531,7 @@ def main():
     # (the committed counts describe the default kernels on the full batch)
     traffic, traffic_src = (load_traffic(args.config)
                             if (scaling == "weak" or world == 1) and not emulated and not args.unmask_variant
-                            and not args.walk_variant and args.fused_big_bytes is None else (None, None))
+                            and not args.walk_variant else (None, None))
     result = {
         "metric": METRIC,
         "value": round(value, 3),

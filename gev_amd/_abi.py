@@ -41,7 +41,7 @@ AUX_SLOT = 128
 HANDLER_NONE = 0
 HANDLER_ECHO_BINARY = 1
 HANDLER_ECHO_TEXT = 2
-TUNE_UNMASK_VARIANT = 1  # 0 = auto (v3 / fused record + unmask per batch), 1 = v5 always, 2 = v3 / v5, 3 = fused always
+TUNE_UNMASK_VARIANT = 1  # 0 = auto (v3 / v5 per batch), 1 = v5 for every batch, 2 = auto with contiguous v5 runs
 TUNE_UNMASK_GRID = 2
 TUNE_ENCODE_VARIANT = 3  # 0 = auto, 1 / 2 = one / two tiles a wave step, 3 / 4 / 5 = two tiles, run mode 0 / 1 / 2
 TUNE_WALK_VARIANT = 4  # 0 = default, 1 = plain chain walk, 2 = no entry table, 3 = writer wave always
@@ -50,7 +50,6 @@ TUNE_SPLIT_LANES = 8  # split header walk: lanes per connection (0 = auto, 1 = n
 TUNE_RETIRED = (5, 6, 9, 10, 11, 12)  # round 1-3 measurement knobs, rejected
 TUNE_SPLIT_MIN_BYTES = 13  # split walk: bytes per segment at least (default 16 384)
 TUNE_SPLIT_LANES_PER_CU = 14  # split walk auto: lanes per CU at most (default 512)
-TUNE_FUSED_BIG_BYTES = 15  # fused path: frames of >= this many padded bytes go as queued 64 KiB pieces
 
 IN_PAD = 64
 MEM_DEFAULT, MEM_FINE, MEM_UNCACHED = 0, 1, 2  # gevws_device_alloc kinds

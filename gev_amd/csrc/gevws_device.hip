@@ -230,10 +230,6 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       if (value < 1024 || value > (1ll << 30)) return GEVWS_ERR_INVALID;
       ctx->split_min_bytes = (uint64_t)value;
       return GEVWS_OK;
-    case GEVWS_TUNE_FUSED_BIG_BYTES:
-      if (value < 4096 || value > (1ll << 40)) return GEVWS_ERR_INVALID;
-      ctx->fused_big_bytes = (uint64_t)value;
-      return GEVWS_OK;
     case GEVWS_TUNE_SPLIT_LANES_PER_CU:
       if (value < 64 || value > 4096) return GEVWS_ERR_INVALID;
       ctx->split_lanes_per_cu = (uint64_t)value;
@@ -320,12 +316,11 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   }
   // walk, scan, bases, record pass (gevws_walk.hip)
   uint32_t* tile_first = nullptr;
-  FusedArgs fa;
   int r = decode_front(ctx, st, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, payload_cap, d_conn_out,
-                       d_summary, ev, &tile_first, &fa);
+                       d_summary, ev, &tile_first);
   if (r != GEVWS_OK) return r;
   if (ev) GEVWS_HIP(hipEventRecord(ev[3], st));
-  r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload, fa);
+  r = launch_unmask(ctx, st, payload_cap, d_in, d_frames, tile_first, d_summary, d_payload);
   if (r != GEVWS_OK) return r;
   if (ev) GEVWS_HIP(hipEventRecord(ev[4], st));
   GEVWS_HIP(hipGetLastError());

@@ -38,16 +38,7 @@ struct gevws_ctx {
   uint64_t stats_conns = 0, prev_frames_per_conn = 0, prev_frame_bytes = 0;
   bool prev_mixed = false;
   uint32_t last_unmask_grid = 0;  // workgroups of the last decode's unmask launch
-  uint32_t* unmask_runs = nullptr;  // the decode's work counters (kWorkCounters, decode scratch)
-  // the fused record + unmask path: frames of at least fused_big_bytes padded
-  // bytes are unmasked as queued pieces; each decode stamps its pieces with
-  // the next decode_gen; the queue sits at the start of the scratch and is
-  // zeroed whenever the scratch is new or the queue grows
-  uint64_t fused_big_bytes = 32 * 1024;
-  bool fused_ok = false;  // this decode's rows suit the fused path (decode_front; unmask variant 0)
-  uint64_t decode_gen = 0;
-  void* pieces_zeroed_at = nullptr;
-  size_t pieces_zeroed_bytes = 0;
+  uint32_t* unmask_runs = nullptr;  // the unmask v5 path's per-XCD run counters (decode scratch)
   uint32_t last_ks = 1;    // lanes per connection of the last multi-kernel decode's walk
   uint32_t split_lanes = 0;  // lanes per connection (k_walk_split); 0 = auto, 1 = off
   uint64_t split_min_bytes = kSplitMinBytes;        // split walk: bytes per segment at least
@@ -129,24 +120,19 @@ int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
                  const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
                  uint8_t* d_payload, uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary);
 // header walk, scan, bases and record pass into the context's scratch; the
-// output-tile -> frame map for the unmask in *tile_first, and in *fa what the
-// fused record + unmask path reads (the record pass leaves a batch to it per
-// unmask_emit_gate).  ev: the timing events 0..2 (walk start, walk end, scan
-// end) or null.
+// output-tile -> frame map for the unmask in *tile_first.  ev: the timing
+// events 0..2 (walk start, walk end, scan end) or null.
 int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
                  const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
                  uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary, hipEvent_t* ev,
-                 uint32_t** tile_first, FusedArgs* fa);
+                 uint32_t** tile_first);
 int walk_variant_count();
 const char* walk_variant_name(int i);
 
 // ---- gevws_unmask.hip
 int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const uint8_t* d_in,
                   const gevws_frame* d_frames, const uint32_t* tile_first, const gevws_summary* d_summary,
-                  uint8_t* d_payload, const FusedArgs& fa);
-// k_walk_emit's gate for the context's unmask variant: 0 = records for every
-// batch, 1 = not for mixed batches (the fused path writes them), 2 = never
-int unmask_emit_gate(const gevws_ctx* ctx);
+                  uint8_t* d_payload);
 int unmask_variant_count();
 const char* unmask_variant_name(int i);
 

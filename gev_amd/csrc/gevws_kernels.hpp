@@ -309,12 +309,6 @@ constexpr uint64_t kWideGridTiles = 2ull << 20;
 // -> 1.86; runs of 32 / 64 tiles in between; profiles/r04/r04_unmask_counter_ab.jsonl).
 // One counter per XCD: one for the whole grid saturates (k_encode6 measured it).
 constexpr uint32_t kUnmaskRunCounters = 8;
-// The decode scratch's work counters, 64 bytes apart, zeroed by k_walk_bases
-// for every decode: slots 0-7 the per-XCD runs above (or the fused record +
-// unmask path's per-XCD row counters), 8 rows finished, 9 pieces queued,
-// 16-23 the per-XCD piece cursors (the fused path, gevws_unmask.hip).
-constexpr uint32_t kWorkCounters = 24;
-constexpr uint32_t kCtrRowsDone = 8, kCtrPieces = 9, kCtrCursor = 16;
 constexpr uint64_t kUnmaskRun = 16;
 constexpr uint64_t kUnmaskRunMinTiles = 64;  // the v3 path's counter runs: tiles a workgroup at least
 
@@ -379,120 +373,4 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t m) {
   return o;
 }
 
-// ------------------------------------------------------------------ walk entries
-// (gevws_walk.hip's counting walk writes them; its record pass and the
-// unmask's fused record + unmask path, gevws_unmask.hip, read them)
-// slot runs start on 32-entry (256-byte) boundaries: the writer wave of the
-// LDS-ring walk stores whole 256-byte groups (k_walk_count ST 2)
-constexpr uint32_t kSlotShift = 5;
-constexpr uint64_t kSlotAlign = 1ull << kSlotShift;
-// 8-byte entry: the key, and b0 | masked << 8 | length form << 9 | payload
-// length << 11.  The header's position is not stored: a row's frames are
-// contiguous from its start, so the record pass recomputes each position as
-// the prefix sum of the frame sizes before it (hlen + L).  A payload length
-// >= kLenEsc is stored as kLenEsc and re-read from the header by the record
-// pass, where the prefix sum gives its position (rare: frames of 2 MiB and
-// more, whose unmask dwarfs one header load).  Round 2's 16-byte entry
-// (position, key, length, meta) cost the walk 0.71 GB of C4's writes and the
-// record pass as many reads (profiles/r03/r03_pmc_split.json).
-constexpr uint32_t kLenEsc = (1u << 21) - 1;
-struct WalkEntry {
-  uint32_t mask;
-  uint32_t w;
-};
-static_assert(sizeof(WalkEntry) == 8, "one dwordx2 per entry");
-// meta: b0 | masked << 8 | hlen << 16 (walk_parse / walk_chain)
-__device__ __forceinline__ WalkEntry make_entry(uint32_t key, uint64_t L, uint32_t meta) {
-  const uint32_t hlen = meta >> 16, masked = (meta >> 8) & 1u;
-  const uint32_t ext = hlen - 2 - 4 * masked;  // 0, 2 or 8 length bytes
-  const uint32_t form = ext == 0 ? 0u : (ext == 2 ? 1u : 2u);
-  const uint32_t l21 = L < kLenEsc ? (uint32_t)L : kLenEsc;
-  return WalkEntry{key, (meta & 0x1ffu) | (form << 9) | (l21 << 11)};
-}
-__device__ __forceinline__ uint32_t entry_hlen(const WalkEntry& e) {
-  const uint32_t form = (e.w >> 9) & 3u;
-  return 2 + (form == 2 ? 8u : 2u * form) + 4 * ((e.w >> 8) & 1u);
-}
-__device__ __forceinline__ uint32_t entry_len21(const WalkEntry& e) { return e.w >> 11; }
-
-__device__ __forceinline__ bool entry_slots_of(const gevws_conn_in& ci, uint32_t c, uint64_t n_entries,
-                                              uint32_t gshift, uint64_t& base, uint64_t& cap) {
-  if (n_entries == 0 || ci.len >= (1ull << 32)) return false;
-  base = kSlotAlign * ((ci.off >> (gshift + kSlotShift)) + (uint64_t)c);
-  cap = kSlotAlign * ((ci.len >> (gshift + kSlotShift)) + 1);
-  return base + cap <= n_entries;
-}
-
-// Segmented inclusive wave scan: a segment starts at every lane with head set
-// (and at lane 0).  Every lane must take part.
-__device__ __forceinline__ uint64_t wave_seg_scan(uint64_t v, bool head) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t vu = __shfl_up(v, d, 64);
-    const bool hu = __shfl_up((int)head, d, 64) != 0;
-    if (lane >= d && !head) {
-      v += vu;
-      head = hu;
-    }
-  }
-  return v;
-}
-
-// One round of entries (lane = frame): each frame's payload length L and the
-// segmented inclusive prefix `ip` of the frame sizes (hlen + L), so a frame
-// starts at (its row's position carry) + ip - (hlen + L).  Escaped lengths
-// (>= kLenEsc) are re-read from the header, lowest lane first: every frame
-// before it in its row is then resolved, so its position is exact.  `head`:
-// the lane starts a row in this round; pbase / coff: the position carry and
-// input offset of the lane's row (every lane must take part: shuffles).
-__device__ __forceinline__ void entry_round(const uint8_t* __restrict__ in, const WalkEntry& q, bool valid, bool head,
-                                            uint64_t pbase, uint64_t coff, uint64_t& L, uint64_t& ip) {
-  L = valid ? entry_len21(q) : 0;
-  bool esc = valid && L == kLenEsc;
-  uint64_t fsz = (valid && !esc) ? entry_hlen(q) + L : 0;
-  ip = wave_seg_scan(fsz, head);
-  for (;;) {
-    const uint64_t m = __ballot(esc);
-    if (m == 0) break;  // wave-uniform
-    if ((threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) {
-      uint64_t lo, hi;
-      load_window(in + coff + pbase + ip, lo, hi);  // (fsz == 0: ip is the frame's start)
-      DevHdr h;
-      parse_header(lo, hi, ~0ull, h);  // parsed by the walk: complete
-      L = h.length;
-      fsz = h.hlen + L;
-      esc = false;
-    }
-    ip = wave_seg_scan(fsz, head);
-  }
-}
-
-
 }  // namespace
-
-// (outside the anonymous namespace: it crosses from gevws_walk.hip's decode_front
-// to gevws_unmask.hip's launcher)
-// What the fused record + unmask path (gevws_unmask.hip) reads besides the
-// input and writes besides the payload: the record pass's rows (the
-// connection table, or k_walk_split's segments with their parent
-// connections' bases), the walk's entries, the frame records it writes, and
-// the scratch it schedules with.
-struct FusedArgs {
-  gevws_frame* frames;               // the records (written here)
-  gevws_summary* sum;                // status := GEVWS_ERR_DEVICE if a wave gave up waiting (never expected)
-  const gevws_conn_in* rows;
-  const gevws_conn_out* rout;        // per row: nframes, first_frame / payload_base (relative with ks)
-  const gevws_conn_out* pout;        // the parent connections (ks > 1) or null
-  const uint8_t* rec_flags;          // per row: entries recorded
-  const void* entries;               // WalkEntry[n_entries]
-  uint64_t n_entries;
-  uint32_t n_rows, ks, gshift, unit_rows;
-  uint32_t* ctr;                     // kWorkCounters slots, 64 bytes apart
-  uint64_t* pieces;                  // the deferred big frames' pieces, 4 x u64 each
-  uint64_t piece_cap;
-  uint64_t big_bytes;                // frames of at least this many padded bytes are deferred
-  uint64_t gen;                      // this decode's stamp on its pieces (queue entries of older decodes differ)
-};
-
-

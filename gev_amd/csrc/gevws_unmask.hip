@@ -578,461 +578,15 @@ __device__ __forceinline__ void unmask_v5_body(const uint8_t* __restrict__ in, c
   }
 }
 
-// ------------------------------------------------------------------ fused record + unmask (mixed batches)
-// The record pass (k_walk_emit) and the unmask (v5) of a batch of mixed frame
-// sizes in ONE kernel, driven by the walk's 8-byte entries instead of the
-// 32-byte records and the tile map: the v5 path read back every record the
-// record pass had just written (C4: 1.40 GB of a 47.95 GB step) and the
-// record pass ran as its own launch (0.48 ms).  Every wave works alone (no
-// workgroup barrier), on whole rows (connections, or k_walk_split's segments):
-//  * rows come in units of A.unit_rows from per-XCD counters (blockIdx mod 8,
-//    the dispatch's round robin), then from the other XCDs' counters;
-//  * a row's frames go in rounds of 256 (4 entries a lane): the entries'
-//    segmented wave scans give each header's position and payload offset
-//    (entry_round, as k_walk_emit), the lane writes its frame's 32-byte record
-//    (= the (ctx, out) of protocol.go:57-58) and its LDS table slot (source -
-//    destination delta, payload end, key);
-//  * the round's payloads are contiguous in the arena: the wave unmasks them
-//    in steps of 8 KiB (8 chunks a lane, 64-lane coalesced 1 KiB spans) --
-//    a step inside one frame streams; otherwise every frame starting in the
-//    step marks its first chunk in the wave's LDS map and one wave prefix max
-//    gives every chunk its frame (ws.Cipher, cipher.go:14-53, phase 0 per
-//    frame, protocol.go:54; pad bytes zero as Go's make);
-//  * frames of at least A.big_bytes padded bytes are not unmasked inline: the
-//    lane queues them as pieces of kPieceBytes (source, destination, length,
-//    key, stamp) and every wave, once no rows are left, takes pieces until
-//    all rows are done and the queue is empty -- so the tail of the row phase
-//    is filled with pieces, and no wave holds a 1 MiB frame alone at the end.
-// Rows without entries (an unordered connection table, a stream >= 4 GiB,
-// more frames than entry slots) are walked header by header by lane 0,
-// 256 frames a round, into the same LDS entries (slow, rare).
-// Queue entries and counters cross XCDs (whose L2s are not coherent): they are
-// written and read as agent-scope atomics (L2-bypassing), a piece's stamp
-// written after its other words are complete (s_waitcnt), a wave's rows
-// counted done after every piece it queued is complete.
-constexpr uint32_t kFusedRound = 256;                 // frames per round (4 entries a lane)
-constexpr uint32_t kFusedStep = 8;                    // chunks per lane per unmask step
-constexpr uint32_t kFusedStepChunks = 2 * 64 * kFusedStep;  // the wave's chunk map, double-buffered
-constexpr uint64_t kPieceBytes = 64 * 1024;           // a deferred frame's piece
-constexpr uint32_t kFusedMaxSpins = 1u << 21;         // a wave waiting for a piece gives up after this many sleeps (~3 s)
-
-struct FusedTab {  // one slot of a round (32 bytes)
-  uint64_t delta;  // src_off - payload_off (mod 2^64)
-  uint64_t end;    // payload_off + length; payload_off for a deferred frame (no inline chunk)
-  uint64_t start;  // payload_off
-  uint32_t key;
-  uint32_t pd;     // padded length, saturated at 2^32 - 16 (such a frame is deferred whatever it is); 0: none
-};
-struct FusedLds {
-  FusedTab* tab;   // [kFusedRound] per wave (the round's frames; lane 0's re-walk entries before that)
-  uint16_t* own;   // [2][64 S] chunk -> slot + 1 (two halves: this step's, the next one's)
-};
-
-__device__ __forceinline__ uint64_t agent_ld64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void agent_st64(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t agent_ld32(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lds_fence() { __asm__ volatile("" ::: "memory"); }
-
-// Bytes [dst, dst + len) of the arena from in[src ...] ^ key (len > 0; the
-// last chunk's bytes past len zeroed), by the whole wave: 16 chunks a lane in
-// flight per batch.
-__device__ __forceinline__ void fused_piece(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint64_t src,
-                                            uint64_t dst, uint64_t len, uint32_t key) {
-  constexpr int U = 16;
-  const uint64_t nch = (len + 15) >> 4;
-  for (uint64_t c0 = 0; c0 < nch; c0 += 64 * U) {
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t c = c0 + (uint64_t)u * 64 + (fresh_tid() & 63);
-      v[u] = u32x4{0, 0, 0, 0};
-      if (c < nch) v[u] = ld16u_stream<true>(in + src + 16 * c);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t c = c0 + (uint64_t)u * 64 + (fresh_tid() & 63);
-      if (c < nch) {
-        u32x4 x = v[u] ^ key;
-        const int64_t rem = (int64_t)len - (int64_t)(16 * c);
-        if (rem < 16) x = keep_bytes(x, rem);
-        st16_nt(out + dst + 16 * c, x);
-      }
-    }
-  }
-}
-
-// The round's payload range [R0, R1): slot s = u * 64 + lane of the wave's
-// LDS table holds a frame's payload offset (start) and padded length (pd; 0:
-// no payload / no frame).  Steps of S KiB (S chunks a lane, 64-lane
-// coalesced 1 KiB spans), software-pipelined: the NEXT step is decided --
-// skip a deferred frame, stream inside one frame, or a chunk -> slot map
-// built in the other half of the wave's double-buffered map -- while this
-// step's loads are in flight (without the overlap the map's chain of LDS round
-// trips sat between every step's loads: C4 7.69 ms).  A chunk keeps only its
-// slot (a byte of packed words) across the loads and re-reads its key and
-// payload end from LDS to store.
-struct FusedStep {
-  uint64_t p;       // step start (payload arena offset)
-  int kind;         // 0 done, 2 stream inside slot s, 3 mapped
-  uint32_t s;       // the slot covering p
-};
-
-template <int S>
-__device__ __forceinline__ void fused_unmask_range(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                   const FusedLds& L, uint64_t R0, uint64_t R1, uint64_t big_bytes) {
-  static_assert(S == 8, "8 chunks a lane (the map's two halves: 2 x 512 slots)");
-  constexpr uint64_t SB = 1024ull * S;  // bytes per step
-  constexpr uint32_t NC = 64 * S;       // chunks per step
-  const uint32_t lane = threadIdx.x & 63;
-  // The step at p (skipping deferred frames) and, for a mapped step, its map in half b.
-  auto plan = [&](uint64_t p, uint32_t b) -> FusedStep {
-    for (;;) {  // wave-uniform
-      if (p >= R1) return FusedStep{p, 0, 0};
-      uint64_t po[4];
-      uint32_t pd[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const u32x4 w = *reinterpret_cast<const u32x4*>(&L.tab[u * 64 + lane].start);  // start, key, pd
-        po[u] = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-        pd[u] = w[3];
-      }
-      // the frame covering p: the last slot with a payload starting at or before it
-      int s = -1;
-#pragma unroll
-      for (int u = 3; u >= 0; --u) {
-        const uint64_t m = __ballot(pd[u] > 0 && po[u] <= p);
-        if (s < 0 && m) s = u * 64 + 63 - __builtin_clzll(m);
-      }
-      if (s < 0) return FusedStep{R1, 0, 0};  // (cannot happen: the round's first payload starts at R0)
-      uint64_t spo = 0, spd = 0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (u == (s >> 6)) {
-          spo = uniform64(__shfl(po[u], s & 63, 64));
-          spd = uniform32((uint32_t)__shfl((int)pd[u], s & 63, 64));
-        }
-      if (spd >= big_bytes) {  // a deferred frame (pieces queued): on to the next payload after p
-        uint64_t nxt = R1;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint64_t m = __ballot(pd[u] > 0 && po[u] > p);
-          if (nxt == R1 && m) nxt = uniform64(__shfl(po[u], __builtin_ctzll(m), 64));
-        }
-        p = nxt;
-        continue;
-      }
-      if (spo + spd >= p + SB) return FusedStep{p, 2, (uint32_t)s};  // the whole step inside frame s
-      // chunk -> slot map: marks of the frames starting inside the step, then
-      // a wave prefix max seeded with slot s
-      uint16_t* own = L.own + b * NC;
-      reinterpret_cast<u32x4*>(own)[lane] = u32x4{0, 0, 0, 0};
-      lds_fence();
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (pd[u] > 0 && po[u] > p && po[u] < p + SB) own[(po[u] - p) >> 4] = (uint16_t)(u * 64 + lane + 1);
-      lds_fence();
-      u32x4 m = reinterpret_cast<const u32x4*>(own)[lane];
-      uint32_t run[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        run[2 * j] = m[j] & 0xffffu;
-        run[2 * j + 1] = m[j] >> 16;
-      }
-#pragma unroll
-      for (int k = 1; k < 8; ++k) run[k] = run[k] > run[k - 1] ? run[k] : run[k - 1];
-      uint32_t inc = run[7];
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
-        if (lane >= (uint32_t)d) inc = inc > y ? inc : y;
-      }
-      uint32_t exc = (uint32_t)__shfl_up((int)inc, 1, 64);
-      if (lane == 0) exc = 0;
-      const uint32_t seed = (uint32_t)s + 1;
-      exc = exc > seed ? exc : seed;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t lo16 = run[2 * j] > exc ? run[2 * j] : exc;
-        const uint32_t hi16 = run[2 * j + 1] > exc ? run[2 * j + 1] : exc;
-        m[j] = lo16 | (hi16 << 16);
-      }
-      reinterpret_cast<u32x4*>(own)[lane] = m;
-      lds_fence();
-      return FusedStep{p, 3, (uint32_t)s};
-    }
-  };
-  uint32_t b = 0;
-  FusedStep cur = plan(R0, b);
-  while (cur.kind != 0) {  // wave-uniform
-    u32x4 v[S];
-    uint32_t sl4[S / 4];  // each chunk's slot, a byte each (mapped steps)
-    uint32_t live = 0;    // chunks with payload bytes
-    uint64_t sdelta = 0, send = 0;
-    uint32_t skey = 0;
-    if (cur.kind == 2) {
-      const FusedTab& te = L.tab[cur.s];
-      sdelta = uniform64(te.delta);
-      send = uniform64(te.end);
-      skey = uniform32(te.key);
-#pragma unroll
-      for (int u = 0; u < S; ++u)
-        v[u] = ld16u_stream<true>(in + (cur.p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16 + sdelta));
-    } else {
-      const uint16_t* own = L.own + b * NC;
-#pragma unroll
-      for (int k = 0; k < S / 4; ++k) sl4[k] = 0;
-#pragma unroll
-      for (int u = 0; u < S; ++u) {
-        const uint32_t c = (uint32_t)u * 64 + (fresh_tid() & 63);
-        const uint64_t q = cur.p + 16ull * c;
-        v[u] = u32x4{0, 0, 0, 0};
-        if (q < R1) {
-          const uint32_t sl = (uint32_t)own[c] - 1u;
-          const u64x2 te = *reinterpret_cast<const u64x2*>(&L.tab[sl]);  // delta, end
-          sl4[u >> 2] |= sl << (8 * (u & 3));
-          if ((int64_t)(te[1] - q) > 0) {
-            live |= 1u << u;
-            v[u] = ld16u_stream<true>(in + (q + te[0]));
-          }
-        }
-      }
-    }
-    // the next step, while this one's loads are in flight
-    __asm__ volatile("" ::: "memory");
-    const FusedStep nxt = plan(cur.p + SB, b ^ 1);
-    if (cur.kind == 2) {
-#pragma unroll
-      for (int u = 0; u < S; ++u) {
-        const uint64_t q = cur.p + (uint64_t)u * 1024 + (fresh_tid() & 63) * 16;
-        u32x4 x = v[u] ^ skey;
-        const int64_t rem = (int64_t)(send - q);
-        if (rem < 16) x = keep_bytes(x, rem);
-        st16_nt(out + q, x);
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < S; ++u) {
-        if (live & (1u << u)) {
-          const uint32_t sl = (sl4[u >> 2] >> (8 * (u & 3))) & 0xffu;
-          const uint64_t q = cur.p + 16ull * ((uint32_t)u * 64 + (fresh_tid() & 63));
-          const int64_t rem = (int64_t)(L.tab[sl].end - q);
-          u32x4 x = v[u] ^ L.tab[sl].key;
-          if (rem < 16) x = keep_bytes(x, rem);
-          st16_nt(out + q, x);
-        }
-      }
-    }
-    cur = nxt;
-    b ^= 1;
-  }
-  lds_fence();  // (the next round's table writes after this round's reads)
-}
-
-// One row: records + inline unmask of its frames below A.big_bytes, pieces of
-// the others queued.
-template <int S>
-__device__ __forceinline__ void fused_row(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                          const FusedArgs& A, const FusedLds& L, uint64_t c, bool unordered) {
-  const uint32_t lane = threadIdx.x & 63;
-  gevws_conn_out o = A.rout[c];
-  if (A.ks) {
-    const gevws_conn_out pr = A.pout[c / A.ks];
-    o.first_frame += pr.first_frame;
-    o.payload_base += pr.payload_base;
-  }
-  const uint64_t cnt = uniform64(o.nframes);
-  if (cnt == 0) return;
-  const gevws_conn_in ci = A.rows[c];
-  const uint64_t coff = uniform64(ci.off), clen = uniform64(ci.len);
-  uint64_t ebase = 0, ecap = 0;
-  const bool rec = A.rec_flags[c] && !unordered &&
-                   entry_slots_of(gevws_conn_in{coff, clen}, (uint32_t)c, A.n_entries, A.gshift, ebase, ecap);
-  const uint64_t f0 = uniform64(o.first_frame);
-  uint64_t carry = uniform64(o.payload_base), pcarry = 0;
-  for (uint64_t k0 = 0; k0 < cnt; k0 += kFusedRound) {
-    WalkEntry q[4];
-    if (rec) {
-      const WalkEntry* ce = reinterpret_cast<const WalkEntry*>(A.entries) + ebase;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint64_t k = k0 + (uint64_t)u * 64 + lane;
-        q[u] = ce[k < cnt ? k : cnt - 1];
-      }
-    } else {  // no entries: lane 0 walks this round's headers into LDS
-      WalkEntry* buf = reinterpret_cast<WalkEntry*>(L.tab);
-      const uint64_t m = cnt - k0 < kFusedRound ? cnt - k0 : kFusedRound;
-      lds_fence();
-      if (lane == 0) {
-        uint64_t pos = pcarry;
-        for (uint64_t i = 0; i < m; ++i) {
-          uint64_t lo, hi;
-          load_window(in + coff + pos, lo, hi);
-          DevHdr h;
-          parse_header(lo, hi, clen - pos, h);  // succeeded in the counting walk
-          buf[i] = make_entry(h.mask, h.length, h.b0 | (h.masked << 8) | (h.hlen << 16));
-          pos += h.hlen + h.length;
-        }
-      }
-      lds_fence();
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint64_t k = (uint64_t)u * 64 + lane;
-        q[u] = buf[k < m ? k : m - 1];
-      }
-      lds_fence();
-    }
-    const uint64_t R0 = carry;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (k0 + (uint64_t)u * 64 >= cnt) {  // wave-uniform: no frames in these slots
-        L.tab[u * 64 + lane].pd = 0;
-        continue;
-      }
-      const uint64_t k = k0 + (uint64_t)u * 64 + lane;
-      const bool valid = k < cnt;
-      uint64_t Ln, ip;
-      entry_round(in, q[u], valid, lane == 0, pcarry, coff, Ln, ip);
-      const uint32_t hlen = entry_hlen(q[u]);
-      const uint64_t fsz = valid ? hlen + Ln : 0;
-      const uint64_t padded = valid ? round16(Ln) : 0;
-      const uint64_t incl = wave_incl_scan(padded);
-      const uint64_t poff = carry + incl - padded;
-      const uint64_t src = coff + pcarry + ip - fsz + hlen;
-      const uint32_t key = q[u].mask;  // 0 for an unmasked frame (the walk zeroes it)
-      const uint32_t pds = padded < 0xfffffff0ull ? (uint32_t)padded : 0xfffffff0u;
-      const bool big = valid && pds >= A.big_bytes;
-      if (valid) {
-        const uint32_t b0 = q[u].w & 0xffu, masked = (q[u].w >> 8) & 1u;
-        const uint32_t flags = (b0 >> 7) | (((b0 & 0x70u) >> 4) << 8) | ((b0 & 0x0fu) << 16) | (masked << 24);
-        u32x4* r = reinterpret_cast<u32x4*>(A.frames + f0 + k);
-        r[0] = u32x4{flags, key, (uint32_t)Ln, (uint32_t)(Ln >> 32)};
-        r[1] = u32x4{(uint32_t)poff, (uint32_t)(poff >> 32), (uint32_t)src, (uint32_t)(src >> 32)};
-      }
-      const uint32_t s = (uint32_t)u * 64 + lane;
-      L.tab[s] = FusedTab{src - poff, big ? poff : poff + Ln, poff, key, pds};
-      if (__ballot(big)) {  // queue the deferred frames' pieces
-        const uint64_t np = big ? (padded + kPieceBytes - 1) / kPieceBytes : 0;
-        const uint64_t ni = wave_incl_scan(np);
-        const uint64_t tot = uniform64(__shfl(ni, 63, 64));
-        uint32_t base = 0;
-        if (lane == 0)
-          base = __hip_atomic_fetch_add(A.ctr + kCtrPieces * 16, (uint32_t)tot, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-        base = uniform32(__shfl((int)base, 0, 64));
-        for (uint64_t j = 0; j < np; ++j) {
-          const uint64_t idx = base + ni - np + j;
-          if (idx >= A.piece_cap) break;  // (sized for the worst case: never)
-          uint64_t* e = A.pieces + 4 * idx;
-          const uint64_t off = j * kPieceBytes;
-          const uint64_t len = Ln - off < kPieceBytes ? Ln - off : kPieceBytes;
-          agent_st64(e + 0, src + off);
-          agent_st64(e + 1, poff + off);
-          agent_st64(e + 2, (len << 32) | key);
-          __builtin_amdgcn_s_waitcnt(0);  // the words above are complete before the stamp
-          agent_st64(e + 3, A.gen);
-        }
-      }
-      carry += uniform64(__shfl(incl, 63, 64));
-      pcarry += uniform64(__shfl(ip, 63, 64));
-    }
-    lds_fence();
-    fused_unmask_range<S>(in, out, L, R0, carry, A.big_bytes);
-  }
-}
-
-template <int S>
-__device__ void fused_body(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                           const gevws_summary* __restrict__ sum, const FusedArgs& A, const FusedLds& L) {
-  if (sum->status != GEVWS_OK) return;
-  const uint32_t lane = threadIdx.x & 63;
-  const bool unordered = (sum->flags & GEVWS_SUMMARY_UNORDERED) != 0;
-  const uint64_t n = A.n_rows;
-  const uint64_t segn = (n + kUnmaskRunCounters - 1) / kUnmaskRunCounters;
-  const uint32_t xc = blockIdx.x % kUnmaskRunCounters;
-  // 1. rows: this XCD's counter, then the others'
-  for (uint32_t x = 0; x < kUnmaskRunCounters;) {
-    const uint32_t sx = (xc + x) % kUnmaskRunCounters;
-    const uint64_t s0 = (uint64_t)sx * segn < n ? (uint64_t)sx * segn : n;
-    const uint64_t s1 = s0 + segn < n ? s0 + segn : n;
-    uint32_t u = 0;
-    if (lane == 0) u = __hip_atomic_fetch_add(A.ctr + sx * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    u = uniform32(__shfl((int)u, 0, 64));
-    const uint64_t r0 = s0 + (uint64_t)u * A.unit_rows;
-    if (r0 >= s1) {
-      ++x;
-      continue;
-    }
-    const uint64_t r1 = r0 + A.unit_rows < s1 ? r0 + A.unit_rows : s1;
-    for (uint64_t c = r0; c < r1; ++c) fused_row<S>(in, out, A, L, c, unordered);
-    __builtin_amdgcn_s_waitcnt(0);  // every piece this wave queued is complete
-    if (lane == 0)
-      __hip_atomic_fetch_add(A.ctr + kCtrRowsDone * 16, (uint32_t)(r1 - r0), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // 2. pieces: the waves of XCD x take queue indices x, x + 8, ... in turn
-  // (one fetch-add each on that XCD's cursor; a compare-and-swap on one
-  // shared cursor serialised thousands of waves per claim: C4 1 982 ms); a
-  // claimed index is processed once queued, or dropped once every row is
-  // done and the queue ended below it
-  uint32_t spins = 0;
-  bool have = false;
-  uint64_t idx = 0;
-  for (;;) {
-    if (!have) {
-      uint32_t k = 0;
-      if (lane == 0)
-        k = __hip_atomic_fetch_add(A.ctr + (kCtrCursor + xc) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      idx = (uint64_t)uniform32((uint32_t)__shfl((int)k, 0, 64)) * kUnmaskRunCounters + xc;
-      have = true;
-    }
-    if (idx >= A.piece_cap) break;  // (beyond any queue this decode can have)
-    if (idx < uniform32(agent_ld32(A.ctr + kCtrPieces * 16))) {
-      const uint64_t* e = A.pieces + 4 * idx;
-      uint32_t wait = 0;
-      while (uniform64(agent_ld64(e + 3)) != A.gen) {  // queued, not yet stamped
-        if (++wait > kFusedMaxSpins) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      if (wait > kFusedMaxSpins) {
-        spins = kFusedMaxSpins + 1;
-        break;
-      }
-      const uint64_t src = uniform64(agent_ld64(e + 0)), dst = uniform64(agent_ld64(e + 1));
-      const uint64_t w2 = uniform64(agent_ld64(e + 2));
-      fused_piece(in, out, src, dst, w2 >> 32, (uint32_t)w2);
-      have = false;
-      spins = 0;
-      continue;
-    }
-    if (uniform32(agent_ld32(A.ctr + kCtrRowsDone * 16)) >= n) {
-      // every row is done, so the piece count is final
-      if (idx >= uniform32(agent_ld32(A.ctr + kCtrPieces * 16))) break;
-      continue;
-    }
-    if (++spins > kFusedMaxSpins) break;
-    __builtin_amdgcn_s_sleep(64);
-  }
-  if (spins > kFusedMaxSpins && lane == 0)  // gave up waiting: the output is incomplete, say so
-    __hip_atomic_store(&A.sum->status, (int32_t)GEVWS_ERR_DEVICE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// The round-4 default unmask (GEVWS_TUNE_UNMASK_VARIANT 2 since round 5): the
-// batch's own statistics pick the window scheme -- batches of equal-size
-// frames (at least half of the frames the size of the one before them on the
-// connection: C1, C2, C3, C5) take v3's 4-tile windows, mixed ones (C4) v5's
-// pipelined 8-tile windows, with the whole (wide) grid for a batch of fewer
-// than kWideGridTiles tiles.  One kernel, one LDS budget, the choice is a
-// uniform branch on the summary the walk wrote.
+// The default unmask: the batch's own statistics pick the window scheme --
+// batches of equal-size frames (at least half of the frames the size of the
+// one before them on the connection: C1, C2, C3, C5) take v3's 4-tile windows,
+// mixed ones (C4) v5's pipelined 8-tile windows, with the whole (wide) grid
+// for a batch of fewer than kWideGridTiles tiles.  One kernel, one LDS
+// budget, the choice is a uniform branch on the summary the walk wrote.
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_auto5(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
-    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs,
-    FusedArgs) {
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs) {
   static_assert(kWinFrames == kWin5Frames, "one frame table for both bodies");
   __shared__ uint32_t s_start[kWinFrames];
   __shared__ int32_t s_lend[kWinFrames];
@@ -1054,8 +608,7 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
 // batch, so the parity tests run it over equal-size frames too.
 __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_v5(
     const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
-    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs,
-    FusedArgs) {
+    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs) {
   __shared__ int32_t s_lend[kWin5Frames];
   __shared__ uint64_t s_delta[kWin5Frames];
   __shared__ uint32_t s_key[kWin5Frames];
@@ -1065,36 +618,6 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4)
   unmask_v5_body<16>(in, frames, tile_first, sum, out, big_grid,
                      WinLds5{s_lend, s_delta, s_key, s_own, s_wtot, s_tmap},
                      sum->payload_bytes / kTile < kWideGridTiles, runs);
-}
-
-// The default since round 5: batches of equal-size frames take v3 (records and
-// tile map from k_walk_emit), mixed ones the fused record + unmask path (the
-// record pass skipped them, k_walk_emit's gate); ALL = the fused path for
-// every batch (GEVWS_TUNE_UNMASK_VARIANT 3; the record pass skips every batch).
-constexpr uint32_t kFusedLdsPerWave = kFusedRound * sizeof(FusedTab) + kFusedStepChunks * 2;
-constexpr uint32_t kV3LdsBytes = kWinFrames * (4 + 4 + 8 + 4) + 16;
-constexpr uint32_t kFusedLdsBytes = (kUnmaskBlock / 64) * kFusedLdsPerWave > kV3LdsBytes
-                                        ? (kUnmaskBlock / 64) * kFusedLdsPerWave : kV3LdsBytes;
-static_assert(4 * kFusedLdsBytes <= 160 * 1024, "four workgroups a CU");
-template <bool ALL, int S = kFusedStep>
-__global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_unmask_fused(
-    const uint8_t* __restrict__ in, const gevws_frame* __restrict__ frames, const uint32_t* __restrict__ tile_first,
-    const gevws_summary* __restrict__ sum, uint8_t* __restrict__ out, uint32_t big_grid, uint32_t* __restrict__ runs,
-    FusedArgs A) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_raw[kFusedLdsBytes];
-  if (!ALL && 2 * sum->run_frames >= sum->frames) {
-    uint32_t* s_start = reinterpret_cast<uint32_t*>(s_raw);
-    int32_t* s_lend = reinterpret_cast<int32_t*>(s_raw + 4 * kWinFrames);
-    uint64_t* s_delta = reinterpret_cast<uint64_t*>(s_raw + 8 * kWinFrames);
-    uint32_t* s_key = reinterpret_cast<uint32_t*>(s_raw + 16 * kWinFrames);
-    uint32_t* s_run = reinterpret_cast<uint32_t*>(s_raw + 20 * kWinFrames);
-    unmask_v3_body<16>(in, frames, tile_first, sum, out, big_grid, WinLds{s_start, s_lend, s_delta, s_key}, runs,
-                       s_run);
-    return;
-  }
-  uint8_t* w = s_raw + (threadIdx.x >> 6) * kFusedLdsPerWave;
-  const FusedLds L{reinterpret_cast<FusedTab*>(w), reinterpret_cast<uint16_t*>(w + kFusedRound * sizeof(FusedTab))};
-  fused_body<S>(in, out, sum, A, L);
 }
 
 // ------------------------------------------------------------------ ws.Cipher on a device buffer
@@ -1126,30 +649,26 @@ __global__ __launch_bounds__(256) void k_cipher(uint8_t* __restrict__ p, uint64_
 }
 
 using UnmaskFn = void (*)(const uint8_t*, const gevws_frame*, const uint32_t*, const gevws_summary*, uint8_t*,
-                         uint32_t, uint32_t*, FusedArgs);
+                         uint32_t, uint32_t*);
 struct UnmaskVariant {
   UnmaskFn fn;
   int unroll;
   const char* name;
-  bool wide = false;   // may launch the wide grid
-  bool runs = true;    // counter runs (v3 / v5) / the fused path's counters
-  int emit_gate = 0;   // k_walk_emit: 0 = every batch, 1 = not for mixed batches, 2 = never (the fused path writes the records)
+  bool wide = false;  // may launch the wide grid (k_unmask_auto)
+  bool runs = true;   // the v5 path's counter runs (else one contiguous run per workgroup)
 };
 // Variant 0 is the default (gevws_ctx_set_tuning(ctx, GEVWS_TUNE_UNMASK_VARIANT, i)).
 // The measurement variants of rounds 1-3 (v3 / v4 window shapes, interleaved
 // searches, phase-profiled builds, other occupancies) are gone from the
 // library; their measurements stay in profiles/ and DESIGN.md §5.
 const UnmaskVariant kUnmaskVariants[] = {
-    {k_unmask_fused<false>, 16,
-     "auto: v3 4-tile windows for batches of equal-size frames; for mixed sizes the fused record + unmask path "
-     "(records and payloads straight from the walk's entries, one wave per row, big frames in queued pieces) when "
-     "the batch has >= 16 rows a wave of 64 KiB - 1 MiB, else round 4's record pass + v5",
-     true, true, 1},
-    {k_unmask_v5, 16, "v5 for every batch (the round-4 mixed-batch path alone)", true, true, 0},
     {k_unmask_auto5, 16,
-     "round 4's default: v3 for equal-size batches, v5 (pipelined 8-tile windows with a chunk -> frame map, records "
-     "read back) for mixed ones", true, true, 0},
-    {k_unmask_fused<true>, 16, "the fused record + unmask path for every batch", true, true, 2},
+     "auto: v3 4-tile windows for batches of equal-size frames, v5 (pipelined 8-tile windows with a chunk -> frame "
+     "map and the tile map cached in LDS) otherwise; non-temporal streaming and window loads; a wide grid for a "
+     "smaller batch of mixed sizes after one on this context", true},
+    {k_unmask_v5, 16, "v5 for every batch (the default's mixed-batch path alone)", true},
+    {k_unmask_auto5, 16, "the default with one contiguous run per workgroup on the v5 path (rounds 1-3; measurement)",
+     true, false},
 };
 constexpr int kNumUnmaskVariants = sizeof(kUnmaskVariants) / sizeof(kUnmaskVariants[0]);
 
@@ -1160,25 +679,17 @@ namespace gevws_impl {
 int unmask_variant_count() { return kNumUnmaskVariants; }
 const char* unmask_variant_name(int i) { return i >= 0 && i < kNumUnmaskVariants ? kUnmaskVariants[i].name : nullptr; }
 
-// Variant 0 takes the fused path only for batches decode_front found suited
-// (ctx->fused_ok); the others run round 4's record pass + v3 / v5 (variant 2).
-static const UnmaskVariant& unmask_variant_of(const gevws_ctx* ctx) {
-  return (ctx->unmask_variant == 0 && !ctx->fused_ok) ? kUnmaskVariants[2] : kUnmaskVariants[ctx->unmask_variant];
-}
-
-int unmask_emit_gate(const gevws_ctx* ctx) { return unmask_variant_of(ctx).emit_gate; }
-
 int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const uint8_t* d_in,
                   const gevws_frame* d_frames, const uint32_t* tile_first, const gevws_summary* d_summary,
-                  uint8_t* d_payload, const FusedArgs& fa) {
-  const UnmaskVariant& v = unmask_variant_of(ctx);
+                  uint8_t* d_payload) {
+  const UnmaskVariant& v = kUnmaskVariants[ctx->unmask_variant];
   const uint64_t ntiles = (payload_cap + kTile - 1) / kTile;
   const uint32_t ucus = (uint32_t)ctx->num_cus;
   const uint64_t norm = 4 * (uint64_t)ucus;
   // the wide grid (kWideGridPerCU per CU) when the previous decode on this
   // context was a batch of mixed sizes (run frames < half) below
-  // kWideGridTiles; the v3 / v5 bodies still use `norm` workgroups unless
-  // this batch is one too (the fused path's waves take rows as they come)
+  // kWideGridTiles; the kernel still uses `norm` workgroups unless this
+  // batch is one too
   const bool wide = v.wide && !ctx->unmask_grid && ctx->stats_known && ctx->prev_mixed &&
                     ntiles < kWideGridTiles && norm <= 0xffffu;
   uint64_t grid = ctx->unmask_grid ? (uint64_t)ctx->unmask_grid : wide ? kWideGridPerCU * (uint64_t)ucus : norm;
@@ -1188,7 +699,7 @@ int launch_unmask(gevws_ctx* ctx, hipStream_t st, uint64_t payload_cap, const ui
   ctx->last_unmask_grid = (uint32_t)grid;
   v.fn<<<(uint32_t)grid, kUnmaskBlock, 0, st>>>(d_in, d_frames, tile_first, d_summary, d_payload,
                                                 ctx->unmask_grid ? 0u : ucus | (wide ? (uint32_t)norm << 16 : 0u),
-                                                v.runs ? ctx->unmask_runs : nullptr, fa);
+                                                v.runs ? ctx->unmask_runs : nullptr);
   return GEVWS_OK;
 }
 

@@ -123,6 +123,47 @@ __device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uin
 constexpr uint64_t kWriterChainsPerCU = 128;  // k_walk_count ST 2 (the writer wave) from n_conns >= this x CUs
 constexpr uint32_t kEntryGranMinShift = 6;        // 64-byte granularity when the table fits
 constexpr uint64_t kEntryBudget = 1ull << 29;     // entries (8 GiB of scratch) at most
+// slot runs start on 32-entry (256-byte) boundaries: the writer wave of the
+// LDS-ring walk stores whole 256-byte groups (k_walk_count ST 2)
+constexpr uint32_t kSlotShift = 5;
+constexpr uint64_t kSlotAlign = 1ull << kSlotShift;
+// 8-byte entry: the key, and b0 | masked << 8 | length form << 9 | payload
+// length << 11.  The header's position is not stored: a row's frames are
+// contiguous from its start, so the record pass recomputes each position as
+// the prefix sum of the frame sizes before it (hlen + L).  A payload length
+// >= kLenEsc is stored as kLenEsc and re-read from the header by the record
+// pass, where the prefix sum gives its position (rare: frames of 2 MiB and
+// more, whose unmask dwarfs one header load).  Round 2's 16-byte entry
+// (position, key, length, meta) cost the walk 0.71 GB of C4's writes and the
+// record pass as many reads (profiles/r03/r03_pmc_split.json).
+constexpr uint32_t kLenEsc = (1u << 21) - 1;
+struct WalkEntry {
+  uint32_t mask;
+  uint32_t w;
+};
+static_assert(sizeof(WalkEntry) == 8, "one dwordx2 per entry");
+// meta: b0 | masked << 8 | hlen << 16 (walk_parse / walk_chain)
+__device__ __forceinline__ WalkEntry make_entry(uint32_t key, uint64_t L, uint32_t meta) {
+  const uint32_t hlen = meta >> 16, masked = (meta >> 8) & 1u;
+  const uint32_t ext = hlen - 2 - 4 * masked;  // 0, 2 or 8 length bytes
+  const uint32_t form = ext == 0 ? 0u : (ext == 2 ? 1u : 2u);
+  const uint32_t l21 = L < kLenEsc ? (uint32_t)L : kLenEsc;
+  return WalkEntry{key, (meta & 0x1ffu) | (form << 9) | (l21 << 11)};
+}
+__device__ __forceinline__ uint32_t entry_hlen(const WalkEntry& e) {
+  const uint32_t form = (e.w >> 9) & 3u;
+  return 2 + (form == 2 ? 8u : 2u * form) + 4 * ((e.w >> 8) & 1u);
+}
+__device__ __forceinline__ uint32_t entry_len21(const WalkEntry& e) { return e.w >> 11; }
+
+__device__ __forceinline__ bool entry_slots_of(const gevws_conn_in& ci, uint32_t c, uint64_t n_entries,
+                                              uint32_t gshift, uint64_t& base, uint64_t& cap) {
+  if (n_entries == 0 || ci.len >= (1ull << 32)) return false;
+  base = kSlotAlign * ((ci.off >> (gshift + kSlotShift)) + (uint64_t)c);
+  cap = kSlotAlign * ((ci.len >> (gshift + kSlotShift)) + 1);
+  return base + cap <= n_entries;
+}
+
 // Connection c breaks the increasing, non-overlapping order the slot runs rely
 // on (its stream starts before the previous one ends).
 __device__ __forceinline__ bool out_of_order(const gevws_conn_in* __restrict__ conns, uint32_t c,
@@ -840,7 +881,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_bases(uint32_t n, gevws_co
                                                             uint32_t* __restrict__ runs = nullptr) {
   // the unmask's per-XCD run counters start at zero (before the capacity check:
   // the unmask reads them whatever the status)
-  if (runs && blockIdx.x == 0 && threadIdx.x < kWorkCounters) runs[threadIdx.x * 16] = 0;
+  if (runs && blockIdx.x == 0 && threadIdx.x < kUnmaskRunCounters) runs[threadIdx.x * 16] = 0;
   if (stats && blockIdx.x == 0 && threadIdx.x == 0) {  // the context's history (split walk, D, wide grid)
     stats[0] = sum->frames;
     stats[1] = sum->payload_len;
@@ -899,11 +940,52 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
 // Connections without recorded entries are re-walked afterwards, one lane per
 // connection.
 
+// Segmented inclusive wave scan: a segment starts at every lane with head set
+// (and at lane 0).  Every lane must take part.
+__device__ __forceinline__ uint64_t wave_seg_scan(uint64_t v, bool head) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t vu = __shfl_up(v, d, 64);
+    const bool hu = __shfl_up((int)head, d, 64) != 0;
+    if (lane >= d && !head) {
+      v += vu;
+      head = hu;
+    }
+  }
+  return v;
+}
+
+// One round of entries (lane = frame): each frame's payload length L and the
+// segmented inclusive prefix `ip` of the frame sizes (hlen + L), so a frame
+// starts at (its row's position carry) + ip - (hlen + L).  Escaped lengths
+// (>= kLenEsc) are re-read from the header, lowest lane first: every frame
+// before it in its row is then resolved, so its position is exact.  `head`:
+// the lane starts a row in this round; pbase / coff: the position carry and
+// input offset of the lane's row (every lane must take part: shuffles).
+__device__ __forceinline__ void entry_round(const uint8_t* __restrict__ in, const WalkEntry& q, bool valid, bool head,
+                                            uint64_t pbase, uint64_t coff, uint64_t& L, uint64_t& ip) {
+  L = valid ? entry_len21(q) : 0;
+  bool esc = valid && L == kLenEsc;
+  uint64_t fsz = (valid && !esc) ? entry_hlen(q) + L : 0;
+  ip = wave_seg_scan(fsz, head);
+  for (;;) {
+    const uint64_t m = __ballot(esc);
+    if (m == 0) break;  // wave-uniform
+    if ((threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) {
+      uint64_t lo, hi;
+      load_window(in + coff + pbase + ip, lo, hi);  // (fsz == 0: ip is the frame's start)
+      DevHdr h;
+      parse_header(lo, hi, ~0ull, h);  // parsed by the walk: complete
+      L = h.length;
+      fsz = h.hlen + L;
+      esc = false;
+    }
+    ip = wave_seg_scan(fsz, head);
+  }
+}
+
 constexpr int kEmitGroup = 16;
-// decode_front's rule for the fused record + unmask path (unmask variant 0)
-constexpr uint64_t kFusedMinRowsPerCU = 256;         // 16 rows a wave at 16 waves a CU
-constexpr uint64_t kFusedMinRowBytes = 64 * 1024;
-constexpr uint64_t kFusedMaxRowBytes = 1024 * 1024;
 constexpr uint64_t kEmitSplitPerCU = 32;  // record-pass workgroups per CU over k_walk_split's rows
 // (Measured and not kept: phase 2 software-pipelined, the next batch's entry
 // loads issued before this batch's rounds -- C4 0.448 -> 0.477 ms, 8-way share
@@ -917,12 +999,9 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
                                                           const WalkEntry* __restrict__ entries, uint64_t n_entries,
                                                           uint32_t gshift, const uint8_t* __restrict__ rec_flags,
                                                           const gevws_conn_out* __restrict__ pout = nullptr,
-                                                          uint32_t ks = 0, int gate = 0) {
+                                                          uint32_t ks = 0) {
   constexpr int U = 4, G = kEmitGroup;
   if (sum->status != GEVWS_OK) return;
-  // gate 1: a batch of mixed sizes gets its records from the fused record +
-  // unmask path instead (k_unmask_fused, the same summary test)
-  if (gate == 1 && 2 * sum->run_frames < sum->frames) return;
   // k_walk_split's segments: frame / payload offsets relative to connection c / ks
   auto out_of = [&](uint64_t c) {
     gevws_conn_out o = cout[c];
@@ -1293,7 +1372,7 @@ int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
 int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
                  const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
                  uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary, hipEvent_t* ev,
-                 uint32_t** tile_first_out, FusedArgs* fa) {
+                 uint32_t** tile_first_out) {
   const uint32_t ncu = (uint32_t)ctx->num_cus;
   // connections per counting workgroup: 64, or fewer so a small batch covers every CU
   const uint32_t cpb = n_conns >= (uint32_t)kCountBlock * ncu ? (uint32_t)kCountBlock
@@ -1337,23 +1416,11 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   // + one sink slot per walk lane after the table (k_walk_count / k_walk_split)
   int r = order_after_last(ctx, st);
   if (r != GEVWS_OK) return r;
-  const size_t run_bytes = kWorkCounters * 64;  // the unmask's work counters, 64 bytes apart
-  // the fused path's piece queue (first in the scratch, so it stays put):
-  // at most payload / kPieceBytes + payload / big_bytes pieces (every deferred
-  // frame is >= big_bytes)
-  const uint64_t piece_cap = payload_cap / (64 * 1024) + payload_cap / ctx->fused_big_bytes + 64;
-  const size_t piece_bytes = ((size_t)piece_cap * 32 + 255) & ~size_t(255);
-  r = ensure_scratch(ctx, piece_bytes + blk_bytes + tile_bytes + run_bytes + flag_bytes + seg_bytes +
+  const size_t run_bytes = kUnmaskRunCounters * 64;  // the unmask's run counters, 64 bytes apart
+  r = ensure_scratch(ctx, blk_bytes + tile_bytes + run_bytes + flag_bytes + seg_bytes +
                               (n_entries + n_v) * sizeof(WalkEntry));
   if (r != GEVWS_OK) return r;
-  if (ctx->pieces_zeroed_at != ctx->scratch || ctx->pieces_zeroed_bytes < piece_bytes) {
-    // a fresh queue: no stale stamp may equal a later decode's (stamps start at 1)
-    GEVWS_HIP(hipMemsetAsync(ctx->scratch, 0, piece_bytes, st));
-    ctx->pieces_zeroed_at = ctx->scratch;
-    ctx->pieces_zeroed_bytes = piece_bytes;
-  }
-  uint64_t* pieces = reinterpret_cast<uint64_t*>(ctx->scratch);
-  char* sp = reinterpret_cast<char*>(ctx->scratch) + piece_bytes;
+  char* sp = reinterpret_cast<char*>(ctx->scratch);
   uint64_t* blk = reinterpret_cast<uint64_t*>(sp);
   uint32_t* tile_first = reinterpret_cast<uint32_t*>(sp + blk_bytes);
   ctx->unmask_runs = reinterpret_cast<uint32_t*>(sp + blk_bytes + tile_bytes);
@@ -1364,36 +1431,6 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   uint8_t* srec = reinterpret_cast<uint8_t*>(segp + n_v * (sizeof(gevws_conn_in) + sizeof(gevws_conn_out)));
   WalkEntry* entries = reinterpret_cast<WalkEntry*>(segp + seg_bytes);
   *tile_first_out = tile_first;
-  *fa = FusedArgs{};
-  fa->frames = d_frames;
-  fa->sum = d_summary;
-  fa->rows = d_conns;
-  fa->rout = d_conn_out;
-  fa->rec_flags = rec_flags;
-  fa->entries = entries;
-  fa->n_entries = wv == 2 ? 0 : n_entries;
-  fa->n_rows = (uint32_t)n_v;
-  fa->gshift = gshift;
-  // the fused record + unmask path pays where every wave gets many rows of
-  // moderate size: a wave writes a row's records and unmasks its payloads
-  // alone, so a few big rows (C5: 256 rows of 4 MiB) or few rows per wave
-  // (C4's 2-way share, 8 a wave) leave waves idle at the end, and tiny rows
-  // (the 8-way share's split segments, 18 KB) pay the per-row latencies
-  // (profiles/r05/r05_fused_ab.jsonl); those batches keep the record pass + v5
-  {
-    const uint64_t per_row = n_v ? in_bytes / n_v : 0;
-    ctx->fused_ok = n_v >= kFusedMinRowsPerCU * (uint64_t)ncu && per_row >= kFusedMinRowBytes &&
-                    per_row <= kFusedMaxRowBytes;
-  }
-  {  // rows per grab: ~16 grabs a wave (4 waves a workgroup, 4 workgroups a CU), at most 64 rows
-    const uint64_t per = n_v / (16ull * 16 * ncu);
-    fa->unit_rows = (uint32_t)(per < 1 ? 1 : (per > 64 ? 64 : per));
-  }
-  fa->ctr = ctx->unmask_runs;
-  fa->pieces = pieces;
-  fa->piece_cap = piece_cap;
-  fa->big_bytes = ctx->fused_big_bytes;
-  fa->gen = ++ctx->decode_gen;
   if (ev) GEVWS_HIP(hipEventRecord(ev[0], st));
   // walk variant 2: no entry table -- the counting walk stores nothing per
   // frame and the record pass re-walks every chain
@@ -1450,17 +1487,9 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
     // load round trip, so more waves share them out)
     const uint64_t ecap = (ks > 1 ? kEmitSplitPerCU : 8) * (uint64_t)ncu;
     if (egrid > ecap) egrid = ecap;
-    const int gate = unmask_emit_gate(ctx);
-    if (gate != 2)
-      k_walk_emit<<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out, d_summary, d_frames,
-                                                            tile_first, entries, ne, gshift, e_rec, e_parent,
-                                                            ks > 1 ? ks : 0, gate);
-    // the fused record + unmask path's rows: the record pass's
-    fa->rows = e_conns;
-    fa->rout = e_out;
-    fa->pout = e_parent;
-    fa->rec_flags = e_rec;
-    fa->ks = ks > 1 ? ks : 0;
+    k_walk_emit<<<(uint32_t)egrid, kWalkBlock, 0, st>>>(d_in, e_conns, (uint32_t)n_v, e_out, d_summary, d_frames,
+                                                          tile_first, entries, ne, gshift, e_rec, e_parent,
+                                                          ks > 1 ? ks : 0);
   }
   GEVWS_HIP(hipGetLastError());
   return GEVWS_OK;

@@ -145,12 +145,11 @@ void *gevws_ctx_stream(const gevws_ctx *ctx);
  * outputs from another stream orders it first, with this or an event. */
 int gevws_ctx_order_after_last(gevws_ctx *ctx, void *stream);
 /* Tuning knobs for measurement and parity tests (defaults are the tuned
- * choice): GEVWS_TUNE_UNMASK_VARIANT the record pass + unmask (0 = default:
- * for batches of equal-size frames the record pass, then v3 4-tile windows;
- * for mixed sizes ONE fused kernel writes the records and unmasks straight
- * from the header walk's entries; 1 = record pass + v5 pipelined 8-tile
- * windows with a chunk -> frame map for every batch; 2 = round 4's default,
- * record pass + v3 / v5 by batch; 3 = the fused kernel for every batch),
+ * choice): GEVWS_TUNE_UNMASK_VARIANT the unmask kernel (0 = default: v3 4-tile
+ * windows for batches of equal-size frames, v5 pipelined 8-tile windows with
+ * a chunk -> frame map for mixed sizes, its workgroups taking runs of 16
+ * tiles from a per-XCD counter; 1 = v5 for every batch; 2 = the default with
+ * one contiguous run per workgroup on the v5 path),
  * GEVWS_TUNE_UNMASK_GRID its workgroup count (0 = auto; when set it caps the
  * encode's grid too), GEVWS_TUNE_ENCODE_VARIANT the encode's step (0 = the
  * default: two 4 KiB tiles a wave step when out_cap / n > 256 bytes, else
@@ -183,12 +182,6 @@ int gevws_ctx_order_after_last(gevws_ctx *ctx, void *stream);
 /* ... and the auto choice doubles the lanes per connection while the walk
  * keeps at most this many lanes per CU (default 512; 64 .. 4 096). */
 #define GEVWS_TUNE_SPLIT_LANES_PER_CU 14
-/* The fused record + unmask path (GEVWS_TUNE_UNMASK_VARIANT 0 on a batch of
- * mixed sizes, or 3): frames of at least this many padded payload bytes are
- * not unmasked by the wave that writes their record but queued as 64 KiB
- * pieces that every wave takes once the rows are done (default 32 768;
- * 4 096 .. 2^40). */
-#define GEVWS_TUNE_FUSED_BIG_BYTES 15
 int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
 /* Lanes per connection the last multi-kernel decode's header walk used (1 =
  * not split; GEVWS_TUNE_SPLIT_LANES), -1 for a null context.  The auto choice

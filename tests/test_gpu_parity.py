@@ -830,73 +830,6 @@ def test_copy_helper_copies_and_rejects_unknown_flags(engine):
         engine.copy_(dst, src, n, grid=0x80000000)
 
 
-def _fused_batch(seed=9090):
-    """Mixed sizes: tiny frames, mid frames around a step (8 KiB) and frames of
-    40-300 KB (deferred as pieces at the default threshold), masked and
-    unmasked, odd lengths, empty frames, tails left buffered -- in connections
-    of very different lengths (one of ~700 frames: three rounds of 256)."""
-    rng = np.random.default_rng(seed)
-    streams = []
-    for c in range(48):
-        s = b""
-        nf = int(rng.integers(0, 40)) if c != 5 else 700
-        for _ in range(nf):
-            r = rng.random()
-            L = (int(rng.integers(0, 130)) if r < 0.5 else int(rng.integers(130, 20000)) if r < 0.9
-                 else int(rng.integers(40000, 300000)))
-            s += wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), int(rng.choice([0, 1, 2, 9, 10])),
-                                 bool(rng.random() < 0.8), 0, bool(rng.random() < 0.85),
-                                 bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
-        if rng.random() < 0.5:
-            s += wo.encode_frame(b"x" * 70, 2, True, 0, True, b"\1\2\3\4")[: int(rng.integers(1, 70))]
-        streams.append(s)
-    return pack_streams(streams)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("big", [4096, 32768, 1 << 40])
-def test_fused_record_unmask_path(engine, big):
-    """The fused record + unmask path (unmask variant 3: every batch; variant
-    0 takes it for this mixed batch) with frames deferred as queued pieces at
-    three thresholds (4 KiB: most payload bytes go through the queue; 2^40:
-    none), bit-exact against the C oracle: records, payload + pad bytes,
-    per-connection results."""
-    from gev_amd import _abi
-    arena, conns = _fused_batch()
-    try:
-        engine.set_tuning(_abi.TUNE_FUSED_BIG_BYTES, big)
-        for v in (0, 3):
-            engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, v)
-            for g in (0, 5, 257):
-                engine.set_tuning(_abi.TUNE_UNMASK_GRID, g)
-                assert_matches_oracle(engine, arena, conns, f"variant {v} big {big} grid {g}")
-    finally:
-        engine.set_tuning(_abi.TUNE_FUSED_BIG_BYTES, 32768)
-        engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 0)
-        engine.set_tuning(_abi.TUNE_UNMASK_GRID, 0)
-
-
-@pytest.mark.gpu
-def test_fused_path_rows_without_entries(engine):
-    """Rows the fused path walks header by header (no entry table: walk variant
-    2; an unordered connection table; a row of 6-byte frames with more frames
-    than entry slots), bit-exact against the C oracle."""
-    from gev_amd import _abi
-    arena, conns = _fused_batch(4343)
-    tiny = b"".join(wo.encode_frame(b"", 9, True, 0, True, b"\5\6\7\x08") for _ in range(3000))
-    arena2, conns2 = pack_streams([tiny, wo.encode_frame(b"q" * 50000, 2, True, 0, True, b"\1\1\1\1") + tiny])
-    try:
-        engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 3)
-        assert_matches_oracle(engine, arena2, conns2, "entry slots overflow")
-        rev = conns[::-1].copy()  # unordered table: no entries are used
-        assert_matches_oracle(engine, arena, rev, "unordered")
-        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 2)
-        assert_matches_oracle(engine, arena, conns, "no entry table")
-    finally:
-        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 0)
-        engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 0)
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("L", [3001, 128])
 def test_v3_counter_runs_equal_frames_across_tiles(engine, L):
