@@ -18,6 +18,7 @@
 # pmc   <tag> <ctrs> -- <bench args>  one rocprofv3 --pmc pass (counters comma-separated)
 # py    <args>             python <args>
 # pyprof <tag> <args>      python <args> under rocprofv3 --kernel-trace --stats -> $OUT/prof_<tag>/
+# sh    <command line>     bash -c <command line> (e.g. the loopback binaries)
 # Time limits: STEP_TIMEOUT (default 300 s) per step, 900 s for `test`.
 R=${GRAFT_REPO_ROOT:-$PWD}; OUT=$R/gpurun_out; mkdir -p $OUT; cd $R
 export TMPDIR=/tmp
@@ -67,6 +68,9 @@ PY
         python -u bench.py --no-cpu --copy-reps 0 "$@" > $log 2> $err; rc=$? ;;
     py)
       timeout -k 10 $to python -u "$@" > $log 2> $err; rc=$?
+      tail -c 1500 $log ;;
+    sh)
+      timeout -k 10 $to bash -c "$*" > $log 2> $err; rc=$?
       tail -c 1500 $log ;;
     pyprof)
       tag=$1; shift
