@@ -1205,7 +1205,28 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
 // writing the records and unmasking payloads of up to kSmallLaneBytes itself
 // (all its chunk loads at once), and the workgroup unmasks the larger ones
 // together.  Output identical to the multi-kernel decode.
+// The whole input (<= 64 KiB + the pad) is staged into LDS first, by
+// independent coalesced 16-byte loads, and every header and payload read after
+// that is an LDS read: a live pass's input sits in mapped pinned host memory,
+// where each of the walk's and the record pass's DEPENDENT header loads was a
+// PCIe round trip (the kernel took ~10 us for 100 connections of 1-2 frames,
+// profiles/r05/r05_loopback_timeline.jsonl).
 constexpr uint32_t kSmallLaneBytes = 256;
+constexpr uint32_t kSmallStage = (uint32_t)(kSmallBytes + GEVWS_IN_PAD) / 16;  // 16-byte chunks of staged input
+
+// 16 bytes at byte `off` of the staged input (any alignment: five aligned
+// dword reads and a byte funnel shift)
+__device__ __forceinline__ u32x4 lds16(const uint32_t* __restrict__ s, uint32_t off) {
+  const uint32_t k = off >> 2, e = off & 3;
+  const uint32_t w0 = s[k], w1 = s[k + 1], w2 = s[k + 2], w3 = s[k + 3], w4 = s[k + 4];
+  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, e), __builtin_amdgcn_alignbyte(w2, w1, e),
+               __builtin_amdgcn_alignbyte(w3, w2, e), __builtin_amdgcn_alignbyte(w4, w3, e)};
+}
+__device__ __forceinline__ void lds_window(const uint32_t* __restrict__ s, uint32_t off, uint64_t& lo, uint64_t& hi) {
+  const u32x4 v = lds16(s, off);
+  lo = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+  hi = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+}
 constexpr uint32_t kSmallBig = kSmallBytes / kSmallLaneBytes;  // larger payloads fit in the input at most this often
 
 __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __restrict__ in, uint64_t in_bytes,
@@ -1219,9 +1240,16 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
   __shared__ uint64_t s_big[kSmallBig][3];  // {src_off, payload_off, length} of the larger payloads
   __shared__ uint32_t s_bkey[kSmallBig];
   __shared__ uint32_t s_nbig;
+  __shared__ __attribute__((aligned(16))) uint32_t s_in[4 * kSmallStage + 4];  // the staged input (+ a dword of slack)
   const uint64_t t0 = done ? gpu_ticks() : 0;
   const uint32_t c = threadIdx.x;
   if (c == 0) s_nbig = 0;
+  if (n) {  // bytes [0, 16 x nst) of the input: every read below is inside [0, in_bytes + 48)
+    const uint32_t nst = (uint32_t)((in_bytes + GEVWS_IN_PAD) / 16);
+    u32x4* st = reinterpret_cast<u32x4*>(s_in);
+    for (uint32_t k = c; k < nst; k += kSmallConns) st[k] = ld16u(in + 16ull * k);
+  }
+  __syncthreads();
   gevws_conn_in ci{0, 0};
   uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0, lastf = ~0ull, pos = 0;
   int32_t st = GEVWS_OK;
@@ -1234,10 +1262,9 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
       st = GEVWS_ERR_INVALID;
       err += 1;
     }
-    const uint8_t* s = in + ci.off;
     for (;;) {  // read.go:19-84 + the protocol.go:47 gate, frame after frame
       uint64_t lo, hi;
-      load_window(s + pos, lo, hi);
+      lds_window(s_in, (uint32_t)(ci.off + pos), lo, hi);
       DevHdr h;
       const int r = parse_header(lo, hi, ci.len - pos, h);
       if (r == GEVWS_ERR_LEN_MSB) {
@@ -1283,11 +1310,10 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
     o.status = st;
     cout[c] = o;
     // records + the lane's own payloads
-    const uint8_t* s = in + ci.off;
     uint64_t q = 0, poff = ex[1];
     for (uint64_t k = 0; k < nf; ++k) {
       uint64_t lo, hi;
-      load_window(s + q, lo, hi);
+      lds_window(s_in, (uint32_t)(ci.off + q), lo, hi);
       DevHdr h;
       parse_header(lo, hi, ci.len - q, h);  // succeeded in the walk above
       const uint64_t src = ci.off + q + h.hlen;
@@ -1301,7 +1327,7 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
         u32x4 x[NCH];
 #pragma unroll
         for (int j = 0; j < NCH; ++j)
-          if ((uint32_t)j < nch) x[j] = ld16u(in + src + 16ull * j);
+          if ((uint32_t)j < nch) x[j] = lds16(s_in, (uint32_t)(src + 16ull * j));
 #pragma unroll
         for (int j = 0; j < NCH; ++j)
           if ((uint32_t)j < nch) {
@@ -1327,7 +1353,7 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
     const uint64_t src = s_big[b][0], poff = s_big[b][1], L = s_big[b][2];
     const uint32_t key = s_bkey[b];
     for (uint64_t j = c; 16 * j < L; j += kSmallConns) {
-      u32x4 y = ld16u(in + src + 16 * j) ^ key;
+      u32x4 y = lds16(s_in, (uint32_t)(src + 16 * j)) ^ key;
       const int64_t rem = (int64_t)L - (int64_t)(16 * j);
       if (rem < 16) y = keep_bytes(y, rem);
       *reinterpret_cast<u32x4*>(payload + poff + 16 * j) = y;
