@@ -247,7 +247,7 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int D, int ST = 0, uint32_t RG = kRing>
+template <int D, int ST = 0>
 __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const uint64_t len, bool rec,
                                            const uint64_t ebase, const uint64_t ecap,
                                            WalkEntry* __restrict__ entries, WalkEntry* __restrict__ sink,
@@ -275,8 +275,8 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
         // room for this group in the ring? (the writer is normally far ahead:
         // it copies a group in a few hundred cycles, a step takes ~1 us)
         if ((nf & 3) == 0)
-          while ((uint32_t)nf + 4 - lds_ld(ring.tail) > RG) __builtin_amdgcn_s_sleep(1);
-        ring.e[nf & (RG - 1)] = e;
+          while ((uint32_t)nf + 4 - lds_ld(ring.tail) > kRing) __builtin_amdgcn_s_sleep(1);
+        ring.e[nf & (kRing - 1)] = e;
         __asm__ volatile("" ::: "memory");  // the entry before the head that publishes it (DS ops run in order)
         if ((nf & 3) == 3) lds_st(ring.head, (uint32_t)nf + 1);
       } else {
@@ -409,10 +409,9 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
 // half-line writes among the walk's random line reads cost far more than their
 // bytes (256-byte groups 1.262 ms on C4, 128-byte 1.284, 64-byte 1.345;
 // profiles/r03/r03_compact_entries_ab.jsonl).
-template <uint32_t WG = kWriterGroup, uint32_t RG = kRing>
 __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries, WalkRing ring, uint64_t ebase,
                                                  uint64_t ecap) {
-  static_assert(WG <= kSlotAlign && 2 * WG == RG, "groups aligned by the slot runs; two groups a ring");
+  static_assert(kWriterGroup <= kSlotAlign, "groups aligned by the slot runs");
   uint32_t t = 0;
   bool fin = false;
   for (;;) {
@@ -420,23 +419,23 @@ __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries
       const uint32_t hv = lds_ld(ring.head);
       __asm__ volatile("" ::: "memory");  // the entries after the head that published them
       const uint32_t h = hv & ~kRingDone;
-      while (h - t >= WG) {
-        WalkEntry g[WG];
+      while (h - t >= kWriterGroup) {
+        WalkEntry g[kWriterGroup];
 #pragma unroll
-        for (uint32_t k = 0; k < WG; ++k) g[k] = ring.e[(t + k) & (RG - 1)];
-        if (ebase != ~0ull && t + WG <= ecap) {
+        for (uint32_t k = 0; k < kWriterGroup; ++k) g[k] = ring.e[(t + k) & (kRing - 1)];
+        if (ebase != ~0ull && t + kWriterGroup <= ecap) {
           u32x4* d = reinterpret_cast<u32x4*>(entries + ebase + t);  // 256-byte aligned
 #pragma unroll
-          for (uint32_t k = 0; k < WG / 2; ++k)
+          for (uint32_t k = 0; k < kWriterGroup / 2; ++k)
             d[k] = u32x4{g[2 * k].mask, g[2 * k].w, g[2 * k + 1].mask, g[2 * k + 1].w};
         }
-        t += WG;
+        t += kWriterGroup;
         __asm__ volatile("" ::: "memory");
         lds_st(ring.tail, t);
       }
       if (hv & kRingDone) {
         for (; t < h; ++t)
-          if (ebase != ~0ull && t < ecap) entries[ebase + t] = ring.e[t & (RG - 1)];
+          if (ebase != ~0ull && t < ecap) entries[ebase + t] = ring.e[t & (kRing - 1)];
         fin = true;
       }
     }
@@ -445,126 +444,15 @@ __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries
   }
 }
 
-// The plain chain walk through the writer wave (D 0, ST 2: a batch of many
-// chains of mixed sizes, C4) with a 128-byte window per lane: a header load
-// fetches the 128 bytes from the header on (8 independent 16-byte loads, the
-// header's own line and the next), parks them in the lane's LDS row, and
-// every following header that lies inside the window is parsed from LDS --
-// one memory round trip for each run of frames that fits in 128 bytes
-// instead of one per frame.  The walk is bound by its longest chain's round
-// trips (C4: 1 132 frames); its line traffic hardly changes, since a small
-// frame's successor header sits in the lines its own header load fetched.
-// Entries, counts and results are exactly walk_chain's.
-constexpr uint32_t kWinBytes = 128;
-constexpr uint32_t kWinRowDw = kWinBytes / 4 + 4;       // + a dword read past the last position (never used)
-constexpr uint32_t kWinRing = 32, kWinGroup = 16;        // (LDS: the row leaves room for 128-byte writer groups)
-
-__device__ __forceinline__ void lds_window16(const uint32_t* __restrict__ r, uint32_t x, uint64_t& lo, uint64_t& hi) {
-  const uint32_t k = x >> 2, e = x & 3;
-  const uint32_t w0 = r[k], w1 = r[k + 1], w2 = r[k + 2], w3 = r[k + 3], w4 = r[k + 4];
-  lo = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, e) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, e) << 32);
-  hi = (uint64_t)__builtin_amdgcn_alignbyte(w3, w2, e) | ((uint64_t)__builtin_amdgcn_alignbyte(w4, w3, e) << 32);
-}
-
-__device__ __forceinline__ void walk_chain_win(const uint8_t* __restrict__ s, const uint64_t len, const uint64_t lim,
-                                               bool rec, const uint64_t ecap, WalkRes& R, WalkRing ring,
-                                               uint32_t* __restrict__ row) {
-  uint64_t nf = R.nf, pb = R.pb, pl = R.pl, same = R.same, lastf = R.lastf, firstf = R.firstf, err = R.err;
-  int32_t st = R.st;
-  uint64_t pos = R.pos;
-  u32x4 v[kWinBytes / 16];
-  // 128 bytes from `at` (<= len): chunks past the readable end (lim: the
-  // input arena + GEVWS_IN_PAD) read as zero; the first is always readable
-  auto fetch = [&](uint64_t at) {
-#pragma unroll
-    for (uint32_t k = 0; k < kWinBytes / 16; ++k) {
-      const uint64_t o = at + 16 * k;
-      v[k] = u32x4{0, 0, 0, 0};
-      if (o + 16 <= lim) v[k] = ld16u(s + o);
-    }
-  };
-  uint64_t wb = pos;  // stream offset of the row's first byte
-  bool in_row = false;
-  fetch(pos);
-  for (;;) {
-    uint64_t lo, hi;
-    if (in_row) {
-      lds_window16(row, (uint32_t)(pos - wb), lo, hi);
-    } else {
-#pragma unroll
-      for (uint32_t k = 0; k < kWinBytes / 16; ++k) reinterpret_cast<u32x4*>(row)[k] = v[k];
-      lo = (uint64_t)v[0][0] | ((uint64_t)v[0][1] << 32);
-      hi = (uint64_t)v[0][2] | ((uint64_t)v[0][3] << 32);
-    }
-    // read.go:19-84 + the protocol.go:47 gate (walk_chain's step)
-    const uint32_t b1 = (uint32_t)(lo >> 8) & 0xffu;
-    const uint32_t masked = b1 >> 7, len7 = b1 & 0x7fu;
-    const bool e16 = len7 == 126, e64 = len7 == 127;
-    const uint32_t hlen = 2 + (e64 ? 8u : (e16 ? 2u : 0u)) + 4 * masked;
-    const uint64_t L64 = __builtin_bswap64((lo >> 16) | (hi << 48));
-    const uint64_t L16 = (((lo >> 16) & 0xff) << 8) | ((lo >> 24) & 0xff);
-    const uint64_t L = e64 ? L64 : (e16 ? L16 : (uint64_t)len7);
-    const uint64_t avail = len - pos;
-    const bool have_hdr = avail >= 6 && avail >= hlen;  // read.go:20-23, U1
-    const bool msb = e64 && (L64 >> 63);                 // read.go:71-73
-    if (!have_hdr || msb || avail - hlen < L) {          // protocol.go:47 gate
-      if (have_hdr && msb) {
-        st = GEVWS_ERR_LEN_MSB;
-        err += 1;
-      }
-      break;
-    }
-    const uint64_t next = pos + hlen + L;  // <= len
-    // the next header: in this row, or a new window requested before the entry's LDS work
-    in_row = next + 16 <= wb + kWinBytes;
-    if (!in_row) {
-      wb = next;
-      fetch(next);
-    }
-    const uint32_t key = (e64 ? (uint32_t)(hi >> 16) : (e16 ? (uint32_t)(lo >> 32) : (uint32_t)(lo >> 16))) &
-                         (0u - masked);
-    const uint32_t meta = ((uint32_t)lo & 0xffu) | (masked << 8) | (hlen << 16);
-    rec = rec && nf < ecap;
-    if ((nf & 3) == 0)
-      while ((uint32_t)nf + 4 - lds_ld(ring.tail) > kWinRing) __builtin_amdgcn_s_sleep(1);
-    ring.e[nf & (kWinRing - 1)] = make_entry(key, L, meta);
-    __asm__ volatile("" ::: "memory");  // the entry before the head that publishes it (DS ops run in order)
-    if ((nf & 3) == 3) lds_st(ring.head, (uint32_t)nf + 1);
-    ++nf;
-    pb += round16(L);
-    pl += L;
-    const uint64_t f = (uint64_t)hlen + L;
-    same += f == lastf;
-    firstf = lastf == ~0ull ? f : firstf;
-    lastf = f;
-    pos = next;
-  }
-  R.pos = pos;
-  R.nf = nf;
-  R.pb = pb;
-  R.pl = pl;
-  R.same = same;
-  R.lastf = lastf;
-  R.firstf = firstf;
-  R.err = err;
-  R.st = st;
-  R.rec = rec;
-  __asm__ volatile("" ::: "memory");
-  lds_st(ring.head, (uint32_t)nf | kRingDone);
-}
-
 // 1. The counting walk: one lane per connection (wave 0), and with ST 2 a
 // second wave that writes the walkers' entries.
-template <int D, int ST, int WIN = 0>
+template <int D, int ST>
 __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_walk_count(
     const uint8_t* __restrict__ in, const gevws_conn_in* __restrict__ conns, uint32_t n,
     gevws_conn_out* __restrict__ cout, uint64_t* __restrict__ blk, WalkEntry* __restrict__ entries, uint64_t n_entries,
     uint32_t gshift, uint32_t cpb, uint64_t in_bytes, uint32_t* __restrict__ done, uint64_t max_frames,
     uint64_t payload_cap, gevws_summary* __restrict__ sum) {
-  static_assert(!WIN || (D == 0 && ST == 2), "the windowed walk: plain, through the writer wave");
-  constexpr uint32_t RG = WIN ? kWinRing : kRing, WG = WIN ? kWinGroup : kWriterGroup;
-  __shared__ WalkEntry s_ring[ST == 2 ? kCountBlock * RG : 1];
-  __shared__ __attribute__((aligned(16))) uint32_t s_row[WIN ? kCountBlock * kWinRowDw : 1];
+  __shared__ WalkEntry s_ring[ST == 2 ? kCountBlock * kRing : 1];
   __shared__ uint32_t s_head[ST == 2 ? kCountBlock : 1], s_tail[ST == 2 ? kCountBlock : 1];
   __shared__ uint64_t s_ebase[ST == 2 ? kCountBlock : 1], s_ecap[ST == 2 ? kCountBlock : 1];
   const uint32_t lane = threadIdx.x & 63;
@@ -590,7 +478,7 @@ __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_wal
     }
     rec0 = entry_slots_of(ci, c, n_entries, gshift, ebase, ecap);
   }
-  const WalkRing ring = {s_ring + lane * RG, s_head + lane, s_tail + lane};
+  const WalkRing ring = {s_ring + lane * kRing, s_head + lane, s_tail + lane};
   if constexpr (ST == 2) {
     if (walker) {
       s_head[lane] = active ? 0u : kRingDone;
@@ -599,15 +487,11 @@ __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_wal
       s_ecap[lane] = ecap;
     }
     __syncthreads();
-    if (!walker) walk_ring_writer<WG, RG>(entries, ring, s_ebase[lane], s_ecap[lane]);
+    if (!walker) walk_ring_writer(entries, ring, s_ebase[lane], s_ecap[lane]);
   }
   if (active) {
     WalkRes R = walk_res_fresh(err, st);
-    if constexpr (WIN != 0)
-      walk_chain_win(in + ci.off, ci.len, in_bytes + GEVWS_IN_PAD - ci.off, rec0, ecap, R, ring,
-                     s_row + lane * kWinRowDw);
-    else
-      walk_chain<D, ST>(in + ci.off, ci.len, rec0, ebase, ecap, entries, entries + n_entries + c, R, ring);
+    walk_chain<D, ST>(in + ci.off, ci.len, rec0, ebase, ecap, entries, entries + n_entries + c, R, ring);
     nf = R.nf;
     pb = R.pb;
     pl = R.pl;
@@ -1486,8 +1370,6 @@ const char* const kWalkVariants[] = {
     "one lane per connection, plain chain walk (D = 0)",
     "no entry table (the record pass re-walks every chain)",
     "entries through the writer wave whatever the batch size (the default's path for >= 128 connections per CU)",
-    "windowed plain walk through the writer wave whatever the batch (128-byte LDS window per lane: one load per run "
-    "of frames that fits in it)",
 };
 constexpr int kNumWalkVariants = sizeof(kWalkVariants) / sizeof(kWalkVariants[0]);
 
@@ -1590,7 +1472,7 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   // profiles/r02/r02_walk_store_count_ab.jsonl); after a decode on this context
   // whose frames were mostly NOT the size of their predecessor the plain
   // chain walk (D = 0) runs instead
-  const bool plain = wv == 1 || wv == 4 || (ctx->stats_known && ctx->prev_mixed);
+  const bool plain = wv == 1 || (wv != 1 && ctx->stats_known && ctx->prev_mixed);
   if (nblk && ks > 1) {
 #define GEVWS_SPLIT(K)                                                                                            \
   (plain ? k_walk_split<K, 0> : k_walk_split<K, 8>)<<<nblk, kCountBlock, 0, st>>>(                                \
@@ -1602,11 +1484,10 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
     else if (ks == 16) GEVWS_SPLIT(16);
     else GEVWS_SPLIT(32);
 #undef GEVWS_SPLIT
-  } else if (nblk && (wv == 3 || wv == 4 || (uint64_t)n_conns >= kWriterChainsPerCU * (uint64_t)ncu)) {
+  } else if (nblk && (wv == 3 || (uint64_t)n_conns >= kWriterChainsPerCU * (uint64_t)ncu)) {
     // many chains: the walk is bound by its line traffic -- entries through
     // each lane's LDS ring to the workgroup's writer wave (k_walk_count ST 2)
-    (plain ? (wv == 4 ? k_walk_count<0, 2, 1> : k_walk_count<0, 2>) : k_walk_count<8, 2>)<<<nblk, 2 * kCountBlock, 0,
-                                                                                            st>>>(
+    (plain ? k_walk_count<0, 2> : k_walk_count<8, 2>)<<<nblk, 2 * kCountBlock, 0, st>>>(
         d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes, done, max_frames, payload_cap,
         d_summary);
   } else if (nblk) {

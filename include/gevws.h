@@ -158,9 +158,7 @@ int gevws_ctx_order_after_last(gevws_ctx *ctx, void *stream);
  * GEVWS_TUNE_WALK_VARIANT the header walk (0 = the
  * default choice per batch; 1 = plain chain walk without the uniform-stream
  * speculation; 2 = no per-frame entries, the record pass re-walks every
- * chain; 3 = the entries through the writer wave whatever the batch size;
- * 4 = the plain walk through the writer wave with a 128-byte window per lane
- * whatever the batch),
+ * chain; 3 = the entries through the writer wave whatever the batch size),
  * GEVWS_TUNE_SMALL_BATCH the input size in bytes (default and maximum
  * 65 536; 0 = never) up to which a batch of at most 256 connections is
  * decoded by ONE kernel launch -- walk, scan, records and unmask in a single

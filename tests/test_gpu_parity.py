@@ -668,7 +668,7 @@ def test_walk_variants_uniform_runs(engine):
     arena, conns = pack_streams([random_stream(rng, int(rng.integers(1, 40))) for _ in range(90)])
     cases.append((arena, conns[rng.permutation(conns.shape[0])]))
     walks = engine.variants(_abi.TUNE_WALK_VARIANT)
-    assert walks == [0, 1, 2, 3, 4]
+    assert walks == [0, 1, 2, 3]
     try:
         for v in walks:
             engine.set_tuning(_abi.TUNE_WALK_VARIANT, v)
@@ -706,7 +706,7 @@ def test_record_pass_groups(engine):
         cases.append(pack_streams([b"".join(wo.encode_frame(bytes(20), 2, True, 0, True, b"\1\2\3\4")
                                             for _ in range(nfr)) for _ in range(40)]))
     try:
-        for v in (0, 3, 2, 4):
+        for v in (0, 3, 2):
             engine.set_tuning(_abi.TUNE_WALK_VARIANT, v)
             for k, (arena, conns) in enumerate(cases):
                 assert_matches_oracle(engine, arena, conns, f"walk variant {v} case {k}")
@@ -747,7 +747,7 @@ def test_escaped_entry_lengths(engine):
     streams += [small(int(rng.integers(0, 20))) + fr(bigs[i % 4]) + small(int(rng.integers(0, 90)))
                 for i in range(6)]
     arena, conns = pack_streams(streams)
-    knobs = [(_abi.TUNE_WALK_VARIANT, v) for v in (1, 2, 3, 4)]
+    knobs = [(_abi.TUNE_WALK_VARIANT, v) for v in (1, 2, 3)]
     knobs += [(_abi.TUNE_SPLIT_LANES, k) for k in (2, 4, 16)]
     defaults = {_abi.TUNE_WALK_VARIANT: 0, _abi.TUNE_SPLIT_LANES: 0}
     try:
