@@ -858,3 +858,52 @@ def test_v3_counter_runs_equal_frames_across_tiles(engine, L):
     finally:
         engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 0)
         engine.set_tuning(_abi.TUNE_UNMASK_GRID, 0)
+
+
+def _frames_of_exactly(rng, nbytes: int) -> bytes:
+    """Masked frames of random sizes whose wire bytes add up to exactly nbytes (0 or >= 6)."""
+    out = b""
+    while nbytes:
+        assert nbytes >= 6
+        if nbytes <= 131:                      # one 6-byte-header frame closes it
+            L = nbytes - 6
+        elif nbytes < 140:                     # a 66-byte frame, then one that closes it
+            L = 60
+        else:
+            L = int(rng.integers(0, min(1200, nbytes - 140)))
+        f = wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), int(rng.choice([0, 1, 2, 9, 10])),
+                            True, 0, True, bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+        out += f
+        nbytes -= len(f)
+    return out
+
+
+@pytest.mark.gpu
+def test_one_launch_decode_at_its_limits(engine):
+    """The one-launch decode stages its whole input (<= 64 KiB + the 64-byte
+    pad) in LDS (round 5): batches of exactly 65 536 bytes -- 256 connections
+    ending on the last byte, the last one with a cut frame; one connection of
+    frames and a 5-byte tail; 255 empty connections beside one 65 522-byte
+    payload frame; a 6-byte frame whose header starts 6 bytes before the end
+    -- bit-exact against the C oracle, in one launch and in the multi-kernel
+    path."""
+    from gev_amd import _abi
+    rng = np.random.default_rng(65536)
+    cases = []
+    streams = [random_stream(rng, int(rng.integers(0, 3)), max_len=200, tail=False) for _ in range(255)]
+    last = 65536 - sum(len(s) for s in streams)
+    streams.append(_frames_of_exactly(rng, last + 300)[:last])  # cut inside a frame
+    cases.append(pack_streams(streams))
+    cases.append(pack_streams([_frames_of_exactly(rng, 65531) + b"\x82\x85\x01\x02\x03"]))
+    big = wo.encode_frame(bytes(rng.integers(0, 256, 65522, dtype=np.uint8)), 2, True, 0, True, b"\x0a\x0b\x0c\x0d")
+    assert len(big) == 65536
+    cases.append(pack_streams([b""] * 255 + [big]))
+    cases.append(pack_streams([_frames_of_exactly(rng, 65530) + wo.encode_frame(b"", 9, True, 0, True, b"\1\2\3\4")]))
+    try:
+        for sb in (65536, 0):
+            engine.set_tuning(_abi.TUNE_SMALL_BATCH, sb)
+            for k, (arena, conns) in enumerate(cases):
+                assert len(arena) == 65536 and conns.shape[0] <= 256, k
+                assert_matches_oracle(engine, arena, conns, f"case {k} small_batch {sb}")
+    finally:
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
