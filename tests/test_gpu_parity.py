@@ -870,7 +870,7 @@ def _frames_of_exactly(rng, nbytes: int) -> bytes:
         elif nbytes < 140:                     # a 66-byte frame, then one that closes it
             L = 60
         else:
-            L = int(rng.integers(0, min(1200, nbytes - 140)))
+            L = int(rng.integers(0, min(1200, nbytes - 140) + 1))
         f = wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), int(rng.choice([0, 1, 2, 9, 10])),
                             True, 0, True, bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
         out += f
