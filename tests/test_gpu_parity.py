@@ -883,8 +883,8 @@ def test_one_launch_decode_at_its_limits(engine):
     """The one-launch decode stages its whole input (<= 64 KiB + the 64-byte
     pad) in LDS (round 5): batches of exactly 65 536 bytes -- 256 connections
     ending on the last byte, the last one with a cut frame; one connection of
-    frames and a 5-byte tail; 255 empty connections beside one 65 522-byte
-    payload frame; a 6-byte frame whose header starts 6 bytes before the end
+    frames and a 5-byte tail; 255 empty connections beside one 65 528-byte
+    payload frame (h = 8); a 6-byte frame whose header starts 6 bytes before the end
     -- bit-exact against the C oracle, in one launch and in the multi-kernel
     path."""
     from gev_amd import _abi
@@ -895,7 +895,7 @@ def test_one_launch_decode_at_its_limits(engine):
     streams.append(_frames_of_exactly(rng, last + 300)[:last])  # cut inside a frame
     cases.append(pack_streams(streams))
     cases.append(pack_streams([_frames_of_exactly(rng, 65531) + b"\x82\x85\x01\x02\x03"]))
-    big = wo.encode_frame(bytes(rng.integers(0, 256, 65522, dtype=np.uint8)), 2, True, 0, True, b"\x0a\x0b\x0c\x0d")
+    big = wo.encode_frame(bytes(rng.integers(0, 256, 65528, dtype=np.uint8)), 2, True, 0, True, b"\x0a\x0b\x0c\x0d")
     assert len(big) == 65536
     cases.append(pack_streams([b""] * 255 + [big]))
     cases.append(pack_streams([_frames_of_exactly(rng, 65530) + wo.encode_frame(b"", 9, True, 0, True, b"\1\2\3\4")]))
