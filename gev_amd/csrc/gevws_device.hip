@@ -146,7 +146,6 @@ gevws_ctx* gevws_ctx_create(int device) {
   DeviceGuard g(device);
   gevws_ctx* ctx = new gevws_ctx();
   ctx->device = device;
-  ctx->lazy_last = getenv("GEVWS_EAGER_LAST") == nullptr;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return nullptr;

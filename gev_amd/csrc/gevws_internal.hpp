@@ -53,7 +53,6 @@ struct gevws_ctx {
   hipStream_t last_stream = nullptr;
   bool has_last = false;
   bool last_recorded = false;  // last_done marks the last call (else it is recorded on demand, order_after_last)
-  bool lazy_last = true;       // A/B (env GEVWS_EAGER_LAST=1 at creation: record every call's event)
   int num_cus = 256;
   uint32_t* d_done = nullptr;  // the decode walk's finished-workgroup counter (zero between calls)
 };
@@ -108,7 +107,6 @@ inline int order_after_last(gevws_ctx* ctx, hipStream_t st) {
 
 inline int mark_last(gevws_ctx* ctx, hipStream_t st, bool lazy = false) {
   ctx->last_signal = -1;  // (the one-launch paths set it after this)
-  lazy = lazy && ctx->lazy_last;
   if (!lazy) GEVWS_HIP(hipEventRecord(ctx->last_done, st));
   ctx->last_stream = st;
   ctx->has_last = true;
