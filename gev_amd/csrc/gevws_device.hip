@@ -176,10 +176,7 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   // the last call may have run on another stream (a caller's): its kernels
   // still read the scratch freed below
-  if (ctx->has_last && ctx->last_done) {
-    if (ctx->last_recorded) (void)hipEventSynchronize(ctx->last_done);
-    else (void)hipDeviceSynchronize();  // (its stream may be gone already: no record on it now)
-  }
+  if (ctx->has_last && ctx->last_done) (void)hipEventSynchronize(ctx->last_done);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->d_sum) (void)hipFree(ctx->d_sum);
   if (ctx->d_done) (void)hipFree(ctx->d_done);

@@ -52,7 +52,6 @@ struct gevws_ctx {
   hipEvent_t last_done = nullptr;
   hipStream_t last_stream = nullptr;
   bool has_last = false;
-  bool last_recorded = false;  // last_done marks the last call (else it is recorded on demand, order_after_last)
   int num_cus = 256;
   uint32_t* d_done = nullptr;  // the decode walk's finished-workgroup counter (zero between calls)
 };
@@ -88,29 +87,16 @@ inline hipStream_t pick_stream(gevws_ctx* ctx, void* stream) {
 }
 
 // Orders this call after the context's previous one when the stream changes.
-// The previous call's completion event is recorded lazily for the one-launch
-// paths (mark_last(.., lazy)): a live pass stays on one stream, and an
-// hipEventRecord per pass cost its host ~1-2 us of the launch phase
-// (gevws_protocol_get_timeline); it is recorded here, on the previous
-// call's stream, the first time another stream needs it (then it also
-// covers whatever that stream took since -- a later point, never an earlier).
 inline int order_after_last(gevws_ctx* ctx, hipStream_t st) {
-  if (ctx->has_last && ctx->last_stream != st) {
-    if (!ctx->last_recorded) {
-      GEVWS_HIP(hipEventRecord(ctx->last_done, ctx->last_stream));
-      ctx->last_recorded = true;
-    }
-    GEVWS_HIP(hipStreamWaitEvent(st, ctx->last_done, 0));
-  }
+  if (ctx->has_last && ctx->last_stream != st) GEVWS_HIP(hipStreamWaitEvent(st, ctx->last_done, 0));
   return GEVWS_OK;
 }
 
-inline int mark_last(gevws_ctx* ctx, hipStream_t st, bool lazy = false) {
+inline int mark_last(gevws_ctx* ctx, hipStream_t st) {
   ctx->last_signal = -1;  // (the one-launch paths set it after this)
-  if (!lazy) GEVWS_HIP(hipEventRecord(ctx->last_done, st));
+  GEVWS_HIP(hipEventRecord(ctx->last_done, st));
   ctx->last_stream = st;
   ctx->has_last = true;
-  ctx->last_recorded = !lazy;
   return GEVWS_OK;
 }
 

@@ -1390,7 +1390,7 @@ int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
                                              payload_cap, d_conn_out, d_summary, ctx->done_flag, seq,
                                              ctx->done_flag ? ctx->ticks : nullptr);
   GEVWS_HIP(hipGetLastError());
-  r = mark_last(ctx, st, true);
+  r = mark_last(ctx, st);
   if (ctx->done_flag) ctx->last_signal = seq;
   return r;
 }
