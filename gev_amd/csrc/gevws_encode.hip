@@ -439,7 +439,9 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(U 
       const uint32_t mis = (uint32_t)(reinterpret_cast<uint64_t>(s0) & 15);  // wave-uniform
       const uint32_t lane = fresh_tid() & 63;
       const int nu = (int)nt * 4;
-      u32x4 v[U];
+      u32x4 v[U];  // (zeroed: else carried round the loop, 121 VGPRs instead of 89)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = u32x4{0, 0, 0, 0};
       if (mis != 0) {
         const uint8_t* a = s0 + lane * 16 - mis;
         uint8_t* d = out + B + lane * 16;
@@ -502,18 +504,35 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(U 
 #pragma unroll
       for (int k = 0; k < MW; ++k) s_map[w][lane * MW + k] = 0;
       wave_lds_order();
+      // frame i's wire offset from the step's first one: out_off[fa] (one
+      // scalar load) + fa's wire size + the sizes of frames 1 .. i-1 (a wave
+      // scan; each of frames 1 .. n-2 starts and ends inside the step, so the
+      // sum fits 32 bits) -- no per-frame out_off reads (C4: 0.35 GB a launch)
+      const uint64_t o_fa = uniform64(out_off[fa]);
+      uint64_t w_fa = 0;
+      uint32_t carry = 0;
 #pragma unroll
       for (int k = 0; k < TF / 64; ++k) {
+        if ((uint64_t)(64 * k) >= n) break;  // (wave-uniform)
         const uint32_t i = lane + 64 * k;
-        if (i < n) {
-          const uint64_t f = fa + i;
-          const u64x2* r = reinterpret_cast<const u64x2*>(fr + f);
-          const u64x2 h2 = r[0], p2 = r[1];
-          const uint64_t oo = out_off[f];
-          gevws_header h;
-          memcpy(&h, &h2, 16);
-          uint64_t hlo, hhi;
-          const uint32_t hl = enc_header(h, hlo, hhi);
+        const bool have = i < n;
+        const uint64_t f = fa + (have ? i : 0);
+        const u64x2* r = reinterpret_cast<const u64x2*>(fr + f);
+        const u64x2 h2 = r[0], p2 = r[1];
+        gevws_header h;
+        memcpy(&h, &h2, 16);
+        uint64_t hlo, hhi;
+        const uint32_t hl = enc_header(h, hlo, hhi);
+        const uint64_t wsz = hl + p2[1];
+        if (k == 0)
+          w_fa = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wsz, 0) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wsz >> 32), 0) << 32);
+        const uint32_t w32 = (have && i >= 1 && (uint64_t)i + 1 < n) ? (uint32_t)wsz : 0u;
+        const uint32_t inc = wave_incl_scan32(w32);
+        const uint32_t ex = carry + inc - w32;
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        if (have) {
+          const uint64_t oo = i == 0 ? o_fa : o_fa + w_fa + ex;
           const int64_t st = (int64_t)(oo - B);
           const int64_t end = st + hl + (int64_t)p2[1];  // the next frame's start
           const int32_t stc = st < -64 ? -64 : (int32_t)st;

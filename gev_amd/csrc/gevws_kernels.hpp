@@ -149,6 +149,16 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
   return x;
 }
 
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
 __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
