@@ -68,8 +68,23 @@ static void log_error_text(const char* what, const std::string& text) {
 // results in place (Protocol::kZeroCopyMax).
 constexpr unsigned kHostFlags = hipHostMallocMapped | hipHostMallocCoherent;
 
-// The device address of mapped host memory, or nullptr.
+// The device address of mapped host memory (this file's hipHostMalloc
+// buffers only), or nullptr.  ROCm maps such memory at its host address (one
+// address space): checked once per process on a mapped allocation, after
+// which no runtime lookup is made -- hipHostGetDevicePointer takes the
+// runtime's memory-map lock and a search per call, and a live pass makes
+// 4-11 of them on the loop's critical path (launch phase 5.2-6.5 -> 4.5-4.9
+// us a pass, profiles/r05/r05f_loopback_timeline.jsonl).
 inline void* device_of(void* h) {
+  static const bool same_address = [] {
+    void* p = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&p, 64, kHostFlags) != hipSuccess || !p) return false;
+    const bool same = hipHostGetDevicePointer(&d, p, 0) == hipSuccess && d == p;
+    (void)hipHostFree(p);
+    return same;
+  }();
+  if (same_address) return h;
   void* d = nullptr;
   return hipHostGetDevicePointer(&d, h, 0) == hipSuccess ? d : nullptr;
 }

@@ -20,4 +20,9 @@ for i in 1 2; do
   run c1_cpu "X=1" tools/ws_loopback_cpu --conns 100 --loops 1 --client-threads 2 --msg 128 || exit 1
   run wss_8loops "X=1" gev_amd/ws_loopback --conns 100 --loops 8 --client-threads 4 --mode wsserver || exit 1
   run wss_8loops_cpu "X=1" tools/ws_loopback_cpu --conns 100 --loops 8 --client-threads 4 --mode wsserver || exit 1
+  if [ -n "$BASE" ]; then  # A/B on one box: the same device shapes with the build in $BASE (ws_loopback + its .so)
+    run c1_split_base "GEVWS_LB_SPLIT=64" $BASE/ws_loopback --conns 100 --loops 1 --client-threads 2 --msg 128 || exit 1
+    run c1_one_base "GEVWS_LB_SPLIT=0" $BASE/ws_loopback --conns 100 --loops 1 --client-threads 2 --msg 128 || exit 1
+    run wss_8loops_base "X=1" $BASE/ws_loopback --conns 100 --loops 8 --client-threads 4 --mode wsserver || exit 1
+  fi
 done
