@@ -113,8 +113,10 @@ def test_encode_capacity_error_leaves_wire_sizes(engine, enc_variant):
 
 def _encode_random(engine):
     rng = np.random.default_rng(41)
+    # (4000, 120) / (2500, 250): 64-128 frames in a two-tile step, the second
+    # round of k_encode6's frame-offset scan
     for trial, (n, maxlen) in enumerate([(1, 0), (5, 10), (300, 3000), (3000, 0), (5000, 20), (200, 70000),
-                                         (60, 200000)]):
+                                         (60, 200000), (4000, 120), (2500, 250)]):
         lens = rng.integers(0, maxlen + 1, n)
         payload = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
         offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
