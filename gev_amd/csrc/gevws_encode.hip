@@ -195,16 +195,13 @@ __device__ __forceinline__ u128 byte_mask(int k0, int k1) {
   return hi & ~lo;
 }
 
-// The LDS frame table of an encode window.  LH: the serialised headers are
-// not kept in LDS (h0 / h1 unused) but rebuilt from the frame's record (an L2
-// hit: the window just loaded it), which frees 16 KiB of LDS per workgroup for
-// occupancy -- k_encode; the one-workgroup k_handle_small keeps them in LDS.
+// The LDS table of the replies k_handle_small assembles (one workgroup).
 struct EncWin {
   const int32_t* start;  // wire start relative to the window, clamped >= -64
   const int32_t* pend;   // payload end relative to the window, clamped
   const uint8_t* hlen;
   const uint64_t* delta;  // payload_off - out_off - hlen (mod 2^64)
-  const uint64_t* h0;     // !LH: serialised header bytes 0-7 / 8-15
+  const uint64_t* h0;     // serialised header bytes 0-7 / 8-15
   const uint64_t* h1;
 };
 
@@ -216,10 +213,8 @@ struct EncWin {
 // payload and the header + start of the next: C2 -2.6 %, C5 -1.6 % against one
 // at a time, profiles/r01/r01_encode_ab_asm2_*.json); further frames (frames of a
 // few bytes) continue one by one.
-template <bool LH>
 __device__ __forceinline__ void enc_assemble_from(u128& acc, int32_t rel, uint64_t a, int kmax, uint32_t j, uint32_t F,
-                                                  const EncWin& W, const uint8_t* __restrict__ payload,
-                                                  const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
+                                                  const EncWin& W, const uint8_t* __restrict__ payload) {
   for (; j < F && W.start[j] < rel + kmax; ++j) {
     const int32_t hs = W.start[j];
     const int32_t ps = hs + (int32_t)W.hlen[j];
@@ -228,14 +223,7 @@ __device__ __forceinline__ void enc_assemble_from(u128& acc, int32_t rel, uint64
     const int32_t h0 = hs > rel ? hs : rel;
     const int32_t h1 = ps < rel + kmax ? ps : rel + kmax;
     if (h0 < h1) {
-      u128 H;
-      if constexpr (LH) {
-        uint64_t hl, hh;
-        enc_header(fr[f_lo + j].hdr, hl, hh);
-        H = (u128)hl | ((u128)hh << 64);
-      } else {
-        H = (u128)W.h0[j] | ((u128)W.h1[j] << 64);
-      }
+      const u128 H = (u128)W.h0[j] | ((u128)W.h1[j] << 64);
       acc |= ((H >> (8 * (h0 - hs))) << (8 * (h0 - rel))) & byte_mask(h0 - rel, h1 - rel);
     }
     // payload bytes [max(ps, rel), min(pe, rel + kmax))
@@ -249,57 +237,56 @@ __device__ __forceinline__ void enc_assemble_from(u128& acc, int32_t rel, uint64
   }
 }
 
-template <bool LH>
-__device__ __forceinline__ u32x4 enc_assemble(int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
-                                              const EncWin& W, const uint8_t* __restrict__ payload,
-                                              const gevws_out_frame* __restrict__ fr, uint64_t f_lo) {
-  const int kmax = (a + 16 <= total) ? 16 : (int)(total - a);
+// enc_assemble in two halves, so a caller can have several chunks' payload
+// loads in flight before it combines any (k_handle_small: over PCIe each
+// round of loads is a round trip): enc_prep computes the first two frames'
+// ranges and issues their loads, enc_finish combines them (and walks the rare
+// further frames of a few bytes one by one).
+struct EncPrep {
+  int kmax;
   int32_t hs[2], h0[2], h1[2], p0[2], p1[2];
   u32x4 pv[2];
   u64x2 hv[2];
+};
+
+__device__ __forceinline__ void enc_prep(EncPrep& P, int32_t rel, uint64_t a, uint64_t total, uint32_t lo, uint32_t F,
+                                         const EncWin& W, const uint8_t* __restrict__ payload) {
+  P.kmax = (a + 16 <= total) ? 16 : (int)(total - a);
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const uint32_t j = lo + k;
-    const bool in = j < F && W.start[j < F ? j : lo] < rel + kmax;
+    const bool in = j < F && W.start[j < F ? j : lo] < rel + P.kmax;
     const uint32_t jj = in ? j : lo;
-    hs[k] = W.start[jj];
-    const int32_t ps = hs[k] + (int32_t)W.hlen[jj];
+    P.hs[k] = W.start[jj];
+    const int32_t ps = P.hs[k] + (int32_t)W.hlen[jj];
     const int32_t pe = W.pend[jj];
-    h0[k] = hs[k] > rel ? hs[k] : rel;
-    h1[k] = in ? (ps < rel + kmax ? ps : rel + kmax) : h0[k];
-    p0[k] = ps > rel ? ps : rel;
-    p1[k] = in ? (pe < rel + kmax ? pe : rel + kmax) : p0[k];
-    pv[k] = u32x4{0, 0, 0, 0};
-    hv[k] = u64x2{0, 0};
-    if (p0[k] < p1[k]) pv[k] = ld16u(payload + (a + (uint64_t)(p0[k] - rel) + W.delta[jj]));
-    if (h0[k] < h1[k]) {
-      if constexpr (LH) hv[k] = *reinterpret_cast<const u64x2*>(fr + f_lo + jj);  // the header half of the record
-      else hv[k] = u64x2{W.h0[jj], W.h1[jj]};
-    }
+    P.h0[k] = P.hs[k] > rel ? P.hs[k] : rel;
+    P.h1[k] = in ? (ps < rel + P.kmax ? ps : rel + P.kmax) : P.h0[k];
+    P.p0[k] = ps > rel ? ps : rel;
+    P.p1[k] = in ? (pe < rel + P.kmax ? pe : rel + P.kmax) : P.p0[k];
+    P.pv[k] = u32x4{0, 0, 0, 0};
+    P.hv[k] = u64x2{0, 0};
+    if (P.p0[k] < P.p1[k]) P.pv[k] = ld16u(payload + (a + (uint64_t)(P.p0[k] - rel) + W.delta[jj]));
+    if (P.h0[k] < P.h1[k]) P.hv[k] = u64x2{W.h0[jj], W.h1[jj]};
   }
+}
+
+__device__ __forceinline__ u32x4 enc_finish(const EncPrep& P, int32_t rel, uint64_t a, uint32_t lo, uint32_t F,
+                                            const EncWin& W, const uint8_t* __restrict__ payload) {
   u128 acc = 0;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    if (h0[k] < h1[k]) {
-      u128 H;
-      if constexpr (LH) {
-        gevws_header hd;
-        memcpy(&hd, &hv[k], 16);
-        uint64_t hl, hh;
-        enc_header(hd, hl, hh);
-        H = (u128)hl | ((u128)hh << 64);
-      } else {
-        H = (u128)hv[k][0] | ((u128)hv[k][1] << 64);
-      }
-      acc |= ((H >> (8 * (h0[k] - hs[k]))) << (8 * (h0[k] - rel))) & byte_mask(h0[k] - rel, h1[k] - rel);
+    if (P.h0[k] < P.h1[k]) {
+      const u128 H = (u128)P.hv[k][0] | ((u128)P.hv[k][1] << 64);
+      acc |= ((H >> (8 * (P.h0[k] - P.hs[k]))) << (8 * (P.h0[k] - rel))) & byte_mask(P.h0[k] - rel, P.h1[k] - rel);
     }
-    if (p0[k] < p1[k]) {
-      const int k0 = p0[k] - rel;
-      acc |= (u128_of(pv[k]) << (8 * k0)) & byte_mask(k0, p1[k] - rel);
+    if (P.p0[k] < P.p1[k]) {
+      const int k0 = P.p0[k] - rel;
+      acc |= (u128_of(P.pv[k]) << (8 * k0)) & byte_mask(k0, P.p1[k] - rel);
     }
   }
-  if (lo + 2 < F && W.start[lo + 2] < rel + kmax)  // more frames in these 16 bytes
-    enc_assemble_from<LH>(acc, rel, a, kmax, lo + 2, F, W, payload, fr, f_lo);
+  if (lo + 2 < F && W.start[lo + 2] < rel + P.kmax)  // more frames in these 16 bytes
+    enc_assemble_from(acc, rel, a, P.kmax, lo + 2, F, W, payload);
   return u32x4_of(acc);
 }
 
@@ -869,8 +856,8 @@ __global__ __launch_bounds__(kWalkBlock) void k_disp_emit(const gevws_frame* __r
 // k_disp_emit's dispatch and the encode's size / scan / FrameToBytes for the
 // replies, in one workgroup -- each step's counts by block scans, the replies'
 // wire image assembled 16 bytes per lane from an LDS table of every reply
-// (enc_assemble: headers rebuilt from the records, payloads by unaligned
-// loads).  Outputs and summaries are exactly the two-step chain's (seven
+// (enc_prep / enc_finish: serialised headers from the table, payloads by
+// unaligned loads).  Outputs and summaries are exactly the two-step chain's (seven
 // launches, ~5 us of GPU time each whatever their size).
 constexpr uint64_t kHandleSmallFrames = kEncWinFrames;
 __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* __restrict__ fr, uint64_t max_frames,
@@ -892,13 +879,17 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
   __shared__ uint64_t s_h0[WF], s_h1[WF];
   __shared__ uint32_t s_status;
   const uint32_t tid = threadIdx.x;
+  // the decode's summary and the first kWalkBlock records in flight together
+  // (mapped host memory in a live pass: one round trip instead of three)
+  gevws_frame in0;
+  if (tid < max_frames) in0 = fr[tid];  // (inside the records' capacity; used below only for f < n)
   const uint64_t n = gated_count(max_frames, dec);
   // 1. dispatch counts (k_disp_count + k_scan_blocks)
   uint64_t rep_n = 0, aux_n = 0, shut_n = 0;
   for (uint64_t f0 = 0; f0 < n; f0 += kWalkBlock) {  // workgroup-uniform
     const uint64_t f = f0 + tid;
     uint32_t op = 0;
-    const int k = f < n ? disp_kind(fr[f].hdr, policy, op) : 0;
+    const int k = f < n ? disp_kind((f0 == 0 ? in0 : fr[f]).hdr, policy, op) : 0;
     const uint64_t v[3] = {(uint64_t)(k != 0), (uint64_t)(k == 2), (uint64_t)(k >= 2)};
     uint64_t ex[3], tot[3];
     block_excl_scan<kWalkBlock, 3>(v, ex, tot);
@@ -925,7 +916,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
       int kind = 0;
       gevws_frame in;
       if (f < n) {
-        in = fr[f];
+        in = f0 == 0 ? in0 : fr[f];
         kind = disp_kind(in.hdr, policy, op);
       }
       const uint64_t v[2] = {(uint64_t)(kind != 0), (uint64_t)(kind == 2)};
@@ -989,16 +980,35 @@ __global__ __launch_bounds__(kWalkBlock) void k_handle_small(const gevws_frame* 
   }
   // 4. the wire image, 16 bytes per lane (the last chunk's tail zeroed inside
   // the GEVWS_OUT_PAD slack)
-  for (uint64_t a = (uint64_t)tid * 16; a < wire; a += (uint64_t)kWalkBlock * 16) {
-    const int32_t rel = (int32_t)a;
-    uint32_t lo = 0, hi = (uint32_t)nr - 1;  // the last reply starting at or before a
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      if (s_start[mid] <= rel) lo = mid; else hi = mid - 1;
+  // (kHandleBatch chunks a lane with their payload loads in flight together:
+  // the payloads sit in mapped host memory, a round trip per round of loads)
+  constexpr int kHandleBatch = 4;
+  const EncWin W{s_start, s_pend, s_hlen, s_delta, s_h0, s_h1};
+  for (uint64_t a0 = (uint64_t)tid * 16; a0 < wire; a0 += (uint64_t)kWalkBlock * 16 * kHandleBatch) {
+    EncPrep P[kHandleBatch];
+    uint32_t lo[kHandleBatch];
+#pragma unroll
+    for (int j = 0; j < kHandleBatch; ++j) {
+      const uint64_t a = a0 + (uint64_t)j * kWalkBlock * 16;
+      lo[j] = 0;
+      if (a < wire) {
+        const int32_t rel = (int32_t)a;
+        uint32_t hi = (uint32_t)nr - 1;  // the last reply starting at or before a
+        while (lo[j] < hi) {
+          const uint32_t mid = (lo[j] + hi + 1) >> 1;
+          if (s_start[mid] <= rel) lo[j] = mid; else hi = mid - 1;
+        }
+        enc_prep(P[j], rel, a, wire, lo[j], (uint32_t)nr, W, payload);
+      }
     }
-    const u32x4 x = enc_assemble<false>(rel, a, wire, lo, (uint32_t)nr, EncWin{s_start, s_pend, s_hlen, s_delta, s_h0, s_h1},
-                                        payload, nullptr, 0);
-    __builtin_memcpy(out + a, &x, 16);
+#pragma unroll
+    for (int j = 0; j < kHandleBatch; ++j) {
+      const uint64_t a = a0 + (uint64_t)j * kWalkBlock * 16;
+      if (a < wire) {
+        const u32x4 x = enc_finish(P[j], (int32_t)a, a, lo[j], (uint32_t)nr, W, payload);
+        __builtin_memcpy(out + a, &x, 16);
+      }
+    }
   }
   signal_done(done, seq, ticks, t0, 1);
 }

@@ -1244,18 +1244,38 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
   const uint64_t t0 = done ? gpu_ticks() : 0;
   const uint32_t c = threadIdx.x;
   if (c == 0) s_nbig = 0;
+  gevws_conn_in ci{0, 0}, cprev{0, 0};
+  if (c < n) {  // (in flight with the staging loads)
+    ci = conns[c];
+    if (c > 0) cprev = conns[c - 1];
+  }
   if (n) {  // bytes [0, 16 x nst) of the input: every read below is inside [0, in_bytes + 48)
+    // kSmallBatch loads a thread in flight at once: over PCIe each round of
+    // dependent-in-time loads costs a round trip (~1 us), so a 27 KB pass is
+    // two rounds instead of seven
+    constexpr int kSmallBatch = 8;
     const uint32_t nst = (uint32_t)((in_bytes + GEVWS_IN_PAD) / 16);
     u32x4* st = reinterpret_cast<u32x4*>(s_in);
-    for (uint32_t k = c; k < nst; k += kSmallConns) st[k] = ld16u(in + 16ull * k);
+    for (uint32_t k0 = 0; k0 < nst; k0 += kSmallBatch * kSmallConns) {
+      u32x4 x[kSmallBatch];
+#pragma unroll
+      for (int j = 0; j < kSmallBatch; ++j) {
+        const uint32_t k = k0 + (uint32_t)j * kSmallConns + c;
+        if (k < nst) x[j] = ld16u(in + 16ull * k);
+      }
+#pragma unroll
+      for (int j = 0; j < kSmallBatch; ++j) {
+        const uint32_t k = k0 + (uint32_t)j * kSmallConns + c;
+        if (k < nst) st[k] = x[j];
+      }
+    }
   }
   __syncthreads();
-  gevws_conn_in ci{0, 0};
   uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0, lastf = ~0ull, pos = 0;
   int32_t st = GEVWS_OK;
   if (c < n) {
-    ci = conns[c];
-    if (out_of_order(conns, c, ci)) err = 1ull << 32;  // informational, as k_walk_count
+    if (c > 0 && (ci.off < cprev.off || ci.off - cprev.off < cprev.len))
+      err = 1ull << 32;  // out of order (out_of_order): informational, as k_walk_count
     if (ci.off > in_bytes || ci.len > in_bytes - ci.off) {
       ci.off = 0;
       ci.len = 0;
