@@ -180,6 +180,7 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->d_sum) (void)hipFree(ctx->d_sum);
   if (ctx->d_done) (void)hipFree(ctx->d_done);
+  if (ctx->d_small_stage) (void)hipFree(ctx->d_small_stage);
   if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
   for (auto& set : ctx->evs)

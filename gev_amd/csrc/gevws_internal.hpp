@@ -53,7 +53,9 @@ struct gevws_ctx {
   hipStream_t last_stream = nullptr;
   bool has_last = false;
   int num_cus = 256;
-  uint32_t* d_done = nullptr;  // the decode walk's finished-workgroup counter (zero between calls)
+  uint32_t* d_done = nullptr;  // the decode walk's finished-workgroup counter (zero between calls); [32]: the
+                               // one-launch decode's staging counter
+  uint64_t* d_small_stage = nullptr;  // the one-launch decode's staged input (live passes, k_decode_small)
 };
 
 namespace gevws_impl {

@@ -1228,6 +1228,10 @@ __device__ __forceinline__ void lds_window(const uint32_t* __restrict__ s, uint3
   hi = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
 }
 constexpr uint32_t kSmallBig = kSmallBytes / kSmallLaneBytes;  // larger payloads fit in the input at most this often
+// A live pass's input is read by up to kSmallStageWGs workgroups, a slice of
+// kSmallSliceChunks 16-byte chunks each (2 KiB: one round of loads a thread)
+constexpr uint32_t kSmallStageWGs = 32;
+constexpr uint64_t kSmallSliceChunks = 128;
 
 __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __restrict__ in, uint64_t in_bytes,
                                                               const gevws_conn_in* __restrict__ conns, uint32_t n,
@@ -1236,8 +1240,11 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
                                                               gevws_conn_out* __restrict__ cout,
                                                               gevws_summary* __restrict__ sum,
                                                               uint32_t* __restrict__ done = nullptr,
-                                                              uint32_t seq = 0, uint64_t* __restrict__ ticks = nullptr) {
+                                                              uint32_t seq = 0, uint64_t* __restrict__ ticks = nullptr,
+                                                              uint64_t* __restrict__ stage_buf = nullptr,
+                                                              uint32_t* __restrict__ stage_done = nullptr) {
   __shared__ uint64_t s_big[kSmallBig][3];  // {src_off, payload_off, length} of the larger payloads
+  __shared__ uint32_t s_last;
   __shared__ uint32_t s_bkey[kSmallBig];
   __shared__ uint32_t s_nbig;
   __shared__ __attribute__((aligned(16))) uint32_t s_in[4 * kSmallStage + 4];  // the staged input (+ a dword of slack)
@@ -1250,13 +1257,60 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
     if (c > 0) cprev = conns[c - 1];
   }
   if (n) {  // bytes [0, 16 x nst) of the input: every read below is inside [0, in_bytes + 48)
-    // kSmallBatch loads a thread in flight at once: over PCIe each round of
-    // dependent-in-time loads costs a round trip (~1 us), so a 27 KB pass is
-    // two rounds instead of seven
+    // kSmallBatch loads a thread in flight at once
     constexpr int kSmallBatch = 8;
     const uint32_t nst = (uint32_t)((in_bytes + GEVWS_IN_PAD) / 16);
     u32x4* st = reinterpret_cast<u32x4*>(s_in);
-    for (uint32_t k0 = 0; k0 < nst; k0 += kSmallBatch * kSmallConns) {
+    const uint32_t nwg = gridDim.x;
+    if (nwg > 1) {
+      // A live pass's input sits in mapped host memory, which one workgroup
+      // reads at ~2.5 GB/s (a 20 KB pass: ~8 us of staging).  So every
+      // workgroup copies its slice of the input into stage_buf (agent-scope
+      // write-through stores, as the walk's partials: L2 is per XCD), and the
+      // last one to finish (stage_done) stages the whole input from there
+      // into its LDS and runs the decode; the others end here.
+      const uint32_t per = (nst + nwg - 1) / nwg;
+      const uint32_t k0 = blockIdx.x * per, k1 = k0 + per < nst ? k0 + per : nst;
+      for (uint32_t kb = k0; kb < k1; kb += kSmallBatch * kSmallConns) {
+        u32x4 x[kSmallBatch];
+#pragma unroll
+        for (int j = 0; j < kSmallBatch; ++j) {
+          const uint32_t k = kb + (uint32_t)j * kSmallConns + c;
+          if (k < k1) x[j] = ld16u(in + 16ull * k);
+        }
+#pragma unroll
+        for (int j = 0; j < kSmallBatch; ++j) {
+          const uint32_t k = kb + (uint32_t)j * kSmallConns + c;
+          if (k < k1) {
+            put_partial(stage_buf + 2ull * k, (uint64_t)x[j][0] | ((uint64_t)x[j][1] << 32));
+            put_partial(stage_buf + 2ull * k + 1, (uint64_t)x[j][2] | ((uint64_t)x[j][3] << 32));
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // this workgroup's stores are done before it counts itself
+      __syncthreads();
+      if (c == 0)
+        s_last = __hip_atomic_fetch_add(stage_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1 ? 1u : 0u;
+      __syncthreads();
+      if (!s_last) return;
+      if (c == 0) __hip_atomic_store(stage_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's
+      for (uint32_t kb = 0; kb < nst; kb += kSmallBatch * kSmallConns) {
+        uint64_t lo[kSmallBatch], hi[kSmallBatch];
+#pragma unroll
+        for (int j = 0; j < kSmallBatch; ++j) {
+          const uint32_t k = kb + (uint32_t)j * kSmallConns + c;
+          if (k < nst) {
+            lo[j] = __hip_atomic_load(stage_buf + 2ull * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi[j] = __hip_atomic_load(stage_buf + 2ull * k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kSmallBatch; ++j) {
+          const uint32_t k = kb + (uint32_t)j * kSmallConns + c;
+          if (k < nst) st[k] = u32x4{(uint32_t)lo[j], (uint32_t)(lo[j] >> 32), (uint32_t)hi[j], (uint32_t)(hi[j] >> 32)};
+        }
+      }
+    } else for (uint32_t k0 = 0; k0 < nst; k0 += kSmallBatch * kSmallConns) {
       u32x4 x[kSmallBatch];
 #pragma unroll
       for (int j = 0; j < kSmallBatch; ++j) {
@@ -1406,9 +1460,23 @@ int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   int r = order_after_last(ctx, st);
   if (r != GEVWS_OK) return r;
   const uint32_t seq = ctx->done_flag ? ++ctx->done_seq : 0u;
-  k_decode_small<<<1, kSmallConns, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
-                                             payload_cap, d_conn_out, d_summary, ctx->done_flag, seq,
-                                             ctx->done_flag ? ctx->ticks : nullptr);
+  // a pass that signals a mapped flag is a live pass over mapped host memory:
+  // its input is read by kSmallStageWGs-wide slices (k_decode_small)
+  uint32_t nwg = 1;
+  if (ctx->done_flag && n_conns) {
+    const uint64_t nst = (in_bytes + GEVWS_IN_PAD) / 16;
+    const uint64_t w = (nst + kSmallSliceChunks - 1) / kSmallSliceChunks;
+    nwg = (uint32_t)(w < kSmallStageWGs ? w : kSmallStageWGs);
+    if (nwg > 1 && !ctx->d_small_stage &&
+        hipMalloc(reinterpret_cast<void**>(&ctx->d_small_stage), 16ull * kSmallStage) != hipSuccess) {
+      ctx->d_small_stage = nullptr;
+      nwg = 1;
+    }
+  }
+  k_decode_small<<<nwg, kSmallConns, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
+                                               payload_cap, d_conn_out, d_summary, ctx->done_flag, seq,
+                                               ctx->done_flag ? ctx->ticks : nullptr, ctx->d_small_stage,
+                                               ctx->d_done + 32);
   GEVWS_HIP(hipGetLastError());
   r = mark_last(ctx, st);
   if (ctx->done_flag) ctx->last_signal = seq;

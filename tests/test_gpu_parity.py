@@ -886,7 +886,9 @@ def test_one_launch_decode_at_its_limits(engine):
     frames and a 5-byte tail; 255 empty connections beside one 65 528-byte
     payload frame (h = 8); a 6-byte frame whose header starts 6 bytes before the end
     -- bit-exact against the C oracle, in one launch and in the multi-kernel
-    path."""
+    path; the one launch also with a completion flag set, which stages the
+    input through 32 workgroups' slices (a live pass's form)."""
+    import torch
     from gev_amd import _abi
     rng = np.random.default_rng(65536)
     cases = []
@@ -899,11 +901,18 @@ def test_one_launch_decode_at_its_limits(engine):
     assert len(big) == 65536
     cases.append(pack_streams([b""] * 255 + [big]))
     cases.append(pack_streams([_frames_of_exactly(rng, 65530) + wo.encode_frame(b"", 9, True, 0, True, b"\1\2\3\4")]))
+    flag = gev_amd.PinnedArena(4096)
     try:
-        for sb in (65536, 0):
+        for sb, flagged in ((65536, False), (65536, True), (0, False)):
             engine.set_tuning(_abi.TUNE_SMALL_BATCH, sb)
+            engine.set_completion_flag(flag if flagged else None, 64)
             for k, (arena, conns) in enumerate(cases):
                 assert len(arena) == 65536 and conns.shape[0] <= 256, k
-                assert_matches_oracle(engine, arena, conns, f"case {k} small_batch {sb}")
+                assert_matches_oracle(engine, arena, conns, f"case {k} small_batch {sb} flagged {flagged}")
+                if flagged:
+                    assert engine.completion_seq > 0
     finally:
         engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+        engine.set_completion_flag(None)
+        torch.cuda.synchronize()
+        flag.close()
