@@ -317,6 +317,8 @@ def main():
                          "against the copy rate in the same clock state (0 = skip)")
     ap.add_argument("--walk-variant", type=int, default=None, help="A/B: header walk variant (GEVWS_TUNE_WALK_VARIANT)")
     ap.add_argument("--unmask-variant", type=int, default=None, help="A/B: unmask kernel variant")
+    ap.add_argument("--unmask-grid", type=int, default=None,
+                    help="A/B: cap the unmask's workgroups (GEVWS_TUNE_UNMASK_GRID; leaves CU slots for a batch in flight)")
     ap.add_argument("--split-lanes", type=int, default=None,
                     help="A/B: split header walk lanes per connection (GEVWS_TUNE_SPLIT_LANES; 0 = auto, 1 = off)")
     ap.add_argument("--emulate-shard", default=None, metavar="R/N",
@@ -363,6 +365,8 @@ def main():
             e.set_tuning(_abi.TUNE_UNMASK_VARIANT, args.unmask_variant)
         if args.split_lanes is not None:
             e.set_tuning(_abi.TUNE_SPLIT_LANES, args.split_lanes)
+        if args.unmask_grid is not None:
+            e.set_tuning(_abi.TUNE_UNMASK_GRID, args.unmask_grid)
     t_setup = time.time()
     scaling = args.scaling or ("strong" if args.config == "c4" else "weak")
     emulated = None
@@ -405,7 +409,9 @@ def main():
     sel = torch.tensor([0, 2, 3], dtype=torch.int64, device=dev)
     sum64 = out.summary.view(torch.int64)
     outs = [out] + [e.alloc_batch(lay.n_conns, max_frames, cap) for e in engs[1:]]
-    streams = [None] if M == 1 else [torch.cuda.Stream(dev) for _ in range(M)]
+    # (alternate priorities: torch's pool maps same-priority streams onto one
+    # hardware queue here, which serialises the batches in flight)
+    streams = [None] if M == 1 else [torch.cuda.Stream(dev, priority=-(k % 2)) for k in range(M)]
     main_stream = torch.cuda.current_stream()
     n_step = [0]
 
@@ -531,7 +537,7 @@ def main():
     # (the committed counts describe the default kernels on the full batch)
     traffic, traffic_src = (load_traffic(args.config)
                             if (scaling == "weak" or world == 1) and not emulated and not args.unmask_variant
-                            and not args.walk_variant else (None, None))
+                            and not args.walk_variant and not args.unmask_grid else (None, None))
     result = {
         "metric": METRIC,
         "value": round(value, 3),

@@ -212,23 +212,25 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 // SPLIT (decode): field 3 holds errors in its low 32 bits and the count of
 // out-of-order connections in its high 32 (k_walk_count) -> summary.errors and
 // GEVWS_SUMMARY_UNORDERED.
-template <bool SPLIT, int NF = kBlkFields>
-__global__ __launch_bounds__(kScanBlock) void k_scan_blocks(uint64_t* __restrict__ blk, uint32_t nblk,
-                                                            uint64_t max_frames, uint64_t payload_cap,
-                                                            gevws_summary* __restrict__ sum) {
+// BS: the workgroup (the decode's scan runs 256 threads: a workgroup of 4
+// waves finds room on a CU beside another batch's unmask, 16 waves do not).
+template <bool SPLIT, int NF = kBlkFields, int BS = kScanBlock>
+__global__ __launch_bounds__(BS) void k_scan_blocks(uint64_t* __restrict__ blk, uint32_t nblk,
+                                                    uint64_t max_frames, uint64_t payload_cap,
+                                                    gevws_summary* __restrict__ sum) {
   // kScanPer consecutive partials per thread: a batch of per-frame blocks
   // (encode / dispatch of 43.8 M frames: 171 K partials) takes a few rounds of
   // the workgroup instead of one round per 1 024 partials
   constexpr int kScanPer = 8;
   uint64_t carry[NF] = {};
-  for (uint64_t base = 0; base < nblk; base += (uint64_t)kScanBlock * kScanPer) {
+  for (uint64_t base = 0; base < nblk; base += (uint64_t)BS * kScanPer) {
     const uint64_t i0 = base + (uint64_t)threadIdx.x * kScanPer;
     uint64_t loc[NF] = {}, ex[NF], tot[NF];
 #pragma unroll
     for (int r = 0; r < kScanPer; ++r)
 #pragma unroll
       for (int k = 0; k < NF; ++k) loc[k] += (i0 + r < nblk) ? blk[(i0 + r) * NF + k] : 0;
-    block_excl_scan<kScanBlock, NF>(loc, ex, tot);
+    block_excl_scan<BS, NF>(loc, ex, tot);
     // fields 0/1 become exclusive bases (frames, arena bytes)
     uint64_t b0 = carry[0] + ex[0], b1 = carry[1] + ex[1];
 #pragma unroll

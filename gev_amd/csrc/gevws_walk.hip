@@ -1554,6 +1554,7 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   // coherent partials it was slower: C1-shaped walk 0.034 -> 0.074 ms,
   // profiles/r02/r02_steps_fused.jsonl).
   const bool fused = nblk > 0 && nblk <= kFusedScanMaxBlocks;
+  constexpr int kDecScanBlock = 256;
   uint32_t* done = fused ? ctx->d_done : nullptr;
   // the walk's uniform-stream speculation (D = 8) pays on long runs of equal
   // frames (C2, C3: -23..-28 %) and costs 2-7 % elsewhere (C1, C4,
@@ -1584,7 +1585,8 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
         d_summary);
   }
   if (ev) GEVWS_HIP(hipEventRecord(ev[1], st));
-  if (!fused) k_scan_blocks<true, kDecFields><<<1, kScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap, d_summary);
+  if (!fused) k_scan_blocks<true, kDecFields, kDecScanBlock><<<1, kDecScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap,
+                                                                                         d_summary);
   if (ev) GEVWS_HIP(hipEventRecord(ev[2], st));
   if (nblk) {
     k_walk_bases<<<nblk, kCountBlock, 0, st>>>(n_conns, d_conn_out, blk, d_summary, rec_flags, cpb_w, ctx->d_stats,
