@@ -53,8 +53,8 @@ struct gevws_ctx {
   hipStream_t last_stream = nullptr;
   bool has_last = false;
   int num_cus = 256;
-  uint32_t* d_done = nullptr;  // the decode walk's finished-workgroup counter (zero between calls); [32]: the
-                               // one-launch decode's staging counter
+  uint32_t* d_done = nullptr;  // 256 B: the decode walk's finished-workgroup counter ([0], zero between calls)
+                               // and the one-launch decode's staging counter ([kSmallStageCounter])
   uint64_t* d_small_stage = nullptr;  // the one-launch decode's staged input (live passes, k_decode_small)
 };
 

@@ -1232,6 +1232,9 @@ constexpr uint32_t kSmallBig = kSmallBytes / kSmallLaneBytes;  // larger payload
 // kSmallSliceChunks 16-byte chunks each (2 KiB: one round of loads a thread)
 constexpr uint32_t kSmallStageWGs = 32;
 constexpr uint64_t kSmallSliceChunks = 128;
+// their finished-workgroup counter: a word of ctx->d_done of its own (the
+// walk's is d_done[0]), 128 bytes apart
+constexpr uint32_t kSmallStageCounter = 32;
 
 __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __restrict__ in, uint64_t in_bytes,
                                                               const gevws_conn_in* __restrict__ conns, uint32_t n,
@@ -1476,7 +1479,7 @@ int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   k_decode_small<<<nwg, kSmallConns, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
                                                payload_cap, d_conn_out, d_summary, ctx->done_flag, seq,
                                                ctx->done_flag ? ctx->ticks : nullptr, ctx->d_small_stage,
-                                               ctx->d_done + 32);
+                                               ctx->d_done + kSmallStageCounter);
   GEVWS_HIP(hipGetLastError());
   r = mark_last(ctx, st);
   if (ctx->done_flag) ctx->last_signal = seq;
