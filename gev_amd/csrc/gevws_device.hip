@@ -5,6 +5,8 @@
 // gevws_walk.hip (header walk, records), gevws_unmask.hip (payload unmask)
 // and gevws_encode.hip (encode, control-frame dispatch); gevws_kernels.hpp
 // holds what they share.
+#include <atomic>
+
 #include "gevws_internal.hpp"
 
 namespace {
@@ -137,6 +139,27 @@ int gevws_device_count(void) {
   return n;
 }
 
+// The priority of the n-th context's stream on a device: 0, -1, 1, -2, 2, ...
+// inside the device's range.  The HIP runtime gives each priority level its
+// own hardware queues, and same-priority streams share that level's few (3 of
+// the default GPU_MAX_HW_QUEUES = 4 on the box): eight event loops' contexts
+// at one priority ran at most 3 loops' kernels at once, cycling the levels
+// runs all 8 (tools/queue_probe.hip, profiles/r05/r05u_queue_probe.jsonl).
+static int ctx_stream_priority(int device) {
+  static std::atomic<uint32_t> seq[64];
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest) return 0;
+  const uint32_t span = (uint32_t)(least - greatest + 1);
+  const uint32_t k = seq[device & 63].fetch_add(1, std::memory_order_relaxed) % span;
+  int p = 0;  // walk 0, -1, 1, -2, 2, ... keeping the first k levels that fall inside [greatest, least]
+  for (uint32_t taken = 0, i = 1;; ++i) {
+    if (taken == k) break;
+    const int c = (i & 1) ? -(int)((i + 1) / 2) : (int)(i / 2);
+    if (c >= greatest && c <= least && ++taken == k) p = c;
+  }
+  return p;
+}
+
 gevws_ctx* gevws_ctx_create(int device) {
   int n = gevws_device_count();
   if (device < 0 || device >= n) {
@@ -146,7 +169,7 @@ gevws_ctx* gevws_ctx_create(int device) {
   DeviceGuard g(device);
   gevws_ctx* ctx = new gevws_ctx();
   ctx->device = device;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, ctx_stream_priority(device)) != hipSuccess) {
     delete ctx;
     return nullptr;
   }

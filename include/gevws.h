@@ -130,7 +130,10 @@ const char *gevws_status_string(int status);
 int gevws_device_count(void);
 
 /* One context per event loop (the reference keeps one per-connection header
- * scratch, protocol.go:37; the batch engine keeps its scratch per loop). */
+ * scratch, protocol.go:37; the batch engine keeps its scratch per loop).
+ * Successive contexts on a device cycle their stream's priority over the
+ * device's range (0, -1, 1, ...): each priority level has its own hardware
+ * queues, so several loops' passes run side by side. */
 gevws_ctx *gevws_ctx_create(int device);
 void gevws_ctx_destroy(gevws_ctx *ctx);
 int gevws_ctx_device(const gevws_ctx *ctx);

@@ -18,6 +18,10 @@ base_runs() {  # A/B on one box: the same device shapes with the build in $BASE 
   run c1_split_base "GEVWS_LB_SPLIT=64" $BASE/ws_loopback --conns 100 --loops 1 --client-threads 2 --msg 128 || return 1
   run c1_one_base "GEVWS_LB_SPLIT=0" $BASE/ws_loopback --conns 100 --loops 1 --client-threads 2 --msg 128 || return 1
   run wss_8loops_base "X=1" $BASE/ws_loopback --conns 100 --loops 8 --client-threads 4 --mode wsserver || return 1
+  if [ -n "$BASE_QUEUES" ]; then  # the base build with more hardware queues per process
+    run wss_8loops_base_q$BASE_QUEUES "GPU_MAX_HW_QUEUES=$BASE_QUEUES" $BASE/ws_loopback --conns 100 --loops 8 \
+      --client-threads 4 --mode wsserver || return 1
+  fi
 }
 for i in 1 2; do
   if [ -n "$BASE" ] && [ -n "$BASE_FIRST" ]; then base_runs || exit 1; fi

@@ -625,3 +625,28 @@ def test_pass_timeline_small_zero_copy_pass(engine):
         assert t[k] > 0, (k, t)
     assert t["ns_gpu_decode"] < t["ns_wait"] < 3 * 10**9, t  # the kernel ran inside the wait
     assert t["ns_gpu_handler"] == 0 and t["ns_gpu_gap"] == 0
+
+
+def test_contexts_cycle_stream_priorities():
+    """One context per event loop: successive contexts on a device cycle their
+    stream's priority over the device's range (each level has its own hardware
+    queues, so eight loops' passes run side by side instead of three at a time,
+    profiles/r05/r05u_queue_probe.jsonl), and each still decodes exactly."""
+    import torch
+
+    least, greatest = torch.cuda.Stream.priority_range()
+    engines = [gev_amd.Engine(0) for _ in range(least - greatest + 1)]
+    prios = [torch.cuda.ExternalStream(int(gev_amd.lib.gevws_ctx_stream(e._ctx)), device="cuda:0").priority
+             for e in engines]
+    assert len(set(prios)) == len(engines), prios
+    rng = np.random.default_rng(9)
+    for e in engines:
+        proto = gev_amd.Protocol(e)
+        c, r = gev_amd.Connection(), gev_amd.RingBuffer(4096)
+        frames = _client_frames(rng, 5)
+        r.write(b"".join(w for _, w in frames))
+        assert proto.unpacket_batch([c], [r]) == 5
+        for data, _ in frames:
+            assert proto.unpacket(c, r)[1] == data
+        proto.close()  # before its engine (Protocol.close)
+        e.close()
