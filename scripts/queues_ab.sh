@@ -2,7 +2,7 @@
 # once (profiles/r05/r05aa_queues_ab.jsonl) for a server build that called
 # setenv("GPU_MAX_HW_QUEUES", "16") in main -- which the HIP runtime, loaded
 # before main, ignored, so those runs are an A/A of two equal builds --
-# beside the CPU twin; beside the CPU twin; a warm-up run, then ROUNDS (default 4)
+# beside the CPU twin; a warm-up run, then ROUNDS (default 4)
 # alternating rounds whose order flips.  Lines -> gpurun_out/${TAG}_queues_ab.jsonl
 R=${GRAFT_REPO_ROOT:-$PWD}; cd $R; mkdir -p gpurun_out
 export GEV_LOG_LEVEL=FATAL
