@@ -409,8 +409,10 @@ def main():
     sel = torch.tensor([0, 2, 3], dtype=torch.int64, device=dev)
     sum64 = out.summary.view(torch.int64)
     outs = [out] + [e.alloc_batch(lay.n_conns, max_frames, cap) for e in engs[1:]]
-    # (alternate priorities: torch's pool maps same-priority streams onto one
-    # hardware queue here, which serialises the batches in flight)
+    # (alternate priorities: each priority level has its own hardware queues,
+    # while same-priority streams share their level's 3 -- tools/queue_probe.hip
+    # -- and two of torch's pool streams landed on one here, which serialised
+    # the batches in flight)
     streams = [None] if M == 1 else [torch.cuda.Stream(dev, priority=-(k % 2)) for k in range(M)]
     main_stream = torch.cuda.current_stream()
     n_step = [0]
