@@ -7,7 +7,9 @@ garbage tails -- through the one-launch path and, with it turned off
 (GEVWS_TUNE_SMALL_BATCH = 0), the multi-kernel path; and the device
 ws.Cipher (cipher.go:14-53) equals the bytewise one at any offset and
 alignment; the device encode (FrameToBytes) equals the C oracle's on
-generated records.  Stream strategies: tests/test_properties.py."""
+generated records; the device handler step (dispatch + encode of the
+replies) equals oracle/ws_oracle.on_message on generated control-heavy
+streams.  Stream strategies: tests/test_properties.py."""
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -91,3 +93,58 @@ def test_device_encode_equals_oracle(engine, case):
     want, woff = ref.encode_batch(fr, payload)
     assert np.array_equal(wire.cpu().numpy(), want)
     assert np.array_equal(off, woff)
+
+
+@st.composite
+def client_frame(draw):
+    """A client frame the handler step answers or ignores: text (any bytes,
+    valid UTF-8 or not), binary, continuation, ping / pong, close with no
+    body, one byte, or any 16-bit code plus any reason, reserved opcodes."""
+    kind = draw(st.sampled_from(["data", "ping", "close", "other"]))
+    key = draw(st.binary(min_size=4, max_size=4))
+    masked = draw(st.booleans())
+    if kind == "data":
+        op = draw(st.sampled_from([wo.OP_TEXT, wo.OP_BINARY, 0]))
+        body = draw(st.one_of(st.binary(max_size=300), st.text(max_size=80).map(lambda t: t.encode())))
+        return wo.encode_frame(body, op, draw(st.booleans()), 0, masked, key)
+    if kind == "ping":
+        return wo.encode_frame(draw(st.binary(max_size=125)), draw(st.sampled_from([0x9, 0xA])), True, 0, masked, key)
+    if kind == "close":
+        body = draw(st.one_of(st.just(b""), st.binary(min_size=1, max_size=1),
+                              st.builds(lambda c, r: c.to_bytes(2, "big") + r, st.integers(0, 65535),
+                                        st.one_of(st.binary(max_size=60), st.text(max_size=30).map(lambda t: t.encode())))))
+        return wo.encode_frame(body[:125], wo.OP_CLOSE, True, 0, masked, key)
+    return wo.encode_frame(draw(st.binary(max_size=20)), draw(st.sampled_from([0x3, 0x7, 0xB, 0xF])), True, 0,
+                           masked, key)
+
+
+@settings(max_examples=150, deadline=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(st.lists(st.lists(client_frame(), min_size=1, max_size=12), min_size=1, max_size=6),
+       st.sampled_from([_abi.HANDLER_NONE, _abi.HANDLER_ECHO_BINARY, _abi.HANDLER_ECHO_TEXT]))
+def test_device_dispatch_equals_oracle(engine, conns_frames, policy):
+    """HandlerWrap.OnMessage + util.HandleClose / HandlePing / HandlePong
+    (wrap.go:38-90, util.go:27-85) on the device, then FrameToBytes of the
+    replies: wire bytes, reply map and the shutdown count equal
+    oracle/ws_oracle.on_message's over the decoded frames."""
+    import torch
+    streams = [b"".join(fs) for fs in conns_frames]
+    arena, conns = pack_streams(streams)
+    dev = torch.device("cuda", engine.device)
+    d_in = torch.zeros(len(arena) + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    d_in[: len(arena)] = torch.from_numpy(np.frombuffer(arena, np.uint8).copy()).to(dev)
+    nf = sum(len(fs) for fs in conns_frames)
+    out = engine.decode(d_in, len(arena), torch.from_numpy(conns.copy()).to(dev), conns.shape[0], aux_slots=nf + 1)
+    wire, reply_of, ds = engine.serve(out, policy)
+    want, shut, reps, k = b"", 0, [], 0
+    for s in streams:
+        for fr in wo.decode_stream(s).frames:
+            r, sd = wo.on_message(fr.header, fr.payload, policy)
+            shut += sd
+            reps.append(-1 if r is None else k)
+            if r is not None:
+                want += r
+                k += 1
+    assert int(ds["errors"]) == shut and int(ds["frames"]) == k
+    assert list(reply_of) == reps
+    assert wire.cpu().numpy().tobytes() == want
