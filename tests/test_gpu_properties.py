@@ -9,7 +9,8 @@ ws.Cipher (cipher.go:14-53) equals the bytewise one at any offset and
 alignment; the device encode (FrameToBytes) equals the C oracle's on
 generated records; the device handler step (dispatch + encode of the
 replies) equals oracle/ws_oracle.on_message on generated control-heavy
-streams.  Stream strategies: tests/test_properties.py."""
+streams; the host Protocol over ring buffers fed in arbitrary chunks hands
+every connection the oracle's frames and keeps its incomplete tail.  Stream strategies: tests/test_properties.py."""
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -19,7 +20,7 @@ import gev_amd
 from gev_amd import _abi
 from oracle import ws_oracle as wo
 from tests._helpers import assert_matches_oracle, pack_streams
-from tests.test_properties import streams
+from tests.test_properties import frame, streams
 
 pytestmark = pytest.mark.gpu
 
@@ -148,3 +149,46 @@ def test_device_dispatch_equals_oracle(engine, conns_frames, policy):
     assert int(ds["errors"]) == shut and int(ds["frames"]) == k
     assert list(reply_of) == reps
     assert wire.cpu().numpy().tobytes() == want
+
+
+@settings(max_examples=100, deadline=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture,
+                                 HealthCheck.data_too_large])
+@given(st.lists(st.tuples(st.lists(frame(), min_size=1, max_size=8), st.integers(0, 13)), min_size=1, max_size=4),
+       st.sampled_from([0, 1 << 30]), st.data())
+def test_protocol_over_rings_equals_oracle(engine, conns_frames, zero_copy_max, data):
+    """The host mirror of websocket.Protocol (protocol.go:38-62, driven as
+    connection.go:208-251 drives it) over ring buffers fed in arbitrary
+    chunks, with batched passes between reads: every connection gets exactly
+    the oracle's frames in order, and the bytes of its trailing incomplete
+    frame stay in its ring (the completeness gate and the carry)."""
+    proto = gev_amd.Protocol(engine)
+    proto.set_zero_copy_max(zero_copy_max)
+    try:
+        n = len(conns_frames)
+        conns = [gev_amd.Connection(upgraded=True) for _ in range(n)]
+        rings = [gev_amd.RingBuffer(data.draw(st.sampled_from([16, 4096]))) for _ in range(n)]
+        wires = [b"".join(fs) + b"".join(fs)[:cut] for fs, cut in conns_frames]  # + a cut-off frame prefix
+        want = [wo.decode_stream(w).frames for w in wires]
+        got = [[] for _ in range(n)]
+        pos = [0] * n
+        while any(pos[i] < len(wires[i]) for i in range(n)):
+            for i in range(n):
+                k = data.draw(st.integers(1, 400))
+                chunk = wires[i][pos[i]:pos[i] + k]
+                pos[i] += len(chunk)
+                if chunk:
+                    rings[i].write(chunk)
+            if data.draw(st.booleans()):
+                proto.unpacket_batch(conns, rings)
+            for i in range(n):
+                while True:
+                    h, d = proto.unpacket(conns[i], rings[i])
+                    if h is None:
+                        break
+                    got[i].append((bytes(h), d))
+        for i in range(n):
+            assert [g for g in got[i]] == [(f.header.pack(), f.payload) for f in want[i]], i
+            assert rings[i].length() == len(wires[i]) - sum(f.header_len + f.header.length for f in want[i]), i
+    finally:
+        proto.close()
