@@ -7,13 +7,16 @@ stream:
   identically: frames, payloads, consumed bytes, status (read.go:19-84,
   protocol.go:38-62, connection.go:208-218);
 * the completeness gate (protocol.go:47 + the ringbuffer contract, §8a a7): a
-  prefix of a stream decodes to a prefix of its frames, and every frame whose
-  h + L bytes lie inside the prefix is emitted;
+  prefix of a stream decodes to a prefix of its frames, and the leading frames
+  whose h + L bytes lie inside the prefix, each starting >= 6 bytes before its
+  end (read.go:20-23), are emitted;
 * the product library's host exports (the boundary's per-frame calls, §8b
   items 1-2): gevws_parse_header_ring over a ring wrapped at any point equals
   the oracle's read_header of the joined bytes, and gevws_cipher equals the
   bytewise ws.Cipher at any offset;
-* the host ring the per-frame path reads from behaves as a byte queue.
+* the host ring the per-frame path reads from behaves as a byte queue;
+* the host HTTP upgrade (handshake.cpp) equals oracle/ws_handshake.py on
+  generated requests.
 Streams mix every length class (7-bit, 16-bit and 64-bit, minimal or not),
 any RSV / opcode, masked and unmasked frames and a garbage tail."""
 import ctypes
@@ -78,13 +81,17 @@ def test_prefix_decodes_to_a_prefix_of_the_frames(s, data):
     assert len(part.frames) <= len(full.frames)
     for a, b in zip(part.frames, full.frames):
         assert a.header.pack() == b.header.pack() and a.payload == b.payload
-    # every frame of the full decode that ends inside the prefix is emitted
-    # (unless the prefix's own parse stopped on an error first)
-    end, inside = 0, 0
+    # the leading frames of the full decode that end inside the prefix AND
+    # start at least 6 bytes before its end are emitted (read.go:20-23: any
+    # header needs 6 readable bytes, even a 2-byte empty frame; Appendix A P1),
+    # unless the prefix's own parse stopped on an error first
+    start, inside = 0, 0
     for fr in full.frames:
-        end += fr.header_len + fr.header.length
-        if end <= cut:
-            inside += 1
+        end = start + fr.header_len + fr.header.length
+        if end > cut or cut - start < 6:
+            break
+        inside += 1
+        start = end
     if part.status == wo.OK:
         assert len(part.frames) == inside
 
@@ -142,3 +149,26 @@ def test_ring_matches_a_byte_queue(size, ops):
         assert a + b == bytes(model)
         assert r.length() == len(model) <= r.capacity()
         assert r.is_empty() == (not model)
+
+
+_hdr_names = st.sampled_from([b"Host", b"Upgrade", b"Connection", b"Sec-WebSocket-Version", b"Sec-WebSocket-Key",
+                              b"Sec-WebSocket-Protocol", b"Sec-WebSocket-Extensions", b"Origin", b"X"])
+_hdr_values = st.one_of(st.sampled_from([b"websocket", b"Upgrade", b"13", b"dGhlIHNhbXBsZSBub25jZQ==", b"chat, superchat",
+                                         b"permessage-deflate; client_max_window_bits", b""]),
+                        st.binary(max_size=40).filter(lambda v: b"\r" not in v and b"\n" not in v))
+
+
+@SETTINGS
+@given(st.lists(st.tuples(_hdr_names, st.sampled_from([b": ", b":", b" :\t"]), _hdr_values), max_size=9),
+       st.sampled_from([b"GET", b"PUT", b"get"]), st.sampled_from([b"HTTP/1.1", b"HTTP/1.0", b"HTTP/2.0", b"HTTP/1.1x"]),
+       st.binary(max_size=8), st.data())
+def test_handshake_equals_oracle(lines, method, proto, tail, data):
+    """Upgrader.Upgrade (ws.go:158-343) in the host C++ (handshake.cpp) equals
+    oracle/ws_handshake.py byte for byte -- response, status, reason, chosen
+    protocol / extensions and bytes consumed -- on generated requests (header
+    names in any order, separators, values of arbitrary bytes), with the
+    request wrapped round the ring at any point."""
+    from tests.test_handshake import _both
+    req = method + b" / " + proto + b"\r\n" + b"".join(k + s + v + b"\r\n" for k, s, v in lines) + b"\r\n"
+    wrap = data.draw(st.one_of(st.none(), st.integers(1, len(req) + len(tail) - 1)))
+    _both(req + tail, wrap_at=wrap)
