@@ -10,7 +10,9 @@ alignment; the device encode (FrameToBytes) equals the C oracle's on
 generated records; the device handler step (dispatch + encode of the
 replies) equals oracle/ws_oracle.on_message on generated control-heavy
 streams; the host Protocol over ring buffers fed in arbitrary chunks hands
-every connection the oracle's frames and keeps its incomplete tail.  Stream strategies: tests/test_properties.py."""
+every connection the oracle's frames and keeps its incomplete tail; the
+split header walk equals the serial chain on generated long streams with
+adversarial content (embedded frame chains, noise, tiny frames).  Stream strategies: tests/test_properties.py."""
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -192,3 +194,48 @@ def test_protocol_over_rings_equals_oracle(engine, conns_frames, zero_copy_max, 
             assert rings[i].length() == len(wires[i]) - sum(f.header_len + f.header.length for f in want[i]), i
     finally:
         proto.close()
+
+
+@st.composite
+def long_stream(draw):
+    """A connection long enough to split (>= 2 KiB): runs of small frames
+    (masked or not, any length form), tiny 2-5 byte frames, an unmasked
+    frame carrying a plausible inner frame chain (guesses inside it confirm
+    on bytes that are not frame starts), noise, and an incomplete tail."""
+    parts = []
+    while sum(len(p) for p in parts) < 2048:
+        kind = draw(st.sampled_from(["small", "tiny", "embedded", "noise"]))
+        if kind == "small":
+            parts.append(b"".join(draw(st.lists(frame(), min_size=1, max_size=40))))
+        elif kind == "tiny":
+            parts.append(b"".join(wo.encode_frame(b"\x00" * draw(st.integers(0, 3)), 2, True, 0, False)
+                                  for _ in range(draw(st.integers(1, 60)))))
+        elif kind == "embedded":
+            inner = b"".join(draw(st.lists(frame(), min_size=1, max_size=30)))
+            parts.append(wo.encode_frame(inner, 2, True, 0, False))
+        else:
+            parts.append(draw(st.binary(min_size=1, max_size=600)))
+    return b"".join(parts) + draw(st.binary(max_size=10))
+
+
+@settings(max_examples=80, deadline=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture,
+                                 HealthCheck.data_too_large, HealthCheck.large_base_example])
+@given(st.lists(long_stream(), min_size=1, max_size=4), st.sampled_from([2, 4, 8, 16, 32]))
+def test_split_walk_equals_oracle(engine, ss, lanes):
+    """The split header walk (k_walk_split: lanes guess frame starts inside a
+    stream, walk between guesses, and a connection whose segments do not meet
+    exactly is re-walked serially) equals the serial chain -- the oracle --
+    bit-exactly on generated long streams, for every lane count, with 1 KiB
+    segments so that small streams split."""
+    arena, conns = pack_streams(ss)
+    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 0)
+    engine.set_tuning(_abi.TUNE_SPLIT_LANES, lanes)
+    engine.set_tuning(_abi.TUNE_SPLIT_MIN_BYTES, 1024)
+    try:
+        assert_matches_oracle(engine, arena, conns, f"lanes={lanes}")
+        assert engine.last_split_lanes == lanes
+    finally:
+        engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
+        engine.set_tuning(_abi.TUNE_SPLIT_MIN_BYTES, 16384)
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
