@@ -12,7 +12,8 @@ replies) equals oracle/ws_oracle.on_message on generated control-heavy
 streams; the host Protocol over ring buffers fed in arbitrary chunks hands
 every connection the oracle's frames and keeps its incomplete tail; the
 split header walk equals the serial chain on generated long streams with
-adversarial content (embedded frame chains, noise, tiny frames).  Stream strategies: tests/test_properties.py."""
+adversarial content (embedded frame chains, noise, tiny frames); the
+unmask's paths (v3 windows, counter runs, v5) over >= 2 MiB batches.  Stream strategies: tests/test_properties.py."""
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -239,3 +240,42 @@ def test_split_walk_equals_oracle(engine, ss, lanes):
         engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
         engine.set_tuning(_abi.TUNE_SPLIT_MIN_BYTES, 16384)
         engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+
+
+def _masked_frames_np(rng, lens, masked, forms):
+    """Frames with random payloads, XOR-masked with numpy (fast for MiBs)."""
+    out = []
+    for L, m, f in zip(lens, masked, forms):
+        key = bytes(rng.integers(0, 256, 4, dtype=np.uint8))
+        p = rng.integers(0, 256, L, dtype=np.uint8)
+        if m:
+            p = p ^ np.resize(np.frombuffer(key, np.uint8), L)
+        out.append(wo.write_header(True, 0, 2, L, m, key, f) + p.tobytes())
+    return out
+
+
+@settings(max_examples=40, deadline=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(st.integers(0, 2**32 - 1), st.booleans(), st.integers(64, 48 * 1024), st.integers(1, 40),
+       st.sampled_from([0, 1, 2]), st.sampled_from([0, 8, 12]))
+def test_unmask_paths_equal_oracle(engine, seed, equal, L, n_conns, variant, grid):
+    """The payload unmask over batches of >= 2 MiB: equal-size frames of any
+    length (the v3 windows and, with a capped grid, the per-XCD counter runs
+    over frames that cross tiles at every alignment) or mixed sizes (v5's
+    chunk -> frame map), masked and unmasked, any length form, every unmask
+    variant and grid: bit-exact against the C oracle."""
+    rng = np.random.default_rng(seed)
+    n = max(2, (2 << 20) // (L + 14) + 1)
+    lens = [L] * n if equal else [int(x) for x in rng.integers(0, 2 * L + 1, n)]
+    masked = [True] * n if equal else [bool(x) for x in rng.integers(0, 2, n)]
+    frames = _masked_frames_np(rng, lens, masked, [None] * n)
+    per = -(-n // n_conns)
+    streams = [b"".join(frames[i:i + per]) for i in range(0, n, per)]
+    arena, conns = pack_streams(streams)
+    engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, variant)
+    engine.set_tuning(_abi.TUNE_UNMASK_GRID, grid)
+    try:
+        assert_matches_oracle(engine, arena, conns, f"equal={equal} L={L} variant={variant} grid={grid}")
+    finally:
+        engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 0)
+        engine.set_tuning(_abi.TUNE_UNMASK_GRID, 0)
