@@ -18,6 +18,20 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C ABI)")
 
 
+# The property tests (tests/test_properties.py, tests/test_gpu_properties.py)
+# run derandomised by default -- the same generated cases every run, so the
+# suite is repeatable -- and explore new cases with
+# GEV_HYPOTHESIS_PROFILE=explore (plus --hypothesis-seed=N to pin a sweep).
+try:
+    from hypothesis import settings as _hsettings
+
+    _hsettings.register_profile("ci", derandomize=True)
+    _hsettings.register_profile("explore", derandomize=False)
+    _hsettings.load_profile(os.environ.get("GEV_HYPOTHESIS_PROFILE", "ci"))
+except ImportError:  # hypothesis is in the image; the property tests need it
+    pass
+
+
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np
