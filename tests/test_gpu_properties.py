@@ -13,7 +13,8 @@ streams; the host Protocol over ring buffers fed in arbitrary chunks hands
 every connection the oracle's frames and keeps its incomplete tail; the
 split header walk equals the serial chain on generated long streams with
 adversarial content (embedded frame chains, noise, tiny frames); the
-unmask's paths (v3 windows, counter runs, v5) over >= 2 MiB batches.  Stream strategies: tests/test_properties.py."""
+unmask's paths (v3 windows, counter runs, v5) over >= 2 MiB batches; the
+one-launch handler step (k_handle_small) against on_message.  Stream strategies: tests/test_properties.py."""
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -279,3 +280,40 @@ def test_unmask_paths_equal_oracle(engine, seed, equal, L, n_conns, variant, gri
     finally:
         engine.set_tuning(_abi.TUNE_UNMASK_VARIANT, 0)
         engine.set_tuning(_abi.TUNE_UNMASK_GRID, 0)
+
+
+@settings(max_examples=120, deadline=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(st.lists(st.lists(client_frame(), min_size=1, max_size=12), min_size=1, max_size=6),
+       st.sampled_from([_abi.HANDLER_NONE, _abi.HANDLER_ECHO_BINARY, _abi.HANDLER_ECHO_TEXT]),
+       st.integers(0, 40))
+def test_one_launch_handler_equals_oracle(engine, conns_frames, policy, slack):
+    """gevws_handle_decoded_async's one-workgroup form (k_handle_small: a
+    live pass's dispatch and FrameToBytes of the replies in ONE launch, its
+    frame count read from the decode's summary on the device, with a frame
+    bound above the decoded count) equals on_message's replies byte for
+    byte, with the same reply map and summaries."""
+    import torch
+    streams = [b"".join(fs) for fs in conns_frames]
+    arena, conns = pack_streams(streams)
+    dev = torch.device("cuda", engine.device)
+    d_in = torch.zeros(len(arena) + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    d_in[: len(arena)] = torch.from_numpy(np.frombuffer(arena, np.uint8).copy()).to(dev)
+    want, shut, reps, k = b"", 0, [], 0
+    for s in streams:
+        for fr in wo.decode_stream(s).frames:
+            r, sd = wo.on_message(fr.header, fr.payload, policy)
+            shut += sd
+            reps.append(-1 if r is None else k)
+            if r is not None:
+                want += r
+                k += 1
+    nf = len(reps)
+    aux = max(nf, 1)
+    out = engine.decode(d_in, len(arena), torch.from_numpy(conns.copy()).to(dev), conns.shape[0], aux_slots=aux)
+    wire, reply_of, ds, es = engine.handle_decoded(out, policy, nf + slack, aux, len(want) + 64)
+    assert int(ds["status"]) == 0 and int(es["status"]) == 0
+    assert int(ds["frames"]) == k and int(ds["errors"]) == shut
+    assert int(es["frames"]) == k and int(es["payload_bytes"]) == len(want)
+    assert list(reply_of) == reps
+    assert wire.cpu().numpy().tobytes() == want
