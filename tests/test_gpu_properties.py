@@ -14,7 +14,8 @@ every connection the oracle's frames and keeps its incomplete tail; the
 split header walk equals the serial chain on generated long streams with
 adversarial content (embedded frame chains, noise, tiny frames); the
 unmask's paths (v3 windows, counter runs, v5) over >= 2 MiB batches; the
-one-launch handler step (k_handle_small) against on_message.  Stream strategies: tests/test_properties.py."""
+one-launch handler step (k_handle_small) against on_message; the cgo entry
+point gevws_decode_host_batch over two-segment host input.  Stream strategies: tests/test_properties.py."""
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -317,3 +318,38 @@ def test_one_launch_handler_equals_oracle(engine, conns_frames, policy, slack):
     assert int(es["frames"]) == k and int(es["payload_bytes"]) == len(want)
     assert list(reply_of) == reps
     assert wire.cpu().numpy().tobytes() == want
+
+
+@settings(max_examples=120, deadline=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(st.lists(streams, min_size=1, max_size=8), st.sampled_from([0, 1 << 30]), st.data())
+def test_decode_host_batch_equals_oracle(engine, ss, zero_copy_max, data):
+    """gevws_decode_host_batch (the cgo entry point: each connection's bytes
+    as the two PeekAll segments of a ring, split anywhere, connection.go:
+    237-244; copies in and out, or zero-copy on mapped memory): per-connection
+    frames / consumed / status, records, src_off relative to the stream and
+    payloads equal the oracle's."""
+    proto = gev_amd.Protocol(engine)
+    proto.set_zero_copy_max(zero_copy_max)
+    try:
+        segs = []
+        for s in ss:
+            cut = data.draw(st.integers(0, len(s)))
+            segs.append((s[:cut], s[cut:]))
+        frames, payload, cout, summ = proto.decode_host(segs)
+        total = 0
+        for ci, s in enumerate(ss):
+            want = wo.decode_stream(s)
+            total += len(want.frames)
+            assert int(cout["nframes"][ci]) == len(want.frames)
+            assert int(cout["consumed"][ci]) == want.consumed
+            assert int(cout["status"][ci]) == want.status
+            for j, fr in enumerate(want.frames):
+                f = frames[int(cout["first_frame"][ci]) + j]
+                assert f.tobytes()[:16] == fr.header.pack()
+                assert int(f["src_off"]) == fr.stream_pos + fr.header_len
+                o = int(f["payload_off"])
+                assert payload[o:o + fr.header.length].tobytes() == fr.payload
+        assert summ.frames == total
+    finally:
+        proto.close()
