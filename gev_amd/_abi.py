@@ -46,6 +46,8 @@ TUNE_UNMASK_GRID = 2
 TUNE_ENCODE_VARIANT = 3  # 0 = auto, 1 / 2 = one / two tiles a wave step, 3 / 4 / 5 = two tiles, run mode 0 / 1 / 2
 TUNE_WALK_VARIANT = 4  # 0 = default, 1 = plain chain walk, 2 = no entry table, 3 = writer wave always
 TUNE_SMALL_BATCH = 7  # one-launch decode up to this many input bytes (0 = never)
+ONE_LAUNCH_MAX_BYTES = 128 * 1024  # GEVWS_ONE_LAUNCH_MAX_BYTES: TUNE_SMALL_BATCH's default and maximum
+ONE_LAUNCH_MAX_CONNS = 1024  # GEVWS_ONE_LAUNCH_MAX_CONNS
 TUNE_SPLIT_LANES = 8  # split header walk: lanes per connection (0 = auto, 1 = never, 2/4/8/16/32)
 TUNE_RETIRED = (5, 6, 9, 10, 11, 12)  # round 1-3 measurement knobs, rejected
 TUNE_SPLIT_MIN_BYTES = 13  # split walk: bytes per segment at least (default 16 384)

@@ -6,6 +6,8 @@
 // and gevws_encode.hip (encode, control-frame dispatch); gevws_kernels.hpp
 // holds what they share.
 #include <atomic>
+#include <cstdlib>
+#include <cstring>
 
 #include "gevws_internal.hpp"
 
@@ -139,25 +141,33 @@ int gevws_device_count(void) {
   return n;
 }
 
-// The priority of the n-th context's stream on a device: 0, -1, 1, -2, 2, ...
-// inside the device's range.  The HIP runtime gives each priority level its
-// own hardware queues, and same-priority streams share that level's few (3 of
-// the default GPU_MAX_HW_QUEUES = 4 on the box): eight event loops' contexts
-// at one priority ran at most 3 loops' kernels at once, cycling the levels
-// runs all 8 (tools/queue_probe.hip, profiles/r05/r05u_queue_probe.jsonl).
+// The priority of the n-th context's stream on a device.  The HIP runtime
+// gives each priority level its own hardware queues, and same-priority
+// streams share that level's few (3 of the default GPU_MAX_HW_QUEUES = 4 on
+// the box): eight event loops' contexts at one priority ran at most 3 loops'
+// kernels at once, cycling the levels runs more (tools/queue_probe.hip,
+// profiles/r05/r05u_queue_probe.jsonl).  By default the cycle is the normal
+// level and the levels BELOW it (0, 1, ... inside the device's range): a
+// context never outranks the application's own work on normal-priority
+// streams, and no loop sits below another loop's level by more than the
+// range allows.  GEVWS_STREAM_PRIORITIES=all adds the levels above
+// normal (0, -1, 1, -2, 2, ...: the most queues, for a process whose only
+// device work is its loops' passes); =normal keeps every context at 0.
 static int ctx_stream_priority(int device) {
   static std::atomic<uint32_t> seq[64];
   int least = 0, greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest) return 0;
-  const uint32_t span = (uint32_t)(least - greatest + 1);
-  const uint32_t k = seq[device & 63].fetch_add(1, std::memory_order_relaxed) % span;
-  int p = 0;  // walk 0, -1, 1, -2, 2, ... keeping the first k levels that fall inside [greatest, least]
-  for (uint32_t taken = 0, i = 1;; ++i) {
-    if (taken == k) break;
-    const int c = (i & 1) ? -(int)((i + 1) / 2) : (int)(i / 2);
-    if (c >= greatest && c <= least && ++taken == k) p = c;
+  const char* e = getenv("GEVWS_STREAM_PRIORITIES");
+  const bool all = e && !strcmp(e, "all");
+  if (e && !strcmp(e, "normal")) return 0;
+  int levels[64];
+  uint32_t nl = 0;
+  levels[nl++] = 0;
+  for (int i = 1; nl < 64 && (i <= least || -i >= greatest); ++i) {
+    if (all && -i >= greatest) levels[nl++] = -i;
+    if (i <= least && nl < 64) levels[nl++] = i;
   }
-  return p;
+  return levels[seq[device & 63].fetch_add(1, std::memory_order_relaxed) % nl];
 }
 
 gevws_ctx* gevws_ctx_create(int device) {
@@ -183,6 +193,8 @@ gevws_ctx* gevws_ctx_create(int device) {
   if (hipMalloc(reinterpret_cast<void**>(&ctx->d_sum), sizeof(gevws_summary)) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&ctx->d_done), 256) != hipSuccess ||
       hipMemset(ctx->d_done, 0, 256) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&ctx->d_walk_part), kWalkPartBytes) != hipSuccess ||
+      hipMemset(ctx->d_walk_part, 0, kWalkPartBytes) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&ctx->h_stats), 64, hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->d_stats), ctx->h_stats, 0) != hipSuccess ||
@@ -204,6 +216,7 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (ctx->d_sum) (void)hipFree(ctx->d_sum);
   if (ctx->d_done) (void)hipFree(ctx->d_done);
   if (ctx->d_small_stage) (void)hipFree(ctx->d_small_stage);
+  if (ctx->d_walk_part) (void)hipFree(ctx->d_walk_part);
   if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
   for (auto& set : ctx->evs)
@@ -239,7 +252,7 @@ int gevws_ctx_set_tuning(gevws_ctx* ctx, int key, int64_t value) {
       ctx->encode_variant = (int)value;
       return GEVWS_OK;
     case GEVWS_TUNE_SMALL_BATCH:
-      if (value < 0 || (uint64_t)value > kSmallBytes) return GEVWS_ERR_INVALID;
+      if (value < 0 || (uint64_t)value > kOneLaunchBytes) return GEVWS_ERR_INVALID;
       ctx->small_bytes = (uint64_t)value;
       return GEVWS_OK;
     case GEVWS_TUNE_SPLIT_LANES:
@@ -325,7 +338,7 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   hipStream_t st = pick_stream(ctx, stream);
   // a small batch with the default kernels: the whole decode in one launch
   // (per-phase timing and the variant knobs keep the multi-kernel path)
-  if (n_conns <= kSmallConns && in_bytes <= ctx->small_bytes && !ctx->timing && ctx->walk_variant == 0 &&
+  if (n_conns <= kOneLaunchConns && in_bytes <= ctx->small_bytes && !ctx->timing && ctx->walk_variant == 0 &&
       ctx->unmask_variant == 0 && ctx->unmask_grid == 0)
     return decode_small(ctx, st, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload, payload_cap,
                         d_conn_out, d_summary);

@@ -493,8 +493,11 @@ __global__ __launch_bounds__(kUnmaskBlock) __attribute__((amdgpu_waves_per_eu(U 
       wave_lds_order();
       // frame i's wire offset from the step's first one: out_off[fa] (one
       // scalar load) + fa's wire size + the sizes of frames 1 .. i-1 (a wave
-      // scan; each of frames 1 .. n-2 starts and ends inside the step, so the
-      // sum fits 32 bits) -- no per-frame out_off reads (C4: 0.35 GB a launch)
+      // scan; each of frames 1 .. n-2 starts and ends inside the step's
+      // U KiB window, so their sum is below U KiB and fits 32 bits; frame 0
+      // and frame n - 1 may be any size and are added in 64 bits) -- no
+      // per-frame out_off reads (C4: 0.35 GB a launch)
+      static_assert((uint64_t)U * 1024 < (1ull << 32), "the interior frames' 32-bit wire-size scan");
       const uint64_t o_fa = uniform64(out_off[fa]);
       uint64_t w_fa = 0;
       uint32_t carry = 0;

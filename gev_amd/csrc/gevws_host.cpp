@@ -297,7 +297,6 @@ class Protocol {
     Staged& sg = pend_.sg;
     const auto tb1 = std::chrono::steady_clock::now();
     tl_.ns_select += ns_since(tb0, tb1);
-    stage_end_ = tb1;
     int64_t r = StageDecode(segs.data(), m, &sg, true);
     if (r < 0) return r;
     pend_.conns.assign(conns, conns + n);
@@ -321,7 +320,7 @@ class Protocol {
     }
     pend_.active = true;
     const auto tb2 = std::chrono::steady_clock::now();
-    tl_.ns_stage += ns_since(tb1, stage_end_);
+    tl_.ns_stage += ns_since(stage_begin_, stage_end_);
     tl_.ns_launch += ns_since(stage_end_, tb2);
     return (int64_t)m;
   }
@@ -687,7 +686,10 @@ class Protocol {
   // table, ONE H2D, enqueue the decode on the context's stream and the D2H of
   // {summary, conn_out} into pinned h_res_ (no synchronisation yet: the caller
   // adds its own copies, then Finish waits).
+  // (stage_begin_ / stage_end_: the staging phase of the pass timeline; a
+  // path that returns before the launch books no staging time)
   int64_t StageDecode(const gevws_host_conn* segs, uint32_t m, Staged* sg, bool allow_zc = false) {
+    stage_begin_ = stage_end_ = std::chrono::steady_clock::now();
     uint64_t total = 0;
     for (uint32_t j = 0; j < m; ++j) total += segs[j].n0 + segs[j].n1;
     sg->cin.resize(m);
@@ -918,7 +920,7 @@ class Protocol {
   gevws_protocol_timeline tl_{};
   uint64_t* h_ticks_ = nullptr;
   double ns_per_tick_ = 10.0;  // 100 MHz unless the device says otherwise
-  std::chrono::steady_clock::time_point stage_end_;
+  std::chrono::steady_clock::time_point stage_begin_, stage_end_;
   bool last_signalled_ = false;
   static uint64_t ns_since(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();

@@ -23,7 +23,7 @@ struct gevws_ctx {
   int unmask_variant = 0;  // GEVWS_TUNE_UNMASK_VARIANT (kUnmaskVariants)
   int unmask_grid = 0;     // 0 = auto
   int encode_variant = 0;  // GEVWS_TUNE_ENCODE_VARIANT (kNumEncodeVariants)
-  uint64_t small_bytes = kSmallBytes;  // one-launch decode (k_decode_small) up to this many input bytes
+  uint64_t small_bytes = kOneLaunchBytes;  // one-launch decode (k_decode_small) up to this many input bytes
   uint32_t* done_flag = nullptr;  // mapped host word the one-launch kernels signal (gevws_ctx_set_completion_flag)
   uint32_t done_seq = 0;
   uint64_t* ticks = nullptr;  // mapped host u64[4]: the one-launch kernels' start / end ticks (gevws_ctx_set_timeline_ticks)
@@ -55,8 +55,19 @@ struct gevws_ctx {
   int num_cus = 256;
   uint32_t* d_done = nullptr;  // 256 B: the decode walk's finished-workgroup counter ([0], zero between calls)
                                // and the one-launch decode's staging counter ([kSmallStageCounter])
-  uint64_t* d_small_stage = nullptr;  // the one-launch decode's staged input (live passes, k_decode_small)
+  // The in-launch cross-workgroup hand-offs' tagged granules (gevws_walk.hip,
+  // "hand-offs"), zeroed at allocation, and the number that tags the next
+  // launch's (never 0):
+  uint64_t* d_walk_part = nullptr;    // the walk's block partials (kFusedScanMaxBlocks x kDecFields x 2)
+  uint64_t* d_small_stage = nullptr;  // a live pass's staged input (k_decode_small; 4 granules a 16-byte chunk)
+  uint32_t hand_seq = 0;
 };
+
+// The tag of a launch's hand-offs.
+inline uint32_t next_hand_tag(gevws_ctx* ctx) {
+  if (++ctx->hand_seq == 0) ctx->hand_seq = 1;
+  return ctx->hand_seq;
+}
 
 namespace gevws_impl {
 

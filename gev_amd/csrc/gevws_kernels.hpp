@@ -49,6 +49,8 @@ constexpr int kDecFields = 5;
 // for longer than the launch they save (C1-shaped batch: walk + scan 46 ->
 // 54 us fused; 256 blocks -- C2, C3, C5, an 8-way C4 share -- save 4-8 us)
 constexpr uint32_t kFusedScanMaxBlocks = 256;
+// their partials as tagged granules (gevws_walk.hip, hand-offs): two per field
+constexpr size_t kWalkPartBytes = (size_t)kFusedScanMaxBlocks * kDecFields * 2 * sizeof(uint64_t);
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ u32x4 ld16u(const uint8_t* p) {
@@ -263,9 +265,15 @@ __global__ __launch_bounds__(BS) void k_scan_blocks(uint64_t* __restrict__ blk, 
 
 // ------------------------------------------------------------------ one-launch passes
 // The small-batch decode (k_decode_small, gevws_walk.hip) and the one-launch
-// handler step (k_handle_small, gevws_encode.hip) run in ONE workgroup.
+// handler step (k_handle_small, gevws_encode.hip) run in ONE workgroup.  The
+// decode has two shapes: 256 lanes and 64 KiB of input staged in LDS (a loop's
+// usual pass), and 1 024 lanes and 128 KiB (146 KB of the 160 KiB LDS: passes
+// of up to 1 024 connections, e.g. the 4 000-connection live shape's ~500).
 constexpr uint32_t kSmallConns = 256;
 constexpr uint64_t kSmallBytes = 64 * 1024;
+constexpr uint32_t kOneLaunchConns = GEVWS_ONE_LAUNCH_MAX_CONNS;
+constexpr uint64_t kOneLaunchBytes = GEVWS_ONE_LAUNCH_MAX_BYTES;
+static_assert(kOneLaunchConns == 1024 && kOneLaunchBytes == 128 * 1024, "k_decode_small's wide shape");
 // A live pass's last kernel announces its end in mapped host memory: every
 // thread's writes (records, payload, summaries) are fenced at system scope,
 // then one lane stores `seq` with a system-scope release (a vector store), so

@@ -13,55 +13,112 @@
 //   k_walk_bases   per-connection bases (block-level scan)
 //   k_walk_emit    the 32-byte records (= ws.Header + offsets) and the
 //                  output-tile -> frame map the unmask reads
-//   k_decode_small a batch of <= 256 connections and 64 KiB: the whole decode,
-//                  unmask included, in one workgroup
+//   k_decode_small a batch of <= 1 024 connections and 128 KiB: the whole
+//                  decode, unmask included, in one workgroup
 #include "gevws_internal.hpp"
 
 namespace {
 
+// ------------------------------------------------------------------ hand-offs
+// Two hand-offs cross workgroups inside one launch: the walk's block partials
+// to its last workgroup (walk_block_done) and a live pass's input, staged by
+// many workgroups, to the one-launch decode's last one (k_decode_small).
+// Both move TAGGED GRANULES: 8 bytes {u32 data, u32 tag}, stored and loaded
+// as agent-scope relaxed 64-bit atomics, the tag being the launch's number
+// (next_hand_tag: never 0; the buffers start zeroed).  The last workgroup is
+// elected by an agent-scope counter (relaxed: the read-modify-writes on it
+// are totally ordered, so exactly one sees nwg - 1) and takes a granule's
+// data only once it has loaded that granule carrying this launch's tag.  A
+// load that returns the tag returns the data of the same store (an atomic
+// is never torn; per-location coherence), so the hand-off rests neither on a
+// release / acquire pair nor on cache behaviour.  On gfx950 the first load
+// carries the tag (the writers' stores are write-through and drained by
+// s_waitcnt before their counter add); the re-load loop is what the memory
+// model guarantees, bounded: a granule that never shows its tag fails the
+// launch (GEVWS_ERR_DEVICE).  A release (buffer_wbl2) in every workgroup and
+// an acquire in the last cost ~1.7 us each on gfx950 (MI355X_MICROARCH.md,
+// the fence rows) against a ~9 us live-pass kernel; the tags cost twice the
+// bytes of a hand-off of a few KB.
+constexpr uint32_t kHandSpin = 1u << 16;  // re-loads of one granule before the launch fails
+__device__ __forceinline__ void put_granule(uint64_t* p, uint32_t v, uint32_t tag) {
+  __hip_atomic_store(p, (uint64_t)v | ((uint64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t load_granule(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The data of the granule at p, loaded as g, once it carries `tag` (bad = 1 if it never did).
+__device__ __forceinline__ uint32_t take_granule(const uint64_t* p, uint64_t g, uint32_t tag, uint32_t& bad) {
+  for (uint32_t i = 0; (uint32_t)(g >> 32) != tag; ++i) {
+    if (i == kHandSpin) {
+      bad = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    g = load_granule(p);
+  }
+  return (uint32_t)g;
+}
+
+// A walk block's partial of field k as two granules (low, high 32 bits).
+__device__ __forceinline__ void put_partial(uint64_t* part, uint32_t b, int k, uint64_t v, uint32_t tag) {
+  uint64_t* p = part + 2 * ((uint64_t)b * kDecFields + k);
+  put_granule(p, (uint32_t)v, tag);
+  put_granule(p + 1, (uint32_t)(v >> 32), tag);
+}
+
 // The decode's partials scan by ONE wave (the walk's last block, see
-// walk_block_done): per round each lane takes 8 consecutive block partials,
-// fields 0/1 become exclusive bases (frames, arena bytes) for k_walk_bases,
+// walk_block_done): per round each lane takes P consecutive block partials
+// (tagged granules, all loads in flight before any is checked), fields 0/1
+// become exclusive bases (frames, arena bytes) for k_walk_bases in blk,
 // every field is totalled into the summary, with the capacity check.
-__device__ void scan_partials_wave(uint64_t* __restrict__ blk, uint32_t nblk, uint64_t max_frames,
-                                   uint64_t payload_cap, gevws_summary* __restrict__ sum) {
-  constexpr int P = 8;
+__device__ void scan_partials_wave(const uint64_t* __restrict__ part, uint32_t tag, uint64_t* __restrict__ blk,
+                                   uint32_t nblk, uint64_t max_frames, uint64_t payload_cap,
+                                   gevws_summary* __restrict__ sum) {
+  constexpr int P = 4;  // 64 x 4 = kFusedScanMaxBlocks: one round
   const int lane = threadIdx.x & 63;
   uint64_t carry[kDecFields] = {0, 0, 0, 0, 0};
+  uint32_t bad = 0;
   for (uint64_t base = 0; base < nblk; base += 64 * P) {  // wave-uniform
     const uint64_t i0 = base + (uint64_t)lane * P;
-    uint64_t loc[kDecFields] = {0, 0, 0, 0, 0};
-    uint64_t loc0[P], loc1[P];  // this lane's partials of fields 0 / 1, for the bases
-#pragma unroll
-    for (int r = 0; r < P; ++r) {
-      loc0[r] = (i0 + r < nblk) ? __hip_atomic_load(blk + (i0 + r) * kDecFields, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT) : 0;
-      loc1[r] = (i0 + r < nblk) ? __hip_atomic_load(blk + (i0 + r) * kDecFields + 1, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT) : 0;
-    }
+    uint64_t g[P][kDecFields][2];
 #pragma unroll
     for (int r = 0; r < P; ++r)
 #pragma unroll
       for (int k = 0; k < kDecFields; ++k)
-        loc[k] += (i0 + r < nblk) ? __hip_atomic_load(blk + (i0 + r) * kDecFields + k, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                  : 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          g[r][k][h] = (i0 + r < nblk) ? load_granule(part + 2 * ((i0 + r) * kDecFields + k) + h) : 0;
+    uint64_t loc[kDecFields] = {0, 0, 0, 0, 0};
+    uint64_t loc0[P], loc1[P];  // this lane's partials of fields 0 / 1, for the bases
+#pragma unroll
+    for (int r = 0; r < P; ++r)
+#pragma unroll
+      for (int k = 0; k < kDecFields; ++k) {
+        uint64_t v = 0;
+        if (i0 + r < nblk) {
+          const uint64_t* q = part + 2 * ((i0 + r) * kDecFields + k);
+          v = (uint64_t)take_granule(q, g[r][k][0], tag, bad) | ((uint64_t)take_granule(q + 1, g[r][k][1], tag, bad) << 32);
+        }
+        loc[k] += v;
+        if (k == 0) loc0[r] = v;
+        if (k == 1) loc1[r] = v;
+      }
     const uint64_t inc0 = wave_incl_scan(loc[0]), inc1 = wave_incl_scan(loc[1]);
     uint64_t b0 = carry[0] + inc0 - loc[0], b1 = carry[1] + inc1 - loc[1];
 #pragma unroll
     for (int r = 0; r < P; ++r) {
       if (i0 + r < nblk) {
         uint64_t* q = blk + (i0 + r) * kDecFields;
-        const uint64_t f0 = loc0[r], f1 = loc1[r];
         q[0] = b0;
         q[1] = b1;
-        b0 += f0;
-        b1 += f1;
+        b0 += loc0[r];
+        b1 += loc1[r];
       }
     }
 #pragma unroll
     for (int k = 0; k < kDecFields; ++k) carry[k] += wave_sum(loc[k]);
   }
+  bad = (uint32_t)wave_sum(bad);
   if (lane == 0) {
     gevws_summary sm;
     memset(&sm, 0, sizeof(sm));
@@ -71,24 +128,22 @@ __device__ void scan_partials_wave(uint64_t* __restrict__ blk, uint32_t nblk, ui
     sm.errors = carry[3] & 0xffffffffull;
     sm.flags = (carry[3] >> 32) ? GEVWS_SUMMARY_UNORDERED : 0u;
     sm.run_frames = carry[4];
-    sm.status = (carry[0] > max_frames || carry[1] > payload_cap) ? GEVWS_ERR_CAPACITY : GEVWS_OK;
+    sm.status = bad ? GEVWS_ERR_DEVICE
+                    : (carry[0] > max_frames || carry[1] > payload_cap) ? GEVWS_ERR_CAPACITY : GEVWS_OK;
     *sum = sm;
   }
 }
 
 // The last of the walk's workgroups to finish (a device-scope counter) scans
-// the partials, so the decode needs no k_scan_blocks launch.  L2 is per XCD
-// and not coherent, and a release fence would write back the whole L2 (the
-// walk's entry stores: measured 2x slower), so only the partials travel
-// coherently: they are stored and loaded as agent-scope atomics (write-through
-// / L2-bypassing), each writer waits for its stores before its workgroup counts
-// itself, and the last workgroup resets the counter for the context's next call.
-__device__ __forceinline__ void put_partial(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uint32_t nblk, uint64_t* __restrict__ blk,
-                                                uint64_t max_frames, uint64_t payload_cap,
-                                                gevws_summary* __restrict__ sum, bool wrote) {
+// the partials, so a decode of <= kFusedScanMaxBlocks blocks needs no
+// k_scan_blocks launch.  The partials travel as tagged granules (hand-offs,
+// above); each writer waits for its stores before its workgroup counts itself
+// (not needed for correctness: it makes the first load of each granule the
+// one that carries the tag), and the last workgroup resets the counter for the
+// context's next call (ordered after this launch by the kernel boundary).
+__device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uint32_t nblk, const uint64_t* __restrict__ part,
+                                                uint32_t tag, uint64_t* __restrict__ blk, uint64_t max_frames,
+                                                uint64_t payload_cap, gevws_summary* __restrict__ sum, bool wrote) {
   __shared__ uint32_t s_last;
   if (wrote) __builtin_amdgcn_s_waitcnt(0);  // the partials' write-through stores are done
   __syncthreads();
@@ -96,7 +151,7 @@ __device__ __forceinline__ void walk_block_done(uint32_t* __restrict__ done, uin
     s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1 ? 1u : 0u;
   __syncthreads();
   if (s_last) {
-    if (threadIdx.x < 64) scan_partials_wave(blk, nblk, max_frames, payload_cap, sum);
+    if (threadIdx.x < 64) scan_partials_wave(part, tag, blk, nblk, max_frames, payload_cap, sum);
     if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -450,8 +505,8 @@ template <int D, int ST>
 __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_walk_count(
     const uint8_t* __restrict__ in, const gevws_conn_in* __restrict__ conns, uint32_t n,
     gevws_conn_out* __restrict__ cout, uint64_t* __restrict__ blk, WalkEntry* __restrict__ entries, uint64_t n_entries,
-    uint32_t gshift, uint32_t cpb, uint64_t in_bytes, uint32_t* __restrict__ done, uint64_t max_frames,
-    uint64_t payload_cap, gevws_summary* __restrict__ sum) {
+    uint32_t gshift, uint32_t cpb, uint64_t in_bytes, uint32_t* __restrict__ done, uint64_t* __restrict__ part,
+    uint32_t tag, uint64_t max_frames, uint64_t payload_cap, gevws_summary* __restrict__ sum) {
   __shared__ WalkEntry s_ring[ST == 2 ? kCountBlock * kRing : 1];
   __shared__ uint32_t s_head[ST == 2 ? kCountBlock : 1], s_tail[ST == 2 ? kCountBlock : 1];
   __shared__ uint64_t s_ebase[ST == 2 ? kCountBlock : 1], s_ecap[ST == 2 ? kCountBlock : 1];
@@ -511,11 +566,11 @@ __global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_wal
   for (int k = 0; k < kDecFields; ++k) {
     const uint64_t s = wave_sum(vals[k]);
     if (threadIdx.x == 0) {
-      if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + k, s);
+      if (done) put_partial(part, blockIdx.x, k, s, tag);
       else blk[(uint64_t)blockIdx.x * kDecFields + k] = s;
     }
   }
-  if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
+  if (done) walk_block_done(done, gridDim.x, part, tag, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
 }
 
 // ------------------------------------------------------------------ 1a''. walk (count), split
@@ -708,7 +763,9 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
                                                             uint64_t* __restrict__ blk,
                                                             WalkEntry* __restrict__ entries, uint64_t n_entries,
                                                             uint32_t gshift, uint32_t cpb, uint64_t in_bytes,
-                                                            uint32_t* __restrict__ done, uint64_t max_frames,
+                                                            uint32_t* __restrict__ done,
+                                                            uint64_t* __restrict__ part, uint32_t tag,
+                                                            uint64_t max_frames,
                                                             uint64_t payload_cap, gevws_summary* __restrict__ sum,
                                                             gevws_conn_in* __restrict__ segs,
                                                             gevws_conn_out* __restrict__ sout,
@@ -863,11 +920,11 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
   for (int k = 0; k < kDecFields; ++k) {
     const uint64_t x = wave_sum(vals[k]);
     if (threadIdx.x == 0) {
-      if (done) put_partial(blk + (uint64_t)blockIdx.x * kDecFields + k, x);
+      if (done) put_partial(part, blockIdx.x, k, x, tag);
       else blk[(uint64_t)blockIdx.x * kDecFields + k] = x;
     }
   }
-  if (done) walk_block_done(done, gridDim.x, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
+  if (done) walk_block_done(done, gridDim.x, part, tag, blk, max_frames, payload_cap, sum, threadIdx.x == 0);
 }
 
 // ------------------------------------------------------------------ 3. walk (emit)
@@ -1198,21 +1255,24 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk_emit(const uint8_t* __restr
 // A live server's pass is small (C1: ~100 connections x 136 B per loop
 // iteration) and pays per launch, not per byte: four kernels cost ~5 us each
 // of GPU time whatever their size (profiles/r02/r02_loopback_*), plus their host
-// launch costs.  Batches of at most kSmallConns connections and
-// GEVWS_TUNE_SMALL_BATCH bytes (default kSmallBytes) run the whole decode in
-// ONE workgroup: each lane walks its connection (k_walk_count's rules), a
-// block scan gives the bases and the summary, each lane re-walks its chain
-// writing the records and unmasking payloads of up to kSmallLaneBytes itself
-// (all its chunk loads at once), and the workgroup unmasks the larger ones
-// together.  Output identical to the multi-kernel decode.
-// The whole input (<= 64 KiB + the pad) is staged into LDS first, by
-// independent coalesced 16-byte loads, and every header and payload read after
-// that is an LDS read: a live pass's input sits in mapped pinned host memory,
-// where each of the walk's and the record pass's DEPENDENT header loads was a
-// PCIe round trip (the kernel took ~10 us for 100 connections of 1-2 frames,
+// launch costs.  Batches of at most kOneLaunchConns connections and
+// GEVWS_TUNE_SMALL_BATCH bytes (default kOneLaunchBytes) run the whole decode
+// in ONE workgroup of NT lanes: each lane walks its connection (k_walk_count's
+// rules), a block scan gives the bases and the summary, each lane re-walks its
+// chain writing the records and unmasking payloads of up to kSmallLaneBytes
+// itself (all its chunk loads at once), and the workgroup unmasks the larger
+// ones together.  Output identical to the multi-kernel decode.
+// The whole input (<= SB + the pad) is staged into LDS first, by independent
+// coalesced 16-byte loads, and every header and payload read after that is an
+// LDS read: a live pass's input sits in mapped pinned host memory, where each
+// of the walk's and the record pass's DEPENDENT header loads was a PCIe round
+// trip (the kernel took ~10 us for 100 connections of 1-2 frames,
 // profiles/r05/r05_loopback_timeline.jsonl).
+// Two shapes (SmallShape): <256 lanes, 64 KiB> for a loop's usual pass and
+// <1 024 lanes, 128 KiB> above it -- 146 KB of LDS, one workgroup per CU --
+// which takes the 4 000-connection live shape's passes (~500 connections,
+// ~67 KB) that used to fall to the multi-kernel decode over mapped memory.
 constexpr uint32_t kSmallLaneBytes = 256;
-constexpr uint32_t kSmallStage = (uint32_t)(kSmallBytes + GEVWS_IN_PAD) / 16;  // 16-byte chunks of staged input
 
 // 16 bytes at byte `off` of the staged input (any alignment: five aligned
 // dword reads and a byte funnel shift)
@@ -1227,67 +1287,84 @@ __device__ __forceinline__ void lds_window(const uint32_t* __restrict__ s, uint3
   lo = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
   hi = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
 }
-constexpr uint32_t kSmallBig = kSmallBytes / kSmallLaneBytes;  // larger payloads fit in the input at most this often
+
+template <uint32_t NT_, uint64_t SB_>
+struct SmallShape {
+  static constexpr uint32_t NT = NT_;  // lanes = connections at most
+  static constexpr uint64_t SB = SB_;  // input bytes at most
+  static constexpr uint32_t kStage = (uint32_t)((SB + GEVWS_IN_PAD) / 16);  // 16-byte chunks of staged input
+  static constexpr uint32_t kBig = (uint32_t)(SB / kSmallLaneBytes);  // larger payloads fit in the input at most this often
+  // staging loads a thread keeps in flight (4 granules a chunk in the hand-off)
+  static constexpr int kBatch = NT >= 1024 ? 4 : 8;
+};
+using SmallNarrow = SmallShape<kSmallConns, kSmallBytes>;
+using SmallWide = SmallShape<kOneLaunchConns, kOneLaunchBytes>;
+
 // A live pass's input is read by up to kSmallStageWGs workgroups, a slice of
-// kSmallSliceChunks 16-byte chunks each (2 KiB: one round of loads a thread)
+// at least kSmallSliceChunks 16-byte chunks each (2 KiB)
 constexpr uint32_t kSmallStageWGs = 32;
 constexpr uint64_t kSmallSliceChunks = 128;
 // their finished-workgroup counter: a word of ctx->d_done of its own (the
 // walk's is d_done[0]), 128 bytes apart
 constexpr uint32_t kSmallStageCounter = 32;
 
-__global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __restrict__ in, uint64_t in_bytes,
-                                                              const gevws_conn_in* __restrict__ conns, uint32_t n,
-                                                              gevws_frame* __restrict__ frames, uint64_t max_frames,
-                                                              uint8_t* __restrict__ payload, uint64_t payload_cap,
-                                                              gevws_conn_out* __restrict__ cout,
-                                                              gevws_summary* __restrict__ sum,
-                                                              uint32_t* __restrict__ done = nullptr,
-                                                              uint32_t seq = 0, uint64_t* __restrict__ ticks = nullptr,
-                                                              uint64_t* __restrict__ stage_buf = nullptr,
-                                                              uint32_t* __restrict__ stage_done = nullptr) {
-  __shared__ uint64_t s_big[kSmallBig][3];  // {src_off, payload_off, length} of the larger payloads
+template <class S>
+__global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restrict__ in, uint64_t in_bytes,
+                                                        const gevws_conn_in* __restrict__ conns, uint32_t n,
+                                                        gevws_frame* __restrict__ frames, uint64_t max_frames,
+                                                        uint8_t* __restrict__ payload, uint64_t payload_cap,
+                                                        gevws_conn_out* __restrict__ cout,
+                                                        gevws_summary* __restrict__ sum,
+                                                        uint32_t* __restrict__ done = nullptr,
+                                                        uint32_t seq = 0, uint64_t* __restrict__ ticks = nullptr,
+                                                        uint64_t* __restrict__ stage_buf = nullptr,
+                                                        uint32_t* __restrict__ stage_done = nullptr,
+                                                        uint32_t tag = 0) {
+  constexpr uint32_t NT = S::NT;
+  constexpr int kBatch = S::kBatch;
+  __shared__ uint64_t s_big[S::kBig][3];  // {src_off, payload_off, length} of the larger payloads
   __shared__ uint32_t s_last;
-  __shared__ uint32_t s_bkey[kSmallBig];
+  __shared__ uint32_t s_bkey[S::kBig];
   __shared__ uint32_t s_nbig;
-  __shared__ __attribute__((aligned(16))) uint32_t s_in[4 * kSmallStage + 4];  // the staged input (+ a dword of slack)
+  __shared__ uint32_t s_bad;
+  __shared__ __attribute__((aligned(16))) uint32_t s_in[4 * S::kStage + 4];  // the staged input (+ a dword of slack)
   const uint64_t t0 = done ? gpu_ticks() : 0;
   const uint32_t c = threadIdx.x;
-  if (c == 0) s_nbig = 0;
+  if (c == 0) {
+    s_nbig = 0;
+    s_bad = 0;
+  }
   gevws_conn_in ci{0, 0}, cprev{0, 0};
   if (c < n) {  // (in flight with the staging loads)
     ci = conns[c];
     if (c > 0) cprev = conns[c - 1];
   }
   if (n) {  // bytes [0, 16 x nst) of the input: every read below is inside [0, in_bytes + 48)
-    // kSmallBatch loads a thread in flight at once
-    constexpr int kSmallBatch = 8;
     const uint32_t nst = (uint32_t)((in_bytes + GEVWS_IN_PAD) / 16);
     u32x4* st = reinterpret_cast<u32x4*>(s_in);
     const uint32_t nwg = gridDim.x;
     if (nwg > 1) {
       // A live pass's input sits in mapped host memory, which one workgroup
       // reads at ~2.5 GB/s (a 20 KB pass: ~8 us of staging).  So every
-      // workgroup copies its slice of the input into stage_buf (agent-scope
-      // write-through stores, as the walk's partials: L2 is per XCD), and the
-      // last one to finish (stage_done) stages the whole input from there
-      // into its LDS and runs the decode; the others end here.
+      // workgroup copies its slice of the input into stage_buf as tagged
+      // granules (hand-offs, above: 4 a 16-byte chunk), and the last one to
+      // finish (stage_done) stages the whole input from there into its LDS
+      // and runs the decode; the others end here.
       const uint32_t per = (nst + nwg - 1) / nwg;
       const uint32_t k0 = blockIdx.x * per, k1 = k0 + per < nst ? k0 + per : nst;
-      for (uint32_t kb = k0; kb < k1; kb += kSmallBatch * kSmallConns) {
-        u32x4 x[kSmallBatch];
+      for (uint32_t kb = k0; kb < k1; kb += kBatch * NT) {
+        u32x4 x[kBatch];
 #pragma unroll
-        for (int j = 0; j < kSmallBatch; ++j) {
-          const uint32_t k = kb + (uint32_t)j * kSmallConns + c;
+        for (int j = 0; j < kBatch; ++j) {
+          const uint32_t k = kb + (uint32_t)j * NT + c;
           if (k < k1) x[j] = ld16u(in + 16ull * k);
         }
 #pragma unroll
-        for (int j = 0; j < kSmallBatch; ++j) {
-          const uint32_t k = kb + (uint32_t)j * kSmallConns + c;
-          if (k < k1) {
-            put_partial(stage_buf + 2ull * k, (uint64_t)x[j][0] | ((uint64_t)x[j][1] << 32));
-            put_partial(stage_buf + 2ull * k + 1, (uint64_t)x[j][2] | ((uint64_t)x[j][3] << 32));
-          }
+        for (int j = 0; j < kBatch; ++j) {
+          const uint32_t k = kb + (uint32_t)j * NT + c;
+          if (k < k1)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) put_granule(stage_buf + 4ull * k + i, x[j][i], tag);
         }
       }
       __builtin_amdgcn_s_waitcnt(0);  // this workgroup's stores are done before it counts itself
@@ -1297,37 +1374,52 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
       __syncthreads();
       if (!s_last) return;
       if (c == 0) __hip_atomic_store(stage_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's
-      for (uint32_t kb = 0; kb < nst; kb += kSmallBatch * kSmallConns) {
-        uint64_t lo[kSmallBatch], hi[kSmallBatch];
+      uint32_t bad = 0;
+      for (uint32_t kb = 0; kb < nst; kb += kBatch * NT) {
+        uint64_t g[kBatch][4];
 #pragma unroll
-        for (int j = 0; j < kSmallBatch; ++j) {
-          const uint32_t k = kb + (uint32_t)j * kSmallConns + c;
+        for (int j = 0; j < kBatch; ++j) {
+          const uint32_t k = kb + (uint32_t)j * NT + c;
+          if (k < nst)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) g[j][i] = load_granule(stage_buf + 4ull * k + i);
+        }
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+          const uint32_t k = kb + (uint32_t)j * NT + c;
           if (k < nst) {
-            lo[j] = __hip_atomic_load(stage_buf + 2ull * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            hi[j] = __hip_atomic_load(stage_buf + 2ull * k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t* q = stage_buf + 4ull * k;
+            st[k] = u32x4{take_granule(q, g[j][0], tag, bad), take_granule(q + 1, g[j][1], tag, bad),
+                          take_granule(q + 2, g[j][2], tag, bad), take_granule(q + 3, g[j][3], tag, bad)};
           }
         }
-#pragma unroll
-        for (int j = 0; j < kSmallBatch; ++j) {
-          const uint32_t k = kb + (uint32_t)j * kSmallConns + c;
-          if (k < nst) st[k] = u32x4{(uint32_t)lo[j], (uint32_t)(lo[j] >> 32), (uint32_t)hi[j], (uint32_t)(hi[j] >> 32)};
-        }
       }
-    } else for (uint32_t k0 = 0; k0 < nst; k0 += kSmallBatch * kSmallConns) {
-      u32x4 x[kSmallBatch];
+      if (bad) s_bad = 1;
+    } else for (uint32_t k0 = 0; k0 < nst; k0 += kBatch * NT) {
+      u32x4 x[kBatch];
 #pragma unroll
-      for (int j = 0; j < kSmallBatch; ++j) {
-        const uint32_t k = k0 + (uint32_t)j * kSmallConns + c;
+      for (int j = 0; j < kBatch; ++j) {
+        const uint32_t k = k0 + (uint32_t)j * NT + c;
         if (k < nst) x[j] = ld16u(in + 16ull * k);
       }
 #pragma unroll
-      for (int j = 0; j < kSmallBatch; ++j) {
-        const uint32_t k = k0 + (uint32_t)j * kSmallConns + c;
+      for (int j = 0; j < kBatch; ++j) {
+        const uint32_t k = k0 + (uint32_t)j * NT + c;
         if (k < nst) st[k] = x[j];
       }
     }
   }
   __syncthreads();
+  if (s_bad) {  // a staged granule never carried this launch's tag (workgroup-uniform)
+    if (c == 0) {
+      gevws_summary sm;
+      memset(&sm, 0, sizeof(sm));
+      sm.status = GEVWS_ERR_DEVICE;
+      *sum = sm;
+    }
+    signal_done(done, seq, ticks, t0, 0);
+    return;
+  }
   uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0, lastf = ~0ull, pos = 0;
   int32_t st = GEVWS_OK;
   if (c < n) {
@@ -1360,7 +1452,7 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
   }
   const uint64_t v[kDecFields] = {nf, pb, pl, err, same};
   uint64_t ex[kDecFields], tot[kDecFields];
-  block_excl_scan<kSmallConns, kDecFields>(v, ex, tot);
+  block_excl_scan<NT, kDecFields>(v, ex, tot);
   const bool ok = tot[0] <= max_frames && tot[1] <= payload_cap;
   if (c == 0) {
     gevws_summary sm;
@@ -1429,7 +1521,7 @@ __global__ __launch_bounds__(kSmallConns) void k_decode_small(const uint8_t* __r
   for (uint32_t b = 0; b < nbig; ++b) {  // the larger payloads, by the whole workgroup
     const uint64_t src = s_big[b][0], poff = s_big[b][1], L = s_big[b][2];
     const uint32_t key = s_bkey[b];
-    for (uint64_t j = c; 16 * j < L; j += kSmallConns) {
+    for (uint64_t j = c; 16 * j < L; j += NT) {
       u32x4 y = lds16(s_in, (uint32_t)(src + 16 * j)) ^ key;
       const int64_t rem = (int64_t)L - (int64_t)(16 * j);
       if (rem < 16) y = keep_bytes(y, rem);
@@ -1457,11 +1549,11 @@ namespace gevws_impl {
 int walk_variant_count() { return kNumWalkVariants; }
 const char* walk_variant_name(int i) { return i >= 0 && i < kNumWalkVariants ? kWalkVariants[i] : nullptr; }
 
-int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
-                 const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
-                 uint8_t* d_payload, uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary) {
-  int r = order_after_last(ctx, st);
-  if (r != GEVWS_OK) return r;
+template <class S>
+static int launch_decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
+                               const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames,
+                               uint64_t max_frames, uint8_t* d_payload, uint64_t payload_cap,
+                               gevws_conn_out* d_conn_out, gevws_summary* d_summary) {
   const uint32_t seq = ctx->done_flag ? ++ctx->done_seq : 0u;
   // a pass that signals a mapped flag is a live pass over mapped host memory:
   // its input is read by kSmallStageWGs-wide slices (k_decode_small)
@@ -1470,20 +1562,40 @@ int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
     const uint64_t nst = (in_bytes + GEVWS_IN_PAD) / 16;
     const uint64_t w = (nst + kSmallSliceChunks - 1) / kSmallSliceChunks;
     nwg = (uint32_t)(w < kSmallStageWGs ? w : kSmallStageWGs);
+    // the staging granules: 4 per 16-byte chunk of the wide shape's input, zeroed once
+    const size_t sbytes = 4ull * sizeof(uint64_t) * SmallWide::kStage;
     if (nwg > 1 && !ctx->d_small_stage &&
-        hipMalloc(reinterpret_cast<void**>(&ctx->d_small_stage), 16ull * kSmallStage) != hipSuccess) {
+        (hipMalloc(reinterpret_cast<void**>(&ctx->d_small_stage), sbytes) != hipSuccess ||
+         hipMemsetAsync(ctx->d_small_stage, 0, sbytes, st) != hipSuccess)) {
+      if (ctx->d_small_stage) (void)hipFree(ctx->d_small_stage);
       ctx->d_small_stage = nullptr;
       nwg = 1;
     }
   }
-  k_decode_small<<<nwg, kSmallConns, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
-                                               payload_cap, d_conn_out, d_summary, ctx->done_flag, seq,
-                                               ctx->done_flag ? ctx->ticks : nullptr, ctx->d_small_stage,
-                                               ctx->d_done + kSmallStageCounter);
+  const uint32_t tag = nwg > 1 ? next_hand_tag(ctx) : 0u;
+  k_decode_small<S><<<nwg, S::NT, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
+                                           payload_cap, d_conn_out, d_summary, ctx->done_flag, seq,
+                                           ctx->done_flag ? ctx->ticks : nullptr, ctx->d_small_stage,
+                                           ctx->d_done + kSmallStageCounter, tag);
   GEVWS_HIP(hipGetLastError());
-  r = mark_last(ctx, st);
+  const int r = mark_last(ctx, st);
   if (ctx->done_flag) ctx->last_signal = seq;
   return r;
+}
+
+int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
+                 const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
+                 uint8_t* d_payload, uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary) {
+  if (n_conns > kOneLaunchConns || in_bytes > kOneLaunchBytes) return GEVWS_ERR_INVALID;
+  const int r = order_after_last(ctx, st);
+  if (r != GEVWS_OK) return r;
+  // the narrow shape whenever the pass fits it: a quarter of the lanes to
+  // launch and synchronise, and a CU keeps room for other work
+  if (n_conns <= kSmallConns && in_bytes <= kSmallBytes)
+    return launch_decode_small<SmallNarrow>(ctx, st, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames,
+                                            d_payload, payload_cap, d_conn_out, d_summary);
+  return launch_decode_small<SmallWide>(ctx, st, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
+                                        payload_cap, d_conn_out, d_summary);
 }
 
 int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
@@ -1559,6 +1671,7 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   const bool fused = nblk > 0 && nblk <= kFusedScanMaxBlocks;
   constexpr int kDecScanBlock = 256;
   uint32_t* done = fused ? ctx->d_done : nullptr;
+  const uint32_t tag = fused ? next_hand_tag(ctx) : 0u;
   // the walk's uniform-stream speculation (D = 8) pays on long runs of equal
   // frames (C2, C3: -23..-28 %) and costs 2-7 % elsewhere (C1, C4,
   // profiles/r02/r02_walk_store_count_ab.jsonl); after a decode on this context
@@ -1568,7 +1681,8 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   if (nblk && ks > 1) {
 #define GEVWS_SPLIT(K)                                                                                            \
   (plain ? k_walk_split<K, 0> : k_walk_split<K, 8>)<<<nblk, kCountBlock, 0, st>>>(                                \
-      d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb_w, in_bytes, done, max_frames, payload_cap, \
+      d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb_w, in_bytes, done, ctx->d_walk_part, tag,     \
+      max_frames, payload_cap,                                                                                      \
       d_summary, segs, sout, srec, ctx->split_min_bytes)
     if (ks == 2) GEVWS_SPLIT(2);
     else if (ks == 4) GEVWS_SPLIT(4);
@@ -1580,12 +1694,12 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
     // many chains: the walk is bound by its line traffic -- entries through
     // each lane's LDS ring to the workgroup's writer wave (k_walk_count ST 2)
     (plain ? k_walk_count<0, 2> : k_walk_count<8, 2>)<<<nblk, 2 * kCountBlock, 0, st>>>(
-        d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes, done, max_frames, payload_cap,
-        d_summary);
+        d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes, done, ctx->d_walk_part, tag,
+        max_frames, payload_cap, d_summary);
   } else if (nblk) {
     (plain ? k_walk_count<0, 0> : k_walk_count<8, 0>)<<<nblk, kCountBlock, 0, st>>>(
-        d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes, done, max_frames, payload_cap,
-        d_summary);
+        d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb, in_bytes, done, ctx->d_walk_part, tag,
+        max_frames, payload_cap, d_summary);
   }
   if (ev) GEVWS_HIP(hipEventRecord(ev[1], st));
   if (!fused) k_scan_blocks<true, kDecFields, kDecScanBlock><<<1, kDecScanBlock, 0, st>>>(blk, nblk, max_frames, payload_cap,

@@ -84,7 +84,6 @@
 #include <cstring>
 #include <random>
 #include <string>
-#include <string>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -95,6 +94,10 @@ namespace wslb {
 
 inline std::atomic<bool> g_stop{false};
 inline std::atomic<uint64_t> g_batches{0}, g_batch_conns{0}, g_frames{0}, g_bad{0}, g_dev_ns{0};
+// frames echoed per server loop (fairness across loops: "loop_echoes_per_s")
+constexpr int kMaxLoops = 64;
+inline std::atomic<uint64_t> g_loop_frames[kMaxLoops];
+inline std::atomic<uint64_t> g_loop_conns[kMaxLoops];  // connections accepted per loop (SO_REUSEPORT hashing)
 // every loop's decoders' pass timelines (Decoder::kTimeline), summed at loop exit
 inline std::mutex g_tl_mu;
 inline gevws_protocol_timeline g_tl{};
@@ -289,6 +292,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
             s->out.insert(s->out.end(), rp, rp + rl);
           }
           g_frames.fetch_add(1, std::memory_order_relaxed);
+          g_loop_frames[index % kMaxLoops].fetch_add(1, std::memory_order_relaxed);
           g_payload.fetch_add(len, std::memory_order_relaxed);
         }
       } else if (st == GEVWS_OK) {
@@ -298,6 +302,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
         s->out.insert(s->out.end(), hdr, hdr + hn);
         s->out.insert(s->out.end(), data, data + len);
         g_frames.fetch_add(1, std::memory_order_relaxed);
+        g_loop_frames[index % kMaxLoops].fetch_add(1, std::memory_order_relaxed);
         g_payload.fetch_add(len, std::memory_order_relaxed);
       } else if (len != 0) {
         s->out.insert(s->out.end(), data, data + len);  // handshake response (wrap.go:40-42)
@@ -384,6 +389,7 @@ void server_loop(int port, int device, std::atomic<int>* ready, int index) {
           gevws_conn_set_upgraded(sc.c, 0);
           conns.emplace(cfd, std::move(sc));
           g_live.fetch_add(1);  // OnConnect
+          g_loop_conns[index % kMaxLoops].fetch_add(1, std::memory_order_relaxed);
           epoll_event ce{};
           ce.events = EPOLLIN;
           ce.data.fd = cfd;
@@ -954,16 +960,37 @@ int loopback_main(int argc, char** argv) {
   std::this_thread::sleep_for(std::chrono::duration<double>(warm));
   const uint64_t f0 = g_frames.load(), b0 = g_batches.load(), c0 = g_batch_conns.load(), d0 = g_dev_ns.load();
   const uint64_t p0 = g_payload.load();
+  std::vector<uint64_t> lf0(kMaxLoops), lf1(kMaxLoops);
+  for (int l = 0; l < kMaxLoops; ++l) lf0[l] = g_loop_frames[l].load();
   const double ts = now_s();
   std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
   const double te = now_s();
   const uint64_t f1 = g_frames.load(), b1 = g_batches.load(), c1 = g_batch_conns.load(), d1 = g_dev_ns.load();
   const uint64_t p1 = g_payload.load();
+  for (int l = 0; l < kMaxLoops; ++l) lf1[l] = g_loop_frames[l].load();
   for (auto& t : clients) t.join();
   g_stop = true;
   for (auto& t : servers) t.join();
   const double dt = te - ts;
   const double mps = (double)(f1 - f0) / dt;
+  // per-loop echo rates and connection counts (loops beyond kMaxLoops share
+  // slots); fairness = min / max over loops of the echo rate per connection
+  std::string per_loop = "[", per_conns = "[";
+  double lmin = 0, lmax = 0;
+  for (int l = 0; l < std::min(loops, kMaxLoops); ++l) {
+    const double r = (double)(lf1[l] - lf0[l]) / dt;
+    const uint64_t nc = g_loop_conns[l].load();
+    const double rc = nc ? r / (double)nc : 0.0;
+    lmin = l == 0 ? rc : std::min(lmin, rc);
+    lmax = l == 0 ? rc : std::max(lmax, rc);
+    char b[64];
+    snprintf(b, sizeof(b), "%s%.0f", l ? ", " : "", r);
+    per_loop += b;
+    snprintf(b, sizeof(b), "%s%llu", l ? ", " : "", (unsigned long long)nc);
+    per_conns += b;
+  }
+  per_loop += "]";
+  per_conns += "]";
   if (!g_cfg.transcript.empty()) {
     FILE* tf = fopen(g_cfg.transcript.c_str(), "w");
     if (!tf) {
@@ -985,14 +1012,16 @@ int loopback_main(int argc, char** argv) {
          "\"mean_conns_per_pass\": %.1f, \"decode_us_per_pass\": %.1f, \"decode_share_of_loop_time\": %.3f, "
          "\"client_checked_echoes\": %llu, \"mode\": \"%s\", \"control_frames\": %llu, "
          "\"async_sends\": %llu, \"closes_answered\": %llu, \"transcript_pairs\": %zu, \"devices\": %d, "
-         "\"pass_timeline_us\": %s, \"errors\": %llu}\n",
+         "\"pass_timeline_us\": %s, \"loop_echoes_per_s\": %s, \"loop_conns\": %s, "
+         "\"loop_min_over_max_per_conn\": %.3f, "
+         "\"errors\": %llu}\n",
          Decoder::path(), Decoder::name(), conns, upgraded.load(), wss ? (size_t)0 : msg, loops, cthreads, dt, mps,
          (double)(p1 - p0) / dt / 1048576.0, (double)(b1 - b0) / dt,
          b1 > b0 ? (double)(c1 - c0) / (double)(b1 - b0) : 0.0,
          b1 > b0 ? (double)(d1 - d0) / 1e3 / (double)(b1 - b0) : 0.0, (double)(d1 - d0) / 1e9 / (dt * loops),
          (unsigned long long)total.load(), wss ? "wsserver" : "echo", (unsigned long long)g_ctrl.load(),
          (unsigned long long)g_sent_async.load(), (unsigned long long)g_closed.load(), g_transcript.size(), ndev,
-         timeline_json().c_str(), (unsigned long long)g_bad.load());
+         timeline_json().c_str(), per_loop.c_str(), per_conns.c_str(), lmax > 0 ? lmin / lmax : 0.0, (unsigned long long)g_bad.load());
   return g_bad.load() == 0 && upgraded.load() == conns ? 0 : 1;
 }
 

@@ -60,6 +60,10 @@ enum {
 #define GEVWS_PAYLOAD_ALIGN 16
 /* Output-arena tile (bytes) of the unmask kernel's work map. */
 #define GEVWS_TILE 4096
+/* The one-launch decode's limits (GEVWS_TUNE_SMALL_BATCH): batches of at most
+ * this many connections and input bytes run as ONE kernel launch. */
+#define GEVWS_ONE_LAUNCH_MAX_CONNS 1024u
+#define GEVWS_ONE_LAUNCH_MAX_BYTES (128u * 1024u)
 
 /* ws.Header, plugins/websocket/ws/frame.go:169-176.  Byte-identical to the Go
  * struct {Fin bool; Rsv byte; OpCode OpCode; Masked bool; Mask [4]byte;
@@ -163,10 +167,11 @@ int gevws_ctx_order_after_last(gevws_ctx *ctx, void *stream);
  * speculation; 2 = no per-frame entries, the record pass re-walks every
  * chain; 3 = the entries through the writer wave whatever the batch size),
  * GEVWS_TUNE_SMALL_BATCH the input size in bytes (default and maximum
- * 65 536; 0 = never) up to which a batch of at most 256 connections is
- * decoded by ONE kernel launch -- walk, scan, records and unmask in a single
- * workgroup -- when every other knob is at its default and per-phase timing
- * is off, GEVWS_TUNE_SPLIT_LANES the lanes per connection of the default
+ * GEVWS_ONE_LAUNCH_MAX_BYTES = 131 072; 0 = never) up to which a batch of at
+ * most GEVWS_ONE_LAUNCH_MAX_CONNS = 1 024 connections is decoded by ONE kernel
+ * launch -- walk, scan, records and unmask in a single workgroup with the
+ * input staged in LDS -- when every other knob is at its default and
+ * per-phase timing is off, GEVWS_TUNE_SPLIT_LANES the lanes per connection of the default
  * walk's split form (k_walk_split: lanes guess frame starts inside the stream
  * and walk the segments between the guesses; a connection whose guesses do
  * not all line up is re-walked serially, so the output never depends on

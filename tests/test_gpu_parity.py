@@ -22,9 +22,9 @@ def small_path(engine, request):
     the multi-kernel path (walk, scan, records, unmask) must give the same
     bytes, so the core parity tests run both."""
     from gev_amd import _abi
-    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536 if request.param == "one_launch" else 0)
+    engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES if request.param == "one_launch" else 0)
     yield request.param
-    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+    engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES)
 
 
 # --------------------------------------------------------------------------- golden vectors
@@ -787,7 +787,7 @@ def test_completion_flag_signals_one_launch_passes(engine):
             seen.append(seq)
         assert seen == sorted(set(seen))
         gpu_decode(engine, *big)
-        assert engine.completion_seq == -1  # > 64 KiB: the multi-kernel decode
+        assert engine.completion_seq == -1  # > 128 KiB: the multi-kernel decode
         torch.cuda.synchronize()
     finally:
         engine.set_completion_flag(None)
@@ -880,39 +880,61 @@ def _frames_of_exactly(rng, nbytes: int) -> bytes:
 
 @pytest.mark.gpu
 def test_one_launch_decode_at_its_limits(engine):
-    """The one-launch decode stages its whole input (<= 64 KiB + the 64-byte
-    pad) in LDS (round 5): batches of exactly 65 536 bytes -- 256 connections
-    ending on the last byte, the last one with a cut frame; one connection of
-    frames and a 5-byte tail; 255 empty connections beside one 65 528-byte
-    payload frame (h = 8); a 6-byte frame whose header starts 6 bytes before the end
-    -- bit-exact against the C oracle, in one launch and in the multi-kernel
-    path; the one launch also with a completion flag set, which stages the
-    input through 32 workgroups' slices (a live pass's form)."""
+    """The one-launch decode stages its whole input in LDS, in two shapes
+    (round 6): 256 lanes / 64 KiB and 1 024 lanes / 128 KiB.  At each shape's
+    limits -- N connections ending on the last byte of exactly B bytes, the
+    last one with a cut frame; one connection of frames and a 5-byte tail;
+    N - 1 empty connections beside one payload frame filling B; a 6-byte frame
+    whose header starts 6 bytes before the end -- and just past the narrow
+    shape's (257 connections; 65 537 bytes): bit-exact against the C oracle in
+    one launch and in the multi-kernel path; the one launch also with a
+    completion flag set, which stages the input through up to 32 workgroups'
+    tagged slices (a live pass's form).  A batch past the wide shape (1 025
+    connections; 131 073 bytes) takes the multi-kernel path."""
     import torch
     from gev_amd import _abi
     rng = np.random.default_rng(65536)
-    cases = []
-    streams = [random_stream(rng, int(rng.integers(0, 3)), max_len=200, tail=False) for _ in range(255)]
-    last = 65536 - sum(len(s) for s in streams)
-    streams.append(_frames_of_exactly(rng, last + 300)[:last])  # cut inside a frame
-    cases.append(pack_streams(streams))
-    cases.append(pack_streams([_frames_of_exactly(rng, 65531) + b"\x82\x85\x01\x02\x03"]))
-    big = wo.encode_frame(bytes(rng.integers(0, 256, 65528, dtype=np.uint8)), 2, True, 0, True, b"\x0a\x0b\x0c\x0d")
-    assert len(big) == 65536
-    cases.append(pack_streams([b""] * 255 + [big]))
-    cases.append(pack_streams([_frames_of_exactly(rng, 65530) + wo.encode_frame(b"", 9, True, 0, True, b"\1\2\3\4")]))
+
+    def at_limits(n_conns, nbytes, max_len):
+        cases = []
+        streams = [random_stream(rng, int(rng.integers(0, 3)), max_len=max_len, tail=False)
+                   for _ in range(n_conns - 1)]
+        last = nbytes - sum(len(s) for s in streams)
+        assert last > 300
+        streams.append(_frames_of_exactly(rng, last + 300)[:last])  # cut inside a frame
+        cases.append(pack_streams(streams))
+        cases.append(pack_streams([_frames_of_exactly(rng, nbytes - 5) + b"\x82\x85\x01\x02\x03"]))
+        L = nbytes - (8 if nbytes - 8 <= 0xFFFF else 14)
+        big = wo.encode_frame(bytes(rng.integers(0, 256, L, dtype=np.uint8)), 2, True, 0, True, b"\x0a\x0b\x0c\x0d")
+        assert len(big) == nbytes
+        cases.append(pack_streams([b""] * (n_conns - 1) + [big]))
+        cases.append(pack_streams([_frames_of_exactly(rng, nbytes - 6) + wo.encode_frame(b"", 9, True, 0, True,
+                                                                                          b"\1\2\3\4")]))
+        return cases
+
+    narrow = at_limits(256, 65536, 200)
+    wide = at_limits(1024, 131072, 100)
+    past_narrow = [pack_streams([random_stream(rng, 1, max_len=120, tail=False) for _ in range(257)]),
+                   pack_streams([_frames_of_exactly(rng, 65537)])]
+    past_wide = [pack_streams([random_stream(rng, 1, max_len=60, tail=False) for _ in range(1025)]),
+                 pack_streams([_frames_of_exactly(rng, 131073)])]
+    for arena, conns in narrow:
+        assert len(arena) == 65536 and conns.shape[0] <= 256
+    for arena, conns in wide:
+        assert len(arena) == 131072 and conns.shape[0] <= 1024
+    assert past_wide[0][1].shape[0] == 1025 and len(past_wide[1][0]) == 131073
     flag = gev_amd.PinnedArena(4096)
     try:
-        for sb, flagged in ((65536, False), (65536, True), (0, False)):
+        for sb, flagged in ((_abi.ONE_LAUNCH_MAX_BYTES, False), (_abi.ONE_LAUNCH_MAX_BYTES, True), (0, False)):
             engine.set_tuning(_abi.TUNE_SMALL_BATCH, sb)
             engine.set_completion_flag(flag if flagged else None, 64)
-            for k, (arena, conns) in enumerate(cases):
-                assert len(arena) == 65536 and conns.shape[0] <= 256, k
+            for k, (arena, conns) in enumerate(narrow + wide + past_narrow + past_wide):
                 assert_matches_oracle(engine, arena, conns, f"case {k} small_batch {sb} flagged {flagged}")
                 if flagged:
-                    assert engine.completion_seq > 0
+                    one = k < len(narrow + wide + past_narrow)
+                    assert (engine.completion_seq > 0) == one, k
     finally:
-        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES)
         engine.set_completion_flag(None)
         torch.cuda.synchronize()
         flag.close()

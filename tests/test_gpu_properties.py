@@ -37,11 +37,11 @@ SETTINGS = settings(max_examples=300, deadline=None,
 @given(st.lists(streams, min_size=1, max_size=8), st.booleans())
 def test_device_decode_equals_oracle(engine, ss, one_launch):
     arena, conns = pack_streams(ss)
-    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536 if one_launch else 0)
+    engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES if one_launch else 0)
     try:
         assert_matches_oracle(engine, arena, conns, f"one_launch={one_launch}")
     finally:
-        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES)
 
 
 @SETTINGS
@@ -241,7 +241,7 @@ def test_split_walk_equals_oracle(engine, ss, lanes):
     finally:
         engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
         engine.set_tuning(_abi.TUNE_SPLIT_MIN_BYTES, 16384)
-        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES)
 
 
 def _masked_frames_np(rng, lens, masked, forms):

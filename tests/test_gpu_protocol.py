@@ -627,18 +627,63 @@ def test_pass_timeline_small_zero_copy_pass(engine):
     assert t["ns_gpu_handler"] == 0 and t["ns_gpu_gap"] == 0
 
 
-def test_contexts_cycle_stream_priorities():
+def test_pass_timeline_with_device_handler(engine):
+    """The timeline's handler slot: a small zero-copy pass with the
+    device handler on chains the one-launch handler step behind the decode;
+    both kernels stamp their ticks, so the pass reports the handler's GPU time
+    and the gap between the two kernels (>= 0), and every pass is answered by
+    the completion flag.  The replies are still oracle/ws_oracle.on_message's."""
+    rng = np.random.default_rng(6)
+    policy = wo.HANDLER_ECHO_TEXT
+    proto = gev_amd.Protocol(engine)
+    proto.set_handler(policy)
+    conns = [gev_amd.Connection() for _ in range(16)]  # ~30 KB: <= 1 024 records, the one-launch handler
+    rings, streams = [], []
+    for c in conns:
+        s = b"".join(_control_mix(rng, 3))
+        r = gev_amd.RingBuffer(4096)
+        r.write(s)
+        rings.append(r)
+        streams.append(s)
+    for k in range(3):
+        proto.unpacket_batch(conns, rings)
+        for c, r, s in zip(conns, rings, streams):
+            for fr in wo.decode_stream(s).frames:
+                h, data = proto.unpacket(c, r)
+                assert data == fr.payload
+                assert proto.reply(c) == wo.on_message(fr.header, fr.payload, policy)
+            r.write(s)
+    t = proto.timeline()
+    st = proto.stats()
+    assert st["chained_handler_passes"] == 3 and st["handler_passes"] == 3, st
+    assert t["passes"] == 3 and t["signalled"] == 3, t
+    assert t["ns_gpu_decode"] > 0 and t["ns_gpu_handler"] > 0 and t["ns_gpu_gap"] >= 0, t
+    assert t["ns_gpu_decode"] + t["ns_gpu_handler"] < t["ns_wait"] + t["ns_launch"], t
+
+
+@pytest.mark.parametrize("mode", ["default", "all", "normal"])
+def test_contexts_cycle_stream_priorities(mode, monkeypatch):
     """One context per event loop: successive contexts on a device cycle their
-    stream's priority over the device's range (each level has its own hardware
-    queues, so eight loops' passes run side by side instead of three at a time,
-    profiles/r05/r05u_queue_probe.jsonl), and each still decodes exactly."""
+    stream's priority (each level has its own hardware queues, so eight loops'
+    passes run side by side instead of three at a time,
+    profiles/r05/r05u_queue_probe.jsonl).  By default only over the normal
+    level and those below it -- a context never outranks the application's
+    own normal-priority work; GEVWS_STREAM_PRIORITIES=all adds the
+    levels above, =normal keeps every context at 0.  Each still decodes
+    exactly."""
     import torch
 
-    least, greatest = torch.cuda.Stream.priority_range()
-    engines = [gev_amd.Engine(0) for _ in range(least - greatest + 1)]
+    if mode != "default":
+        monkeypatch.setenv("GEVWS_STREAM_PRIORITIES", mode)
+    engines = [gev_amd.Engine(0) for _ in range(6)]
     prios = [torch.cuda.ExternalStream(int(gev_amd.lib.gevws_ctx_stream(e._ctx)), device="cuda:0").priority
              for e in engines]
-    assert len(set(prios)) == len(engines), prios
+    if mode == "normal":
+        assert set(prios) == {0}, prios
+    elif mode == "default":
+        assert min(prios) == 0 and len(set(prios)) >= 2, prios  # (the box's range is -1 .. 1)
+    else:
+        assert min(prios) < 0 < max(prios) and len(set(prios)) >= 3, prios
     rng = np.random.default_rng(9)
     for e in engines:
         proto = gev_amd.Protocol(e)

@@ -118,7 +118,7 @@ def test_split_walk_matches_oracle(engine, split_cases, lanes, min_seg):
     finally:
         engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
         engine.set_tuning(_abi.TUNE_SPLIT_MIN_BYTES, 16384)
-        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES)
 
 
 def test_split_walk_streams_outside_the_arena(engine, split_cases):
@@ -180,7 +180,7 @@ def test_split_walk_auto_choice(engine, split_cases):
         assert_matches_oracle(engine, *bigs, "auto: big frames again")
         assert engine.last_split_lanes == 1
     finally:
-        engine.set_tuning(_abi.TUNE_SMALL_BATCH, 65536)
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES)
 
 
 def test_wide_unmask_grid_after_mixed_batch(engine):
