@@ -82,6 +82,23 @@ def build_layout(name: str, rank: int, conns: int | None, world: int = 1, scalin
     return lay, lay
 
 
+HBM_BYTES_PER_GPU = 288 * 10**9  # MI355X HBM3E
+
+
+def hbm_need_bytes(lay, inflight: int = 1) -> int:
+    """Device memory one rank allocates for its batch, an upper estimate
+    checked before anything is allocated: the input arena (+ pad), the frame
+    descriptors and connection table, and per batch in flight the outputs
+    (payload arena, 32-byte records, 24-byte per-connection results) and the
+    decode context's scratch -- the walk's 8-byte frame entries (one per 64
+    input bytes, in 32-entry slot runs per connection), the output-tile map
+    and the block partials (gevws_walk.hip decode_front)."""
+    entries = 32 * ((lay.arena_bytes >> 11) + lay.n_conns + 1) * 8
+    scratch = entries + (lay.payload_padded // 4096 + 2) * 4 + lay.n_conns * 64 + (1 << 20)
+    out = lay.payload_padded + 16 + lay.n_frames * 32 + lay.n_conns * 24 + 4096
+    return lay.arena_bytes + 64 + lay.desc.nbytes + lay.conns.nbytes + inflight * (out + scratch)
+
+
 def cpu_sample_layout(name: str, mib: int = 256):
     """A bounded sample of the same workload for the CPU baseline: `mib` MiB of
     payload (>= 64 MiB of input per thread, so the sample is not cache-resident)."""
@@ -134,7 +151,7 @@ def all_host_threads() -> int:
         return os.cpu_count() or 1
 
 
-def cpu_baseline(name: str, seconds: float, threads: int, vectorized: bool = False):
+def cpu_baseline(name: str, seconds: float, threads: int, vectorized: bool = False, alloc: str = "fresh"):
     import numpy as np
     from gev_amd import workloads as w
     from oracle import ref
@@ -143,12 +160,15 @@ def cpu_baseline(name: str, seconds: float, threads: int, vectorized: bool = Fal
     lay = cpu_sample_layout(name, min(4096, max(256, 64 * threads)))
     arena = np.concatenate([w.synth_host(lay), np.zeros(64, np.uint8)])
     secs, pb, nf = ref.bench_pipeline(arena, lay.conns[:, 0], lay.conns[:, 1], threads=threads,
-                                      min_seconds=seconds, vectorized=vectorized)
-    return dict(value=round(pb / secs / 2**30, 4), unit="GiB/s", cores=threads, kind="port",
+                                      min_seconds=seconds, vectorized=vectorized, alloc=alloc)
+    where = (f"make() from a per-thread bump arena of {ref.fresh_arena_bytes() >> 20} MiB (2 x the LLC a CPU sees, "
+             "at least 64 MiB; fresh memory as Go's swept spans)" if alloc == "fresh" else
+             "make() as calloc/free per frame (glibc recycles one cache-warm chunk)")
+    return dict(value=round(pb / secs / 2**30, 4), unit="GiB/s", cores=threads, kind="port", alloc=alloc,
                 frames_per_s=round(nf / secs, 1), host=host_cpu_info(),
                 sample=(f"{lay.name}, {lay.n_conns} connections round-robin over {threads} thread(s), "
                         f"repeated for >= {seconds:.0f} s; oracle/ws_ref.c per-frame UnPacket pipeline "
-                        "(header parse, zero-filled make, ring Read copy, Cipher u64 loop), "
+                        f"(header parse, zero-filled make, ring Read copy, Cipher u64 loop); {where}; "
                         + ("gcc -O3 -mavx2 (auto-vectorised)" if vectorized else "gcc -O2 -fno-tree-vectorize")))
 
 
@@ -281,6 +301,7 @@ def dry_run(args) -> None:
     lay, glob = build_layout(args.config, rank, args.conns, world, scaling)
     counts = torch.tensor([lay.n_frames, lay.payload_len, 0], dtype=torch.int64)
     dist.reduce_counts(counts)
+    need_max = int(dist.max_over_ranks(float(hbm_need_bytes(lay, max(1, args.inflight))), "cpu"))
     dist.barrier()
     elapsed = dist.max_over_ranks(0.0, "cpu")
     if rank == 0:
@@ -293,7 +314,7 @@ def dry_run(args) -> None:
                        "global_connections": glob.n_conns if scaling == "strong" else glob.n_conns * world,
                        "parallelism": f"connections sharded over {world} rank(s); {dist.backend()} all-reduce of counts"},
             "decoded_per_step": {"frames": c[0], "payload_bytes": c[1], "errors": c[2], "ranks_summed": world},
-            "max_over_ranks_s": elapsed, "dry_run": True}), flush=True)
+            "hbm_need_bytes_per_rank": need_max, "max_over_ranks_s": elapsed, "dry_run": True}), flush=True)
     dist.finalize()
 
 
@@ -382,6 +403,13 @@ def main():
         raise SystemExit(f"rank {rank}: no connections in this rank's share ({glob.n_conns} in the batch)")
     log(f"rank {rank}: {lay.name}: {lay.n_frames} frames, {lay.n_conns} connections, "
         f"{lay.arena_bytes / 2**30:.2f} GiB in, {lay.payload_padded / 2**30:.2f} GiB out")
+    # every rank checks its device memory before allocating: a rank that cannot
+    # hold its batch exits non-zero here (no line, nothing launched)
+    need = hbm_need_bytes(lay, M)
+    free_b, total_b = torch.cuda.mem_get_info(dev)
+    if need > free_b:
+        raise SystemExit(f"rank {rank}: the batch needs {need / 2**30:.1f} GiB of device memory, "
+                         f"{free_b / 2**30:.1f} GiB free of {total_b / 2**30:.1f} GiB; refusing to run")
     if args.input_mem == "default":
         arena = torch.empty(lay.arena_bytes + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
         arena[lay.arena_bytes:] = 0
@@ -600,6 +628,15 @@ def main():
         log("cpu baseline (1 thread, auto-vectorised build)...")
         result["cpu_baseline_vectorized"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0), 1,
                                                          vectorized=True)
+        # the same pipeline with make() recycling one cache-warm chunk (calloc /
+        # free): the flattering variant, beside the fresh-memory legs above
+        log("cpu baseline (1 thread, cache-hot allocation)...")
+        result["cpu_baseline_cache_hot"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0), 1,
+                                                        alloc="cache_hot")
+        if "cpu_baseline_quota" in result:
+            log(f"cpu baseline ({nq} threads, cache-hot allocation)...")
+            result["cpu_baseline_quota_cache_hot"] = cpu_baseline(args.config, max(args.cpu_seconds / 2, 1.0), nq,
+                                                                  alloc="cache_hot")
     print(json.dumps(result), flush=True)
     dist.finalize()
 

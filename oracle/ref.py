@@ -45,6 +45,9 @@ def vec_lib():
         L.wsref_bench_pipeline.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_int, ctypes.c_double,
                                            P, P, P]
         L.wsref_bench_pipeline.restype = ctypes.c_double
+        L.wsref_bench_pipeline_alloc.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_int, ctypes.c_double,
+                                                 ctypes.c_int, ctypes.c_uint64, P, P, P]
+        L.wsref_bench_pipeline_alloc.restype = ctypes.c_double
         _VEC = L
     return _VEC
 
@@ -68,6 +71,9 @@ def lib():
         L.wsref_bench_pipeline.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_int, ctypes.c_double,
                                            P, P, P]
         L.wsref_bench_pipeline.restype = ctypes.c_double
+        L.wsref_bench_pipeline_alloc.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_int, ctypes.c_double,
+                                                 ctypes.c_int, ctypes.c_uint64, P, P, P]
+        L.wsref_bench_pipeline_alloc.restype = ctypes.c_double
         _LIB = L
     return _LIB
 
@@ -115,18 +121,51 @@ def decode_batch(arena: np.ndarray, conn_off: np.ndarray, conn_len: np.ndarray,
                 total_payload=tp)
 
 
+ALLOC_FRESH, ALLOC_CACHE_HOT = 0, 1  # ws_ref.c WSREF_ALLOC_*
+
+
+def llc_slice_bytes() -> int:
+    """The last-level cache one CPU sees (cpu0's highest cache index), or 32 MiB."""
+    base = "/sys/devices/system/cpu/cpu0/cache"
+    best = 0
+    try:
+        for d in os.listdir(base):
+            if not d.startswith("index"):
+                continue
+            sz = open(os.path.join(base, d, "size")).read().strip()
+            mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}.get(sz[-1:], 1)
+            best = max(best, int(sz.rstrip("KMG")) * mult)
+    except (OSError, ValueError):
+        pass
+    return best or (32 << 20)
+
+
+def fresh_arena_bytes() -> int:
+    """Per-thread arena of the fresh-allocation mode: twice the LLC one CPU
+    sees, at least 64 MiB -- a thread's destinations are never cache-resident."""
+    return max(64 << 20, 2 * llc_slice_bytes())
+
+
 def bench_pipeline(arena: np.ndarray, conn_off: np.ndarray, conn_len: np.ndarray,
-                   threads: int = 1, min_seconds: float = 10.0, vectorized: bool = False):
+                   threads: int = 1, min_seconds: float = 10.0, vectorized: bool = False,
+                   alloc: str = "fresh"):
     """Time the reference per-frame pipeline; returns (seconds, payload_bytes, frames).
-    vectorized=True times the -O3 -mavx2 build of the same C source."""
+    vectorized=True times the -O3 -mavx2 build of the same C source.  alloc:
+    "fresh" (each frame's zero-filled destination from a per-thread bump arena
+    of fresh_arena_bytes(), as Go's make hands out swept memory) or
+    "cache_hot" (calloc / free per frame: glibc recycles one warm chunk)."""
     pb = np.zeros(1, dtype=np.uint64)
     nf = np.zeros(1, dtype=np.uint64)
     ck = np.zeros(1, dtype=np.uint64)
     conn_off = np.ascontiguousarray(conn_off, dtype=np.uint64)
     conn_len = np.ascontiguousarray(conn_len, dtype=np.uint64)
     L = vec_lib() if vectorized else lib()
-    secs = L.wsref_bench_pipeline(_ptr(arena), _ptr(conn_off), _ptr(conn_len), conn_off.size,
-                                      threads, min_seconds, _ptr(pb), _ptr(nf), _ptr(ck))
+    mode = {"fresh": ALLOC_FRESH, "cache_hot": ALLOC_CACHE_HOT}[alloc]
+    secs = L.wsref_bench_pipeline_alloc(_ptr(arena), _ptr(conn_off), _ptr(conn_len), conn_off.size,
+                                        threads, min_seconds, mode, fresh_arena_bytes(),
+                                        _ptr(pb), _ptr(nf), _ptr(ck))
+    if secs < 0:
+        raise MemoryError("wsref_bench_pipeline_alloc: arena allocation failed")
     return secs, int(pb[0]), int(nf[0])
 
 

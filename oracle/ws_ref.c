@@ -147,9 +147,35 @@ int64_t wsref_decode_batch(const uint8_t *in, const uint64_t *conn_off, const ui
  * The reference per-frame pipeline, as UnPacket does it for each frame:
  * header parse; payload := make([]byte, L) (zero-filled); ring.Read(payload)
  * (memcpy); Cipher if masked; the slice is handed to the handler and later
- * collected (free).  A checksum keeps the work observable. */
+ * collected.  A checksum keeps the work observable.
+ *
+ * Where make's memory comes from (alloc_mode):
+ *   WSREF_ALLOC_FRESH (the baseline): a per-thread bump arena, reset when it
+ *     runs out, whose size keeps the threads' arenas together larger than the
+ *     host's last-level cache -- each frame's destination is memory the loop
+ *     has not touched for a while, as Go's make hands out spans the collector
+ *     swept (protocol.go:50), zero-filled like make;
+ *   WSREF_ALLOC_CACHE_HOT: calloc + free per frame -- glibc hands the same
+ *     chunk back each time, so the destination stays in L1/L2 (flatters the
+ *     CPU; kept as a second number). */
+enum { WSREF_ALLOC_FRESH = 0, WSREF_ALLOC_CACHE_HOT = 1 };
+
+typedef struct {
+    uint8_t *base;
+    uint64_t cap, top;
+} bump_arena;
+
+static uint8_t *arena_make(bump_arena *a, size_t L) {
+    const uint64_t need = (L + 63) & ~(uint64_t)63;
+    if (a->top + need > a->cap) a->top = 0;  /* the sweep starts over: the oldest memory */
+    uint8_t *p = a->base + a->top;
+    a->top += need;
+    memset(p, 0, L);  /* make's zero fill */
+    return p;
+}
+
 static uint64_t pipeline_stream(const uint8_t *s, uint64_t len, uint64_t *frames_out,
-                                uint64_t *payload_out) {
+                                uint64_t *payload_out, bump_arena *arena) {
     uint64_t pos = 0, nf = 0, pb = 0, ck = 0;
     for (;;) {
         wsref_header h;
@@ -157,11 +183,11 @@ static uint64_t pipeline_stream(const uint8_t *s, uint64_t len, uint64_t *frames
         if (wsref_read_header(s + pos, len - pos, &h, &hl) != WSREF_OK) break;
         if (len - pos - hl < (uint64_t)h.length) break;
         size_t L = (size_t)h.length;
-        uint8_t *payload = (uint8_t *)calloc(L ? L : 1, 1);
+        uint8_t *payload = arena ? arena_make(arena, L) : (uint8_t *)calloc(L ? L : 1, 1);
         memcpy(payload, s + pos + hl, L);
         if (h.masked) wsref_cipher(payload, L, h.mask, 0);
         if (L) ck += payload[0] + payload[L - 1];
-        free(payload);
+        if (!arena) free(payload);
         pos += hl + L;
         nf++;
         pb += L;
@@ -179,6 +205,7 @@ typedef struct {
     uint64_t frames, payload, checksum;
     int iters;
     double seconds;
+    bump_arena *arena;
 } bench_arg;
 
 static double now_s(void) {
@@ -195,7 +222,7 @@ static void *bench_thread(void *p) {
         /* connections assigned round-robin to loops, load_balance.go:7-14 */
         for (uint32_t c = a->tid; c < a->n_conns; c += a->nthreads)
             a->checksum += pipeline_stream(a->in + a->conn_off[c], a->conn_len[c], &a->frames,
-                                           &a->payload);
+                                           &a->payload, a->arena);
         a->iters++;
         a->seconds = now_s() - t0;
     } while (a->seconds < a->min_seconds);
@@ -203,17 +230,34 @@ static void *bench_thread(void *p) {
 }
 
 /* Runs the pipeline over the batch repeatedly (>= min_seconds) on `threads`
- * threads; returns wall seconds, total payload bytes and frames processed. */
-double wsref_bench_pipeline(const uint8_t *in, const uint64_t *conn_off, const uint64_t *conn_len,
-                            uint32_t n_conns, int threads, double min_seconds,
-                            uint64_t *payload_bytes, uint64_t *frames, uint64_t *checksum) {
+ * threads; returns wall seconds, total payload bytes and frames processed.
+ * alloc_mode: WSREF_ALLOC_FRESH with arena_bytes per thread (its pages are
+ * touched before the clock starts), or WSREF_ALLOC_CACHE_HOT.  -1 on an
+ * arena allocation failure. */
+double wsref_bench_pipeline_alloc(const uint8_t *in, const uint64_t *conn_off, const uint64_t *conn_len,
+                                  uint32_t n_conns, int threads, double min_seconds, int alloc_mode,
+                                  uint64_t arena_bytes, uint64_t *payload_bytes, uint64_t *frames,
+                                  uint64_t *checksum) {
     if (threads < 1) threads = 1;
     bench_arg *args = (bench_arg *)calloc((size_t)threads, sizeof(bench_arg));
     pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    bump_arena *arenas = alloc_mode == WSREF_ALLOC_FRESH ? (bump_arena *)calloc((size_t)threads, sizeof(bump_arena))
+                                                         : NULL;
+    /* the largest frame must fit an arena */
+    uint64_t maxf = 0;
+    for (uint32_t c = 0; c < n_conns; c++) maxf = conn_len[c] > maxf ? conn_len[c] : maxf;
+    if (arena_bytes < maxf + 64) arena_bytes = maxf + 64;
+    double wall = -1;
+    for (int i = 0; arenas && i < threads; i++) {
+        arenas[i].base = (uint8_t *)malloc(arena_bytes);
+        if (!arenas[i].base) goto out;
+        memset(arenas[i].base, 1, arena_bytes);  /* fault the pages in before the clock */
+        arenas[i].cap = arena_bytes;
+    }
     double t0 = now_s();
     for (int i = 0; i < threads; i++) {
         args[i] = (bench_arg){in, conn_off, conn_len, n_conns, (uint32_t)i, (uint32_t)threads,
-                              min_seconds, 0, 0, 0, 0, 0.0};
+                              min_seconds, 0, 0, 0, 0, 0.0, arenas ? &arenas[i] : NULL};
         pthread_create(&th[i], NULL, bench_thread, &args[i]);
     }
     uint64_t pb = 0, nf = 0, ck = 0;
@@ -223,13 +267,23 @@ double wsref_bench_pipeline(const uint8_t *in, const uint64_t *conn_off, const u
         nf += args[i].frames;
         ck += args[i].checksum;
     }
-    double wall = now_s() - t0;
+    wall = now_s() - t0;
     *payload_bytes = pb;
     *frames = nf;
     *checksum = ck;
+out:
+    for (int i = 0; arenas && i < threads; i++) free(arenas[i].base);
+    free(arenas);
     free(args);
     free(th);
     return wall;
+}
+
+double wsref_bench_pipeline(const uint8_t *in, const uint64_t *conn_off, const uint64_t *conn_len,
+                            uint32_t n_conns, int threads, double min_seconds,
+                            uint64_t *payload_bytes, uint64_t *frames, uint64_t *checksum) {
+    return wsref_bench_pipeline_alloc(in, conn_off, conn_len, n_conns, threads, min_seconds,
+                                      WSREF_ALLOC_CACHE_HOT, 0, payload_bytes, frames, checksum);
 }
 
 /* ------------------------------------------------------------------ outbound encode

@@ -9,6 +9,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -132,3 +134,48 @@ def test_parent_rccl_check_uses_kfd_topology(tmp_path):
                      {"GEV_DIST_BACKEND": "nccl", "GEV_KFD_TOPOLOGY": root1})
     assert "parent touched" not in r.stderr
     assert r.returncode == 3 and "needs 2 GPUs" in r.stderr and "launching" not in r.stderr
+
+
+def _eight_rank_dry_run(config, scaling):
+    import bench
+    r = _run(["--gpus", "8", "--dry-run", "--config", config, "--scaling", scaling], {"GEV_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r)
+    assert d["n_gpus"] == 8 and d["dry_run"] is True and d["value"] is None and d["scaling"] == scaling
+    c = d["decoded_per_step"]
+    assert c["ranks_summed"] == 8 and c["errors"] == 0
+    # every rank's batch fits one MI355X with room to spare (checked again on the device, bench.main)
+    assert 0 < d["hbm_need_bytes_per_rank"] < 0.9 * bench.HBM_BYTES_PER_GPU
+    return d, c
+
+
+@pytest.mark.parametrize("config,frames,size", [("c2", 262144, 4096), ("c3", 1048576, 65536)])
+def test_eight_ranks_weak_counts_every_rank(config, frames, size):
+    """The driver's top scaling point: 8 self-launched
+    ranks over gloo, weak scaling of C2 and of the headline C3 (the driver's
+    default) -- one JSON line, n_gpus 8, the count all-reduce summing 8 ranks'
+    full batches."""
+    d, c = _eight_rank_dry_run(config, "weak")
+    assert c["frames"] == 8 * frames and c["payload_bytes"] == 8 * frames * size
+    assert d["config"]["global_connections"] == 8 * d["config"]["connections_per_gpu"]
+
+
+def test_eight_ranks_strong_c4_split_covers_batch():
+    """8 ranks, C4 strong scaling: the LPT shares of the one global batch sum
+    to exactly its frames and payload bytes."""
+    import bench
+    glob, _ = bench.build_layout("c4", 0, None)
+    d, c = _eight_rank_dry_run("c4", "strong")
+    assert c["frames"] == glob.n_frames and c["payload_bytes"] == glob.payload_len
+    assert d["config"]["global_connections"] == glob.n_conns
+
+
+def test_hbm_need_of_the_headline_batch_fits_one_gpu():
+    """C3 at full size (64 GiB in, 64 GiB out) is checked up front against the
+    device's free memory; the estimate itself fits an MI355X's 288 GB, and a
+    second batch in flight adds its outputs and scratch."""
+    import bench
+    lay, _ = bench.build_layout("c3", 0, None)
+    one, two = bench.hbm_need_bytes(lay, 1), bench.hbm_need_bytes(lay, 2)
+    assert 2 * lay.payload_len < one < bench.HBM_BYTES_PER_GPU
+    assert two - one >= lay.payload_padded

@@ -354,3 +354,29 @@ def test_utf8_validation_is_strict():
     bad = [b"\xff", b"\xc0\xaf", b"\xed\xa0\x80", b"\xe2\x82", b"\xf4\x90\x80\x80", b"\xe0\x80\xaf", b"a\x80"]
     assert all(wo.utf8_valid(x.encode()) for x in ok)
     assert not any(wo.utf8_valid(b) for b in bad)
+
+
+@pytest.mark.parametrize("alloc", ["fresh", "cache_hot"])
+@pytest.mark.parametrize("vectorized", [False, True])
+def test_cpu_baseline_pipeline_allocation_modes(alloc, vectorized):
+    """The CPU baseline's per-frame pipeline (oracle/ws_ref.c, bench.py
+    cpu_baseline) in both allocation modes and both builds processes whole
+    passes over the batch: on one thread its payload bytes and frames are
+    exact multiples of the batch's own (each of 3 threads repeats its own
+    share of the connections)."""
+    rng = np.random.default_rng(7)
+    streams = [b"".join(wo.encode_frame(bytes(rng.integers(0, 256, int(L), dtype=np.uint8)), 2, True, 0, True,
+                                        b"\x01\x02\x03\x04") for L in rng.integers(0, 70000, 6))
+               for _ in range(5)]
+    arena = np.frombuffer(b"".join(streams) + bytes(64), np.uint8).copy()
+    lens = np.array([len(s) for s in streams], np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    want = ref.decode_batch(arena[:-64], offs, lens)
+    per_pass_bytes, per_pass_frames = int(want["frames"]["length"].sum()), want["frames"].shape[0]
+    for threads in (1, 3):
+        secs, pb, nf = ref.bench_pipeline(arena, offs, lens, threads=threads, min_seconds=0.05,
+                                          vectorized=vectorized, alloc=alloc)
+        assert secs > 0 and nf > 0 and pb > 0
+        if threads == 1:
+            assert pb * per_pass_frames == nf * per_pass_bytes
+    assert ref.fresh_arena_bytes() >= 64 << 20
