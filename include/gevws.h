@@ -136,8 +136,11 @@ int gevws_device_count(void);
 /* One context per event loop (the reference keeps one per-connection header
  * scratch, protocol.go:37; the batch engine keeps its scratch per loop).
  * Successive contexts on a device cycle their stream's priority over the
- * device's range (0, -1, 1, ...): each priority level has its own hardware
- * queues, so several loops' passes run side by side. */
+ * normal level and the levels below it (0, 1, ...): each priority level has
+ * its own hardware queues, so several loops' passes run side by side, and a
+ * context never outranks the application's normal-priority work.  The
+ * environment variable GEVWS_STREAM_PRIORITIES=all adds the levels above
+ * normal (0, -1, 1, ...); =normal keeps every context at 0. */
 gevws_ctx *gevws_ctx_create(int device);
 void gevws_ctx_destroy(gevws_ctx *ctx);
 int gevws_ctx_device(const gevws_ctx *ctx);
@@ -197,6 +200,11 @@ int gevws_ctx_set_tuning(gevws_ctx *ctx, int key, int64_t value);
  * has shown long chains of small frames (>= 256 frames per connection of <= 4
  * KiB each). */
 int gevws_ctx_last_split_lanes(const gevws_ctx *ctx);
+/* Connections of the last multi-kernel decode's split walk whose guesses did
+ * not line up, so the walk re-walked them serially (0 when it was not split;
+ * -1 for a null context or a device error).  Waits for the context's last
+ * call.  Measurement: each costs its whole chain's serial walk. */
+int64_t gevws_ctx_last_split_fallbacks(gevws_ctx *ctx);
 /* Completion signal of the one-launch kernels (a live pass's: the small-batch
  * decode and gevws_handle_decoded_async's one-workgroup form).  With d_flag
  * (the device address of a 32-bit word in mapped, coherent host memory) set,
