@@ -44,6 +44,40 @@ def test_device_decode_equals_oracle(engine, ss, one_launch):
         engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES)
 
 
+@pytest.fixture(scope="module")
+def live_flag():
+    import torch
+    a = gev_amd.PinnedArena(4096)
+    yield a
+    torch.cuda.synchronize()
+    a.close()
+
+
+@settings(max_examples=150, deadline=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture,
+                                 HealthCheck.data_too_large])
+@given(st.lists(streams, min_size=1, max_size=24), st.integers(1, 16))
+def test_live_pass_decode_equals_oracle(engine, live_flag, ss, copies):
+    """A live pass's form: with a completion flag set, the
+    one-launch decode stages its input through up to 32 workgroups' tagged
+    granules before the last one decodes -- on generated batches of up to
+    384 connections, so both one-launch shapes (256 lanes / 64 KiB, 1 024
+    lanes / 128 KiB) and, past them, the multi-kernel path run; bit-exact
+    against the C oracle, and the flag carries this launch's number exactly
+    when the decode was one launch."""
+    batch = ss * copies
+    arena, conns = pack_streams(batch)
+    engine.set_completion_flag(live_flag, 64)
+    try:
+        assert_matches_oracle(engine, arena, conns, f"{len(batch)} connections, {len(arena)} bytes")
+        one = len(batch) <= _abi.ONE_LAUNCH_MAX_CONNS and len(arena) <= _abi.ONE_LAUNCH_MAX_BYTES
+        assert (engine.completion_seq > 0) == one
+        if one:
+            assert int(live_flag.host[64:68].view(np.uint32)[0]) == engine.completion_seq
+    finally:
+        engine.set_completion_flag(None)
+
+
 @SETTINGS
 @given(st.binary(min_size=1, max_size=600), st.binary(min_size=4, max_size=4), st.integers(0, 1 << 20),
        st.integers(0, 15))
