@@ -204,3 +204,31 @@ def test_wide_unmask_grid_after_mixed_batch(engine):
     assert engine.last_unmask_grid > 4 * ncu
     _synth_decode_verify(engine, uniform, check_slice_conns=4)
     assert engine.last_unmask_grid <= 4 * ncu
+
+
+def test_split_walk_counts_its_serial_rewalks(engine, split_cases):
+    """gevws_ctx_last_split_fallbacks: the connections whose guesses did not
+    line up and were re-walked serially.  A payload carrying a plausible
+    embedded chain makes guesses that are not frame starts (every such
+    connection re-walked), chains of small frames are accepted as guessed
+    (none), an unsplit decode reports 0 -- and the output is the oracle's
+    every time."""
+    from gev_amd import _abi
+    engine.set_tuning(_abi.TUNE_SMALL_BATCH, 0)
+    engine.set_tuning(_abi.TUNE_SPLIT_LANES, 16)
+    try:
+        counts = {}
+        for name in ("embedded_chain", "small", "power"):
+            arena, conns = split_cases[name]
+            assert_matches_oracle(engine, arena, conns, f"fallbacks: {name}")
+            assert engine.last_split_lanes == 16
+            counts[name] = engine.last_split_fallbacks
+            assert 0 <= counts[name] <= conns.shape[0], (name, counts[name])
+        assert counts["embedded_chain"] > 0, counts
+        assert counts["small"] == 0, counts
+        engine.set_tuning(_abi.TUNE_SPLIT_LANES, 1)
+        assert_matches_oracle(engine, *split_cases["embedded_chain"], "fallbacks: unsplit")
+        assert engine.last_split_lanes == 1 and engine.last_split_fallbacks == 0
+    finally:
+        engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
+        engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES)
