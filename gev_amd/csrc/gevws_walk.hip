@@ -302,7 +302,7 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int D, int ST = 0>
+template <int D, int ST = 0, uint32_t RING = kRing>
 __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const uint64_t len, bool rec,
                                            const uint64_t ebase, const uint64_t ecap,
                                            WalkEntry* __restrict__ entries, WalkEntry* __restrict__ sink,
@@ -330,8 +330,8 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
         // room for this group in the ring? (the writer is normally far ahead:
         // it copies a group in a few hundred cycles, a step takes ~1 us)
         if ((nf & 3) == 0)
-          while ((uint32_t)nf + 4 - lds_ld(ring.tail) > kRing) __builtin_amdgcn_s_sleep(1);
-        ring.e[nf & (kRing - 1)] = e;
+          while ((uint32_t)nf + 4 - lds_ld(ring.tail) > RING) __builtin_amdgcn_s_sleep(1);
+        ring.e[nf & (RING - 1)] = e;
         __asm__ volatile("" ::: "memory");  // the entry before the head that publishes it (DS ops run in order)
         if ((nf & 3) == 3) lds_st(ring.head, (uint32_t)nf + 1);
       } else {
@@ -464,9 +464,11 @@ __device__ __forceinline__ void walk_chain(const uint8_t* __restrict__ s, const 
 // half-line writes among the walk's random line reads cost far more than their
 // bytes (256-byte groups 1.262 ms on C4, 128-byte 1.284, 64-byte 1.345;
 // profiles/r03/r03_compact_entries_ab.jsonl).
+template <uint32_t GROUP = kWriterGroup, uint32_t RING = kRing>
 __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries, WalkRing ring, uint64_t ebase,
                                                  uint64_t ecap) {
-  static_assert(kWriterGroup <= kSlotAlign, "groups aligned by the slot runs");
+  static_assert(GROUP <= kSlotAlign && kSlotAlign % GROUP == 0 && RING % GROUP == 0 && GROUP % 4 == 0,
+                "groups aligned by the slot runs, whole groups in the ring");
   uint32_t t = 0;
   bool fin = false;
   for (;;) {
@@ -474,23 +476,23 @@ __device__ __forceinline__ void walk_ring_writer(WalkEntry* __restrict__ entries
       const uint32_t hv = lds_ld(ring.head);
       __asm__ volatile("" ::: "memory");  // the entries after the head that published them
       const uint32_t h = hv & ~kRingDone;
-      while (h - t >= kWriterGroup) {
-        WalkEntry g[kWriterGroup];
+      while (h - t >= GROUP) {
+        WalkEntry g[GROUP];
 #pragma unroll
-        for (uint32_t k = 0; k < kWriterGroup; ++k) g[k] = ring.e[(t + k) & (kRing - 1)];
-        if (ebase != ~0ull && t + kWriterGroup <= ecap) {
-          u32x4* d = reinterpret_cast<u32x4*>(entries + ebase + t);  // 256-byte aligned
+        for (uint32_t k = 0; k < GROUP; ++k) g[k] = ring.e[(t + k) & (RING - 1)];
+        if (ebase != ~0ull && t + GROUP <= ecap) {
+          u32x4* d = reinterpret_cast<u32x4*>(entries + ebase + t);  // 8 x GROUP-byte aligned
 #pragma unroll
-          for (uint32_t k = 0; k < kWriterGroup / 2; ++k)
+          for (uint32_t k = 0; k < GROUP / 2; ++k)
             d[k] = u32x4{g[2 * k].mask, g[2 * k].w, g[2 * k + 1].mask, g[2 * k + 1].w};
         }
-        t += kWriterGroup;
+        t += GROUP;
         __asm__ volatile("" ::: "memory");
         lds_st(ring.tail, t);
       }
       if (hv & kRingDone) {
         for (; t < h; ++t)
-          if (ebase != ~0ull && t < ecap) entries[ebase + t] = ring.e[t & (kRing - 1)];
+          if (ebase != ~0ull && t < ecap) entries[ebase + t] = ring.e[t & (RING - 1)];
         fin = true;
       }
     }
@@ -756,8 +758,20 @@ __device__ __forceinline__ bool sync_search(const uint8_t* __restrict__ s, uint6
   return false;
 }
 
-template <int KS, int D>
-__global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __restrict__ in,
+// ST 2: the walkers' entries go through each lane's LDS ring to a second
+// (writer) wave, as k_walk_count's ST 2 -- a walking lane then issues no
+// global stores, so its header loads never wait behind entry stores.  The
+// ring (kSplitRing entries a lane, stored in kSplitGroup-entry groups) shares
+// its LDS with the guess rows, which are done with before the first entry:
+// 19 KB a workgroup, 8 workgroups of two waves per CU.
+constexpr uint32_t kSplitRing = 32;
+constexpr uint32_t kSplitGroup = 16;
+constexpr uint32_t kSplitLdsWords = (kCountBlock * kSyncRow > 2 * kCountBlock * kSplitRing)
+                                        ? kCountBlock * kSyncRow
+                                        : 2 * kCountBlock * kSplitRing;  // dwords: guess rows | rings
+
+template <int KS, int D, int ST>
+__global__ __launch_bounds__(ST == 2 ? 2 * kCountBlock : kCountBlock) void k_walk_split(const uint8_t* __restrict__ in,
                                                             const gevws_conn_in* __restrict__ conns, uint32_t n,
                                                             gevws_conn_out* __restrict__ cout,
                                                             uint64_t* __restrict__ blk,
@@ -770,12 +784,18 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
                                                             gevws_conn_in* __restrict__ segs,
                                                             gevws_conn_out* __restrict__ sout,
                                                             uint8_t* __restrict__ srec,
-                                                            uint64_t min_seg = kSplitMinBytes) {
+                                                            uint64_t min_seg = kSplitMinBytes,
+                                                            uint32_t* __restrict__ fallbacks = nullptr) {
   static_assert(KS >= 2 && KS <= (int)kSplitMaxLanes && (KS & (KS - 1)) == 0, "KS: a power of two");
-  __shared__ uint32_t s_row[kCountBlock * kSyncRow];
+  static_assert(ST == 0 || ST == 2, "entries from the lanes or through the writer wave");
+  __shared__ __attribute__((aligned(16))) uint32_t s_lds[ST == 2 ? kSplitLdsWords : kCountBlock * kSyncRow];
+  __shared__ uint32_t s_head[ST == 2 ? kCountBlock : 1], s_tail[ST == 2 ? kCountBlock : 1];
+  __shared__ uint64_t s_ebase[ST == 2 ? kCountBlock : 1], s_ecap[ST == 2 ? kCountBlock : 1];
+  uint32_t* const s_row = s_lds;  // the guess rows (step 1), then the rings (step 3)
+  const bool walker = ST != 2 || threadIdx.x < 64;
   const uint32_t lane = threadIdx.x & 63, i = lane % KS;
-  const uint32_t c = blockIdx.x * cpb + threadIdx.x / KS;
-  const bool active = threadIdx.x / KS < cpb && c < n;
+  const uint32_t c = blockIdx.x * cpb + lane / KS;
+  const bool active = walker && lane / KS < cpb && c < n;
   const uint64_t v = (uint64_t)c * KS + i;
   gevws_conn_in ci = {0, 0};
   bool oob = false;
@@ -797,7 +817,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
       const uint64_t seg = ci.len / kc, t = ci.len * i / kc;
       const uint64_t step = seg / (2 * kSyncWindows) > kSyncWin ? seg / (2 * kSyncWindows) : kSyncWin;
       const uint32_t m0 = (uint32_t)s[1] >> 7;  // the first frame's mask bit (len >= 2 x kSplitMinBytes)
-      found = sync_search(s, ci.len, t, step, t + seg * 3 / 4, m0, s_row + (threadIdx.x) * kSyncRow, b);
+      found = sync_search(s, ci.len, t, step, t + seg * 3 / 4, m0, s_row + lane * kSyncRow, b);
     }
   }
   // 2. a segment ends at the next lane's guess (or the stream's end);
@@ -816,7 +836,21 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
   uint64_t ebase = 0, ecap = 0;
   const bool rec0 = active && entry_slots_of(sg, (uint32_t)v, n_entries, gshift, ebase, ecap);
   WalkRes R = walk_res_fresh();
-  if (active) walk_chain<D>(in + sg.off, sg.len, rec0, ebase, ecap, entries, entries + n_entries + v, R);
+  if constexpr (ST == 2) {
+    const WalkRing ring = {reinterpret_cast<WalkEntry*>(s_lds) + lane * kSplitRing, s_head + lane, s_tail + lane};
+    if (walker) {
+      s_head[lane] = active ? 0u : kRingDone;
+      s_tail[lane] = 0;
+      s_ebase[lane] = rec0 ? ebase : ~0ull;
+      s_ecap[lane] = ecap;
+    }
+    __syncthreads();  // every guess row read: the rings may take the LDS
+    if (!walker) walk_ring_writer<kSplitGroup, kSplitRing>(entries, ring, s_ebase[lane], s_ecap[lane]);
+    else if (active)
+      walk_chain<D, 2, kSplitRing>(in + sg.off, sg.len, rec0, ebase, ecap, entries, entries + n_entries + v, R, ring);
+  } else if (active) {
+    walk_chain<D>(in + sg.off, sg.len, rec0, ebase, ecap, entries, entries + n_entries + v, R);
+  }
   // 4. stitch the group's KS lanes (every lane takes part in the shuffles)
   const bool last = found && end == ci.len;
   const bool ok = !found || last || (R.st == GEVWS_OK && R.pos == slen);
@@ -888,6 +922,7 @@ __global__ __launch_bounds__(kCountBlock) void k_walk_split(const uint8_t* __res
       } else {
         // a guess missed: the whole chain, serially (no entries: the record
         // pass re-walks it as one segment)
+        if (fallbacks) atomicAdd(fallbacks, 1u);  // (gevws_ctx_last_split_fallbacks)
         WalkRes S = walk_res_fresh();
         walk_chain<0>(s, ci.len, false, 0, 0, entries, entries + n_entries + v, S);
         nf = S.nf;
@@ -1307,6 +1342,9 @@ constexpr uint64_t kSmallSliceChunks = 128;
 // their finished-workgroup counter: a word of ctx->d_done of its own (the
 // walk's is d_done[0]), 128 bytes apart
 constexpr uint32_t kSmallStageCounter = 32;
+// ... and the split walk's count of connections re-walked serially after a
+// missed guess (gevws_ctx_last_split_fallbacks), a word of its own too
+constexpr uint32_t kSplitFallbackCounter = 48;
 
 template <class S>
 __global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restrict__ in, uint64_t in_bytes,
@@ -1539,6 +1577,7 @@ const char* const kWalkVariants[] = {
     "one lane per connection, plain chain walk (D = 0)",
     "no entry table (the record pass re-walks every chain)",
     "entries through the writer wave whatever the batch size (the default's path for >= 128 connections per CU)",
+    "the default, with the split walk's entries stored by the walking lanes (no writer wave; measurement)",
 };
 constexpr int kNumWalkVariants = sizeof(kWalkVariants) / sizeof(kWalkVariants[0]);
 
@@ -1547,6 +1586,7 @@ constexpr int kNumWalkVariants = sizeof(kWalkVariants) / sizeof(kWalkVariants[0]
 namespace gevws_impl {
 
 int walk_variant_count() { return kNumWalkVariants; }
+uint32_t split_fallback_counter() { return kSplitFallbackCounter; }
 const char* walk_variant_name(int i) { return i >= 0 && i < kNumWalkVariants ? kWalkVariants[i] : nullptr; }
 
 template <class S>
@@ -1620,7 +1660,7 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   // are long chains of small frames (the previous decode's)
   const int wv = ctx->walk_variant;
   uint32_t ks = 1;
-  if (wv == 0 && n_conns) {
+  if ((wv == 0 || wv == 4) && n_conns) {
     if (ctx->split_lanes >= 2) {
       ks = ctx->split_lanes;
     } else if (ctx->split_lanes == 0 && in_bytes / n_conns >= 2 * kSplitMinBytes && ctx->stats_known &&
@@ -1679,11 +1719,16 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
   // chain walk (D = 0) runs instead
   const bool plain = wv == 1 || (wv != 1 && ctx->stats_known && ctx->prev_mixed);
   if (nblk && ks > 1) {
+    // entries through the writer wave (walk variant 4: from the walking lanes, the round-5 form)
+    const bool writer = wv != 4;
+    GEVWS_HIP(hipMemsetAsync(ctx->d_done + kSplitFallbackCounter, 0, sizeof(uint32_t), st));
 #define GEVWS_SPLIT(K)                                                                                            \
-  (plain ? k_walk_split<K, 0> : k_walk_split<K, 8>)<<<nblk, kCountBlock, 0, st>>>(                                \
+  (writer ? (plain ? k_walk_split<K, 0, 2> : k_walk_split<K, 8, 2>)                                               \
+          : (plain ? k_walk_split<K, 0, 0> : k_walk_split<K, 8, 0>))<<<nblk, writer ? 2 * kCountBlock : kCountBlock, \
+                                                                      0, st>>>(                                     \
       d_in, d_conns, n_conns, d_conn_out, blk, entries, ne, gshift, cpb_w, in_bytes, done, ctx->d_walk_part, tag,     \
       max_frames, payload_cap,                                                                                      \
-      d_summary, segs, sout, srec, ctx->split_min_bytes)
+      d_summary, segs, sout, srec, ctx->split_min_bytes, ctx->d_done + kSplitFallbackCounter)
     if (ks == 2) GEVWS_SPLIT(2);
     else if (ks == 4) GEVWS_SPLIT(4);
     else if (ks == 8) GEVWS_SPLIT(8);

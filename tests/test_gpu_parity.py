@@ -668,7 +668,7 @@ def test_walk_variants_uniform_runs(engine):
     arena, conns = pack_streams([random_stream(rng, int(rng.integers(1, 40))) for _ in range(90)])
     cases.append((arena, conns[rng.permutation(conns.shape[0])]))
     walks = engine.variants(_abi.TUNE_WALK_VARIANT)
-    assert walks == [0, 1, 2, 3]
+    assert walks == [0, 1, 2, 3, 4]
     try:
         for v in walks:
             engine.set_tuning(_abi.TUNE_WALK_VARIANT, v)

@@ -102,20 +102,24 @@ def split_cases():
     return _cases()
 
 
-@pytest.mark.parametrize("lanes,min_seg", [(0, 16384), (2, 16384), (4, 16384), (8, 16384), (16, 16384),
-                                           (32, 16384), (32, 4096), (16, 1024)])
-def test_split_walk_matches_oracle(engine, split_cases, lanes, min_seg):
+@pytest.mark.parametrize("lanes,min_seg,wv", [(0, 16384, 0), (2, 16384, 0), (4, 16384, 0), (8, 16384, 0),
+                                              (16, 16384, 0), (32, 16384, 0), (32, 4096, 0), (16, 1024, 0),
+                                              (16, 16384, 4), (2, 1024, 4)])
+def test_split_walk_matches_oracle(engine, split_cases, lanes, min_seg, wv):
     """Every lane count (32: two connections per wave), and shorter minimum
     segments (GEVWS_TUNE_SPLIT_MIN_BYTES: more guesses per connection, each
-    nearer the previous one)."""
+    nearer the previous one); entries through the writer wave (the default)
+    and from the walking lanes (walk variant 4)."""
     from gev_amd import _abi
     engine.set_tuning(_abi.TUNE_SMALL_BATCH, 0)
     engine.set_tuning(_abi.TUNE_SPLIT_LANES, lanes)
     engine.set_tuning(_abi.TUNE_SPLIT_MIN_BYTES, min_seg)
+    engine.set_tuning(_abi.TUNE_WALK_VARIANT, wv)
     try:
         for name, (arena, conns) in split_cases.items():
-            assert_matches_oracle(engine, arena, conns, f"split lanes {lanes} min {min_seg}: {name}")
+            assert_matches_oracle(engine, arena, conns, f"split lanes {lanes} min {min_seg} walk {wv}: {name}")
     finally:
+        engine.set_tuning(_abi.TUNE_WALK_VARIANT, 0)
         engine.set_tuning(_abi.TUNE_SPLIT_LANES, 0)
         engine.set_tuning(_abi.TUNE_SPLIT_MIN_BYTES, 16384)
         engine.set_tuning(_abi.TUNE_SMALL_BATCH, _abi.ONE_LAUNCH_MAX_BYTES)
