@@ -609,7 +609,12 @@ constexpr uint32_t kSplitAutoMaxLanes = 16;  // the auto choice's largest split
 // small frames splitting shortens; a batch of big frames -- C2, C3, C5 --
 // pays the guesses for nothing)
 constexpr uint64_t kSplitMinFramesPerConn = 256;
-constexpr uint64_t kSplitMaxConnsPerCU = 32;  // more chains keep the walk busy unsplit (C4 1/4 share: +5 %)
+// more chains keep the walk busy unsplit: with the writer wave the 4-way C4
+// share (64 per CU) walks faster split 8 ways (2.698 -> 2.645 ms a step), the
+// 2-way (128 per CU) and the full batch slower at any split
+// (profiles/r06/r06i_split_rule.jsonl; round 2-5, without the writer, the
+// 4-way share lost 5 % split)
+constexpr uint64_t kSplitMaxConnsPerCU = 64;
 constexpr uint64_t kSplitMaxFrameBytes = 4096;
 
 __device__ __forceinline__ bool sync_plausible1(uint32_t b0, uint32_t b1, uint32_t m0) {

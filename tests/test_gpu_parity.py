@@ -412,7 +412,8 @@ def _c4_full(engine, lay, n_check: int = 64, expect_split=None):
 def test_c4_full_size_and_lpt_shards(engine):
     """BASELINE config 4 exactly as bench.py builds it (16 GiB power-law
     payload over 65 536 connections, 43.8 M frames) on one GPU, then rank 0's
-    and rank 7's greedy-LPT shares of the 8-way strong split."""
+    and rank 7's greedy-LPT shares of the 8-way strong split and rank 0's of
+    the 4-way."""
     import torch
     import bench
     from gev_amd import workloads as w
@@ -427,6 +428,10 @@ def test_c4_full_size_and_lpt_shards(engine):
         assert part.n_conns == 65536 // 8 or abs(part.n_conns - 65536 // 8) < 65536 // 16
         ncu = torch.cuda.get_device_properties(engine.device).multi_processor_count
         _c4_full(engine, part, expect_split=16 if part.n_conns <= 32 * ncu else None)
+    # rank 0's 4-way share (64 connections per CU): split 8 ways since round 6
+    # (entries through the writer wave, profiles/r06/r06i_split_rule.jsonl)
+    part = w.shard_lpt(glob, 0, 4)
+    _c4_full(engine, part, expect_split=8 if part.n_conns <= 64 * ncu else None)
 
 
 def test_c4_power_law_property(engine):
