@@ -489,7 +489,8 @@ def main():
                              f"status={int(sk['status'])}")
     del desc
 
-    walk_info = {"split_lanes": eng.last_split_lanes}
+    last = engs[(args.steps + args.warmup - 1) % M]  # the context of the last step
+    walk_info = {"split_lanes": last.last_split_lanes, "split_fallbacks": last.last_split_fallbacks}
     # achievable-bandwidth ceiling on this box, after the timed region: the
     # unmask kernel's streaming loop minus XOR / frame lookup (gevws_copy_async)
     # over the same byte count into the payload arena -- from the payload's

@@ -203,6 +203,12 @@ class Engine:
         """Lanes per connection of the last multi-kernel decode's header walk (1 = not split)."""
         return int(lib.gevws_ctx_last_split_lanes(self._ctx))
 
+    @property
+    def last_split_fallbacks(self) -> int:
+        """Connections the last multi-kernel decode's split walk re-walked
+        serially after a missed guess (0 when not split; waits for the decode)."""
+        return int(lib.gevws_ctx_last_split_fallbacks(self._ctx))
+
     @staticmethod
     def variant_name(i: int, key: int = _abi.TUNE_UNMASK_VARIANT) -> Optional[str]:
         n = lib.gevws_tuning_name(key, i)
@@ -251,6 +257,34 @@ class Engine:
             out.payload.data_ptr(), payload_cap, out.conn_out.data_ptr(), out.summary.data_ptr())
         if st != OK:
             raise RuntimeError(f"gevws_decode_batch_async: {status_string(st)}")
+
+    def decode_post(self, arena, in_bytes: int, conns, n_conns: int, out: Batch, max_frames: int,
+                    payload_cap: int) -> None:
+        """gevws_decode_batch_post: a live pass on the context's stream, posted
+        to the resident decode service when it is on (set_service) and the
+        pass fits it, else launched; completion_seq tells which word to wait for."""
+        st = lib.gevws_decode_batch_post(
+            self._ctx, arena.data_ptr(), in_bytes, conns.data_ptr() if n_conns else None, n_conns,
+            out.frames.data_ptr(), max_frames, out.payload.data_ptr(), payload_cap, out.conn_out.data_ptr(),
+            out.summary.data_ptr())
+        if st != OK:
+            raise RuntimeError(f"gevws_decode_batch_post: {status_string(st)}")
+
+    def set_service(self, on: bool) -> None:
+        """gevws_ctx_set_service: the resident decode service (False stops it)."""
+        st = lib.gevws_ctx_set_service(self._ctx, 1 if on else 0)
+        if st != OK:
+            raise RuntimeError(f"gevws_ctx_set_service: {status_string(st)}")
+
+    def service_stop(self) -> None:
+        """gevws_ctx_service_stop: end the live instance (the next post starts another)."""
+        lib.gevws_ctx_service_stop(self._ctx)
+
+    def service_stats(self) -> dict:
+        """gevws_ctx_service_stats: service instances launched, passes posted to them."""
+        la, po = ctypes.c_int64(), ctypes.c_int64()
+        lib.gevws_ctx_service_stats(self._ctx, ctypes.byref(la), ctypes.byref(po))
+        return {"launches": la.value, "posts": po.value}
 
     def decode(self, arena, in_bytes: int, conns, n_conns: int, max_frames: Optional[int] = None,
                payload_cap: Optional[int] = None, stream=None, aux_slots: int = 0) -> Batch:
@@ -843,6 +877,13 @@ class Protocol:
         if st != OK:
             raise RuntimeError(f"reply: {status_string(st)}")
         return (ctypes.string_at(out, n.value) if n.value else None), bool(sh.value)
+
+    def set_service(self, on: bool) -> None:
+        """gevws_protocol_set_service: zero-copy passes without a handler step
+        go to the context's resident decode service (no launch call)."""
+        st = lib.gevws_protocol_set_service(self._p, 1 if on else 0)
+        if st != OK:
+            raise RuntimeError(f"gevws_protocol_set_service: {status_string(st)}")
 
     def set_zero_copy_max(self, nbytes: int) -> None:
         """gevws_protocol_set_zero_copy_max: batched passes over at most

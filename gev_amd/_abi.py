@@ -100,7 +100,8 @@ class ProtocolStats(ctypes.Structure):
     _fields_ = [("device_passes", ctypes.c_uint64), ("conns_staged", ctypes.c_uint64),
                 ("bytes_staged", ctypes.c_uint64), ("gated", ctypes.c_uint64),
                 ("zero_copy_passes", ctypes.c_uint64), ("handler_passes", ctypes.c_uint64),
-                ("chained_handler_passes", ctypes.c_uint64), ("signalled_passes", ctypes.c_uint64)]
+                ("chained_handler_passes", ctypes.c_uint64), ("signalled_passes", ctypes.c_uint64),
+                ("service_passes", ctypes.c_uint64), ("service_misses", ctypes.c_uint64)]
 
 
 class ProtocolTimeline(ctypes.Structure):
@@ -181,6 +182,7 @@ SIGNATURES = {
     "gevws_ctx_set_timing": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_ctx_set_tuning": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_last_split_lanes": (ctypes.c_int, [P]),
+    "gevws_ctx_last_split_fallbacks": (ctypes.c_int64, [P]),
     "gevws_ctx_last_unmask_grid": (ctypes.c_int, [P]),
     "gevws_tuning_name": (ctypes.c_char_p, [ctypes.c_int, ctypes.c_int64]),
     "gevws_ctx_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32)]),
@@ -193,6 +195,11 @@ SIGNATURES = {
     "gevws_dispatch_decoded_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_int, P, ctypes.c_uint64,
                                                     ctypes.c_uint64, P, P, P]),
     "gevws_ctx_set_completion_flag": (ctypes.c_int, [P, P]),
+    "gevws_ctx_set_service": (ctypes.c_int, [P, ctypes.c_int]),
+    "gevws_ctx_service_stop": (ctypes.c_int, [P]),
+    "gevws_ctx_service_stats": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "gevws_decode_batch_post": (ctypes.c_int, [P, P, ctypes.c_uint64, P, ctypes.c_uint32, P, ctypes.c_uint64, P,
+                                               ctypes.c_uint64, P, P]),
     "gevws_ctx_completion_seq": (ctypes.c_int64, [P]),
     "gevws_handle_decoded_async": (ctypes.c_int, [P, P, P, ctypes.c_uint64, P, ctypes.c_int, P, ctypes.c_uint64,
                                                   ctypes.c_uint64, P, P, P, P, ctypes.c_uint64, P, P]),
@@ -247,6 +254,7 @@ SIGNATURES = {
     "gevws_protocol_get_stats": (None, [P, ctypes.POINTER(ProtocolStats)]),
     "gevws_protocol_get_timeline": (None, [P, ctypes.POINTER(ProtocolTimeline)]),
     "gevws_protocol_set_zero_copy_max": (None, [P, ctypes.c_uint64]),
+    "gevws_protocol_set_service": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_protocol_set_handler": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_comm_create": (P, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "gevws_comm_destroy": (None, [P]),

@@ -190,6 +190,9 @@ gevws_ctx* gevws_ctx_create(int device) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+    ctx->wall_khz = (uint64_t)khz;
   if (hipMalloc(reinterpret_cast<void**>(&ctx->d_sum), sizeof(gevws_summary)) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&ctx->d_done), 256) != hipSuccess ||
       hipMemset(ctx->d_done, 0, 256) != hipSuccess ||
@@ -208,6 +211,7 @@ gevws_ctx* gevws_ctx_create(int device) {
 void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (!ctx) return;
   DeviceGuard g(ctx->device);
+  service_stop(ctx);  // (its instance returns at once: the stream drains)
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   // the last call may have run on another stream (a caller's): its kernels
   // still read the scratch freed below
@@ -218,6 +222,8 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (ctx->d_small_stage) (void)hipFree(ctx->d_small_stage);
   if (ctx->d_walk_part) (void)hipFree(ctx->d_walk_part);
   if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
+  if (ctx->svc_box) (void)hipHostFree(ctx->svc_box);
+  if (ctx->d_svc_ctl) (void)hipFree(ctx->d_svc_ctl);
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
   for (auto& set : ctx->evs)
     for (auto& e : set.e) (void)hipEventDestroy(e);
@@ -284,6 +290,17 @@ const char* gevws_tuning_name(int key, int64_t value) {
 }
 
 int gevws_ctx_last_split_lanes(const gevws_ctx* ctx) { return ctx ? (int)ctx->last_ks : -1; }
+
+int64_t gevws_ctx_last_split_fallbacks(gevws_ctx* ctx) {
+  if (!ctx) return -1;
+  if (ctx->last_ks <= 1) return 0;
+  DeviceGuard g(ctx->device);
+  uint32_t n = 0;
+  if ((ctx->has_last && hipEventSynchronize(ctx->last_done) != hipSuccess) ||
+      hipMemcpy(&n, ctx->d_done + split_fallback_counter(), sizeof(n), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return (int64_t)n;
+}
 
 int gevws_ctx_set_completion_flag(gevws_ctx* ctx, uint32_t* d_flag) {
   if (!ctx) return GEVWS_ERR_INVALID;
@@ -362,6 +379,60 @@ int gevws_decode_batch_async(gevws_ctx* ctx, void* stream, const uint8_t* d_in, 
   if (ev) GEVWS_HIP(hipEventRecord(ev[4], st));
   GEVWS_HIP(hipGetLastError());
   return mark_last(ctx, st);
+}
+
+int gevws_ctx_set_service(gevws_ctx* ctx, int enable) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  if (!enable) {
+    service_stop(ctx);
+    ctx->svc_enabled = false;
+    return GEVWS_OK;
+  }
+  if (!ctx->svc_box) {
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, 4096, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !h)
+      return GEVWS_ERR_DEVICE;
+    memset(h, 0, 4096);
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+      (void)hipHostFree(h);
+      return GEVWS_ERR_DEVICE;
+    }
+    ctx->svc_box = static_cast<ServiceBox*>(h);
+    ctx->svc_box_dev = static_cast<ServiceBox*>(d);
+  }
+  ctx->svc_enabled = true;
+  return GEVWS_OK;
+}
+
+int gevws_ctx_service_stop(gevws_ctx* ctx) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  service_stop(ctx);
+  return GEVWS_OK;
+}
+
+int gevws_ctx_service_stats(const gevws_ctx* ctx, int64_t* launches, int64_t* posts) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  if (launches) *launches = ctx->svc_launches;
+  if (posts) *posts = ctx->svc_posts;
+  return GEVWS_OK;
+}
+
+int gevws_decode_batch_post(gevws_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const gevws_conn_in* d_conns,
+                            uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames, uint8_t* d_payload,
+                            uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary) {
+  if (!ctx || !d_summary) return GEVWS_ERR_INVALID;
+  if (n_conns && (!d_in || !d_conns || !d_conn_out)) return GEVWS_ERR_INVALID;
+  if (max_frames > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  if (!ctx->timing && ctx->walk_variant == 0 && ctx->unmask_variant == 0 && ctx->unmask_grid == 0 &&
+      in_bytes <= ctx->small_bytes &&
+      service_post(ctx, ctx->stream, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload, payload_cap,
+                   d_conn_out, d_summary))
+    return GEVWS_OK;
+  return gevws_decode_batch_async(ctx, ctx->stream, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
+                                  payload_cap, d_conn_out, d_summary);
 }
 
 int gevws_decode_batch(gevws_ctx* ctx, void* stream, const uint8_t* d_in, uint64_t in_bytes,

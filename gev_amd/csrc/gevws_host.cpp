@@ -485,6 +485,13 @@ class Protocol {
     return GEVWS_OK;
   }
   void SetZeroCopyMax(uint64_t bytes) { zc_max_ = bytes; }
+  // The context's resident decode service for this protocol's zero-copy
+  // passes without a handler step (gevws_ctx_set_service).
+  int SetService(int on) {
+    const int r = gevws_ctx_set_service(ctx_, on);
+    if (r == GEVWS_OK) service_ = on != 0;
+    return r;
+  }
 
  private:
   struct DeviceScope {
@@ -677,6 +684,7 @@ class Protocol {
     bool zc = false;       // zero-copy pass: kernels on the pinned buffers themselves
     bool flagged = false;  // its one-launch kernels signal the protocol's flag word
     int64_t seq = -1;      // ... with this number (taken right after its launches)
+    bool posted = false;   // posted to the context's resident decode service
     std::shared_ptr<uint8_t> arena;  // zero-copy: the payload arena the kernels write
     uint64_t arena_cap = 0;
     gevws_summary sum{};
@@ -734,8 +742,9 @@ class Protocol {
     return Launch(sg);
   }
 
-  int64_t Launch(Staged* sg) {
+  int64_t Launch(Staged* sg, bool may_post = true) {
     hipStream_t st = (hipStream_t)gevws_ctx_stream(ctx_);
+    sg->posted = false;
     if (sg->zc) {
       const uint32_t m = (uint32_t)sg->cin.size();
       if (!grow_host(&h_out_, &h_out_cap_, std::max<uint64_t>(sg->max_frames, 1) * sizeof(gevws_frame)))
@@ -750,10 +759,23 @@ class Protocol {
       void* dfr = sg->arena ? device_of(h_out_) : nullptr;
       void* dpay = sg->arena ? device_of(sg->arena.get()) : nullptr;
       if (!din || !dres || !dfr || !dpay) return fail();
-      const int r = gevws_decode_batch_async(ctx_, st, din + sg->coff, sg->total, (gevws_conn_in*)din, m,
-                                             (gevws_frame*)dfr, sg->max_frames, (uint8_t*)dpay, sg->payload_cap,
-                                             (gevws_conn_out*)(dres + sizeof(gevws_summary)), (gevws_summary*)dres);
+      // (with the resident service on and no handler chained behind, the
+      // pass is posted to it instead of launched: gevws_decode_batch_post)
+      const bool post = may_post && service_ && handler_ < 0 && sg->flagged;
+      int64_t posts0 = 0, posts1 = 0;
+      if (post) (void)gevws_ctx_service_stats(ctx_, nullptr, &posts0);
+      const int r = post
+                        ? gevws_decode_batch_post(ctx_, din + sg->coff, sg->total, (gevws_conn_in*)din, m,
+                                                  (gevws_frame*)dfr, sg->max_frames, (uint8_t*)dpay, sg->payload_cap,
+                                                  (gevws_conn_out*)(dres + sizeof(gevws_summary)), (gevws_summary*)dres)
+                        : gevws_decode_batch_async(ctx_, st, din + sg->coff, sg->total, (gevws_conn_in*)din, m,
+                                                   (gevws_frame*)dfr, sg->max_frames, (uint8_t*)dpay, sg->payload_cap,
+                                                   (gevws_conn_out*)(dres + sizeof(gevws_summary)),
+                                                   (gevws_summary*)dres);
       sg->seq = gevws_ctx_completion_seq(ctx_);
+      if (post) (void)gevws_ctx_service_stats(ctx_, nullptr, &posts1);
+      sg->posted = posts1 > posts0;  // (else launched)
+      if (sg->posted) ++stats_.service_passes;
       return r;
     }
     if (!grow_dev(&d_frames_, &d_frames_cap_, sg->max_frames * sizeof(gevws_frame)) ||
@@ -803,7 +825,7 @@ class Protocol {
     }
     return true;
   }
-  int64_t Wait(const Staged* sg) {
+  int64_t Wait(Staged* sg) {
     last_signalled_ = false;
     const int64_t seq = (sg->zc && sg->flagged) ? sg->seq : -1;
     if (seq >= 0) {
@@ -819,7 +841,17 @@ class Protocol {
         __builtin_ia32_pause();
       }
     }
-    return hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_)) == hipSuccess ? 0 : fail();
+    if (service_) (void)gevws_ctx_service_stop(ctx_);  // (a live instance would hold the stream)
+    if (hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_)) != hipSuccess) return fail();
+    if (seq >= 0 && __atomic_load_n(h_flag_, __ATOMIC_ACQUIRE) == (uint32_t)seq) {
+      last_signalled_ = true;
+    } else if (sg->posted) {
+      // the service's instance ended without the pass (not seen): launch it
+      ++stats_.service_misses;
+      if (Launch(sg, false) < 0 || hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_)) != hipSuccess)
+        return fail();
+    }
+    return 0;
   }
 
   // Waits for the pass (and whatever the caller enqueued after it); on
@@ -843,6 +875,7 @@ class Protocol {
   // follow an enqueued H2D copy or a zero-copy kernel still reading the
   // pinned staging, which the next pass would overwrite.
   int64_t fail() {
+    if (ctx_ && service_) (void)gevws_ctx_service_stop(ctx_);
     if (ctx_) (void)hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_));
     log_error("device: ", GEVWS_ERR_DEVICE);
     return GEVWS_ERR_DEVICE;
@@ -872,6 +905,7 @@ class Protocol {
     return true;
   }
   void release() {
+    if (ctx_ && service_) (void)gevws_ctx_set_service(ctx_, 0);
     if (ctx_) (void)hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_));
     if (h_flag_) {
       if (ctx_) (void)gevws_ctx_set_completion_flag(ctx_, nullptr);
@@ -910,6 +944,7 @@ class Protocol {
   uint64_t epoch_ = 0;
   uint64_t zc_max_ = GEVWS_ZERO_COPY_MAX_DEFAULT;
   int handler_ = -1;  // device handler policy (GEVWS_HANDLER_*), -1 = none
+  bool service_ = false;  // passes posted to the context's resident decode service
   uint8_t *h_rof_ = nullptr, *h_roff_ = nullptr, *h_hs_ = nullptr;  // handler outputs (mapped pinned)
   uint64_t h_rof_cap_ = 0, h_roff_cap_ = 0, h_hs_cap_ = 0;
   void* d_rep_ = nullptr;  // reply records (gevws_out_frame)
@@ -1010,6 +1045,11 @@ void gevws_protocol_get_stats(const gevws_protocol* p, gevws_protocol_stats* out
 
 void gevws_protocol_set_zero_copy_max(gevws_protocol* p, uint64_t bytes) {
   if (p) p->SetZeroCopyMax(bytes);
+}
+
+int gevws_protocol_set_service(gevws_protocol* p, int on) {
+  if (!p) return GEVWS_ERR_INVALID;
+  return p->SetService(on);
 }
 
 int gevws_protocol_set_handler(gevws_protocol* p, int policy) {

@@ -8,6 +8,17 @@
 
 #include "gevws_kernels.hpp"
 
+// The resident decode service's mailbox (k_decode_service, gevws_walk.hip):
+// mapped, coherent host memory written by the host, read by the kernel.
+constexpr int kServiceArgs = 10;  // in, in_bytes, conns, n, frames, max_frames, payload, payload_cap, cout, sum
+struct ServiceBox {
+  uint64_t req;                 // the posted pass: {its generation << 32 | its number}, stored last (release)
+  uint32_t gen;                 // the live generation: an instance of another one returns once no pass of
+                                //   its own is pending
+  uint32_t ack;                 // (written by the kernel) the number of the last pass taken
+  uint64_t args[kServiceArgs];  // the posted pass's arguments (device addresses and sizes)
+};
+
 struct gevws_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -61,12 +72,33 @@ struct gevws_ctx {
   uint64_t* d_walk_part = nullptr;    // the walk's block partials (kFusedScanMaxBlocks x kDecFields x 2)
   uint64_t* d_small_stage = nullptr;  // a live pass's staged input (k_decode_small; 4 granules a 16-byte chunk)
   uint32_t hand_seq = 0;
+  // the resident decode service (gevws_ctx_set_service)
+  bool svc_enabled = false;      // posting allowed
+  bool svc_live = false;         // an instance of this generation is on the stream
+  ServiceBox* svc_box = nullptr;  // mapped host memory (host address = device address on ROCm, checked)
+  ServiceBox* svc_box_dev = nullptr;
+  uint32_t svc_gen = 0, svc_last = 0;  // generation; the last pass number posted
+  uint32_t* svc_flag = nullptr;   // the completion word / ticks the live instance signals
+  const uint32_t* svc_flag_host = nullptr;  // (the word's host address)
+  uint64_t* svc_ticks = nullptr;
+  int64_t svc_t_launch_ns = 0;    // host clock at the live instance's launch
+  uint64_t* d_svc_ctl = nullptr;  // the instance's broadcast granules (k_decode_service), zeroed at allocation
+  uint32_t svc_t0 = 0, svc_passes = 0;  // the live instance's tags [t0, t0 + kServiceMaxPasses); passes posted
+  int64_t svc_launches = 0, svc_posts = 0;  // (gevws_ctx_service_stats)
+  uint64_t wall_khz = 100000;     // the GPU's constant-rate clock (hipDeviceAttributeWallClockRate)
 };
 
 // The tag of a launch's hand-offs.
 inline uint32_t next_hand_tag(gevws_ctx* ctx) {
   if (++ctx->hand_seq == 0) ctx->hand_seq = 1;
   return ctx->hand_seq;
+}
+// n consecutive tags, none 0: the first.
+inline uint32_t reserve_hand_tags(gevws_ctx* ctx, uint32_t n) {
+  if ((uint64_t)ctx->hand_seq + n > 0xFFFFFFFFull) ctx->hand_seq = 0;
+  const uint32_t t0 = ctx->hand_seq + 1;
+  ctx->hand_seq += n;
+  return t0;
 }
 
 namespace gevws_impl {
@@ -99,8 +131,19 @@ inline hipStream_t pick_stream(gevws_ctx* ctx, void* stream) {
   return reinterpret_cast<hipStream_t>(stream);
 }
 
-// Orders this call after the context's previous one when the stream changes.
+// Ends the live service instance (if any): bumping the mailbox's generation
+// makes it return within a poll once the pass posted to it (if any) is done,
+// so work enqueued behind it on the stream runs after that pass, at once.
+inline void service_stop(gevws_ctx* ctx) {
+  if (!ctx->svc_live) return;
+  __atomic_store_n(&ctx->svc_box->gen, ++ctx->svc_gen, __ATOMIC_RELEASE);
+  ctx->svc_live = false;
+}
+
+// Orders this call after the context's previous one when the stream changes
+// (and ends the service instance first: every launcher calls this).
 inline int order_after_last(gevws_ctx* ctx, hipStream_t st) {
+  service_stop(ctx);
   if (ctx->has_last && ctx->last_stream != st) GEVWS_HIP(hipStreamWaitEvent(st, ctx->last_done, 0));
   return GEVWS_OK;
 }
@@ -132,6 +175,11 @@ inline int ensure_scratch(gevws_ctx* ctx, size_t bytes) {
 int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
                  const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
                  uint8_t* d_payload, uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary);
+// a narrow-shape live pass posted to the context's resident decode service
+// (launched first if none is live), or false (gevws_decode_batch_post)
+bool service_post(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
+                  const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
+                  uint8_t* d_payload, uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary);
 // header walk, scan, bases and record pass into the context's scratch; the
 // output-tile -> frame map for the unmask in *tile_first.  ev: the timing
 // events 0..2 (walk start, walk end, scan end) or null.
@@ -140,6 +188,7 @@ int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
                  uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary, hipEvent_t* ev,
                  uint32_t** tile_first);
 int walk_variant_count();
+uint32_t split_fallback_counter();  // the word of ctx->d_done the split walk counts its serial re-walks in
 const char* walk_variant_name(int i);
 
 // ---- gevws_unmask.hip

@@ -15,6 +15,8 @@
 //                  output-tile -> frame map the unmask reads
 //   k_decode_small a batch of <= 1 024 connections and 128 KiB: the whole
 //                  decode, unmask included, in one workgroup
+#include <chrono>
+
 #include "gevws_internal.hpp"
 
 namespace {
@@ -1351,18 +1353,21 @@ constexpr uint32_t kSmallStageCounter = 32;
 // missed guess (gevws_ctx_last_split_fallbacks), a word of its own too
 constexpr uint32_t kSplitFallbackCounter = 48;
 
+// The body of the one-launch decode (k_decode_small, and each pass of the
+// resident service k_decode_service); every return is workgroup-uniform.
+// With nwg > 1 the nwg workgroups (this one is wg) count themselves in on
+// stage_done after staging their slice of the input (nslices of them, the
+// rest empty); true for the workgroup that decoded (and signalled).
 template <class S>
-__global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restrict__ in, uint64_t in_bytes,
-                                                        const gevws_conn_in* __restrict__ conns, uint32_t n,
-                                                        gevws_frame* __restrict__ frames, uint64_t max_frames,
-                                                        uint8_t* __restrict__ payload, uint64_t payload_cap,
-                                                        gevws_conn_out* __restrict__ cout,
-                                                        gevws_summary* __restrict__ sum,
-                                                        uint32_t* __restrict__ done = nullptr,
-                                                        uint32_t seq = 0, uint64_t* __restrict__ ticks = nullptr,
-                                                        uint64_t* __restrict__ stage_buf = nullptr,
-                                                        uint32_t* __restrict__ stage_done = nullptr,
-                                                        uint32_t tag = 0) {
+__device__ __forceinline__ bool decode_small_body(const uint8_t* __restrict__ in, uint64_t in_bytes,
+                                                  const gevws_conn_in* __restrict__ conns, uint32_t n,
+                                                  gevws_frame* __restrict__ frames, uint64_t max_frames,
+                                                  uint8_t* __restrict__ payload, uint64_t payload_cap,
+                                                  gevws_conn_out* __restrict__ cout, gevws_summary* __restrict__ sum,
+                                                  uint32_t* __restrict__ done, uint32_t seq,
+                                                  uint64_t* __restrict__ ticks, uint64_t* __restrict__ stage_buf,
+                                                  uint32_t* __restrict__ stage_done, uint32_t tag, uint32_t nwg,
+                                                  uint32_t wg, uint32_t nslices) {
   constexpr uint32_t NT = S::NT;
   constexpr int kBatch = S::kBatch;
   __shared__ uint64_t s_big[S::kBig][3];  // {src_off, payload_off, length} of the larger payloads
@@ -1385,7 +1390,6 @@ __global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restric
   if (n) {  // bytes [0, 16 x nst) of the input: every read below is inside [0, in_bytes + 48)
     const uint32_t nst = (uint32_t)((in_bytes + GEVWS_IN_PAD) / 16);
     u32x4* st = reinterpret_cast<u32x4*>(s_in);
-    const uint32_t nwg = gridDim.x;
     if (nwg > 1) {
       // A live pass's input sits in mapped host memory, which one workgroup
       // reads at ~2.5 GB/s (a 20 KB pass: ~8 us of staging).  So every
@@ -1393,8 +1397,8 @@ __global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restric
       // granules (hand-offs, above: 4 a 16-byte chunk), and the last one to
       // finish (stage_done) stages the whole input from there into its LDS
       // and runs the decode; the others end here.
-      const uint32_t per = (nst + nwg - 1) / nwg;
-      const uint32_t k0 = blockIdx.x * per, k1 = k0 + per < nst ? k0 + per : nst;
+      const uint32_t per = (nst + nslices - 1) / nslices;
+      const uint32_t k0 = wg < nslices ? wg * per : nst, k1 = k0 + per < nst ? k0 + per : nst;
       for (uint32_t kb = k0; kb < k1; kb += kBatch * NT) {
         u32x4 x[kBatch];
 #pragma unroll
@@ -1415,7 +1419,7 @@ __global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restric
       if (c == 0)
         s_last = __hip_atomic_fetch_add(stage_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1 ? 1u : 0u;
       __syncthreads();
-      if (!s_last) return;
+      if (!s_last) return false;
       if (c == 0) __hip_atomic_store(stage_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's
       uint32_t bad = 0;
       for (uint32_t kb = 0; kb < nst; kb += kBatch * NT) {
@@ -1461,7 +1465,7 @@ __global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restric
       *sum = sm;
     }
     signal_done(done, seq, ticks, t0, 0);
-    return;
+    return true;
   }
   uint64_t nf = 0, pb = 0, pl = 0, err = 0, same = 0, lastf = ~0ull, pos = 0;
   int32_t st = GEVWS_OK;
@@ -1511,7 +1515,7 @@ __global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restric
   }
   if (!ok) {  // capacity error: nothing written (uniform)
     signal_done(done, seq, ticks, t0, 0);
-    return;
+    return true;
   }
   if (c < n) {
     gevws_conn_out o;
@@ -1572,6 +1576,163 @@ __global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restric
     }
   }
   signal_done(done, seq, ticks, t0, 0);
+  return true;
+}
+
+template <class S>
+__global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restrict__ in, uint64_t in_bytes,
+                                                        const gevws_conn_in* __restrict__ conns, uint32_t n,
+                                                        gevws_frame* __restrict__ frames, uint64_t max_frames,
+                                                        uint8_t* __restrict__ payload, uint64_t payload_cap,
+                                                        gevws_conn_out* __restrict__ cout,
+                                                        gevws_summary* __restrict__ sum,
+                                                        uint32_t* __restrict__ done = nullptr,
+                                                        uint32_t seq = 0, uint64_t* __restrict__ ticks = nullptr,
+                                                        uint64_t* __restrict__ stage_buf = nullptr,
+                                                        uint32_t* __restrict__ stage_done = nullptr,
+                                                        uint32_t tag = 0) {
+  (void)decode_small_body<S>(in, in_bytes, conns, n, frames, max_frames, payload, payload_cap, cout, sum, done, seq,
+                             ticks, stage_buf, stage_done, tag, gridDim.x, blockIdx.x, gridDim.x);
+}
+
+// ------------------------------------------------------------------ 3d. the resident decode service
+// A live pass's launch call costs its loop ~5 us of host time whatever the
+// pass (the HIP runtime's).  With the service on (gevws_ctx_set_service), a
+// context keeps one instance of this kernel resident on its stream --
+// kSmallStageWGs workgroups, as many as a launched live pass stages its input
+// with -- and the host posts passes to it instead of launching them: the
+// pass's arguments into the mailbox in mapped host memory, then a 64-bit word
+// {generation, pass number}.
+//
+// Lane 0 of workgroup 0 polls the mailbox and broadcasts each pass it takes
+// to the other workgroups as tagged granules in device memory (ctl: the
+// command, the arguments' halves), tag t0 + k for the instance's k-th pass
+// (the host reserves the instance's tags [t0, t0 + kServiceMaxPasses)).  A
+// pass then runs as the launched one does (decode_small_body, narrow shape):
+// the first `slices` workgroups each stage a slice and count themselves in,
+// the last one decodes and signals the completion word (a pass of one slice:
+// workgroup 0 alone, from the input); the rest skip it.
+//
+// Every wave reaches an exit.  With no pass of its own pending, workgroup 0
+// ends the instance when the mailbox's live generation is no longer its own
+// (the host bumps it before any other work on the context's stream, before a
+// new instance, and to stop) or at its deadline (life_ticks of the GPU's
+// constant-rate clock after its start; the host posts only within half of
+// it): it waits for its last pass's done granule -- every workgroup has taken
+// that pass -- and then stores the exit granule (tag t0), which the others
+// poll beside the command; they also end at twice the deadline on their own.
+// A posted pass is tagged with its instance's generation and the host posts
+// the next only once the last has signalled, so none is lost (the one posted
+// before a stop still runs, the work behind it waits on the stream) and none
+// runs twice.
+constexpr uint32_t kServiceMaxPasses = 1u << 16;
+// ctl: the command {the pass's slices}, its number, the arguments' halves, exit, done
+constexpr uint32_t kSvcCmd = 0, kSvcSeq = 1, kSvcArgs = 2, kSvcExit = kSvcArgs + 2 * kServiceArgs,
+                   kSvcDone = kSvcExit + 1, kSvcCtlGranules = kSvcDone + 1;
+
+// The launched live pass's input slices (launch_decode_small), at most g.
+__host__ __device__ inline uint32_t small_slices(uint64_t in_bytes, uint32_t n, uint32_t g) {
+  const uint64_t w = ((in_bytes + GEVWS_IN_PAD) / 16 + kSmallSliceChunks - 1) / kSmallSliceChunks;
+  return n == 0 ? 1u : w < g ? (uint32_t)w : g;
+}
+
+template <class S>
+__global__ __launch_bounds__(S::NT) void k_decode_service(ServiceBox* __restrict__ box, uint32_t gen, uint32_t req0,
+                                                          uint64_t life_ticks, uint32_t* __restrict__ done,
+                                                          uint64_t* __restrict__ ticks, uint64_t* __restrict__ ctl,
+                                                          uint64_t* __restrict__ stage_buf,
+                                                          uint32_t* __restrict__ stage_done, uint32_t t0) {
+  __shared__ uint32_t s_k, s_slices, s_req;
+  __shared__ uint64_t s_a[kServiceArgs];
+  const uint64_t t_start = gpu_ticks();
+  const uint32_t wg = blockIdx.x, G = gridDim.x;
+  uint32_t last = req0;  // (lane 0 of workgroup 0) the last pass taken
+  uint32_t k = 0;        // (lane 0) the instance's last pass number seen
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t slices = 0, req = 0;  // 0: end
+      if (wg == 0) {
+        while (k + 1 < kServiceMaxPasses) {
+          const uint64_t w = __hip_atomic_load(&box->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+          if ((uint32_t)(w >> 32) == gen && (uint32_t)w != last) {  // a pass of this instance's
+            last = req = (uint32_t)w;
+            break;
+          }
+          if (__hip_atomic_load(&box->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != gen ||
+              gpu_ticks() - t_start >= life_ticks)
+            break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (req) {
+          const uint32_t tag = t0 + ++k;
+          for (int i = 0; i < kServiceArgs; ++i)
+            s_a[i] = __hip_atomic_load(&box->args[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(&box->ack, req, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // (the box is free)
+          slices = small_slices(s_a[1], (uint32_t)s_a[3], G);
+          if (slices > 1) {  // (the workgroups past its slices take a pass as a number only)
+            for (int i = 0; i < kServiceArgs; ++i) {
+              put_granule(ctl + kSvcArgs + 2 * i, (uint32_t)s_a[i], tag);
+              put_granule(ctl + kSvcArgs + 2 * i + 1, (uint32_t)(s_a[i] >> 32), tag);
+            }
+            put_granule(ctl + kSvcSeq, req, tag);
+          }
+          put_granule(ctl + kSvcCmd, slices, tag);
+        } else {
+          // pass k is done, so every workgroup has taken it
+          if (k)
+            for (uint64_t t1 = gpu_ticks(); (uint32_t)(load_granule(ctl + kSvcDone) >> 32) != t0 + k &&
+                                            gpu_ticks() - t1 < life_ticks;)
+              __builtin_amdgcn_s_sleep(2);
+          put_granule(ctl + kSvcExit, 0u, t0);
+        }
+      } else {
+        for (;;) {
+          const uint64_t g = load_granule(ctl + kSvcCmd);
+          const uint32_t d = (uint32_t)(g >> 32) - t0;
+          if (d > k && d < kServiceMaxPasses) {  // a pass not seen yet (skipped unless it has a slice for us)
+            k = d;
+            if ((uint32_t)g > wg) {
+              slices = (uint32_t)g;
+              break;
+            }
+            continue;
+          }
+          if ((uint32_t)(load_granule(ctl + kSvcExit) >> 32) == t0 || gpu_ticks() - t_start >= 2 * life_ticks) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        // a pass with a slice for us: its arguments stay until every workgroup with one has taken it
+        uint32_t bad = 0;
+        const uint32_t tag = t0 + k;
+        for (int i = 0; slices && i < kServiceArgs; ++i) {
+          const uint64_t* p = ctl + kSvcArgs + 2 * i;
+          const uint32_t lo = take_granule(p, load_granule(p), tag, bad);
+          const uint32_t hi = take_granule(p + 1, load_granule(p + 1), tag, bad);
+          s_a[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+        if (slices) req = take_granule(ctl + kSvcSeq, load_granule(ctl + kSvcSeq), tag, bad);
+        if (bad) slices = 0;  // (never seen: the pass then waits for the host's fallback)
+      }
+      s_k = k;
+      s_slices = slices;
+      s_req = req;
+    }
+    __syncthreads();
+    const uint32_t slices = s_slices;
+    if (!slices) return;
+    // The pass's input was written after this kernel started (a launched
+    // kernel's start would have dropped stale lines): without a launch, each
+    // wave drops them itself -- the host's release of the pass (its req store)
+    // reaches this workgroup through the granules, so acquire at system scope.
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint32_t tag = t0 + s_k;
+    const bool decoded = decode_small_body<S>(
+        reinterpret_cast<const uint8_t*>(s_a[0]), s_a[1], reinterpret_cast<const gevws_conn_in*>(s_a[2]),
+        (uint32_t)s_a[3], reinterpret_cast<gevws_frame*>(s_a[4]), s_a[5], reinterpret_cast<uint8_t*>(s_a[6]), s_a[7],
+        reinterpret_cast<gevws_conn_out*>(s_a[8]), reinterpret_cast<gevws_summary*>(s_a[9]), done, s_req, ticks,
+        stage_buf, stage_done, tag, slices, wg, slices);
+    if (decoded && threadIdx.x == 0) put_granule(ctl + kSvcDone, 0u, tag);
+    __syncthreads();  // (s_a and the body's LDS reused by the next pass)
+  }
 }
 
 // GEVWS_TUNE_WALK_VARIANT values (0 = the default choice per batch).
@@ -1594,6 +1755,19 @@ int walk_variant_count() { return kNumWalkVariants; }
 uint32_t split_fallback_counter() { return kSplitFallbackCounter; }
 const char* walk_variant_name(int i) { return i >= 0 && i < kNumWalkVariants ? kWalkVariants[i] : nullptr; }
 
+// A live pass's staging granules (4 per 16-byte chunk of the wide shape's input), zeroed once.
+static bool ensure_small_stage(gevws_ctx* ctx, hipStream_t st) {
+  if (ctx->d_small_stage) return true;
+  const size_t sbytes = 4ull * sizeof(uint64_t) * SmallWide::kStage;
+  if (hipMalloc(reinterpret_cast<void**>(&ctx->d_small_stage), sbytes) != hipSuccess ||
+      hipMemsetAsync(ctx->d_small_stage, 0, sbytes, st) != hipSuccess) {
+    if (ctx->d_small_stage) (void)hipFree(ctx->d_small_stage);
+    ctx->d_small_stage = nullptr;
+    return false;
+  }
+  return true;
+}
+
 template <class S>
 static int launch_decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
                                const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames,
@@ -1604,18 +1778,8 @@ static int launch_decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_
   // its input is read by kSmallStageWGs-wide slices (k_decode_small)
   uint32_t nwg = 1;
   if (ctx->done_flag && n_conns) {
-    const uint64_t nst = (in_bytes + GEVWS_IN_PAD) / 16;
-    const uint64_t w = (nst + kSmallSliceChunks - 1) / kSmallSliceChunks;
-    nwg = (uint32_t)(w < kSmallStageWGs ? w : kSmallStageWGs);
-    // the staging granules: 4 per 16-byte chunk of the wide shape's input, zeroed once
-    const size_t sbytes = 4ull * sizeof(uint64_t) * SmallWide::kStage;
-    if (nwg > 1 && !ctx->d_small_stage &&
-        (hipMalloc(reinterpret_cast<void**>(&ctx->d_small_stage), sbytes) != hipSuccess ||
-         hipMemsetAsync(ctx->d_small_stage, 0, sbytes, st) != hipSuccess)) {
-      if (ctx->d_small_stage) (void)hipFree(ctx->d_small_stage);
-      ctx->d_small_stage = nullptr;
-      nwg = 1;
-    }
+    nwg = small_slices(in_bytes, n_conns, kSmallStageWGs);
+    if (nwg > 1 && !ensure_small_stage(ctx, st)) nwg = 1;
   }
   const uint32_t tag = nwg > 1 ? next_hand_tag(ctx) : 0u;
   k_decode_small<S><<<nwg, S::NT, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
@@ -1626,6 +1790,88 @@ static int launch_decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_
   const int r = mark_last(ctx, st);
   if (ctx->done_flag) ctx->last_signal = seq;
   return r;
+}
+
+// The service's instance lives kServiceLifeMs of the GPU's clock from its
+// start; the host posts to it only within kServiceUseMs of its launch, then
+// replaces it (the old one returns at the generation bump, the new one starts
+// behind it on the stream), so a posted pass always finds its instance.
+constexpr uint64_t kServiceLifeMs = 200;
+constexpr int64_t kServiceUseMs = 100;
+
+static int64_t host_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// A narrow-shape live pass posted to the context's resident service (an
+// instance launched first when none is live, or the live one is too old or
+// signals elsewhere), or false: launch it as usual.  The mailbox is never
+// overwritten before the instance has taken the last pass posted (ack), and
+// the live instance gets the next pass only once the last has signalled (its
+// workgroups are free); otherwise the pass is launched, behind the instance.
+bool service_post(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
+                  const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
+                  uint8_t* d_payload, uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary) {
+  if (!ctx->svc_enabled || !ctx->svc_box || !ctx->done_flag || st != ctx->stream || n_conns > kSmallConns ||
+      in_bytes > kSmallBytes)
+    return false;
+  if (__atomic_load_n(&ctx->svc_box->ack, __ATOMIC_ACQUIRE) != ctx->svc_last) return false;
+  const int64_t now = host_ns();
+  if (ctx->svc_live) {
+    if (now - ctx->svc_t_launch_ns > kServiceUseMs * 1000000 || ctx->svc_flag != ctx->done_flag ||
+        ctx->svc_ticks != ctx->ticks || ctx->svc_passes + 2 >= kServiceMaxPasses)
+      service_stop(ctx);  // (replaced below, behind it on the stream)
+    else if ((int32_t)(__atomic_load_n(ctx->svc_flag_host, __ATOMIC_ACQUIRE) - ctx->svc_last) < 0)
+      return false;  // the last pass still runs
+  }
+  if (!ctx->svc_live) {
+    hipPointerAttribute_t pa;
+    if (hipPointerGetAttributes(&pa, ctx->done_flag) != hipSuccess || !pa.hostPointer) return false;
+    if (!ensure_small_stage(ctx, st)) return false;
+    if (!ctx->d_svc_ctl) {
+      const size_t cb = kSvcCtlGranules * sizeof(uint64_t);
+      if (hipMalloc(reinterpret_cast<void**>(&ctx->d_svc_ctl), cb) != hipSuccess) {
+        ctx->d_svc_ctl = nullptr;
+        return false;
+      }
+      if (hipMemsetAsync(ctx->d_svc_ctl, 0, cb, st) != hipSuccess) return false;
+    }
+    if (ctx->has_last && ctx->last_stream != st && hipStreamWaitEvent(st, ctx->last_done, 0) != hipSuccess)
+      return false;
+    const uint32_t gen = ++ctx->svc_gen;
+    const uint32_t t0 = reserve_hand_tags(ctx, kServiceMaxPasses);
+    __atomic_store_n(&ctx->svc_box->gen, gen, __ATOMIC_RELEASE);
+    k_decode_service<SmallNarrow><<<kSmallStageWGs, SmallNarrow::NT, 0, st>>>(
+        ctx->svc_box_dev, gen, ctx->svc_last, kServiceLifeMs * ctx->wall_khz, ctx->done_flag, ctx->ticks,
+        ctx->d_svc_ctl, ctx->d_small_stage, ctx->d_done + kSmallStageCounter, t0);
+    if (hipGetLastError() != hipSuccess || mark_last(ctx, st) != GEVWS_OK) {
+      __atomic_store_n(&ctx->svc_box->gen, ++ctx->svc_gen, __ATOMIC_RELEASE);
+      return false;
+    }
+    ctx->svc_live = true;
+    ctx->svc_t_launch_ns = now;
+    ctx->svc_flag = ctx->done_flag;
+    ctx->svc_flag_host = static_cast<const uint32_t*>(pa.hostPointer);
+    ctx->svc_ticks = ctx->ticks;
+    ctx->svc_t0 = t0;
+    ctx->svc_passes = 0;
+    ++ctx->svc_launches;
+  }
+  uint32_t seq = ++ctx->done_seq;
+  if (seq == 0) seq = ++ctx->done_seq;  // (0: no pass, to the kernel)
+  const uint64_t a[kServiceArgs] = {reinterpret_cast<uint64_t>(d_in),      in_bytes,
+                                    reinterpret_cast<uint64_t>(d_conns),   n_conns,
+                                    reinterpret_cast<uint64_t>(d_frames),  max_frames,
+                                    reinterpret_cast<uint64_t>(d_payload), payload_cap,
+                                    reinterpret_cast<uint64_t>(d_conn_out), reinterpret_cast<uint64_t>(d_summary)};
+  for (int k = 0; k < kServiceArgs; ++k) __atomic_store_n(&ctx->svc_box->args[k], a[k], __ATOMIC_RELAXED);
+  __atomic_store_n(&ctx->svc_box->req, ((uint64_t)ctx->svc_gen << 32) | seq, __ATOMIC_RELEASE);  // after the args
+  ctx->svc_last = seq;
+  ctx->last_signal = seq;
+  ++ctx->svc_passes;
+  ++ctx->svc_posts;
+  return true;
 }
 
 int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,

@@ -5,7 +5,9 @@
 // PeekAll segments gathered into pinned staging, H2D, decode, D2H), then
 // websocket.(*Protocol).UnPacket per connection hands the frames out.  Small
 // passes run zero-copy on mapped host memory (gevws_protocol_set_zero_copy_max;
-// env GEVWS_LB_ZERO_COPY_MAX overrides the default for an A/B).
+// env GEVWS_LB_ZERO_COPY_MAX overrides the default for an A/B); with
+// GEVWS_LB_SERVICE=1 they are posted to the context's resident decode service
+// (gevws_protocol_set_service) instead of launched.
 #include "ws_loopback.hpp"
 
 namespace {
@@ -28,6 +30,11 @@ struct DeviceDecoder {
       gevws_protocol_set_zero_copy_max(p, strtoull(zc, nullptr, 10));
     if (const char* sb = getenv("GEVWS_LB_SMALL_BATCH"))  // A/B: 0 = multi-kernel decode for small passes
       gevws_ctx_set_tuning(ctx, GEVWS_TUNE_SMALL_BATCH, (int64_t)strtoll(sb, nullptr, 10));
+    if (const char* sv = getenv("GEVWS_LB_SERVICE"))  // 1: passes posted to a resident decode service
+      if (atoi(sv) == 1 && gevws_protocol_set_service(p, 1) != GEVWS_OK) {
+        fprintf(stderr, "ws_loopback: gevws_protocol_set_service failed\n");
+        exit(2);
+      }
     u = gevws_upgrader_new();  // &ws.Upgrader{} as benchmarks/websocket/server.go:52
     gevws_protocol_set_upgrader(p, u);
   }
@@ -67,7 +74,12 @@ struct DeviceDecoder {
     return gevws_protocol_reply(p, s->c, out, len, shutdown_write);
   }
   static constexpr bool kTimeline = true;
-  void timeline(gevws_protocol_timeline* t) const { gevws_protocol_get_timeline(p, t); }
+  void timeline(gevws_protocol_timeline* t) const {
+    gevws_protocol_get_timeline(p, t);
+    gevws_protocol_stats s;
+    gevws_protocol_get_stats(p, &s);
+    wslb::g_service_passes += s.service_passes;
+  }
   static const char* name() { return "device"; }
   static const char* path() { return "batched device decode (gevws_protocol_unpacket_batch) -> UnPacket"; }
 };

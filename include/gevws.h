@@ -215,6 +215,25 @@ int64_t gevws_ctx_last_split_fallbacks(gevws_ctx *ctx);
  * stores, or -1 when that call ended with another kernel or copy (the caller
  * synchronises the stream as usual). */
 int gevws_ctx_set_completion_flag(gevws_ctx *ctx, uint32_t *d_flag);
+/* The resident decode service (opt-in; a live loop's passes without the launch
+ * call's ~5 us of host time).  With it on and a completion flag set,
+ * gevws_decode_batch_post hands a pass of at most 256 connections and 64 KiB
+ * to a kernel kept resident on the context's stream (launched by the first
+ * post; 32 workgroups, as many as a launched live pass stages its input with):
+ * the pass's arguments go into a mailbox in mapped host memory, the kernel
+ * polls it, decodes exactly as the one-launch decode and stores the pass's
+ * number in the completion word.  One pass at a time: a post before the last
+ * posted pass has signalled is launched instead, behind it.  Any other call
+ * that enqueues work on the context ends the instance first (the pass posted
+ * before it still runs, and that work runs behind it); an instance also ends
+ * 200 ms after its start (the next post replaces it after 100 ms).  While one
+ * is live the context's stream does not drain: call gevws_ctx_service_stop
+ * before synchronising it directly.  enable = 0 stops it and turns posting
+ * off (the default).  gevws_ctx_service_stats: instances launched and passes
+ * posted to them, since the context's creation. */
+int gevws_ctx_set_service(gevws_ctx *ctx, int enable);
+int gevws_ctx_service_stop(gevws_ctx *ctx);
+int gevws_ctx_service_stats(const gevws_ctx *ctx, int64_t *launches, int64_t *posts);
 /* With a completion flag set: d_ticks (device address of 4 u64 in mapped,
  * coherent host memory, or NULL = off) receives, before the flag, each
  * one-launch kernel's start and end tick of the GPU's constant-rate wall
@@ -252,6 +271,16 @@ int gevws_decode_batch_async(gevws_ctx *ctx, void *stream, const uint8_t *d_in, 
                              gevws_frame *d_frames, uint64_t max_frames,
                              uint8_t *d_payload, uint64_t payload_cap,
                              gevws_conn_out *d_conn_out, gevws_summary *d_summary);
+/* A live pass on the context's own stream: posted to the resident decode
+ * service when it is on (gevws_ctx_set_service), a completion flag is set and
+ * the pass fits its shape (<= 256 connections, <= 64 KiB), else
+ * exactly gevws_decode_batch_async on the context's stream.  Either way the
+ * caller waits for gevws_ctx_completion_seq in the completion word (-1: the
+ * stream). */
+int gevws_decode_batch_post(gevws_ctx *ctx, const uint8_t *d_in, uint64_t in_bytes,
+                            const gevws_conn_in *d_conns, uint32_t n_conns, gevws_frame *d_frames,
+                            uint64_t max_frames, uint8_t *d_payload, uint64_t payload_cap,
+                            gevws_conn_out *d_conn_out, gevws_summary *d_summary);
 
 /* Synchronous form: same work, waits, copies the summary to *h_summary and
  * returns its status. */
@@ -523,6 +552,9 @@ typedef struct gevws_protocol_stats {
     uint64_t signalled_passes;       /* waits answered by the kernels' completion
                                       * flag (gevws_ctx_set_completion_flag)
                                       * instead of a stream synchronisation */
+    uint64_t service_passes;  /* passes posted to the resident decode service */
+    uint64_t service_misses;  /* of those, launched again after the instance
+                               * ended without them (not expected) */
 } gevws_protocol_stats;
 void gevws_protocol_get_stats(const gevws_protocol *p, gevws_protocol_stats *out);
 
@@ -572,6 +604,10 @@ int gevws_protocol_set_handler(gevws_protocol *p, int policy);
 int gevws_protocol_reply(const gevws_protocol *p, const gevws_conn *c, const uint8_t **reply, uint64_t *len,
                          int *shutdown_write);
 void gevws_protocol_set_zero_copy_max(gevws_protocol *p, uint64_t bytes);
+/* The protocol's zero-copy passes without a handler step go to its context's
+ * resident decode service (gevws_ctx_set_service, gevws_decode_batch_post):
+ * no launch call on the loop's path.  on = 0 stops it (the default). */
+int gevws_protocol_set_service(gevws_protocol *p, int on);
 
 /* One connection's buffered bytes in host memory, as ringbuffer.PeekAll()
  * returns them (first, end) -- e.g. two Go slices passed through cgo. */

@@ -174,3 +174,12 @@ def test_wsserver_close_connection_mirror(close_frame):
     assert (d["live_after_connect"], d["live_after_close"], d["live_at_end"]) == (10, 5, 0)
     if close_frame:
         assert d["closes_answered"] == 5
+
+
+def test_c1_loopback_resident_service():
+    """GEVWS_LB_SERVICE=1: the live server's zero-copy passes are posted to the
+    context's resident decode service (no launch call); every echo is still
+    checked byte for byte, and the passes really went there."""
+    d = _run("gev_amd/ws_loopback", conns=100, seconds=1.5, env={"GEVWS_LB_SERVICE": "1"})
+    tl = d["pass_timeline_us"]
+    assert tl["service_share"] > 0.9 and tl["signalled_share"] > 0.9, tl
