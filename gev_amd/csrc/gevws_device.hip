@@ -215,7 +215,7 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   // the last call may have run on another stream (a caller's): its kernels
   // still read the scratch freed below
-  if (ctx->has_last && ctx->last_done) (void)hipEventSynchronize(ctx->last_done);
+  if (ctx->has_last && ctx->last_done && last_event(ctx) == GEVWS_OK) (void)hipEventSynchronize(ctx->last_done);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->d_sum) (void)hipFree(ctx->d_sum);
   if (ctx->d_done) (void)hipFree(ctx->d_done);
@@ -296,7 +296,7 @@ int64_t gevws_ctx_last_split_fallbacks(gevws_ctx* ctx) {
   if (ctx->last_ks <= 1) return 0;
   DeviceGuard g(ctx->device);
   uint32_t n = 0;
-  if ((ctx->has_last && hipEventSynchronize(ctx->last_done) != hipSuccess) ||
+  if ((ctx->has_last && (last_event(ctx) != GEVWS_OK || hipEventSynchronize(ctx->last_done) != hipSuccess)) ||
       hipMemcpy(&n, ctx->d_done + split_fallback_counter(), sizeof(n), hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return (int64_t)n;

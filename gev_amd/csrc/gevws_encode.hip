@@ -1161,7 +1161,7 @@ int gevws_handle_decoded_async(gevws_ctx* ctx, void* stream, const gevws_frame* 
                                            d_replies, d_reply_of, d_disp_summary, d_out, out_cap, d_out_off,
                                            d_enc_summary, ctx->done_flag, seq, ctx->done_flag ? ctx->ticks : nullptr);
   GEVWS_HIP(hipGetLastError());
-  r = mark_last(ctx, st);
+  r = mark_last(ctx, st);  // (recorded now: see mark_last_lazy)
   if (ctx->done_flag) ctx->last_signal = seq;
   return r;
 }

@@ -63,6 +63,7 @@ struct gevws_ctx {
   hipEvent_t last_done = nullptr;
   hipStream_t last_stream = nullptr;
   bool has_last = false;
+  bool last_recorded = true;  // last_done marks the last call (else: recorded when first needed)
   int num_cus = 256;
   uint32_t* d_done = nullptr;  // 256 B: the decode walk's finished-workgroup counter ([0], zero between calls)
                                // and the one-launch decode's staging counter ([kSmallStageCounter])
@@ -142,9 +143,22 @@ inline void service_stop(gevws_ctx* ctx) {
 
 // Orders this call after the context's previous one when the stream changes
 // (and ends the service instance first: every launcher calls this).
+// last_done, recorded now if the last call left it to its first use.
+inline int last_event(gevws_ctx* ctx) {
+  if (ctx->has_last && !ctx->last_recorded) {
+    GEVWS_HIP(hipEventRecord(ctx->last_done, ctx->last_stream));
+    ctx->last_recorded = true;
+  }
+  return GEVWS_OK;
+}
+
 inline int order_after_last(gevws_ctx* ctx, hipStream_t st) {
   service_stop(ctx);
-  if (ctx->has_last && ctx->last_stream != st) GEVWS_HIP(hipStreamWaitEvent(st, ctx->last_done, 0));
+  if (ctx->has_last && ctx->last_stream != st) {
+    const int r = last_event(ctx);
+    if (r != GEVWS_OK) return r;
+    GEVWS_HIP(hipStreamWaitEvent(st, ctx->last_done, 0));
+  }
   return GEVWS_OK;
 }
 
@@ -153,6 +167,25 @@ inline int mark_last(gevws_ctx* ctx, hipStream_t st) {
   GEVWS_HIP(hipEventRecord(ctx->last_done, st));
   ctx->last_stream = st;
   ctx->has_last = true;
+  ctx->last_recorded = true;
+  return GEVWS_OK;
+}
+
+// A one-launch call on the context's own stream, where only this context
+// enqueues work: its event is recorded only when something needs it (another
+// stream's call, a synchronisation, destroy) -- an event recorded later on
+// that stream marks this call and nothing foreign.  Saves a live pass the
+// hipEventRecord call (C1's launch phase 4.7-5.5 -> 3.4-3.9 us,
+// profiles/r06/r06n_lb_ab.jsonl).  The one-launch decode only: with the
+// handler step chained behind it lazy too (no marker between a pass and the
+// next), the wsserver shape lost 25 % (r06m_lb_ab.jsonl: launch 13-15 ->
+// 21-24 us, its decode kernel 9.4 -> 11 us), so k_handle_small records.
+inline int mark_last_lazy(gevws_ctx* ctx, hipStream_t st) {
+  if (st != ctx->stream) return mark_last(ctx, st);
+  ctx->last_signal = -1;
+  ctx->last_stream = st;
+  ctx->has_last = true;
+  ctx->last_recorded = false;
   return GEVWS_OK;
 }
 

@@ -1787,7 +1787,7 @@ static int launch_decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_
                                            ctx->done_flag ? ctx->ticks : nullptr, ctx->d_small_stage,
                                            ctx->d_done + kSmallStageCounter, tag);
   GEVWS_HIP(hipGetLastError());
-  const int r = mark_last(ctx, st);
+  const int r = mark_last_lazy(ctx, st);
   if (ctx->done_flag) ctx->last_signal = seq;
   return r;
 }
@@ -1837,7 +1837,8 @@ bool service_post(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t 
       }
       if (hipMemsetAsync(ctx->d_svc_ctl, 0, cb, st) != hipSuccess) return false;
     }
-    if (ctx->has_last && ctx->last_stream != st && hipStreamWaitEvent(st, ctx->last_done, 0) != hipSuccess)
+    if (ctx->has_last && ctx->last_stream != st &&
+        (last_event(ctx) != GEVWS_OK || hipStreamWaitEvent(st, ctx->last_done, 0) != hipSuccess))
       return false;
     const uint32_t gen = ++ctx->svc_gen;
     const uint32_t t0 = reserve_hand_tags(ctx, kServiceMaxPasses);
@@ -1845,7 +1846,7 @@ bool service_post(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t 
     k_decode_service<SmallNarrow><<<kSmallStageWGs, SmallNarrow::NT, 0, st>>>(
         ctx->svc_box_dev, gen, ctx->svc_last, kServiceLifeMs * ctx->wall_khz, ctx->done_flag, ctx->ticks,
         ctx->d_svc_ctl, ctx->d_small_stage, ctx->d_done + kSmallStageCounter, t0);
-    if (hipGetLastError() != hipSuccess || mark_last(ctx, st) != GEVWS_OK) {
+    if (hipGetLastError() != hipSuccess || mark_last_lazy(ctx, st) != GEVWS_OK) {
       __atomic_store_n(&ctx->svc_box->gen, ++ctx->svc_gen, __ATOMIC_RELEASE);
       return false;
     }

@@ -510,6 +510,48 @@ def test_one_context_two_streams_is_ordered(engine):
         assert np.array_equal(out.payload_host(), want["payload"])
 
 
+def test_own_stream_live_pass_then_other_stream_is_ordered(engine):
+    """A one-launch call on the context's own stream leaves its last-call
+    event to be recorded when first needed (mark_last_lazy): a live pass
+    posted there (gevws_decode_batch_post, staged through the context's
+    granules by up to 32 workgroups) and one issued right after it on a
+    torch stream (the same granules) still run in order, so both decode
+    right -- five times over."""
+    import torch
+    import gev_amd
+    rng = np.random.default_rng(18)
+    dev = torch.device("cuda", engine.device)
+    flag = gev_amd.PinnedArena(4096)
+    engine.set_completion_flag(flag, 64)
+    try:
+        for rep in range(5):
+            batches = []
+            for nconn in (200, 150):
+                streams = [random_stream(rng, int(rng.integers(1, 6)), max_len=200) for _ in range(nconn)]
+                arena, conns = pack_streams(streams)
+                a = np.frombuffer(arena, np.uint8).copy()
+                d_in = torch.zeros(a.size + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+                d_in[: a.size] = torch.from_numpy(a).to(dev)
+                d_c = torch.from_numpy(conns.copy()).to(dev)
+                mf, cap = a.size // 2 + 1, a.size * 9 + 64
+                batches.append((a, conns, d_in, d_c, engine.alloc_batch(nconn, mf, cap), mf, cap))
+            torch.cuda.synchronize()
+            (a, conns, d_in, d_c, out, mf, cap), second = batches
+            engine.decode_post(d_in, a.size, d_c, conns.shape[0], out, mf, cap)  # the context's stream
+            s1 = torch.cuda.Stream(dev)
+            a, conns, d_in, d_c, out, mf, cap = second
+            engine.decode_async(d_in, a.size, d_c, conns.shape[0], out, mf, cap, stream=s1)
+            torch.cuda.synchronize()
+            for a, conns, d_in, d_c, out, mf, cap in batches:
+                assert int(out.summary_host()["status"]) == 0, rep
+                want = ref.decode_batch(a, conns[:, 0], conns[:, 1])
+                assert out.frames_host().tobytes() == want["frames"].tobytes(), rep
+                assert np.array_equal(out.payload_host(), want["payload"]), rep
+    finally:
+        engine.set_completion_flag(None)
+        flag.close()
+
+
 def test_every_unmask_variant_big_frames_all_alignments(engine):
     """Each unmask variant (the default's aligned-load streaming path included)
     over frames >= 16 tiles whose payloads start at all 16 source alignments,
