@@ -280,6 +280,23 @@ class Engine:
         """gevws_ctx_service_stop: end the live instance (the next post starts another)."""
         lib.gevws_ctx_service_stop(self._ctx)
 
+    def set_direct(self, on: bool) -> None:
+        """gevws_ctx_set_direct: live passes written into the context's own AQL queue."""
+        st = lib.gevws_ctx_set_direct(self._ctx, 1 if on else 0)
+        if st != OK:
+            raise RuntimeError(f"gevws_ctx_set_direct: {status_string(st)}")
+
+    @property
+    def direct_dispatches(self) -> int:
+        """gevws_ctx_direct_dispatches: passes written into the context's own queue so far."""
+        return int(lib.gevws_ctx_direct_dispatches(self._ctx))
+
+    def synchronize(self) -> None:
+        """gevws_ctx_synchronize: everything the context enqueued (stream, own queue, service)."""
+        st = lib.gevws_ctx_synchronize(self._ctx)
+        if st != OK:
+            raise RuntimeError(f"gevws_ctx_synchronize: {status_string(st)}")
+
     def service_stats(self) -> dict:
         """gevws_ctx_service_stats: service instances launched, passes posted to them."""
         la, po = ctypes.c_int64(), ctypes.c_int64()
@@ -884,6 +901,13 @@ class Protocol:
         st = lib.gevws_protocol_set_service(self._p, 1 if on else 0)
         if st != OK:
             raise RuntimeError(f"gevws_protocol_set_service: {status_string(st)}")
+
+    def set_direct(self, on: bool) -> None:
+        """gevws_protocol_set_direct: zero-copy passes without a handler step
+        are written into the context's own AQL queue (no HIP launch call)."""
+        st = lib.gevws_protocol_set_direct(self._p, 1 if on else 0)
+        if st != OK:
+            raise RuntimeError(f"gevws_protocol_set_direct: {status_string(st)}")
 
     def set_zero_copy_max(self, nbytes: int) -> None:
         """gevws_protocol_set_zero_copy_max: batched passes over at most

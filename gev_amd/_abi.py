@@ -198,6 +198,9 @@ SIGNATURES = {
     "gevws_ctx_set_service": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_ctx_service_stop": (ctypes.c_int, [P]),
     "gevws_ctx_service_stats": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "gevws_ctx_set_direct": (ctypes.c_int, [P, ctypes.c_int]),
+    "gevws_ctx_direct_dispatches": (ctypes.c_int64, [P]),
+    "gevws_ctx_synchronize": (ctypes.c_int, [P]),
     "gevws_decode_batch_post": (ctypes.c_int, [P, P, ctypes.c_uint64, P, ctypes.c_uint32, P, ctypes.c_uint64, P,
                                                ctypes.c_uint64, P, P]),
     "gevws_ctx_completion_seq": (ctypes.c_int64, [P]),
@@ -255,6 +258,7 @@ SIGNATURES = {
     "gevws_protocol_get_timeline": (None, [P, ctypes.POINTER(ProtocolTimeline)]),
     "gevws_protocol_set_zero_copy_max": (None, [P, ctypes.c_uint64]),
     "gevws_protocol_set_service": (ctypes.c_int, [P, ctypes.c_int]),
+    "gevws_protocol_set_direct": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_protocol_set_handler": (ctypes.c_int, [P, ctypes.c_int]),
     "gevws_comm_create": (P, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "gevws_comm_destroy": (None, [P]),

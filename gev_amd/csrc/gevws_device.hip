@@ -212,6 +212,7 @@ void gevws_ctx_destroy(gevws_ctx* ctx) {
   if (!ctx) return;
   DeviceGuard g(ctx->device);
   service_stop(ctx);  // (its instance returns at once: the stream drains)
+  direct_close(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   // the last call may have run on another stream (a caller's): its kernels
   // still read the scratch freed below
@@ -304,6 +305,7 @@ int64_t gevws_ctx_last_split_fallbacks(gevws_ctx* ctx) {
 
 int gevws_ctx_set_completion_flag(gevws_ctx* ctx, uint32_t* d_flag) {
   if (!ctx) return GEVWS_ERR_INVALID;
+  if (d_flag != ctx->done_flag) direct_forget_flag(ctx);
   ctx->done_flag = d_flag;
   ctx->last_signal = -1;
   return GEVWS_OK;
@@ -412,6 +414,34 @@ int gevws_ctx_service_stop(gevws_ctx* ctx) {
   return GEVWS_OK;
 }
 
+int gevws_ctx_set_direct(gevws_ctx* ctx, int enable) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  if (!enable) direct_forget_flag(ctx);
+  ctx->direct_enabled = enable != 0;
+  return GEVWS_OK;
+}
+
+int64_t gevws_ctx_direct_dispatches(const gevws_ctx* ctx) { return ctx ? ctx->direct_dispatches : -1; }
+
+int gevws_ctx_synchronize(gevws_ctx* ctx) {
+  if (!ctx) return GEVWS_ERR_INVALID;
+  DeviceGuard g(ctx->device);
+  service_stop(ctx);
+  if (ctx->last_direct) {
+    const int r = direct_drain(ctx);
+    if (r != GEVWS_OK) return r;
+    ctx->last_direct = false;
+  }
+  GEVWS_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->has_last && ctx->last_stream != ctx->stream) {
+    const int r = last_event(ctx);
+    if (r != GEVWS_OK) return r;
+    GEVWS_HIP(hipEventSynchronize(ctx->last_done));
+  }
+  return GEVWS_OK;
+}
+
 int gevws_ctx_service_stats(const gevws_ctx* ctx, int64_t* launches, int64_t* posts) {
   if (!ctx) return GEVWS_ERR_INVALID;
   if (launches) *launches = ctx->svc_launches;
@@ -426,6 +456,11 @@ int gevws_decode_batch_post(gevws_ctx* ctx, const uint8_t* d_in, uint64_t in_byt
   if (n_conns && (!d_in || !d_conns || !d_conn_out)) return GEVWS_ERR_INVALID;
   if (max_frames > 0xFFFFFFFFull) return GEVWS_ERR_INVALID;
   DeviceGuard g(ctx->device);
+  if (!ctx->timing && ctx->walk_variant == 0 && ctx->unmask_variant == 0 && ctx->unmask_grid == 0 &&
+      in_bytes <= ctx->small_bytes &&
+      direct_post(ctx, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload, payload_cap, d_conn_out,
+                  d_summary))
+    return GEVWS_OK;
   if (!ctx->timing && ctx->walk_variant == 0 && ctx->unmask_variant == 0 && ctx->unmask_grid == 0 &&
       in_bytes <= ctx->small_bytes &&
       service_post(ctx, ctx->stream, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload, payload_cap,

@@ -492,6 +492,11 @@ class Protocol {
     if (r == GEVWS_OK) service_ = on != 0;
     return r;
   }
+  int SetDirect(int on) {
+    const int r = gevws_ctx_set_direct(ctx_, on);
+    if (r == GEVWS_OK) direct_ = on != 0;
+    return r;
+  }
 
  private:
   struct DeviceScope {
@@ -761,7 +766,7 @@ class Protocol {
       if (!din || !dres || !dfr || !dpay) return fail();
       // (with the resident service on and no handler chained behind, the
       // pass is posted to it instead of launched: gevws_decode_batch_post)
-      const bool post = may_post && service_ && handler_ < 0 && sg->flagged;
+      const bool post = may_post && (service_ || direct_) && handler_ < 0 && sg->flagged;
       int64_t posts0 = 0, posts1 = 0;
       if (post) (void)gevws_ctx_service_stats(ctx_, nullptr, &posts0);
       const int r = post
@@ -841,15 +846,14 @@ class Protocol {
         __builtin_ia32_pause();
       }
     }
-    if (service_) (void)gevws_ctx_service_stop(ctx_);  // (a live instance would hold the stream)
-    if (hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_)) != hipSuccess) return fail();
+    // (the stream, a live service instance -- stopped first -- and direct passes)
+    if (gevws_ctx_synchronize(ctx_) != GEVWS_OK) return fail();
     if (seq >= 0 && __atomic_load_n(h_flag_, __ATOMIC_ACQUIRE) == (uint32_t)seq) {
       last_signalled_ = true;
     } else if (sg->posted) {
       // the service's instance ended without the pass (not seen): launch it
       ++stats_.service_misses;
-      if (Launch(sg, false) < 0 || hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_)) != hipSuccess)
-        return fail();
+      if (Launch(sg, false) < 0 || gevws_ctx_synchronize(ctx_) != GEVWS_OK) return fail();
     }
     return 0;
   }
@@ -875,8 +879,7 @@ class Protocol {
   // follow an enqueued H2D copy or a zero-copy kernel still reading the
   // pinned staging, which the next pass would overwrite.
   int64_t fail() {
-    if (ctx_ && service_) (void)gevws_ctx_service_stop(ctx_);
-    if (ctx_) (void)hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_));
+    if (ctx_) (void)gevws_ctx_synchronize(ctx_);  // (a service instance stopped, direct passes drained too)
     log_error("device: ", GEVWS_ERR_DEVICE);
     return GEVWS_ERR_DEVICE;
   }
@@ -906,7 +909,8 @@ class Protocol {
   }
   void release() {
     if (ctx_ && service_) (void)gevws_ctx_set_service(ctx_, 0);
-    if (ctx_) (void)hipStreamSynchronize((hipStream_t)gevws_ctx_stream(ctx_));
+    if (ctx_ && direct_) (void)gevws_ctx_set_direct(ctx_, 0);
+    if (ctx_) (void)gevws_ctx_synchronize(ctx_);
     if (h_flag_) {
       if (ctx_) (void)gevws_ctx_set_completion_flag(ctx_, nullptr);
       (void)hipHostFree(h_flag_);
@@ -945,6 +949,7 @@ class Protocol {
   uint64_t zc_max_ = GEVWS_ZERO_COPY_MAX_DEFAULT;
   int handler_ = -1;  // device handler policy (GEVWS_HANDLER_*), -1 = none
   bool service_ = false;  // passes posted to the context's resident decode service
+  bool direct_ = false;   // passes written into the context's own queue (gevws_ctx_set_direct)
   uint8_t *h_rof_ = nullptr, *h_roff_ = nullptr, *h_hs_ = nullptr;  // handler outputs (mapped pinned)
   uint64_t h_rof_cap_ = 0, h_roff_cap_ = 0, h_hs_cap_ = 0;
   void* d_rep_ = nullptr;  // reply records (gevws_out_frame)
@@ -1050,6 +1055,11 @@ void gevws_protocol_set_zero_copy_max(gevws_protocol* p, uint64_t bytes) {
 int gevws_protocol_set_service(gevws_protocol* p, int on) {
   if (!p) return GEVWS_ERR_INVALID;
   return p->SetService(on);
+}
+
+int gevws_protocol_set_direct(gevws_protocol* p, int on) {
+  if (!p) return GEVWS_ERR_INVALID;
+  return p->SetDirect(on);
 }
 
 int gevws_protocol_set_handler(gevws_protocol* p, int policy) {

@@ -19,6 +19,27 @@ struct ServiceBox {
   uint64_t args[kServiceArgs];  // the posted pass's arguments (device addresses and sizes)
 };
 
+// The one-launch decode's arguments as one by-value kernel argument, so a
+// dispatch written straight into an AQL queue (gevws_direct.cpp) lays out the
+// kernarg segment exactly as the kernel reads it (k_decode_small_direct).
+struct DirectDecodeArgs {
+  const uint8_t* in;
+  uint64_t in_bytes;
+  const gevws_conn_in* conns;
+  gevws_frame* frames;
+  uint64_t max_frames;
+  uint8_t* payload;
+  uint64_t payload_cap;
+  gevws_conn_out* cout;
+  gevws_summary* sum;
+  uint32_t* done;
+  uint64_t* ticks;
+  uint64_t* stage_buf;
+  uint32_t* stage_done;
+  uint32_t n, seq, tag, nwg;
+};
+struct DirectQueue;  // gevws_direct.cpp
+
 struct gevws_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -87,6 +108,12 @@ struct gevws_ctx {
   uint32_t svc_t0 = 0, svc_passes = 0;  // the live instance's tags [t0, t0 + kServiceMaxPasses); passes posted
   int64_t svc_launches = 0, svc_posts = 0;  // (gevws_ctx_service_stats)
   uint64_t wall_khz = 100000;     // the GPU's constant-rate clock (hipDeviceAttributeWallClockRate)
+  // direct dispatch (gevws_ctx_set_direct): live passes written into the
+  // context's own AQL queue instead of launched through the HIP runtime
+  bool direct_enabled = false;
+  DirectQueue* direct = nullptr;
+  bool last_direct = false;  // the last call went to that queue (not the stream)
+  int64_t direct_dispatches = 0;
 };
 
 // The tag of a launch's hand-offs.
@@ -141,8 +168,6 @@ inline void service_stop(gevws_ctx* ctx) {
   ctx->svc_live = false;
 }
 
-// Orders this call after the context's previous one when the stream changes
-// (and ends the service instance first: every launcher calls this).
 // last_done, recorded now if the last call left it to its first use.
 inline int last_event(gevws_ctx* ctx) {
   if (ctx->has_last && !ctx->last_recorded) {
@@ -152,8 +177,20 @@ inline int last_event(gevws_ctx* ctx) {
   return GEVWS_OK;
 }
 
+// gevws_direct.cpp: waits until every pass dispatched to the context's own
+// queue has signalled (GEVWS_ERR_DEVICE past 10 s).
+int direct_drain(gevws_ctx* ctx);
+
+// Orders this call after the context's previous one when the stream changes
+// or the previous one went to the context's own queue (and ends the service
+// instance first: every launcher calls this).
 inline int order_after_last(gevws_ctx* ctx, hipStream_t st) {
   service_stop(ctx);
+  if (ctx->last_direct) {
+    const int r = direct_drain(ctx);
+    if (r != GEVWS_OK) return r;
+    ctx->last_direct = false;
+  }
   if (ctx->has_last && ctx->last_stream != st) {
     const int r = last_event(ctx);
     if (r != GEVWS_OK) return r;
@@ -208,6 +245,14 @@ inline int ensure_scratch(gevws_ctx* ctx, size_t bytes) {
 int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,
                  const gevws_conn_in* d_conns, uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames,
                  uint8_t* d_payload, uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary);
+// a live pass written into the context's own AQL queue, or false (gevws_direct.cpp)
+bool direct_dispatch(gevws_ctx* ctx, int wide, const DirectDecodeArgs& a);
+void direct_close(gevws_ctx* ctx);
+// drains the direct passes and drops the completion word they signal (it is being replaced or freed)
+void direct_forget_flag(gevws_ctx* ctx);
+bool direct_post(gevws_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const gevws_conn_in* d_conns,
+                 uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames, uint8_t* d_payload,
+                 uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary);
 // a narrow-shape live pass posted to the context's resident decode service
 // (launched first if none is live), or false (gevws_decode_batch_post)
 bool service_post(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,

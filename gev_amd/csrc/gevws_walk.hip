@@ -1595,6 +1595,15 @@ __global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restric
                              ticks, stage_buf, stage_done, tag, gridDim.x, blockIdx.x, gridDim.x);
 }
 
+// The same with its arguments in one by-value struct: the form a dispatch
+// written straight into the context's own AQL queue takes (gevws_direct.cpp).
+template <class S>
+__global__ __launch_bounds__(S::NT) void k_decode_small_direct(DirectDecodeArgs a) {
+  (void)decode_small_body<S>(a.in, a.in_bytes, a.conns, a.n, a.frames, a.max_frames, a.payload, a.payload_cap,
+                             a.cout, a.sum, a.done, a.seq, a.ticks, a.stage_buf, a.stage_done, a.tag, a.nwg,
+                             blockIdx.x, a.nwg);
+}
+
 // ------------------------------------------------------------------ 3d. the resident decode service
 // A live pass's launch call costs its loop ~5 us of host time whatever the
 // pass (the HIP runtime's).  With the service on (gevws_ctx_set_service), a
@@ -1752,6 +1761,10 @@ constexpr int kNumWalkVariants = sizeof(kWalkVariants) / sizeof(kWalkVariants[0]
 namespace gevws_impl {
 
 int walk_variant_count() { return kNumWalkVariants; }
+const void* direct_kernel_stub(int wide) {
+  return wide ? reinterpret_cast<const void*>(&k_decode_small_direct<SmallWide>)
+              : reinterpret_cast<const void*>(&k_decode_small_direct<SmallNarrow>);
+}
 uint32_t split_fallback_counter() { return kSplitFallbackCounter; }
 const char* walk_variant_name(int i) { return i >= 0 && i < kNumWalkVariants ? kWalkVariants[i] : nullptr; }
 
@@ -1826,6 +1839,10 @@ bool service_post(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t 
       return false;  // the last pass still runs
   }
   if (!ctx->svc_live) {
+    if (ctx->last_direct) {  // (passes on the context's own queue finish first)
+      if (direct_drain(ctx) != GEVWS_OK) return false;
+      ctx->last_direct = false;
+    }
     hipPointerAttribute_t pa;
     if (hipPointerGetAttributes(&pa, ctx->done_flag) != hipSuccess || !pa.hostPointer) return false;
     if (!ensure_small_stage(ctx, st)) return false;
@@ -1888,6 +1905,47 @@ int decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t i
                                             d_payload, payload_cap, d_conn_out, d_summary);
   return launch_decode_small<SmallWide>(ctx, st, d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
                                         payload_cap, d_conn_out, d_summary);
+}
+
+// A live pass written into the context's own AQL queue (gevws_direct.cpp),
+// or false: launch it as usual.  Same kernel body, shape and staging as the
+// launched one-launch decode.
+bool direct_post(gevws_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const gevws_conn_in* d_conns,
+                 uint32_t n_conns, gevws_frame* d_frames, uint64_t max_frames, uint8_t* d_payload,
+                 uint64_t payload_cap, gevws_conn_out* d_conn_out, gevws_summary* d_summary) {
+  if (!ctx->direct_enabled || !ctx->done_flag || n_conns > kOneLaunchConns || in_bytes > kOneLaunchBytes)
+    return false;
+  service_stop(ctx);
+  const int wide = n_conns <= kSmallConns && in_bytes <= kSmallBytes ? 0 : 1;
+  uint32_t nwg = n_conns ? small_slices(in_bytes, n_conns, kSmallStageWGs) : 1u;
+  if (nwg > 1 && !ctx->d_small_stage) {  // (allocated and zeroed on the stream, once)
+    if (!ensure_small_stage(ctx, ctx->stream)) nwg = 1;
+    else if (hipStreamSynchronize(ctx->stream) != hipSuccess) return false;
+  }
+  DirectDecodeArgs a;
+  a.in = d_in;
+  a.in_bytes = in_bytes;
+  a.conns = d_conns;
+  a.frames = d_frames;
+  a.max_frames = max_frames;
+  a.payload = d_payload;
+  a.payload_cap = payload_cap;
+  a.cout = d_conn_out;
+  a.sum = d_summary;
+  a.done = ctx->done_flag;
+  a.ticks = ctx->ticks;
+  a.stage_buf = ctx->d_small_stage;
+  a.stage_done = ctx->d_done + kSmallStageCounter;
+  a.n = n_conns;
+  uint32_t seq = ctx->done_seq + 1;
+  if (seq == 0) seq = 1;
+  a.seq = seq;
+  a.tag = nwg > 1 ? next_hand_tag(ctx) : 0u;
+  a.nwg = nwg;
+  if (!direct_dispatch(ctx, wide, a)) return false;
+  ctx->done_seq = seq;
+  ctx->last_signal = seq;
+  return true;
 }
 
 int decode_front(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_in, uint64_t in_bytes,

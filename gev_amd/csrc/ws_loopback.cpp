@@ -7,7 +7,8 @@
 // passes run zero-copy on mapped host memory (gevws_protocol_set_zero_copy_max;
 // env GEVWS_LB_ZERO_COPY_MAX overrides the default for an A/B); with
 // GEVWS_LB_SERVICE=1 they are posted to the context's resident decode service
-// (gevws_protocol_set_service) instead of launched.
+// (gevws_protocol_set_service), with GEVWS_LB_DIRECT=1 written into the
+// context's own AQL queue (gevws_protocol_set_direct), instead of launched.
 #include "ws_loopback.hpp"
 
 namespace {
@@ -33,6 +34,11 @@ struct DeviceDecoder {
     if (const char* sv = getenv("GEVWS_LB_SERVICE"))  // 1: passes posted to a resident decode service
       if (atoi(sv) == 1 && gevws_protocol_set_service(p, 1) != GEVWS_OK) {
         fprintf(stderr, "ws_loopback: gevws_protocol_set_service failed\n");
+        exit(2);
+      }
+    if (const char* dd = getenv("GEVWS_LB_DIRECT"))  // 1: passes written into the context's own AQL queue
+      if (atoi(dd) == 1 && gevws_protocol_set_direct(p, 1) != GEVWS_OK) {
+        fprintf(stderr, "ws_loopback: gevws_protocol_set_direct failed\n");
         exit(2);
       }
     u = gevws_upgrader_new();  // &ws.Upgrader{} as benchmarks/websocket/server.go:52
@@ -79,6 +85,7 @@ struct DeviceDecoder {
     gevws_protocol_stats s;
     gevws_protocol_get_stats(p, &s);
     wslb::g_service_passes += s.service_passes;
+    wslb::g_direct_passes += gevws_ctx_direct_dispatches(ctx);
   }
   static const char* name() { return "device"; }
   static const char* path() { return "batched device decode (gevws_protocol_unpacket_batch) -> UnPacket"; }

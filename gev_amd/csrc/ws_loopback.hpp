@@ -102,6 +102,7 @@ inline std::atomic<uint64_t> g_loop_conns[kMaxLoops];  // connections accepted p
 inline std::mutex g_tl_mu;
 inline gevws_protocol_timeline g_tl{};
 inline std::atomic<uint64_t> g_service_passes{0};  // of those, posted to a resident decode service
+inline std::atomic<uint64_t> g_direct_passes{0};   // ... written into a context's own AQL queue
 inline void add_timeline(const gevws_protocol_timeline& t) {
   std::lock_guard<std::mutex> g(g_tl_mu);
   g_tl.passes += t.passes;
@@ -877,10 +878,10 @@ inline std::string timeline_json() {
   snprintf(b, sizeof(b),
            "{\"passes\": %llu, \"select\": %.2f, \"stage\": %.2f, \"launch\": %.2f, \"wait\": %.2f, "
            "\"deliver\": %.2f, \"signalled_share\": %.3f, \"gpu_decode\": %.2f, \"gpu_handler\": %.2f, "
-           "\"gpu_gap\": %.2f, \"service_share\": %.3f}",
+           "\"gpu_gap\": %.2f, \"service_share\": %.3f, \"direct_share\": %.3f}",
            (unsigned long long)t.passes, t.ns_select / p / 1e3, t.ns_stage / p / 1e3, t.ns_launch / p / 1e3,
            t.ns_wait / p / 1e3, t.ns_deliver / p / 1e3, t.signalled / p, t.ns_gpu_decode / s / 1e3,
-           t.ns_gpu_handler / s / 1e3, t.ns_gpu_gap / s / 1e3, g_service_passes.load() / p);
+           t.ns_gpu_handler / s / 1e3, t.ns_gpu_gap / s / 1e3, g_service_passes.load() / p, g_direct_passes.load() / p);
   return b;
 }
 

@@ -234,6 +234,21 @@ int gevws_ctx_set_completion_flag(gevws_ctx *ctx, uint32_t *d_flag);
 int gevws_ctx_set_service(gevws_ctx *ctx, int enable);
 int gevws_ctx_service_stop(gevws_ctx *ctx);
 int gevws_ctx_service_stats(const gevws_ctx *ctx, int64_t *launches, int64_t *posts);
+/* Direct dispatch (opt-in; takes precedence over the service): with it on and
+ * a completion flag set, gevws_decode_batch_post writes a pass that fits the
+ * one-launch decode (<= GEVWS_ONE_LAUNCH_MAX_CONNS / _BYTES) as one AQL
+ * dispatch packet into an HSA queue the context owns -- the same kernel body,
+ * without the HIP runtime's launch call on the caller's path.  Work the
+ * context enqueues on a stream after such passes first waits (on the host)
+ * for their completion words, and a direct pass after stream work waits for
+ * that work.  If the runtime's loader does not expose the kernels, the
+ * context falls back to launching (gevws_ctx_direct_dispatches stays 0).
+ * enable = 0 waits for the outstanding direct passes and turns it off. */
+int gevws_ctx_set_direct(gevws_ctx *ctx, int enable);
+int64_t gevws_ctx_direct_dispatches(const gevws_ctx *ctx);
+/* Waits for everything the context has enqueued: its stream, the passes on
+ * its own queue, a live service instance (stopped first). */
+int gevws_ctx_synchronize(gevws_ctx *ctx);
 /* With a completion flag set: d_ticks (device address of 4 u64 in mapped,
  * coherent host memory, or NULL = off) receives, before the flag, each
  * one-launch kernel's start and end tick of the GPU's constant-rate wall
@@ -608,6 +623,10 @@ void gevws_protocol_set_zero_copy_max(gevws_protocol *p, uint64_t bytes);
  * resident decode service (gevws_ctx_set_service, gevws_decode_batch_post):
  * no launch call on the loop's path.  on = 0 stops it (the default). */
 int gevws_protocol_set_service(gevws_protocol *p, int on);
+/* The same for direct dispatch (gevws_ctx_set_direct): the protocol's
+ * zero-copy passes without a handler step are written into its context's
+ * own queue.  on = 0 turns it off (the default). */
+int gevws_protocol_set_direct(gevws_protocol *p, int on);
 
 /* One connection's buffered bytes in host memory, as ringbuffer.PeekAll()
  * returns them (first, end) -- e.g. two Go slices passed through cgo. */

@@ -12,7 +12,7 @@ run() {  # run <label> <env> <binary> <args...>
   local label=$1 envv=$2 bin=$3; shift 3
   env $envv timeout -k 5 60 $bin --seconds ${SECONDS_PER_RUN:-3} "$@" | grep '^{' | \
     python3 -c "import sys,json; d=json.loads(sys.stdin.read()); d['label']='$label'; print(json.dumps(d))" >> $OUT || return 1
-  tail -1 $OUT | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); t=d.get('pass_timeline_us') or {}; print(d['label'], d['echoes_per_s'], t.get('launch'), t.get('wait'), t.get('gpu_decode'), t.get('signalled_share'), t.get('service_share'))"
+  tail -1 $OUT | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); t=d.get('pass_timeline_us') or {}; print(d['label'], d['echoes_per_s'], t.get('launch'), t.get('wait'), t.get('gpu_decode'), t.get('signalled_share'), t.get('service_share'), t.get('direct_share'))"
 }
 run warmup GEVWS_NOP=1 gev_amd/ws_loopback $C1 || exit 1
 for i in $(seq ${ROUNDS:-3}); do
@@ -20,10 +20,13 @@ for i in $(seq ${ROUNDS:-3}); do
     args=${!shape}
     if [ $((i % 2)) = 1 ]; then
       run ${shape}_dev GEVWS_NOP=1 gev_amd/ws_loopback $args || exit 1
-      run ${shape}_svc GEVWS_LB_SERVICE=1 gev_amd/ws_loopback $args || exit 1
+      [ "${NO_SVC:-0}" = 1 ] || run ${shape}_svc GEVWS_LB_SERVICE=1 gev_amd/ws_loopback $args || exit 1
     else
-      run ${shape}_svc GEVWS_LB_SERVICE=1 gev_amd/ws_loopback $args || exit 1
+      [ "${NO_SVC:-0}" = 1 ] || run ${shape}_svc GEVWS_LB_SERVICE=1 gev_amd/ws_loopback $args || exit 1
       run ${shape}_dev GEVWS_NOP=1 gev_amd/ws_loopback $args || exit 1
+    fi
+    if [ "${DIRECT:-0}" = 1 ]; then  # the context's own AQL queue (gevws_ctx_set_direct)
+      run ${shape}_direct GEVWS_LB_DIRECT=1 gev_amd/ws_loopback $args || exit 1
     fi
     run ${shape}_cpu GEVWS_NOP=1 tools/ws_loopback_cpu $args || exit 1
   done

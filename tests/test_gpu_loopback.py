@@ -183,3 +183,11 @@ def test_c1_loopback_resident_service():
     d = _run("gev_amd/ws_loopback", conns=100, seconds=1.5, env={"GEVWS_LB_SERVICE": "1"})
     tl = d["pass_timeline_us"]
     assert tl["service_share"] > 0.9 and tl["signalled_share"] > 0.9, tl
+
+
+def test_c1_loopback_direct_dispatch():
+    """GEVWS_LB_DIRECT=1: the live server's zero-copy passes are written into
+    each context's own AQL queue; every echo still checked byte for byte."""
+    d = _run("gev_amd/ws_loopback", conns=100, seconds=1.5, env={"GEVWS_LB_DIRECT": "1"})
+    tl = d["pass_timeline_us"]
+    assert tl["direct_share"] > 0.9 and tl["signalled_share"] > 0.9, tl
