@@ -85,6 +85,7 @@ struct gevws_ctx {
   hipStream_t last_stream = nullptr;
   bool has_last = false;
   bool last_recorded = true;  // last_done marks the last call (else: recorded when first needed)
+  bool prev_small_decode = false;  // the last call was a one-launch decode (mark_last_lazy)
   int num_cus = 256;
   uint32_t* d_done = nullptr;  // 256 B: the decode walk's finished-workgroup counter ([0], zero between calls)
                                // and the one-launch decode's staging counter ([kSmallStageCounter])
@@ -205,6 +206,7 @@ inline int mark_last(gevws_ctx* ctx, hipStream_t st) {
   ctx->last_stream = st;
   ctx->has_last = true;
   ctx->last_recorded = true;
+  ctx->prev_small_decode = false;
   return GEVWS_OK;
 }
 
@@ -213,10 +215,12 @@ inline int mark_last(gevws_ctx* ctx, hipStream_t st) {
 // stream's call, a synchronisation, destroy) -- an event recorded later on
 // that stream marks this call and nothing foreign.  Saves a live pass the
 // hipEventRecord call (C1's launch phase 4.7-5.5 -> 3.4-3.9 us,
-// profiles/r06/r06n_lb_ab.jsonl).  The one-launch decode only: with the
-// handler step chained behind it lazy too (no marker between a pass and the
-// next), the wsserver shape lost 25 % (r06m_lb_ab.jsonl: launch 13-15 ->
-// 21-24 us, its decode kernel 9.4 -> 11 us), so k_handle_small records.
+// profiles/r06/r06n_lb_ab.jsonl).  Only a one-launch decode that follows
+// another: with the handler step chained behind it lazy too the wsserver
+// shape lost 25 % (r06m_lb_ab.jsonl: launch 13-15 -> 21-24 us, its decode
+// kernel 9.4 -> 11 us), and with the decode alone lazy behind a recorded
+// handler step 10-20 % on another box (r06t_lb_ab.jsonl); so passes that
+// chain anything behind the decode keep every record.
 inline int mark_last_lazy(gevws_ctx* ctx, hipStream_t st) {
   if (st != ctx->stream) return mark_last(ctx, st);
   ctx->last_signal = -1;

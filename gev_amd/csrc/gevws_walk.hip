@@ -1800,7 +1800,8 @@ static int launch_decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_
                                            ctx->done_flag ? ctx->ticks : nullptr, ctx->d_small_stage,
                                            ctx->d_done + kSmallStageCounter, tag);
   GEVWS_HIP(hipGetLastError());
-  const int r = mark_last_lazy(ctx, st);
+  const int r = ctx->prev_small_decode ? mark_last_lazy(ctx, st) : mark_last(ctx, st);
+  ctx->prev_small_decode = true;
   if (ctx->done_flag) ctx->last_signal = seq;
   return r;
 }
