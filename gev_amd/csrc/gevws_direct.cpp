@@ -250,9 +250,16 @@ bool direct_dispatch(gevws_ctx* ctx, int wide, const DirectDecodeArgs& a) {
   if (ctx->has_last && !ctx->last_direct &&
       (last_event(ctx) != GEVWS_OK || hipEventSynchronize(ctx->last_done) != hipSuccess))
     return false;
+  // The packet slot and the kernarg slot are claimed only once both are free
+  // (a single-producer queue: nothing else moves the write index), so a
+  // failed wait leaves no half-claimed slot for the packet processor to stall on.
   hsa_queue_t* q = dq->q;
-  const uint64_t idx = hsa_queue_add_write_index_scacq_screl(q, 1);
-  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) __builtin_ia32_pause();
+  const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return false;
+    __builtin_ia32_pause();
+  }
   // the kernarg slot: free once the dispatch that used it last has signalled
   const uint32_t slot = (uint32_t)(idx % DirectQueue::kSlots);
   if (idx >= DirectQueue::kSlots && !wait_word(dq->flag_host, dq->slot_seq[slot])) return false;
@@ -281,6 +288,7 @@ bool direct_dispatch(gevws_ctx* ctx, int wide, const DirectDecodeArgs& a) {
                           (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                           (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
   const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+  hsa_queue_store_write_index_screlease(q, idx + 1);
   __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
   hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
   dq->last_seq = a.seq;

@@ -28,12 +28,11 @@ def host_result(out):
     return dict(summary=s, frames=out.frames_host(), conn_out=out.conn_out_host(), payload=out.payload_host())
 
 
-def assert_matches_oracle(engine, arena: bytes | np.ndarray, conns: np.ndarray, tag: str = ""):
-    """GPU decode == C oracle decode, bit-exact, incl. the zeroed pad bytes."""
-    a = np.frombuffer(arena, np.uint8).copy() if isinstance(arena, (bytes, bytearray)) else arena
+def check_against_oracle(got: dict, a: np.ndarray, conns: np.ndarray, tag: str = "") -> None:
+    """A decode's host-side results (host_result) == the C oracle's on the
+    same input, bit-exact, incl. the zeroed pad bytes."""
     conns = np.ascontiguousarray(conns, dtype=np.int64).reshape(-1, 2)
     want = ref.decode_batch(a, conns[:, 0], conns[:, 1])
-    got = host_result(gpu_decode(engine, a, conns))
     s = got["summary"]
     assert int(s["status"]) == 0, tag
     assert int(s["frames"]) == want["frames"].shape[0], tag
@@ -48,7 +47,56 @@ def assert_matches_oracle(engine, arena: bytes | np.ndarray, conns: np.ndarray, 
     assert got["frames"].tobytes() == want["frames"].tobytes(), tag
     assert int(s["run_frames"]) == oracle_run_frames(want, conns), tag
     assert np.array_equal(got["payload"], want["payload"]), tag
+
+
+def assert_matches_oracle(engine, arena: bytes | np.ndarray, conns: np.ndarray, tag: str = ""):
+    """GPU decode == C oracle decode, bit-exact, incl. the zeroed pad bytes."""
+    a = np.frombuffer(arena, np.uint8).copy() if isinstance(arena, (bytes, bytearray)) else arena
+    conns = np.ascontiguousarray(conns, dtype=np.int64).reshape(-1, 2)
+    got = host_result(gpu_decode(engine, a, conns))
+    check_against_oracle(got, a, conns, tag)
     return got
+
+
+def random_batch(rng, n_conns: int, max_len: int = 300, frames=(1, 6)):
+    """n_conns random streams (random_stream) packed back to back: (arena, conns)."""
+    ss = [random_stream(rng, int(rng.integers(*frames)), max_len=max_len) for _ in range(n_conns)]
+    arena = b"".join(ss)
+    lens = np.array([len(s) for s in ss], np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    return np.frombuffer(arena, np.uint8).copy(), np.stack([offs, lens], 1)
+
+
+def post_and_wait(engine, flag, a: np.ndarray, conns: np.ndarray, timeout: float = 5.0):
+    """gevws_decode_batch_post of one live pass (inputs resident first: a post
+    is not stream-ordered behind torch's copies), then a wait for its number
+    in the completion word at flag.host[64:68]; returns its host-side
+    results and the device tensors it used."""
+    import time
+    import torch
+    import gev_amd
+    dev = torch.device("cuda", engine.device)
+    d_in = torch.zeros(a.size + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
+    if a.size:
+        d_in[: a.size] = torch.from_numpy(a).to(dev)
+    n = conns.shape[0]
+    d_conns = torch.from_numpy(np.ascontiguousarray(conns)).to(dev) if n else torch.zeros((1, 2), dtype=torch.int64,
+                                                                                           device=dev)
+    max_frames = a.size // 2 + 1
+    payload_cap = a.size + 16 * min(max_frames, a.size // 64 + 64) + 64
+    out = engine.alloc_batch(n, max_frames, payload_cap)
+    # (torch's stream only: a device-wide synchronize would wait for a
+    # resident service instance's life to end)
+    torch.cuda.current_stream(dev).synchronize()
+    engine.decode_post(d_in, a.size, d_conns, n, out, max_frames, payload_cap)
+    seq = engine.completion_seq
+    assert seq > 0
+    word = flag.host[64:68].view(np.uint32)
+    t0 = time.monotonic()
+    while int(word[0]) != seq:
+        assert time.monotonic() - t0 < timeout, f"pass {seq} never signalled (word {int(word[0])})"
+    # the outputs are read on torch's stream, beside a resident instance
+    return host_result(out), (d_in, d_conns, out)
 
 
 def oracle_run_frames(want, conns) -> int:

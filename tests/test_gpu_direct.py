@@ -13,8 +13,7 @@ import pytest
 
 import gev_amd
 from gev_amd import _abi
-from tests._helpers import assert_matches_oracle, host_result
-from tests.test_gpu_service import _batch, _check, _post
+from tests._helpers import assert_matches_oracle, check_against_oracle, host_result, post_and_wait, random_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -40,11 +39,11 @@ def test_direct_passes_equal_oracle(engine, direct):
     posted = 0
     for i in range(80):
         n = int(rng.choice([1, 5, 64, 200, 256, 300, 700, 1024]))
-        a, conns = _batch(rng, n, max_len=int(rng.choice([40, 120, 400])), frames=(1, 4))
+        a, conns = random_batch(rng, n, max_len=int(rng.choice([40, 120, 400])), frames=(1, 4))
         if a.size > _abi.ONE_LAUNCH_MAX_BYTES:
             continue
-        got, _ = _post(engine, direct, a, conns)
-        _check(got, a, conns, f"pass {i}: {n} connections, {a.size} bytes")
+        got, _ = post_and_wait(engine, direct, a, conns)
+        check_against_oracle(got, a, conns, f"pass {i}: {n} connections, {a.size} bytes")
         posted += 1
     assert posted >= 40
     assert engine.direct_dispatches - d0 == posted, (engine.direct_dispatches, d0, posted)
@@ -58,13 +57,13 @@ def test_direct_interleaved_with_launched_calls(engine, direct):
     rng = np.random.default_rng(72)
     dev = torch.device("cuda", engine.device)
     for i in range(6):
-        a, conns = _batch(rng, 150)
-        got, _ = _post(engine, direct, a, conns)
-        _check(got, a, conns, f"direct {i}")
-        a2, conns2 = _batch(rng, 20, max_len=9000)  # past the one-launch limit: launched, multi-kernel
+        a, conns = random_batch(rng, 150)
+        got, _ = post_and_wait(engine, direct, a, conns)
+        check_against_oracle(got, a, conns, f"direct {i}")
+        a2, conns2 = random_batch(rng, 20, max_len=9000)  # past the one-launch limit: launched, multi-kernel
         assert_matches_oracle(engine, a2, conns2, f"launched {i}")
         # a direct pass, then at once a one-launch pass on another stream (same staging granules)
-        a3, conns3 = _batch(rng, 120)
+        a3, conns3 = random_batch(rng, 120)
         d_in = torch.zeros(a3.size + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
         d_in[: a3.size] = torch.from_numpy(a3).to(dev)
         d_c = torch.from_numpy(np.ascontiguousarray(conns3)).to(dev)
@@ -80,22 +79,22 @@ def test_direct_interleaved_with_launched_calls(engine, direct):
         s1 = torch.cuda.Stream(dev)
         engine.decode_async(d_in, a3.size, d_c, conns3.shape[0], out, mf, cap, stream=s1)
         torch.cuda.synchronize()
-        _check(host_result(out4), a, conns, f"direct before stream {i}")
-        _check(host_result(out), a3, conns3, f"stream after direct {i}")
+        check_against_oracle(host_result(out4), a, conns, f"direct before stream {i}")
+        check_against_oracle(host_result(out), a3, conns3, f"stream after direct {i}")
 
 
 def test_direct_synchronize_and_off(engine, direct):
     """gevws_ctx_synchronize waits for direct passes; set_direct(False)
     launches again (the dispatch count stops)."""
     rng = np.random.default_rng(73)
-    a, conns = _batch(rng, 64)
-    got, _ = _post(engine, direct, a, conns)
+    a, conns = random_batch(rng, 64)
+    got, _ = post_and_wait(engine, direct, a, conns)
     engine.synchronize()
-    _check(got, a, conns, "direct")
+    check_against_oracle(got, a, conns, "direct")
     engine.set_direct(False)
     d0 = engine.direct_dispatches
-    got, _ = _post(engine, direct, a, conns)
-    _check(got, a, conns, "launched")
+    got, _ = post_and_wait(engine, direct, a, conns)
+    check_against_oracle(got, a, conns, "launched")
     assert engine.direct_dispatches == d0
 
 

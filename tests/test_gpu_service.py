@@ -16,9 +16,8 @@ import pytest
 
 import gev_amd
 from gev_amd import _abi
-from oracle import ref
 from oracle import ws_oracle as wo
-from tests._helpers import assert_matches_oracle, host_result, oracle_run_frames, random_stream
+from tests._helpers import assert_matches_oracle, check_against_oracle, post_and_wait, random_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -36,59 +35,6 @@ def service(engine):
     flag.close()
 
 
-def _batch(rng, n_conns, max_len=300, frames=(1, 6)):
-    ss = [random_stream(rng, int(rng.integers(*frames)), max_len=max_len) for _ in range(n_conns)]
-    arena = b"".join(ss)
-    lens = np.array([len(s) for s in ss], np.int64)
-    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
-    return np.frombuffer(arena, np.uint8).copy(), np.stack([offs, lens], 1)
-
-
-def _post(engine, flag, a, conns, timeout=5.0):
-    """Post one pass (inputs resident first: a post is not stream-ordered
-    behind torch's copies), wait for its number in the completion word and
-    return it with its outputs."""
-    import torch
-    dev = torch.device("cuda", engine.device)
-    d_in = torch.zeros(a.size + gev_amd.IN_PAD, dtype=torch.uint8, device=dev)
-    if a.size:
-        d_in[: a.size] = torch.from_numpy(a).to(dev)
-    n = conns.shape[0]
-    d_conns = torch.from_numpy(np.ascontiguousarray(conns)).to(dev) if n else torch.zeros((1, 2), dtype=torch.int64,
-                                                                                           device=dev)
-    max_frames = a.size // 2 + 1
-    payload_cap = a.size + 16 * min(max_frames, a.size // 64 + 64) + 64
-    out = engine.alloc_batch(n, max_frames, payload_cap)
-    # (torch's stream only: a device-wide synchronize would wait for the
-    # resident instance's life to end)
-    torch.cuda.current_stream(dev).synchronize()
-    engine.decode_post(d_in, a.size, d_conns, n, out, max_frames, payload_cap)
-    seq = engine.completion_seq
-    assert seq > 0
-    word = flag.host[64:68].view(np.uint32)
-    t0 = time.monotonic()
-    while int(word[0]) != seq:
-        assert time.monotonic() - t0 < timeout, f"pass {seq} never signalled (word {int(word[0])})"
-    # the outputs are read on torch's stream, beside the resident instance
-    return host_result(out), (d_in, d_conns, out)
-
-
-def _check(got, a, conns, tag):
-    want = ref.decode_batch(a, conns[:, 0], conns[:, 1])
-    s = got["summary"]
-    assert int(s["status"]) == 0, tag
-    assert int(s["frames"]) == want["frames"].shape[0], tag
-    assert int(s["payload_bytes"]) == want["total_payload"], tag
-    co = got["conn_out"]
-    assert np.array_equal(co["nframes"], want["conn_nframes"]), tag
-    assert np.array_equal(co["consumed"], want["conn_consumed"]), tag
-    assert np.array_equal(co["status"], want["conn_status"]), tag
-    assert np.array_equal(co["first_frame"], want["conn_first"]), tag
-    assert got["frames"].tobytes() == want["frames"].tobytes(), tag
-    assert int(s["run_frames"]) == oracle_run_frames(want, conns), tag
-    assert np.array_equal(got["payload"], want["payload"]), tag
-
-
 def test_service_passes_equal_oracle(engine, service):
     """60 posted passes of 1..256 connections (one slice, decoded by
     workgroup 0 alone, up to 32 slices staged by every workgroup), one
@@ -97,11 +43,11 @@ def test_service_passes_equal_oracle(engine, service):
     s0 = engine.service_stats()
     for i in range(60):
         n = int(rng.choice([1, 3, 17, 100, 256]))
-        a, conns = _batch(rng, n, max_len=int(rng.choice([60, 300, 900])))
+        a, conns = random_batch(rng, n, max_len=int(rng.choice([60, 300, 900])))
         if a.size > _abi.ONE_LAUNCH_MAX_BYTES // 2:
             continue
-        got, _ = _post(engine, service, a, conns)
-        _check(got, a, conns, f"pass {i}: {n} connections, {a.size} bytes")
+        got, _ = post_and_wait(engine, service, a, conns)
+        check_against_oracle(got, a, conns, f"pass {i}: {n} connections, {a.size} bytes")
     s1 = engine.service_stats()
     assert s1["posts"] - s0["posts"] >= 40, (s0, s1)
     # one instance, replaced at most every 100 ms
@@ -113,7 +59,7 @@ def test_service_edges(engine, service):
     narrow shape's limit: 32 slices); errors per connection (MSB length)."""
     rng = np.random.default_rng(62)
     cases = [(np.zeros(0, np.uint8), np.zeros((0, 2), np.int64))]
-    a, conns = _batch(rng, 5)
+    a, conns = random_batch(rng, 5)
     conns[2, 1] = 0
     conns[4, 1] -= 3  # a frame cut short: left for the next read
     cases.append((a, conns))
@@ -124,9 +70,9 @@ def test_service_edges(engine, service):
     a = np.frombuffer(bad + bad, np.uint8).copy()
     cases.append((a, np.array([[0, len(bad)], [len(bad), len(bad)]], np.int64)))
     for i, (a, conns) in enumerate(cases):
-        got, _ = _post(engine, service, a, conns)
+        got, _ = post_and_wait(engine, service, a, conns)
         if conns.shape[0]:
-            _check(got, a, conns, f"case {i}")
+            check_against_oracle(got, a, conns, f"case {i}")
         else:
             assert int(got["summary"]["status"]) == 0 and int(got["summary"]["frames"]) == 0
 
@@ -141,28 +87,28 @@ def test_service_ends_for_launched_calls_and_relaunches(engine, service):
     s0 = engine.service_stats()
     posts = 0
     for i in range(8):
-        a, conns = _batch(rng, 40)
-        got, _ = _post(engine, service, a, conns)
-        _check(got, a, conns, f"posted {i}")
+        a, conns = random_batch(rng, 40)
+        got, _ = post_and_wait(engine, service, a, conns)
+        check_against_oracle(got, a, conns, f"posted {i}")
         posts += 1
-        a2, conns2 = _batch(rng, 30, max_len=5000)
+        a2, conns2 = random_batch(rng, 30, max_len=5000)
         assert_matches_oracle(engine, a2, conns2, f"launched {i}")
     s1 = engine.service_stats()
     assert s1["posts"] - s0["posts"] == posts and s1["launches"] - s0["launches"] == posts, (s0, s1)
-    a, conns = _batch(rng, 300, max_len=80)  # past 256 connections: the wide one-launch shape, launched
-    got, _ = _post(engine, service, a, conns)
-    _check(got, a, conns, "300 connections")
+    a, conns = random_batch(rng, 300, max_len=80)  # past 256 connections: the wide one-launch shape, launched
+    got, _ = post_and_wait(engine, service, a, conns)
+    check_against_oracle(got, a, conns, "300 connections")
     s2 = engine.service_stats()
     assert s2["posts"] == s1["posts"], (s1, s2)
-    a, conns = _batch(rng, 20)
-    got, _ = _post(engine, service, a, conns)
+    a, conns = random_batch(rng, 20)
+    got, _ = post_and_wait(engine, service, a, conns)
     engine.service_stop()
-    got2, _ = _post(engine, service, a, conns)
-    _check(got, a, conns, "before stop")
-    _check(got2, a, conns, "after stop")
+    got2, _ = post_and_wait(engine, service, a, conns)
+    check_against_oracle(got, a, conns, "before stop")
+    check_against_oracle(got2, a, conns, "after stop")
     time.sleep(0.25)  # past the use window (100 ms) and the instance's life (200 ms)
-    got3, _ = _post(engine, service, a, conns)
-    _check(got3, a, conns, "after 250 ms")
+    got3, _ = post_and_wait(engine, service, a, conns)
+    check_against_oracle(got3, a, conns, "after 250 ms")
     s3 = engine.service_stats()
     assert s3["posts"] - s2["posts"] == 3 and s3["launches"] - s2["launches"] == 3, (s2, s3)
 
@@ -172,9 +118,9 @@ def test_service_off_launches(engine, service):
     rng = np.random.default_rng(64)
     engine.set_service(False)
     s0 = engine.service_stats()
-    a, conns = _batch(rng, 50)
-    got, _ = _post(engine, service, a, conns)
-    _check(got, a, conns, "service off")
+    a, conns = random_batch(rng, 50)
+    got, _ = post_and_wait(engine, service, a, conns)
+    check_against_oracle(got, a, conns, "service off")
     assert engine.service_stats() == s0
 
 
