@@ -30,7 +30,15 @@ extern "C" {
  * measurement exports (gevws_gather_async, gevws_unmask_profile,
  * gevws_ctx_last_walk_budget, gevws_ctx_last_resumed; tuning keys 5, 6, 9-12)
  * removed in round 4 are counted here too. */
-#define GEVWS_ABI_VERSION 2
+/* 3 (round 6): gevws_protocol_stats grew two fields (service_passes,
+ * service_misses) -- a caller built against version 2 passes a smaller
+ * struct to gevws_protocol_get_stats -- and the one-launch decode's limits
+ * rose to GEVWS_ONE_LAUNCH_MAX_CONNS / _BYTES.  Added: the resident service
+ * (gevws_ctx_set_service, _service_stop, _service_stats,
+ * gevws_decode_batch_post, gevws_protocol_set_service), direct dispatch
+ * (gevws_ctx_set_direct, _direct_dispatches, gevws_protocol_set_direct),
+ * gevws_ctx_synchronize, gevws_ctx_last_split_fallbacks. */
+#define GEVWS_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- status codes */
 enum {

@@ -52,7 +52,7 @@ def test_struct_layouts_match_reference():
 
 
 def test_status_strings_and_version():
-    assert gev_amd.lib.gevws_abi_version() == 2  # round 5: split-stream calls removed
+    assert gev_amd.lib.gevws_abi_version() == 3  # round 6: gevws_protocol_stats grew
     assert gev_amd.status_string(gev_amd.NEED_MORE) == "header error: not enough"  # read.go:15
     assert gev_amd.status_string(gev_amd.ERR_LEN_MSB) == "header error: the most significant bit must be 0"
 
