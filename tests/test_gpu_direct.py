@@ -131,3 +131,26 @@ def test_protocol_zero_copy_passes_dispatched_direct(engine):
     finally:
         proto.set_direct(False)
         proto.close()
+
+
+def test_direct_and_service_on_one_context(engine, direct):
+    """Both forms on: posts go to the context's own queue; with direct off
+    they go to the resident service (the direct passes drained first), and
+    back again (the service instance stopped first).  Every pass exact."""
+    rng = np.random.default_rng(75)
+    engine.set_service(True)
+    try:
+        for round_ in range(3):
+            for form in ("direct", "service"):
+                engine.set_direct(form == "direct")
+                d0, s0 = engine.direct_dispatches, engine.service_stats()["posts"]
+                for i in range(4):
+                    a, conns = random_batch(rng, int(rng.choice([10, 100, 250])), max_len=100, frames=(1, 3))
+                    assert a.size <= _abi.ONE_LAUNCH_MAX_BYTES // 2  # (the service's narrow shape)
+                    got, _ = post_and_wait(engine, direct, a, conns)
+                    check_against_oracle(got, a, conns, f"{form} {round_}.{i}")
+                moved = engine.direct_dispatches - d0, engine.service_stats()["posts"] - s0
+                assert moved == ((4, 0) if form == "direct" else (0, 4)), (form, moved)
+    finally:
+        engine.set_service(False)
+        engine.set_direct(True)  # (the fixture turns it off)
