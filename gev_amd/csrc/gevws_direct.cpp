@@ -21,6 +21,7 @@
 #include <hsa/hsa_ven_amd_loader.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <string>
 
@@ -41,6 +42,7 @@ struct DirectQueue {
   uint32_t* flag_dev = nullptr;
   uint32_t last_seq = 0;  // the last dispatch's completion number
   uint64_t dispatched = 0;
+  int failed = 0;  // set by the queue's error callback (a faulting packet): no further dispatch or wait
 };
 
 namespace gevws_impl {
@@ -141,6 +143,15 @@ hsa_status_t find_cpu_kernarg_pool(hsa_agent_t a, void* data) {
   return pool->handle ? HSA_STATUS_INFO_BREAK : HSA_STATUS_SUCCESS;
 }
 
+// The runtime's report of an asynchronous queue error (a packet that
+// faulted): recorded, so waits and dispatches on this queue fail at once.
+void on_queue_error(hsa_status_t status, hsa_queue_t*, void* data) {
+  __atomic_store_n(&static_cast<DirectQueue*>(data)->failed, 1, __ATOMIC_RELEASE);
+  const char* msg = nullptr;
+  (void)hsa_status_string(status, &msg);
+  fprintf(stderr, "[gevws] direct dispatch queue error: %s\n", msg ? msg : "?");
+}
+
 void close_queue(DirectQueue* dq) {
   if (!dq) return;
   if (dq->q) (void)hsa_queue_destroy(dq->q);
@@ -190,7 +201,7 @@ DirectQueue* open_queue(gevws_ctx* ctx) {
   (void)hsa_agent_get_info(dq->agent, HSA_AGENT_INFO_QUEUE_MIN_SIZE, &qmin);
   uint32_t qsize = 64;
   while (qsize < qmin) qsize *= 2;
-  if (hsa_queue_create(dq->agent, qsize, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &dq->q) !=
+  if (hsa_queue_create(dq->agent, qsize, HSA_QUEUE_TYPE_SINGLE, on_queue_error, dq, UINT32_MAX, UINT32_MAX, &dq->q) !=
       HSA_STATUS_SUCCESS) {
     dq->q = nullptr;
     close_queue(dq);
@@ -208,12 +219,15 @@ DirectQueue* open_queue(gevws_ctx* ctx) {
   return dq;
 }
 
-// Spins until the completion word carries seq or later (false past 10 s).
-bool wait_word(const volatile uint32_t* w, uint32_t seq) {
+// Spins until the completion word carries seq or later (false past 10 s, or
+// at once once the queue has reported an error).
+bool wait_word(const DirectQueue* dq, const volatile uint32_t* w, uint32_t seq) {
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t i = 1;; ++i) {
     if ((int32_t)(__atomic_load_n(w, __ATOMIC_ACQUIRE) - seq) >= 0) return true;
-    if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return false;
+    if ((i & 1023) == 0 && (__atomic_load_n(&dq->failed, __ATOMIC_ACQUIRE) ||
+                            std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)))
+      return false;
     __builtin_ia32_pause();
   }
 }
@@ -223,7 +237,7 @@ bool wait_word(const volatile uint32_t* w, uint32_t seq) {
 int direct_drain(gevws_ctx* ctx) {
   DirectQueue* dq = ctx->direct;
   if (!dq || !dq->dispatched || !dq->flag_host) return GEVWS_OK;
-  return wait_word(dq->flag_host, dq->last_seq) ? GEVWS_OK : GEVWS_ERR_DEVICE;
+  return wait_word(dq, dq->flag_host, dq->last_seq) ? GEVWS_OK : GEVWS_ERR_DEVICE;
 }
 
 // One live pass written into the context's queue (the kernel: shape `wide`,
@@ -235,6 +249,7 @@ bool direct_dispatch(gevws_ctx* ctx, int wide, const DirectDecodeArgs& a) {
     return false;
   }
   DirectQueue* dq = ctx->direct;
+  if (__atomic_load_n(&dq->failed, __ATOMIC_ACQUIRE)) return false;
   const DirectQueue::Kernel& k = dq->k[wide];
   // the completion word's host address (the pass waits on it; so do drains)
   if (dq->flag_dev != a.done) {
@@ -262,7 +277,7 @@ bool direct_dispatch(gevws_ctx* ctx, int wide, const DirectDecodeArgs& a) {
   }
   // the kernarg slot: free once the dispatch that used it last has signalled
   const uint32_t slot = (uint32_t)(idx % DirectQueue::kSlots);
-  if (idx >= DirectQueue::kSlots && !wait_word(dq->flag_host, dq->slot_seq[slot])) return false;
+  if (idx >= DirectQueue::kSlots && !wait_word(dq, dq->flag_host, dq->slot_seq[slot])) return false;
   uint8_t* karg = dq->kernargs + (size_t)slot * DirectQueue::kSlotBytes;
   memcpy(karg, &a, sizeof(a));
   dq->slot_seq[slot] = a.seq;

@@ -1,4 +1,5 @@
 # round 6: direct dispatch and the resident service switched on one context
+# (re-run after the direct queue got its error callback)
 # (tests/test_gpu_direct.py::test_direct_and_service_on_one_context), with
 # the ABI-3 build; the direct and service tests again.
 set -o pipefail
