@@ -397,6 +397,15 @@ class Engine:
         if st != OK:
             raise RuntimeError(f"gevws_ctx_set_completion_flag: {status_string(st)}")
 
+    def set_timeline_ticks(self, arena: Optional["PinnedArena"], offset: int = 0) -> None:
+        """gevws_ctx_set_timeline_ticks: the one-launch kernels stamp their start /
+        end ticks (GPU constant-rate clock) into 4 u64 at arena.host[offset:offset+32]
+        before they signal (None: off)."""
+        addr = arena.at(offset).data_ptr() if arena is not None else None
+        st = lib.gevws_ctx_set_timeline_ticks(self._ctx, addr)
+        if st != OK:
+            raise RuntimeError(f"gevws_ctx_set_timeline_ticks: {status_string(st)}")
+
     @property
     def completion_seq(self) -> int:
         """gevws_ctx_completion_seq: the number the last call's last kernel

@@ -37,6 +37,7 @@ struct DirectDecodeArgs {
   uint64_t* stage_buf;
   uint32_t* stage_done;
   uint32_t n, seq, tag, nwg;
+  uint64_t* phase;  // (measurement: GEVWS_PHASE_TICKS)
 };
 struct DirectQueue;  // gevws_direct.cpp
 

@@ -167,8 +167,49 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
   return x;
 }
 
-// Block exclusive scan of NV u64 values per thread (blockDim.x = BS).
-// Returns exclusive prefixes in ex[], block totals in tot[].
+// Block exclusive scan of NV u64 values per thread (blockDim.x = BS; every
+// lane of the workgroup calls it).  Returns exclusive prefixes in ex[],
+// block totals in tot[].  DPP wave scans (wave_incl_scan64_dpp, below) and
+// one LDS exchange of the wave totals: the shuffle form's ds_bpermute round
+// trips cost the one-launch decode 2.5 us of a 100-connection pass
+// (profiles/r06/README.md, r06z / r06aa).
+template <int BS, int NV>
+__device__ __forceinline__ void block_excl_scan(const uint64_t (&v)[NV], uint64_t (&ex)[NV],
+                                                uint64_t (&tot)[NV]);
+
+// Wave64 inclusive scans by DPP (no LDS round trips; every lane active):
+// row_shr 1 / 2 / 4 / 8 scan each row of 16 lanes (lanes shifted in from
+// outside the row read 0: bound_ctrl), then row_bcast:15 adds row 0's total
+// into row 1 and row 2's into row 3, and row_bcast:31 adds lane 31's running
+// total into rows 2 and 3 (the masked-off rows keep `old` = 0).  The shuffle
+// forms above cost a ds_bpermute (an LDS round trip) per step and 32-bit half.
+template <int CTRL, int ROWS, bool BOUND>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, BOUND);
+}
+template <int CTRL, int ROWS, bool BOUND>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+  return (uint64_t)dpp32<CTRL, ROWS, BOUND>((uint32_t)x) | ((uint64_t)dpp32<CTRL, ROWS, BOUND>((uint32_t)(x >> 32)) << 32);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan32_dpp(uint32_t x) {
+  x += dpp32<0x111, 0xf, true>(x);   // row_shr:1
+  x += dpp32<0x112, 0xf, true>(x);   // row_shr:2
+  x += dpp32<0x114, 0xf, true>(x);   // row_shr:4
+  x += dpp32<0x118, 0xf, true>(x);   // row_shr:8
+  x += dpp32<0x142, 0xa, false>(x);  // row_bcast:15 -> rows 1, 3
+  x += dpp32<0x143, 0xc, false>(x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_incl_scan64_dpp(uint64_t x) {
+  x += dpp64<0x111, 0xf, true>(x);
+  x += dpp64<0x112, 0xf, true>(x);
+  x += dpp64<0x114, 0xf, true>(x);
+  x += dpp64<0x118, 0xf, true>(x);
+  x += dpp64<0x142, 0xa, false>(x);
+  x += dpp64<0x143, 0xc, false>(x);
+  return x;
+}
+
 template <int BS, int NV>
 __device__ __forceinline__ void block_excl_scan(const uint64_t (&v)[NV], uint64_t (&ex)[NV],
                                                 uint64_t (&tot)[NV]) {
@@ -178,18 +219,51 @@ __device__ __forceinline__ void block_excl_scan(const uint64_t (&v)[NV], uint64_
   uint64_t inc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    inc[k] = wave_incl_scan(v[k]);
+    inc[k] = wave_incl_scan64_dpp(v[k]);
     if (lane == 63) s_w[k][w] = inc[k];
   }
   __syncthreads();
-  // lane j reads wave j's total: one LDS load per field instead of NW
-  // (unrolled over NV x NW it took 160 VGPRs at NV = 5 and spilled)
-  static_assert(NW <= 64, "one lane per wave total");
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    const uint64_t sj = lane < NW ? s_w[k][lane] : 0;
-    ex[k] = wave_sum(lane < w ? sj : 0) + inc[k] - v[k];
-    tot[k] = wave_sum(sj);
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {  // (broadcast LDS reads: every lane the same word)
+      const uint64_t t = s_w[k][j];
+      before += j < w ? t : 0u;
+      all += t;
+    }
+    ex[k] = before + inc[k] - v[k];
+    tot[k] = all;
+  }
+  __syncthreads();
+}
+
+// Block exclusive scan of NV u32 values per thread (blockDim.x = BS) on DPP
+// wave scans: one LDS exchange of the wave totals.  For sums known to fit
+// 32 bits (the one-launch decode's, whose input is at most 128 KiB).
+template <int BS, int NV>
+__device__ __forceinline__ void block_excl_scan32(const uint32_t (&v)[NV], uint32_t (&ex)[NV], uint32_t (&tot)[NV]) {
+  constexpr int NW = BS / 64;
+  __shared__ uint32_t s_w[NV][NW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    inc[k] = wave_incl_scan32_dpp(v[k]);
+    if (lane == 63) s_w[k][w] = inc[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {  // (broadcast LDS reads: every lane the same word)
+      const uint32_t t = s_w[k][j];
+      before += j < w ? t : 0u;
+      all += t;
+    }
+    ex[k] = before + inc[k] - v[k];
+    tot[k] = all;
   }
   __syncthreads();
 }

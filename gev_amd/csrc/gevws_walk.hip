@@ -1367,7 +1367,8 @@ __device__ __forceinline__ bool decode_small_body(const uint8_t* __restrict__ in
                                                   uint32_t* __restrict__ done, uint32_t seq,
                                                   uint64_t* __restrict__ ticks, uint64_t* __restrict__ stage_buf,
                                                   uint32_t* __restrict__ stage_done, uint32_t tag, uint32_t nwg,
-                                                  uint32_t wg, uint32_t nslices) {
+                                                  uint32_t wg, uint32_t nslices,
+                                                  uint64_t* __restrict__ phase = nullptr) {
   constexpr uint32_t NT = S::NT;
   constexpr int kBatch = S::kBatch;
   __shared__ uint64_t s_big[S::kBig][3];  // {src_off, payload_off, length} of the larger payloads
@@ -1457,6 +1458,7 @@ __device__ __forceinline__ bool decode_small_body(const uint8_t* __restrict__ in
     }
   }
   __syncthreads();
+  if (phase && c == 0) phase[0] = gpu_ticks();  // (measurement: the input is in LDS)
   if (s_bad) {  // a staged granule never carried this launch's tag (workgroup-uniform)
     if (c == 0) {
       gevws_summary sm;
@@ -1497,9 +1499,17 @@ __device__ __forceinline__ bool decode_small_body(const uint8_t* __restrict__ in
       pos += f;
     }
   }
-  const uint64_t v[kDecFields] = {nf, pb, pl, err, same};
-  uint64_t ex[kDecFields], tot[kDecFields];
-  block_excl_scan<NT, kDecFields>(v, ex, tot);
+  // The five sums fit 32 bits here (input <= 128 KiB, <= 1 024 lanes): the
+  // DPP scan (block_excl_scan32) instead of the 64-bit shuffle scan, 2.5 us
+  // of a 100-connection pass (tools/live_pass_probe.py, GEVWS_PHASE_TICKS).
+  // Field 3 carries the errors (<= 2 a lane) in its low 16 bits and the
+  // out-of-order lanes in its high 16.
+  const uint32_t v[kDecFields] = {(uint32_t)nf, (uint32_t)pb, (uint32_t)pl,
+                                  (uint32_t)(err & 0xffffu) | ((uint32_t)(err >> 32) << 16), (uint32_t)same};
+  uint32_t ex[kDecFields], tot[kDecFields];
+  if (phase && c == 0) phase[1] = gpu_ticks();  // (measurement: this lane's chain parsed)
+  block_excl_scan32<NT, kDecFields>(v, ex, tot);
+  if (phase && c == 0) phase[2] = gpu_ticks();  // (measurement: the workgroup's scan done)
   const bool ok = tot[0] <= max_frames && tot[1] <= payload_cap;
   if (c == 0) {
     gevws_summary sm;
@@ -1507,8 +1517,8 @@ __device__ __forceinline__ bool decode_small_body(const uint8_t* __restrict__ in
     sm.frames = tot[0];
     sm.payload_bytes = tot[1];
     sm.payload_len = tot[2];
-    sm.errors = tot[3] & 0xffffffffull;
-    sm.flags = (tot[3] >> 32) ? GEVWS_SUMMARY_UNORDERED : 0u;
+    sm.errors = tot[3] & 0xffffu;
+    sm.flags = (tot[3] >> 16) ? GEVWS_SUMMARY_UNORDERED : 0u;
     sm.run_frames = tot[4];
     sm.status = ok ? GEVWS_OK : GEVWS_ERR_CAPACITY;
     *sum = sm;
@@ -1575,6 +1585,7 @@ __device__ __forceinline__ bool decode_small_body(const uint8_t* __restrict__ in
       *reinterpret_cast<u32x4*>(payload + poff + 16 * j) = y;
     }
   }
+  if (phase && c == 0) phase[3] = gpu_ticks();  // (measurement: every output store issued)
   signal_done(done, seq, ticks, t0, 0);
   return true;
 }
@@ -1590,9 +1601,9 @@ __global__ __launch_bounds__(S::NT) void k_decode_small(const uint8_t* __restric
                                                         uint32_t seq = 0, uint64_t* __restrict__ ticks = nullptr,
                                                         uint64_t* __restrict__ stage_buf = nullptr,
                                                         uint32_t* __restrict__ stage_done = nullptr,
-                                                        uint32_t tag = 0) {
+                                                        uint32_t tag = 0, uint64_t* __restrict__ phase = nullptr) {
   (void)decode_small_body<S>(in, in_bytes, conns, n, frames, max_frames, payload, payload_cap, cout, sum, done, seq,
-                             ticks, stage_buf, stage_done, tag, gridDim.x, blockIdx.x, gridDim.x);
+                             ticks, stage_buf, stage_done, tag, gridDim.x, blockIdx.x, gridDim.x, phase);
 }
 
 // The same with its arguments in one by-value struct: the form a dispatch
@@ -1601,7 +1612,7 @@ template <class S>
 __global__ __launch_bounds__(S::NT) void k_decode_small_direct(DirectDecodeArgs a) {
   (void)decode_small_body<S>(a.in, a.in_bytes, a.conns, a.n, a.frames, a.max_frames, a.payload, a.payload_cap,
                              a.cout, a.sum, a.done, a.seq, a.ticks, a.stage_buf, a.stage_done, a.tag, a.nwg,
-                             blockIdx.x, a.nwg);
+                             blockIdx.x, a.nwg, a.phase);
 }
 
 // ------------------------------------------------------------------ 3d. the resident decode service
@@ -1768,6 +1779,18 @@ const void* direct_kernel_stub(int wide) {
 uint32_t split_fallback_counter() { return kSplitFallbackCounter; }
 const char* walk_variant_name(int i) { return i >= 0 && i < kNumWalkVariants ? kWalkVariants[i] : nullptr; }
 
+// GEVWS_PHASE_TICKS=1 (measurement, tools/live_pass_probe.py): a one-launch
+// decode also stamps, into the timeline ticks' words 2-5 (past the 4 the ABI
+// documents: the caller's buffer must hold 6), when its input was in LDS,
+// lane 0's chain parsed, the workgroup's scan done, its last store issued.
+static uint64_t* phase_ticks(const gevws_ctx* ctx) {
+  static const bool on = [] {
+    const char* e = getenv("GEVWS_PHASE_TICKS");
+    return e && e[0] == '1';
+  }();
+  return on && ctx->done_flag && ctx->ticks ? ctx->ticks + 2 : nullptr;
+}
+
 // A live pass's staging granules (4 per 16-byte chunk of the wide shape's input), zeroed once.
 static bool ensure_small_stage(gevws_ctx* ctx, hipStream_t st) {
   if (ctx->d_small_stage) return true;
@@ -1798,7 +1821,7 @@ static int launch_decode_small(gevws_ctx* ctx, hipStream_t st, const uint8_t* d_
   k_decode_small<S><<<nwg, S::NT, 0, st>>>(d_in, in_bytes, d_conns, n_conns, d_frames, max_frames, d_payload,
                                            payload_cap, d_conn_out, d_summary, ctx->done_flag, seq,
                                            ctx->done_flag ? ctx->ticks : nullptr, ctx->d_small_stage,
-                                           ctx->d_done + kSmallStageCounter, tag);
+                                           ctx->d_done + kSmallStageCounter, tag, phase_ticks(ctx));
   GEVWS_HIP(hipGetLastError());
   const int r = ctx->prev_small_decode ? mark_last_lazy(ctx, st) : mark_last(ctx, st);
   ctx->prev_small_decode = true;
@@ -1943,6 +1966,7 @@ bool direct_post(gevws_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const g
   a.seq = seq;
   a.tag = nwg > 1 ? next_hand_tag(ctx) : 0u;
   a.nwg = nwg;
+  a.phase = phase_ticks(ctx);
   if (!direct_dispatch(ctx, wide, a)) return false;
   ctx->done_seq = seq;
   ctx->last_signal = seq;

@@ -21,9 +21,9 @@ for i in $(seq ${ROUNDS:-3}); do
     args=${!shape}
     if [ $((i % 2)) = 1 ]; then
       run ${shape}_new GEVWS_NOP=1 gev_amd/ws_loopback $args || exit 1
-      run ${shape}_base GEVWS_NOP=1 ab_base/ws_loopback $args || exit 1
+      run ${shape}_base GEVWS_NOP=1 ${BASE:-ab_base}/ws_loopback $args || exit 1
     else
-      run ${shape}_base GEVWS_NOP=1 ab_base/ws_loopback $args || exit 1
+      run ${shape}_base GEVWS_NOP=1 ${BASE:-ab_base}/ws_loopback $args || exit 1
       run ${shape}_new GEVWS_NOP=1 gev_amd/ws_loopback $args || exit 1
     fi
     if [ "$shape" = WSS ] && [ "${PRIO_ALL:-0}" = 1 ]; then
