@@ -1042,17 +1042,17 @@ __device__ __forceinline__ void emit_record(gevws_frame* __restrict__ frames, ui
 // Segmented inclusive wave scan: a segment starts at every lane with head set
 // (and at lane 0).  Every lane must take part.
 __device__ __forceinline__ uint64_t wave_seg_scan(uint64_t v, bool head) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t vu = __shfl_up(v, d, 64);
-    const bool hu = __shfl_up((int)head, d, 64) != 0;
-    if (lane >= d && !head) {
-      v += vu;
-      head = hu;
-    }
-  }
-  return v;
+  // The wave's plain inclusive scan (DPP) minus its value just before this
+  // lane's segment, whose first lane is the highest head at or below it (the
+  // wave's lane 0 if none): one ballot and one shuffle instead of a shuffled
+  // value and head flag at each of six steps.
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t incl = wave_incl_scan64_dpp(v);
+  const uint64_t heads = __ballot(head);
+  const uint64_t upto = lane == 63 ? heads : heads & ((2ull << lane) - 1);
+  const int h = upto ? 63 - __builtin_clzll(upto) : 0;
+  const uint64_t before = __shfl(incl, h > 0 ? h - 1 : 0, 64);
+  return h > 0 ? incl - before : incl;
 }
 
 // One round of entries (lane = frame): each frame's payload length L and the
