@@ -38,6 +38,7 @@ struct DirectQueue {
   static constexpr uint32_t kSlotBytes = 512;
   uint8_t* kernargs = nullptr;  // kSlots x kSlotBytes, fine-grained host memory
   uint32_t slot_seq[kSlots] = {};  // the completion number of the dispatch that last used a slot
+  bool slot_used[kSlots] = {};     // ... if that dispatch may not have signalled yet
   const volatile uint32_t* flag_host = nullptr;  // the completion word the dispatches signal (host address)
   uint32_t* flag_dev = nullptr;
   uint32_t last_seq = 0;  // the last dispatch's completion number
@@ -259,7 +260,7 @@ bool direct_dispatch(gevws_ctx* ctx, int wide, const DirectDecodeArgs& a) {
     dq->flag_dev = a.done;
     dq->flag_host = static_cast<const volatile uint32_t*>(pa.hostPointer);
     dq->dispatched = 0;
-    memset(dq->slot_seq, 0, sizeof(dq->slot_seq));
+    memset(dq->slot_used, 0, sizeof(dq->slot_used));  // (drained above)
   }
   // work the context enqueued on its stream before this pass runs first
   if (ctx->has_last && !ctx->last_direct &&
@@ -277,10 +278,11 @@ bool direct_dispatch(gevws_ctx* ctx, int wide, const DirectDecodeArgs& a) {
   }
   // the kernarg slot: free once the dispatch that used it last has signalled
   const uint32_t slot = (uint32_t)(idx % DirectQueue::kSlots);
-  if (idx >= DirectQueue::kSlots && !wait_word(dq, dq->flag_host, dq->slot_seq[slot])) return false;
+  if (dq->slot_used[slot] && !wait_word(dq, dq->flag_host, dq->slot_seq[slot])) return false;
   uint8_t* karg = dq->kernargs + (size_t)slot * DirectQueue::kSlotBytes;
   memcpy(karg, &a, sizeof(a));
   dq->slot_seq[slot] = a.seq;
+  dq->slot_used[slot] = true;
   auto* pkt = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (idx & (q->size - 1));
   const uint32_t nt = wide ? 1024u : 256u;
   pkt->workgroup_size_x = (uint16_t)nt;
@@ -323,7 +325,7 @@ void direct_forget_flag(gevws_ctx* ctx) {
   dq->flag_host = nullptr;  // (the word may be freed next)
   dq->flag_dev = nullptr;
   dq->dispatched = 0;
-  memset(dq->slot_seq, 0, sizeof(dq->slot_seq));  // every slot free: its dispatch has signalled
+  memset(dq->slot_used, 0, sizeof(dq->slot_used));  // every slot free: its dispatch has signalled
 }
 
 void direct_close(gevws_ctx* ctx) {
